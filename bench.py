@@ -1,0 +1,276 @@
+#!/usr/bin/env python3
+"""Benchmark: lattice contraction GFLOP/s (+ permute GB/s) -- BASELINE.json metric.
+
+Workload (N = 1): BASELINE.json configs[1], the 16^4 lattice spin x color contraction
+  v0 `tnsxyzc` {16,64,4,16,16,16,3} x v1 `tNSxyzc` -> vr `tNSns` {16,64,4,64,4},
+  complex<double>, through superbblas_amd.contraction (the drop-in C-ABI).  One step = one
+  contraction call (= one strided batched complex GEMM m = n = 256, k = 12288, batch 16 on MFMA,
+  1.031e11 flop).  Inputs are resident in HBM before the timed region.
+N > 1 (one process per GPU, RCCL): weak scaling -- every rank owns a 16^4 block of a lattice of
+  16*px x 16*py x 16*pz x 16 sites (xyz grid 2x1x1 / 2x2x1 / 2x2x2), the contraction sums over
+  xyz so each rank runs the same local GEMM and the partial tNSns outputs are reduced into rank
+  0's output through the library's remap communicator (RCCL over xGMI).
+Side measurements on the same run (reported as extra fields): the dist.cpp permute
+  xyztsc -> tnsxyzc (64 slices, GB/s) and the 16^4 3x3-block BSR SpMM (config 3).
+cpu_baseline: the real reference (oracle/_ref/ref_bench: header-only superbblas + OpenBLAS,
+  OpenMP over the batch) timed on this box's host cores on a bounded sample (the 16^4, n = 16
+  contraction), or the oracle restatement when the reference build is absent.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_FP64_TFLOPS = 78.6   # MI355X FP64 matrix (dense), MI355X_MICROARCH.md / BASELINE.md
+PEAK_HBM_GBPS = 8000.0    # HBM3E spec
+
+
+def vol(d):
+    n = 1
+    for x in d:
+        n *= x
+    return n
+
+
+def fill(t, seed):
+    g = torch.Generator(device=t.device)
+    g.manual_seed(seed)
+    r = torch.rand(t.numel(), 2, generator=g, device=t.device, dtype=torch.float64) * 2 - 1
+    t.copy_(torch.view_as_complex(r))
+
+
+def cpu_baseline(threads):
+    """Time the reference CPU path on a bounded sample."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "ref_bench")
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads), OPENBLAS_NUM_THREADS="1")
+    if os.path.exists(exe):
+        try:
+            out = subprocess.run([exe, "contraction", "16", "16", "3"], env=env, timeout=300,
+                                 capture_output=True, text=True, check=True).stdout
+            r = json.loads(out.strip().splitlines()[-1])
+            return {"value": round(r["gflops"], 2), "unit": "GFLOP/s", "cores": r["threads"],
+                    "kind": "reference",
+                    "sample": "superbblas::contraction tnsxyzc x tNSxyzc -> tNSns, 16^4, n=16, "
+                              "complex<double>, 3 reps (OpenMP over t, OpenBLAS zgemm per t)"}
+        except Exception as e:  # pragma: no cover
+            print("cpu_baseline: reference run failed: %s" % e, file=sys.stderr)
+    # restatement (oracle/oracle.c) on a small sample
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _common import oracle_gemm, random_valued
+    m = n = 64
+    k, b = 1536, 8
+    a = random_valued(m * k * b, np.complex128, 1)
+    bb = random_valued(n * k * b, np.complex128, 2)
+    c = np.zeros(m * n * b, np.complex128)
+    t = time.perf_counter()
+    oracle_gemm("T", "N", m, n, k, 1.0, a, k, m * k, bb, k, n * k, 0.0, c, m, m * n, b)
+    t = time.perf_counter() - t
+    return {"value": round(8.0 * m * n * k * b / t / 1e9, 2), "unit": "GFLOP/s", "cores": threads,
+            "kind": "port", "sample": "oracle xgemm_batch_strided 'T','N' 64x64x1536 batch 8"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--L", type=int, default=16)
+    ap.add_argument("--n", type=int, default=64)
+    ap.add_argument("--no-side", action="store_true", help="skip permute/BSR side measurements")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    import superbblas_amd as sb
+
+    comm = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+        comm = sb.Comm.from_torch_distributed(local_rank)
+
+    L, n = args.L, args.n
+    grid = {1: [1, 1, 1], 2: [2, 1, 1], 4: [2, 2, 1], 8: [2, 2, 2]}.get(world)
+    if grid is None:
+        raise SystemExit("unsupported --gpus %d" % world)
+    # global lattice (weak scaling over x, y, z)
+    gdim0 = [L, n, 4, L * grid[0], L * grid[1], L * grid[2], 3]  # tnsxyzc
+    gdimr = [L, n, 4, n, 4]  # tNSns
+    procs = [1, 1, 1] + grid + [1]
+    p0 = sb.basic_partitioning("tnsxyzc", gdim0, procs, "xyz", world, 1)
+    pr = [([0] * 5, gdimr)] + [([0] * 5, [0] * 5)] * (world - 1)  # output on rank 0
+    local0 = p0[rank][1]
+    v0 = torch.empty(vol(local0), dtype=torch.complex128, device=dev)
+    v1 = torch.empty(vol(local0), dtype=torch.complex128, device=dev)
+    vr = torch.zeros(vol(pr[rank][1]) if rank == 0 else 1, dtype=torch.complex128, device=dev)
+    fill(v0, 1 + rank)
+    fill(v1, 101 + rank)
+    z7, z5 = [0] * 7, [0] * 5
+
+    def step():
+        sb.contraction(1.0, p0, z7, gdim0, gdim0, "tnsxyzc", False, [v0], p0, z7, gdim0, gdim0,
+                       "tNSxyzc", False, [v1], 0.0, pr, z5, gdimr, gdimr, "tNSns", [vr],
+                       comm=comm)
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record()
+        step()
+        ev[i][1].record()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    step_ms = [a.elapsed_time(b) for a, b in ev]
+    kernel_s = float(np.mean(step_ms)) / 1e3
+
+    flops_rank = 8.0 * L * (L ** 3 * 3) * (n * 4) ** 2  # 8 * volT * volA * volB * volC
+    total_flops = flops_rank * world * args.steps
+    value = total_flops / elapsed / 1e9
+    achieved = flops_rank / kernel_s / 1e12
+
+    side = {}
+    if not args.no_side:
+        side.update(permute_bench(sb, dev, L, n))
+        side.update(bsr_bench(sb, dev, L))
+    base = None
+    if rank == 0 and not args.no_cpu:
+        base = cpu_baseline(int(os.environ.get("OMP_NUM_THREADS", "16")))
+
+    if rank == 0:
+        line = {
+            "metric": "lattice contraction GFLOP/s + permute GB/s, 16^4 spin×color, 1/2/4/8 GPUs",
+            "value": round(value, 2),
+            "unit": "GFLOP/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "complex<f64>",
+            "data": "synthetic (uniform [-1,1) complex, seeded)",
+            "config": {"workload": "configs[1]: 16^4 lattice spin x color contraction "
+                                   "tnsxyzc x tNSxyzc -> tNSns, n=64, complex<double>"
+                                   + ("" if world == 1 else
+                                      "; weak scaling, xyz grid %s, 16^4 sites per GPU, "
+                                      "partial outputs reduced to rank 0 over RCCL" % grid),
+                       "L": L, "n": n, "gemm": "T,N m=n=%d k=%d batch=%d" % (4 * n, L ** 3 * 3, L),
+                       "parallelism": "xyz domain decomposition" if world > 1 else "single GPU"},
+            "roofline": {"bound": "mfma", "achieved": round(achieved, 3),
+                         "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved / PEAK_FP64_TFLOPS, 4), "traffic": None,
+                         "kernel": "contraction step: gemm_kernel<double,cplx> + splitk_reduce "
+                                   "(HIP events on the library stream)"},
+            "cpu_baseline": base,
+        }
+        line.update(side)
+        print(json.dumps(line))
+    if comm is not None:
+        comm.close()
+        torch.distributed.destroy_process_group()
+
+
+def permute_bench(sb, dev, L, n, reps=3):
+    """dist.cpp:237-266: copy xyztsc into every n-slice of tnsxyzc (complex<double>)."""
+    d0 = [L, L, L, L, 4, 3]
+    d1 = [L, n, 4, L, L, L, 3]
+    a = torch.empty(vol(d0), dtype=torch.complex128, device=dev)
+    fill(a, 7)
+    b = torch.empty(vol(d1), dtype=torch.complex128, device=dev)
+    p0, p1 = [([0] * 6, d0)], [([0] * 7, d1)]
+
+    def run():
+        for k in range(n):
+            sb.copy(1.0, p0, "xyztsc", [0] * 6, d0, d0, [a], p1, "tnsxyzc", [0, k, 0, 0, 0, 0, 0],
+                    d1, [b])
+    run()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        run()
+    e.record()
+    torch.cuda.synchronize()
+    t = s.elapsed_time(e) / 1e3 / reps
+    gbps = 32.0 * vol(d1) / t / 1e9
+    return {"permute_GBps": round(gbps, 1), "permute_frac_hbm": round(gbps / PEAK_HBM_GBPS, 4),
+            "permute_ms": round(t * 1e3, 3)}
+
+
+def bsr_bench(sb, dev, L, ncols=12, reps=5):
+    """config 3: 16^4 periodic 9-point stencil, 3x3 blocks, complex<double>."""
+    dim = [L, L, L, L, 1, 3]
+    V = L ** 4
+    sites = np.array(np.unravel_index(np.arange(V), (L, L, L, L))).T
+    jj = np.zeros((V, 9, 6), np.int32)
+    jj[:, 0, :4] = sites
+    k = 1
+    for d in range(4):
+        for s in (-1, 1):
+            c = sites.copy()
+            c[:, d] = (c[:, d] + s) % L
+            jj[:, k, :4] = c
+            k += 1
+    ii = np.full(V, 9, np.int32)
+    vals = torch.empty(V * 9 * 9, dtype=torch.complex128, device=dev)
+    fill(vals, 9)
+    full = [([0] * 6, dim)]
+    op = sb.create_bsr(full, dim, full, dim, [1, 1, 1, 1, 1, 3], [1, 1, 1, 1, 1, 3], False,
+                       [torch.from_numpy(ii).to(dev)], [torch.from_numpy(jj.reshape(-1)).to(dev)],
+                       [vals])
+    dimx = [1, L, L, L, L, 1, 3, ncols]
+    x = torch.empty(vol(dimx), dtype=torch.complex128, device=dev)
+    fill(x, 10)
+    y = torch.empty_like(x)
+    px = [([0] * 8, dimx)]
+
+    def run():
+        sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", px, "pXYZTSCn", [0] * 8, dimx, dimx, [x], 0.0,
+                      px, "pxyztscn", [0] * 8, dimx, dimx, "p", [y])
+    run()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        run()
+    e.record()
+    torch.cuda.synchronize()
+    t = s.elapsed_time(e) / 1e3 / reps
+    flops = 8.0 * 81 * V * ncols
+    bytes_ = 16.0 * (81 * V + 2 * 3 * V * ncols) + 4.0 * (9 * V + V + 1)
+    op.destroy()
+    return {"bsr_GFLOPs": round(flops / t / 1e9, 1), "bsr_GBps": round(bytes_ / t / 1e9, 1),
+            "bsr_ncols": ncols, "bsr_ms": round(t * 1e3, 4)}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,167 @@
+/*
+ * sbx.h -- C ABI of superbblas_amd, the MI355X-native implementation of superbblas's
+ * distributed tensor-contraction hot path.
+ *
+ * This is the drop-in boundary.  The reference (eromero-vlc/superbblas) exposes a header-only
+ * C++ template API (include/superbblas.h); `include/superbblas.h` in this repository keeps those
+ * exact template signatures and flattens the compile-time ranks into the runtime descriptors
+ * below.  Every entry point returns SBX_OK (0) on success or a negative status; the message of
+ * the last failure is available from sbx_last_error() (the C++ layer rethrows it as
+ * std::runtime_error, matching the reference's error behaviour, platform.h:226-243).
+ *
+ * Conventions shared by all entry points
+ *  - Coordinates and sizes are `int` (reference `IndexType`, tensor.h:47-52).
+ *  - A partition array for a tensor of rank N is `nprocs*ncomponents` items of {from[N],size[N]},
+ *    i.e. the memory image of `std::vector<PartitionItem<N>>` (dist.h:39-45, 3251-3261).
+ *  - Labels are strings of one character per dimension (tensor.h:265-276).
+ *  - `co` is SBX_SLOW_TO_FAST or SBX_FAST_TO_SLOW (tensor.h:56-60).
+ *  - Scalars (alpha, beta) are passed as two doubles {re, im}; the imaginary part is ignored
+ *    for real types.
+ *  - Tensor data pointers are caller-owned device (or host) pointers; the library never frees
+ *    them (blas.h:268-269).  All GPU work is enqueued on the library stream of each device
+ *    (platform.h:448-467); call sbx_sync() before reading results on the host.
+ *  - `comm` is NULL for a single process (reference SelfComm, dist.h:142-149) or a communicator
+ *    created by sbx_comm_create (replaces MPI_Comm; RCCL over xGMI underneath).
+ *  - `session` must be 0 (cache.h:269).  Masks are not supported (pass NULL).
+ */
+#ifndef SUPERBBLAS_AMD_SBX_H
+#define SUPERBBLAS_AMD_SBX_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SBX_OK 0
+#define SBX_ERROR (-1)
+
+/* Scalar types (reference supported_type, blas.h:57-65 / performance.h:29-48) */
+enum sbx_dtype { SBX_FLOAT = 0, SBX_DOUBLE = 1, SBX_CFLOAT = 2, SBX_CDOUBLE = 3, SBX_INT = 4, SBX_SIZE_T = 5 };
+/* CoorOrder (tensor.h:56-60) */
+enum sbx_coor_order { SBX_SLOW_TO_FAST = 0, SBX_FAST_TO_SLOW = 1 };
+/* CopyAdd (tensor.h:62-66) */
+enum sbx_copy_add { SBX_COPY = 0, SBX_ADD = 1 };
+/* MatrixLayout (bsr.h:28-31) */
+enum sbx_matrix_layout { SBX_ROW_MAJOR = 0, SBX_COLUMN_MAJOR = 1 };
+/* platform (platform.h:105-109); CUDA does not exist here, HIP == GPU */
+enum sbx_platform { SBX_CPU = 0, SBX_GPU = 1 };
+
+/* Context{plat, device} (platform.h:757-773) */
+typedef struct sbx_context {
+    int plat;
+    int device;
+} sbx_context;
+
+typedef struct sbx_comm_s *sbx_comm; /* replaces MPI_Comm (dist.h:120-149) */
+typedef struct sbx_bsr_s *sbx_bsr;   /* replaces BSR_handle* (bsr.h:34-52) */
+
+/* ---- errors / runtime (platform.h:757-841, blas.h:965-988, alloc.h:398-443) ---- */
+
+/* Message of the last failed call on this thread */
+const char *sbx_last_error(void);
+/* Library version {major, minor} (version.h:4-5) */
+int sbx_version(int *major, int *minor);
+/* getGpuDevicesCount (platform.h:818-825) */
+int sbx_get_gpu_devices_count(int *n);
+/* sync(Context) (blas.h:965-974) */
+int sbx_sync(sbx_context ctx);
+/* The stream all work of `device` is enqueued on (getGpuAllocStream, platform.h:448-467) */
+int sbx_stream_get(int device, void **stream);
+/* Replace the library stream of `device` by a caller-owned hipStream_t (NULL restores the default) */
+int sbx_stream_set(int device, void *stream);
+/* clearCaches (alloc.h:437-443): release cached plans and scratch memory */
+int sbx_clear_caches(void);
+/* clearHandles (platform.h:828-838): destroy library streams and communicator handles */
+int sbx_clear_handles(void);
+/* allocate / deallocate (alloc.h:398-430) on a context */
+int sbx_allocate(unsigned long long bytes, sbx_context ctx, void **ptr);
+int sbx_deallocate(void *ptr, sbx_context ctx);
+
+/* ---- communicator (replaces MPI; dist.h:1426-1773 send_receive) ---- */
+
+/* Fill `id` (128 bytes) with a fresh RCCL unique id; call on one rank and broadcast it */
+int sbx_comm_unique_id(unsigned char *id);
+/* Create the communicator of `nprocs` ranks; `device` is this rank's GPU */
+int sbx_comm_create(int nprocs, int rank, const unsigned char *id, int device, sbx_comm *comm);
+int sbx_comm_rank(sbx_comm comm, int *rank, int *nprocs);
+int sbx_comm_destroy(sbx_comm comm);
+
+/* ---- partitioning helpers (dist.h:3318-3509, 3744-3825) ---- */
+
+/* partitioning_distributed_procs (dist.h:3318-3383): procs[nd] out */
+int sbx_partitioning_distributed_procs(int nd, const char *order, const int *dim,
+                                       const char *dist_labels, int nprocs, int *procs);
+/* basic_partitioning(order, dim, procs, dist_labels, nprocs, ncomponents) (dist.h:3393-3460);
+   out must hold max(nprocs, prod(procs))*ncomponents items of 2*nd ints */
+int sbx_basic_partitioning(int nd, const char *order, const int *dim, const int *procs,
+                           const char *dist_labels, int nprocs, int ncomponents, int *out);
+/* basic_partitioning(dim, procs, nprocs, replicate, ext_power) (dist.h:3475-3509) */
+int sbx_basic_partitioning_ext(int nd, const int *dim, const int *procs, int nprocs,
+                               int replicate, const int *ext_power, int *out);
+/* make_hole(from, size, hole_from, hole_size, dim) (dist.h:3802-3825); out holds up to nd
+   items of 2*nd ints, *nout receives the count */
+int sbx_make_hole(int nd, const int *from, const int *size, const int *hole_from,
+                  const int *hole_size, const int *dim, int *out, int *nout);
+
+/* ---- copy (dist.h:3583-3602 no-MPI / 3534-3558 MPI) ----
+   v1[from1 + P(c - from0)] (=|+=) alpha * v0[c] for c in [from0, from0+size0) (periodic),
+   P maps labels o0 -> o1; t0 -> t1 element conversion. */
+int sbx_copy(int nd0, int nd1, const double *alpha, int t0, int t1,
+             const int *p0, int ncomponents0, const char *o0, const int *from0, const int *size0,
+             const int *dim0, const void *const *v0, const sbx_context *ctx0,
+             const int *p1, int ncomponents1, const char *o1, const int *from1, const int *dim1,
+             void *const *v1, const sbx_context *ctx1, sbx_comm comm, int co, int copyadd,
+             int session);
+
+/* ---- contraction (dist.h:3701-3731 no-MPI / 3628-3662 MPI) ----
+   vr = alpha * sum_{labels in o0 and o1, not in o_r} conj?(v0) conj?(v1) + beta * vr */
+int sbx_contraction(int nd0, int nd1, int ndr, int t, const double *alpha,
+                    const int *p0, const int *from0, const int *size0, const int *dim0,
+                    int ncomponents0, const char *o0, int conj0, const void *const *v0,
+                    const sbx_context *ctx0,
+                    const int *p1, const int *from1, const int *size1, const int *dim1,
+                    int ncomponents1, const char *o1, int conj1, const void *const *v1,
+                    const sbx_context *ctx1, const double *beta,
+                    const int *pr, const int *fromr, const int *sizer, const int *dimr,
+                    int ncomponentsr, const char *o_r, void *const *vr, const sbx_context *ctxr,
+                    sbx_comm comm, int co, int session);
+
+/* ---- BSR operator (bsr.h:2440-2454 create_bsr, 2516-2543 bsr_krylov, 2495 destroy_bsr,
+   2554-2580 bsr_get_preferred_layout) ----
+   ii[c]: number of nonzero blocks of each block row of component c (not a prefix sum);
+   jj[c]: nd ints per nonzero block, the domain coordinate of the block relative to the domain
+   partition's `from` (a -1 first coordinate skips the block, ELL form). */
+int sbx_create_bsr(int nd, int ni, int t, const int *pim, const int *dimi, const int *pdm,
+                   const int *dimd, int ncomponents, const int *blockim, const int *blockdm,
+                   int blockImFast, const int *const *ii, const int *const *jj,
+                   const void *const *v, const sbx_context *ctx, sbx_comm comm, int co,
+                   sbx_bsr *bsrh, int session);
+int sbx_bsr_krylov(sbx_bsr bsrh, int nd, int ni, int nx, int ny, int t, const double *alpha,
+                   const char *oim, const char *odm, const int *px, int ncomponents,
+                   const char *ox, const int *fromx, const int *sizex, const int *dimx,
+                   const void *const *vx, const double *beta, const int *py, const char *oy,
+                   const int *fromy, const int *sizey, const int *dimy, char okr,
+                   void *const *vy, const sbx_context *ctx, sbx_comm comm, int co, int session);
+int sbx_bsr_get_preferred_layout(sbx_bsr bsrh, int ncomponents, const sbx_context *ctx,
+                                 sbx_comm comm, int co, int *layout_x, int *layout_y);
+int sbx_destroy_bsr(sbx_bsr bsrh);
+
+/* ---- kernel-level entry points (the local hot path, for direct callers and benchmarks) ---- */
+
+/* xgemm_batch_strided (blas.h:662-810; CPU blas_cpu_tmpl.hpp:376-478): BLAS column-major,
+   transa/transb in {'N','T','C'} */
+int sbx_xgemm_batch_strided(int t, char transa, char transb, int m, int n, int k,
+                            const double *alpha, const void *a, int lda, long long stridea,
+                            const void *b, int ldb, long long strideb, const double *beta,
+                            void *c, int ldc, long long stridec, int batch, int device);
+
+/* local_copy on one device (tensor.h:1055-1129): single component copy with labels */
+int sbx_local_copy(int nd0, int nd1, const double *alpha, int t0, int t1, const char *o0,
+                   const int *from0, const int *size0, const int *dim0, const void *v0,
+                   const char *o1, const int *from1, const int *dim1, void *v1, int co,
+                   int copyadd, int device);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SUPERBBLAS_AMD_SBX_H */

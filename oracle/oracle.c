@@ -1,0 +1,363 @@
+/*
+ * oracle.c -- CPU restatement of superbblas's algorithms for the hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (superbblas_amd/, include/) links or calls
+ * this file; only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use it, as the
+ * checker.  It is pinned against the real reference (header-only superbblas compiled from
+ * /root/reference by oracle/Makefile into oracle/_ref/, linked with the OpenBLAS that ships in
+ * this image) through the golden fixtures in tests/golden/ (tests/test_oracle_golden.py).
+ *
+ * Each function cites the reference lines it restates (eromero-vlc/superbblas @ 2025-03-02).
+ * Plain C99, complex arithmetic written out (re, im) so the evaluation order is explicit.
+ *
+ * Types: 0 float, 1 double, 2 complex<float>, 3 complex<double>, 4 int, 5 size_t
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+enum { T_FLOAT = 0, T_DOUBLE = 1, T_CFLOAT = 2, T_CDOUBLE = 3, T_INT = 4, T_SIZE_T = 5 };
+
+static int is_complex(int t) { return t == T_CFLOAT || t == T_CDOUBLE; }
+static size_t elem_size(int t) {
+    switch (t) {
+    case T_FLOAT: return 4;
+    case T_DOUBLE: return 8;
+    case T_CFLOAT: return 8;
+    case T_CDOUBLE: return 16;
+    case T_INT: return 4;
+    default: return 8;
+    }
+}
+
+/* load element i of an array of type t as (re, im) doubles */
+static void load(int t, const void *p, long i, double *re, double *im) {
+    switch (t) {
+    case T_FLOAT: *re = ((const float *)p)[i]; *im = 0; break;
+    case T_DOUBLE: *re = ((const double *)p)[i]; *im = 0; break;
+    case T_CFLOAT: *re = ((const float *)p)[2 * i]; *im = ((const float *)p)[2 * i + 1]; break;
+    case T_CDOUBLE: *re = ((const double *)p)[2 * i]; *im = ((const double *)p)[2 * i + 1]; break;
+    case T_INT: *re = ((const int *)p)[i]; *im = 0; break;
+    default: *re = (double)((const uint64_t *)p)[i]; *im = 0; break;
+    }
+}
+static void store(int t, void *p, long i, double re, double im) {
+    switch (t) {
+    case T_FLOAT: ((float *)p)[i] = (float)re; break;
+    case T_DOUBLE: ((double *)p)[i] = re; break;
+    case T_CFLOAT: ((float *)p)[2 * i] = (float)re; ((float *)p)[2 * i + 1] = (float)im; break;
+    case T_CDOUBLE: ((double *)p)[2 * i] = re; ((double *)p)[2 * i + 1] = im; break;
+    case T_INT: ((int *)p)[i] = (int)re; break;
+    default: ((uint64_t *)p)[i] = (uint64_t)re; break;
+    }
+}
+
+/* strides of a dense array, SlowToFast (co=0) or FastToSlow (co=1) (tensor.h:282-297) */
+static void get_strides(int nd, const int *dim, int co, long *s) {
+    if (nd == 0) return;
+    if (co == 0) {
+        s[nd - 1] = 1;
+        for (int i = nd - 1; i >= 1; --i) s[i - 1] = s[i] * dim[i];
+    } else {
+        s[0] = 1;
+        for (int i = 1; i < nd; ++i) s[i] = s[i - 1] * dim[i - 1];
+    }
+}
+
+static long vol(int nd, const int *d) {
+    long v = 1;
+    for (int i = 0; i < nd; ++i) v *= d[i];
+    return v;
+}
+
+static int normalize_coor(long c, int dim) {
+    if (dim == 0) return 0;
+    long r = c % dim;
+    return (int)(r < 0 ? r + dim : r);
+}
+
+/*
+ * Single-component copy (the semantics of superbblas::copy for one component covering the
+ * whole tensor: dist.h:3583-3602 -> local_copy tensor.h:1055-1129 -> copy_n(_blocking)):
+ *   v1[(from1 + P(c - from0)) mod dim1] (=|+=) alpha * v0[(from0 + c) mod dim0],
+ *   c in [0, size0); labels of o1 missing in o0 take from1.
+ * With alpha == 1 the value is moved without a multiplication (copy_n.h:147-244 uses a plain
+ * assignment for alpha == 1); Add computes w + alpha*v.
+ */
+int oracle_copy(int nd0, int nd1, const double *alpha, int t0, int t1, const char *o0,
+                const int *from0, const int *size0, const int *dim0, const void *v0,
+                const char *o1, const int *from1, const int *dim1, void *v1, int co, int add) {
+    long s0[64], s1[64];
+    int perm[64]; /* perm[j]: position in o0 of label o1[j], or -1 */
+    if (nd0 > 64 || nd1 > 64) return -1;
+    get_strides(nd0, dim0, co, s0);
+    get_strides(nd1, dim1, co, s1);
+    for (int j = 0; j < nd1; ++j) {
+        perm[j] = -1;
+        for (int i = 0; i < nd0; ++i)
+            if (o0[i] == o1[j]) perm[j] = i;
+    }
+    const long n = vol(nd0, size0);
+    const int one = alpha[0] == 1 && alpha[1] == 0;
+    int cc[64];
+    for (long k = 0; k < n; ++k) {
+        /* decode k in FastToSlow order of size0 (get_permutation, tensor.h:815-845) */
+        long rem = k;
+        if (co == 0) {
+            for (int i = nd0 - 1; i >= 0; --i) {
+                cc[i] = (int)(rem % size0[i]);
+                rem /= size0[i];
+            }
+        } else {
+            for (int i = 0; i < nd0; ++i) {
+                cc[i] = (int)(rem % size0[i]);
+                rem /= size0[i];
+            }
+        }
+        long i0 = 0, i1 = 0;
+        for (int i = 0; i < nd0; ++i) i0 += (long)normalize_coor((long)from0[i] + cc[i], dim0[i]) * s0[i];
+        for (int j = 0; j < nd1; ++j) {
+            const long c = perm[j] >= 0 ? cc[perm[j]] : 0;
+            i1 += (long)normalize_coor((long)from1[j] + c, dim1[j]) * s1[j];
+        }
+        if (one && !add && t0 == t1) {
+            memcpy((char *)v1 + i1 * elem_size(t1), (const char *)v0 + i0 * elem_size(t0),
+                   elem_size(t0));
+            continue;
+        }
+        double re, im, wr = 0, wi = 0;
+        load(t0, v0, i0, &re, &im);
+        if (!one) {
+            const double r2 = alpha[0] * re - alpha[1] * im, i2 = alpha[0] * im + alpha[1] * re;
+            re = is_complex(t0) ? r2 : alpha[0] * re;
+            im = is_complex(t0) ? i2 : 0;
+        }
+        if (add) {
+            load(t1, v1, i1, &wr, &wi);
+            re += wr;
+            im += wi;
+        }
+        store(t1, v1, i1, re, im);
+    }
+    return 0;
+}
+
+/*
+ * Column-major strided batched GEMM (CPU xgemm_batch_strided, blas_cpu_tmpl.hpp:405-477:
+ * OpenMP over the batch, one GEMM per batch entry; GEMM semantics of BLAS ?gemm):
+ *   C_b = alpha * op(A_b) * op(B_b) + beta * C_b, beta == 0 overwrites C.
+ * Complex products are accumulated in the 4-multiplication form in k order.
+ */
+int oracle_xgemm_batch_strided(int t, char ta, char tb, int m, int n, int k, const double *alpha,
+                               const void *a, int lda, long sa, const void *b, int ldb, long sb,
+                               const double *beta, void *c, int ldc, long sc, int batch) {
+    const int cplx = is_complex(t);
+    const int tA = (ta == 'T' || ta == 't' || ta == 'C' || ta == 'c');
+    const int cA = (ta == 'C' || ta == 'c');
+    const int tB = (tb == 'T' || tb == 't' || tb == 'C' || tb == 'c');
+    const int cB = (tb == 'C' || tb == 'c');
+#pragma omp parallel for schedule(static)
+    for (int bb = 0; bb < batch; ++bb) {
+        for (int j = 0; j < n; ++j) {
+            for (int i = 0; i < m; ++i) {
+                double sr = 0, si = 0;
+                for (int kk = 0; kk < k; ++kk) {
+                    double ar, ai, br, bi;
+                    load(t, a, (long)bb * sa + (tA ? kk + (long)i * lda : i + (long)kk * lda), &ar, &ai);
+                    load(t, b, (long)bb * sb + (tB ? j + (long)kk * ldb : kk + (long)j * ldb), &br, &bi);
+                    if (cA) ai = -ai;
+                    if (cB) bi = -bi;
+                    sr += ar * br - ai * bi;
+                    si += ar * bi + ai * br;
+                }
+                const long ci = (long)bb * sc + i + (long)j * ldc;
+                double rr = alpha[0] * sr - (cplx ? alpha[1] * si : 0);
+                double ri = cplx ? alpha[0] * si + alpha[1] * sr : 0;
+                if (beta[0] != 0 || (cplx && beta[1] != 0)) {
+                    double cr, cim;
+                    load(t, c, ci, &cr, &cim);
+                    rr += beta[0] * cr - (cplx ? beta[1] * cim : 0);
+                    ri += cplx ? beta[0] * cim + beta[1] * cr : 0;
+                }
+                store(t, c, ci, rr, ri);
+            }
+        }
+    }
+    return 0;
+}
+
+/*
+ * Contraction of single-component tensors by labels (dist.h:3701-3731 -> contraction_normalized
+ * dist.h:3092-3196 -> local_contraction_normalized tensor.h:1475-1598), restated as the einsum it
+ * computes over the boxes [from, from+size) of each tensor (periodic):
+ *   vr[from_r + c_r] = alpha * sum_{c summed} conj?(v0[from0 + c0]) * conj?(v1[from1 + c1])
+ *                      + beta * vr[from_r + c_r]
+ * Labels in o0 and o1 but not in o_r are summed.  beta == 0 overwrites (tensor.h:1511-1512).
+ */
+int oracle_contraction(int t, int nd0, const char *o0, const int *from0, const int *size0,
+                       const int *dim0, int conj0, const void *v0, int nd1, const char *o1,
+                       const int *from1, const int *size1, const int *dim1, int conj1,
+                       const void *v1, int ndr, const char *o_r, const int *fromr,
+                       const int *sizer, const int *dimr, void *vr, const double *alpha,
+                       const double *beta, int co) {
+    /* all distinct labels and their sizes */
+    char lab[192];
+    int lsz[192], nl = 0;
+    const char *os[3] = {o0, o1, o_r};
+    const int nds[3] = {nd0, nd1, ndr};
+    const int *szs[3] = {size0, size1, sizer};
+    for (int q = 0; q < 3; ++q)
+        for (int i = 0; i < nds[q]; ++i) {
+            int f = -1;
+            for (int l = 0; l < nl; ++l)
+                if (lab[l] == os[q][i]) f = l;
+            if (f < 0) {
+                lab[nl] = os[q][i];
+                lsz[nl] = szs[q][i];
+                ++nl;
+            } else if (lsz[f] != szs[q][i]) {
+                return -2; /* some dimension does not match */
+            }
+        }
+    long s0[64], s1[64], sr[64];
+    get_strides(nd0, dim0, co, s0);
+    get_strides(nd1, dim1, co, s1);
+    get_strides(ndr, dimr, co, sr);
+    int p0[64], p1[64], pr[64];
+    for (int i = 0; i < nd0; ++i)
+        for (int l = 0; l < nl; ++l)
+            if (lab[l] == o0[i]) p0[i] = l;
+    for (int i = 0; i < nd1; ++i)
+        for (int l = 0; l < nl; ++l)
+            if (lab[l] == o1[i]) p1[i] = l;
+    for (int i = 0; i < ndr; ++i)
+        for (int l = 0; l < nl; ++l)
+            if (lab[l] == o_r[i]) pr[i] = l;
+    /* summed labels: not in o_r */
+    int summed[192], ns = 0, free_[192], nf = 0;
+    for (int l = 0; l < nl; ++l) {
+        int inr = 0;
+        for (int i = 0; i < ndr; ++i)
+            if (o_r[i] == lab[l]) inr = 1;
+        if (inr)
+            free_[nf++] = l;
+        else
+            summed[ns++] = l;
+    }
+    long nout = 1, nsum = 1;
+    for (int f = 0; f < nf; ++f) nout *= lsz[free_[f]];
+    for (int s = 0; s < ns; ++s) nsum *= lsz[summed[s]];
+    const int cplx = is_complex(t);
+#pragma omp parallel for schedule(static)
+    for (long o = 0; o < nout; ++o) {
+        int c[192];
+        long rem = o;
+        for (int f = nf - 1; f >= 0; --f) {
+            c[free_[f]] = (int)(rem % lsz[free_[f]]);
+            rem /= lsz[free_[f]];
+        }
+        double accr = 0, acci = 0;
+        for (long q = 0; q < nsum; ++q) {
+            long r2 = q;
+            for (int s = ns - 1; s >= 0; --s) {
+                c[summed[s]] = (int)(r2 % lsz[summed[s]]);
+                r2 /= lsz[summed[s]];
+            }
+            long i0 = 0, i1 = 0;
+            for (int i = 0; i < nd0; ++i)
+                i0 += (long)normalize_coor((long)from0[i] + c[p0[i]], dim0[i]) * s0[i];
+            for (int i = 0; i < nd1; ++i)
+                i1 += (long)normalize_coor((long)from1[i] + c[p1[i]], dim1[i]) * s1[i];
+            double ar, ai, br, bi;
+            load(t, v0, i0, &ar, &ai);
+            load(t, v1, i1, &br, &bi);
+            if (conj0) ai = -ai;
+            if (conj1) bi = -bi;
+            accr += ar * br - ai * bi;
+            acci += ar * bi + ai * br;
+        }
+        long ir = 0;
+        for (int i = 0; i < ndr; ++i)
+            ir += (long)normalize_coor((long)fromr[i] + c[pr[i]], dimr[i]) * sr[i];
+        double rr = alpha[0] * accr - (cplx ? alpha[1] * acci : 0);
+        double ri = cplx ? alpha[0] * acci + alpha[1] * accr : 0;
+        if (beta[0] != 0 || (cplx && beta[1] != 0)) {
+            double yr, yi;
+            load(t, vr, ir, &yr, &yi);
+            rr += beta[0] * yr - (cplx ? beta[1] * yi : 0);
+            ri += cplx ? beta[0] * yi + beta[1] * yr : 0;
+        }
+        store(t, vr, ir, rr, ri);
+    }
+    return 0;
+}
+
+/*
+ * BSR operator on one component (create_bsr -> get_bsr_indices bsr.h:1424-1468, builtin CPU
+ * operator bsr.h:535-650, no Kronecker):
+ *   ii[r]   number of nonzero blocks of block row r (not a prefix sum)
+ *   jj      nd ints per nonzero: domain coordinate of the block (periodic in dimd);
+ *           a first coordinate of -1 skips the block
+ *   v       blocks of bi x bd; element (row c, col e) at c*bd + e, or c + e*bi if block_im_fast
+ *   x       x(d, col): x[d*ldx + col] if x_row_major else x[d + col*ldx]
+ *   y       y(i, col) = alpha * sum A(i, d) x(d, col)   (overwritten; add=1 accumulates)
+ */
+int oracle_bsr(int t, int nd, const int *dimd, int co, long block_rows, int bi, int bd,
+               const int *ii, const int *jj, const void *v, int block_im_fast, const void *x,
+               long ldx, int x_row_major, void *y, long ldy, int y_row_major, long ncols,
+               const double *alpha, int add) {
+    long sd[64];
+    get_strides(nd, dimd, co, sd);
+    long *rowptr = (long *)malloc(sizeof(long) * (block_rows + 1));
+    rowptr[0] = 0;
+    for (long r = 0; r < block_rows; ++r) rowptr[r + 1] = rowptr[r] + ii[r];
+    const int cplx = is_complex(t);
+#pragma omp parallel for schedule(static)
+    for (long r = 0; r < block_rows; ++r) {
+        for (int c = 0; c < bi; ++c) {
+            for (long col = 0; col < ncols; ++col) {
+                double accr = 0, acci = 0;
+                for (long j = rowptr[r]; j < rowptr[r + 1]; ++j) {
+                    const int *cj = jj + j * nd;
+                    if (cj[0] == -1) continue; /* bsr.h:1453 */
+                    long d0 = 0;
+                    for (int q = 0; q < nd; ++q) d0 += (long)normalize_coor(cj[q], dimd[q]) * sd[q];
+                    for (int e = 0; e < bd; ++e) {
+                        double ar, ai, xr, xi;
+                        load(t, v, j * bi * bd + (block_im_fast ? c + (long)e * bi : (long)c * bd + e),
+                             &ar, &ai);
+                        const long d = d0 + e;
+                        load(t, x, x_row_major ? d * ldx + col : d + col * ldx, &xr, &xi);
+                        accr += ar * xr - ai * xi;
+                        acci += ar * xi + ai * xr;
+                    }
+                }
+                const long img = r * bi + c;
+                const long yi = y_row_major ? img * ldy + col : img + col * ldy;
+                double rr = alpha[0] * accr - (cplx ? alpha[1] * acci : 0);
+                double ri = cplx ? alpha[0] * acci + alpha[1] * accr : 0;
+                if (add) {
+                    double wr, wi;
+                    load(t, y, yi, &wr, &wi);
+                    rr += wr;
+                    ri += wi;
+                }
+                store(t, y, yi, rr, ri);
+            }
+        }
+    }
+    free(rowptr);
+    return 0;
+}
+
+int oracle_num_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}

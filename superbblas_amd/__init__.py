@@ -1,0 +1,432 @@
+"""superbblas_amd -- MI355X-native implementation of superbblas's distributed tensor
+contraction hot path.
+
+The product is the C-ABI shared library ``libsuperbblas_amd.so`` (HIP kernels for gfx950 +
+C++ planner + RCCL communicator, declared in ``include/superbblas_amd/sbx.h``).  C++ callers use
+the drop-in template header ``include/superbblas.h``; this module is the Python mirror of the
+same operator interface (``copy``, ``contraction``, ``create_bsr``/``bsr_krylov``/``destroy_bsr``,
+``basic_partitioning`` ...) over ``ctypes``, used by the tests and the benchmark.
+
+Reference interface: eromero-vlc/superbblas include/superbblas/dist.h:3534-3742 (copy,
+contraction), bsr.h:2269-2580 (BSR), dist.h:3264-3509 (partitioning), platform.h:757-841.
+
+PyTorch is plumbing only (device memory and streams).  There is no CPU fallback: importing the
+module fails loudly if the HIP library has not been built.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Iterable, List, Optional, Sequence, Tuple
+
+import torch  # noqa: F401  (load torch's HIP runtime before the library)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "libsuperbblas_amd.so")
+
+if not os.path.exists(_LIB_PATH):
+    raise ImportError(
+        "superbblas_amd: native library %s not found; run __graft_entry__.build() "
+        "(or `make -C superbblas_amd/csrc`) first" % _LIB_PATH)
+
+_lib = ctypes.CDLL(_LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+LIB_PATH = _LIB_PATH
+
+# ---- enums (tensor.h:56-66, bsr.h:28-31, platform.h:105-109) ----
+SlowToFast, FastToSlow = 0, 1
+Copy, Add = 0, 1
+RowMajor, ColumnMajor = 0, 1
+CPU, GPU = 0, 1
+FLOAT, DOUBLE, CFLOAT, CDOUBLE, INT, SIZE_T = range(6)
+
+_DTYPES = {
+    torch.float32: FLOAT,
+    torch.float64: DOUBLE,
+    torch.complex64: CFLOAT,
+    torch.complex128: CDOUBLE,
+    torch.int32: INT,
+    torch.int64: SIZE_T,
+    torch.uint64: SIZE_T,
+}
+
+
+class SuperbblasError(RuntimeError):
+    """Raised when a library call fails (the reference throws std::runtime_error)."""
+
+
+class _Ctx(ctypes.Structure):
+    _fields_ = [("plat", ctypes.c_int), ("device", ctypes.c_int)]
+
+
+_c_int_p = ctypes.POINTER(ctypes.c_int)
+_c_double_p = ctypes.POINTER(ctypes.c_double)
+_c_void_pp = ctypes.POINTER(ctypes.c_void_p)
+_ctx_p = ctypes.POINTER(_Ctx)
+
+_lib.sbx_last_error.restype = ctypes.c_char_p
+
+
+def _check(rc: int):
+    if rc != 0:
+        raise SuperbblasError(_lib.sbx_last_error().decode())
+
+
+def _ints(xs: Sequence[int]):
+    arr = (ctypes.c_int * max(1, len(xs)))(*[int(x) for x in xs])
+    return arr
+
+
+def _scalar(a) -> ctypes.Array:
+    a = complex(a)
+    return (ctypes.c_double * 2)(a.real, a.imag)
+
+
+def _partition(p: Sequence[Tuple[Sequence[int], Sequence[int]]], nd: int):
+    flat: List[int] = []
+    for item in p:
+        frm, size = item
+        if len(frm) != nd or len(size) != nd:
+            raise SuperbblasError("partition item with wrong rank")
+        flat += list(frm) + list(size)
+    return _ints(flat)
+
+
+def _ctx_of(t: torch.Tensor) -> _Ctx:
+    if t.is_cuda:
+        return _Ctx(GPU, t.device.index if t.device.index is not None else 0)
+    return _Ctx(CPU, -1)
+
+
+def _ptrs(ts: Sequence[torch.Tensor]):
+    return (ctypes.c_void_p * max(1, len(ts)))(*[t.data_ptr() for t in ts])
+
+
+def _ctxs(ts: Sequence[torch.Tensor]):
+    return (_Ctx * max(1, len(ts)))(*[_ctx_of(t) for t in ts])
+
+
+def _dtype_of(ts: Sequence[torch.Tensor]) -> int:
+    dts = {t.dtype for t in ts}
+    if len(dts) != 1:
+        raise SuperbblasError("all components of a tensor must have the same dtype")
+    dt = dts.pop()
+    if dt not in _DTYPES:
+        raise SuperbblasError("unsupported dtype %s" % dt)
+    return _DTYPES[dt]
+
+
+def _bind_stream(ts: Iterable[torch.Tensor]):
+    """Enqueue library work on torch's current stream of every device involved."""
+    devs = {t.device.index for t in ts if t.is_cuda}
+    for d in devs:
+        s = torch.cuda.current_stream(d).cuda_stream
+        _check(_lib.sbx_stream_set(d, ctypes.c_void_p(s)))
+
+
+def _check_sizes(p, rank, ncomp, v, what):
+    for i in range(ncomp):
+        frm, size = p[rank * ncomp + i]
+        n = 1
+        for s in size:
+            n *= s
+        if v[i].numel() < n or not v[i].is_contiguous():
+            raise SuperbblasError("%s: component %d has %d elements, the partition needs %d "
+                                  "(contiguous)" % (what, i, v[i].numel(), n))
+
+
+# ---------------------------------------------------------------------------------------------
+# runtime
+# ---------------------------------------------------------------------------------------------
+
+def version() -> Tuple[int, int]:
+    ma, mi = ctypes.c_int(), ctypes.c_int()
+    _check(_lib.sbx_version(ctypes.byref(ma), ctypes.byref(mi)))
+    return ma.value, mi.value
+
+
+def get_gpu_devices_count() -> int:
+    """getGpuDevicesCount (platform.h:818-825)"""
+    n = ctypes.c_int()
+    _check(_lib.sbx_get_gpu_devices_count(ctypes.byref(n)))
+    return n.value
+
+
+def sync(device: int = 0):
+    """sync(Context) (blas.h:965-974): wait for the library stream of `device`."""
+    _check(_lib.sbx_sync(_Ctx(GPU, device)))
+
+
+def stream(device: int = 0) -> int:
+    """hipStream_t the library uses for `device`."""
+    s = ctypes.c_void_p()
+    _check(_lib.sbx_stream_get(device, ctypes.byref(s)))
+    return s.value or 0
+
+
+def set_stream(device: int, hip_stream: Optional[int]):
+    _check(_lib.sbx_stream_set(device, ctypes.c_void_p(hip_stream or 0)))
+
+
+def clear_caches():
+    """clearCaches (alloc.h:437-443)"""
+    _check(_lib.sbx_clear_caches())
+
+
+# ---------------------------------------------------------------------------------------------
+# communicator (replaces MPI_Comm; RCCL underneath)
+# ---------------------------------------------------------------------------------------------
+
+class Comm:
+    """A communicator over `nprocs` processes, one GPU each (RCCL over xGMI)."""
+
+    def __init__(self, nprocs: int, rank: int, unique_id: bytes, device: int):
+        self.nprocs, self.rank, self.device = nprocs, rank, device
+        h = ctypes.c_void_p()
+        buf = (ctypes.c_ubyte * 128).from_buffer_copy(unique_id)
+        _check(_lib.sbx_comm_create(nprocs, rank, buf, device, ctypes.byref(h)))
+        self._h = h
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (ctypes.c_ubyte * 128)()
+        _check(_lib.sbx_comm_unique_id(buf))
+        return bytes(buf)
+
+    @classmethod
+    def from_torch_distributed(cls, device: int) -> "Comm":
+        """Create the communicator of the current torch.distributed group: rank 0 makes the
+        RCCL unique id and broadcasts it through the process group (any backend)."""
+        import torch.distributed as dist
+        rank, n = dist.get_rank(), dist.get_world_size()
+        obj = [cls.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        return cls(n, rank, obj[0], device)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if self._h:
+            _check(_lib.sbx_comm_destroy(self._h))
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _comm(comm: Optional[Comm]):
+    return comm.handle if comm is not None else None
+
+
+def _nprocs_rank(comm: Optional[Comm]):
+    return (comm.nprocs, comm.rank) if comm is not None else (1, 0)
+
+
+# ---------------------------------------------------------------------------------------------
+# partitioning helpers (dist.h:3264-3509, 3744-3825)
+# ---------------------------------------------------------------------------------------------
+
+def partitioning_distributed_procs(order: str, dim: Sequence[int], dist_labels: str,
+                                   nprocs: int) -> List[int]:
+    nd = len(dim)
+    out = _ints([0] * nd)
+    _check(_lib.sbx_partitioning_distributed_procs(nd, order.encode(), _ints(dim),
+                                                   dist_labels.encode(), nprocs, out))
+    return list(out[:nd])
+
+
+def basic_partitioning(order: Optional[str], dim: Sequence[int], procs: Sequence[int],
+                       dist_labels: Optional[str], nprocs: int = -1, ncomponents: int = 1):
+    """basic_partitioning(order, dim, procs, dist_labels, nprocs, ncomponents)"""
+    nd = len(dim)
+    vol = 1
+    for p in procs:
+        vol *= p
+    n = (vol if nprocs < 0 else nprocs) * ncomponents
+    out = _ints([0] * (n * 2 * nd))
+    _check(_lib.sbx_basic_partitioning(nd, order.encode() if order else None, _ints(dim),
+                                       _ints(procs), dist_labels.encode() if dist_labels else None,
+                                       nprocs, ncomponents, out))
+    return [(list(out[k * 2 * nd:k * 2 * nd + nd]), list(out[k * 2 * nd + nd:(k + 1) * 2 * nd]))
+            for k in range(n)]
+
+
+def basic_partitioning_ext(dim: Sequence[int], procs: Sequence[int], nprocs: int = -1,
+                           replicate: bool = False, ext_power: Optional[Sequence[int]] = None):
+    """basic_partitioning(dim, procs, nprocs, replicate, ext_power)"""
+    nd = len(dim)
+    vol = 1
+    for p in procs:
+        vol *= p
+    n = vol if nprocs < 0 else nprocs
+    out = _ints([0] * (n * 2 * nd))
+    _check(_lib.sbx_basic_partitioning_ext(nd, _ints(dim), _ints(procs), nprocs, int(replicate),
+                                           _ints(ext_power) if ext_power else None, out))
+    return [(list(out[k * 2 * nd:k * 2 * nd + nd]), list(out[k * 2 * nd + nd:(k + 1) * 2 * nd]))
+            for k in range(n)]
+
+
+def make_hole(frm, size, hole_from, hole_size, dim):
+    nd = len(dim)
+    out = _ints([0] * (nd * 2 * nd))
+    nout = ctypes.c_int()
+    _check(_lib.sbx_make_hole(nd, _ints(frm), _ints(size), _ints(hole_from), _ints(hole_size),
+                              _ints(dim), out, ctypes.byref(nout)))
+    return [(list(out[k * 2 * nd:k * 2 * nd + nd]), list(out[k * 2 * nd + nd:(k + 1) * 2 * nd]))
+            for k in range(nout.value)]
+
+
+# ---------------------------------------------------------------------------------------------
+# copy / contraction (dist.h:3534-3742)
+# ---------------------------------------------------------------------------------------------
+
+def copy(alpha, p0, o0: str, from0, size0, dim0, v0: Sequence[torch.Tensor], p1, o1: str, from1,
+         dim1, v1: Sequence[torch.Tensor], co: int = SlowToFast, copyadd: int = Copy,
+         comm: Optional[Comm] = None):
+    """v1[from1 + P(c - from0)] (=|+=) alpha * v0[c]  for c in [from0, from0 + size0)."""
+    nprocs, rank = _nprocs_rank(comm)
+    nd0, nd1 = len(o0), len(o1)
+    nc0, nc1 = len(v0), len(v1)
+    if len(p0) != nprocs * nc0 or len(p1) != nprocs * nc1:
+        raise SuperbblasError("partition is incompatible with the communicator/components")
+    _check_sizes(p0, rank, nc0, v0, "copy origin")
+    _check_sizes(p1, rank, nc1, v1, "copy destination")
+    _bind_stream(list(v0) + list(v1))
+    _check(_lib.sbx_copy(nd0, nd1, _scalar(alpha), _dtype_of(v0), _dtype_of(v1),
+                         _partition(p0, nd0), nc0, o0.encode(), _ints(from0), _ints(size0),
+                         _ints(dim0), _ptrs(v0), _ctxs(v0), _partition(p1, nd1), nc1, o1.encode(),
+                         _ints(from1), _ints(dim1), _ptrs(v1), _ctxs(v1), _comm(comm), co, copyadd,
+                         0))
+
+
+def contraction(alpha, p0, from0, size0, dim0, o0: str, conj0: bool, v0, p1, from1, size1, dim1,
+                o1: str, conj1: bool, v1, beta, pr, fromr, sizer, dimr, o_r: str, vr,
+                co: int = SlowToFast, comm: Optional[Comm] = None):
+    """vr = alpha * sum over the labels in o0 and o1 but not in o_r of v0 * v1 + beta * vr."""
+    nprocs, rank = _nprocs_rank(comm)
+    nd0, nd1, ndr = len(o0), len(o1), len(o_r)
+    nc0, nc1, ncr = len(v0), len(v1), len(vr)
+    for p, nc, what in ((p0, nc0, "v0"), (p1, nc1, "v1"), (pr, ncr, "vr")):
+        if len(p) != nprocs * nc:
+            raise SuperbblasError("%s: partition is incompatible with the communicator" % what)
+    _check_sizes(p0, rank, nc0, v0, "contraction v0")
+    _check_sizes(p1, rank, nc1, v1, "contraction v1")
+    _check_sizes(pr, rank, ncr, vr, "contraction vr")
+    t = _dtype_of(list(v0) + list(v1) + list(vr))
+    _bind_stream(list(v0) + list(v1) + list(vr))
+    _check(_lib.sbx_contraction(
+        nd0, nd1, ndr, t, _scalar(alpha),
+        _partition(p0, nd0), _ints(from0), _ints(size0), _ints(dim0), nc0, o0.encode(),
+        int(conj0), _ptrs(v0), _ctxs(v0),
+        _partition(p1, nd1), _ints(from1), _ints(size1), _ints(dim1), nc1, o1.encode(),
+        int(conj1), _ptrs(v1), _ctxs(v1), _scalar(beta),
+        _partition(pr, ndr), _ints(fromr), _ints(sizer), _ints(dimr), ncr, o_r.encode(),
+        _ptrs(vr), _ctxs(vr), _comm(comm), co, 0))
+
+
+def local_copy(alpha, o0: str, from0, size0, dim0, v0: torch.Tensor, o1: str, from1, dim1,
+               v1: torch.Tensor, co: int = SlowToFast, copyadd: int = Copy):
+    """Single-component copy on one device (tensor.h:1055-1129)."""
+    _bind_stream([v0, v1])
+    _check(_lib.sbx_local_copy(len(o0), len(o1), _scalar(alpha), _DTYPES[v0.dtype],
+                               _DTYPES[v1.dtype], o0.encode(), _ints(from0), _ints(size0),
+                               _ints(dim0), ctypes.c_void_p(v0.data_ptr()), o1.encode(),
+                               _ints(from1), _ints(dim1), ctypes.c_void_p(v1.data_ptr()), co,
+                               copyadd, v1.device.index or 0))
+
+
+def xgemm_batch_strided(transa: str, transb: str, m: int, n: int, k: int, alpha, a, lda: int,
+                        stridea: int, b, ldb: int, strideb: int, beta, c, ldc: int, stridec: int,
+                        batch: int):
+    """BLAS column-major strided batched GEMM (blas.h:662-810) on MFMA."""
+    _bind_stream([a, b, c])
+    _check(_lib.sbx_xgemm_batch_strided(
+        _DTYPES[c.dtype], ctypes.c_char(transa.encode()), ctypes.c_char(transb.encode()), m, n, k,
+        _scalar(alpha), ctypes.c_void_p(a.data_ptr()), lda, ctypes.c_longlong(stridea),
+        ctypes.c_void_p(b.data_ptr()), ldb, ctypes.c_longlong(strideb), _scalar(beta),
+        ctypes.c_void_p(c.data_ptr()), ldc, ctypes.c_longlong(stridec), batch,
+        c.device.index or 0))
+
+
+# ---------------------------------------------------------------------------------------------
+# BSR operator (bsr.h:2269-2580)
+# ---------------------------------------------------------------------------------------------
+
+class BSR:
+    """Handle of a block-sparse operator (BSR_handle, bsr.h:34-52).  Keeps references to the
+    nonzero values (they must stay alive until destroy, bsr.h:2284)."""
+
+    def __init__(self, handle, nd, ni, dtype, co, keep):
+        self._h, self.nd, self.ni, self.dtype, self.co, self._keep = handle, nd, ni, dtype, co, keep
+
+    @property
+    def handle(self):
+        return self._h
+
+    def destroy(self):
+        if self._h:
+            _check(_lib.sbx_destroy_bsr(self._h))
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+
+def create_bsr(pim, dimi, pdm, dimd, blockim, blockdm, block_im_fast: bool,
+               ii: Sequence[torch.Tensor], jj: Sequence[torch.Tensor],
+               v: Sequence[torch.Tensor], co: int = SlowToFast,
+               comm: Optional[Comm] = None) -> BSR:
+    """create_bsr<Nd,Ni,T> (bsr.h:2440-2454).  ii[c]: int32 nonzero blocks per block row;
+    jj[c]: int32 [nnz, Nd] domain coordinates; v[c]: nonzero blocks."""
+    nd, ni = len(dimd), len(dimi)
+    nc = len(v)
+    h = ctypes.c_void_p()
+    t = _dtype_of(v)
+    iip = (ctypes.c_void_p * nc)(*[x.data_ptr() for x in ii])
+    jjp = (ctypes.c_void_p * nc)(*[x.data_ptr() for x in jj])
+    _bind_stream(list(v))
+    _check(_lib.sbx_create_bsr(nd, ni, t, _partition(pim, ni), _ints(dimi), _partition(pdm, nd),
+                               _ints(dimd), nc, _ints(blockim), _ints(blockdm), int(block_im_fast),
+                               iip, jjp, _ptrs(v), _ctxs(v), _comm(comm), co, ctypes.byref(h), 0))
+    return BSR(h, nd, ni, t, co, (list(ii), list(jj), list(v)))
+
+
+def bsr_krylov(alpha, bsr: BSR, oim: str, odm: str, px, ox: str, fromx, sizex, dimx, vx, beta,
+               py, oy: str, fromy, sizey, dimy, okr: Optional[str], vy, co: int = SlowToFast,
+               comm: Optional[Comm] = None):
+    """y = alpha * A x (+ beta y) (bsr.h:2516-2543)."""
+    nx, ny = len(ox), len(oy)
+    nc = len(vx)
+    t = _dtype_of(list(vx) + list(vy))
+    _bind_stream(list(vx) + list(vy))
+    _check(_lib.sbx_bsr_krylov(
+        bsr.handle, bsr.nd, bsr.ni, nx, ny, t, _scalar(alpha), oim.encode(), odm.encode(),
+        _partition(px, nx), nc, ox.encode(), _ints(fromx), _ints(sizex), _ints(dimx), _ptrs(vx),
+        _scalar(beta), _partition(py, ny), oy.encode(), _ints(fromy), _ints(sizey), _ints(dimy),
+        ctypes.c_char((okr or "\0").encode()), _ptrs(vy), _ctxs(vx), _comm(comm), co, 0))
+
+
+def bsr_get_preferred_layout(bsr: BSR, ncomponents: int = 1, co: int = SlowToFast,
+                             comm: Optional[Comm] = None):
+    lx, ly = _ints([0] * ncomponents), _ints([0] * ncomponents)
+    ctxs = (_Ctx * ncomponents)(*[_Ctx(GPU, 0)] * ncomponents)
+    _check(_lib.sbx_bsr_get_preferred_layout(bsr.handle, ncomponents, ctxs, _comm(comm), co, lx,
+                                             ly))
+    return list(lx[:ncomponents]), list(ly[:ncomponents])
+
+
+__all__ = [
+    "SlowToFast", "FastToSlow", "Copy", "Add", "RowMajor", "ColumnMajor", "SuperbblasError",
+    "Comm", "copy", "contraction", "local_copy", "xgemm_batch_strided", "create_bsr",
+    "bsr_krylov", "bsr_get_preferred_layout", "basic_partitioning", "basic_partitioning_ext",
+    "partitioning_distributed_procs", "make_hole", "sync", "stream", "set_stream",
+    "clear_caches", "get_gpu_devices_count", "version", "LIB_PATH",
+]

@@ -1,0 +1,397 @@
+// BSR operator: creation and distributed application (bsr_krylov).
+//
+// Reference: create_bsr / get_bsr_components / get_bsr_indices (bsr.h:2440-2454, 1269-1354,
+// 1424-1468), local_bsr_krylov_check (bsr.h:1589-1943), get_output_partition and
+// detail::bsr_krylov (bsr.h:2020-2266).
+//  * the image partition `pi` says which rows each component owns; the domain partition `pd`
+//    (usually the image partition extended by the stencil halo) says which part of x each
+//    component reads;  x is brought to the domain partition (the halo exchange), each
+//    component runs the SpMM kernel, and the image pieces are copied/added into y.
+//  * x / y are used in place when their partition and layout already match (the common case
+//    of the lattice tests and the benchmarks); otherwise through temporaries.
+// Not yet supported (next tier): Kronecker BSR, powers > 1, contracting with
+// the image side of the operator (transposed application).
+#include "plan.h"
+
+#include <algorithm>
+
+namespace sbx {
+
+struct BsrComp {
+    int dev = -1;
+    long block_rows = 0;
+    int *ii = nullptr; // device CSR row pointers
+    int *jj = nullptr; // device first domain index per nonzero block
+    const void *v = nullptr;
+    int nnz_per_row = -1;
+};
+
+struct BsrOp {
+    int nd = 0, ni = 0, dtype = SBX_CDOUBLE;
+    Coor dimi, dimd, blocki, blockd;
+    bool block_im_fast = false;
+    int nprocs = 1, rank = 0, ncomponents = 1;
+    std::vector<std::vector<Range>> pi, pd; // SlowToFast, all ranks
+    std::vector<BsrComp> comps;             // this rank's components
+    int co = SBX_SLOW_TO_FAST;
+    ~BsrOp() {
+        for (auto &c : comps) {
+            if (c.dev >= 0) {
+                (void)hipSetDevice(c.dev);
+                (void)hipStreamSynchronize(get_stream(c.dev));
+            }
+            if (c.ii) (void)hipFree(c.ii);
+            if (c.jj) (void)hipFree(c.jj);
+        }
+    }
+};
+
+BsrOp *bsr_create(int nd, int ni, int dtype, const std::vector<std::vector<Range>> &pi,
+                  const Coor &dimi, const std::vector<std::vector<Range>> &pd, const Coor &dimd,
+                  const Coor &blocki, const Coor &blockd, bool block_im_fast,
+                  const std::vector<const int *> &ii, const std::vector<const int *> &jj,
+                  const std::vector<const void *> &v, const std::vector<int> &devs, bool reverse_jj,
+                  const Comm &comm) {
+    std::unique_ptr<BsrOp> op(new BsrOp());
+    op->nd = nd;
+    op->ni = ni;
+    op->dtype = dtype;
+    op->dimi = dimi;
+    op->dimd = dimd;
+    op->blocki = blocki;
+    op->blockd = blockd;
+    op->block_im_fast = block_im_fast;
+    op->nprocs = comm.nprocs;
+    op->rank = comm.rank;
+    op->pi = pi;
+    op->pd = pd;
+    const long bi = volume(blocki), bd = volume(blockd);
+    const int ncomp = (int)pi[comm.rank].size();
+    op->ncomponents = ncomp;
+    for (int c = 0; c < ncomp; ++c) {
+        BsrComp bc;
+        bc.dev = devs[c];
+        if (bc.dev < 0) throw Error("create_bsr: only GPU contexts are supported");
+        const Range &ri = pi[comm.rank][c], &rd = pd[comm.rank][c];
+        const long nii = bi > 0 ? volume(ri.size) / bi : 0;
+        bc.block_rows = nii;
+        bc.v = v[c];
+        if (nii == 0 || volume(rd.size) == 0) {
+            bc.block_rows = 0;
+            op->comps.push_back(bc);
+            continue;
+        }
+        // ii: number of nonzero blocks per block row (host or device memory)
+        std::vector<int> hii(nii);
+        set_device(bc.dev);
+        SBX_HIP_CHECK(hipMemcpy(hii.data(), ii[c], sizeof(int) * nii, hipMemcpyDefault));
+        std::vector<int> rowptr(nii + 1, 0);
+        bool same = true;
+        for (long i = 0; i < nii; ++i) {
+            rowptr[i + 1] = rowptr[i] + hii[i];
+            same &= (hii[i] == hii[0]);
+        }
+        const long nnz = rowptr[nii];
+        bc.nnz_per_row = same ? hii[0] : -1;
+        std::vector<int> hjj_coor((std::size_t)nnz * nd);
+        if (nnz > 0)
+            SBX_HIP_CHECK(hipMemcpy(hjj_coor.data(), jj[c], sizeof(int) * nnz * nd,
+                                    hipMemcpyDefault));
+        // linear domain index of each block (get_bsr_indices, bsr.h:1451-1459): periodic
+        // coordinates over the component's domain dims
+        const std::vector<long> st = strides_slow_to_fast(rd.size);
+        std::vector<int> hjj(nnz);
+        bool minus_one = false;
+        for (long k = 0; k < nnz; ++k) {
+            const int *cc = &hjj_coor[(std::size_t)k * nd];
+            const int first = cc[0]; // the user's first coordinate (bsr.h:1453)
+            if (first == -1) {
+                hjj[k] = -1;
+                minus_one = true;
+                continue;
+            }
+            long idx = 0;
+            for (int d = 0; d < nd; ++d) {
+                const int coor = reverse_jj ? cc[nd - 1 - d] : cc[d];
+                idx += (long)normalize_coor(coor, rd.size[d]) * st[d];
+            }
+            if (idx > 0x7fffffffL) throw Error("Ups! IndexType isn't big enough");
+            hjj[k] = (int)idx;
+        }
+        if (minus_one && !same)
+            throw Error("bsr: unsupported nonzero pattern specification, some domain coordinates "
+                        "have -1 but not all block rows have the same number of nonzero blocks");
+        SBX_HIP_CHECK(hipMalloc(&bc.ii, sizeof(int) * (nii + 1)));
+        SBX_HIP_CHECK(hipMalloc(&bc.jj, sizeof(int) * std::max(1L, nnz)));
+        SBX_HIP_CHECK(hipMemcpy(bc.ii, rowptr.data(), sizeof(int) * (nii + 1), hipMemcpyHostToDevice));
+        if (nnz > 0)
+            SBX_HIP_CHECK(hipMemcpy(bc.jj, hjj.data(), sizeof(int) * nnz, hipMemcpyHostToDevice));
+        op->comps.push_back(bc);
+    }
+    return op.release();
+}
+
+void bsr_destroy(BsrOp *op) { delete op; }
+
+namespace {
+
+struct Group {
+    bool ok;
+    long stride, vol;
+};
+Group group_of(const std::string &group, const std::string &labels, const Coor &size) {
+    const std::vector<long> st = strides_slow_to_fast(size);
+    Group g{true, 0, 1};
+    int prev = -1;
+    for (char c : group) {
+        auto i = labels.find(c);
+        if (i == std::string::npos) return Group{false, 0, 0};
+        if (size[i] == 1) continue;
+        g.vol *= size[i];
+        if (prev >= 0 && st[prev] != st[i] * (long)size[i]) g.ok = false;
+        prev = (int)i;
+    }
+    if (prev >= 0) g.stride = st[prev];
+    return g;
+}
+
+/// Dense layout of a (domain-or-image labels, C labels) array: row major (C fastest) or column
+/// major (C slowest); ld is the stride of the slow group
+struct Layout {
+    bool ok, row_major;
+    long ld;
+};
+Layout dense_layout(const std::string &spatial, const std::string &cl, const std::string &labels,
+                    const Coor &size) {
+    const Group gs = group_of(spatial, labels, size), gc = group_of(cl, labels, size);
+    if (!gs.ok || !gc.ok) return Layout{false, false, 0};
+    const long vs = gs.vol, vc = gc.vol;
+    if (vc <= 1) return Layout{gs.stride == 1 || vs <= 1, true, 1};
+    if (vs <= 1) return Layout{true, true, 1};
+    if (gc.stride == 1 && gs.stride == vc) return Layout{true, true, vc};
+    if (gs.stride == 1 && gc.stride == vs) return Layout{true, false, vs};
+    return Layout{false, false, 0};
+}
+
+} // namespace
+
+void bsr_krylov(const BsrOp &op, const Scalar &alpha, const std::string &oi,
+                const std::string &od, const DistTensor &x, const Coor &fromx, const Coor &sizex,
+                const Scalar &beta, const DistTensor &y, const Coor &fromy, const Coor &sizey,
+                char okr, const Comm &comm) {
+    if ((int)oi.size() != op.ni || (int)od.size() != op.nd)
+        throw Error("bsr_krylov: labels don't match the operator");
+    if (comm.nprocs != op.nprocs) throw Error("bsr_krylov: communicator mismatch");
+    // Label classes (bsr.h:1722-1795): x has domain labels + C (+ okr); y image labels + C (+okr)
+    std::string C;
+    for (int i = 0; i < x.nd(); ++i) {
+        const char c = x.labels[i];
+        if (od.find(c) != std::string::npos) {
+            if (sizex[i] != op.dimd[od.find(c)])
+                throw Error("bsr_krylov: dimensions of the dense input tensor doesn't match the "
+                            "sparse tensor");
+            continue;
+        }
+        if (oi.find(c) != std::string::npos)
+            throw Error("bsr_krylov: contracting with the image space is not supported yet");
+        if (okr != 0 && c == okr) {
+            if (sizex[i] > 1)
+                throw Error("The power dimension on the input vector has a size larger than one");
+            continue;
+        }
+        if (y.labels.find(c) == std::string::npos)
+            throw Error("Dimension label for the dense input vector doesn't match the input "
+                        "sparse dimensions nor the dense output dimensions");
+        C += c;
+    }
+    int power = 1;
+    for (int i = 0; i < y.nd(); ++i) {
+        const char c = y.labels[i];
+        if (oi.find(c) != std::string::npos) {
+            if (sizey[i] != op.dimi[oi.find(c)])
+                throw Error("bsr_krylov: dimensions of the dense output tensor doesn't match the "
+                            "sparse tensor");
+        } else if (okr != 0 && c == okr) {
+            power = sizey[i];
+        } else if (C.find(c) == std::string::npos) {
+            throw Error("Dimension label for the dense output vector doesn't match the input "
+                        "sparse dimensions nor the dense input dimensions");
+        } else if (sizey[i] != sizex[x.labels.find(c)]) {
+            throw Error("bsr_krylov: dimensions of the dense output tensor doesn't match");
+        }
+    }
+    if (power > 1) throw Error("bsr_krylov: powers larger than one are not supported yet");
+    for (int i = 0; i < op.nd; ++i)
+        if (op.blockd[i] > 1 && op.blockd[i] != op.dimd[i])
+            throw Error("Still not supported partially blocking a dimension");
+    if (x.dtype != op.dtype || y.dtype != op.dtype) throw Error("bsr_krylov: type mismatch");
+    const int dtype = op.dtype;
+    const std::size_t es = dtype_size(dtype);
+    const int bi = (int)volume(op.blocki), bd = (int)volume(op.blockd);
+
+    // Temporaries' layouts: row major (C fastest)
+    const std::string lx = od + C, ly = oi + C;
+    Coor sizeC(C.size());
+    for (std::size_t k = 0; k < C.size(); ++k) sizeC[k] = sizex[x.labels.find(C[k])];
+    const long volC = volume(sizeC);
+
+    // x_ / y_ in coordinates relative to the regions (domain coord d <-> x coord fromx + d)
+    DistTensor tx, ty;
+    tx.labels = lx;
+    ty.labels = ly;
+    tx.dim = op.dimd;
+    tx.dim.insert(tx.dim.end(), sizeC.begin(), sizeC.end());
+    ty.dim = op.dimi;
+    ty.dim.insert(ty.dim.end(), sizeC.begin(), sizeC.end());
+    tx.dtype = ty.dtype = dtype;
+    tx.ranges.resize(comm.nprocs);
+    ty.ranges.resize(comm.nprocs);
+    // needed x range of each component (in x coordinates) and direct-use decisions
+    struct CompPlan {
+        bool xdirect = false, ydirect = false;
+        int xi = -1, yi = -1;
+        Layout lxl{}, lyl{};
+    };
+    std::vector<std::vector<CompPlan>> plans(comm.nprocs);
+    std::vector<Scratch> bufs;
+    std::vector<void *> my_x, my_y;
+    std::vector<Layout> my_lx, my_ly;
+    for (int rk = 0; rk < comm.nprocs; ++rk) {
+        for (int c = 0; c < (int)op.pi[rk].size(); ++c) {
+            const Range &rd = op.pd[rk][c], &ri = op.pi[rk][c];
+            Range nx{rd.from, rd.size}, ny{ri.from, ri.size};
+            for (std::size_t k = 0; k < C.size(); ++k) {
+                nx.from.push_back(0);
+                nx.size.push_back(sizeC[k]);
+                ny.from.push_back(0);
+                ny.size.push_back(sizeC[k]);
+            }
+            CompPlan cp;
+            // x in place: same rank component whose range (shifted by fromx) equals nx
+            if (rk < (int)x.ranges.size())
+                for (int j = 0; j < (int)x.ranges[rk].size(); ++j) {
+                    const Range &r = x.ranges[rk][j];
+                    bool eq = true;
+                    for (int i = 0; i < x.nd() && eq; ++i) {
+                        const char l = x.labels[i];
+                        auto k = lx.find(l);
+                        if (k == std::string::npos) { // okr label
+                            eq = r.size[i] == 1 && r.from[i] == fromx[i];
+                            continue;
+                        }
+                        eq = r.size[i] == nx.size[k] &&
+                             normalize_coor((long)r.from[i] - fromx[i], x.dim[i]) == nx.from[k];
+                    }
+                    if (!eq) continue;
+                    Layout l = dense_layout(od, C, x.labels, r.size);
+                    if (!l.ok) continue;
+                    if (comm.nprocs == 1 && rk == comm.rank && x.dev[j] != op.comps[c].dev) continue;
+                    cp.xdirect = true;
+                    cp.xi = j;
+                    cp.lxl = l;
+                    break;
+                }
+            if (!cp.xdirect) tx.ranges[rk].push_back(nx);
+            if (rk < (int)y.ranges.size())
+                for (int j = 0; j < (int)y.ranges[rk].size(); ++j) {
+                    const Range &r = y.ranges[rk][j];
+                    bool eq = true;
+                    for (int i = 0; i < y.nd() && eq; ++i) {
+                        const char l = y.labels[i];
+                        auto k = ly.find(l);
+                        if (k == std::string::npos) {
+                            eq = r.size[i] == 1 && r.from[i] == fromy[i];
+                            continue;
+                        }
+                        eq = r.size[i] == ny.size[k] &&
+                             normalize_coor((long)r.from[i] - fromy[i], y.dim[i]) == ny.from[k];
+                    }
+                    if (!eq) continue;
+                    Layout l = dense_layout(oi, C, y.labels, r.size);
+                    if (!l.ok) continue;
+                    if (comm.nprocs == 1 && rk == comm.rank && y.dev[j] != op.comps[c].dev) continue;
+                    // the output region must be exactly this component and no other component
+                    // of y may overlap it (replicas need the copy path)
+                    cp.ydirect = y.ranges[rk].size() == 1 && comm.nprocs == 1;
+                    cp.yi = j;
+                    cp.lyl = l;
+                    break;
+                }
+            if (!cp.ydirect) ty.ranges[rk].push_back(ny);
+            if (rk == comm.rank) {
+                const int dev = op.comps[c].dev;
+                if (cp.xdirect) {
+                    my_x.push_back(x.ptr[cp.xi]);
+                    my_lx.push_back(cp.lxl);
+                } else {
+                    bufs.emplace_back(volume(nx.size) * es, dev);
+                    tx.ptr.push_back(bufs.back().ptr);
+                    tx.dev.push_back(dev);
+                    my_x.push_back(bufs.back().ptr);
+                    my_lx.push_back(Layout{true, true, volC});
+                }
+                if (cp.ydirect) {
+                    my_y.push_back(y.ptr[cp.yi]);
+                    my_ly.push_back(cp.lyl);
+                } else {
+                    bufs.emplace_back(volume(ny.size) * es, dev);
+                    ty.ptr.push_back(bufs.back().ptr);
+                    ty.dev.push_back(dev);
+                    my_y.push_back(bufs.back().ptr);
+                    my_ly.push_back(Layout{true, true, volC});
+                }
+            }
+            plans[rk].push_back(cp);
+        }
+    }
+
+    // Bring x to the domain partition (halo exchange)
+    bool need_x = false, need_y = false;
+    for (auto &r : tx.ranges) need_x |= !r.empty();
+    for (auto &r : ty.ranges) need_y |= !r.empty();
+    if (need_x) {
+        Coor from1(lx.size(), 0);
+        dist_copy(Scalar{1, 0}, x, fromx, sizex, tx, from1, false, comm);
+    }
+    // Output scaling for the in-place path
+    const bool direct_all = !need_y;
+    if (direct_all && !beta.is_zero() && !beta.is_one())
+        dist_copy(beta, y, fromy, sizey, y, fromy, false, comm);
+
+    // Local SpMM
+    for (int c = 0; c < (int)op.comps.size(); ++c) {
+        const BsrComp &bc = op.comps[c];
+        if (bc.block_rows == 0) continue;
+        BsrDesc d;
+        d.t = dtype;
+        d.block_rows = bc.block_rows;
+        d.bi = bi;
+        d.bd = bd;
+        d.ii = bc.ii;
+        d.jj = bc.jj;
+        d.v = bc.v;
+        d.block_im_fast = op.block_im_fast;
+        d.num_nnz_per_row = bc.nnz_per_row;
+        d.x = my_x[c];
+        d.x_row_major = my_lx[c].row_major;
+        d.ldx = my_lx[c].ld;
+        d.y = my_y[c];
+        d.y_row_major = my_ly[c].row_major;
+        d.ldy = my_ly[c].ld;
+        d.ncols = volC;
+        d.alpha = alpha;
+        d.add = plans[comm.rank][c].ydirect ? !beta.is_zero() : false;
+        launch_bsr(d, bc.dev);
+    }
+
+    // Copy/add the image pieces into y
+    if (need_y) {
+        if (!beta.is_zero() && !beta.is_one())
+            dist_copy(beta, y, fromy, sizey, y, fromy, false, comm);
+        Coor from0(ly.size(), 0), size0 = op.dimi;
+        size0.insert(size0.end(), sizeC.begin(), sizeC.end());
+        dist_copy(Scalar{1, 0}, ty, from0, size0, y, fromy, !beta.is_zero(), comm);
+    }
+}
+
+} // namespace sbx

@@ -1,0 +1,539 @@
+// extern "C" entry points (include/superbblas_amd/sbx.h).
+//
+// Converts the flat C descriptors into the planner's DistTensor form (SlowToFast internally),
+// mirrors host (CPU-context) components through device scratch so that every data movement
+// and every flop runs on the GPU, and turns C++ exceptions into status codes.
+#include "plan.h"
+
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <mutex>
+
+namespace sbx {
+BsrOp *bsr_create(int nd, int ni, int dtype, const std::vector<std::vector<Range>> &pi,
+                  const Coor &dimi, const std::vector<std::vector<Range>> &pd, const Coor &dimd,
+                  const Coor &blocki, const Coor &blockd, bool block_im_fast,
+                  const std::vector<const int *> &ii, const std::vector<const int *> &jj,
+                  const std::vector<const void *> &v, const std::vector<int> &devs, bool reverse_jj,
+                  const Comm &comm);
+void bsr_destroy(BsrOp *op);
+void bsr_krylov(const BsrOp &op, const Scalar &alpha, const std::string &oi,
+                const std::string &od, const DistTensor &x, const Coor &fromx, const Coor &sizex,
+                const Scalar &beta, const DistTensor &y, const Coor &fromy, const Coor &sizey,
+                char okr, const Comm &comm);
+void set_user_stream(int device, hipStream_t s);
+void destroy_streams();
+void trim_pools();
+} // namespace sbx
+
+struct sbx_comm_s {
+    sbx::Comm c;
+};
+struct sbx_bsr_s {
+    sbx::BsrOp *op = nullptr;
+    int co = SBX_SLOW_TO_FAST;
+    int nd = 0, ni = 0, dtype = 0;
+};
+
+using namespace sbx;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+template <typename F> int guard(F &&f) {
+    try {
+        f();
+        return SBX_OK;
+    } catch (const std::exception &e) {
+        g_last_error = e.what();
+    } catch (...) {
+        g_last_error = "unknown error";
+    }
+    return SBX_ERROR;
+}
+
+Coor to_coor(const int *p, int n, bool rev) {
+    Coor c(n);
+    for (int i = 0; i < n; ++i) c[i] = p ? p[rev ? n - 1 - i : i] : 0;
+    return c;
+}
+
+std::string to_labels(const char *o, int n, bool rev, const char *what) {
+    if (!o) throw Error(std::string(what) + ": null labels");
+    if ((int)std::strlen(o) != n)
+        throw Error(std::string("the length of `") + what +
+                    "` doesn't match the template parameter");
+    std::string s(o, n);
+    if (rev) std::reverse(s.begin(), s.end());
+    for (int i = 0; i < n; ++i)
+        for (int j = i + 1; j < n; ++j)
+            if (s[i] == s[j]) throw Error(std::string(what) + " has repeated labels");
+    return s;
+}
+
+Comm get_comm(sbx_comm c) { return c ? c->c : Comm{}; }
+
+/// Partition array -> ranges per rank (dist.h:3251-3261)
+std::vector<std::vector<Range>> to_ranges(const int *p, int nd, int ncomponents, const Comm &comm,
+                                          bool rev) {
+    if (!p) throw Error("null partition");
+    if (ncomponents < 1) throw Error("invalid number of components");
+    std::vector<std::vector<Range>> r(comm.nprocs);
+    for (int rk = 0; rk < comm.nprocs; ++rk)
+        for (int c = 0; c < ncomponents; ++c) {
+            const int *item = p + (std::size_t)(rk * ncomponents + c) * 2 * nd;
+            Range x{to_coor(item, nd, rev), to_coor(item + nd, nd, rev)};
+            if (volume(x.size) == 0) {
+                x.from.assign(nd, 0);
+                x.size.assign(nd, 0);
+            }
+            r[rk].push_back(x);
+        }
+    return r;
+}
+
+/// Host components are mirrored through device scratch; this keeps the record to copy back
+struct Mirror {
+    std::vector<Scratch> bufs;
+    struct Back {
+        void *host;
+        void *dev;
+        std::size_t bytes;
+        int device;
+    };
+    std::vector<Back> back;
+    int device = 0;
+    bool any = false;
+};
+
+int pick_device(std::initializer_list<std::pair<const sbx_context *, int>> ctxs, const Comm &comm) {
+    if (comm.device >= 0) return comm.device;
+    for (auto &c : ctxs)
+        for (int i = 0; i < c.second; ++i)
+            if (c.first[i].plat == SBX_GPU) return c.first[i].device;
+    return 0;
+}
+
+DistTensor make_tensor(int nd, const char *o, const int *dim, const int *p, int ncomponents,
+                       const void *const *v, const sbx_context *ctx, int dtype, const Comm &comm,
+                       bool rev, Mirror &mirror, bool is_output, const char *what) {
+    DistTensor t;
+    t.labels = to_labels(o, nd, rev, what);
+    t.dim = to_coor(dim, nd, rev);
+    t.dtype = dtype;
+    t.ranges = to_ranges(p, nd, ncomponents, comm, rev);
+    for (int i = 0; i < nd; ++i)
+        if (t.dim[i] < 0) throw Error("negative dimension");
+    for (int c = 0; c < ncomponents; ++c) {
+        const Range &r = t.ranges[comm.rank][c];
+        for (int i = 0; i < nd; ++i)
+            if (r.size[i] > t.dim[i] || r.from[i] < 0 || (t.dim[i] > 0 && r.from[i] >= t.dim[i] && r.size[i] > 0))
+                throw Error(std::string(what) + ": invalid partition");
+        const std::size_t bytes = volume(r.size) * dtype_size(dtype);
+        void *ptr = const_cast<void *>(v ? v[c] : nullptr);
+        if (ctx[c].plat == SBX_GPU) {
+            t.ptr.push_back(ptr);
+            t.dev.push_back(ctx[c].device);
+        } else {
+            // host component: mirror to the device
+            mirror.any = true;
+            mirror.bufs.emplace_back(bytes, mirror.device);
+            void *d = mirror.bufs.back().ptr;
+            if (bytes > 0) {
+                set_device(mirror.device);
+                SBX_HIP_CHECK(hipMemcpyAsync(d, ptr, bytes, hipMemcpyHostToDevice,
+                                             get_stream(mirror.device)));
+            }
+            if (is_output && bytes > 0) mirror.back.push_back({ptr, d, bytes, mirror.device});
+            t.ptr.push_back(d);
+            t.dev.push_back(mirror.device);
+        }
+    }
+    return t;
+}
+
+void finish_mirror(Mirror &m) {
+    if (!m.any) return;
+    for (auto &b : m.back) {
+        set_device(b.device);
+        SBX_HIP_CHECK(
+            hipMemcpyAsync(b.host, b.dev, b.bytes, hipMemcpyDeviceToHost, get_stream(b.device)));
+    }
+    set_device(m.device);
+    SBX_HIP_CHECK(hipStreamSynchronize(get_stream(m.device)));
+}
+
+Scalar to_scalar(const double *a) { return a ? Scalar{a[0], a[1]} : Scalar{1, 0}; }
+
+void check_session(int session) {
+    if (session != 0) throw Error("only session 0 is supported");
+}
+
+} // namespace
+
+extern "C" {
+
+const char *sbx_last_error(void) { return g_last_error.c_str(); }
+
+int sbx_version(int *major, int *minor) {
+    return guard([&] {
+        if (major) *major = 0;
+        if (minor) *minor = 2;
+    });
+}
+
+int sbx_get_gpu_devices_count(int *n) {
+    return guard([&] {
+        int c = 0;
+        if (hipGetDeviceCount(&c) != hipSuccess) {
+            (void)hipGetLastError();
+            c = 0;
+        }
+        *n = c;
+    });
+}
+
+int sbx_sync(sbx_context ctx) {
+    return guard([&] {
+        if (ctx.plat != SBX_GPU) return;
+        set_device(ctx.device);
+        SBX_HIP_CHECK(hipStreamSynchronize(get_stream(ctx.device)));
+    });
+}
+
+int sbx_stream_get(int device, void **stream) {
+    return guard([&] { *stream = (void *)get_stream(device); });
+}
+
+int sbx_stream_set(int device, void *stream) {
+    return guard([&] { set_user_stream(device, (hipStream_t)stream); });
+}
+
+int sbx_clear_caches(void) {
+    return guard([&] { trim_pools(); });
+}
+
+int sbx_clear_handles(void) {
+    return guard([&] { destroy_streams(); });
+}
+
+int sbx_allocate(unsigned long long bytes, sbx_context ctx, void **ptr) {
+    return guard([&] {
+        if (ctx.plat == SBX_GPU) {
+            set_device(ctx.device);
+            SBX_HIP_CHECK(hipMalloc(ptr, bytes));
+        } else {
+            SBX_HIP_CHECK(hipHostMalloc(ptr, bytes, hipHostMallocDefault));
+        }
+    });
+}
+
+int sbx_deallocate(void *ptr, sbx_context ctx) {
+    return guard([&] {
+        if (!ptr) return;
+        if (ctx.plat == SBX_GPU) {
+            set_device(ctx.device);
+            SBX_HIP_CHECK(hipStreamSynchronize(get_stream(ctx.device)));
+            SBX_HIP_CHECK(hipFree(ptr));
+        } else {
+            SBX_HIP_CHECK(hipHostFree(ptr));
+        }
+    });
+}
+
+int sbx_comm_unique_id(unsigned char *id) {
+    return guard([&] {
+        ncclUniqueId u;
+        ncclResult_t r = ncclGetUniqueId(&u);
+        if (r != ncclSuccess) throw Error(std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+        static_assert(sizeof(ncclUniqueId) == 128, "unexpected ncclUniqueId size");
+        std::memcpy(id, &u, sizeof(u));
+    });
+}
+
+int sbx_comm_create(int nprocs, int rank, const unsigned char *id, int device, sbx_comm *comm) {
+    return guard([&] {
+        if (nprocs < 1 || rank < 0 || rank >= nprocs) throw Error("invalid rank/nprocs");
+        std::unique_ptr<sbx_comm_s> c(new sbx_comm_s());
+        c->c.nprocs = nprocs;
+        c->c.rank = rank;
+        c->c.device = device;
+        if (nprocs > 1) {
+            set_device(device);
+            ncclUniqueId u;
+            std::memcpy(&u, id, sizeof(u));
+            ncclComm_t nc;
+            ncclResult_t r = ncclCommInitRank(&nc, nprocs, u, rank);
+            if (r != ncclSuccess)
+                throw Error(std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+            c->c.nccl = nc;
+        }
+        *comm = c.release();
+    });
+}
+
+int sbx_comm_rank(sbx_comm comm, int *rank, int *nprocs) {
+    return guard([&] {
+        const Comm c = get_comm(comm);
+        if (rank) *rank = c.rank;
+        if (nprocs) *nprocs = c.nprocs;
+    });
+}
+
+int sbx_comm_destroy(sbx_comm comm) {
+    return guard([&] {
+        if (!comm) return;
+        if (comm->c.nccl) ncclCommDestroy((ncclComm_t)comm->c.nccl);
+        delete comm;
+    });
+}
+
+int sbx_partitioning_distributed_procs(int nd, const char *order, const int *dim,
+                                       const char *dist_labels, int nprocs, int *procs) {
+    return guard([&] {
+        Coor p = partitioning_distributed_procs(std::string(order, nd), to_coor(dim, nd, false),
+                                                dist_labels ? dist_labels : "", (unsigned)nprocs);
+        for (int i = 0; i < nd; ++i) procs[i] = p[i];
+    });
+}
+
+int sbx_basic_partitioning(int nd, const char *order, const int *dim, const int *procs,
+                           const char *dist_labels, int nprocs, int ncomponents, int *out) {
+    return guard([&] {
+        auto r = basic_partitioning(order, to_coor(dim, nd, false), to_coor(procs, nd, false),
+                                    dist_labels, nprocs, ncomponents);
+        for (std::size_t k = 0; k < r.size(); ++k)
+            for (int i = 0; i < nd; ++i) {
+                out[k * 2 * nd + i] = r[k].from[i];
+                out[k * 2 * nd + nd + i] = r[k].size[i];
+            }
+    });
+}
+
+int sbx_basic_partitioning_ext(int nd, const int *dim, const int *procs, int nprocs,
+                               int replicate, const int *ext_power, int *out) {
+    return guard([&] {
+        auto r = basic_partitioning_ext(to_coor(dim, nd, false), to_coor(procs, nd, false), nprocs,
+                                        replicate != 0,
+                                        ext_power ? to_coor(ext_power, nd, false) : Coor(nd, 0));
+        for (std::size_t k = 0; k < r.size(); ++k)
+            for (int i = 0; i < nd; ++i) {
+                out[k * 2 * nd + i] = r[k].from[i];
+                out[k * 2 * nd + nd + i] = r[k].size[i];
+            }
+    });
+}
+
+int sbx_make_hole(int nd, const int *from, const int *size, const int *hole_from,
+                  const int *hole_size, const int *dim, int *out, int *nout) {
+    return guard([&] {
+        auto r = make_hole(Range{to_coor(from, nd, false), to_coor(size, nd, false)},
+                           Range{to_coor(hole_from, nd, false), to_coor(hole_size, nd, false)},
+                           to_coor(dim, nd, false));
+        if ((int)r.size() > nd) throw Error("make_hole: unexpected number of pieces");
+        for (std::size_t k = 0; k < r.size(); ++k)
+            for (int i = 0; i < nd; ++i) {
+                out[k * 2 * nd + i] = r[k].from[i];
+                out[k * 2 * nd + nd + i] = r[k].size[i];
+            }
+        *nout = (int)r.size();
+    });
+}
+
+int sbx_copy(int nd0, int nd1, const double *alpha, int t0, int t1, const int *p0,
+             int ncomponents0, const char *o0, const int *from0, const int *size0, const int *dim0,
+             const void *const *v0, const sbx_context *ctx0, const int *p1, int ncomponents1,
+             const char *o1, const int *from1, const int *dim1, void *const *v1,
+             const sbx_context *ctx1, sbx_comm comm, int co, int copyadd, int session) {
+    return guard([&] {
+        check_session(session);
+        const Comm c = get_comm(comm);
+        const bool rev = co == SBX_FAST_TO_SLOW;
+        Mirror m;
+        m.device = pick_device({{ctx0, ncomponents0}, {ctx1, ncomponents1}}, c);
+        DistTensor a = make_tensor(nd0, o0, dim0, p0, ncomponents0, v0, ctx0, t0, c, rev, m, false, "o0");
+        DistTensor b = make_tensor(nd1, o1, dim1, p1, ncomponents1, (const void *const *)v1, ctx1,
+                                   t1, c, rev, m, true, "o1");
+        dist_copy(to_scalar(alpha), a, to_coor(from0, nd0, rev), to_coor(size0, nd0, rev), b,
+                  to_coor(from1, nd1, rev), copyadd == SBX_ADD, c);
+        finish_mirror(m);
+    });
+}
+
+int sbx_local_copy(int nd0, int nd1, const double *alpha, int t0, int t1, const char *o0,
+                   const int *from0, const int *size0, const int *dim0, const void *v0,
+                   const char *o1, const int *from1, const int *dim1, void *v1, int co,
+                   int copyadd, int device) {
+    return guard([&] {
+        const bool rev = co == SBX_FAST_TO_SLOW;
+        DistTensor a, b;
+        a.labels = to_labels(o0, nd0, rev, "o0");
+        a.dim = to_coor(dim0, nd0, rev);
+        a.dtype = t0;
+        a.ranges = {{Range{Coor(nd0, 0), a.dim}}};
+        a.ptr = {const_cast<void *>(v0)};
+        a.dev = {device};
+        b.labels = to_labels(o1, nd1, rev, "o1");
+        b.dim = to_coor(dim1, nd1, rev);
+        b.dtype = t1;
+        b.ranges = {{Range{Coor(nd1, 0), b.dim}}};
+        b.ptr = {v1};
+        b.dev = {device};
+        dist_copy(to_scalar(alpha), a, to_coor(from0, nd0, rev), to_coor(size0, nd0, rev), b,
+                  to_coor(from1, nd1, rev), copyadd == SBX_ADD, Comm{});
+    });
+}
+
+int sbx_contraction(int nd0, int nd1, int ndr, int t, const double *alpha, const int *p0,
+                    const int *from0, const int *size0, const int *dim0, int ncomponents0,
+                    const char *o0, int conj0, const void *const *v0, const sbx_context *ctx0,
+                    const int *p1, const int *from1, const int *size1, const int *dim1,
+                    int ncomponents1, const char *o1, int conj1, const void *const *v1,
+                    const sbx_context *ctx1, const double *beta, const int *pr,
+                    const int *fromr, const int *sizer, const int *dimr, int ncomponentsr,
+                    const char *o_r, void *const *vr, const sbx_context *ctxr, sbx_comm comm,
+                    int co, int session) {
+    return guard([&] {
+        check_session(session);
+        if (t != SBX_FLOAT && t != SBX_DOUBLE && t != SBX_CFLOAT && t != SBX_CDOUBLE)
+            throw Error("contraction: unsupported type");
+        const Comm c = get_comm(comm);
+        const bool rev = co == SBX_FAST_TO_SLOW;
+        Mirror m;
+        m.device = pick_device({{ctx0, ncomponents0}, {ctx1, ncomponents1}, {ctxr, ncomponentsr}}, c);
+        DistTensor a = make_tensor(nd0, o0, dim0, p0, ncomponents0, v0, ctx0, t, c, rev, m, false, "o0");
+        DistTensor b = make_tensor(nd1, o1, dim1, p1, ncomponents1, v1, ctx1, t, c, rev, m, false, "o1");
+        DistTensor r = make_tensor(ndr, o_r, dimr, pr, ncomponentsr, (const void *const *)vr, ctxr,
+                                   t, c, rev, m, true, "o_r");
+        dist_contraction(to_scalar(alpha), a, to_coor(from0, nd0, rev), to_coor(size0, nd0, rev),
+                         conj0 != 0, b, to_coor(from1, nd1, rev), to_coor(size1, nd1, rev),
+                         conj1 != 0, to_scalar(beta), r, to_coor(fromr, ndr, rev),
+                         to_coor(sizer, ndr, rev), c);
+        finish_mirror(m);
+    });
+}
+
+int sbx_create_bsr(int nd, int ni, int t, const int *pim, const int *dimi, const int *pdm,
+                   const int *dimd, int ncomponents, const int *blockim, const int *blockdm,
+                   int blockImFast, const int *const *ii, const int *const *jj,
+                   const void *const *v, const sbx_context *ctx, sbx_comm comm, int co,
+                   sbx_bsr *bsrh, int session) {
+    return guard([&] {
+        check_session(session);
+        const Comm c = get_comm(comm);
+        const bool rev = co == SBX_FAST_TO_SLOW;
+        std::vector<const int *> vii, vjj;
+        std::vector<const void *> vv;
+        std::vector<int> devs;
+        for (int i = 0; i < ncomponents; ++i) {
+            vii.push_back(ii[i]);
+            vjj.push_back(jj[i]);
+            vv.push_back(v[i]);
+            if (ctx[i].plat != SBX_GPU) throw Error("create_bsr: only GPU contexts are supported");
+            devs.push_back(ctx[i].device);
+        }
+        std::unique_ptr<sbx_bsr_s> h(new sbx_bsr_s());
+        h->op = bsr_create(nd, ni, t, to_ranges(pim, ni, ncomponents, c, rev), to_coor(dimi, ni, rev),
+                           to_ranges(pdm, nd, ncomponents, c, rev), to_coor(dimd, nd, rev),
+                           to_coor(blockim, ni, rev), to_coor(blockdm, nd, rev), blockImFast != 0,
+                           vii, vjj, vv, devs, rev, c);
+        h->co = co;
+        h->nd = nd;
+        h->ni = ni;
+        h->dtype = t;
+        *bsrh = h.release();
+    });
+}
+
+int sbx_bsr_krylov(sbx_bsr bsrh, int nd, int ni, int nx, int ny, int t, const double *alpha,
+                   const char *oim, const char *odm, const int *px, int ncomponents,
+                   const char *ox, const int *fromx, const int *sizex, const int *dimx,
+                   const void *const *vx, const double *beta, const int *py, const char *oy,
+                   const int *fromy, const int *sizey, const int *dimy, char okr,
+                   void *const *vy, const sbx_context *ctx, sbx_comm comm, int co, int session) {
+    return guard([&] {
+        check_session(session);
+        if (!bsrh || !bsrh->op) throw Error("bsr_krylov: invalid handle");
+        if (bsrh->nd != nd || bsrh->ni != ni || bsrh->dtype != t)
+            throw Error("Given BSR handle doesn't match the template parameters Nd, Ni, or T");
+        if (co != bsrh->co)
+            throw Error("Unsupported to use a different coordinate ordering that one used to "
+                        "create the matrix");
+        const Comm c = get_comm(comm);
+        const bool rev = co == SBX_FAST_TO_SLOW;
+        Mirror m;
+        m.device = pick_device({{ctx, ncomponents}}, c);
+        DistTensor x = make_tensor(nx, ox, dimx, px, ncomponents, vx, ctx, t, c, rev, m, false, "ox");
+        DistTensor y = make_tensor(ny, oy, dimy, py, ncomponents, (const void *const *)vy, ctx, t,
+                                   c, rev, m, true, "oy");
+        bsr_krylov(*bsrh->op, to_scalar(alpha), to_labels(oim, ni, rev, "oim"),
+                   to_labels(odm, nd, rev, "odm"), x, to_coor(fromx, nx, rev),
+                   to_coor(sizex, nx, rev), to_scalar(beta), y, to_coor(fromy, ny, rev),
+                   to_coor(sizey, ny, rev), okr, c);
+        finish_mirror(m);
+    });
+}
+
+int sbx_bsr_get_preferred_layout(sbx_bsr bsrh, int ncomponents, const sbx_context *ctx,
+                                 sbx_comm comm, int co, int *layout_x, int *layout_y) {
+    return guard([&] {
+        (void)ctx;
+        (void)comm;
+        (void)co;
+        if (!bsrh) throw Error("invalid handle");
+        for (int i = 0; i < ncomponents; ++i) {
+            layout_x[i] = SBX_ROW_MAJOR;
+            layout_y[i] = SBX_ROW_MAJOR;
+        }
+    });
+}
+
+int sbx_destroy_bsr(sbx_bsr bsrh) {
+    return guard([&] {
+        if (!bsrh) return;
+        bsr_destroy(bsrh->op);
+        delete bsrh;
+    });
+}
+
+int sbx_xgemm_batch_strided(int t, char transa, char transb, int m, int n, int k,
+                            const double *alpha, const void *a, int lda, long long stridea,
+                            const void *b, int ldb, long long strideb, const double *beta,
+                            void *c, int ldc, long long stridec, int batch, int device) {
+    return guard([&] {
+        auto norm = [](char x) {
+            if (x == 'n' || x == 'N') return 'N';
+            if (x == 't' || x == 'T') return 'T';
+            if (x == 'c' || x == 'C') return 'C';
+            throw Error("Not valid value of trans");
+        };
+        const char ta = norm(transa), tb = norm(transb);
+        GemmDesc d;
+        d.t = t;
+        d.m = m;
+        d.n = n;
+        d.k = k;
+        d.batch = batch;
+        d.a = a;
+        d.sa_m = ta == 'N' ? 1 : lda;
+        d.sa_k = ta == 'N' ? lda : 1;
+        d.sa_b = stridea;
+        d.conja = ta == 'C';
+        d.b = b;
+        d.sb_k = tb == 'N' ? 1 : ldb;
+        d.sb_n = tb == 'N' ? ldb : 1;
+        d.sb_b = strideb;
+        d.conjb = tb == 'C';
+        d.c = c;
+        d.sc_m = 1;
+        d.sc_n = ldc;
+        d.sc_b = stridec;
+        d.alpha = to_scalar(alpha);
+        d.beta = to_scalar(beta);
+        launch_gemm(d, device);
+    });
+}
+
+} // extern "C"

@@ -1,0 +1,362 @@
+// Local and distributed tensor contraction.
+//
+// Reference: suggested_orders_for_contraction + local_contraction_normalized
+// (tensor.h:1271-1598) and contraction_normalized / get_partitions_for_contraction
+// (dist.h:3039-3196).  The label classes are the reference's:
+//   T: in o0, o1 and o_r (batch);  A: in o0 and o1 only (summed);
+//   B: in o0 and o_r only;          C: in o1 and o_r only.
+// The reference maps a contraction onto one strided batched GEMM after permuting each operand
+// into a normalised order when needed.  The GEMM kernel here takes arbitrary strides for the
+// batch, row, column and summed groups (and conjugation of either operand), so an operand is
+// only copied when one of its label groups is not a single contiguous run of memory, or when
+// its distribution does not match the work partition.
+#include "plan.h"
+
+#include <algorithm>
+
+namespace sbx {
+
+namespace {
+
+struct GroupStride {
+    bool ok;
+    long stride, vol;
+};
+
+/// Stride/volume of a label group in a dense array; !ok if the group labels (in the given
+/// order, size-1 labels ignored) are not one contiguous run of memory
+GroupStride group_stride(const std::string &group, const std::string &labels, const Coor &size) {
+    const std::vector<long> st = strides_slow_to_fast(size);
+    GroupStride g{true, 0, 1};
+    int prev = -1;
+    for (char c : group) {
+        auto i = labels.find(c);
+        if (i == std::string::npos) throw Error("contraction: internal label error");
+        if (size[i] == 1) continue;
+        g.vol *= size[i];
+        if (prev >= 0 && st[prev] != st[i] * (long)size[i]) g.ok = false;
+        prev = (int)i;
+    }
+    if (prev >= 0) g.stride = st[prev];
+    return g;
+}
+
+Range translate(const Range &r, const std::string &la, const Coor &fromA, const Coor &dimA,
+                const std::string &lb, const Coor &fromB, const Coor &dimB) {
+    Range o{Coor(lb.size()), Coor(lb.size())};
+    for (std::size_t j = 0; j < lb.size(); ++j) {
+        auto i = la.find(lb[j]);
+        if (i == std::string::npos) {
+            o.from[j] = fromB[j];
+            o.size[j] = 1;
+        } else {
+            o.from[j] = normalize_coor(
+                (long)normalize_coor((long)r.from[i] - fromA[i] + dimA[i], dimA[i]) + fromB[j],
+                dimB[j]);
+            o.size[j] = r.size[i];
+        }
+    }
+    return o;
+}
+
+/// Reorder the entries of `c` (labels `from`) into labels `to`
+Coor reorder(const Coor &c, const std::string &from, const std::string &to) {
+    Coor r(to.size());
+    for (std::size_t j = 0; j < to.size(); ++j) r[j] = c[from.find(to[j])];
+    return r;
+}
+
+} // namespace
+
+void local_contraction(const Scalar &alpha, const Local &x, bool conjx, const Local &y,
+                       bool conjy, const Scalar &beta, const Local &r) {
+    // Label classes from the point of view of the GEMM: T batch, K summed, M rows (in x and r),
+    // N columns (in y and r).  Group orders: T, K, M as in x; N as in y.
+    std::string T, K, M, N;
+    for (char c : x.labels) {
+        const bool iny = y.labels.find(c) != std::string::npos;
+        const bool inr = r.labels.find(c) != std::string::npos;
+        if (iny && inr)
+            T += c;
+        else if (iny)
+            K += c;
+        else if (inr)
+            M += c;
+        else
+            throw Error("o0 has unmatched dimensions");
+    }
+    for (char c : y.labels) {
+        const bool inx = x.labels.find(c) != std::string::npos;
+        const bool inr = r.labels.find(c) != std::string::npos;
+        if (!inx && inr)
+            N += c;
+        else if (!inx)
+            throw Error("o1 has unmatched directions");
+    }
+    if (r.labels.size() != T.size() + M.size() + N.size())
+        throw Error("o_r has unmatched dimensions");
+    const auto gx_t = group_stride(T, x.labels, x.size), gx_k = group_stride(K, x.labels, x.size),
+               gx_m = group_stride(M, x.labels, x.size);
+    const auto gy_t = group_stride(T, y.labels, y.size), gy_k = group_stride(K, y.labels, y.size),
+               gy_n = group_stride(N, y.labels, y.size);
+    const auto gr_t = group_stride(T, r.labels, r.size), gr_m = group_stride(M, r.labels, r.size),
+               gr_n = group_stride(N, r.labels, r.size);
+    if (!(gx_t.ok && gx_k.ok && gx_m.ok && gy_t.ok && gy_k.ok && gy_n.ok && gr_t.ok && gr_m.ok &&
+          gr_n.ok))
+        throw Error("local_contraction: operands need reordering");
+    if (gx_t.vol != gy_t.vol || gx_t.vol != gr_t.vol || gx_k.vol != gy_k.vol ||
+        gx_m.vol != gr_m.vol || gy_n.vol != gr_n.vol)
+        throw Error("some dimension does not match");
+    if (x.dev != y.dev || x.dev != r.dev) throw Error("all arrays should be on the same device");
+    if (x.dtype != y.dtype || x.dtype != r.dtype) throw Error("contraction: mixed types");
+    GemmDesc d;
+    d.t = x.dtype;
+    d.m = gx_m.vol;
+    d.n = gy_n.vol;
+    d.k = gx_k.vol;
+    d.batch = gx_t.vol;
+    d.a = x.ptr;
+    d.sa_m = gx_m.stride;
+    d.sa_k = gx_k.stride;
+    d.sa_b = gx_t.stride;
+    d.conja = conjx;
+    d.b = y.ptr;
+    d.sb_k = gy_k.stride;
+    d.sb_n = gy_n.stride;
+    d.sb_b = gy_t.stride;
+    d.conjb = conjy;
+    d.c = r.ptr;
+    d.sc_m = gr_m.stride;
+    d.sc_n = gr_n.stride;
+    d.sc_b = gr_t.stride;
+    d.alpha = alpha;
+    d.beta = beta;
+    if (volume(x.size) == 0 || volume(y.size) == 0) d.k = 0;
+    launch_gemm(d, x.dev);
+}
+
+void dist_contraction(const Scalar &alpha, const DistTensor &v0, const Coor &from0,
+                      const Coor &size0, bool conj0, const DistTensor &v1, const Coor &from1,
+                      const Coor &size1, bool conj1, const Scalar &beta, const DistTensor &vr,
+                      const Coor &fromr, const Coor &sizer, const Comm &comm) {
+    // check_dimensions (tensor.h:623-646)
+    for (int i = 0; i < v0.nd(); ++i) {
+        auto j = v1.labels.find(v0.labels[i]);
+        if (j != std::string::npos && size1[j] != size0[i])
+            throw Error("some dimension does not match");
+        auto k = vr.labels.find(v0.labels[i]);
+        if (k != std::string::npos && sizer[k] != size0[i])
+            throw Error("some dimension does not match");
+    }
+    for (int i = 0; i < v1.nd(); ++i) {
+        auto k = vr.labels.find(v1.labels[i]);
+        if (k != std::string::npos && sizer[k] != size1[i])
+            throw Error("some dimension does not match");
+    }
+    for (int i = 0; i < vr.nd(); ++i)
+        if (v0.labels.find(vr.labels[i]) == std::string::npos &&
+            v1.labels.find(vr.labels[i]) == std::string::npos)
+            throw Error("o_r has unmatched dimensions");
+    for (int i = 0; i < v0.nd(); ++i)
+        if (v1.labels.find(v0.labels[i]) == std::string::npos &&
+            vr.labels.find(v0.labels[i]) == std::string::npos)
+            throw Error("o0 has unmatched dimensions");
+    for (int i = 0; i < v1.nd(); ++i)
+        if (v0.labels.find(v1.labels[i]) == std::string::npos &&
+            vr.labels.find(v1.labels[i]) == std::string::npos)
+            throw Error("o1 has unmatched directions");
+    if (v0.dtype != v1.dtype || v0.dtype != vr.dtype) throw Error("contraction: mixed types");
+
+    const int dtype = v0.dtype;
+    const std::size_t es = dtype_size(dtype);
+
+    // Work is partitioned like the larger operand (dist.h:3050-3056)
+    const bool swap = volume(size0) < volume(size1);
+    const DistTensor &X = swap ? v1 : v0, &Y = swap ? v0 : v1;
+    const Coor &fromX = swap ? from1 : from0, &sizeX = swap ? size1 : size0;
+    const Coor &fromY = swap ? from0 : from1, &sizeY = swap ? size0 : size1;
+    const bool conjX = swap ? conj1 : conj0, conjY = swap ? conj0 : conj1;
+
+    // Canonical group orders: T, K, M from X; N from Y
+    std::string T, K, M, N;
+    for (char c : X.labels) {
+        const bool iny = Y.labels.find(c) != std::string::npos;
+        const bool inr = vr.labels.find(c) != std::string::npos;
+        if (iny && inr)
+            T += c;
+        else if (iny)
+            K += c;
+        else
+            M += c;
+    }
+    for (char c : Y.labels)
+        if (X.labels.find(c) == std::string::npos) N += c;
+    const std::string lX = T + M + K, lY = T + N + K, lR = T + N + M; // temporaries' layouts
+
+    auto layout_ok = [&](const std::string &labels, const Coor &size,
+                         std::initializer_list<const std::string *> groups) {
+        for (const std::string *g : groups)
+            if (!group_stride(*g, labels, size).ok) return false;
+        return true;
+    };
+    auto same = [](const Range &a, const Range &b) { return a.from == b.from && a.size == b.size; };
+
+    // Pieces of the work: X's ranges restricted to the box, repetitions removed (dist.h:3001-3028)
+    struct WorkPiece {
+        int rank, comp;
+        Range px;        // in X coordinates (global)
+        Range py, pr;    // needed ranges of Y and of the output (global coordinates)
+        int ydirect = -1; // local Y component usable in place
+        bool xdirect = false;
+    };
+    std::vector<WorkPiece> work;
+    {
+        std::vector<Range> prev;
+        const Range box{fromX, sizeX};
+        for (int rk = 0; rk < comm.nprocs; ++rk) {
+            for (int i = 0; i < (int)X.ranges[rk].size(); ++i) {
+                const Range &rx = X.ranges[rk][i];
+                if (volume(rx.size) == 0) continue;
+                std::vector<Range> fs = intersection(box, rx, X.dim);
+                for (const Range &h : prev) {
+                    std::vector<Range> nfs;
+                    for (const Range &f : fs) {
+                        if (intersection(f, h, X.dim).empty())
+                            nfs.push_back(f);
+                        else {
+                            auto hh = make_hole(f, h, X.dim);
+                            nfs.insert(nfs.end(), hh.begin(), hh.end());
+                        }
+                    }
+                    fs.swap(nfs);
+                }
+                prev.push_back(rx);
+                for (const Range &f : fs) {
+                    if (volume(f.size) == 0) continue;
+                    WorkPiece w;
+                    w.rank = rk;
+                    w.comp = i;
+                    w.px = f;
+                    w.py = translate(f, X.labels, fromX, X.dim, Y.labels, fromY, Y.dim);
+                    for (int j = 0; j < Y.nd(); ++j)
+                        if (X.labels.find(Y.labels[j]) == std::string::npos) {
+                            w.py.from[j] = fromY[j];
+                            w.py.size[j] = sizeY[j];
+                        }
+                    w.pr = translate(f, X.labels, fromX, X.dim, vr.labels, fromr, vr.dim);
+                    for (int j = 0; j < vr.nd(); ++j)
+                        if (X.labels.find(vr.labels[j]) == std::string::npos) {
+                            const auto k = Y.labels.find(vr.labels[j]);
+                            w.pr.from[j] = fromr[j];
+                            w.pr.size[j] = sizeY[k];
+                        }
+                    // in-place use of X's component
+                    w.xdirect = same(f, rx) &&
+                                layout_ok(X.labels, rx.size, {&T, &M, &K});
+                    // in-place use of a Y component on the same rank
+                    for (int j = 0; j < (int)Y.ranges[rk].size(); ++j) {
+                        const Range &ry = Y.ranges[rk][j];
+                        if (same(w.py, ry) &&
+                            layout_ok(Y.labels, ry.size, {&T, &N, &K}) &&
+                            (comm.nprocs > 1 || rk != comm.rank || Y.dev[j] == X.dev[i])) {
+                            w.ydirect = j;
+                            break;
+                        }
+                    }
+                    work.push_back(w);
+                }
+            }
+        }
+    }
+
+    // Single-process, single piece whose output is exactly one component: GEMM in place with beta
+    if (comm.nprocs == 1 && work.size() == 1 && work[0].xdirect && work[0].ydirect >= 0 &&
+        vr.ranges[0].size() == 1 && same(work[0].pr, vr.ranges[0][0]) &&
+        layout_ok(vr.labels, vr.ranges[0][0].size, {&T, &N, &M}) &&
+        vr.dev[0] == X.dev[work[0].comp]) {
+        const WorkPiece &w = work[0];
+        Local lx{X.ptr[w.comp], X.dev[w.comp], X.ranges[0][w.comp].size, X.labels, dtype};
+        Local ly{Y.ptr[w.ydirect], Y.dev[w.ydirect], Y.ranges[0][w.ydirect].size, Y.labels, dtype};
+        Local lr{vr.ptr[0], vr.dev[0], vr.ranges[0][0].size, vr.labels, dtype};
+        local_contraction(alpha, lx, conjX, ly, conjY, beta, lr);
+        return;
+    }
+
+    // 1) vr <- beta * vr on the box (dist.h:3145-3146)
+    if (!beta.is_one()) dist_copy(beta, vr, fromr, sizer, vr, fromr, false, comm);
+    if (alpha.is_zero() || work.empty()) return;
+
+    // 2) temporaries for this rank's pieces; bring X / Y pieces that cannot be used in place
+    DistTensor tx, ty, tr;
+    tx.labels = lX;
+    tx.dim = reorder(X.dim, X.labels, lX);
+    ty.labels = lY;
+    ty.dim = reorder(Y.dim, Y.labels, lY);
+    tr.labels = lR;
+    tr.dim = reorder(vr.dim, vr.labels, lR);
+    tx.dtype = ty.dtype = tr.dtype = dtype;
+    tx.ranges.resize(comm.nprocs);
+    ty.ranges.resize(comm.nprocs);
+    tr.ranges.resize(comm.nprocs);
+    std::vector<Scratch> bufs;
+    struct LocalWork {
+        Local x, y, r;
+    };
+    std::vector<LocalWork> lw;
+    for (const WorkPiece &w : work) {
+        const bool mine = w.rank == comm.rank;
+        const int dev = mine ? X.dev[w.comp] : -1;
+        LocalWork l;
+        if (!w.xdirect) {
+            Range r{reorder(w.px.from, X.labels, lX), reorder(w.px.size, X.labels, lX)};
+            tx.ranges[w.rank].push_back(r);
+            if (mine) {
+                bufs.emplace_back(volume(r.size) * es, dev);
+                tx.ptr.push_back(bufs.back().ptr);
+                tx.dev.push_back(dev);
+                l.x = Local{bufs.back().ptr, dev, r.size, lX, dtype};
+            }
+        } else if (mine) {
+            l.x = Local{X.ptr[w.comp], dev, X.ranges[w.rank][w.comp].size, X.labels, dtype};
+        }
+        if (w.ydirect < 0) {
+            Range r{reorder(w.py.from, Y.labels, lY), reorder(w.py.size, Y.labels, lY)};
+            ty.ranges[w.rank].push_back(r);
+            if (mine) {
+                bufs.emplace_back(volume(r.size) * es, dev);
+                ty.ptr.push_back(bufs.back().ptr);
+                ty.dev.push_back(dev);
+                l.y = Local{bufs.back().ptr, dev, r.size, lY, dtype};
+            }
+        } else if (mine) {
+            l.y = Local{Y.ptr[w.ydirect], Y.dev[w.ydirect], Y.ranges[w.rank][w.ydirect].size,
+                        Y.labels, dtype};
+        }
+        {
+            Range r{reorder(w.pr.from, vr.labels, lR), reorder(w.pr.size, vr.labels, lR)};
+            tr.ranges[w.rank].push_back(r);
+            if (mine) {
+                bufs.emplace_back(volume(r.size) * es, dev);
+                tr.ptr.push_back(bufs.back().ptr);
+                tr.dev.push_back(dev);
+                l.r = Local{bufs.back().ptr, dev, r.size, lR, dtype};
+            }
+        }
+        if (mine) lw.push_back(l);
+    }
+    const Coor tfromX = reorder(fromX, X.labels, lX), tfromY = reorder(fromY, Y.labels, lY);
+    bool need_x = false, need_y = false;
+    for (auto &rk : tx.ranges) need_x |= !rk.empty();
+    for (auto &rk : ty.ranges) need_y |= !rk.empty();
+    if (need_x) dist_copy(Scalar{1, 0}, X, fromX, sizeX, tx, tfromX, false, comm);
+    if (need_y) dist_copy(Scalar{1, 0}, Y, fromY, sizeY, ty, tfromY, false, comm);
+
+    // 3) local contractions into the partial outputs
+    for (const LocalWork &l : lw) local_contraction(alpha, l.x, conjX, l.y, conjY, Scalar{0, 0}, l.r);
+
+    // 4) reduce the partial outputs into vr (dist.h:3183-3186)
+    const Coor tfromr = reorder(fromr, vr.labels, lR), tsizer = reorder(sizer, vr.labels, lR);
+    dist_copy(Scalar{1, 0}, tr, tfromr, tsizer, vr, fromr, true, comm);
+}
+
+} // namespace sbx

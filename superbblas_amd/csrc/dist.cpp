@@ -1,0 +1,420 @@
+// Distributed copy and contraction over partitioned tensors.
+//
+// Reference behaviour (restated, not translated):
+//  * copy_request (dist.h:2264-2438): every (origin component, destination component) pair
+//    copies the overlap of their ranges; the pieces on other ranks travel through the remap
+//    communicator; `Copy` zeroes destination elements without an origin (has_full_support,
+//    dist.h:666-700); `Add` adds the contribution of every origin component.
+//  * send_receive (dist.h:1426-1573): pack per destination rank -> MPI_Ialltoallv -> unpack.
+//    Here: pack kernels on the device stream -> RCCL grouped ncclSend/ncclRecv (an all-to-all
+//    with per-peer byte counts over xGMI) -> unpack kernels, all stream ordered: no host sync.
+//  * contraction_normalized (dist.h:3092-3196): scale the output by beta, partition the work
+//    like the larger operand (repetitions removed), bring the other operand to that partition,
+//    contract locally, reduce the partial outputs into the output with an Add copy.
+//
+// MI355X-specific choices:
+//  * `Copy` pieces are de-duplicated per destination (a replicated origin is read once, the
+//    local replica first), which gives the reference's values with less traffic.
+//  * operands already laid out so that every label group (T, contracted, free) is a single
+//    stride are used in place: no normalising copies (the reference's `reorder_tensor` copies
+//    whenever the order differs from its preferred one).
+//  * the common single-process case runs the GEMM directly into the output with beta.
+#include "plan.h"
+
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cassert>
+#include <map>
+
+namespace sbx {
+
+namespace {
+
+//
+// Helpers
+//
+
+/// Map coordinates of the copy region from tensor A (labels la) to tensor B (labels lb):
+/// cB = fromB + (cA - fromA) for common labels, fromB for labels only in B
+Range translate(const Range &r, const std::string &la, const Coor &fromA, const Coor &dimA,
+                const std::string &lb, const Coor &fromB, const Coor &dimB) {
+    Range o{Coor(lb.size()), Coor(lb.size())};
+    for (std::size_t j = 0; j < lb.size(); ++j) {
+        auto i = la.find(lb[j]);
+        if (i == std::string::npos) {
+            o.from[j] = fromB[j];
+            o.size[j] = 1;
+        } else {
+            o.from[j] = normalize_coor(
+                (long)normalize_coor((long)r.from[i] - fromA[i] + dimA[i], dimA[i]) + fromB[j],
+                dimB[j]);
+            o.size[j] = r.size[i];
+        }
+    }
+    if (volume(o.size) == 0) o.size.assign(lb.size(), 0);
+    return o;
+}
+
+/// One box to copy between two local arrays
+struct Piece {
+    int a, b;      // global component index of the origin / destination
+    Coor src_from; // local coordinates in the origin component (origin labels)
+    Coor dst_from; // local coordinates in the destination component (destination labels)
+    Coor size;     // in origin labels
+};
+
+struct CompRef {
+    int rank, idx; // rank and index within the rank
+};
+
+std::vector<CompRef> flatten_components(const DistTensor &t) {
+    std::vector<CompRef> r;
+    for (int rk = 0; rk < (int)t.ranges.size(); ++rk)
+        for (int i = 0; i < (int)t.ranges[rk].size(); ++i) r.push_back({rk, i});
+    return r;
+}
+
+/// Split a piece where its box wraps around the local (periodic, full-dimension) component
+void split_wraps(Piece p, const Coor &src_comp_size, const Coor &dst_comp_size,
+                 const std::vector<int> &perm_s2d, std::vector<Piece> &out) {
+    for (std::size_t k = 0; k < p.size.size(); ++k) {
+        if (p.src_from[k] + p.size[k] > src_comp_size[k]) {
+            const int t = src_comp_size[k] - p.src_from[k];
+            Piece p1 = p, p2 = p;
+            p1.size[k] = t;
+            p2.size[k] -= t;
+            p2.src_from[k] = 0;
+            if (perm_s2d[k] >= 0) {
+                const int kd = perm_s2d[k];
+                p2.dst_from[kd] = normalize_coor((long)p.dst_from[kd] + t, dst_comp_size[kd]);
+            }
+            split_wraps(p1, src_comp_size, dst_comp_size, perm_s2d, out);
+            split_wraps(p2, src_comp_size, dst_comp_size, perm_s2d, out);
+            return;
+        }
+    }
+    for (std::size_t k = 0; k < p.size.size(); ++k) {
+        if (perm_s2d[k] < 0) continue;
+        const int kd = perm_s2d[k];
+        if (p.dst_from[kd] + p.size[k] > dst_comp_size[kd]) {
+            const int t = dst_comp_size[kd] - p.dst_from[kd];
+            Piece p1 = p, p2 = p;
+            p1.size[k] = t;
+            p2.size[k] -= t;
+            p2.dst_from[kd] = 0;
+            p2.src_from[k] = normalize_coor((long)p.src_from[k] + t, src_comp_size[k]);
+            split_wraps(p1, src_comp_size, dst_comp_size, perm_s2d, out);
+            split_wraps(p2, src_comp_size, dst_comp_size, perm_s2d, out);
+            return;
+        }
+    }
+    out.push_back(p);
+}
+
+/// Plan all the pieces of a distributed copy (every rank computes the same global list)
+std::vector<Piece> plan_copy(const DistTensor &src, const Coor &from0, const Coor &size0,
+                             const DistTensor &dst, const Coor &from1, bool add, int my_rank) {
+    const std::vector<CompRef> sc = flatten_components(src), dc = flatten_components(dst);
+    // perm_s2d[k]: destination dim of origin dim k (-1 if absent)
+    std::vector<int> perm_s2d(src.nd(), -1);
+    for (int k = 0; k < src.nd(); ++k) {
+        auto j = dst.labels.find(src.labels[k]);
+        if (j != std::string::npos) perm_s2d[k] = (int)j;
+    }
+    const Range region0{from0, size0};
+
+    std::vector<Piece> out;
+    for (int bi = 0; bi < (int)dc.size(); ++bi) {
+        const Range &rb = dst.ranges[dc[bi].rank][dc[bi].idx];
+        if (volume(rb.size) == 0) continue;
+        // Origin components in priority order: same rank first (for Copy de-duplication)
+        std::vector<int> order(sc.size());
+        for (int i = 0; i < (int)sc.size(); ++i) order[i] = i;
+        if (!add) {
+            auto prio = [&](int x) {
+                if (sc[x].rank != dc[bi].rank) return 2;
+                return sc[x].idx == dc[bi].idx ? 0 : 1;
+            };
+            std::stable_sort(order.begin(), order.end(),
+                             [&](int x, int y) { return prio(x) < prio(y); });
+        }
+        std::vector<Range> covered; // destination global ranges already assigned (Copy)
+        for (int ai : order) {
+            const Range &ra = src.ranges[sc[ai].rank][sc[ai].idx];
+            if (volume(ra.size) == 0) continue;
+            for (const Range &s : intersection(region0, ra, src.dim)) {
+                const Range t =
+                    translate(s, src.labels, from0, src.dim, dst.labels, from1, dst.dim);
+                std::vector<Range> ds = intersection(t, rb, dst.dim);
+                if (!add) {
+                    // remove what other origins already provide
+                    for (const Range &cv : covered) {
+                        std::vector<Range> nds;
+                        for (const Range &d : ds) {
+                            if (intersection(d, cv, dst.dim).empty()) {
+                                nds.push_back(d);
+                            } else {
+                                auto h = make_hole(d, cv, dst.dim);
+                                nds.insert(nds.end(), h.begin(), h.end());
+                            }
+                        }
+                        ds.swap(nds);
+                    }
+                }
+                for (const Range &d : ds) {
+                    if (volume(d.size) == 0) continue;
+                    if (!add) covered.push_back(d);
+                    const Range sback =
+                        translate(d, dst.labels, from1, dst.dim, src.labels, from0, src.dim);
+                    Piece p;
+                    p.a = ai;
+                    p.b = bi;
+                    p.size.resize(src.nd());
+                    p.src_from.resize(src.nd());
+                    p.dst_from.resize(dst.nd());
+                    for (int k = 0; k < src.nd(); ++k) {
+                        p.size[k] = perm_s2d[k] >= 0 ? d.size[perm_s2d[k]] : 1;
+                        p.src_from[k] =
+                            normalize_coor((long)sback.from[k] - ra.from[k], src.dim[k]);
+                    }
+                    for (int k = 0; k < dst.nd(); ++k)
+                        p.dst_from[k] = normalize_coor((long)d.from[k] - rb.from[k], dst.dim[k]);
+                    split_wraps(p, ra.size, rb.size, perm_s2d, out);
+                }
+            }
+        }
+        (void)my_rank;
+    }
+    return out;
+}
+
+long offset_of(const Coor &from, const std::vector<long> &strides) {
+    long o = 0;
+    for (std::size_t i = 0; i < from.size(); ++i) o += (long)from[i] * strides[i];
+    return o;
+}
+
+/// Box copy between two local arrays on the same device
+void local_piece_copy(const Scalar &alpha, int src_t, const void *src, const Coor &src_size,
+                      const Coor &src_from, int dst_t, void *dst, const Coor &dst_size,
+                      const Coor &dst_from, const Coor &box, const std::vector<int> &perm_s2d,
+                      bool add, int device) {
+    const std::vector<long> ss = strides_slow_to_fast(src_size), ds = strides_slow_to_fast(dst_size);
+    BoxCopyDesc d;
+    d.src_t = src_t;
+    d.dst_t = dst_t;
+    d.src = (const char *)src + dtype_size(src_t) * offset_of(src_from, ss);
+    d.dst = (char *)dst + dtype_size(dst_t) * offset_of(dst_from, ds);
+    d.size.resize(box.size());
+    d.src_stride = ss;
+    d.dst_stride.resize(box.size());
+    for (std::size_t k = 0; k < box.size(); ++k) {
+        d.size[k] = box[k];
+        d.dst_stride[k] = perm_s2d[k] >= 0 ? ds[perm_s2d[k]] : 0;
+    }
+    d.alpha = alpha;
+    d.add = add;
+    launch_box_copy(d, device);
+}
+
+/// Cross-device stream ordering: make `to` wait for the work enqueued so far on `from`
+void stream_wait(int from, int to) {
+    if (from == to) return;
+    hipEvent_t ev;
+    set_device(from);
+    SBX_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    SBX_HIP_CHECK(hipEventRecord(ev, get_stream(from)));
+    set_device(to);
+    SBX_HIP_CHECK(hipStreamWaitEvent(get_stream(to), ev, 0));
+    SBX_HIP_CHECK(hipEventDestroy(ev));
+}
+
+void nccl_check(ncclResult_t r, const char *what) {
+    if (r != ncclSuccess)
+        throw Error(std::string("RCCL error in ") + what + ": " + ncclGetErrorString(r));
+}
+
+} // namespace
+
+//
+// Distributed copy
+//
+
+void dist_copy(const Scalar &alpha, const DistTensor &src, const Coor &from0, const Coor &size0,
+               const DistTensor &dst, const Coor &from1, bool add, const Comm &comm) {
+    if ((int)src.ranges.size() != comm.nprocs || (int)dst.ranges.size() != comm.nprocs)
+        throw Error("copy: partition is incompatible with the communicator");
+    if (src.nd() != (int)from0.size() || src.nd() != (int)size0.size() ||
+        dst.nd() != (int)from1.size())
+        throw Error("copy: invalid coordinates");
+    // check_isomorphic (tensor.h:495-507): origin labels absent in the destination have size 1
+    for (int k = 0; k < src.nd(); ++k) {
+        auto j = dst.labels.find(src.labels[k]);
+        if (j == std::string::npos) {
+            if (size0[k] > 1) throw Error("Invalid copy operation");
+        } else if (size0[k] > dst.dim[j]) {
+            throw Error("Invalid copy operation");
+        }
+    }
+    if (volume(size0) == 0) return;
+
+    const std::vector<CompRef> sc = flatten_components(src), dc = flatten_components(dst);
+    std::vector<int> perm_s2d(src.nd(), -1);
+    for (int k = 0; k < src.nd(); ++k) {
+        auto j = dst.labels.find(src.labels[k]);
+        if (j != std::string::npos) perm_s2d[k] = (int)j;
+    }
+
+    // Zero the destination region when copying (the reference zeroes it when the origin lacks
+    // full support, dist.h:2356-2382; zeroing always is equivalent and simpler)
+    const bool zero_all = !add && (alpha.is_zero());
+    const Range region1 = translate(Range{from0, size0}, src.labels, from0, src.dim, dst.labels,
+                                    from1, dst.dim);
+    // local destination components on this rank
+    auto zero_region = [&]() {
+        for (int i = 0; i < (int)dst.ranges[comm.rank].size(); ++i) {
+            const Range &rb = dst.ranges[comm.rank][i];
+            if (volume(rb.size) == 0) continue;
+            for (const Range &z : intersection(region1, rb, dst.dim)) {
+                Piece p;
+                p.size = z.size;
+                p.dst_from.resize(dst.nd());
+                for (int k = 0; k < dst.nd(); ++k)
+                    p.dst_from[k] = normalize_coor((long)z.from[k] - rb.from[k], dst.dim[k]);
+                p.src_from = p.dst_from;
+                std::vector<int> id(dst.nd());
+                for (int k = 0; k < dst.nd(); ++k) id[k] = k;
+                std::vector<Piece> ps;
+                split_wraps(p, rb.size, rb.size, id, ps);
+                for (const Piece &q : ps)
+                    local_piece_copy(Scalar{0, 0}, dst.dtype, dst.ptr[i], rb.size, q.dst_from,
+                                     dst.dtype, dst.ptr[i], rb.size, q.dst_from, q.size, id,
+                                     false, dst.dev[i]);
+            }
+        }
+    };
+    if (zero_all) {
+        zero_region();
+        return;
+    }
+
+    const std::vector<Piece> pieces = plan_copy(src, from0, size0, dst, from1, add, comm.rank);
+
+    if (!add) {
+        // Zero the part of the local destination not covered by any piece
+        bool full = true;
+        {
+            // covered volume per local destination component vs. region volume
+            std::vector<long> need(dst.ranges[comm.rank].size(), 0), got(need.size(), 0);
+            for (int i = 0; i < (int)need.size(); ++i) {
+                const Range &rb = dst.ranges[comm.rank][i];
+                if (volume(rb.size) == 0) continue;
+                for (const Range &z : intersection(region1, rb, dst.dim)) need[i] += volume(z.size);
+            }
+            for (const Piece &p : pieces)
+                if (dc[p.b].rank == comm.rank) got[dc[p.b].idx] += volume(p.size);
+            for (std::size_t i = 0; i < need.size(); ++i) full &= (need[i] == got[i]);
+        }
+        if (!full) zero_region();
+    }
+
+    // Local pieces
+    for (const Piece &p : pieces) {
+        const CompRef &ca = sc[p.a], &cb = dc[p.b];
+        if (ca.rank != comm.rank || cb.rank != comm.rank) continue;
+        const Range &ra = src.ranges[ca.rank][ca.idx];
+        const Range &rb = dst.ranges[cb.rank][cb.idx];
+        const int da = src.dev[ca.idx], db = dst.dev[cb.idx];
+        if (da == db) {
+            local_piece_copy(alpha, src.dtype, src.ptr[ca.idx], ra.size, p.src_from, dst.dtype,
+                             dst.ptr[cb.idx], rb.size, p.dst_from, p.size, perm_s2d, add, db);
+        } else {
+            // pack on the origin device, peer copy, unpack on the destination device
+            const long n = volume(p.size);
+            const std::size_t bytes = n * dtype_size(src.dtype);
+            Scratch sbuf(bytes, da);
+            std::vector<int> id(src.nd());
+            for (int k = 0; k < src.nd(); ++k) id[k] = k;
+            local_piece_copy(Scalar{1, 0}, src.dtype, src.ptr[ca.idx], ra.size, p.src_from,
+                             src.dtype, sbuf.ptr, p.size, Coor(src.nd(), 0), p.size, id, false, da);
+            Scratch dbuf(bytes, db);
+            stream_wait(da, db);
+            set_device(db);
+            SBX_HIP_CHECK(hipMemcpyPeerAsync(dbuf.ptr, db, sbuf.ptr, da, bytes, get_stream(db)));
+            local_piece_copy(alpha, src.dtype, dbuf.ptr, p.size, Coor(src.nd(), 0), dst.dtype,
+                             dst.ptr[cb.idx], rb.size, p.dst_from, p.size, perm_s2d, add, db);
+            stream_wait(db, da); // keep sbuf alive until the peer copy is done
+        }
+    }
+
+    if (comm.nprocs == 1) return;
+
+    // Remote pieces: pack per peer, RCCL all-to-all (grouped send/recv), unpack
+    const int device = comm.device;
+    const std::size_t es = dtype_size(src.dtype);
+    std::vector<std::size_t> send_bytes(comm.nprocs, 0), recv_bytes(comm.nprocs, 0);
+    for (const Piece &p : pieces) {
+        const CompRef &ca = sc[p.a], &cb = dc[p.b];
+        if (ca.rank == cb.rank) continue;
+        if (ca.rank == comm.rank) send_bytes[cb.rank] += volume(p.size) * es;
+        if (cb.rank == comm.rank) recv_bytes[ca.rank] += volume(p.size) * es;
+    }
+    std::vector<std::size_t> send_off(comm.nprocs + 1, 0), recv_off(comm.nprocs + 1, 0);
+    for (int q = 0; q < comm.nprocs; ++q) {
+        send_off[q + 1] = send_off[q] + (send_bytes[q] + 255) / 256 * 256;
+        recv_off[q + 1] = recv_off[q] + (recv_bytes[q] + 255) / 256 * 256;
+    }
+    if (send_off[comm.nprocs] == 0 && recv_off[comm.nprocs] == 0) {
+        // nothing to exchange for this rank, but peers may still exchange among themselves
+    }
+    Scratch sbuf(send_off[comm.nprocs], device), rbuf(recv_off[comm.nprocs], device);
+    std::vector<int> id(src.nd());
+    for (int k = 0; k < src.nd(); ++k) id[k] = k;
+    {
+        std::vector<std::size_t> cur(send_off.begin(), send_off.end() - 1);
+        for (const Piece &p : pieces) {
+            const CompRef &ca = sc[p.a], &cb = dc[p.b];
+            if (ca.rank != comm.rank || cb.rank == comm.rank) continue;
+            if (src.dev[ca.idx] != device)
+                throw Error("copy: with a communicator every component must be on the "
+                            "communicator's device");
+            local_piece_copy(Scalar{1, 0}, src.dtype, src.ptr[ca.idx],
+                             src.ranges[ca.rank][ca.idx].size, p.src_from, src.dtype,
+                             (char *)sbuf.ptr + cur[cb.rank], p.size, Coor(src.nd(), 0), p.size,
+                             id, false, device);
+            cur[cb.rank] += volume(p.size) * es;
+        }
+    }
+    set_device(device);
+    hipStream_t s = get_stream(device);
+    ncclComm_t nc = (ncclComm_t)comm.nccl;
+    nccl_check(ncclGroupStart(), "ncclGroupStart");
+    for (int q = 0; q < comm.nprocs; ++q) {
+        if (q == comm.rank) continue;
+        if (send_bytes[q] > 0)
+            nccl_check(ncclSend((char *)sbuf.ptr + send_off[q], send_bytes[q], ncclChar, q, nc, s),
+                       "ncclSend");
+        if (recv_bytes[q] > 0)
+            nccl_check(ncclRecv((char *)rbuf.ptr + recv_off[q], recv_bytes[q], ncclChar, q, nc, s),
+                       "ncclRecv");
+    }
+    nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+    {
+        std::vector<std::size_t> cur(recv_off.begin(), recv_off.end() - 1);
+        for (const Piece &p : pieces) {
+            const CompRef &ca = sc[p.a], &cb = dc[p.b];
+            if (cb.rank != comm.rank || ca.rank == comm.rank) continue;
+            if (dst.dev[cb.idx] != device)
+                throw Error("copy: with a communicator every component must be on the "
+                            "communicator's device");
+            local_piece_copy(alpha, src.dtype, (char *)rbuf.ptr + cur[ca.rank], p.size,
+                             Coor(src.nd(), 0), dst.dtype, dst.ptr[cb.idx],
+                             dst.ranges[cb.rank][cb.idx].size, p.dst_from, p.size, perm_s2d, add,
+                             device);
+            cur[ca.rank] += volume(p.size) * es;
+        }
+    }
+}
+
+} // namespace sbx

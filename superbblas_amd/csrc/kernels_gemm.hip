@@ -1,0 +1,404 @@
+// Batched (complex) GEMM on CDNA4 matrix cores -- the local contraction of superbblas.
+//
+// Replaces the reference's `xgemm_batch_strided` -> `rocblas_gemm_strided_batched_ex`
+// (blas.h:662-810, called from local_contraction_normalized, tensor.h:1567-1597) with a
+// hand-written MFMA kernel:
+//  * f64 / complex<f64>: v_mfma_f64_16x16x4_f64; f32 / complex<f32>: v_mfma_f32_16x16x4_f32.
+//    There is no complex MFMA, so a complex tile product issues 4 real MFMAs
+//    (re*re - im*im, re*im + im*re; the 4M form, not Gauss' 3M, to stay close to BLAS
+//    rounding).  Conjugation flips the sign of the imaginary part when the tile is staged.
+//  * Operands are staged global -> registers -> LDS (async-stage split: the next K-slab is
+//    loaded into registers while the current one is consumed from LDS), in a [row][k] image
+//    padded by one element so that the 16-byte fragment reads are bank-conflict free.
+//  * The thread -> element map of a stage load follows whichever operand stride is unit
+//    (k-contiguous or m/n-contiguous), so both `T` and `N` layouts read coalesced rows.
+//  * Split-K over workgroups when the output has too few tiles to fill 256 CUs (the
+//    lattice contraction has m = n = 256, k = 12288, batch = 16: only 256 64x64 tiles);
+//    the partial slabs are summed in a fixed order by a second kernel, so results are
+//    deterministic.
+//  * XCD-aware workgroup numbering: the tiles of one (batch, k-split) group are dealt to one
+//    XCD so that their shared A/B panels hit that XCD's L2.
+#include "sbx_internal.h"
+
+#include <algorithm>
+
+namespace sbx {
+namespace {
+
+template <typename R> struct Mfma;
+template <> struct Mfma<double> {
+    typedef double acc_t __attribute__((ext_vector_type(4)));
+    static __device__ __forceinline__ acc_t mma(double a, double b, acc_t c) {
+        return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+    }
+    // C/D map of v_mfma_f64_16x16x4_f64: col = lane&15, row = (lane>>4) + 4*reg
+    static __device__ __forceinline__ int row(int lane, int r) { return (lane >> 4) + 4 * r; }
+};
+template <> struct Mfma<float> {
+    typedef float acc_t __attribute__((ext_vector_type(4)));
+    static __device__ __forceinline__ acc_t mma(float a, float b, acc_t c) {
+        return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+    }
+    // C/D map of v_mfma_f32_16x16x4_f32: col = lane&15, row = 4*(lane>>4) + reg
+    static __device__ __forceinline__ int row(int lane, int r) { return ((lane >> 4) << 2) + r; }
+};
+
+template <typename R, bool CPLX> struct Elem;
+template <> struct Elem<double, true> { typedef double2 type; };
+template <> struct Elem<double, false> { typedef double type; };
+template <> struct Elem<float, true> { typedef float2 type; };
+template <> struct Elem<float, false> { typedef float type; };
+
+template <typename E> __device__ __forceinline__ E zero_elem() { return E{}; }
+__device__ __forceinline__ double2 conj_if(double2 v, bool c) { return c ? double2{v.x, -v.y} : v; }
+__device__ __forceinline__ float2 conj_if(float2 v, bool c) { return c ? float2{v.x, -v.y} : v; }
+__device__ __forceinline__ double conj_if(double v, bool) { return v; }
+__device__ __forceinline__ float conj_if(float v, bool) { return v; }
+
+struct GemmKArgs {
+    long m, n, k, batch;
+    const void *a;
+    long sa_m, sa_k, sa_b;
+    const void *b;
+    long sb_k, sb_n, sb_b;
+    void *c;
+    long sc_m, sc_n, sc_b;
+    double alpha_re, alpha_im, beta_re, beta_im;
+    int conja, conjb;
+    int splits;
+    long kchunk;
+    void *work;
+    int tm, tn;
+};
+
+// out = alpha*v (+ beta*old)
+template <typename R>
+__device__ __forceinline__ void epilogue_store(R *cptr, R vr, R vi, const GemmKArgs &p, bool cplx) {
+    if (cplx) {
+        R ar = (R)p.alpha_re, ai = (R)p.alpha_im;
+        R outr = ar * vr - ai * vi, outi = ar * vi + ai * vr;
+        if (p.beta_re != 0 || p.beta_im != 0) {
+            R br = (R)p.beta_re, bi = (R)p.beta_im;
+            R cr = cptr[0], ci = cptr[1];
+            outr += br * cr - bi * ci;
+            outi += br * ci + bi * cr;
+        }
+        cptr[0] = outr;
+        cptr[1] = outi;
+    } else {
+        R out = (R)p.alpha_re * vr;
+        if (p.beta_re != 0) out += (R)p.beta_re * cptr[0];
+        cptr[0] = out;
+    }
+}
+
+template <typename R, bool CPLX, bool AK, bool BK, int BM, int BN, int BKK, int WM, int WN>
+__global__ void __launch_bounds__(WM *WN * 64) gemm_kernel(const GemmKArgs p) {
+    typedef typename Elem<R, CPLX>::type E;
+    typedef typename Mfma<R>::acc_t acc_t;
+    constexpr int NTH = WM * WN * 64;
+    constexpr int LDK = BKK + 1; // padded [row][k] image
+    constexpr int EA = BM * BKK / NTH;
+    constexpr int EB = BN * BKK / NTH;
+    static_assert(EA * NTH == BM * BKK && EB * NTH == BN * BKK, "tile/threads mismatch");
+    constexpr int WTM = BM / WM, WTN = BN / WN; // wave tile
+    constexpr int MT = WTM / 16, NT = WTN / 16;
+    static_assert(MT * 16 == WTM && NT * 16 == WTN && BKK % 4 == 0, "bad wave tile");
+
+    __shared__ E As[BM * LDK];
+    __shared__ E Bs[BN * LDK];
+
+    // XCD-aware remap: consecutive logical workgroups share an XCD (bijective form)
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
+    const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+
+    const int ti = wg % p.tm;
+    int rest = wg / p.tm;
+    const int tj = rest % p.tn;
+    rest /= p.tn;
+    const int split = rest % p.splits;
+    const long bb = rest / p.splits;
+
+    const long m0 = (long)ti * BM, n0 = (long)tj * BN;
+    const long k_begin = (long)split * p.kchunk;
+    const long k_end = min(p.k, k_begin + p.kchunk);
+
+    const E *__restrict__ A = (const E *)p.a + bb * p.sa_b;
+    const E *__restrict__ B = (const E *)p.b + bb * p.sb_b;
+    const int tid = threadIdx.x;
+    const bool conja = p.conja != 0, conjb = p.conjb != 0;
+
+    E ra[EA], rb[EB];
+    auto load_stage = [&](long k0) {
+#pragma unroll
+        for (int i = 0; i < EA; ++i) {
+            const int e = tid + NTH * i;
+            const int row = AK ? e / BKK : e % BM;
+            const int kk = AK ? e % BKK : e / BM;
+            const long gi = m0 + row, gk = k0 + kk;
+            ra[i] = (gi < p.m && gk < k_end) ? A[gi * p.sa_m + gk * p.sa_k] : zero_elem<E>();
+        }
+#pragma unroll
+        for (int i = 0; i < EB; ++i) {
+            const int e = tid + NTH * i;
+            const int col = BK ? e / BKK : e % BN;
+            const int kk = BK ? e % BKK : e / BN;
+            const long gj = n0 + col, gk = k0 + kk;
+            rb[i] = (gj < p.n && gk < k_end) ? B[gk * p.sb_k + gj * p.sb_n] : zero_elem<E>();
+        }
+    };
+    auto store_stage = [&]() {
+#pragma unroll
+        for (int i = 0; i < EA; ++i) {
+            const int e = tid + NTH * i;
+            const int row = AK ? e / BKK : e % BM;
+            const int kk = AK ? e % BKK : e / BM;
+            As[row * LDK + kk] = conj_if(ra[i], conja);
+        }
+#pragma unroll
+        for (int i = 0; i < EB; ++i) {
+            const int e = tid + NTH * i;
+            const int col = BK ? e / BKK : e % BN;
+            const int kk = BK ? e % BKK : e / BN;
+            Bs[col * LDK + kk] = conj_if(rb[i], conjb);
+        }
+    };
+
+    const int lane = tid & 63, wid = tid >> 6;
+    const int wm = wid / WN, wn = wid % WN;
+    const int frow = wm * WTM + (lane & 15); // fragment row (A) / col (B) in the tile
+    const int fcol = wn * WTN + (lane & 15);
+    const int kq = lane >> 4;
+
+    acc_t accR[MT][NT], accI[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            accR[i][j] = acc_t{0, 0, 0, 0};
+            accI[i][j] = acc_t{0, 0, 0, 0};
+        }
+
+    long k0 = k_begin;
+    if (k0 < k_end) load_stage(k0);
+    for (; k0 < k_end; k0 += BKK) {
+        __syncthreads(); // the previous slab is no longer read
+        store_stage();
+        __syncthreads();
+        if (k0 + BKK < k_end) load_stage(k0 + BKK); // in flight while this slab is consumed
+#pragma unroll
+        for (int kk = 0; kk < BKK; kk += 4) {
+            E af[MT], bf[NT];
+#pragma unroll
+            for (int i = 0; i < MT; ++i) af[i] = As[(frow + 16 * i) * LDK + kk + kq];
+#pragma unroll
+            for (int j = 0; j < NT; ++j) bf[j] = Bs[(fcol + 16 * j) * LDK + kk + kq];
+            if constexpr (CPLX) {
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+#pragma unroll
+                    for (int j = 0; j < NT; ++j) {
+                        accR[i][j] = Mfma<R>::mma(af[i].x, bf[j].x, accR[i][j]);
+                        accI[i][j] = Mfma<R>::mma(af[i].x, bf[j].y, accI[i][j]);
+                    }
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+#pragma unroll
+                    for (int j = 0; j < NT; ++j) {
+                        accR[i][j] = Mfma<R>::mma(-af[i].y, bf[j].y, accR[i][j]);
+                        accI[i][j] = Mfma<R>::mma(af[i].y, bf[j].x, accI[i][j]);
+                    }
+            } else {
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+#pragma unroll
+                    for (int j = 0; j < NT; ++j)
+                        accR[i][j] = Mfma<R>::mma(af[i], bf[j], accR[i][j]);
+            }
+        }
+    }
+
+    // Epilogue
+    const int ccol = lane & 15;
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const long gi = m0 + wm * WTM + 16 * i + Mfma<R>::row(lane, r);
+                const long gj = n0 + wn * WTN + 16 * j + ccol;
+                if (gi >= p.m || gj >= p.n) continue;
+                const R vr = accR[i][j][r];
+                const R vi = CPLX ? accI[i][j][r] : R(0);
+                if (p.splits == 1) {
+                    R *cptr = (R *)((E *)p.c + bb * p.sc_b + gi * p.sc_m + gj * p.sc_n);
+                    epilogue_store<R>(cptr, vr, vi, p, CPLX);
+                } else {
+                    E *w = (E *)p.work + (((long)split * p.batch + bb) * p.n + gj) * p.m + gi;
+                    if constexpr (CPLX)
+                        *w = E{vr, vi};
+                    else
+                        *w = vr;
+                }
+            }
+}
+
+// C = alpha * sum_s W[s] + beta * C, summed in split order (deterministic)
+template <typename R, bool CPLX>
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(const GemmKArgs p) {
+    typedef typename Elem<R, CPLX>::type E;
+    const long total = p.batch * p.n * p.m;
+    const long slab = total;
+    for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+         idx += (long)gridDim.x * blockDim.x) {
+        const long gi = idx % p.m;
+        const long gj = (idx / p.m) % p.n;
+        const long bb = idx / (p.m * p.n);
+        const E *w = (const E *)p.work + idx;
+        R sr = 0, si = 0;
+        for (int s = 0; s < p.splits; ++s) {
+            if constexpr (CPLX) {
+                E v = w[s * slab];
+                sr += v.x;
+                si += v.y;
+            } else {
+                sr += w[s * slab];
+            }
+        }
+        R *cptr = (R *)((E *)p.c + bb * p.sc_b + gi * p.sc_m + gj * p.sc_n);
+        epilogue_store<R>(cptr, sr, si, p, CPLX);
+    }
+}
+
+// C = beta * C (k == 0)
+template <typename R, bool CPLX>
+__global__ void __launch_bounds__(256) scale_c_kernel(const GemmKArgs p) {
+    typedef typename Elem<R, CPLX>::type E;
+    const long total = p.batch * p.n * p.m;
+    for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+         idx += (long)gridDim.x * blockDim.x) {
+        const long gi = idx % p.m;
+        const long gj = (idx / p.m) % p.n;
+        const long bb = idx / (p.m * p.n);
+        R *cptr = (R *)((E *)p.c + bb * p.sc_b + gi * p.sc_m + gj * p.sc_n);
+        GemmKArgs q = p;
+        q.alpha_re = 0;
+        q.alpha_im = 0;
+        epilogue_store<R>(cptr, R(0), R(0), q, CPLX);
+    }
+}
+
+template <typename R, bool CPLX, bool AK, bool BK>
+void launch_tiled(const GemmKArgs &p0, int device, hipStream_t stream) {
+    constexpr int BM = 64, BN = 64, BKK = 16, WM = 2, WN = 2;
+    GemmKArgs p = p0;
+    p.tm = (int)((p.m + BM - 1) / BM);
+    p.tn = (int)((p.n + BN - 1) / BN);
+    const long tiles = (long)p.tm * p.tn * p.batch;
+    // Split K so that ~4 workgroups per CU are in flight; keep >= 256-deep chunks.
+    const long target = 1024;
+    long splits = 1;
+    if (tiles < target) {
+        splits = (target + tiles - 1) / tiles;
+        const long max_splits = std::max(1L, p.k / 256);
+        splits = std::min(splits, max_splits);
+    }
+    long kchunk = (p.k + splits - 1) / splits;
+    kchunk = (kchunk + BKK - 1) / BKK * BKK;
+    splits = std::max(1L, (p.k + kchunk - 1) / kchunk);
+    p.splits = (int)splits;
+    p.kchunk = kchunk;
+    typedef typename Elem<R, CPLX>::type E;
+    Scratch work;
+    if (splits > 1) {
+        work = Scratch(sizeof(E) * splits * p.batch * p.m * p.n, device);
+        p.work = work.ptr;
+    }
+    const long nwg = tiles * splits;
+    if (nwg > 0x7fffffffL) throw Error("gemm: grid too large");
+    hipLaunchKernelGGL((gemm_kernel<R, CPLX, AK, BK, BM, BN, BKK, WM, WN>), dim3((unsigned)nwg),
+                       dim3(WM * WN * 64), 0, stream, p);
+    SBX_HIP_CHECK(hipGetLastError());
+    if (splits > 1) {
+        const long total = p.batch * p.m * p.n;
+        const long blocks = std::min((total + 255) / 256, 4096L);
+        hipLaunchKernelGGL((splitk_reduce_kernel<R, CPLX>), dim3((unsigned)blocks), dim3(256), 0,
+                           stream, p);
+        SBX_HIP_CHECK(hipGetLastError());
+    }
+}
+
+template <typename R, bool CPLX> void launch_typed(const GemmKArgs &p, int device, hipStream_t s) {
+    // Pick the stage-load thread map from the unit stride of each operand
+    const bool ak = (p.sa_k == 1) || (p.sa_m != 1 && std::labs(p.sa_k) <= std::labs(p.sa_m));
+    const bool bk = (p.sb_k == 1) || (p.sb_n != 1 && std::labs(p.sb_k) <= std::labs(p.sb_n));
+    if (ak && bk)
+        launch_tiled<R, CPLX, true, true>(p, device, s);
+    else if (ak && !bk)
+        launch_tiled<R, CPLX, true, false>(p, device, s);
+    else if (!ak && bk)
+        launch_tiled<R, CPLX, false, true>(p, device, s);
+    else
+        launch_tiled<R, CPLX, false, false>(p, device, s);
+}
+
+template <typename R, bool CPLX> void launch_scale(const GemmKArgs &p, hipStream_t s) {
+    const long total = p.batch * p.m * p.n;
+    if (total == 0) return;
+    const long blocks = std::min((total + 255) / 256, 4096L);
+    hipLaunchKernelGGL((scale_c_kernel<R, CPLX>), dim3((unsigned)blocks), dim3(256), 0, s, p);
+    SBX_HIP_CHECK(hipGetLastError());
+}
+
+} // namespace
+
+void launch_gemm(const GemmDesc &d, int device) {
+    if (d.m == 0 || d.n == 0 || d.batch == 0) return;
+    set_device(device);
+    hipStream_t s = get_stream(device);
+    GemmKArgs p{};
+    p.m = d.m;
+    p.n = d.n;
+    p.k = d.k;
+    p.batch = d.batch;
+    p.a = d.a;
+    p.sa_m = d.sa_m;
+    p.sa_k = d.sa_k;
+    p.sa_b = d.sa_b;
+    p.b = d.b;
+    p.sb_k = d.sb_k;
+    p.sb_n = d.sb_n;
+    p.sb_b = d.sb_b;
+    p.c = d.c;
+    p.sc_m = d.sc_m;
+    p.sc_n = d.sc_n;
+    p.sc_b = d.sc_b;
+    p.alpha_re = d.alpha.re;
+    p.alpha_im = dtype_is_complex(d.t) ? d.alpha.im : 0;
+    p.beta_re = d.beta.re;
+    p.beta_im = dtype_is_complex(d.t) ? d.beta.im : 0;
+    p.conja = d.conja;
+    p.conjb = d.conjb;
+    p.splits = 1;
+    p.kchunk = d.k;
+    const bool scale_only = (d.k == 0 || (p.alpha_re == 0 && p.alpha_im == 0));
+    switch (d.t) {
+    case SBX_CDOUBLE:
+        scale_only ? launch_scale<double, true>(p, s) : launch_typed<double, true>(p, device, s);
+        break;
+    case SBX_DOUBLE:
+        scale_only ? launch_scale<double, false>(p, s) : launch_typed<double, false>(p, device, s);
+        break;
+    case SBX_CFLOAT:
+        scale_only ? launch_scale<float, true>(p, s) : launch_typed<float, true>(p, device, s);
+        break;
+    case SBX_FLOAT:
+        scale_only ? launch_scale<float, false>(p, s) : launch_typed<float, false>(p, device, s);
+        break;
+    default: throw Error("gemm: unsupported type");
+    }
+}
+
+} // namespace sbx

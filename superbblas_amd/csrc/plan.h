@@ -1,0 +1,126 @@
+// Host planner: periodic range algebra, partitions and distributed tensor descriptors.
+//
+// Restated from the reference's behaviour (not its code):
+//  * periodic intersections            dist.h:345-558
+//  * translate/shift ranges            dist.h:568-653
+//  * make_hole                         dist.h:3744-3825
+//  * basic_partitioning,
+//    partitioning_distributed_procs    dist.h:3264-3509
+// All coordinates are handled internally in SlowToFast order; FastToSlow inputs are reversed
+// at the API boundary (the reference does the same, e.g. tensor.h:718-727, 1282-1293).
+#pragma once
+
+#include "sbx_internal.h"
+
+#include <functional>
+#include <map>
+#include <string>
+#include <vector>
+
+namespace sbx {
+
+struct BsrOp;
+
+using Coor = std::vector<int>;
+
+struct Range {
+    Coor from, size;
+};
+
+inline long volume(const Coor &c) {
+    long v = 1;
+    for (int x : c) v *= x;
+    return v;
+}
+
+/// coor mod dim, also for negative values (dist.h:330-333)
+inline int normalize_coor(long c, int dim) {
+    if (dim == 0) return 0;
+    long r = c % dim;
+    return (int)(r < 0 ? r + dim : r);
+}
+
+/// Strides of a dense array of dims `size` in SlowToFast order (tensor.h:282-297)
+inline std::vector<long> strides_slow_to_fast(const Coor &size) {
+    std::vector<long> s(size.size());
+    long acc = 1;
+    for (int i = (int)size.size() - 1; i >= 0; --i) {
+        s[i] = acc;
+        acc *= size[i];
+    }
+    return s;
+}
+
+/// All ranges resulting from intersecting two ranges on a periodic lattice (dist.h:370-497)
+std::vector<Range> intersection(const Range &a, const Range &b, const Coor &dim);
+/// Intersect a list of ranges with a range
+std::vector<Range> intersection(const std::vector<Range> &as, const Range &b, const Coor &dim);
+
+/// Subranges of `r` after removing `hole` (dist.h:3744-3825)
+std::vector<Range> make_hole(const Range &r, const Range &hole, const Coor &dim);
+
+/// partitioning_distributed_procs (dist.h:3318-3383)
+Coor partitioning_distributed_procs(const std::string &order, const Coor &dim,
+                                    const std::string &dist_labels, unsigned nprocs);
+/// basic_partitioning with labels (dist.h:3393-3460)
+std::vector<Range> basic_partitioning(const char *order, const Coor &dim, const Coor &procs,
+                                      const char *dist_labels, int nprocs, int ncomponents);
+/// basic_partitioning with extension (dist.h:3475-3509)
+std::vector<Range> basic_partitioning_ext(const Coor &dim, const Coor &procs, int nprocs,
+                                          bool replicate, const Coor &ext_power);
+
+/// Position of each label of `to` in `from` (-1 if absent) (tensor.h:417-440)
+std::vector<int> find_permutation(const std::string &from, const std::string &to);
+
+/// Communicator: nprocs == 1 means a single process (SelfComm, dist.h:142-149)
+struct Comm {
+    int nprocs = 1;
+    int rank = 0;
+    int device = -1;
+    void *nccl = nullptr; // ncclComm_t
+};
+
+/// A distributed tensor as seen by one process.
+///  - `ranges[r]` are the (global, periodic) ranges held by the components of rank r;
+///  - `ptr`/`dev` are the local data of this rank's components, dense arrays of
+///    `ranges[rank][i].size` elements in label order `labels` (SlowToFast);
+///  - dev < 0 means host memory.
+struct DistTensor {
+    std::string labels;
+    Coor dim;
+    int dtype = SBX_CDOUBLE;
+    std::vector<std::vector<Range>> ranges;
+    std::vector<void *> ptr;
+    std::vector<int> dev;
+    int nd() const { return (int)labels.size(); }
+};
+
+/// A single-component view used by the local kernels
+struct Local {
+    void *ptr;
+    int dev;
+    Coor size; // local dims
+    std::string labels;
+    int dtype;
+};
+
+//
+// Distributed operations (dist.cpp)
+//
+
+/// copy: dst[from1 + P(c - from0)] (=|+=) alpha * src[c] for c in [from0, from0+size0)
+void dist_copy(const Scalar &alpha, const DistTensor &src, const Coor &from0, const Coor &size0,
+               const DistTensor &dst, const Coor &from1, bool add, const Comm &comm);
+
+/// contraction: vr = alpha * contract(v0, v1) + beta * vr over the boxes [from, from+size)
+void dist_contraction(const Scalar &alpha, const DistTensor &v0, const Coor &from0,
+                      const Coor &size0, bool conj0, const DistTensor &v1, const Coor &from1,
+                      const Coor &size1, bool conj1, const Scalar &beta, const DistTensor &vr,
+                      const Coor &fromr, const Coor &sizer, const Comm &comm);
+
+/// Local contraction of three dense single-component arrays on one device (GEMM mapping of
+/// tensor.h:1475-1598, generalised to arbitrary strides)
+void local_contraction(const Scalar &alpha, const Local &x, bool conjx, const Local &y,
+                       bool conjy, const Scalar &beta, const Local &r);
+
+} // namespace sbx

@@ -1,0 +1,136 @@
+// Device runtime: per-device library streams and the stream-ordered scratch pool.
+//
+// Reference: platform.h:173-221 (Gpu context), 304-409 (stream helpers), 448-467
+// (getGpuAllocStream: every GPU op of a device is enqueued on one library stream) and
+// alloc.h:91-391 (hipMallocAsync on the alloc stream + a cached scratch-buffer pool).
+// On ROCm the stream-ordered allocator already is a caching pool; raising its release
+// threshold keeps freed scratch resident so steady-state calls do no driver allocations.
+#include "sbx_internal.h"
+
+#include <mutex>
+
+namespace sbx {
+
+namespace {
+struct DeviceState {
+    hipStream_t own = nullptr;  // stream created by the library
+    hipStream_t user = nullptr; // stream set by the caller (sbx_stream_set)
+    bool pool_configured = false;
+};
+std::mutex g_mutex;
+std::vector<DeviceState> &states() {
+    static std::vector<DeviceState> s;
+    return s;
+}
+DeviceState &state(int device) {
+    auto &s = states();
+    if (device < 0) throw Error("invalid device id");
+    if ((int)s.size() <= device) s.resize(device + 1);
+    return s[device];
+}
+} // namespace
+
+void set_device(int device) {
+    int cur = -1;
+    SBX_HIP_CHECK(hipGetDevice(&cur));
+    if (cur != device) SBX_HIP_CHECK(hipSetDevice(device));
+}
+
+hipStream_t get_stream(int device) {
+    std::lock_guard<std::mutex> g(g_mutex);
+    DeviceState &st = state(device);
+    if (st.user) return st.user;
+    if (!st.own) {
+        set_device(device);
+        SBX_HIP_CHECK(hipStreamCreateWithFlags(&st.own, hipStreamNonBlocking));
+    }
+    return st.own;
+}
+
+void set_user_stream(int device, hipStream_t s) {
+    std::lock_guard<std::mutex> g(g_mutex);
+    state(device).user = s;
+}
+
+void destroy_streams() {
+    std::lock_guard<std::mutex> g(g_mutex);
+    for (std::size_t d = 0; d < states().size(); ++d) {
+        DeviceState &st = states()[d];
+        if (st.own) {
+            (void)hipSetDevice((int)d);
+            (void)hipStreamSynchronize(st.own);
+            (void)hipStreamDestroy(st.own);
+            st.own = nullptr;
+        }
+    }
+}
+
+void *scratch_alloc(std::size_t bytes, int device) {
+    if (bytes == 0) return nullptr;
+    set_device(device);
+    {
+        std::lock_guard<std::mutex> g(g_mutex);
+        DeviceState &st = state(device);
+        if (!st.pool_configured) {
+            hipMemPool_t pool;
+            if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+                uint64_t threshold = UINT64_MAX;
+                (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &threshold);
+            }
+            st.pool_configured = true;
+        }
+    }
+    void *p = nullptr;
+    hipError_t e = hipMallocAsync(&p, bytes, get_stream(device));
+    if (e != hipSuccess) {
+        // Mirror alloc.h:104-168: release the cached memory and retry once
+        (void)hipGetLastError();
+        (void)hipStreamSynchronize(get_stream(device));
+        hipMemPool_t pool;
+        if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) (void)hipMemPoolTrimTo(pool, 0);
+        SBX_HIP_CHECK(hipMallocAsync(&p, bytes, get_stream(device)));
+    }
+    return p;
+}
+
+void scratch_free(void *p, int device) {
+    if (!p) return;
+    set_device(device);
+    SBX_HIP_CHECK(hipFreeAsync(p, get_stream(device)));
+}
+
+void trim_pools() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return;
+    for (int d = 0; d < n && d < (int)states().size(); ++d) {
+        (void)hipSetDevice(d);
+        (void)hipDeviceSynchronize();
+        hipMemPool_t pool;
+        if (hipDeviceGetDefaultMemPool(&pool, d) == hipSuccess) (void)hipMemPoolTrimTo(pool, 0);
+    }
+}
+
+Scratch::Scratch(std::size_t bytes_, int device_) : device(device_), bytes(bytes_) {
+    ptr = scratch_alloc(bytes, device);
+}
+Scratch::~Scratch() {
+    if (ptr) {
+        try {
+            scratch_free(ptr, device);
+        } catch (...) {
+        }
+    }
+}
+
+int pointer_device(const void *p) {
+    if (!p) return -1;
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return -1;
+    }
+    if (attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged) return attr.device;
+    return -1;
+}
+
+} // namespace sbx

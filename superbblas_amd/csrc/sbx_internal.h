@@ -1,0 +1,158 @@
+// Internal declarations shared by the superbblas_amd HIP library.
+//
+// The library is the MI355X-native replacement of superbblas's distributed tensor
+// contraction hot path (reference: include/superbblas/{dist,tensor,copy_n,blas,bsr}.h).
+// Everything user-visible goes through the C-ABI declared in include/superbblas_amd/sbx.h;
+// this header is private to the .so.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <array>
+#include <complex>
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/superbblas_amd/sbx.h"
+
+namespace sbx {
+
+/// Error type; the C-ABI layer turns it into a status code + sbx_last_error()
+struct Error : public std::runtime_error {
+    explicit Error(const std::string &s) : std::runtime_error(s) {}
+};
+
+#define SBX_HIP_CHECK(expr)                                                                        \
+    do {                                                                                           \
+        hipError_t sbx_e_ = (expr);                                                                \
+        if (sbx_e_ != hipSuccess)                                                                  \
+            throw ::sbx::Error(std::string("HIP error `") + hipGetErrorString(sbx_e_) + "` at " +  \
+                               __FILE__ + ":" + std::to_string(__LINE__) + " in " #expr);          \
+    } while (0)
+
+/// Size in bytes of a scalar type
+inline std::size_t dtype_size(int t) {
+    switch (t) {
+    case SBX_FLOAT: return 4;
+    case SBX_DOUBLE: return 8;
+    case SBX_CFLOAT: return 8;
+    case SBX_CDOUBLE: return 16;
+    case SBX_INT: return 4;
+    case SBX_SIZE_T: return 8;
+    default: throw Error("unsupported dtype");
+    }
+}
+inline bool dtype_is_complex(int t) { return t == SBX_CFLOAT || t == SBX_CDOUBLE; }
+
+/// A complex scalar carried through the host planner (alpha/beta)
+struct Scalar {
+    double re = 0, im = 0;
+    bool is_zero() const { return re == 0 && im == 0; }
+    bool is_one() const { return re == 1 && im == 0; }
+};
+
+//
+// Runtime (runtime.cpp)
+//
+
+/// Library stream of a device (created lazily, or set by the user with sbx_stream_set)
+hipStream_t get_stream(int device);
+/// Make `device` current for the calling thread
+void set_device(int device);
+/// Stream-ordered scratch allocation (hipMallocAsync pool with a high release threshold)
+void *scratch_alloc(std::size_t bytes, int device);
+void scratch_free(void *p, int device);
+
+/// RAII scratch buffer on a device, freed in stream order
+struct Scratch {
+    void *ptr = nullptr;
+    int device = -1;
+    std::size_t bytes = 0;
+    Scratch() {}
+    Scratch(std::size_t bytes, int device);
+    Scratch(const Scratch &) = delete;
+    Scratch &operator=(const Scratch &) = delete;
+    Scratch(Scratch &&o) noexcept : ptr(o.ptr), device(o.device), bytes(o.bytes) {
+        o.ptr = nullptr;
+    }
+    Scratch &operator=(Scratch &&o) noexcept {
+        std::swap(ptr, o.ptr);
+        std::swap(device, o.device);
+        std::swap(bytes, o.bytes);
+        return *this;
+    }
+    ~Scratch();
+};
+
+/// Device id owning a pointer, or -1 for host memory
+int pointer_device(const void *p);
+
+//
+// Kernels (kernels_*.hip); all enqueue on get_stream(device)
+//
+
+/// Strided batched GEMM, BLAS column-major semantics (reference blas.h:662-810):
+///   C_b = alpha * op(A_b) * op(B_b) + beta * C_b,  b < batch.
+/// Generalised to arbitrary strides: op(A)(i,k) = A[i*sa_m + k*sa_k + b*sa_b] (conjugated if
+/// conja), op(B)(k,j) = B[k*sb_k + j*sb_n + b*sb_b] (conj if conjb), C(i,j) = C[i*sc_m + j*sc_n +
+/// b*sc_b].  `t` is one of SBX_FLOAT/DOUBLE/CFLOAT/CDOUBLE.
+struct GemmDesc {
+    int t;
+    long m, n, k, batch;
+    const void *a;
+    long sa_m, sa_k, sa_b;
+    bool conja;
+    const void *b;
+    long sb_k, sb_n, sb_b;
+    bool conjb;
+    void *c;
+    long sc_m, sc_n, sc_b;
+    Scalar alpha, beta;
+};
+void launch_gemm(const GemmDesc &d, int device);
+
+/// N-dimensional strided box copy (the MI355X version of copy_n / copy_n_blocking,
+/// reference copy_n.h:77-244, 584-950):
+///   dst[sum_i c_i*dst_stride_i] (=|+=) alpha * src[sum_i c_i*src_stride_i],  c < size
+/// with element type conversion src_t -> dst_t.
+struct BoxCopyDesc {
+    int src_t, dst_t;
+    const void *src;
+    void *dst;
+    std::vector<long> size, src_stride, dst_stride; // in elements
+    Scalar alpha;
+    bool add;
+};
+void launch_box_copy(const BoxCopyDesc &d, int device);
+
+/// Fill `n` elements of type `t` with zeros
+void launch_zero(void *p, std::size_t bytes, int device);
+
+/// BSR SpMM on one component (reference bsr.h:535-650 builtin loop, bsr.h:855-928 GPU):
+///   y[row-block i] = alpha * sum_{j in row i} V_j * x[jj_j],  for every rhs column
+struct BsrDesc {
+    int t;
+    long block_rows; ///< number of block rows
+    int bi, bd;      ///< block image / domain sizes
+    const int *ii;   ///< CSR row pointer (block_rows+1), device
+    const int *jj;   ///< first domain index of each nonzero block (-1 = skip), device
+    const void *v;   ///< nonzero blocks, bi*bd each
+    bool block_im_fast;
+    int num_nnz_per_row; ///< >0 if all rows have the same count (ELL), else -1
+    const void *x;
+    long ldx;
+    bool x_row_major; ///< x(d, col) = x[d*ldx + col] if row major, else x[d + col*ldx]
+    void *y;
+    long ldy;
+    bool y_row_major;
+    long ncols;
+    Scalar alpha;
+    bool add; ///< y += (instead of y =)
+};
+void launch_bsr(const BsrDesc &d, int device);
+
+} // namespace sbx

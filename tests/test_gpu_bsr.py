@@ -1,0 +1,71 @@
+"""bsr_krylov on the GPU vs the oracle's builtin BSR loop (bsr.h:535-650), on the 9-point
+lattice stencil of tests/bsr.cpp:169-255 with its integer-valued nonzeros (exact)."""
+import numpy as np
+import pytest
+
+from _common import T_CDOUBLE, oracle_bsr, rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def lattice_operator(L, spin, color, dtype=np.complex128):
+    """9-point periodic stencil on an L^4 lattice, blocks (spin*color)^2, image = domain =
+    xyztsc; jj coordinates relative to the (whole) domain (bsr.cpp:169-255)."""
+    dim = [L, L, L, L, spin, color]
+    vol = L ** 4
+    b = spin * color
+    sites = np.array(np.unravel_index(np.arange(vol), (L, L, L, L))).T
+    jj, nb = [], 0
+    for s in sites:
+        nbrs = [s.copy()]
+        for d in range(4):
+            if L == 1:
+                continue
+            for dr in (-1, 1):
+                c = s.copy()
+                c[d] = (c[d] + dr) % L
+                nbrs.append(c)
+                if L <= 2:
+                    break
+        nb = len(nbrs)
+        for c in nbrs:
+            jj.append(list(c) + [0, 0])
+    jj = np.array(jj, dtype=np.int32)
+    ii = np.full(vol, nb, dtype=np.int32)
+    nnz = vol * nb
+    k = np.arange(nnz * b * b, dtype=np.int64)
+    vals = ((k * 3 + 1) % 7 - 3) + 1j * ((k * 5 + 2) % 9 - 4)
+    return dim, ii, jj, vals.astype(dtype), nb
+
+
+@pytest.mark.parametrize("spin,color,ncols", [(1, 3, 1), (1, 3, 5), (4, 3, 2)])
+@pytest.mark.parametrize("y_layout", ["row", "col"])
+def test_bsr_lattice(gpu, spin, color, ncols, y_layout):
+    import torch
+    import superbblas_amd as sb
+    L = 4
+    dim, ii, jj, vals, nb = lattice_operator(L, spin, color)
+    b = spin * color
+    vol = L ** 4
+    x = (np.arange(vol * b * ncols) % 17 - 8 + 1j * (np.arange(vol * b * ncols) % 5)).astype(
+        np.complex128)
+    # x: pXYZTSCn (row major, n fastest)
+    yref = np.zeros(vol * b * ncols, np.complex128)
+    oracle_bsr(T_CDOUBLE, dim, 0, vol, b, b, ii, jj, vals, False, x, ncols, True, yref,
+               ncols if y_layout == "row" else vol * b, y_layout == "row", ncols, 1.0)
+    full = [([0] * 6, dim)]
+    op = sb.create_bsr(full, dim, full, dim, [1, 1, 1, 1, spin, color], [1, 1, 1, 1, spin, color],
+                       False, [torch.from_numpy(ii).to(gpu)], [torch.from_numpy(jj).to(gpu)],
+                       [torch.from_numpy(vals).to(gpu)])
+    dimx = [1, L, L, L, L, spin, color, ncols]
+    tx = torch.from_numpy(x).to(gpu)
+    if y_layout == "row":
+        oy, dimy = "pxyztscn", [1, L, L, L, L, spin, color, ncols]
+    else:
+        oy, dimy = "pnxyztsc", [1, ncols, L, L, L, L, spin, color]
+    ty = torch.zeros(vol * b * ncols, dtype=torch.complex128, device=gpu)
+    sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", [([0] * 8, dimx)], "pXYZTSCn", [0] * 8, dimx, dimx,
+                  [tx], 0.0, [([0] * 8, dimy)], oy, [0] * 8, dimy, dimy, "p", [ty])
+    torch.cuda.synchronize()
+    assert rel_err(ty.cpu().numpy(), yref) == 0.0
+    op.destroy()

@@ -1,0 +1,154 @@
+"""copy()/permute on the GPU vs the oracle: bit-exact for data movement (north_star)."""
+import itertools
+
+import numpy as np
+import pytest
+
+from _common import index_valued, int_valued, oracle_copy
+
+pytestmark = pytest.mark.gpu
+
+
+def _vol(d):
+    n = 1
+    for x in d:
+        n *= x
+    return n
+
+
+def _gpu_local_copy(gpu, alpha, o0, from0, size0, dim0, v0, o1, from1, dim1, v1, co=0, add=False):
+    import torch
+    import superbblas_amd as sb
+    t0 = torch.from_numpy(v0).to(gpu)
+    t1 = torch.from_numpy(v1).to(gpu)
+    sb.copy(alpha, [([0] * len(o0), list(dim0))], o0, from0, size0, dim0, [t0],
+            [([0] * len(o1), list(dim1))], o1, from1, dim1, [t1], co=co,
+            copyadd=sb.Add if add else sb.Copy)
+    torch.cuda.synchronize()
+    return t1.cpu().numpy()
+
+
+def test_lattice_permute_slices(gpu):
+    """The dist.cpp permute benchmark (dist.cpp:237-266): xyztsc -> slice n of tnsxyzc."""
+    L, n = 4, 3
+    dim0 = [L, L, L, L, 4, 3]
+    dim1 = [L, n, 4, L, L, L, 3]
+    v0 = index_valued(_vol(dim0), np.complex128)
+    v1 = np.zeros(_vol(dim1), np.complex128)
+    ref = v1.copy()
+    out = v1.copy()
+    for k in range(n):
+        oracle_copy(1.0, "xyztsc", [0] * 6, dim0, dim0, v0, "tnsxyzc", [0, k, 0, 0, 0, 0, 0],
+                    dim1, ref)
+        out = _gpu_local_copy(gpu, 1.0, "xyztsc", [0] * 6, dim0, dim0, v0, "tnsxyzc",
+                              [0, k, 0, 0, 0, 0, 0], dim1, out)
+    assert np.array_equal(out.view(np.uint8), ref.view(np.uint8))
+
+
+@pytest.mark.parametrize("dtype", [np.complex128, np.float64, np.complex64, np.float32, np.int32,
+                                   np.uint64])
+def test_permutations_bitexact(gpu, dtype):
+    rng = np.random.default_rng(7)
+    labels = "abcde"
+    dim = [3, 4, 5, 2, 6]
+    for trial in range(12):
+        perm = rng.permutation(5)
+        o1 = "".join(labels[p] for p in perm)
+        dim1 = [dim[p] for p in perm]
+        from0 = [int(rng.integers(0, d)) for d in dim]
+        size0 = [int(rng.integers(1, d + 1)) for d in dim]
+        from1 = [int(rng.integers(0, d)) for d in dim1]
+        v0 = index_valued(_vol(dim), dtype)
+        v1 = int_valued(_vol(dim1), dtype, seed=trial) if np.dtype(dtype).kind in "fc" else \
+            np.arange(_vol(dim1)).astype(dtype)
+        ref = v1.copy()
+        oracle_copy(1.0, labels, from0, size0, dim, v0, o1, from1, dim1, ref)
+        out = _gpu_local_copy(gpu, 1.0, labels, from0, size0, dim, v0, o1, from1, dim1, v1.copy())
+        assert np.array_equal(out.view(np.uint8), ref.view(np.uint8)), (trial, o1, from0, size0)
+
+
+@pytest.mark.parametrize("add", [False, True])
+def test_alpha_add_and_conversion(gpu, add):
+    labels, dim = "xyzw", [5, 3, 4, 7]
+    o1, dim1 = "wzxy", [7, 4, 5, 3]
+    for t0, t1 in [(np.complex128, np.complex128), (np.complex64, np.complex128),
+                   (np.complex128, np.complex64), (np.float32, np.float64)]:
+        v0 = int_valued(_vol(dim), t0, 1)
+        v1 = int_valued(_vol(dim1), t1, 2)
+        ref = v1.copy()
+        alpha = 2.0 - 1.0j if np.dtype(t0).kind == "c" else 2.0
+        oracle_copy(alpha, labels, [1, 0, 2, 3], [4, 3, 2, 7], dim, v0, o1, [0, 1, 4, 2], dim1,
+                    ref, add=add)
+        out = _gpu_local_copy(gpu, alpha, labels, [1, 0, 2, 3], [4, 3, 2, 7], dim, v0, o1,
+                              [0, 1, 4, 2], dim1, v1.copy(), add=add)
+        assert np.array_equal(out, ref)
+
+
+def test_fast_to_slow_and_missing_labels(gpu):
+    # origin label of size 1 absent in the destination; destination label absent in the origin
+    v0 = index_valued(2 * 1 * 5 * 3, np.complex128)
+    v1 = int_valued(5 * 4 * 2 * 3, np.complex128)
+    for co in (0, 1):
+        ref = v1.copy()
+        oracle_copy(1.0, "abcd", [0, 0, 1, 0], [2, 1, 3, 3], [2, 1, 5, 3], v0, "cqad",
+                    [2, 3, 0, 0], [5, 4, 2, 3], ref, co=co)
+        out = _gpu_local_copy(gpu, 1.0, "abcd", [0, 0, 1, 0], [2, 1, 3, 3], [2, 1, 5, 3], v0,
+                              "cqad", [2, 3, 0, 0], [5, 4, 2, 3], v1.copy(), co=co)
+        assert np.array_equal(out.view(np.uint8), ref.view(np.uint8))
+
+
+def test_multicomponent_redistribution(gpu):
+    """Copy between two different partitions of the same tensor, several components per
+    process (the reference's --components mode, contract.cpp:452-461)."""
+    import torch
+    import superbblas_amd as sb
+    dim = [6, 4, 5, 3]
+    o = "xyzc"
+    v = index_valued(_vol(dim), np.complex128)
+    p0 = sb.basic_partitioning(o, dim, [3, 1, 1, 1], "x", 3, 1)
+    p1 = sb.basic_partitioning("czyx", [3, 5, 4, 6], [1, 2, 2, 1], "zy", 4, 1)
+    # components of the origin: slices of v
+    comps0 = []
+    for frm, size in p0:
+        full = v.reshape(dim)
+        sl = full[frm[0]:frm[0] + size[0], frm[1]:frm[1] + size[1], frm[2]:frm[2] + size[2],
+                  frm[3]:frm[3] + size[3]]
+        comps0.append(torch.from_numpy(np.ascontiguousarray(sl).ravel()).to(gpu))
+    comps1 = [torch.zeros(_vol(size), dtype=torch.complex128, device=gpu) for _, size in p1]
+    sb.copy(1.0, p0, o, [0] * 4, dim, dim, comps0, p1, "czyx", [0] * 4, [3, 5, 4, 6], comps1)
+    torch.cuda.synchronize()
+    full1 = v.reshape(dim).transpose(3, 2, 1, 0)
+    for (frm, size), c in zip(p1, comps1):
+        exp = full1[frm[0]:frm[0] + size[0], frm[1]:frm[1] + size[1], frm[2]:frm[2] + size[2],
+                    frm[3]:frm[3] + size[3]]
+        assert np.array_equal(c.cpu().numpy(), np.ascontiguousarray(exp).ravel())
+
+
+def test_periodic_shift(gpu):
+    """The z-shift of dist.cpp:268-296: from1[z] = 1 wraps around the periodic lattice."""
+    dim = [2, 3, 4, 4, 5, 3]
+    o = "tnsxzc"
+    v0 = index_valued(_vol(dim), np.complex128)
+    v1 = np.zeros_like(v0)
+    ref = v1.copy()
+    oracle_copy(1.0, o, [0] * 6, dim, dim, v0, o, [0, 0, 0, 0, 1, 0], dim, ref)
+    out = _gpu_local_copy(gpu, 1.0, o, [0] * 6, dim, dim, v0, o, [0, 0, 0, 0, 1, 0], dim, v1)
+    assert np.array_equal(out, ref)
+
+
+def test_host_components(gpu):
+    """A CPU-context origin (the tests gather to/scatter from host tensors)."""
+    import torch
+    import superbblas_amd as sb
+    dim = [4, 6]
+    v0 = index_valued(24, np.complex128)
+    t0 = torch.from_numpy(v0)  # host
+    t1 = torch.zeros(24, dtype=torch.complex128, device=gpu)
+    sb.copy(1.0, [([0, 0], dim)], "ab", [0, 0], dim, dim, [t0], [([0, 0], [6, 4])], "ba", [0, 0],
+            [6, 4], [t1])
+    torch.cuda.synchronize()
+    assert np.array_equal(t1.cpu().numpy(), v0.reshape(4, 6).T.ravel())
+    back = torch.zeros(24, dtype=torch.complex128)
+    sb.copy(1.0, [([0, 0], [6, 4])], "ba", [0, 0], [6, 4], [6, 4], [t1], [([0, 0], dim)], "ab",
+            [0, 0], dim, [back])
+    assert np.array_equal(back.numpy(), v0)

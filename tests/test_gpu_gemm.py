@@ -1,0 +1,74 @@
+"""Batched GEMM kernel (MFMA) vs the oracle's column-major batched GEMM
+(blas_cpu_tmpl.hpp:405-477 restated in oracle/oracle.c).  Tolerance: 1e-10 relative
+(Frobenius) for f64/complex<f64> (north_star), 1e-5 for f32/complex<f32>."""
+import numpy as np
+import pytest
+
+from _common import oracle_gemm, random_valued, rel_err
+
+pytestmark = pytest.mark.gpu
+
+TOL = {np.complex128: 1e-10, np.float64: 1e-10, np.complex64: 1e-5, np.float32: 1e-5}
+
+
+def _run(gpu, dtype, ta, tb, m, n, k, batch, alpha, beta, pad=0):
+    import torch
+    import superbblas_amd as sb
+    lda = (m if ta == "N" else k) + pad
+    ldb = (k if tb == "N" else n) + pad
+    ldc = m + pad
+    sa = lda * (k if ta == "N" else m) + pad
+    sb_ = ldb * (n if tb == "N" else k) + pad
+    sc = ldc * n + pad
+    a = random_valued(sa * batch, dtype, 1)
+    b = random_valued(sb_ * batch, dtype, 2)
+    c = random_valued(sc * batch, dtype, 3)
+    ref = c.copy()
+    oracle_gemm(ta, tb, m, n, k, alpha, a, lda, sa, b, ldb, sb_, beta, ref, ldc, sc, batch)
+    ta_, tb_, tc_ = (torch.from_numpy(x).to(gpu) for x in (a, b, c))
+    sb.xgemm_batch_strided(ta, tb, m, n, k, alpha, ta_, lda, sa, tb_, ldb, sb_, beta, tc_, ldc,
+                           sc, batch)
+    torch.cuda.synchronize()
+    out = tc_.cpu().numpy()
+    return out, ref
+
+
+@pytest.mark.parametrize("dtype", [np.complex128, np.float64, np.complex64, np.float32])
+@pytest.mark.parametrize("ta,tb", [("N", "N"), ("T", "N"), ("N", "T"), ("T", "T"), ("C", "N"),
+                                   ("C", "T"), ("N", "C")])
+def test_gemm_small(gpu, dtype, ta, tb):
+    out, ref = _run(gpu, dtype, ta, tb, 37, 21, 45, 3, 1.5 - 0.5j, 0.25 + 1j, pad=3)
+    assert rel_err(out, ref) < TOL[dtype]
+
+
+@pytest.mark.parametrize("dtype", [np.complex128, np.float64])
+def test_gemm_lattice_shape(gpu, dtype):
+    # the config-2 GEMM shape scaled down: ('T','N', m = n = 64, k = 1536, batch = 8)
+    out, ref = _run(gpu, dtype, "T", "N", 64, 64, 1536, 8, 1.0, 0.0)
+    assert rel_err(out, ref) < TOL[dtype]
+
+
+@pytest.mark.parametrize("m,n,k,batch", [(1, 1, 1, 1), (1, 7, 300, 2), (65, 1, 17, 3),
+                                         (130, 66, 5, 1), (16, 16, 4000, 2)])
+def test_gemm_edges(gpu, m, n, k, batch):
+    out, ref = _run(gpu, np.complex128, "T", "N", m, n, k, batch, 1.0, -1.0)
+    assert rel_err(out, ref) < 1e-10
+
+
+def test_gemm_k0_and_alpha0(gpu):
+    out, ref = _run(gpu, np.complex128, "N", "N", 8, 8, 0, 2, 1.0, 2.0)
+    assert rel_err(out, ref) < 1e-14
+    out, ref = _run(gpu, np.complex128, "N", "N", 8, 8, 8, 2, 0.0, 0.0)
+    assert np.all(out == 0)
+
+
+def test_gemm_beta0_ignores_nan(gpu):
+    """beta == 0 overwrites C (tensor.h:1511-1512): NaNs in C must not propagate."""
+    import torch
+    import superbblas_amd as sb
+    a = torch.ones(16 * 16, dtype=torch.complex128, device=gpu)
+    b = torch.ones(16 * 16, dtype=torch.complex128, device=gpu)
+    c = torch.full((16 * 16,), float("nan"), dtype=torch.complex128, device=gpu)
+    sb.xgemm_batch_strided("N", "N", 16, 16, 16, 1.0, a, 16, 0, b, 16, 0, 0.0, c, 16, 0, 1)
+    torch.cuda.synchronize()
+    assert torch.all(c == 16)
