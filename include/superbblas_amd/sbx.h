@@ -66,8 +66,10 @@ int sbx_get_gpu_devices_count(int *n);
 int sbx_sync(sbx_context ctx);
 /* The stream all work of `device` is enqueued on (getGpuAllocStream, platform.h:448-467) */
 int sbx_stream_get(int device, void **stream);
-/* Replace the library stream of `device` by a caller-owned hipStream_t (NULL restores the default) */
+/* Enqueue the work of `device` on a caller-owned hipStream_t (NULL = the null stream) */
 int sbx_stream_set(int device, void *stream);
+/* Go back to the library's own (non-blocking) stream of `device` */
+int sbx_stream_reset(int device);
 /* clearCaches (alloc.h:437-443): release cached plans and scratch memory */
 int sbx_clear_caches(void);
 /* clearHandles (platform.h:828-838): destroy library streams and communicator handles */

@@ -67,9 +67,77 @@ _ctx_p = ctypes.POINTER(_Ctx)
 _lib.sbx_last_error.restype = ctypes.c_char_p
 
 
+
 def _check(rc: int):
     if rc != 0:
         raise SuperbblasError(_lib.sbx_last_error().decode())
+
+
+import array as _array
+
+_VP = ctypes.c_void_p
+_I = ctypes.c_int
+
+
+class _Pack:
+    """All integer arguments of one call in ONE int32 buffer (and the data pointers in one
+    uint64 buffer): a single allocation instead of one ctypes array per argument, which is
+    what dominates the host cost of a call from Python."""
+    __slots__ = ("ints", "offs", "ptrs", "poffs")
+
+    def __init__(self):
+        self.ints = _array.array("i")
+        self.offs = []
+        self.ptrs = _array.array("Q")
+        self.poffs = []
+
+    def add(self, xs):
+        self.offs.append(len(self.ints))
+        self.ints.extend(xs)
+        return len(self.offs) - 1
+
+    def add_partition(self, p, nd):
+        self.offs.append(len(self.ints))
+        for frm, size in p:
+            if len(frm) != nd or len(size) != nd:
+                raise SuperbblasError("partition item with wrong rank")
+            self.ints.extend(frm)
+            self.ints.extend(size)
+        return len(self.offs) - 1
+
+    def add_ctxs(self, ts):
+        self.offs.append(len(self.ints))
+        for t in ts:
+            if t.is_cuda:
+                self.ints.append(GPU)
+                self.ints.append(t.device.index or 0)
+            else:
+                self.ints.append(CPU)
+                self.ints.append(-1)
+        return len(self.offs) - 1
+
+    def add_ptrs(self, ts):
+        self.poffs.append(len(self.ptrs))
+        for t in ts:
+            self.ptrs.append(t.data_ptr())
+        return len(self.poffs) - 1
+
+    def addrs(self):
+        if not self.ints:
+            self.ints.append(0)
+        if not self.ptrs:
+            self.ptrs.append(0)
+        bi = self.ints.buffer_info()[0]
+        bp = self.ptrs.buffer_info()[0]
+        return [bi + 4 * o for o in self.offs], [bp + 8 * o for o in self.poffs]
+
+
+_lib.sbx_copy.argtypes = [_I, _I, _VP, _I, _I, _VP, _I, ctypes.c_char_p, _VP, _VP, _VP, _VP, _VP,
+                          _VP, _I, ctypes.c_char_p, _VP, _VP, _VP, _VP, _VP, _I, _I, _I]
+_lib.sbx_contraction.argtypes = (
+    [_I, _I, _I, _I, _VP] +
+    [_VP, _VP, _VP, _VP, _I, ctypes.c_char_p, _I, _VP, _VP] * 2 + [_VP] +
+    [_VP, _VP, _VP, _VP, _I, ctypes.c_char_p, _VP, _VP, _VP, _I, _I])
 
 
 def _ints(xs: Sequence[int]):
@@ -116,21 +184,27 @@ def _dtype_of(ts: Sequence[torch.Tensor]) -> int:
     return _DTYPES[dt]
 
 
+_bound_streams = {}
+
+
 def _bind_stream(ts: Iterable[torch.Tensor]):
     """Enqueue library work on torch's current stream of every device involved."""
-    devs = {t.device.index for t in ts if t.is_cuda}
-    for d in devs:
-        s = torch.cuda.current_stream(d).cuda_stream
-        _check(_lib.sbx_stream_set(d, ctypes.c_void_p(s)))
+    for t in ts:
+        if t.is_cuda:
+            d = t.device.index or 0
+            s = torch.cuda.current_stream(d).cuda_stream
+            if _bound_streams.get(d) != s:
+                _check(_lib.sbx_stream_set(d, ctypes.c_void_p(s)))
+                _bound_streams[d] = s
 
 
 def _check_sizes(p, rank, ncomp, v, what):
     for i in range(ncomp):
-        frm, size = p[rank * ncomp + i]
+        size = p[rank * ncomp + i][1]
         n = 1
         for s in size:
             n *= s
-        if v[i].numel() < n or not v[i].is_contiguous():
+        if n and (v[i].numel() < n or not v[i].is_contiguous()):
             raise SuperbblasError("%s: component %d has %d elements, the partition needs %d "
                                   "(contiguous)" % (what, i, v[i].numel(), n))
 
@@ -165,7 +239,12 @@ def stream(device: int = 0) -> int:
 
 
 def set_stream(device: int, hip_stream: Optional[int]):
-    _check(_lib.sbx_stream_set(device, ctypes.c_void_p(hip_stream or 0)))
+    """Enqueue the library's work for `device` on `hip_stream` (0 = the null stream); None
+    restores the library's own stream."""
+    if hip_stream is None:
+        _check(_lib.sbx_stream_reset(device))
+    else:
+        _check(_lib.sbx_stream_set(device, ctypes.c_void_p(hip_stream)))
 
 
 def clear_caches():
@@ -296,12 +375,25 @@ def copy(alpha, p0, o0: str, from0, size0, dim0, v0: Sequence[torch.Tensor], p1,
         raise SuperbblasError("partition is incompatible with the communicator/components")
     _check_sizes(p0, rank, nc0, v0, "copy origin")
     _check_sizes(p1, rank, nc1, v1, "copy destination")
-    _bind_stream(list(v0) + list(v1))
-    _check(_lib.sbx_copy(nd0, nd1, _scalar(alpha), _dtype_of(v0), _dtype_of(v1),
-                         _partition(p0, nd0), nc0, o0.encode(), _ints(from0), _ints(size0),
-                         _ints(dim0), _ptrs(v0), _ctxs(v0), _partition(p1, nd1), nc1, o1.encode(),
-                         _ints(from1), _ints(dim1), _ptrs(v1), _ctxs(v1), _comm(comm), co, copyadd,
-                         0))
+    t0, t1 = _dtype_of(v0), _dtype_of(v1)
+    _bind_stream(v0)
+    _bind_stream(v1)
+    k = _Pack()
+    k.add_partition(p0, nd0)
+    k.add(from0)
+    k.add(size0)
+    k.add(dim0)
+    k.add_ctxs(v0)
+    k.add_partition(p1, nd1)
+    k.add(from1)
+    k.add(dim1)
+    k.add_ctxs(v1)
+    k.add_ptrs(v0)
+    k.add_ptrs(v1)
+    a, pp = k.addrs()
+    _check(_lib.sbx_copy(nd0, nd1, _scalar(alpha), t0, t1, a[0], nc0, o0.encode(), a[1], a[2],
+                         a[3], pp[0], a[4], a[5], nc1, o1.encode(), a[6], a[7], pp[1], a[8],
+                         _comm(comm), co, copyadd, 0))
 
 
 def contraction(alpha, p0, from0, size0, dim0, o0: str, conj0: bool, v0, p1, from1, size1, dim1,
@@ -311,22 +403,32 @@ def contraction(alpha, p0, from0, size0, dim0, o0: str, conj0: bool, v0, p1, fro
     nprocs, rank = _nprocs_rank(comm)
     nd0, nd1, ndr = len(o0), len(o1), len(o_r)
     nc0, nc1, ncr = len(v0), len(v1), len(vr)
-    for p, nc, what in ((p0, nc0, "v0"), (p1, nc1, "v1"), (pr, ncr, "vr")):
-        if len(p) != nprocs * nc:
-            raise SuperbblasError("%s: partition is incompatible with the communicator" % what)
+    if len(p0) != nprocs * nc0 or len(p1) != nprocs * nc1 or len(pr) != nprocs * ncr:
+        raise SuperbblasError("partition is incompatible with the communicator")
     _check_sizes(p0, rank, nc0, v0, "contraction v0")
     _check_sizes(p1, rank, nc1, v1, "contraction v1")
     _check_sizes(pr, rank, ncr, vr, "contraction vr")
-    t = _dtype_of(list(v0) + list(v1) + list(vr))
-    _bind_stream(list(v0) + list(v1) + list(vr))
+    t = _dtype_of(v0)
+    if _dtype_of(v1) != t or _dtype_of(vr) != t:
+        raise SuperbblasError("contraction: all tensors must have the same dtype")
+    _bind_stream(v0)
+    _bind_stream(v1)
+    _bind_stream(vr)
+    k = _Pack()
+    for p, nd, f, sz, dm, v in ((p0, nd0, from0, size0, dim0, v0), (p1, nd1, from1, size1, dim1, v1),
+                                (pr, ndr, fromr, sizer, dimr, vr)):
+        k.add_partition(p, nd)
+        k.add(f)
+        k.add(sz)
+        k.add(dm)
+        k.add_ctxs(v)
+        k.add_ptrs(v)
+    a, pp = k.addrs()
     _check(_lib.sbx_contraction(
         nd0, nd1, ndr, t, _scalar(alpha),
-        _partition(p0, nd0), _ints(from0), _ints(size0), _ints(dim0), nc0, o0.encode(),
-        int(conj0), _ptrs(v0), _ctxs(v0),
-        _partition(p1, nd1), _ints(from1), _ints(size1), _ints(dim1), nc1, o1.encode(),
-        int(conj1), _ptrs(v1), _ctxs(v1), _scalar(beta),
-        _partition(pr, ndr), _ints(fromr), _ints(sizer), _ints(dimr), ncr, o_r.encode(),
-        _ptrs(vr), _ctxs(vr), _comm(comm), co, 0))
+        a[0], a[1], a[2], a[3], nc0, o0.encode(), int(conj0), pp[0], a[4],
+        a[5], a[6], a[7], a[8], nc1, o1.encode(), int(conj1), pp[1], a[9], _scalar(beta),
+        a[10], a[11], a[12], a[13], ncr, o_r.encode(), pp[2], a[14], _comm(comm), co, 0))
 
 
 def local_copy(alpha, o0: str, from0, size0, dim0, v0: torch.Tensor, o1: str, from1, dim1,

@@ -22,7 +22,7 @@ void bsr_krylov(const BsrOp &op, const Scalar &alpha, const std::string &oi,
                 const std::string &od, const DistTensor &x, const Coor &fromx, const Coor &sizex,
                 const Scalar &beta, const DistTensor &y, const Coor &fromy, const Coor &sizey,
                 char okr, const Comm &comm);
-void set_user_stream(int device, hipStream_t s);
+void set_user_stream(int device, hipStream_t s, bool has_user);
 void destroy_streams();
 void trim_pools();
 } // namespace sbx
@@ -208,7 +208,11 @@ int sbx_stream_get(int device, void **stream) {
 }
 
 int sbx_stream_set(int device, void *stream) {
-    return guard([&] { set_user_stream(device, (hipStream_t)stream); });
+    return guard([&] { set_user_stream(device, (hipStream_t)stream, true); });
+}
+
+int sbx_stream_reset(int device) {
+    return guard([&] { set_user_stream(device, nullptr, false); });
 }
 
 int sbx_clear_caches(void) {

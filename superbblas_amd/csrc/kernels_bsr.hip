@@ -9,6 +9,12 @@
 //    rhs; for a column-major output consecutive lanes take consecutive image components/rows
 //    and read consecutive 16-byte pieces of the row-ordered nonzero blocks.
 //  * Bound: HBM (the nonzero blocks are streamed once; x is re-read through L2/MALL).
+//  * ELL operators (every block row has the same number of nonzero blocks -- the lattice
+//    stencils) use bsr_ell_kernel: a workgroup streams the nonzero blocks of a chunk of block
+//    rows into LDS with coalesced 16-byte loads (the value stream is the dominant HBM traffic),
+//    then every thread computes all `bi` outputs of one (block row, rhs column) pair reading the
+//    blocks from LDS (broadcast across the rhs lanes) and x from global memory (contiguous along
+//    the rhs for row-major x).
 #include "sbx_internal.h"
 
 #include <algorithm>
@@ -123,6 +129,93 @@ __global__ void __launch_bounds__(256) bsr_kernel(const BsrArgs p) {
     }
 }
 
+constexpr int ELL_LDS_BYTES = 41472; // 32 block rows x 9 blocks x 3x3 complex<double>
+
+template <typename E, int BI, int BD, bool YROW, bool XROW>
+__global__ void __launch_bounds__(256) bsr_ell_kernel(const BsrArgs p, int nnz, int rb) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    E *vals = (E *)smem;
+    const E *__restrict__ v = (const E *)p.v;
+    const E *__restrict__ x = (const E *)p.x;
+    E *__restrict__ y = (E *)p.y;
+    constexpr int BLK = BI * BD;
+    const long row0 = (long)blockIdx.x * rb;
+    const int nrows = (int)min((long)rb, p.block_rows - row0);
+    // 1) stream this chunk's nonzero blocks into LDS (contiguous in the ELL value array)
+    const long vbase = row0 * nnz * BLK;
+    const int nv = nrows * nnz * BLK;
+    for (int e0 = threadIdx.x; e0 < nv; e0 += 256 * 4) {
+        E t[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int e = e0 + 256 * q;
+            t[q] = v[vbase + min(e, nv - 1)]; // clamped: no per-load branch
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int e = e0 + 256 * q;
+            if (e < nv) vals[e] = t[q];
+        }
+    }
+    __syncthreads();
+    // 2) every thread computes the BI outputs of (block row, rhs column) pairs
+    const long npairs = (long)nrows * p.ncols;
+    for (long q = threadIdx.x; q < npairs; q += 256) {
+        int r;
+        long col;
+        if (YROW) {
+            r = (int)(q / p.ncols);
+            col = q % p.ncols;
+        } else {
+            r = (int)(q % nrows);
+            col = q / nrows;
+        }
+        E acc[BI];
+#pragma unroll
+        for (int c = 0; c < BI; ++c) acc[c] = Ops<E>::zero();
+        const int *jj = p.jj + (row0 + r) * nnz;
+        const E *vr = vals + r * nnz * BLK;
+        for (int j = 0; j < nnz; ++j) {
+            const int d0 = jj[j];
+            if (d0 < 0) continue;
+            const E *vb = vr + j * BLK;
+#pragma unroll
+            for (int e = 0; e < BD; ++e) {
+                const E xv = XROW ? x[(long)(d0 + e) * p.ldx + col] : x[(d0 + e) + col * p.ldx];
+#pragma unroll
+                for (int c = 0; c < BI; ++c) {
+                    const E a = p.block_im_fast ? vb[c + e * BI] : vb[c * BD + e];
+                    acc[c] = Ops<E>::fma(a, xv, acc[c]);
+                }
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < BI; ++c) {
+            const long img = (row0 + r) * BI + c;
+            E *yp = YROW ? y + img * p.ldy + col : y + img + col * p.ldy;
+            const E out = Ops<E>::scale(acc[c], p.alpha_re, p.alpha_im);
+            *yp = p.add ? Ops<E>::add(*yp, out) : out;
+        }
+    }
+}
+
+template <typename E, int BI, int BD>
+void launch_ell(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_t s) {
+    const int blk_bytes = nnz * BI * BD * (int)sizeof(E);
+    const int rb = std::max(1, ELL_LDS_BYTES / std::max(1, blk_bytes));
+    const long blocks = (a.block_rows + rb - 1) / rb;
+    const size_t lds = (size_t)rb * blk_bytes;
+    if (yrow && xrow)
+        hipLaunchKernelGGL((bsr_ell_kernel<E, BI, BD, true, true>), dim3(blocks), dim3(256), lds, s, a, nnz, rb);
+    else if (yrow && !xrow)
+        hipLaunchKernelGGL((bsr_ell_kernel<E, BI, BD, true, false>), dim3(blocks), dim3(256), lds, s, a, nnz, rb);
+    else if (!yrow && xrow)
+        hipLaunchKernelGGL((bsr_ell_kernel<E, BI, BD, false, true>), dim3(blocks), dim3(256), lds, s, a, nnz, rb);
+    else
+        hipLaunchKernelGGL((bsr_ell_kernel<E, BI, BD, false, false>), dim3(blocks), dim3(256), lds, s, a, nnz, rb);
+    SBX_HIP_CHECK(hipGetLastError());
+}
+
 template <typename E, int BI, int BD>
 void launch_layouts(const BsrArgs &a, bool yrow, bool xrow, long blocks, hipStream_t s) {
     if (yrow && xrow)
@@ -137,10 +230,17 @@ void launch_layouts(const BsrArgs &a, bool yrow, bool xrow, long blocks, hipStre
     SBX_HIP_CHECK(hipGetLastError());
 }
 
-template <typename E> void launch_typed(const BsrArgs &a, bool yrow, bool xrow, hipStream_t s) {
+template <typename E>
+void launch_typed(const BsrArgs &a, int nnz_per_row, bool yrow, bool xrow, hipStream_t s) {
     const long total = a.block_rows * a.bi * a.ncols;
     const long blocks = std::min((total + 255) / 256, 65536L);
-    if (a.bi == 3 && a.bd == 3)
+    const bool ell = nnz_per_row > 0 &&
+                     (long)nnz_per_row * a.bi * a.bd * (long)sizeof(E) <= ELL_LDS_BYTES;
+    if (ell && a.bi == 3 && a.bd == 3)
+        launch_ell<E, 3, 3>(a, nnz_per_row, yrow, xrow, s);
+    else if (ell && a.bi == 12 && a.bd == 12)
+        launch_ell<E, 12, 12>(a, nnz_per_row, yrow, xrow, s);
+    else if (a.bi == 3 && a.bd == 3)
         launch_layouts<E, 3, 3>(a, yrow, xrow, blocks, s);
     else if (a.bi == 12 && a.bd == 12)
         launch_layouts<E, 12, 12>(a, yrow, xrow, blocks, s);
@@ -171,10 +271,10 @@ void launch_bsr(const BsrDesc &d, int device) {
     a.alpha_im = d.alpha.im;
     a.add = d.add ? 1 : 0;
     switch (d.t) {
-    case SBX_CDOUBLE: return launch_typed<double2>(a, d.y_row_major, d.x_row_major, s);
-    case SBX_CFLOAT: return launch_typed<float2>(a, d.y_row_major, d.x_row_major, s);
-    case SBX_DOUBLE: return launch_typed<double>(a, d.y_row_major, d.x_row_major, s);
-    case SBX_FLOAT: return launch_typed<float>(a, d.y_row_major, d.x_row_major, s);
+    case SBX_CDOUBLE: return launch_typed<double2>(a, d.num_nnz_per_row, d.y_row_major, d.x_row_major, s);
+    case SBX_CFLOAT: return launch_typed<float2>(a, d.num_nnz_per_row, d.y_row_major, d.x_row_major, s);
+    case SBX_DOUBLE: return launch_typed<double>(a, d.num_nnz_per_row, d.y_row_major, d.x_row_major, s);
+    case SBX_FLOAT: return launch_typed<float>(a, d.num_nnz_per_row, d.y_row_major, d.x_row_major, s);
     default: throw Error("bsr: unsupported type");
     }
 }

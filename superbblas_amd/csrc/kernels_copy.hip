@@ -125,7 +125,8 @@ __global__ void __launch_bounds__(256) copy_contig_kernel(const S *__restrict__ 
         put<ADD, D>(dst + idx, scale<D>(conv<D, S>(src[idx]), alpha));
 }
 
-constexpr int TILE_ELEMS = 3072; // LDS tile capacity in elements (<= 48 KB for 16-B elements)
+/// LDS tile capacity in elements: 24 KB of tile per workgroup whatever the element size
+template <typename D> constexpr int tile_elems() { return (int)(24576 / sizeof(D)) > 3072 ? 3072 : (int)(24576 / sizeof(D)); }
 
 struct TiledArgs {
     uint32_t R, TU, TV;     // run length, tile sizes (items)
@@ -147,7 +148,7 @@ struct TiledArgs {
 
 template <typename S, typename D, bool ADD>
 __global__ void __launch_bounds__(256) copy_tiled_kernel(const TiledArgs p) {
-    __shared__ D tile[TILE_ELEMS + 64];
+    __shared__ D tile[tile_elems<D>() + 64];
     __shared__ long su[256], du[256]; // per-item offsets of the U chain (TU <= 256)
 
     const S *__restrict__ src = (const S *)p.src;
@@ -189,28 +190,45 @@ __global__ void __launch_bounds__(256) copy_tiled_kernel(const TiledArgs p) {
     __syncthreads();
 
     const uint32_t ld = p.TU * p.R + 1; // padded LDS row (one row per v)
+    constexpr int EPT = 4;              // elements per thread in flight
     // Read phase: r fastest, then u (contiguous in the source), then v
     const uint32_t nread = p.R * p.TU * nv_t;
-    for (uint32_t e = threadIdx.x; e < nread; e += 256) {
-        const uint32_t ru = p.fRTU.div(e);
-        const uint32_t v = ru;
-        const uint32_t rem = e - ru * (p.R * p.TU);
-        const uint32_t u = p.fR.div(rem);
-        const uint32_t r = rem - u * p.R;
-        if (u < nu_t)
-            tile[v * ld + u * p.R + r] = conv<D, S>(src[sbase + su[u] + (long)v * p.vsst + r]);
+    for (uint32_t e0 = threadIdx.x; e0 < nread; e0 += 256 * EPT) {
+        D v[EPT];
+        uint32_t li[EPT];
+#pragma unroll
+        for (int q = 0; q < EPT; ++q) {
+            const uint32_t e = e0 + 256 * q;
+            const uint32_t vv = p.fRTU.div(e);
+            const uint32_t rem = e - vv * (p.R * p.TU);
+            const uint32_t u = p.fR.div(rem);
+            const uint32_t r = rem - u * p.R;
+            const bool ok = e < nread && u < nu_t;
+            li[q] = ok ? vv * ld + u * p.R + r : 0xffffffffu;
+            // clamped (always valid) address: the loads of the EPT elements are all issued
+            // before the first use instead of one branch + wait per element
+            const uint32_t uc = ok ? u : 0, vc = ok ? vv : 0, rc = ok ? r : 0;
+            v[q] = conv<D, S>(src[sbase + su[uc] + (long)vc * p.vsst + rc]);
+        }
+#pragma unroll
+        for (int q = 0; q < EPT; ++q)
+            if (li[q] != 0xffffffffu) tile[li[q]] = v[q];
     }
     __syncthreads();
     // Write phase: r fastest, then v (contiguous in the destination), then u
     const uint32_t nwrite = p.R * p.TV * nu_t;
-    for (uint32_t e = threadIdx.x; e < nwrite; e += 256) {
-        const uint32_t u = p.fRTV.div(e);
-        const uint32_t rem = e - u * (p.R * p.TV);
-        const uint32_t v = p.fR.div(rem);
-        const uint32_t r = rem - v * p.R;
-        if (v < nv_t)
-            put<ADD, D>(dst + dbase + du[u] + (long)v * p.vdst + r,
-                        scale<D>(tile[v * ld + u * p.R + r], p.alpha));
+    for (uint32_t e0 = threadIdx.x; e0 < nwrite; e0 += 256 * EPT) {
+#pragma unroll
+        for (int q = 0; q < EPT; ++q) {
+            const uint32_t e = e0 + 256 * q;
+            const uint32_t u = p.fRTV.div(e);
+            const uint32_t rem = e - u * (p.R * p.TV);
+            const uint32_t vv = p.fR.div(rem);
+            const uint32_t r = rem - vv * p.R;
+            if (e < nwrite && vv < nv_t)
+                put<ADD, D>(dst + dbase + du[u] + (long)vv * p.vdst + r,
+                            scale<D>(tile[vv * ld + u * p.R + r], p.alpha));
+        }
     }
 }
 
@@ -322,14 +340,15 @@ void launch_pair(const BoxCopyDesc &d, const Norm &n, long total, hipStream_t st
     long NU = 1;
     for (int i : U) NU *= n.size[i];
     const long NV = n.size[V];
-    // Tile sizes: aim for >= 64-element contiguous runs on both sides within the LDS budget
-    long TU = std::min(NU, std::max(1L, (64 + R - 1) / R));
-    long TV = std::min(NV, std::max(1L, (long)TILE_ELEMS / (R * TU)));
-    while (TU < NU && TU < 256 && R * (TU * 2) * TV <= TILE_ELEMS) TU *= 2;
-    TU = std::min(TU, NU);
-    TU = std::min(TU, 256L);
-    TV = std::min(NV, std::max(1L, (long)TILE_ELEMS / (R * TU)));
-    if (R * TU * TV + TV > TILE_ELEMS + 64) throw Error("copy: internal tile sizing error");
+    // Tile sizes: contiguous runs of ~48-96 elements on both sides (>= 768 B for 16-byte
+    // elements) and ~1.5K elements per workgroup so several workgroups share a CU
+    const long budget = tile_elems<D>();
+    long TU = std::min(NU, std::max(1L, (48 + R - 1) / R));
+    long TV = std::min(NV, std::max(1L, budget / (R * TU)));
+    while (TU < NU && TU < 256 && R * TU * 2 * TV <= budget && R * TU < R * TV) TU *= 2;
+    TU = std::min(std::min(TU, NU), 256L);
+    TV = std::min(NV, std::max(1L, budget / (R * TU)));
+    if (R * TU * TV + TV > tile_elems<D>() + 64) throw Error("copy: internal tile sizing error");
     a.R = (uint32_t)R;
     a.TU = (uint32_t)TU;
     a.TV = (uint32_t)TV;

@@ -55,6 +55,27 @@ __device__ __forceinline__ float2 conj_if(float2 v, bool c) { return c ? float2{
 __device__ __forceinline__ double conj_if(double v, bool) { return v; }
 __device__ __forceinline__ float conj_if(float v, bool) { return v; }
 
+/// 16/8/4-byte load through a buffer descriptor: an offset past the descriptor's range returns
+/// zero, which is how out-of-tile elements are padded (no per-load branch, so the compiler keeps
+/// every stage load in flight behind the MFMAs instead of waiting after each one).
+template <typename E> __device__ __forceinline__ E buf_load(__amdgpu_buffer_rsrc_t r, unsigned off);
+template <> __device__ __forceinline__ double2 buf_load<double2>(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    return __builtin_bit_cast(double2, v);
+}
+template <> __device__ __forceinline__ double buf_load<double>(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    auto v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+    return __builtin_bit_cast(double, v);
+}
+template <> __device__ __forceinline__ float2 buf_load<float2>(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    auto v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+    return __builtin_bit_cast(float2, v);
+}
+template <> __device__ __forceinline__ float buf_load<float>(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    auto v = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+    return __builtin_bit_cast(float, v);
+}
+
 struct GemmKArgs {
     long m, n, k, batch;
     const void *a;
@@ -69,6 +90,7 @@ struct GemmKArgs {
     long kchunk;
     void *work;
     int tm, tn;
+    unsigned a_bytes, b_bytes; // extent of one batch entry of A / B (buffer descriptor range)
 };
 
 // out = alpha*v (+ beta*old)
@@ -130,6 +152,12 @@ __global__ void __launch_bounds__(WM *WN * 64) gemm_kernel(const GemmKArgs p) {
     const bool conja = p.conja != 0, conjb = p.conjb != 0;
 
     E ra[EA], rb[EB];
+    // Wave-uniform buffer descriptors of this batch entry (T8/T20 of the CDNA guide)
+    const __amdgpu_buffer_rsrc_t rsA =
+        __builtin_amdgcn_make_buffer_rsrc((void *)A, (short)0, (int)p.a_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsB =
+        __builtin_amdgcn_make_buffer_rsrc((void *)B, (short)0, (int)p.b_bytes, 0x00020000);
+    constexpr unsigned OOB = 0x80000000u; // past any descriptor range: loads return 0
     auto load_stage = [&](long k0) {
 #pragma unroll
         for (int i = 0; i < EA; ++i) {
@@ -137,7 +165,9 @@ __global__ void __launch_bounds__(WM *WN * 64) gemm_kernel(const GemmKArgs p) {
             const int row = AK ? e / BKK : e % BM;
             const int kk = AK ? e % BKK : e / BM;
             const long gi = m0 + row, gk = k0 + kk;
-            ra[i] = (gi < p.m && gk < k_end) ? A[gi * p.sa_m + gk * p.sa_k] : zero_elem<E>();
+            const bool ok = gi < p.m && gk < k_end;
+            const unsigned off = ok ? (unsigned)((gi * p.sa_m + gk * p.sa_k) * sizeof(E)) : OOB;
+            ra[i] = buf_load<E>(rsA, off);
         }
 #pragma unroll
         for (int i = 0; i < EB; ++i) {
@@ -145,7 +175,9 @@ __global__ void __launch_bounds__(WM *WN * 64) gemm_kernel(const GemmKArgs p) {
             const int col = BK ? e / BKK : e % BN;
             const int kk = BK ? e % BKK : e / BN;
             const long gj = n0 + col, gk = k0 + kk;
-            rb[i] = (gj < p.n && gk < k_end) ? B[gk * p.sb_k + gj * p.sb_n] : zero_elem<E>();
+            const bool ok = gj < p.n && gk < k_end;
+            const unsigned off = ok ? (unsigned)((gk * p.sb_k + gj * p.sb_n) * sizeof(E)) : OOB;
+            rb[i] = buf_load<E>(rsB, off);
         }
     };
     auto store_stage = [&]() {
@@ -290,20 +322,34 @@ __global__ void __launch_bounds__(256) scale_c_kernel(const GemmKArgs p) {
     }
 }
 
-template <typename R, bool CPLX, bool AK, bool BK>
-void launch_tiled(const GemmKArgs &p0, int device, hipStream_t stream) {
-    constexpr int BM = 64, BN = 64, BKK = 16, WM = 2, WN = 2;
+/// Launch one tile configuration; `splits` <= 0 picks the split-K factor automatically
+template <typename R, bool CPLX, bool AK, bool BK, int BM, int BN, int BKK, int WM, int WN>
+void launch_tiled_cfg(const GemmKArgs &p0, int device, hipStream_t stream, long splits = 0,
+                      long target_wgs = 1024) {
     GemmKArgs p = p0;
     p.tm = (int)((p.m + BM - 1) / BM);
     p.tn = (int)((p.n + BN - 1) / BN);
     const long tiles = (long)p.tm * p.tn * p.batch;
-    // Split K so that ~4 workgroups per CU are in flight; keep >= 256-deep chunks.
-    const long target = 1024;
-    long splits = 1;
-    if (tiles < target) {
-        splits = (target + tiles - 1) / tiles;
-        const long max_splits = std::max(1L, p.k / 256);
-        splits = std::min(splits, max_splits);
+    if (splits <= 0) {
+        // Split K so that ~target_wgs workgroups are in flight; keep >= 256-deep chunks.
+        splits = 1;
+        if (tiles < target_wgs) {
+            splits = (target_wgs + tiles - 1) / tiles;
+            const long max_splits = std::max(1L, p.k / 256);
+            splits = std::min(splits, max_splits);
+        }
+    }
+    {
+        typedef typename Elem<R, CPLX>::type E0;
+        const long ea = ((p.m - 1) * std::labs(p.sa_m) + (p.k - 1) * std::labs(p.sa_k) + 1) *
+                        (long)sizeof(E0);
+        const long eb = ((p.k - 1) * std::labs(p.sb_k) + (p.n - 1) * std::labs(p.sb_n) + 1) *
+                        (long)sizeof(E0);
+        if (ea >= 0x7fffffffL || eb >= 0x7fffffffL || p.sa_m < 0 || p.sa_k < 0 || p.sb_k < 0 ||
+            p.sb_n < 0)
+            throw Error("gemm: operand batch entries of 2 GiB or more are not supported yet");
+        p.a_bytes = (unsigned)ea;
+        p.b_bytes = (unsigned)eb;
     }
     long kchunk = (p.k + splits - 1) / splits;
     kchunk = (kchunk + BKK - 1) / BKK * BKK;
@@ -330,6 +376,11 @@ void launch_tiled(const GemmKArgs &p0, int device, hipStream_t stream) {
     }
 }
 
+template <typename R, bool CPLX, bool AK, bool BK>
+void launch_tiled(const GemmKArgs &p, int device, hipStream_t stream) {
+    launch_tiled_cfg<R, CPLX, AK, BK, 64, 64, 16, 2, 2>(p, device, stream);
+}
+
 template <typename R, bool CPLX> void launch_typed(const GemmKArgs &p, int device, hipStream_t s) {
     // Pick the stage-load thread map from the unit stride of each operand
     const bool ak = (p.sa_k == 1) || (p.sa_m != 1 && std::labs(p.sa_k) <= std::labs(p.sa_m));
@@ -352,12 +403,7 @@ template <typename R, bool CPLX> void launch_scale(const GemmKArgs &p, hipStream
     SBX_HIP_CHECK(hipGetLastError());
 }
 
-} // namespace
-
-void launch_gemm(const GemmDesc &d, int device) {
-    if (d.m == 0 || d.n == 0 || d.batch == 0) return;
-    set_device(device);
-    hipStream_t s = get_stream(device);
+GemmKArgs make_args(const GemmDesc &d) {
     GemmKArgs p{};
     p.m = d.m;
     p.n = d.n;
@@ -383,6 +429,16 @@ void launch_gemm(const GemmDesc &d, int device) {
     p.conjb = d.conjb;
     p.splits = 1;
     p.kchunk = d.k;
+    return p;
+}
+
+} // namespace
+
+void launch_gemm(const GemmDesc &d, int device) {
+    if (d.m == 0 || d.n == 0 || d.batch == 0) return;
+    set_device(device);
+    hipStream_t s = get_stream(device);
+    GemmKArgs p = make_args(d);
     const bool scale_only = (d.k == 0 || (p.alpha_re == 0 && p.alpha_im == 0));
     switch (d.t) {
     case SBX_CDOUBLE:

@@ -14,7 +14,8 @@ namespace sbx {
 namespace {
 struct DeviceState {
     hipStream_t own = nullptr;  // stream created by the library
-    hipStream_t user = nullptr; // stream set by the caller (sbx_stream_set)
+    hipStream_t user = nullptr; // stream set by the caller (sbx_stream_set); may be the null stream
+    bool has_user = false;
     bool pool_configured = false;
 };
 std::mutex g_mutex;
@@ -39,7 +40,7 @@ void set_device(int device) {
 hipStream_t get_stream(int device) {
     std::lock_guard<std::mutex> g(g_mutex);
     DeviceState &st = state(device);
-    if (st.user) return st.user;
+    if (st.has_user) return st.user;
     if (!st.own) {
         set_device(device);
         SBX_HIP_CHECK(hipStreamCreateWithFlags(&st.own, hipStreamNonBlocking));
@@ -47,9 +48,10 @@ hipStream_t get_stream(int device) {
     return st.own;
 }
 
-void set_user_stream(int device, hipStream_t s) {
+void set_user_stream(int device, hipStream_t s, bool has_user) {
     std::lock_guard<std::mutex> g(g_mutex);
     state(device).user = s;
+    state(device).has_user = has_user;
 }
 
 void destroy_streams() {
