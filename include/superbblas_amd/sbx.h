@@ -99,10 +99,11 @@ int sbx_basic_partitioning(int nd, const char *order, const int *dim, const int 
 /* basic_partitioning(dim, procs, nprocs, replicate, ext_power) (dist.h:3475-3509) */
 int sbx_basic_partitioning_ext(int nd, const int *dim, const int *procs, int nprocs,
                                int replicate, const int *ext_power, int *out);
-/* make_hole(from, size, hole_from, hole_size, dim) (dist.h:3802-3825); out holds up to nd
-   items of 2*nd ints, *nout receives the count */
+/* make_hole(from, size, hole_from, hole_size, dim) (dist.h:3802-3825); out holds up to maxout
+   items of 2*nd ints (periodic wraps can split the result into more than nd boxes; 4*nd*2^nd is a
+   safe bound), *nout receives the count */
 int sbx_make_hole(int nd, const int *from, const int *size, const int *hole_from,
-                  const int *hole_size, const int *dim, int *out, int *nout);
+                  const int *hole_size, const int *dim, int maxout, int *out, int *nout);
 
 /* ---- copy (dist.h:3583-3602 no-MPI / 3534-3558 MPI) ----
    v1[from1 + P(c - from0)] (=|+=) alpha * v0[c] for c in [from0, from0+size0) (periodic),

@@ -352,10 +352,11 @@ def basic_partitioning_ext(dim: Sequence[int], procs: Sequence[int], nprocs: int
 
 def make_hole(frm, size, hole_from, hole_size, dim):
     nd = len(dim)
-    out = _ints([0] * (nd * 2 * nd))
+    maxout = 4 * max(nd, 1) * (1 << min(nd, 6))
+    out = _ints([0] * (maxout * 2 * nd))
     nout = ctypes.c_int()
     _check(_lib.sbx_make_hole(nd, _ints(frm), _ints(size), _ints(hole_from), _ints(hole_size),
-                              _ints(dim), out, ctypes.byref(nout)))
+                              _ints(dim), maxout, out, ctypes.byref(nout)))
     return [(list(out[k * 2 * nd:k * 2 * nd + nd]), list(out[k * 2 * nd + nd:(k + 1) * 2 * nd]))
             for k in range(nout.value)]
 

@@ -331,12 +331,12 @@ int sbx_basic_partitioning_ext(int nd, const int *dim, const int *procs, int npr
 }
 
 int sbx_make_hole(int nd, const int *from, const int *size, const int *hole_from,
-                  const int *hole_size, const int *dim, int *out, int *nout) {
+                  const int *hole_size, const int *dim, int maxout, int *out, int *nout) {
     return guard([&] {
         auto r = make_hole(Range{to_coor(from, nd, false), to_coor(size, nd, false)},
                            Range{to_coor(hole_from, nd, false), to_coor(hole_size, nd, false)},
                            to_coor(dim, nd, false));
-        if ((int)r.size() > nd) throw Error("make_hole: unexpected number of pieces");
+        if ((int)r.size() > maxout) throw Error("make_hole: output buffer too small");
         for (std::size_t k = 0; k < r.size(); ++k)
             for (int i = 0; i < nd; ++i) {
                 out[k * 2 * nd + i] = r[k].from[i];

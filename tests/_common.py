@@ -111,7 +111,10 @@ def index_valued(n, dtype):
     i = np.arange(n, dtype=np.int64)
     dt = np.dtype(dtype)
     if dt.kind == "c":
-        return (i.astype(np.float64) - 1j * i.astype(np.float64)).astype(dt)
+        out = np.empty(n, dt)
+        out.real = i
+        out.imag = -i.astype(np.float64)
+        return out
     return i.astype(dt)
 
 

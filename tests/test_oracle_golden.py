@@ -1,0 +1,103 @@
+"""Pin the oracle (oracle/oracle.c, the CPU restatement) and the library's host planner against
+golden vectors produced by the real reference (tests/golden, oracle/ref_golden.cpp).  CPU only."""
+import numpy as np
+import pytest
+
+from _common import oracle_bsr, oracle_contraction, oracle_copy, T_CDOUBLE
+from _golden import NPT, gen, manifest, output, vol
+
+
+def _is_replicated(p, dim):
+    return len(p) > 1 and all(list(s) == list(dim) and not any(f) for f, s in p)
+
+
+@pytest.mark.parametrize("case", manifest("copy"), ids=lambda c: "copy%d" % c["id"])
+def test_oracle_copy(case):
+    t0, t1 = NPT[case["t0"]], NPT[case["t1"]]
+    v0 = gen(case["gen0"], vol(case["dim0"]), 1, t0)
+    v1 = gen(case["gen1"], vol(case["dim1"]), 2, t1)
+    reps = len(case["p0"]) if (case["add"] and _is_replicated(case["p0"], case["dim0"])) else 1
+    for _ in range(reps):
+        oracle_copy(complex(*case["alpha"]), case["o0"], case["from0"], case["size0"],
+                    case["dim0"], v0, case["o1"], case["from1"], case["dim1"], v1,
+                    add=case["add"])
+    ref = output(case, t1)
+    assert np.array_equal(v1.view(np.uint8), ref.view(np.uint8))
+
+
+@pytest.mark.parametrize("case", manifest("contraction"), ids=lambda c: "contr%d" % c["id"])
+def test_oracle_contraction(case):
+    t = NPT[case["t"]]
+    v0 = gen("int", vol(case["dim0"]), 1, t)
+    v1 = gen("int", vol(case["dim1"]), 2, t)
+    vr = gen("int", vol(case["dimr"]), 3, t)
+    oracle_contraction(complex(*case["alpha"]), case["o0"], case["from0"], case["size0"],
+                       case["dim0"], case["conj0"], v0, case["o1"], case["from1"], case["size1"],
+                       case["dim1"], case["conj1"], v1, complex(*case["beta"]), case["o_r"],
+                       case["fromr"], case["sizer"], case["dimr"], vr)
+    ref = output(case, t)
+    # integer-valued inputs: the sums are exact in f64, so the restatement must match exactly
+    assert np.array_equal(vr, ref)
+
+
+def lattice_operator(L, spin, color):
+    """The operator of oracle/ref_golden.cpp bsr_case on one component (whole domain)."""
+    b = spin * color
+    V = L ** 4
+    sites = np.array(np.unravel_index(np.arange(V), (L, L, L, L))).T
+    jj = np.zeros((V, 9, 6), np.int32)
+    jj[:, 0, :4] = sites
+    k = 1
+    for d in range(4):
+        for s in (-1, 1):
+            c = sites.copy()
+            c[:, d] = (c[:, d] + s) % L
+            jj[:, k, :4] = c
+            k += 1
+    ii = np.full(V, 9, np.int32)
+    vals = gen("int", V * 9 * b * b, 4, np.complex128)
+    return ii, jj.reshape(-1), vals
+
+
+@pytest.mark.parametrize("case", manifest("bsr"), ids=lambda c: "bsr%d" % c["id"])
+def test_oracle_bsr(case):
+    L, spin, color, ncols = case["L"], case["spin"], case["color"], case["ncols"]
+    b = spin * color
+    V = L ** 4
+    ii, jj, vals = lattice_operator(L, spin, color)
+    x = gen("int", V * b * ncols, 5, np.complex128)
+    y = gen("int", V * b * ncols, 6, np.complex128)
+    oracle_bsr(T_CDOUBLE, [L, L, L, L, spin, color], 0, V, b, b, ii, jj, vals, False, x, ncols,
+               True, y, ncols, True, ncols, 1.0)
+    assert np.array_equal(y, output(case, np.complex128))
+
+
+# ---- host planner (the library's C++ partitioning helpers; no GPU needed) ----
+
+def test_partitioning_distributed_procs():
+    import superbblas_amd as sb
+    for c in manifest("pdp"):
+        assert sb.partitioning_distributed_procs(c["order"], c["dim"], c["dist"],
+                                                 c["nprocs"]) == c["procs"], c
+
+
+def test_basic_partitioning():
+    import superbblas_amd as sb
+    for c in manifest("bp"):
+        p = sb.basic_partitioning(c["order"], c["dim"], c["procs"], c["dist"], c["nprocs"],
+                                  c["ncomponents"])
+        assert [[list(f), list(s)] for f, s in p] == c["p"], c
+
+
+def test_basic_partitioning_ext():
+    import superbblas_amd as sb
+    for c in manifest("bpe"):
+        p = sb.basic_partitioning_ext(c["dim"], c["procs"], c["nprocs"], c["replicate"], c["ext"])
+        assert [[list(f), list(s)] for f, s in p] == c["p"], c
+
+
+def test_make_hole():
+    import superbblas_amd as sb
+    for c in manifest("hole"):
+        r = sb.make_hole(c["from"], c["size"], c["hfrom"], c["hsize"], c["dim"])
+        assert [[list(f), list(s)] for f, s in r] == c["r"], c
