@@ -84,6 +84,19 @@ int sbx_deallocate(void *ptr, sbx_context ctx);
 int sbx_comm_unique_id(unsigned char *id);
 /* Create the communicator of `nprocs` ranks; `device` is this rank's GPU */
 int sbx_comm_create(int nprocs, int rank, const unsigned char *id, int device, sbx_comm *comm);
+/* Host all-to-all exchange: send sendbytes[q] bytes at sendbuf+senddispls[q] to rank q and
+   receive recvbytes[q] bytes from rank q into recvbuf+recvdispls[q] (MPI_Alltoallv with byte
+   counts); returns 0 on success.  Buffers are pinned host memory owned by the library. */
+typedef int (*sbx_alltoallv_fn)(const void *sendbuf, const unsigned long long *sendbytes,
+                                const unsigned long long *senddispls, void *recvbuf,
+                                const unsigned long long *recvbytes,
+                                const unsigned long long *recvdispls, void *user);
+/* Communicator whose exchanges are staged through pinned host memory and `fn` (the reference's
+   non-GPU-aware MPI path, dist.h:1426-1500: pack on the device, copy to the host, alltoallv,
+   copy back, unpack).  Lets an MPI application keep its MPI_Comm (wrap MPI_Alltoallv) and lets
+   several ranks share one GPU, which RCCL refuses. */
+int sbx_comm_create_host(int nprocs, int rank, int device, sbx_alltoallv_fn fn, void *user,
+                         sbx_comm *comm);
 int sbx_comm_rank(sbx_comm comm, int *rank, int *nprocs);
 int sbx_comm_destroy(sbx_comm comm);
 
@@ -114,6 +127,16 @@ int sbx_copy(int nd0, int nd1, const double *alpha, int t0, int t1,
              const int *p1, int ncomponents1, const char *o1, const int *from1, const int *dim1,
              void *const *v1, const sbx_context *ctx1, sbx_comm comm, int co, int copyadd,
              int session);
+
+/* Exchange plan of sbx_copy as seen by `rank` of `nprocs` (host only, no GPU work; the
+   reference get_indices_to_send / get_indices_to_receive, dist.h:1789-1900, 2321-2324):
+   send[q] / recv[q] = elements sent to / received from rank q, *local = elements moved within
+   the rank.  For inspection and tests of the multi-process plan. */
+int sbx_copy_plan(int nd0, int nd1, const int *p0, int ncomponents0, const char *o0,
+                  const int *from0, const int *size0, const int *dim0, const int *p1,
+                  int ncomponents1, const char *o1, const int *from1, const int *dim1, int nprocs,
+                  int rank, int co, int copyadd, long long *send, long long *recv,
+                  long long *local);
 
 /* ---- contraction (dist.h:3701-3731 no-MPI / 3628-3662 MPI) ----
    vr = alpha * sum_{labels in o0 and o1, not in o_r} conj?(v0) conj?(v1) + beta * vr */

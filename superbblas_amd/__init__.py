@@ -68,6 +68,7 @@ _lib.sbx_last_error.restype = ctypes.c_char_p
 
 
 
+
 def _check(rc: int):
     if rc != 0:
         raise SuperbblasError(_lib.sbx_last_error().decode())
@@ -256,15 +257,64 @@ def clear_caches():
 # communicator (replaces MPI_Comm; RCCL underneath)
 # ---------------------------------------------------------------------------------------------
 
-class Comm:
-    """A communicator over `nprocs` processes, one GPU each (RCCL over xGMI)."""
+_ULLP = ctypes.POINTER(ctypes.c_ulonglong)
+_ALLTOALLV_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, _ULLP, _ULLP, ctypes.c_void_p,
+                                 _ULLP, _ULLP, ctypes.c_void_p)
+_lib.sbx_comm_create_host.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _ALLTOALLV_FN,
+                                      ctypes.c_void_p, ctypes.c_void_p]
 
-    def __init__(self, nprocs: int, rank: int, unique_id: bytes, device: int):
+
+class Comm:
+    """A communicator over `nprocs` processes.  Default transport: RCCL over xGMI (one GPU per
+    process).  `Comm.host_staged` builds the host-staged transport instead (pinned host buffers
+    + a torch.distributed all-to-all, any backend), the reference's non-GPU-aware MPI path."""
+
+    def __init__(self, nprocs: int, rank: int, unique_id: Optional[bytes], device: int,
+                 _host_fn=None):
         self.nprocs, self.rank, self.device = nprocs, rank, device
         h = ctypes.c_void_p()
-        buf = (ctypes.c_ubyte * 128).from_buffer_copy(unique_id)
-        _check(_lib.sbx_comm_create(nprocs, rank, buf, device, ctypes.byref(h)))
+        self._fn = _host_fn
+        if _host_fn is None:
+            buf = (ctypes.c_ubyte * 128).from_buffer_copy(unique_id)
+            _check(_lib.sbx_comm_create(nprocs, rank, buf, device, ctypes.byref(h)))
+        else:
+            _check(_lib.sbx_comm_create_host(nprocs, rank, device, _host_fn, None,
+                                             ctypes.byref(h)))
         self._h = h
+
+    @classmethod
+    def host_staged(cls, device: int, group=None) -> "Comm":
+        """Communicator of the current torch.distributed group whose exchanges go through
+        pinned host memory and ``all_to_all_single`` on ``group`` (e.g. gloo).  Several ranks
+        may share a GPU."""
+        import numpy as _np
+        import torch.distributed as dist
+        rank, n = dist.get_rank(group), dist.get_world_size(group)
+
+        def exchange(sbuf, sbytes, sdispl, rbuf, rbytes, rdispl, _user):
+            try:
+                sb_, sd_ = [sbytes[q] for q in range(n)], [sdispl[q] for q in range(n)]
+                rb_, rd_ = [rbytes[q] for q in range(n)], [rdispl[q] for q in range(n)]
+                send = _np.zeros(sum(sb_), _np.uint8)
+                o = 0
+                for q in range(n):
+                    if sb_[q]:
+                        ctypes.memmove(send.ctypes.data + o, sbuf + sd_[q], sb_[q])
+                    o += sb_[q]
+                recv = torch.empty(sum(rb_), dtype=torch.uint8)
+                dist.all_to_all_single(recv, torch.from_numpy(send), rb_, sb_, group=group)
+                o = 0
+                for q in range(n):
+                    if rb_[q]:
+                        ctypes.memmove(rbuf + rd_[q], recv.data_ptr() + o, rb_[q])
+                    o += rb_[q]
+                return 0
+            except Exception as e:  # never let an exception cross the C boundary
+                import sys
+                print("superbblas_amd host all-to-all failed: %r" % e, file=sys.stderr)
+                return 1
+
+        return cls(n, rank, None, device, _host_fn=_ALLTOALLV_FN(exchange))
 
     @staticmethod
     def unique_id() -> bytes:
@@ -352,6 +402,8 @@ def basic_partitioning_ext(dim: Sequence[int], procs: Sequence[int], nprocs: int
 
 def make_hole(frm, size, hole_from, hole_size, dim):
     nd = len(dim)
+    if not all(len(x) == nd for x in (frm, size, hole_from, hole_size)):
+        raise SuperbblasError("make_hole: coordinates of different rank")
     maxout = 4 * max(nd, 1) * (1 << min(nd, 6))
     out = _ints([0] * (maxout * 2 * nd))
     nout = ctypes.c_int()
@@ -395,6 +447,24 @@ def copy(alpha, p0, o0: str, from0, size0, dim0, v0: Sequence[torch.Tensor], p1,
     _check(_lib.sbx_copy(nd0, nd1, _scalar(alpha), t0, t1, a[0], nc0, o0.encode(), a[1], a[2],
                          a[3], pp[0], a[4], a[5], nc1, o1.encode(), a[6], a[7], pp[1], a[8],
                          _comm(comm), co, copyadd, 0))
+
+
+def copy_plan(p0, o0: str, from0, size0, dim0, ncomponents0: int, p1, o1: str, from1, dim1,
+              ncomponents1: int, nprocs: int, rank: int, co: int = SlowToFast,
+              copyadd: int = Copy):
+    """Host-side exchange plan of `copy` as rank `rank` of `nprocs` would run it (no GPU work):
+    returns (send[q], recv[q], local) element counts."""
+    nd0, nd1 = len(o0), len(o1)
+    if len(p0) != nprocs * ncomponents0 or len(p1) != nprocs * ncomponents1:
+        raise SuperbblasError("partition is incompatible with nprocs/components")
+    send = (ctypes.c_longlong * nprocs)()
+    recv = (ctypes.c_longlong * nprocs)()
+    local = ctypes.c_longlong()
+    _check(_lib.sbx_copy_plan(nd0, nd1, _partition(p0, nd0), ncomponents0, o0.encode(),
+                              _ints(from0), _ints(size0), _ints(dim0), _partition(p1, nd1),
+                              ncomponents1, o1.encode(), _ints(from1), _ints(dim1), nprocs, rank,
+                              co, copyadd, send, recv, ctypes.byref(local)))
+    return list(send), list(recv), local.value
 
 
 def contraction(alpha, p0, from0, size0, dim0, o0: str, conj0: bool, v0, p1, from1, size1, dim1,
@@ -528,7 +598,7 @@ def bsr_get_preferred_layout(bsr: BSR, ncomponents: int = 1, co: int = SlowToFas
 
 __all__ = [
     "SlowToFast", "FastToSlow", "Copy", "Add", "RowMajor", "ColumnMajor", "SuperbblasError",
-    "Comm", "copy", "contraction", "local_copy", "xgemm_batch_strided", "create_bsr",
+    "Comm", "copy", "copy_plan", "contraction", "local_copy", "xgemm_batch_strided", "create_bsr",
     "bsr_krylov", "bsr_get_preferred_layout", "basic_partitioning", "basic_partitioning_ext",
     "partitioning_distributed_procs", "make_hole", "sync", "stream", "set_stream",
     "clear_caches", "get_gpu_devices_count", "version", "LIB_PATH",

@@ -29,6 +29,7 @@ void trim_pools();
 
 struct sbx_comm_s {
     sbx::Comm c;
+    std::unique_ptr<sbx::HostStage> stage;
 };
 struct sbx_bsr_s {
     sbx::BsrOp *op = nullptr;
@@ -278,6 +279,23 @@ int sbx_comm_create(int nprocs, int rank, const unsigned char *id, int device, s
     });
 }
 
+int sbx_comm_create_host(int nprocs, int rank, int device, sbx_alltoallv_fn fn, void *user,
+                         sbx_comm *comm) {
+    return guard([&] {
+        if (nprocs < 1 || rank < 0 || rank >= nprocs) throw Error("invalid rank/nprocs");
+        if (!fn) throw Error("comm_create_host: null all-to-all callback");
+        std::unique_ptr<sbx_comm_s> c(new sbx_comm_s());
+        c->c.nprocs = nprocs;
+        c->c.rank = rank;
+        c->c.device = device;
+        c->c.host_fn = fn;
+        c->c.host_user = user;
+        c->stage.reset(new HostStage());
+        c->c.stage = c->stage.get();
+        *comm = c.release();
+    });
+}
+
 int sbx_comm_rank(sbx_comm comm, int *rank, int *nprocs) {
     return guard([&] {
         const Comm c = get_comm(comm);
@@ -363,6 +381,36 @@ int sbx_copy(int nd0, int nd1, const double *alpha, int t0, int t1, const int *p
         dist_copy(to_scalar(alpha), a, to_coor(from0, nd0, rev), to_coor(size0, nd0, rev), b,
                   to_coor(from1, nd1, rev), copyadd == SBX_ADD, c);
         finish_mirror(m);
+    });
+}
+
+int sbx_copy_plan(int nd0, int nd1, const int *p0, int ncomponents0, const char *o0,
+                  const int *from0, const int *size0, const int *dim0, const int *p1,
+                  int ncomponents1, const char *o1, const int *from1, const int *dim1, int nprocs,
+                  int rank, int co, int copyadd, long long *send, long long *recv,
+                  long long *local) {
+    return guard([&] {
+        if (nprocs < 1 || rank < 0 || rank >= nprocs) throw Error("copy_plan: invalid rank");
+        const bool rev = co == SBX_FAST_TO_SLOW;
+        Comm c;
+        c.nprocs = nprocs;
+        c.rank = rank;
+        DistTensor a, b;
+        a.labels = to_labels(o0, nd0, rev, "o0");
+        a.dim = to_coor(dim0, nd0, rev);
+        a.ranges = to_ranges(p0, nd0, ncomponents0, c, rev);
+        b.labels = to_labels(o1, nd1, rev, "o1");
+        b.dim = to_coor(dim1, nd1, rev);
+        b.ranges = to_ranges(p1, nd1, ncomponents1, c, rev);
+        std::vector<long> s, r;
+        long l = 0;
+        copy_plan_counts(a, to_coor(from0, nd0, rev), to_coor(size0, nd0, rev), b,
+                         to_coor(from1, nd1, rev), copyadd == SBX_ADD, rank, s, r, l);
+        for (int q = 0; q < nprocs; ++q) {
+            send[q] = s[q];
+            recv[q] = r[q];
+        }
+        *local = l;
     });
 }
 

@@ -235,11 +235,72 @@ void nccl_check(ncclResult_t r, const char *what) {
         throw Error(std::string("RCCL error in ") + what + ": " + ncclGetErrorString(r));
 }
 
+/// Exchange packed per-peer buffers through the host callback of a host-staged communicator
+void host_exchange(const Comm &comm, const void *sdev, const std::vector<std::size_t> &send_bytes,
+                   const std::vector<std::size_t> &send_off, void *rdev,
+                   const std::vector<std::size_t> &recv_bytes,
+                   const std::vector<std::size_t> &recv_off, hipStream_t s) {
+    HostStage &st = *comm.stage;
+    const std::size_t ns = send_off.back(), nr = recv_off.back();
+    if (st.send_cap < ns) {
+        if (st.send) SBX_HIP_CHECK(hipHostFree(st.send));
+        st.send = nullptr;
+        st.send_cap = 0;
+        SBX_HIP_CHECK(hipHostMalloc(&st.send, ns, hipHostMallocDefault));
+        st.send_cap = ns;
+    }
+    if (st.recv_cap < nr) {
+        if (st.recv) SBX_HIP_CHECK(hipHostFree(st.recv));
+        st.recv = nullptr;
+        st.recv_cap = 0;
+        SBX_HIP_CHECK(hipHostMalloc(&st.recv, nr, hipHostMallocDefault));
+        st.recv_cap = nr;
+    }
+    if (ns) SBX_HIP_CHECK(hipMemcpyAsync(st.send, sdev, ns, hipMemcpyDeviceToHost, s));
+    SBX_HIP_CHECK(hipStreamSynchronize(s));
+    std::vector<unsigned long long> sb(comm.nprocs), sd(comm.nprocs), rb(comm.nprocs),
+        rd(comm.nprocs);
+    for (int q = 0; q < comm.nprocs; ++q) {
+        const bool self = q == comm.rank;
+        sb[q] = self ? 0 : send_bytes[q];
+        sd[q] = send_off[q];
+        rb[q] = self ? 0 : recv_bytes[q];
+        rd[q] = recv_off[q];
+    }
+    const int rc = comm.host_fn(st.send, sb.data(), sd.data(), st.recv, rb.data(), rd.data(),
+                                comm.host_user);
+    if (rc != 0) throw Error("copy: the host all-to-all callback failed (" + std::to_string(rc) + ")");
+    if (nr) SBX_HIP_CHECK(hipMemcpyAsync(rdev, st.recv, nr, hipMemcpyHostToDevice, s));
+}
+
 } // namespace
+
+HostStage::~HostStage() {
+    if (send) (void)hipHostFree(send);
+    if (recv) (void)hipHostFree(recv);
+}
 
 //
 // Distributed copy
 //
+
+void copy_plan_counts(const DistTensor &src, const Coor &from0, const Coor &size0,
+                      const DistTensor &dst, const Coor &from1, bool add, int rank,
+                      std::vector<long> &send, std::vector<long> &recv, long &local) {
+    const int nprocs = (int)src.ranges.size();
+    send.assign(nprocs, 0);
+    recv.assign(nprocs, 0);
+    local = 0;
+    if (volume(size0) == 0) return;
+    const std::vector<CompRef> sc = flatten_components(src), dc = flatten_components(dst);
+    for (const Piece &p : plan_copy(src, from0, size0, dst, from1, add, rank)) {
+        const int ra = sc[p.a].rank, rb = dc[p.b].rank;
+        const long n = volume(p.size);
+        if (ra == rank && rb == rank) local += n;
+        else if (ra == rank) send[rb] += n;
+        else if (rb == rank) recv[ra] += n;
+    }
+}
 
 void dist_copy(const Scalar &alpha, const DistTensor &src, const Coor &from0, const Coor &size0,
                const DistTensor &dst, const Coor &from1, bool add, const Comm &comm) {
@@ -388,18 +449,29 @@ void dist_copy(const Scalar &alpha, const DistTensor &src, const Coor &from0, co
     }
     set_device(device);
     hipStream_t s = get_stream(device);
-    ncclComm_t nc = (ncclComm_t)comm.nccl;
-    nccl_check(ncclGroupStart(), "ncclGroupStart");
-    for (int q = 0; q < comm.nprocs; ++q) {
-        if (q == comm.rank) continue;
-        if (send_bytes[q] > 0)
-            nccl_check(ncclSend((char *)sbuf.ptr + send_off[q], send_bytes[q], ncclChar, q, nc, s),
-                       "ncclSend");
-        if (recv_bytes[q] > 0)
-            nccl_check(ncclRecv((char *)rbuf.ptr + recv_off[q], recv_bytes[q], ncclChar, q, nc, s),
-                       "ncclRecv");
+    if (comm.nccl) {
+        // RCCL: grouped point-to-point send/recv straight from/to device memory (xGMI)
+        ncclComm_t nc = (ncclComm_t)comm.nccl;
+        nccl_check(ncclGroupStart(), "ncclGroupStart");
+        for (int q = 0; q < comm.nprocs; ++q) {
+            if (q == comm.rank) continue;
+            if (send_bytes[q] > 0)
+                nccl_check(ncclSend((char *)sbuf.ptr + send_off[q], send_bytes[q], ncclChar, q,
+                                    nc, s),
+                           "ncclSend");
+            if (recv_bytes[q] > 0)
+                nccl_check(ncclRecv((char *)rbuf.ptr + recv_off[q], recv_bytes[q], ncclChar, q,
+                                    nc, s),
+                           "ncclRecv");
+        }
+        nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+    } else if (comm.host_fn && comm.stage) {
+        // Host-staged: device -> pinned host, the caller's all-to-all, pinned host -> device
+        // (the reference's non-GPU-aware MPI path, dist.h:1426-1500)
+        host_exchange(comm, sbuf.ptr, send_bytes, send_off, rbuf.ptr, recv_bytes, recv_off, s);
+    } else {
+        throw Error("copy: the communicator has no transport");
     }
-    nccl_check(ncclGroupEnd(), "ncclGroupEnd");
     {
         std::vector<std::size_t> cur(recv_off.begin(), recv_off.end() - 1);
         for (const Piece &p : pieces) {

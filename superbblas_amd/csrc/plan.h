@@ -73,11 +73,27 @@ std::vector<Range> basic_partitioning_ext(const Coor &dim, const Coor &procs, in
 std::vector<int> find_permutation(const std::string &from, const std::string &to);
 
 /// Communicator: nprocs == 1 means a single process (SelfComm, dist.h:142-149)
+/// Host all-to-all callback of a host-staged communicator (sbx_alltoallv_fn in sbx.h)
+typedef int (*HostAlltoallv)(const void *sendbuf, const unsigned long long *sendbytes,
+                             const unsigned long long *senddispls, void *recvbuf,
+                             const unsigned long long *recvbytes,
+                             const unsigned long long *recvdispls, void *user);
+
+/// Pinned host staging buffers of a host-staged communicator (grown on demand, reused)
+struct HostStage {
+    void *send = nullptr, *recv = nullptr;
+    std::size_t send_cap = 0, recv_cap = 0;
+    ~HostStage();
+};
+
 struct Comm {
     int nprocs = 1;
     int rank = 0;
     int device = -1;
-    void *nccl = nullptr; // ncclComm_t
+    void *nccl = nullptr;            // ncclComm_t (RCCL transport: device buffers over xGMI)
+    HostAlltoallv host_fn = nullptr; // host-staged transport (e.g. MPI_Alltoallv, gloo)
+    void *host_user = nullptr;
+    HostStage *stage = nullptr;      // owned by the sbx_comm handle
 };
 
 /// A distributed tensor as seen by one process.
@@ -111,6 +127,12 @@ struct Local {
 /// copy: dst[from1 + P(c - from0)] (=|+=) alpha * src[c] for c in [from0, from0+size0)
 void dist_copy(const Scalar &alpha, const DistTensor &src, const Coor &from0, const Coor &size0,
                const DistTensor &dst, const Coor &from1, bool add, const Comm &comm);
+
+/// Element counts of the exchange dist_copy would do on `rank`: send[q] / recv[q] elements to /
+/// from rank q (q != rank) and `local` elements moved within the rank (no GPU work)
+void copy_plan_counts(const DistTensor &src, const Coor &from0, const Coor &size0,
+                      const DistTensor &dst, const Coor &from1, bool add, int rank,
+                      std::vector<long> &send, std::vector<long> &recv, long &local);
 
 /// contraction: vr = alpha * contract(v0, v1) + beta * vr over the boxes [from, from+size)
 void dist_contraction(const Scalar &alpha, const DistTensor &v0, const Coor &from0,

@@ -1,0 +1,199 @@
+"""One rank of the multi-process GPU parity run (launched by tests/test_gpu_dist.py through
+torch.distributed.run).  Every rank holds its components on the GPU; the library redistributes
+them through its communicator (RCCL, or the host-staged transport so several ranks can share one
+GPU); rank 0 gathers the results and compares them with the oracle on the global tensors.
+
+Cases (all multi-rank: the exchange, pack/unpack kernels and reductions run for real):
+  copy   -- lattice field distributed over t, copied permuted/shifted/wrapped into a tensor
+            distributed over x (Copy and Add)  [dist.h:2264-2438]
+  contr  -- tnsxyzc x tNSxyzc -> tNSns with v0 split over z, v1 split over t (redistributed),
+            output on rank 0 (cross-rank reduction) and output split over t with beta != 0
+            [dist.h:3092-3196]
+  bsr    -- 9-point stencil operator split over t with a halo domain partition, x split over t,
+            y split over t  [bsr.h:2107-2266]
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+
+from _common import (T_CDOUBLE, oracle_bsr, oracle_contraction, oracle_copy,  # noqa: E402
+                     rel_err)
+from _golden import gen, piece, put_piece, vol  # noqa: E402
+
+
+def scatter(sb, glob, dim, p, rank, nc, dev):
+    return [torch.from_numpy(piece(glob, dim, *p[rank * nc + i])).to(dev) for i in range(nc)]
+
+
+def gather(glob_init, dim, p, nc, local):
+    """Every rank contributes its components; returns the assembled global tensor on all ranks."""
+    mine = [t.cpu().numpy() for t in local]
+    allc = [None] * dist.get_world_size()
+    dist.all_gather_object(allc, mine)
+    g = glob_init.copy()
+    for rk, comps in enumerate(allc):
+        for i, c in enumerate(comps):
+            f, s = p[rk * nc + i]
+            if vol(s):
+                put_piece(g, dim, f, s, c)
+    return g
+
+
+def case_copy(sb, comm, rank, n, dev):
+    dim0, dim1 = [4, 4, 2, 6], [6, 2, 4, 4]
+    p0 = sb.basic_partitioning("xyzt", dim0, [1, 1, 1, n], "t", n, 1)
+    p1 = sb.basic_partitioning("tzyx", dim1, [1, 1, 1, n], "x", n, 1)
+    g0 = gen("index", vol(dim0), 1, np.complex128)
+    for add in (False, True):
+        g1 = gen("int", vol(dim1), 2, np.complex128)
+        v0 = scatter(sb, g0, dim0, p0, rank, 1, dev)
+        v1 = scatter(sb, g1, dim1, p1, rank, 1, dev)
+        sb.copy(2.0 if add else 1.0, p0, "xyzt", [1, 2, 0, 3], [3, 4, 2, 5], dim0, v0, p1,
+                "tzyx", [2, 0, 1, 3], dim1, v1, copyadd=sb.Add if add else sb.Copy, comm=comm)
+        torch.cuda.synchronize()
+        out = gather(np.zeros_like(g1), dim1, p1, 1, v1)
+        ref = g1.copy()
+        oracle_copy(2.0 if add else 1.0, "xyzt", [1, 2, 0, 3], [3, 4, 2, 5], dim0, g0, "tzyx",
+                    [2, 0, 1, 3], dim1, ref, add=add)
+        # untouched destination elements live in their owner's component: compare everything
+        assert np.array_equal(out.view(np.uint8), ref.view(np.uint8)), ("copy", add)
+
+
+def case_contraction(sb, comm, rank, n, dev):
+    L, nn = 4, 2
+    d0 = [L, nn, 4, L, L, L * n, 3]  # tnsxyzc, z grows with the ranks (weak scaling)
+    dr = [L, nn, 4, nn, 4]  # tNSns
+    p0 = sb.basic_partitioning("tnsxyzc", d0, [1, 1, 1, 1, 1, n, 1], "z", n, 1)
+    p1 = sb.basic_partitioning("tNSxyzc", d0, [n, 1, 1, 1, 1, 1, 1], "t", n, 1)
+    g0 = gen("int", vol(d0), 1, np.complex128)
+    g1 = gen("int", vol(d0), 2, np.complex128)
+    v0 = scatter(sb, g0, d0, p0, rank, 1, dev)
+    v1 = scatter(sb, g1, d0, p1, rank, 1, dev)
+    z7, z5 = [0] * 7, [0] * 5
+    # (a) output on rank 0 only, beta = 0
+    pr = [([0] * 5, dr)] + [([0] * 5, [0] * 5)] * (n - 1)
+    gr = gen("int", vol(dr), 3, np.complex128)
+    vr = scatter(sb, gr, dr, pr, rank, 1, dev)
+    if vr[0].numel() == 0:
+        vr = [torch.zeros(1, dtype=torch.complex128, device=dev)]
+    sb.contraction(1.0, p0, z7, d0, d0, "tnsxyzc", False, v0, p1, z7, d0, d0, "tNSxyzc", False,
+                   v1, 0.0, pr, z5, dr, dr, "tNSns", vr, comm=comm)
+    torch.cuda.synchronize()
+    out = gather(np.zeros_like(gr), dr, pr, 1, vr[:1] if rank == 0 else [vr[0][:0]])
+    ref = np.zeros_like(gr)
+    oracle_contraction(1.0, "tnsxyzc", z7, d0, d0, False, g0, "tNSxyzc", z7, d0, d0, False, g1,
+                       0.0, "tNSns", z5, dr, dr, ref)
+    assert np.array_equal(out, ref), "contraction (a)"
+    # (b) output split over t, conj v0, complex alpha/beta, a shifted window in t
+    pr = sb.basic_partitioning("tNSns", dr, [n, 1, 1, 1, 1], "t", n, 1)
+    vr = scatter(sb, gr, dr, pr, rank, 1, dev)
+    alpha, beta = 0.5 - 1j, -1 + 0.25j
+    sb.contraction(alpha, p0, [1, 0, 0, 0, 0, 0, 0], d0, d0, "tnsxyzc", True, v0, p1,
+                   [1, 0, 0, 0, 0, 0, 0], d0, d0, "tNSxyzc", False, v1, beta, pr,
+                   [2, 0, 0, 0, 0], dr, dr, "tNSns", vr, comm=comm)
+    torch.cuda.synchronize()
+    out = gather(np.zeros_like(gr), dr, pr, 1, vr)
+    ref = gr.copy()
+    oracle_contraction(alpha, "tnsxyzc", [1, 0, 0, 0, 0, 0, 0], d0, d0, True, g0, "tNSxyzc",
+                       [1, 0, 0, 0, 0, 0, 0], d0, d0, False, g1, beta, "tNSns", [2, 0, 0, 0, 0],
+                       dr, dr, ref)
+    assert np.array_equal(out, ref), "contraction (b)"
+
+
+def case_bsr(sb, comm, rank, n, dev, ncols=3):
+    L = 4
+    Lt = 2 * n
+    dim = [L, L, L, Lt, 1, 3]
+    b = 3
+    pi = sb.basic_partitioning("xyztsc", dim, [1, 1, 1, n, 1, 1], "xyzt", n, 1)
+    # domain partition: image plus a one-site halo in every lattice direction (bsr.cpp:61-79)
+    pd = []
+    for f, s in pi:
+        f, s = list(f), list(s)
+        for d in range(4):
+            s[d] = min(dim[d], s[d] + 2)
+            f[d] = (f[d] - 1) % dim[d] if s[d] < dim[d] else 0
+        pd.append((f, s))
+    f, s = pi[rank]
+    sites = np.array(np.unravel_index(np.arange(vol(s[:4])), s[:4])).T + np.array(f[:4])
+    dom = np.array(dim[:4])
+    jj, rows = [], []
+    for st in sites:
+        for k, (d, dr) in enumerate([(None, 0)] + [(d, dr) for d in range(4) for dr in (-1, 1)]):
+            c = st.copy()
+            if d is not None:
+                c[d] += dr
+            jj.append(list((c - np.array(pd[rank][0][:4])) % dom) + [0, 0])
+    gsite = np.ravel_multi_index(tuple((sites % dom).T), dim[:4])
+    allv = gen("int", vol(dim[:4]) * 9 * b * b, 4, np.complex128).reshape(-1, 9 * b * b)
+    vals = np.ascontiguousarray(allv[gsite]).ravel()
+    ii = np.full(len(sites), 9, np.int32)
+    op = sb.create_bsr(pi, dim, pd, dim, [1, 1, 1, 1, 1, 3], [1, 1, 1, 1, 1, 3], False,
+                       [torch.from_numpy(ii).to(dev)],
+                       [torch.from_numpy(np.array(jj, np.int32).ravel()).to(dev)],
+                       [torch.from_numpy(vals).to(dev)], comm=comm)
+    dimx = [1, L, L, L, Lt, 1, 3, ncols]
+    px = sb.basic_partitioning("pXYZTSCn", dimx, [1, 1, 1, 1, n, 1, 1, 1], "XYZT", n, 1)
+    gx = gen("int", vol(dimx), 5, np.complex128)
+    gy = gen("int", vol(dimx), 6, np.complex128)
+    vx = scatter(sb, gx, dimx, px, rank, 1, dev)
+    vy = scatter(sb, gy, dimx, px, rank, 1, dev)
+    z8 = [0] * 8
+    sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", px, "pXYZTSCn", z8, dimx, dimx, vx, 0.0, px,
+                  "pxyztscn", z8, dimx, dimx, "p", vy, comm=comm)
+    torch.cuda.synchronize()
+    op.destroy()
+    out = gather(np.zeros_like(gy), dimx, px, 1, vy)
+    # oracle on the whole lattice: the same operator in one component
+    allsites = np.array(np.unravel_index(np.arange(vol(dim[:4])), dim[:4])).T
+    jg = []
+    for st in allsites:
+        for d, dr in [(None, 0)] + [(d, dr) for d in range(4) for dr in (-1, 1)]:
+            c = st.copy()
+            if d is not None:
+                c[d] += dr
+            jg.append(list(c % dom) + [0, 0])
+    ref = np.zeros_like(gy)
+    V = vol(dim[:4])
+    oracle_bsr(T_CDOUBLE, dim, 0, V, b, b, np.full(V, 9, np.int32),
+               np.array(jg, np.int32).ravel(), allv.ravel(), False, gx, ncols, True, ref, ncols,
+               True, ncols, 1.0)
+    assert np.array_equal(out, ref), "bsr"
+
+
+def main():
+    dist.init_process_group("gloo")
+    rank, n = dist.get_rank(), dist.get_world_size()
+    ndev = torch.cuda.device_count()
+    dev_idx = int(os.environ.get("LOCAL_RANK", "0")) % ndev
+    torch.cuda.set_device(dev_idx)
+    dev = torch.device("cuda", dev_idx)
+    import superbblas_amd as sb
+    transport = os.environ.get("SBX_TEST_TRANSPORT", "host")
+    if transport == "rccl":
+        comm = sb.Comm.from_torch_distributed(dev_idx)
+    else:
+        comm = sb.Comm.host_staged(dev_idx)
+    cases = os.environ.get("SBX_TEST_CASES", "copy,contr,bsr").split(",")
+    if "copy" in cases:
+        case_copy(sb, comm, rank, n, dev)
+    if "contr" in cases:
+        case_contraction(sb, comm, rank, n, dev)
+    if "bsr" in cases:
+        case_bsr(sb, comm, rank, n, dev)
+    dist.barrier()
+    comm.close()
+    dist.destroy_process_group()
+    if rank == 0:
+        print("DIST OK ranks=%d transport=%s cases=%s" % (n, transport, ",".join(cases)))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,120 @@
+"""Replay the reference's golden vectors (tests/golden, produced by oracle/ref_golden.cpp from the
+real reference) through the library on the GPU, component by component as the reference ran them.
+
+Multi-component cases put the odd components in host memory, so the same call also exercises
+mixed host/device components (the reference allows a Context per component, platform.h:757-773).
+Copies and the integer-valued contractions / BSR products are exact, so every comparison is
+bit-exact."""
+import numpy as np
+import pytest
+
+from _golden import NPT, gen, manifest, output, piece, put_piece, vol
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(i, n, gpu):
+    return gpu if (n == 1 or i % 2 == 0) else "cpu"
+
+
+def _scatter(glob, dim, p, gpu):
+    import torch
+    return [torch.from_numpy(piece(glob, dim, f, s)).to(_dev(i, len(p), gpu))
+            for i, (f, s) in enumerate(p)]
+
+
+def _gather(comps, dim, p, dtype):
+    g = np.zeros(vol(dim), dtype)
+    for (f, s), c in zip(p, comps):
+        put_piece(g, dim, f, s, c.cpu().numpy())
+    return g
+
+
+@pytest.mark.parametrize("case", manifest("copy"), ids=lambda c: "copy%d" % c["id"])
+def test_golden_copy(gpu, case):
+    import torch
+    import superbblas_amd as sb
+    t0, t1 = NPT[case["t0"]], NPT[case["t1"]]
+    g0 = gen(case["gen0"], vol(case["dim0"]), 1, t0)
+    g1 = gen(case["gen1"], vol(case["dim1"]), 2, t1)
+    v0 = _scatter(g0, case["dim0"], case["p0"], gpu)
+    v1 = _scatter(g1, case["dim1"], case["p1"], gpu)
+    sb.copy(complex(*case["alpha"]) if np.dtype(t0).kind == "c" else case["alpha"][0],
+            case["p0"], case["o0"], case["from0"], case["size0"], case["dim0"], v0,
+            case["p1"], case["o1"], case["from1"], case["dim1"], v1,
+            copyadd=sb.Add if case["add"] else sb.Copy)
+    torch.cuda.synchronize()
+    out = _gather(v1, case["dim1"], case["p1"], t1)
+    ref = output(case, t1)
+    assert np.array_equal(out.view(np.uint8), ref.view(np.uint8))
+
+
+@pytest.mark.parametrize("case", manifest("contraction"), ids=lambda c: "contr%d" % c["id"])
+def test_golden_contraction(gpu, case):
+    import torch
+    import superbblas_amd as sb
+    t = NPT[case["t"]]
+    v0 = _scatter(gen("int", vol(case["dim0"]), 1, t), case["dim0"], case["p0"], gpu)
+    v1 = _scatter(gen("int", vol(case["dim1"]), 2, t), case["dim1"], case["p1"], gpu)
+    vr = _scatter(gen("int", vol(case["dimr"]), 3, t), case["dimr"], case["pr"], gpu)
+    cplx = np.dtype(t).kind == "c"
+    alpha = complex(*case["alpha"]) if cplx else case["alpha"][0]
+    beta = complex(*case["beta"]) if cplx else case["beta"][0]
+    sb.contraction(alpha, case["p0"], case["from0"], case["size0"], case["dim0"], case["o0"],
+                   case["conj0"], v0, case["p1"], case["from1"], case["size1"], case["dim1"],
+                   case["o1"], case["conj1"], v1, beta, case["pr"], case["fromr"], case["sizer"],
+                   case["dimr"], case["o_r"], vr)
+    torch.cuda.synchronize()
+    out = _gather(vr, case["dimr"], case["pr"], t)
+    # integer-valued inputs: every partial sum is exact in f64
+    assert np.array_equal(out, output(case, t))
+
+
+def _bsr_component(L, spin, color, pi_c, pd_c):
+    """ii/jj/nonzeros of one component of ref_golden.cpp bsr_case (tests/bsr.cpp:169-255)."""
+    b = spin * color
+    dimi = list(pi_c[1][:4])
+    sites = np.array(np.unravel_index(np.arange(vol(dimi)), dimi)).T + np.array(pi_c[0][:4])
+    dom = np.array([L, L, L, L])
+    jj = []
+    for s in sites:
+        nb = [s.copy()]
+        for d in range(4):
+            for dr in (-1, 1):
+                c = s.copy()
+                c[d] += dr
+                nb.append(c)
+        for c in nb:
+            jj.append(list((c - np.array(pd_c[0][:4])) % dom) + [0, 0])
+    glob_site = ((sites[:, 0] * L + sites[:, 1]) * L + sites[:, 2]) * L + sites[:, 3]
+    allv = gen("int", L ** 4 * 9 * b * b, 4, np.complex128).reshape(L ** 4, 9 * b * b)
+    vals = np.ascontiguousarray(allv[glob_site]).ravel()
+    ii = np.full(len(sites), 9, np.int32)
+    return ii, np.array(jj, np.int32).ravel(), vals
+
+
+@pytest.mark.parametrize("case", manifest("bsr"), ids=lambda c: "bsr%d" % c["id"])
+def test_golden_bsr(gpu, case):
+    import torch
+    import superbblas_amd as sb
+    L, spin, color, ncols = case["L"], case["spin"], case["color"], case["ncols"]
+    dim = [L, L, L, L, spin, color]
+    iis, jjs, vs = [], [], []
+    for pi_c, pd_c in zip(case["pi"], case["pd"]):
+        ii, jj, v = _bsr_component(L, spin, color, pi_c, pd_c)
+        iis.append(torch.from_numpy(ii).to(gpu))
+        jjs.append(torch.from_numpy(jj).to(gpu))
+        vs.append(torch.from_numpy(v).to(gpu))
+    blk = [1, 1, 1, 1, spin, color]
+    op = sb.create_bsr(case["pi"], dim, case["pd"], dim, blk, blk, False, iis, jjs, vs)
+    dimx = [1, L, L, L, L, spin, color, ncols]
+    gx = gen("int", vol(dimx), 5, np.complex128)
+    gy = gen("int", vol(dimx), 6, np.complex128)
+    vx = [torch.from_numpy(piece(gx, dimx, f, s)).to(gpu) for f, s in case["px"]]
+    vy = [torch.from_numpy(piece(gy, dimx, f, s)).to(gpu) for f, s in case["py"]]
+    sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", case["px"], "pXYZTSCn", [0] * 8, dimx, dimx, vx,
+                  0.0, case["py"], "pxyztscn", [0] * 8, dimx, dimx, "p", vy)
+    torch.cuda.synchronize()
+    op.destroy()
+    out = _gather(vy, dimx, case["py"], np.complex128)
+    assert np.array_equal(out, output(case, np.complex128))
