@@ -78,6 +78,16 @@ int sbx_clear_handles(void);
 int sbx_allocate(unsigned long long bytes, sbx_context ctx, void **ptr);
 int sbx_deallocate(void *ptr, sbx_context ctx);
 
+/* ---- kernel timers (reportTimings / resetTimings, performance.h:356-518) ----
+   When enabled, every GPU kernel family ("gemm", "gemm_splitk_reduce", "copy", "bsr") is
+   bracketed by HIP events on the stream it is launched on; totals are summed on query. */
+int sbx_timings_enable(int on);
+int sbx_timings_reset(void);
+/* total milliseconds and launch count of one kernel family (synchronizes its events) */
+int sbx_timings_get(const char *name, double *ms, long long *calls);
+/* "name calls total_ms" per line into buf (truncated to len-1 chars) */
+int sbx_timings_report(char *buf, int len);
+
 /* ---- communicator (replaces MPI; dist.h:1426-1773 send_receive) ---- */
 
 /* Fill `id` (128 bytes) with a fresh RCCL unique id; call on one rank and broadcast it */

@@ -248,6 +248,28 @@ def set_stream(device: int, hip_stream: Optional[int]):
         _check(_lib.sbx_stream_set(device, ctypes.c_void_p(hip_stream)))
 
 
+def timings_enable(on: bool = True):
+    """Time every GPU kernel family with HIP events on its launch stream (reportTimings)."""
+    _check(_lib.sbx_timings_enable(int(on)))
+
+
+def timings_reset():
+    _check(_lib.sbx_timings_reset())
+
+
+def timings_get(name: str) -> Tuple[float, int]:
+    """(total milliseconds, launches) of a kernel family: gemm, gemm_splitk_reduce, copy, bsr."""
+    ms, calls = ctypes.c_double(), ctypes.c_longlong()
+    _check(_lib.sbx_timings_get(name.encode(), ctypes.byref(ms), ctypes.byref(calls)))
+    return ms.value, calls.value
+
+
+def timings_report() -> str:
+    buf = ctypes.create_string_buffer(8192)
+    _check(_lib.sbx_timings_report(buf, len(buf)))
+    return buf.value.decode()
+
+
 def clear_caches():
     """clearCaches (alloc.h:437-443)"""
     _check(_lib.sbx_clear_caches())
@@ -601,5 +623,6 @@ __all__ = [
     "Comm", "copy", "copy_plan", "contraction", "local_copy", "xgemm_batch_strided", "create_bsr",
     "bsr_krylov", "bsr_get_preferred_layout", "basic_partitioning", "basic_partitioning_ext",
     "partitioning_distributed_procs", "make_hole", "sync", "stream", "set_stream",
-    "clear_caches", "get_gpu_devices_count", "version", "LIB_PATH",
+    "clear_caches", "timings_enable", "timings_reset", "timings_get", "timings_report",
+    "get_gpu_devices_count", "version", "LIB_PATH",
 ]

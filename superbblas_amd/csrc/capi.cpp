@@ -248,6 +248,32 @@ int sbx_deallocate(void *ptr, sbx_context ctx) {
     });
 }
 
+int sbx_timings_enable(int on) {
+    return guard([&] { timings_enable(on != 0); });
+}
+
+int sbx_timings_reset(void) {
+    return guard([&] { timings_reset(); });
+}
+
+int sbx_timings_get(const char *name, double *ms, long long *calls) {
+    return guard([&] {
+        if (!name || !ms || !calls) throw Error("timings_get: null argument");
+        timings_get(name, ms, calls);
+    });
+}
+
+int sbx_timings_report(char *buf, int len) {
+    return guard([&] {
+        const std::string r = timings_report();
+        if (buf && len > 0) {
+            const int n = std::min((int)r.size(), len - 1);
+            std::memcpy(buf, r.data(), n);
+            buf[n] = 0;
+        }
+    });
+}
+
 int sbx_comm_unique_id(unsigned char *id) {
     return guard([&] {
         ncclUniqueId u;

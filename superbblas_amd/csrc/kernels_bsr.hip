@@ -205,6 +205,7 @@ void launch_ell(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_t s) 
     const int rb = std::max(1, ELL_LDS_BYTES / std::max(1, blk_bytes));
     const long blocks = (a.block_rows + rb - 1) / rb;
     const size_t lds = (size_t)rb * blk_bytes;
+    KernelTimer timer("bsr", s);
     if (yrow && xrow)
         hipLaunchKernelGGL((bsr_ell_kernel<E, BI, BD, true, true>), dim3(blocks), dim3(256), lds, s, a, nnz, rb);
     else if (yrow && !xrow)
@@ -218,6 +219,7 @@ void launch_ell(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_t s) 
 
 template <typename E, int BI, int BD>
 void launch_layouts(const BsrArgs &a, bool yrow, bool xrow, long blocks, hipStream_t s) {
+    KernelTimer timer("bsr", s);
     if (yrow && xrow)
         hipLaunchKernelGGL((bsr_kernel<E, BI, BD, true, true>), dim3(blocks), dim3(256), 0, s, a);
     else if (yrow && !xrow)

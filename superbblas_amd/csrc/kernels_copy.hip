@@ -282,6 +282,7 @@ void launch_pair(const BoxCopyDesc &d, const Norm &n, long total, hipStream_t st
     // Fully contiguous on both sides
     if (n.size.size() == 1 && n.ss[0] == 1 && n.ds[0] == 1) {
         const long blocks = std::min((total + 255) / 256, 8192L);
+        KernelTimer timer("copy", stream);
         hipLaunchKernelGGL((copy_contig_kernel<S, D, ADD>), dim3((unsigned)blocks), dim3(256), 0,
                            stream, src, dst, total, alpha);
         SBX_HIP_CHECK(hipGetLastError());
@@ -330,6 +331,7 @@ void launch_pair(const BoxCopyDesc &d, const Norm &n, long total, hipStream_t st
         a.dstp = dst;
         a.alpha = alpha;
         const long blocks = std::min((total + 255) / 256, 8192L);
+        KernelTimer timer("copy", stream);
         hipLaunchKernelGGL((copy_direct_kernel<S, D, ADD>), dim3((unsigned)blocks), dim3(256), 0,
                            stream, a);
         SBX_HIP_CHECK(hipGetLastError());
@@ -385,6 +387,7 @@ void launch_pair(const BoxCopyDesc &d, const Norm &n, long total, hipStream_t st
     a.alpha = alpha;
     const long blocks = (long)a.ntu * a.ntv * NW;
     if (blocks >= (1L << 31)) throw Error("copy: grid too large");
+    KernelTimer timer("copy", stream);
     hipLaunchKernelGGL((copy_tiled_kernel<S, D, ADD>), dim3((unsigned)blocks), dim3(256), 0,
                        stream, a);
     SBX_HIP_CHECK(hipGetLastError());

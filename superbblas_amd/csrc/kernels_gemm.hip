@@ -21,6 +21,7 @@
 #include "sbx_internal.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace sbx {
 namespace {
@@ -277,6 +278,199 @@ __global__ void __launch_bounds__(WM *WN * 64) gemm_kernel(const GemmKArgs p) {
             }
 }
 
+// ---------------------------------------------------------------------------------------------
+// complex<double> kernel with LDS-DMA staging (buffer_load_dwordx4 ... lds)
+//
+// One complex<double> is exactly one 16-byte LDS-DMA lane, so both operands go global -> LDS
+// with no VGPR round trip and no ds_write pass.  Per operand the LDS image of a 16-deep K slab
+// is either
+//   K-major  [row][16 k], 256-B rows, the 16-B column XOR-swizzled by (row & 15) on the SOURCE
+//            address (the DMA destination is lane-linear), so the 16 lanes of a fragment read
+//            (16 rows, same k) hit 16 different bank groups;
+//   M-major  [16 k][rows] (operand contiguous along m / n), read conflict-free as is.
+// Two LDS buffers, one barrier per slab: the DMA of slab s+1 is in flight while slab s feeds the
+// MFMAs (the barrier's vmcnt(0) retires it one slab later).  Out-of-range rows/k read zero
+// through the buffer descriptor (no branches).  Conjugation flips the fragment's imaginary sign.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ unsigned lds_addr(const void *p) {
+    return (unsigned)(size_t)(const __attribute__((address_space(3))) void *)p;
+}
+
+template <bool XK, int R, int BKK, int NTH>
+struct DmaOperand {
+    static_assert(BKK == 8 || BKK == 16, "slab depth");
+    static constexpr int NI = R * BKK / NTH; // 16-B DMA lanes per thread per slab
+    static_assert(NI * NTH == R * BKK, "tile/threads mismatch");
+    unsigned roff[NI]; // byte offset of this lane's element at k0 = 0
+    int kl[NI];        // k within the slab fetched by each instruction
+    bool rok[NI];
+    // K-major image: 16-B column swizzle so that the 16 rows of a fragment read hit distinct
+    // bank groups (256-B rows: col ^ row; 128-B rows: col ^ (row / 2), two rows per bank row)
+    static __device__ __forceinline__ int swz(int row) {
+        return BKK == 16 ? (row & 15) : ((row >> 1) & 7);
+    }
+    __device__ __forceinline__ void init(int tid, long r0, long nrows, long s_r, long s_k) {
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int slot = tid + NTH * i; // lane-linear LDS slot of this lane
+            int r, k;
+            if (XK) {
+                r = slot / BKK;
+                k = (slot % BKK) ^ swz(r);
+            } else {
+                r = slot % R;
+                k = slot / R;
+            }
+            const long gr = r0 + r;
+            rok[i] = gr < nrows;
+            kl[i] = k;
+            roff[i] = (unsigned)((rok[i] ? gr : 0) * s_r * 16 + (long)k * s_k * 16);
+        }
+    }
+    // issue the DMA of slab [k0, k0+BKK) into the image at `lds_base`
+    __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, const char *lds_base,
+                                          int wave, long k0, long k_end, long s_k) const {
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const bool ok = rok[i] && (k0 + kl[i] < k_end);
+            const unsigned off = ok ? roff[i] + (unsigned)(k0 * s_k * 16) : 0x80000000u;
+            // inline asm so that hipcc does not wait vmcnt(0) before every ds_read of the
+            // other buffer (it cannot tell the DMA target from the buffer being read); the
+            // kernel retires the DMA itself with an explicit vmcnt(0) before its barrier
+            const unsigned dst = lds_addr(lds_base) + (unsigned)(i * NTH + wave * 64) * 16;
+            asm volatile("s_mov_b32 m0, %1\n\t"
+                         "s_nop 0\n\t"
+                         "buffer_load_dwordx4 %0, %2, 0 offen lds"
+                         :
+                         : "v"(off), "s"(dst), "s"(rs)
+                         : "memory", "m0");
+        }
+    }
+    // LDS slot of fragment element (row, k) of the slab image
+    static __device__ __forceinline__ int slot(int row, int k) {
+        return XK ? row * BKK + (k ^ swz(row)) : k * R + row;
+    }
+};
+
+template <bool AK, bool BK, int BM, int BN, int BKK, int WM, int WN>
+__global__ void __launch_bounds__(WM *WN * 64) gemm_z_dma_kernel(const GemmKArgs p) {
+    typedef typename Mfma<double>::acc_t acc_t;
+    constexpr int NTH = WM * WN * 64;
+    constexpr int WTM = BM / WM, WTN = BN / WN;
+    constexpr int MT = WTM / 16, NT = WTN / 16;
+    constexpr int SLAB = (BM + BN) * BKK; // double2 per slab (A then B)
+    static_assert(MT * 16 == WTM && NT * 16 == WTN, "bad wave tile");
+    typedef DmaOperand<AK, BM, BKK, NTH> OpA;
+    typedef DmaOperand<BK, BN, BKK, NTH> OpB;
+    __shared__ double2 lds[2 * SLAB]; // the only LDS object of the kernel
+
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
+    const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+    const int ti = wg % p.tm;
+    int rest = wg / p.tm;
+    const int tj = rest % p.tn;
+    rest /= p.tn;
+    const int split = rest % p.splits;
+    const long bb = rest / p.splits;
+    const long m0 = (long)ti * BM, n0 = (long)tj * BN;
+    const long k_begin = (long)split * p.kchunk;
+    const long k_end = min(p.k, k_begin + p.kchunk);
+
+    const double2 *A = (const double2 *)p.a + bb * p.sa_b;
+    const double2 *B = (const double2 *)p.b + bb * p.sb_b;
+    const __amdgpu_buffer_rsrc_t rsA =
+        __builtin_amdgcn_make_buffer_rsrc((void *)A, (short)0, (int)p.a_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsB =
+        __builtin_amdgcn_make_buffer_rsrc((void *)B, (short)0, (int)p.b_bytes, 0x00020000);
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    OpA da;
+    OpB db;
+    da.init(tid, m0, p.m, p.sa_m, p.sa_k);
+    db.init(tid, n0, p.n, p.sb_n, p.sb_k);
+
+    const int wm = wave / WN, wn = wave % WN;
+    const int frow = wm * WTM + (lane & 15), fcol = wn * WTN + (lane & 15), kq = lane >> 4;
+    const double sa = p.conja ? -1.0 : 1.0, sb = p.conjb ? -1.0 : 1.0;
+
+    acc_t accR[MT][NT], accI[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+            accR[i][j] = acc_t{0, 0, 0, 0};
+            accI[i][j] = acc_t{0, 0, 0, 0};
+        }
+
+    const long nslab = (k_end - k_begin + BKK - 1) / BKK;
+    const char *const base = (const char *)lds;
+    if (nslab > 0) {
+        da.issue(rsA, base, wave, k_begin, k_end, p.sa_k);
+        db.issue(rsB, base + BM * BKK * 16, wave, k_begin, k_end, p.sb_k);
+    }
+    for (long s = 0; s < nslab; ++s) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // this wave's DMA of slab s landed
+        __syncthreads(); // ... and every wave's; the other buffer is free again
+        const int cur = (int)(s & 1);
+        if (s + 1 < nslab) {
+            const char *nb = base + (size_t)(cur ^ 1) * SLAB * 16;
+            const long kn = k_begin + (s + 1) * BKK;
+            da.issue(rsA, nb, wave, kn, k_end, p.sa_k);
+            db.issue(rsB, nb + BM * BKK * 16, wave, kn, k_end, p.sb_k);
+        }
+        const double2 *As = lds + cur * SLAB;
+        const double2 *Bs = As + BM * BKK;
+#pragma unroll
+        for (int kk = 0; kk < BKK; kk += 4) {
+            double2 af[MT], bf[NT];
+#pragma unroll
+            for (int i = 0; i < MT; ++i) af[i] = As[OpA::slot(frow + 16 * i, kk + kq)];
+#pragma unroll
+            for (int j = 0; j < NT; ++j) bf[j] = Bs[OpB::slot(fcol + 16 * j, kk + kq)];
+#pragma unroll
+            for (int i = 0; i < MT; ++i) af[i].y *= sa;
+#pragma unroll
+            for (int j = 0; j < NT; ++j) bf[j].y *= sb;
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int j = 0; j < NT; ++j) {
+                    accR[i][j] = Mfma<double>::mma(af[i].x, bf[j].x, accR[i][j]);
+                    accI[i][j] = Mfma<double>::mma(af[i].x, bf[j].y, accI[i][j]);
+                }
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int j = 0; j < NT; ++j) {
+                    accR[i][j] = Mfma<double>::mma(-af[i].y, bf[j].y, accR[i][j]);
+                    accI[i][j] = Mfma<double>::mma(af[i].y, bf[j].x, accI[i][j]);
+                }
+        }
+    }
+
+    const int ccol = lane & 15;
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const long gi = m0 + wm * WTM + 16 * i + Mfma<double>::row(lane, r);
+                const long gj = n0 + wn * WTN + 16 * j + ccol;
+                if (gi >= p.m || gj >= p.n) continue;
+                const double vr = accR[i][j][r], vi = accI[i][j][r];
+                if (p.splits == 1) {
+                    double *cptr = (double *)((double2 *)p.c + bb * p.sc_b + gi * p.sc_m + gj * p.sc_n);
+                    epilogue_store<double>(cptr, vr, vi, p, true);
+                } else {
+                    double2 *w = (double2 *)p.work + (((long)split * p.batch + bb) * p.n + gj) * p.m + gi;
+                    *w = double2{vr, vi};
+                }
+            }
+}
+
 // C = alpha * sum_s W[s] + beta * C, summed in split order (deterministic)
 template <typename R, bool CPLX>
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(const GemmKArgs p) {
@@ -322,63 +516,103 @@ __global__ void __launch_bounds__(256) scale_c_kernel(const GemmKArgs p) {
     }
 }
 
-/// Launch one tile configuration; `splits` <= 0 picks the split-K factor automatically
-template <typename R, bool CPLX, bool AK, bool BK, int BM, int BN, int BKK, int WM, int WN>
-void launch_tiled_cfg(const GemmKArgs &p0, int device, hipStream_t stream, long splits = 0,
-                      long target_wgs = 1024) {
-    GemmKArgs p = p0;
+/// Grid shape, split-K factor, descriptor ranges and the split-K workspace of one launch
+/// (`splits` <= 0 picks the split-K factor so that ~target_wgs workgroups are in flight)
+template <typename E>
+long prepare_launch(GemmKArgs &p, int BM, int BN, int BKK, long splits, long target_wgs,
+                    Scratch &work, int device) {
     p.tm = (int)((p.m + BM - 1) / BM);
     p.tn = (int)((p.n + BN - 1) / BN);
     const long tiles = (long)p.tm * p.tn * p.batch;
     if (splits <= 0) {
-        // Split K so that ~target_wgs workgroups are in flight; keep >= 256-deep chunks.
         splits = 1;
         if (tiles < target_wgs) {
             splits = (target_wgs + tiles - 1) / tiles;
-            const long max_splits = std::max(1L, p.k / 256);
+            const long max_splits = std::max(1L, p.k / 256); // keep >= 256-deep chunks
             splits = std::min(splits, max_splits);
         }
     }
-    {
-        typedef typename Elem<R, CPLX>::type E0;
-        const long ea = ((p.m - 1) * std::labs(p.sa_m) + (p.k - 1) * std::labs(p.sa_k) + 1) *
-                        (long)sizeof(E0);
-        const long eb = ((p.k - 1) * std::labs(p.sb_k) + (p.n - 1) * std::labs(p.sb_n) + 1) *
-                        (long)sizeof(E0);
-        if (ea >= 0x7fffffffL || eb >= 0x7fffffffL || p.sa_m < 0 || p.sa_k < 0 || p.sb_k < 0 ||
-            p.sb_n < 0)
-            throw Error("gemm: operand batch entries of 2 GiB or more are not supported yet");
-        p.a_bytes = (unsigned)ea;
-        p.b_bytes = (unsigned)eb;
-    }
+    const long ea = ((p.m - 1) * std::labs(p.sa_m) + (p.k - 1) * std::labs(p.sa_k) + 1) *
+                    (long)sizeof(E);
+    const long eb = ((p.k - 1) * std::labs(p.sb_k) + (p.n - 1) * std::labs(p.sb_n) + 1) *
+                    (long)sizeof(E);
+    if (ea >= 0x7fffffffL || eb >= 0x7fffffffL || p.sa_m < 0 || p.sa_k < 0 || p.sb_k < 0 ||
+        p.sb_n < 0)
+        throw Error("gemm: operand batch entries of 2 GiB or more are not supported yet");
+    p.a_bytes = (unsigned)ea;
+    p.b_bytes = (unsigned)eb;
     long kchunk = (p.k + splits - 1) / splits;
     kchunk = (kchunk + BKK - 1) / BKK * BKK;
     splits = std::max(1L, (p.k + kchunk - 1) / kchunk);
     p.splits = (int)splits;
     p.kchunk = kchunk;
-    typedef typename Elem<R, CPLX>::type E;
-    Scratch work;
+    p.work = nullptr;
     if (splits > 1) {
         work = Scratch(sizeof(E) * splits * p.batch * p.m * p.n, device);
         p.work = work.ptr;
     }
     const long nwg = tiles * splits;
     if (nwg > 0x7fffffffL) throw Error("gemm: grid too large");
-    hipLaunchKernelGGL((gemm_kernel<R, CPLX, AK, BK, BM, BN, BKK, WM, WN>), dim3((unsigned)nwg),
-                       dim3(WM * WN * 64), 0, stream, p);
+    return nwg;
+}
+
+template <typename R, bool CPLX>
+void launch_reduce(const GemmKArgs &p, hipStream_t stream) {
+    if (p.splits <= 1) return;
+    const long total = p.batch * p.m * p.n;
+    const long blocks = std::min((total + 255) / 256, 4096L);
+    KernelTimer timer("gemm_splitk_reduce", stream);
+    hipLaunchKernelGGL((splitk_reduce_kernel<R, CPLX>), dim3((unsigned)blocks), dim3(256), 0,
+                       stream, p);
     SBX_HIP_CHECK(hipGetLastError());
-    if (splits > 1) {
-        const long total = p.batch * p.m * p.n;
-        const long blocks = std::min((total + 255) / 256, 4096L);
-        hipLaunchKernelGGL((splitk_reduce_kernel<R, CPLX>), dim3((unsigned)blocks), dim3(256), 0,
-                           stream, p);
+}
+
+/// Launch one tile configuration of the register-staged kernel
+template <typename R, bool CPLX, bool AK, bool BK, int BM, int BN, int BKK, int WM, int WN>
+void launch_tiled_cfg(const GemmKArgs &p0, int device, hipStream_t stream, long splits = 0,
+                      long target_wgs = 1024) {
+    GemmKArgs p = p0;
+    Scratch work;
+    const long nwg = prepare_launch<typename Elem<R, CPLX>::type>(p, BM, BN, BKK, splits,
+                                                                   target_wgs, work, device);
+    {
+        KernelTimer timer("gemm", stream);
+        hipLaunchKernelGGL((gemm_kernel<R, CPLX, AK, BK, BM, BN, BKK, WM, WN>),
+                           dim3((unsigned)nwg), dim3(WM * WN * 64), 0, stream, p);
         SBX_HIP_CHECK(hipGetLastError());
     }
+    launch_reduce<R, CPLX>(p, stream);
+}
+
+/// Launch one tile configuration of the LDS-DMA complex<double> kernel
+template <bool AK, bool BK, int BM, int BN, int BKK, int WM, int WN>
+void launch_dma_cfg(const GemmKArgs &p0, int device, hipStream_t stream, long splits = 0,
+                    long target_wgs = 1024) {
+    GemmKArgs p = p0;
+    Scratch work;
+    const long nwg = prepare_launch<double2>(p, BM, BN, BKK, splits, target_wgs, work, device);
+    {
+        KernelTimer timer("gemm", stream);
+        hipLaunchKernelGGL((gemm_z_dma_kernel<AK, BK, BM, BN, BKK, WM, WN>),
+                           dim3((unsigned)nwg), dim3(WM * WN * 64), 0, stream, p);
+        SBX_HIP_CHECK(hipGetLastError());
+    }
+    launch_reduce<double, true>(p, stream);
 }
 
 template <typename R, bool CPLX, bool AK, bool BK>
 void launch_tiled(const GemmKArgs &p, int device, hipStream_t stream) {
-    launch_tiled_cfg<R, CPLX, AK, BK, 64, 64, 16, 2, 2>(p, device, stream);
+    // complex<double>: LDS-DMA kernel; 128x128 tiles (8 waves, one workgroup per CU) when the
+    // output is large enough, else 64x64 (tools/gemm_tune.hip: 67.5 / 65.5 TFLOP/s on the
+    // 16^4 lattice contraction, 86 % / 83 % of the 78.6 TFLOP/s FP64 matrix peak)
+    if constexpr (std::is_same<R, double>::value && CPLX) {
+        if (p.m >= 128 && p.n >= 128)
+            launch_dma_cfg<AK, BK, 128, 128, 8, 4, 2>(p, device, stream, 0, 256);
+        else
+            launch_dma_cfg<AK, BK, 64, 64, 8, 2, 2>(p, device, stream, 0, 1024);
+    }
+    else
+        launch_tiled_cfg<R, CPLX, AK, BK, 64, 64, 16, 2, 2>(p, device, stream);
 }
 
 template <typename R, bool CPLX> void launch_typed(const GemmKArgs &p, int device, hipStream_t s) {

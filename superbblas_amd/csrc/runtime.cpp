@@ -7,6 +7,7 @@
 // threshold keeps freed scratch resident so steady-state calls do no driver allocations.
 #include "sbx_internal.h"
 
+#include <map>
 #include <mutex>
 
 namespace sbx {
@@ -133,6 +134,82 @@ int pointer_device(const void *p) {
     }
     if (attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged) return attr.device;
     return -1;
+}
+
+//
+// Kernel timers
+//
+namespace {
+struct TimerState {
+    bool on = false;
+    struct Pending {
+        std::string name;
+        hipEvent_t a, b;
+    };
+    std::vector<Pending> pending;
+    std::map<std::string, std::pair<double, long long>> totals;
+};
+TimerState &timers() {
+    static TimerState t;
+    return t;
+}
+std::mutex g_timer_mutex;
+void drain_timers() {
+    TimerState &t = timers();
+    for (auto &p : t.pending) {
+        float ms = 0;
+        SBX_HIP_CHECK(hipEventSynchronize(p.b));
+        SBX_HIP_CHECK(hipEventElapsedTime(&ms, p.a, p.b));
+        auto &e = t.totals[p.name];
+        e.first += ms;
+        e.second += 1;
+        (void)hipEventDestroy(p.a);
+        (void)hipEventDestroy(p.b);
+    }
+    t.pending.clear();
+}
+} // namespace
+
+void timings_enable(bool on) {
+    std::lock_guard<std::mutex> g(g_timer_mutex);
+    timers().on = on;
+}
+bool timings_enabled() { return timers().on; }
+void timings_reset() {
+    std::lock_guard<std::mutex> g(g_timer_mutex);
+    drain_timers();
+    timers().totals.clear();
+}
+void timings_get(const char *name, double *ms, long long *calls) {
+    std::lock_guard<std::mutex> g(g_timer_mutex);
+    drain_timers();
+    auto it = timers().totals.find(name);
+    *ms = it == timers().totals.end() ? 0.0 : it->second.first;
+    *calls = it == timers().totals.end() ? 0 : it->second.second;
+}
+std::string timings_report() {
+    std::lock_guard<std::mutex> g(g_timer_mutex);
+    drain_timers();
+    std::string r;
+    for (auto &e : timers().totals)
+        r += e.first + " " + std::to_string(e.second.second) + " " +
+             std::to_string(e.second.first) + "\n";
+    return r;
+}
+KernelTimer::KernelTimer(const char *n, hipStream_t s) : name(n), stream(s) {
+    if (!timers().on) return;
+    hipEvent_t a;
+    SBX_HIP_CHECK(hipEventCreate(&a));
+    SBX_HIP_CHECK(hipEventRecord(a, s));
+    ev0 = a;
+}
+KernelTimer::~KernelTimer() {
+    if (!ev0) return;
+    hipEvent_t b;
+    if (hipEventCreate(&b) != hipSuccess) return;
+    (void)hipEventRecord(b, stream);
+    std::lock_guard<std::mutex> g(g_timer_mutex);
+    timers().pending.push_back({name, (hipEvent_t)ev0, b});
 }
 
 } // namespace sbx

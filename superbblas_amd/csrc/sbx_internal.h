@@ -91,6 +91,24 @@ struct Scratch {
 /// Device id owning a pointer, or -1 for host memory
 int pointer_device(const void *p);
 
+/// Per-kernel-family GPU timers (the reference's reportTimings / resetTimings,
+/// performance.h:356-518, measured with HIP events on the launching stream).  When enabled,
+/// a KernelTimer around a launch records an event pair; timings_get() synchronizes and sums.
+void timings_enable(bool on);
+bool timings_enabled();
+void timings_reset();
+/// total milliseconds and number of launches of `name` (0 if never timed)
+void timings_get(const char *name, double *ms, long long *calls);
+/// "name calls total_ms" lines of every timed family
+std::string timings_report();
+struct KernelTimer {
+    const char *name;
+    hipStream_t stream;
+    void *ev0 = nullptr;
+    KernelTimer(const char *name, hipStream_t s);
+    ~KernelTimer();
+};
+
 //
 // Kernels (kernels_*.hip); all enqueue on get_stream(device)
 //

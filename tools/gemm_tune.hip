@@ -1,11 +1,13 @@
 // Tuning harness for the batched complex GEMM (not part of the product).  Includes the kernel
 // translation unit and times tile/split variants on the lattice contraction shape with HIP
-// events.  Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/gemm_tune.hip
-//                superbblas_amd/csrc/runtime.cpp -o gemm_tune
+// events; every variant's output is checked against the register-staged kernel.
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -mllvm -amdgpu-mfma-vgpr-form \
+//        tools/gemm_tune.hip superbblas_amd/csrc/runtime.cpp -o tools/gemm_tune
 #include "../superbblas_amd/csrc/kernels_gemm.hip"
 
+#include <cmath>
 #include <cstdio>
-#include <random>
+#include <vector>
 
 using namespace sbx;
 
@@ -19,25 +21,54 @@ __global__ void fill_kernel(double *p, long n, unsigned seed) {
     }
 }
 
-template <int BM, int BN, int BKK, int WM, int WN>
-void run(const char *name, GemmKArgs p, long splits, long target, int reps, double flops) {
+static double max_rel(const std::vector<double> &a, const std::vector<double> &b) {
+    double num = 0, den = 0;
+    for (size_t i = 0; i < a.size(); ++i) {
+        num = std::max(num, std::fabs(a[i] - b[i]));
+        den = std::max(den, std::fabs(b[i]));
+    }
+    return num / (den > 0 ? den : 1);
+}
+
+template <typename F>
+void run(const char *name, F launch, const GemmKArgs &p, int reps, double flops,
+         const std::vector<double> *ref, double *C, size_t nc) {
     hipStream_t s = get_stream(0);
-    for (int i = 0; i < 2; ++i)
-        launch_tiled_cfg<double, true, true, true, BM, BN, BKK, WM, WN>(p, 0, s, splits, target);
+    (void)hipMemsetAsync(C, 0, nc * sizeof(double), s);
+    launch(p, s);
+    (void)hipStreamSynchronize(s);
+    double err = -1;
+    if (ref) {
+        std::vector<double> h(nc);
+        (void)hipMemcpy(h.data(), C, nc * sizeof(double), hipMemcpyDeviceToHost);
+        err = max_rel(h, *ref);
+    }
     hipEvent_t a, b;
     (void)hipEventCreate(&a);
     (void)hipEventCreate(&b);
     (void)hipEventRecord(a, s);
-    for (int i = 0; i < reps; ++i)
-        launch_tiled_cfg<double, true, true, true, BM, BN, BKK, WM, WN>(p, 0, s, splits, target);
+    for (int i = 0; i < reps; ++i) launch(p, s);
     (void)hipEventRecord(b, s);
     (void)hipEventSynchronize(b);
     float ms = 0;
     (void)hipEventElapsedTime(&ms, a, b);
     ms /= reps;
-    std::printf("%-34s splits=%-3ld target=%-5ld  %8.3f ms  %7.2f TFLOP/s\n", name, splits,
-                target, ms, flops / (ms * 1e-3) / 1e12);
+    std::printf("%-40s %8.3f ms  %7.2f TFLOP/s  err %.2e\n", name, ms,
+                flops / (ms * 1e-3) / 1e12, err);
 }
+
+#define REG(BM, BN, BKK, WM, WN, SPL, TGT)                                                      \
+    run("reg " #BM "x" #BN "x" #BKK " w" #WM "x" #WN " s" #SPL " t" #TGT,                         \
+        [&](const GemmKArgs &q, hipStream_t s) {                                                 \
+            launch_tiled_cfg<double, true, true, true, BM, BN, BKK, WM, WN>(q, 0, s, SPL, TGT);  \
+        },                                                                                       \
+        p, reps, flops, &ref, C, nc)
+#define DMA(BM, BN, BKK, WM, WN, SPL, TGT)                                                      \
+    run("dma " #BM "x" #BN "x" #BKK " w" #WM "x" #WN " s" #SPL " t" #TGT,                         \
+        [&](const GemmKArgs &q, hipStream_t s) {                                                 \
+            launch_dma_cfg<true, true, BM, BN, BKK, WM, WN>(q, 0, s, SPL, TGT);                   \
+        },                                                                                       \
+        p, reps, flops, &ref, C, nc)
 
 int main(int argc, char **argv) {
     const long L = 16, n = 64;
@@ -45,7 +76,8 @@ int main(int argc, char **argv) {
     double *A, *B, *C;
     (void)hipMalloc(&A, sizeof(double) * 2 * m * k * batch);
     (void)hipMalloc(&B, sizeof(double) * 2 * nn * k * batch);
-    (void)hipMalloc(&C, sizeof(double) * 2 * m * nn * batch);
+    const size_t nc = 2 * m * nn * batch;
+    (void)hipMalloc(&C, sizeof(double) * nc);
     fill_kernel<<<4096, 256>>>(A, 2 * m * k * batch, 1);
     fill_kernel<<<4096, 256>>>(B, 2 * nn * k * batch, 2);
     (void)hipDeviceSynchronize();
@@ -60,16 +92,29 @@ int main(int argc, char **argv) {
     GemmKArgs p = make_args(d);
     const double flops = 8.0 * m * nn * k * batch;
     const int reps = argc > 1 ? atoi(argv[1]) : 10;
-    run<64, 64, 16, 2, 2>("64x64x16 w2x2", p, 0, 1024, reps, flops);
-    run<64, 64, 16, 2, 2>("64x64x16 w2x2", p, 0, 512, reps, flops);
-    run<64, 64, 16, 2, 2>("64x64x16 w2x2", p, 0, 2048, reps, flops);
-    run<64, 64, 32, 2, 2>("64x64x32 w2x2", p, 0, 512, reps, flops);
-    run<64, 64, 32, 2, 2>("64x64x32 w2x2", p, 0, 1024, reps, flops);
-    run<64, 64, 8, 2, 2>("64x64x8 w2x2", p, 0, 1024, reps, flops);
-    run<128, 64, 16, 4, 2>("128x64x16 w4x2", p, 0, 512, reps, flops);
-    run<128, 64, 16, 4, 2>("128x64x16 w4x2", p, 0, 1024, reps, flops);
-    run<128, 128, 16, 4, 2>("128x128x16 w4x2", p, 0, 256, reps, flops);
-    run<128, 128, 16, 4, 2>("128x128x16 w4x2", p, 0, 512, reps, flops);
-    run<64, 64, 16, 2, 2>("64x64x16 w2x2 (again)", p, 0, 1024, reps, flops);
+    // reference output: register-staged kernel
+    std::vector<double> ref(nc);
+    launch_tiled_cfg<double, true, true, true, 64, 64, 16, 2, 2>(p, 0, get_stream(0), 0, 1024);
+    (void)hipStreamSynchronize(get_stream(0));
+    (void)hipMemcpy(ref.data(), C, nc * sizeof(double), hipMemcpyDeviceToHost);
+
+    REG(64, 64, 16, 2, 2, 0, 1024);
+    DMA(64, 64, 16, 2, 2, 0, 1024);
+    DMA(128, 128, 16, 4, 2, 0, 256);
+    DMA(128, 128, 8, 4, 2, 0, 256);
+    DMA(128, 128, 8, 4, 2, 0, 512);
+    DMA(128, 128, 8, 2, 2, 0, 512);
+    DMA(128, 128, 8, 2, 2, 0, 1024);
+    DMA(64, 64, 8, 2, 2, 0, 1024);
+    DMA(64, 64, 8, 2, 2, 0, 2048);
+    DMA(128, 64, 8, 2, 2, 0, 1024);
+    DMA(128, 64, 8, 4, 1, 0, 1024);
+    DMA(128, 64, 8, 2, 1, 0, 1024);
+    DMA(256, 64, 8, 4, 1, 0, 512);
+    DMA(256, 128, 8, 4, 2, 0, 256);
+    DMA(256, 128, 8, 4, 2, 0, 512);
+    DMA(128, 256, 8, 2, 4, 0, 256);
+    DMA(256, 256, 8, 4, 4, 0, 256);
+    DMA(128, 128, 16, 4, 2, 0, 256);
     return 0;
 }
