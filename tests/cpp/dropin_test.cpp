@@ -1,0 +1,232 @@
+// Application-side check of the drop-in header (include/superbblas.h): the calls below are
+// written exactly as a superbblas user writes them (compare the reference's tests/contract.cpp
+// and tests/bsr.cpp usage), compiled with g++ against libsuperbblas_amd.so only.  Results are
+// compared with naive host loops on integer-valued data, so every comparison is exact.
+#include "superbblas.h"
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+using namespace superbblas;
+using Z = std::complex<double>;
+
+static int failures = 0;
+#define CHECK(c, msg)                                                                              \
+    do {                                                                                           \
+        if (!(c)) {                                                                                \
+            std::printf("FAIL: %s\n", msg);                                                        \
+            ++failures;                                                                            \
+        }                                                                                          \
+    } while (0)
+
+static Z val(long g, int seed) {
+    return Z((double)((7 * g + 3 + 13 * seed) % 11 - 5), (double)((5 * g + 1 + 7 * seed) % 13 - 6));
+}
+
+template <std::size_t N> static long vol(const Coor<N> &d) {
+    long v = 1;
+    for (auto x : d) v *= x;
+    return v;
+}
+
+// host <-> device through superbblas::copy with a CPU and a GPU context
+template <std::size_t N> static Z *upload(const std::vector<Z> &h, const Coor<N> &dim, const char *o) {
+    Context cpu = createCpuContext(), gpu = createGpuContext(0);
+    Z *d = allocate<Z>(h.size(), gpu);
+    PartitionItem<N> p{Coor<N>{}, dim};
+    const Z *src = h.data();
+    copy<N, N, Z, Z>(1.0, &p, 1, o, Coor<N>{}, dim, dim, &src, nullptr, &cpu, &p, 1, o, Coor<N>{},
+                     dim, &d, nullptr, &gpu, SlowToFast, Copy);
+    return d;
+}
+template <std::size_t N> static std::vector<Z> download(Z *d, const Coor<N> &dim, const char *o) {
+    Context cpu = createCpuContext(), gpu = createGpuContext(0);
+    std::vector<Z> h(vol(dim));
+    PartitionItem<N> p{Coor<N>{}, dim};
+    const Z *src = d;
+    Z *dst = h.data();
+    copy<N, N, Z, Z>(1.0, &p, 1, o, Coor<N>{}, dim, dim, &src, nullptr, &gpu, &p, 1, o, Coor<N>{},
+                     dim, &dst, nullptr, &cpu, SlowToFast, Copy);
+    sync(gpu);
+    return h;
+}
+
+int main() {
+    if (getGpuDevicesCount() == 0) {
+        std::printf("no GPU\n");
+        return 2;
+    }
+    Context gpu = createGpuContext(0);
+    const int L = 4, n = 2, s = 4, c = 3;
+
+    // ---- contraction: tnsxyzc x tNSxyzc -> tNSns (tests/contract.cpp's lattice form) ----
+    {
+        const Coor<7> d0{L, n, s, L, L, L, c};
+        const Coor<5> dr{L, n, s, n, s};
+        std::vector<Z> h0(vol(d0)), h1(vol(d0)), hr(vol(dr), Z(0));
+        for (long i = 0; i < vol(d0); ++i) h0[i] = val(i, 1), h1[i] = val(i, 2);
+        Z *v0 = upload<7>(h0, d0, "tnsxyzc"), *v1 = upload<7>(h1, d0, "tNSxyzc");
+        Z *vr = upload<5>(hr, dr, "tNSns");
+        PartitionItem<7> p0{Coor<7>{}, d0};
+        PartitionItem<5> pr{Coor<5>{}, dr};
+        const Z *c0 = v0, *c1 = v1;
+        contraction<7, 7, 5, Z>(Z(1), &p0, {{}}, d0, d0, 1, "tnsxyzc", false, &c0, &gpu, &p0,
+                                {{}}, d0, d0, 1, "tNSxyzc", false, &c1, &gpu, Z(0), &pr, {{}}, dr,
+                                dr, 1, "tNSns", &vr, &gpu, SlowToFast);
+        auto out = download<5>(vr, dr, "tNSns");
+        // naive: r[t,N,S,n,s] = sum_{xyzc} v0[t,n,s,x,y,z,c] v1[t,N,S,x,y,z,c]
+        const long V = (long)L * L * L * c;
+        bool ok = true;
+        for (int t = 0; t < L; ++t)
+            for (int N = 0; N < n; ++N)
+                for (int S = 0; S < s; ++S)
+                    for (int nn = 0; nn < n; ++nn)
+                        for (int ss = 0; ss < s; ++ss) {
+                            Z acc = 0;
+                            for (long a = 0; a < V; ++a)
+                                acc += h0[((t * n + nn) * s + ss) * V + a] *
+                                       h1[((t * n + N) * s + S) * V + a];
+                            ok &= out[(((t * n + N) * s + S) * n + nn) * s + ss] == acc;
+                        }
+        CHECK(ok, "contraction tnsxyzc x tNSxyzc -> tNSns");
+        deallocate(v0, gpu);
+        deallocate(v1, gpu);
+        deallocate(vr, gpu);
+    }
+
+    // ---- copy: xyztsc into slice n=1 of tnsxyzc (the permute of tests/dist.cpp) ----
+    {
+        const Coor<6> d0{L, L, L, L, s, c};
+        const Coor<7> d1{L, n, s, L, L, L, c};
+        std::vector<Z> h0(vol(d0)), h1(vol(d1), Z(0));
+        for (long i = 0; i < vol(d0); ++i) h0[i] = Z((double)i, -(double)i);
+        Z *v0 = upload<6>(h0, d0, "xyztsc"), *v1 = upload<7>(h1, d1, "tnsxyzc");
+        PartitionItem<6> p0{Coor<6>{}, d0};
+        PartitionItem<7> p1{Coor<7>{}, d1};
+        const Z *c0 = v0;
+        copy<6, 7, Z, Z>(1.0, &p0, 1, "xyztsc", Coor<6>{}, d0, d0, &c0, nullptr, &gpu, &p1, 1,
+                         "tnsxyzc", Coor<7>{0, 1, 0, 0, 0, 0, 0}, d1, &v1, nullptr, &gpu,
+                         SlowToFast, Copy);
+        auto out = download<7>(v1, d1, "tnsxyzc");
+        bool ok = true;
+        for (int x = 0; x < L; ++x)
+            for (int y = 0; y < L; ++y)
+                for (int z = 0; z < L; ++z)
+                    for (int t = 0; t < L; ++t)
+                        for (int ss = 0; ss < s; ++ss)
+                            for (int cc = 0; cc < c; ++cc) {
+                                const long i0 = ((((x * L + y) * L + z) * L + t) * s + ss) * c + cc;
+                                const long i1 =
+                                    (((((t * n + 1) * s + ss) * L + x) * L + y) * L + z) * c + cc;
+                                ok &= out[i1] == h0[i0];
+                                ok &= out[i1 - (long)s * L * L * L * c] == Z(0);
+                            }
+        CHECK(ok, "copy xyztsc -> tnsxyzc[n=1]");
+        deallocate(v0, gpu);
+        deallocate(v1, gpu);
+    }
+
+    // ---- BSR: 9-point periodic stencil, 3x3 blocks, x pXYZTSCn -> y pxyztscn (tests/bsr.cpp) ----
+    {
+        const Coor<6> dim{L, L, L, L, 1, c};
+        const long V = (long)L * L * L * L;
+        std::vector<IndexType> ii(V, 9);
+        std::vector<Coor<6>> jj;
+        for (long i = 0; i < V; ++i) {
+            Coor<6> cc{(int)(i / (L * L * L)), (int)(i / (L * L) % L), (int)(i / L % L),
+                       (int)(i % L), 0, 0};
+            jj.push_back(cc);
+            for (int d = 0; d < 4; ++d)
+                for (int dir = -1; dir < 2; dir += 2) {
+                    Coor<6> q = cc;
+                    q[d] = (q[d] + dir + L) % L;
+                    jj.push_back(q);
+                }
+        }
+        std::vector<Z> hv(V * 9 * c * c);
+        for (long i = 0; i < (long)hv.size(); ++i) hv[i] = val(i, 4);
+        Z *dv = allocate<Z>(hv.size(), gpu);
+        IndexType *dii = allocate<IndexType>(ii.size(), gpu);
+        Coor<6> *djj = allocate<Coor<6>>(jj.size(), gpu);
+        {
+            Context cpu = createCpuContext();
+            const Coor<1> dn{(int)hv.size()};
+            PartitionItem<1> pn{Coor<1>{}, dn};
+            const Z *src = hv.data();
+            copy<1, 1, Z, Z>(1.0, &pn, 1, "i", Coor<1>{}, dn, dn, &src, nullptr, &cpu, &pn, 1,
+                             "i", Coor<1>{}, dn, &dv, nullptr, &gpu, SlowToFast, Copy);
+            const Coor<1> di{(int)ii.size()};
+            PartitionItem<1> pi{Coor<1>{}, di};
+            const IndexType *si = ii.data();
+            copy<1, 1, IndexType, IndexType>(1, &pi, 1, "i", Coor<1>{}, di, di, &si, nullptr,
+                                             &cpu, &pi, 1, "i", Coor<1>{}, di, &dii, nullptr,
+                                             &gpu, SlowToFast, Copy);
+            const Coor<1> dj{(int)(jj.size() * 6)};
+            PartitionItem<1> pj{Coor<1>{}, dj};
+            const IndexType *sj = (const IndexType *)jj.data();
+            IndexType *tj = (IndexType *)djj;
+            copy<1, 1, IndexType, IndexType>(1, &pj, 1, "i", Coor<1>{}, dj, dj, &sj, nullptr,
+                                             &cpu, &pj, 1, "i", Coor<1>{}, dj, &tj, nullptr,
+                                             &gpu, SlowToFast, Copy);
+        }
+        PartitionItem<6> pop{Coor<6>{}, dim};
+        const Coor<6> block{1, 1, 1, 1, 1, c};
+        BSR_handle *op = nullptr;
+        const Z *cv = dv;
+        create_bsr<6, 6, Z>(&pop, dim, &pop, dim, 1, block, block, false, &dii, &djj, &cv, &gpu,
+                            SlowToFast, &op);
+        const int nc = 2;
+        const Coor<8> dx{1, L, L, L, L, 1, c, nc};
+        std::vector<Z> hx(vol(dx)), hy(vol(dx), Z(0));
+        for (long i = 0; i < vol(dx); ++i) hx[i] = val(i, 5);
+        Z *vx = upload<8>(hx, dx, "pXYZTSCn"), *vy = upload<8>(hy, dx, "pxyztscn");
+        PartitionItem<8> px{Coor<8>{}, dx};
+        const Z *cx = vx;
+        bsr_krylov<6, 6, 8, 8, Z>(Z(1), op, "xyztsc", "XYZTSC", &px, 1, "pXYZTSCn", {{}}, dx, dx,
+                                  &cx, Z(0), &px, "pxyztscn", {{}}, dx, dx, 'p', &vy, &gpu,
+                                  SlowToFast);
+        auto out = download<8>(vy, dx, "pxyztscn");
+        bool ok = true;
+        for (long r = 0; r < V; ++r)
+            for (int i = 0; i < c; ++i)
+                for (int col = 0; col < nc; ++col) {
+                    Z acc = 0;
+                    for (int k = 0; k < 9; ++k) {
+                        const Coor<6> &q = jj[r * 9 + k];
+                        const long site = ((q[0] * L + q[1]) * L + q[2]) * L + q[3];
+                        for (int j = 0; j < c; ++j)
+                            acc += hv[((r * 9 + k) * c + i) * c + j] * hx[(site * c + j) * nc + col];
+                    }
+                    ok &= out[(r * c + i) * nc + col] == acc;
+                }
+        CHECK(ok, "bsr_krylov 9-point stencil");
+        destroy_bsr(op);
+        deallocate(vx, gpu);
+        deallocate(vy, gpu);
+        deallocate(dv, gpu);
+        deallocate(dii, gpu);
+        deallocate(djj, gpu);
+    }
+
+    // ---- error behaviour: invalid calls throw std::runtime_error (platform.h:226-243) ----
+    {
+        bool thrown = false;
+        try {
+            const Coor<2> d{2, 2};
+            PartitionItem<2> p{Coor<2>{}, d};
+            std::vector<Z> h(4);
+            const Z *src = h.data();
+            Z *dst = h.data();
+            Context cpu = createCpuContext();
+            copy<2, 2, Z, Z>(1.0, &p, 1, "ab", Coor<2>{}, d, d, &src, nullptr, &cpu, &p, 1, "cd",
+                             Coor<2>{}, d, &dst, nullptr, &cpu, SlowToFast, Copy);
+        } catch (const std::runtime_error &) {
+            thrown = true;
+        }
+        CHECK(thrown, "invalid copy labels must throw");
+    }
+
+    if (failures == 0) std::printf("DROPIN OK\n");
+    return failures == 0 ? 0 : 1;
+}
