@@ -77,6 +77,22 @@ def cpu_baseline(threads):
             "kind": "port", "sample": "oracle xgemm_batch_strided 'T','N' 64x64x1536 batch 8"}
 
 
+def pmc_traffic(kernel_substr):
+    """HBM bytes per launch of a kernel from the latest committed PMC pass (profiles/rNN_pmc.json,
+    made by tools/pmc_summary.py from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of this
+    bench).  PMC counters cannot be read inside a timed run, so they come from that pass."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        ks = json.load(f)["kernels"]
+    for k, v in ks.items():
+        if kernel_substr in k:
+            return v["hbm_bytes"], os.path.relpath(files[-1], ROOT) + ": " + k
+    return None, None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -171,6 +187,7 @@ def main():
     if rank == 0 and not args.no_cpu:
         base = cpu_baseline(int(os.environ.get("OMP_NUM_THREADS", "16")))
 
+    traffic, traffic_src = pmc_traffic("gemm_z_dma_kernel<true, true, 128, 128, 8, 4, 2>")
     if rank == 0:
         line = {
             "metric": "lattice contraction GFLOP/s + permute GB/s, 16^4 spin×color, 1/2/4/8 GPUs",
@@ -194,7 +211,10 @@ def main():
                        "parallelism": "xyz domain decomposition" if world > 1 else "single GPU"},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 3),
                          "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / PEAK_FP64_TFLOPS, 4), "traffic": None,
+                         "frac": round(achieved / PEAK_FP64_TFLOPS, 4),
+                         "traffic": traffic, "traffic_unit": "bytes per launch",
+                         "traffic_source": traffic_src,
+                         "algorithmic_bytes": 16.0 * (2 * vol(local0) + vol(gdimr)),
                          "kernel": "gemm_z_dma_kernel<128x128x8, 8 waves> (FP64 MFMA "
                                    "16x16x4, complex 4M), %d launches, %.4f ms avg "
                                    "(HIP events on its launch stream)" % (gemm_calls,
