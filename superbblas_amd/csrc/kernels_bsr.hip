@@ -129,36 +129,39 @@ __global__ void __launch_bounds__(256) bsr_kernel(const BsrArgs p) {
     }
 }
 
-constexpr int ELL_LDS_BYTES = 41472; // 32 block rows x 9 blocks x 3x3 complex<double>
+constexpr int ELL_LDS_BYTES = 24576; // per workgroup: several workgroups share a CU
 
 template <typename E, int BI, int BD, bool YROW, bool XROW>
 __global__ void __launch_bounds__(256) bsr_ell_kernel(const BsrArgs p, int nnz, int rb) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int BLK = BI * BD;
     E *vals = (E *)smem;
+    int *cols = (int *)(smem + (size_t)rb * nnz * BLK * sizeof(E));
     const E *__restrict__ v = (const E *)p.v;
     const E *__restrict__ x = (const E *)p.x;
     E *__restrict__ y = (E *)p.y;
-    constexpr int BLK = BI * BD;
-    const long row0 = (long)blockIdx.x * rb;
+    // consecutive chunks of block rows on one XCD: neighbouring sites share x rows in its L2
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int chunk = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    const long row0 = (long)chunk * rb;
     const int nrows = (int)min((long)rb, p.block_rows - row0);
-    // 1) stream this chunk's nonzero blocks into LDS (contiguous in the ELL value array)
+    // 1) stream the chunk's nonzero blocks (contiguous in the ELL value array) and block
+    //    columns into LDS, 8 loads in flight per thread
     const long vbase = row0 * nnz * BLK;
     const int nv = nrows * nnz * BLK;
-    for (int e0 = threadIdx.x; e0 < nv; e0 += 256 * 4) {
-        E t[4];
+    for (int e0 = threadIdx.x; e0 < nv; e0 += 256 * 8) {
+        E t[8];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int e = e0 + 256 * q;
-            t[q] = v[vbase + min(e, nv - 1)]; // clamped: no per-load branch
-        }
+        for (int q = 0; q < 8; ++q) t[q] = v[vbase + min(e0 + 256 * q, nv - 1)];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int e = e0 + 256 * q;
-            if (e < nv) vals[e] = t[q];
-        }
+        for (int q = 0; q < 8; ++q)
+            if (e0 + 256 * q < nv) vals[e0 + 256 * q] = t[q];
     }
+    for (int e = threadIdx.x; e < nrows * nnz; e += 256) cols[e] = p.jj[row0 * nnz + e];
     __syncthreads();
-    // 2) every thread computes the BI outputs of (block row, rhs column) pairs
+    // 2) every thread computes the BI outputs of (block row, rhs column) pairs; the x rows of
+    //    block j+1 are fetched while block j is applied
     const long npairs = (long)nrows * p.ncols;
     for (long q = threadIdx.x; q < npairs; q += 256) {
         int r;
@@ -173,21 +176,35 @@ __global__ void __launch_bounds__(256) bsr_ell_kernel(const BsrArgs p, int nnz, 
         E acc[BI];
 #pragma unroll
         for (int c = 0; c < BI; ++c) acc[c] = Ops<E>::zero();
-        const int *jj = p.jj + (row0 + r) * nnz;
+        const int *jr = cols + r * nnz;
         const E *vr = vals + r * nnz * BLK;
+        auto fetch = [&](int d0, E *xv) {
+            const long d = d0 < 0 ? 0 : d0;
+#pragma unroll
+            for (int e = 0; e < BD; ++e)
+                xv[e] = XROW ? x[(d + e) * p.ldx + col] : x[(d + e) + col * p.ldx];
+        };
+        E xn[BD];
+        int dn = jr[0];
+        fetch(dn, xn);
         for (int j = 0; j < nnz; ++j) {
-            const int d0 = jj[j];
-            if (d0 < 0) continue;
+            E xc[BD];
+#pragma unroll
+            for (int e = 0; e < BD; ++e) xc[e] = xn[e];
+            const int dc = dn;
+            if (j + 1 < nnz) {
+                dn = jr[j + 1];
+                fetch(dn, xn);
+            }
+            if (dc < 0) continue;
             const E *vb = vr + j * BLK;
 #pragma unroll
-            for (int e = 0; e < BD; ++e) {
-                const E xv = XROW ? x[(long)(d0 + e) * p.ldx + col] : x[(d0 + e) + col * p.ldx];
+            for (int e = 0; e < BD; ++e)
 #pragma unroll
                 for (int c = 0; c < BI; ++c) {
                     const E a = p.block_im_fast ? vb[c + e * BI] : vb[c * BD + e];
-                    acc[c] = Ops<E>::fma(a, xv, acc[c]);
+                    acc[c] = Ops<E>::fma(a, xc[e], acc[c]);
                 }
-            }
         }
 #pragma unroll
         for (int c = 0; c < BI; ++c) {
@@ -202,9 +219,12 @@ __global__ void __launch_bounds__(256) bsr_ell_kernel(const BsrArgs p, int nnz, 
 template <typename E, int BI, int BD>
 void launch_ell(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_t s) {
     const int blk_bytes = nnz * BI * BD * (int)sizeof(E);
-    const int rb = std::max(1, ELL_LDS_BYTES / std::max(1, blk_bytes));
+    int rb = std::max(1, ELL_LDS_BYTES / std::max(1, blk_bytes));
+    // about one (row, rhs) pair per thread
+    if (a.ncols <= 256) rb = (int)std::min<long>(rb, std::max(1L, 256 / a.ncols));
     const long blocks = (a.block_rows + rb - 1) / rb;
-    const size_t lds = (size_t)rb * blk_bytes;
+    if (blocks >= (1L << 31)) throw Error("bsr: grid too large");
+    const size_t lds = (size_t)rb * blk_bytes + (size_t)rb * nnz * sizeof(int);
     KernelTimer timer("bsr", s);
     if (yrow && xrow)
         hipLaunchKernelGGL((bsr_ell_kernel<E, BI, BD, true, true>), dim3(blocks), dim3(256), lds, s, a, nnz, rb);
@@ -237,11 +257,9 @@ void launch_typed(const BsrArgs &a, int nnz_per_row, bool yrow, bool xrow, hipSt
     const long total = a.block_rows * a.bi * a.ncols;
     const long blocks = std::min((total + 255) / 256, 65536L);
     const bool ell = nnz_per_row > 0 &&
-                     (long)nnz_per_row * a.bi * a.bd * (long)sizeof(E) <= ELL_LDS_BYTES;
+                     (long)nnz_per_row * (a.bi * a.bd * (long)sizeof(E) + 4) <= ELL_LDS_BYTES;
     if (ell && a.bi == 3 && a.bd == 3)
         launch_ell<E, 3, 3>(a, nnz_per_row, yrow, xrow, s);
-    else if (ell && a.bi == 12 && a.bd == 12)
-        launch_ell<E, 12, 12>(a, nnz_per_row, yrow, xrow, s);
     else if (a.bi == 3 && a.bd == 3)
         launch_layouts<E, 3, 3>(a, yrow, xrow, blocks, s);
     else if (a.bi == 12 && a.bd == 12)
