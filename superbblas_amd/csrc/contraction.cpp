@@ -135,6 +135,15 @@ void local_contraction(const Scalar &alpha, const Local &x, bool conjx, const Lo
     launch_gemm(d, x.dev);
 }
 
+/// A sub-slab [c0, c0+n) of the slowest label of a dense local array
+Local slab(const Local &l, long c0, long n, std::size_t es) {
+    Local r = l;
+    const long inner = volume(l.size) / std::max(1, l.size[0]);
+    r.ptr = (char *)l.ptr + (std::size_t)(c0 * inner) * es;
+    r.size[0] = (int)n;
+    return r;
+}
+
 void dist_contraction(const Scalar &alpha, const DistTensor &v0, const Coor &from0,
                       const Coor &size0, bool conj0, const DistTensor &v1, const Coor &from1,
                       const Coor &size1, bool conj1, const Scalar &beta, const DistTensor &vr,
@@ -351,11 +360,55 @@ void dist_contraction(const Scalar &alpha, const DistTensor &v0, const Coor &fro
     if (need_x) dist_copy(Scalar{1, 0}, X, fromX, sizeX, tx, tfromX, false, comm);
     if (need_y) dist_copy(Scalar{1, 0}, Y, fromY, sizeY, ty, tfromY, false, comm);
 
+    const Coor tfromr = reorder(fromr, vr.labels, lR), tsizer = reorder(sizer, vr.labels, lR);
+
+    // 3+4 pipelined: with other ranks in the reduction, split the leading T label into chunks;
+    // chunk c's partial output is reduced into vr (pack, RCCL exchange, Add unpack) on the
+    // side stream while the GEMMs of chunk c+1 run on the main stream
+    // The decision uses only information every rank holds (the global work list), so all ranks
+    // issue the same sequence of collective copies.
+    int nchunks = 1;
+    if (comm.nprocs > 1 && !T.empty() && tsizer[0] > 1) {
+        bool ok = true;
+        for (const WorkPiece &w : work) {
+            const char xf = w.xdirect ? X.labels[0] : lX[0];
+            const char yf = w.ydirect >= 0 ? Y.labels[0] : lY[0];
+            const Coor prs = reorder(w.pr.size, vr.labels, lR);
+            ok &= xf == T[0] && yf == T[0] && prs[0] == tsizer[0];
+        }
+        for (const LocalWork &l : lw) ok &= l.x.size[0] == tsizer[0] && l.y.size[0] == tsizer[0];
+        if (ok) nchunks = (int)std::min<long>(4, tsizer[0]);
+    }
+    if (nchunks > 1) {
+        const int dev = !lw.empty() ? lw[0].r.dev : (comm.device >= 0 ? comm.device : vr.dev.empty() ? 0 : vr.dev[0]);
+        const hipStream_t main_s = get_stream(dev), side_s = get_side_stream(dev);
+        const long tn = tsizer[0];
+        for (int c = 0; c < nchunks; ++c) {
+            const long c0 = tn * c / nchunks, c1 = tn * (c + 1) / nchunks;
+            if (c1 == c0) continue;
+            for (const LocalWork &l : lw)
+                local_contraction(alpha, slab(l.x, c0, c1 - c0, es), conjX,
+                                  slab(l.y, c0, c1 - c0, es), conjY, Scalar{0, 0},
+                                  slab(l.r, c0, c1 - c0, es));
+            stream_after(side_s, main_s);
+            {
+                StreamOverride so(dev, side_s);
+                Coor f0 = tfromr, s0 = tsizer, f1 = fromr;
+                f0[0] = (int)normalize_coor((long)f0[0] + c0, tr.dim[0]);
+                s0[0] = (int)(c1 - c0);
+                const int tr_in_vr = (int)vr.labels.find(lR[0]);
+                f1[tr_in_vr] = (int)normalize_coor((long)f1[tr_in_vr] + c0, vr.dim[tr_in_vr]);
+                dist_copy(Scalar{1, 0}, tr, f0, s0, vr, f1, true, comm);
+            }
+        }
+        stream_after(main_s, side_s); // join: vr complete, temporaries free in order
+        return;
+    }
+
     // 3) local contractions into the partial outputs
     for (const LocalWork &l : lw) local_contraction(alpha, l.x, conjX, l.y, conjY, Scalar{0, 0}, l.r);
 
     // 4) reduce the partial outputs into vr (dist.h:3183-3186)
-    const Coor tfromr = reorder(fromr, vr.labels, lR), tsizer = reorder(sizer, vr.labels, lR);
     dist_copy(Scalar{1, 0}, tr, tfromr, tsizer, vr, fromr, true, comm);
 }
 

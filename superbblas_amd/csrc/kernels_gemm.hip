@@ -51,7 +51,7 @@ template <> struct Elem<float, true> { typedef float2 type; };
 template <> struct Elem<float, false> { typedef float type; };
 
 template <typename E> __device__ __forceinline__ E zero_elem() { return E{}; }
-__device__ __forceinline__ double2 conj_if(double2 v, bool c) { return c ? double2{v.x, -v.y} : v; }
+[[maybe_unused]] __device__ __forceinline__ double2 conj_if(double2 v, bool c) { return c ? double2{v.x, -v.y} : v; }
 __device__ __forceinline__ float2 conj_if(float2 v, bool c) { return c ? float2{v.x, -v.y} : v; }
 __device__ __forceinline__ double conj_if(double v, bool) { return v; }
 __device__ __forceinline__ float conj_if(float v, bool) { return v; }
@@ -60,7 +60,7 @@ __device__ __forceinline__ float conj_if(float v, bool) { return v; }
 /// zero, which is how out-of-tile elements are padded (no per-load branch, so the compiler keeps
 /// every stage load in flight behind the MFMAs instead of waiting after each one).
 template <typename E> __device__ __forceinline__ E buf_load(__amdgpu_buffer_rsrc_t r, unsigned off);
-template <> __device__ __forceinline__ double2 buf_load<double2>(__amdgpu_buffer_rsrc_t r, unsigned off) {
+template <> [[maybe_unused]] __device__ __forceinline__ double2 buf_load<double2>(__amdgpu_buffer_rsrc_t r, unsigned off) {
     auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
     return __builtin_bit_cast(double2, v);
 }

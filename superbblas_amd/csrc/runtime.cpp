@@ -15,6 +15,7 @@ namespace sbx {
 namespace {
 struct DeviceState {
     hipStream_t own = nullptr;  // stream created by the library
+    hipStream_t side = nullptr; // second library stream (overlapped exchanges)
     hipStream_t user = nullptr; // stream set by the caller (sbx_stream_set); may be the null stream
     bool has_user = false;
     bool pool_configured = false;
@@ -49,6 +50,41 @@ hipStream_t get_stream(int device) {
     return st.own;
 }
 
+hipStream_t get_side_stream(int device) {
+    std::lock_guard<std::mutex> g(g_mutex);
+    DeviceState &st = state(device);
+    if (!st.side) {
+        set_device(device);
+        SBX_HIP_CHECK(hipStreamCreateWithFlags(&st.side, hipStreamNonBlocking));
+    }
+    return st.side;
+}
+
+void stream_after(hipStream_t to, hipStream_t from) {
+    if (to == from) return;
+    hipEvent_t ev;
+    SBX_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    SBX_HIP_CHECK(hipEventRecord(ev, from));
+    SBX_HIP_CHECK(hipStreamWaitEvent(to, ev, 0));
+    SBX_HIP_CHECK(hipEventDestroy(ev));
+}
+
+StreamOverride::StreamOverride(int dev, hipStream_t s) : device(dev) {
+    std::lock_guard<std::mutex> g(g_mutex);
+    DeviceState &st = state(dev);
+    prev = st.user;
+    prev_user = st.has_user;
+    st.user = s;
+    st.has_user = true;
+}
+
+StreamOverride::~StreamOverride() {
+    std::lock_guard<std::mutex> g(g_mutex);
+    DeviceState &st = state(device);
+    st.user = prev;
+    st.has_user = prev_user;
+}
+
 void set_user_stream(int device, hipStream_t s, bool has_user) {
     std::lock_guard<std::mutex> g(g_mutex);
     state(device).user = s;
@@ -64,6 +100,12 @@ void destroy_streams() {
             (void)hipStreamSynchronize(st.own);
             (void)hipStreamDestroy(st.own);
             st.own = nullptr;
+        }
+        if (st.side) {
+            (void)hipSetDevice((int)d);
+            (void)hipStreamSynchronize(st.side);
+            (void)hipStreamDestroy(st.side);
+            st.side = nullptr;
         }
     }
 }

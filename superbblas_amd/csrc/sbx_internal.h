@@ -63,6 +63,18 @@ struct Scalar {
 hipStream_t get_stream(int device);
 /// Make `device` current for the calling thread
 void set_device(int device);
+/// Second library stream of a device (exchanges that overlap work on get_stream)
+hipStream_t get_side_stream(int device);
+/// Order: work enqueued later on `to` waits for the work enqueued so far on `from`
+void stream_after(hipStream_t to, hipStream_t from);
+/// While alive, get_stream(device) returns `s` (the library's work is redirected to it)
+struct StreamOverride {
+    int device;
+    hipStream_t prev;
+    bool prev_user;
+    StreamOverride(int device, hipStream_t s);
+    ~StreamOverride();
+};
 /// Stream-ordered scratch allocation (hipMallocAsync pool with a high release threshold)
 void *scratch_alloc(std::size_t bytes, int device);
 void scratch_free(void *p, int device);

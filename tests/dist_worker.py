@@ -83,9 +83,14 @@ def case_contraction(sb, comm, rank, n, dev):
     vr = scatter(sb, gr, dr, pr, rank, 1, dev)
     if vr[0].numel() == 0:
         vr = [torch.zeros(1, dtype=torch.complex128, device=dev)]
+    sb.timings_enable(True)
+    sb.timings_reset()
     sb.contraction(1.0, p0, z7, d0, d0, "tnsxyzc", False, v0, p1, z7, d0, d0, "tNSxyzc", False,
                    v1, 0.0, pr, z5, dr, dr, "tNSns", vr, comm=comm)
     torch.cuda.synchronize()
+    # the cross-rank reduction is pipelined: one GEMM per chunk of t (4 chunks of 1)
+    assert sb.timings_get("gemm")[1] == L, sb.timings_report()
+    sb.timings_enable(False)
     out = gather(np.zeros_like(gr), dr, pr, 1, vr[:1] if rank == 0 else [vr[0][:0]])
     ref = np.zeros_like(gr)
     oracle_contraction(1.0, "tnsxyzc", z7, d0, d0, False, g0, "tNSxyzc", z7, d0, d0, False, g1,
