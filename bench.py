@@ -102,11 +102,16 @@ def main():
     ap.add_argument("--n", type=int, default=64)
     ap.add_argument("--no-side", action="store_true", help="skip permute/BSR side measurements")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="rehearsal of the N>1 path on a box with fewer GPUs than ranks: ranks "
+                         "share GPUs, gloo process group, host-staged exchanges (not a bench)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.share_gpu:
+        local_rank %= torch.cuda.device_count()
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     import superbblas_amd as sb
@@ -114,8 +119,12 @@ def main():
     comm = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
-        comm = sb.Comm.from_torch_distributed(local_rank)
+        if args.share_gpu:
+            dist.init_process_group("gloo")
+            comm = sb.Comm.host_staged(local_rank)
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+            comm = sb.Comm.from_torch_distributed(local_rank)
 
     L, n = args.L, args.n
     grid = {1: [1, 1, 1], 2: [2, 1, 1], 4: [2, 2, 1], 8: [2, 2, 2]}.get(world)
@@ -164,7 +173,8 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device="cpu" if args.share_gpu else dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     step_ms = [a.elapsed_time(b) for a, b in ev]
@@ -177,7 +187,10 @@ def main():
     flops_rank = 8.0 * L * (L ** 3 * 3) * (n * 4) ** 2  # 8 * volT * volA * volB * volC
     total_flops = flops_rank * world * args.steps
     value = total_flops / elapsed / 1e9
-    achieved = flops_rank / kernel_s / 1e12  # flops of one launch / its average duration
+    # flops of one launch (a step's GEMM is split in T chunks when a cross-rank reduction is
+    # pipelined behind it) / the launch's average duration
+    flops_launch = flops_rank * args.steps / max(gemm_calls, 1)
+    achieved = flops_launch / kernel_s / 1e12
 
     side = {}
     if not args.no_side:
@@ -219,12 +232,15 @@ def main():
                                    "16x16x4, complex 4M), %d launches, %.4f ms avg "
                                    "(HIP events on its launch stream)" % (gemm_calls,
                                                                           kernel_s * 1e3),
-                         "flops_per_launch": flops_rank,
+                         "flops_per_launch": flops_launch,
                          "step_TFLOPs": round(flops_rank / step_s / 1e12, 3),
                          "splitk_reduce_ms_avg": round(red_ms / max(red_calls, 1), 4)},
             "cpu_baseline": base,
         }
         line.update(side)
+        if args.share_gpu:
+            line["rehearsal"] = ("ranks shared %d GPU(s) with host-staged exchanges: a test of the "
+                                 "N>1 path, not a measurement" % torch.cuda.device_count())
         print(json.dumps(line))
     if comm is not None:
         comm.close()
