@@ -1,12 +1,11 @@
-// Device runtime: per-device library streams and the stream-ordered scratch pool.
+// Device runtime: per-device library streams, the scratch-memory cache and kernel timers.
 //
 // Reference: platform.h:173-221 (Gpu context), 304-409 (stream helpers), 448-467
-// (getGpuAllocStream: every GPU op of a device is enqueued on one library stream) and
-// alloc.h:91-391 (hipMallocAsync on the alloc stream + a cached scratch-buffer pool).
-// On ROCm the stream-ordered allocator already is a caching pool; raising its release
-// threshold keeps freed scratch resident so steady-state calls do no driver allocations.
+// (getGpuAllocStream: every GPU op of a device is enqueued on one library stream),
+// alloc.h:91-391 (cached scratch buffers) and performance.h:356-518 (timings).
 #include "sbx_internal.h"
 
+#include <cstdlib>
 #include <map>
 #include <mutex>
 
@@ -18,7 +17,6 @@ struct DeviceState {
     hipStream_t side = nullptr; // second library stream (overlapped exchanges)
     hipStream_t user = nullptr; // stream set by the caller (sbx_stream_set); may be the null stream
     bool has_user = false;
-    bool pool_configured = false;
 };
 std::mutex g_mutex;
 std::vector<DeviceState> &states() {
@@ -110,48 +108,110 @@ void destroy_streams() {
     }
 }
 
+//
+// Scratch memory: a caching allocator over hipMalloc (the reference's allocateBufferResouce
+// cache, alloc.h:323-391).  A freed block goes back to a per-device free list together with an
+// event recorded on the stream that last used it; a later allocation reuses it at once on the
+// same stream (stream order) or after waiting on that event from another stream.  Blocks stay
+// mapped for the life of the cache: hipMallocAsync's pool was measured to hand back reused
+// memory with stale contents after many queued launches on this platform, so it is not used.
+//
+namespace {
+struct Block {
+    void *p;
+    std::size_t bytes;
+    hipStream_t stream;
+    hipEvent_t ev;
+};
+struct Cache {
+    std::multimap<std::size_t, Block> free_blocks;
+    std::map<void *, std::size_t> live;
+    std::size_t cached_bytes = 0;
+};
+std::mutex g_cache_mutex;
+std::vector<Cache> &caches() {
+    static std::vector<Cache> c;
+    return c;
+}
+Cache &cache(int device) {
+    auto &c = caches();
+    if ((int)c.size() <= device) c.resize(device + 1);
+    return c[device];
+}
+std::size_t round_bytes(std::size_t b) {
+    if (b <= 256) return 256;
+    if (b < (2u << 20)) {
+        std::size_t r = 256;
+        while (r < b) r <<= 1;
+        return r;
+    }
+    return (b + (2u << 20) - 1) / (2u << 20) * (2u << 20);
+}
+/// Return every cached block of `device` to the driver (callers hold g_cache_mutex)
+void release_cached(int device) {
+    Cache &c = cache(device);
+    if (c.free_blocks.empty()) return;
+    (void)hipDeviceSynchronize();
+    for (auto &e : c.free_blocks) {
+        if (e.second.ev) (void)hipEventDestroy(e.second.ev);
+        (void)hipFree(e.second.p);
+    }
+    c.free_blocks.clear();
+    c.cached_bytes = 0;
+}
+} // namespace
+
 void *scratch_alloc(std::size_t bytes, int device) {
     if (bytes == 0) return nullptr;
     set_device(device);
-    {
-        std::lock_guard<std::mutex> g(g_mutex);
-        DeviceState &st = state(device);
-        if (!st.pool_configured) {
-            hipMemPool_t pool;
-            if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
-                uint64_t threshold = UINT64_MAX;
-                (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &threshold);
-            }
-            st.pool_configured = true;
+    const hipStream_t s = get_stream(device);
+    const std::size_t rb = round_bytes(bytes);
+    std::lock_guard<std::mutex> g(g_cache_mutex);
+    Cache &c = cache(device);
+    auto it = c.free_blocks.lower_bound(rb);
+    if (it != c.free_blocks.end() && it->first <= 2 * rb) {
+        Block b = it->second;
+        c.free_blocks.erase(it);
+        c.cached_bytes -= b.bytes;
+        if (b.ev) {
+            if (b.stream != s) SBX_HIP_CHECK(hipStreamWaitEvent(s, b.ev, 0));
+            SBX_HIP_CHECK(hipEventDestroy(b.ev));
         }
+        c.live[b.p] = b.bytes;
+        return b.p;
     }
     void *p = nullptr;
-    hipError_t e = hipMallocAsync(&p, bytes, get_stream(device));
-    if (e != hipSuccess) {
-        // Mirror alloc.h:104-168: release the cached memory and retry once
+    if (hipMalloc(&p, rb) != hipSuccess) {
+        // out of memory: give the cached blocks back and retry once (alloc.h:104-168)
         (void)hipGetLastError();
-        (void)hipStreamSynchronize(get_stream(device));
-        hipMemPool_t pool;
-        if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) (void)hipMemPoolTrimTo(pool, 0);
-        SBX_HIP_CHECK(hipMallocAsync(&p, bytes, get_stream(device)));
+        release_cached(device);
+        SBX_HIP_CHECK(hipMalloc(&p, rb));
     }
+    c.live[p] = rb;
     return p;
 }
 
 void scratch_free(void *p, int device) {
     if (!p) return;
     set_device(device);
-    SBX_HIP_CHECK(hipFreeAsync(p, get_stream(device)));
+    const hipStream_t s = get_stream(device);
+    std::lock_guard<std::mutex> g(g_cache_mutex);
+    Cache &c = cache(device);
+    auto it = c.live.find(p);
+    if (it == c.live.end()) throw Error("scratch_free: unknown pointer");
+    Block b{p, it->second, s, nullptr};
+    c.live.erase(it);
+    SBX_HIP_CHECK(hipEventCreateWithFlags(&b.ev, hipEventDisableTiming));
+    SBX_HIP_CHECK(hipEventRecord(b.ev, s));
+    c.free_blocks.emplace(b.bytes, b);
+    c.cached_bytes += b.bytes;
 }
 
 void trim_pools() {
-    int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess) return;
-    for (int d = 0; d < n && d < (int)states().size(); ++d) {
+    std::lock_guard<std::mutex> g(g_cache_mutex);
+    for (int d = 0; d < (int)caches().size(); ++d) {
         (void)hipSetDevice(d);
-        (void)hipDeviceSynchronize();
-        hipMemPool_t pool;
-        if (hipDeviceGetDefaultMemPool(&pool, d) == hipSuccess) (void)hipMemPoolTrimTo(pool, 0);
+        release_cached(d);
     }
 }
 

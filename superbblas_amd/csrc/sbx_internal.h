@@ -75,7 +75,7 @@ struct StreamOverride {
     StreamOverride(int device, hipStream_t s);
     ~StreamOverride();
 };
-/// Stream-ordered scratch allocation (hipMallocAsync pool with a high release threshold)
+/// Stream-ordered scratch allocation (caching allocator over hipMalloc, see runtime.cpp)
 void *scratch_alloc(std::size_t bytes, int device);
 void scratch_free(void *p, int device);
 

@@ -7,6 +7,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <string>
 #include <vector>
 
 using namespace sbx;
@@ -47,7 +48,11 @@ void run(const char *name, F launch, const GemmKArgs &p, int reps, double flops,
     (void)hipEventCreate(&a);
     (void)hipEventCreate(&b);
     (void)hipEventRecord(a, s);
-    for (int i = 0; i < reps; ++i) launch(p, s);
+    static const bool sync_each = getenv("SYNC_EACH") != nullptr;
+    for (int i = 0; i < reps; ++i) {
+        launch(p, s);
+        if (sync_each) (void)hipStreamSynchronize(s);
+    }
     (void)hipEventRecord(b, s);
     (void)hipEventSynchronize(b);
     float ms = 0;
@@ -72,7 +77,8 @@ void run(const char *name, F launch, const GemmKArgs &p, int reps, double flops,
 
 int main(int argc, char **argv) {
     const long L = 16, n = 64;
-    const long m = 4 * n, nn = 4 * n, k = L * L * L * 3, batch = L;
+    const long m = 4 * n, nn = 4 * n, k = L * L * L * 3;
+    const long batch = argc > 2 ? atol(argv[2]) : L;
     double *A, *B, *C;
     (void)hipMalloc(&A, sizeof(double) * 2 * m * k * batch);
     (void)hipMalloc(&B, sizeof(double) * 2 * nn * k * batch);
@@ -98,23 +104,13 @@ int main(int argc, char **argv) {
     (void)hipStreamSynchronize(get_stream(0));
     (void)hipMemcpy(ref.data(), C, nc * sizeof(double), hipMemcpyDeviceToHost);
 
-    REG(64, 64, 16, 2, 2, 0, 1024);
-    DMA(64, 64, 16, 2, 2, 0, 1024);
-    DMA(128, 128, 16, 4, 2, 0, 256);
-    DMA(128, 128, 8, 4, 2, 0, 256);
-    DMA(128, 128, 8, 4, 2, 0, 512);
-    DMA(128, 128, 8, 2, 2, 0, 512);
-    DMA(128, 128, 8, 2, 2, 0, 1024);
-    DMA(64, 64, 8, 2, 2, 0, 1024);
-    DMA(64, 64, 8, 2, 2, 0, 2048);
-    DMA(128, 64, 8, 2, 2, 0, 1024);
-    DMA(128, 64, 8, 4, 1, 0, 1024);
-    DMA(128, 64, 8, 2, 1, 0, 1024);
-    DMA(256, 64, 8, 4, 1, 0, 512);
-    DMA(256, 128, 8, 4, 2, 0, 256);
-    DMA(256, 128, 8, 4, 2, 0, 512);
-    DMA(128, 256, 8, 2, 4, 0, 256);
-    DMA(256, 256, 8, 4, 4, 0, 256);
-    DMA(128, 128, 16, 4, 2, 0, 256);
+    const char *only = getenv("ONLY");
+    for (int rep = 0; rep < 3; ++rep) {
+        if (!only || std::string(only) == "a") DMA(128, 128, 8, 4, 2, 0, 256);
+        if (!only || std::string(only) == "b") DMA(128, 128, 16, 4, 2, 0, 256);
+        if (!only || std::string(only) == "c") DMA(128, 64, 8, 2, 2, 0, 512);
+        if (!only || std::string(only) == "d") REG(64, 64, 16, 2, 2, 0, 1024);
+        if (only && std::string(only) == "e") DMA(128, 128, 8, 4, 2, 1, 1);
+    }
     return 0;
 }
