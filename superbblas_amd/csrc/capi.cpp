@@ -399,6 +399,10 @@ int sbx_copy(int nd0, int nd1, const double *alpha, int t0, int t1, const int *p
         check_session(session);
         const Comm c = get_comm(comm);
         const bool rev = co == SBX_FAST_TO_SLOW;
+        check_copy_args(to_labels(o0, nd0, rev, "o0"), to_coor(from0, nd0, rev),
+                        to_coor(size0, nd0, rev), to_coor(dim0, nd0, rev),
+                        to_labels(o1, nd1, rev, "o1"), to_coor(from1, nd1, rev),
+                        to_coor(dim1, nd1, rev));
         Mirror m;
         m.device = pick_device({{ctx0, ncomponents0}, {ctx1, ncomponents1}}, c);
         DistTensor a = make_tensor(nd0, o0, dim0, p0, ncomponents0, v0, ctx0, t0, c, rev, m, false, "o0");
@@ -479,6 +483,9 @@ int sbx_contraction(int nd0, int nd1, int ndr, int t, const double *alpha, const
             throw Error("contraction: unsupported type");
         const Comm c = get_comm(comm);
         const bool rev = co == SBX_FAST_TO_SLOW;
+        check_contraction_args(to_labels(o0, nd0, rev, "o0"), to_coor(size0, nd0, rev),
+                               to_labels(o1, nd1, rev, "o1"), to_coor(size1, nd1, rev),
+                               to_labels(o_r, ndr, rev, "o_r"), to_coor(sizer, ndr, rev), t, t, t);
         Mirror m;
         m.device = pick_device({{ctx0, ncomponents0}, {ctx1, ncomponents1}, {ctxr, ncomponentsr}}, c);
         DistTensor a = make_tensor(nd0, o0, dim0, p0, ncomponents0, v0, ctx0, t, c, rev, m, false, "o0");

@@ -135,6 +135,41 @@ void local_contraction(const Scalar &alpha, const Local &x, bool conjx, const Lo
     launch_gemm(d, x.dev);
 }
 
+void check_contraction_args(const std::string &l0, const Coor &size0, const std::string &l1,
+                            const Coor &size1, const std::string &lr, const Coor &sizer, int t0,
+                            int t1, int tr) {
+    if (size0.size() != l0.size() || size1.size() != l1.size() || sizer.size() != lr.size())
+        throw Error("contraction: invalid coordinates");
+    if (t0 != t1 || t0 != tr) throw Error("contraction: mixed types");
+    if (t0 == SBX_INT || t0 == SBX_SIZE_T) throw Error("contraction: unsupported type");
+    // check_dimensions (tensor.h:623-646)
+    for (int i = 0; i < (int)l0.size(); ++i) {
+        auto j = l1.find(l0[i]);
+        if (j != std::string::npos && size1[j] != size0[i])
+            throw Error("some dimension does not match");
+        auto k = lr.find(l0[i]);
+        if (k != std::string::npos && sizer[k] != size0[i])
+            throw Error("some dimension does not match");
+    }
+    for (int i = 0; i < (int)l1.size(); ++i) {
+        auto k = lr.find(l1[i]);
+        if (k != std::string::npos && sizer[k] != size1[i])
+            throw Error("some dimension does not match");
+    }
+    for (int i = 0; i < (int)lr.size(); ++i)
+        if (l0.find(lr[i]) == std::string::npos &&
+            l1.find(lr[i]) == std::string::npos)
+            throw Error("o_r has unmatched dimensions");
+    for (int i = 0; i < (int)l0.size(); ++i)
+        if (l1.find(l0[i]) == std::string::npos &&
+            lr.find(l0[i]) == std::string::npos)
+            throw Error("o0 has unmatched dimensions");
+    for (int i = 0; i < (int)l1.size(); ++i)
+        if (l0.find(l1[i]) == std::string::npos &&
+            lr.find(l1[i]) == std::string::npos)
+            throw Error("o1 has unmatched directions");
+}
+
 /// A sub-slab [c0, c0+n) of the slowest label of a dense local array
 Local slab(const Local &l, long c0, long n, std::size_t es) {
     Local r = l;
@@ -148,32 +183,8 @@ void dist_contraction(const Scalar &alpha, const DistTensor &v0, const Coor &fro
                       const Coor &size0, bool conj0, const DistTensor &v1, const Coor &from1,
                       const Coor &size1, bool conj1, const Scalar &beta, const DistTensor &vr,
                       const Coor &fromr, const Coor &sizer, const Comm &comm) {
-    // check_dimensions (tensor.h:623-646)
-    for (int i = 0; i < v0.nd(); ++i) {
-        auto j = v1.labels.find(v0.labels[i]);
-        if (j != std::string::npos && size1[j] != size0[i])
-            throw Error("some dimension does not match");
-        auto k = vr.labels.find(v0.labels[i]);
-        if (k != std::string::npos && sizer[k] != size0[i])
-            throw Error("some dimension does not match");
-    }
-    for (int i = 0; i < v1.nd(); ++i) {
-        auto k = vr.labels.find(v1.labels[i]);
-        if (k != std::string::npos && sizer[k] != size1[i])
-            throw Error("some dimension does not match");
-    }
-    for (int i = 0; i < vr.nd(); ++i)
-        if (v0.labels.find(vr.labels[i]) == std::string::npos &&
-            v1.labels.find(vr.labels[i]) == std::string::npos)
-            throw Error("o_r has unmatched dimensions");
-    for (int i = 0; i < v0.nd(); ++i)
-        if (v1.labels.find(v0.labels[i]) == std::string::npos &&
-            vr.labels.find(v0.labels[i]) == std::string::npos)
-            throw Error("o0 has unmatched dimensions");
-    for (int i = 0; i < v1.nd(); ++i)
-        if (v0.labels.find(v1.labels[i]) == std::string::npos &&
-            vr.labels.find(v1.labels[i]) == std::string::npos)
-            throw Error("o1 has unmatched directions");
+    check_contraction_args(v0.labels, size0, v1.labels, size1, vr.labels, sizer, v0.dtype,
+                           v1.dtype, vr.dtype);
     if (v0.dtype != v1.dtype || v0.dtype != vr.dtype) throw Error("contraction: mixed types");
 
     const int dtype = v0.dtype;

@@ -284,6 +284,23 @@ HostStage::~HostStage() {
 // Distributed copy
 //
 
+void check_copy_args(const std::string &l0, const Coor &from0, const Coor &size0,
+                     const Coor &dim0, const std::string &l1, const Coor &from1,
+                     const Coor &dim1) {
+    if (from0.size() != l0.size() || size0.size() != l0.size() || dim0.size() != l0.size() ||
+        from1.size() != l1.size() || dim1.size() != l1.size())
+        throw Error("copy: invalid coordinates");
+    for (std::size_t k = 0; k < l0.size(); ++k) {
+        if (size0[k] < 0 || size0[k] > dim0[k]) throw Error("copy: invalid size0");
+        const auto j = l1.find(l0[k]);
+        if (j == std::string::npos) {
+            if (size0[k] > 1) throw Error("Invalid copy operation");
+        } else if (size0[k] > dim1[j]) {
+            throw Error("Invalid copy operation");
+        }
+    }
+}
+
 void copy_plan_counts(const DistTensor &src, const Coor &from0, const Coor &size0,
                       const DistTensor &dst, const Coor &from1, bool add, int rank,
                       std::vector<long> &send, std::vector<long> &recv, long &local) {

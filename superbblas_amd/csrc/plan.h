@@ -128,6 +128,15 @@ struct Local {
 void dist_copy(const Scalar &alpha, const DistTensor &src, const Coor &from0, const Coor &size0,
                const DistTensor &dst, const Coor &from1, bool add, const Comm &comm);
 
+/// Host-only argument checks, run before any device work (the reference validates first:
+/// tensor.h:495-507 check_isomorphic, tensor.h:623-646 check_dimensions)
+void check_copy_args(const std::string &l0, const Coor &from0, const Coor &size0,
+                     const Coor &dim0, const std::string &l1, const Coor &from1,
+                     const Coor &dim1);
+void check_contraction_args(const std::string &l0, const Coor &size0, const std::string &l1,
+                            const Coor &size1, const std::string &lr, const Coor &sizer, int t0,
+                            int t1, int tr);
+
 /// Element counts of the exchange dist_copy would do on `rank`: send[q] / recv[q] elements to /
 /// from rank q (q != rank) and `local` elements moved within the rank (no GPU work)
 void copy_plan_counts(const DistTensor &src, const Coor &from0, const Coor &size0,
