@@ -72,3 +72,12 @@ def test_gemm_beta0_ignores_nan(gpu):
     sb.xgemm_batch_strided("N", "N", 16, 16, 16, 1.0, a, 16, 0, b, 16, 0, 0.0, c, 16, 0, 1)
     torch.cuda.synchronize()
     assert torch.all(c == 16)
+
+
+@pytest.mark.parametrize("dtype", [np.complex128, np.float64, np.complex64, np.float32])
+@pytest.mark.parametrize("ta,tb", [("T", "N"), ("N", "N"), ("N", "T"), ("C", "N"), ("T", "C")])
+@pytest.mark.parametrize("m,n,k", [(96, 80, 128), (256, 192, 512)])
+def test_gemm_granule_shapes(gpu, dtype, ta, tb, m, n, k):
+    # extents that are multiples of the 16-byte granule of every type: the LDS-DMA kernel path
+    out, ref = _run(gpu, dtype, ta, tb, m, n, k, 3, 0.5 + 1j, -0.75)
+    assert rel_err(out, ref) < TOL[dtype]

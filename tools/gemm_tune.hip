@@ -71,7 +71,7 @@ void run(const char *name, F launch, const GemmKArgs &p, int reps, double flops,
 #define DMA(BM, BN, BKK, WM, WN, SPL, TGT)                                                      \
     run("dma " #BM "x" #BN "x" #BKK " w" #WM "x" #WN " s" #SPL " t" #TGT,                         \
         [&](const GemmKArgs &q, hipStream_t s) {                                                 \
-            launch_dma_cfg<true, true, BM, BN, BKK, WM, WN>(q, 0, s, SPL, TGT);                   \
+            launch_dma_cfg<double, true, true, true, BM, BN, BKK, WM, WN>(q, 0, s, SPL, TGT);                   \
         },                                                                                       \
         p, reps, flops, &ref, C, nc)
 
