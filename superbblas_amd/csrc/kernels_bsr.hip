@@ -219,21 +219,40 @@ __global__ void __launch_bounds__(256) bsr_ell_kernel(const BsrArgs p, int nnz, 
 
 // Large blocks (12x12 spin x color, the Wilson-like operator): block-row products on the FP64
 // matrix cores.  A wave owns ROWS block rows and a tile of 16 rhs columns and computes, for each
-// of its block rows, the 16x16 tile  Y_i = sum_j A_ij X_j  with v_mfma_f64_16x16x4_f64 (tile rows
+// of its block rows, the 16x16 tile  Y_i = sum_j A_ij X_j  with v_mfma_f64_16x16x4_f64 or
+// v_mfma_f32_16x16x4f32 (tile rows
 // >= BI are padding), K running over the BD domain rows of every nonzero block (BD/4 steps per
 // block, 4 real MFMAs per complex step).  The ROWS block rows are interleaved so their loads are
 // in flight together and their MFMA chains are independent.  Fragments come straight from
 // global memory: lane l reads A_ij[l&15][k+(l>>4)] and x[d_j+k+(l>>4)][col0+(l&15)]
 // (contiguous along the rhs for row-major x); out-of-range rows, columns and skipped blocks
 // (-1 columns) are clamped loads replaced by zero, so the loop has no divergent branches.
-template <bool CPLX> struct BsrMfmaElem;
-template <> struct BsrMfmaElem<true> { typedef double2 type; };
-template <> struct BsrMfmaElem<false> { typedef double type; };
-
-template <bool CPLX, int BI, int BD, int ROWS, bool YROW, bool XROW>
-__global__ void __launch_bounds__(256) bsr_mfma_kernel(const BsrArgs p, long ntiles_n) {
-    typedef typename BsrMfmaElem<CPLX>::type E;
+template <typename R, bool CPLX> struct BsrMfmaElem;
+template <> struct BsrMfmaElem<double, true> { typedef double2 type; };
+template <> struct BsrMfmaElem<double, false> { typedef double type; };
+template <> struct BsrMfmaElem<float, true> { typedef float2 type; };
+template <> struct BsrMfmaElem<float, false> { typedef float type; };
+// 16x16x4 MFMA per real type and its C/D row map (col = lane & 15)
+template <typename R> struct BsrMfma;
+template <> struct BsrMfma<double> {
     typedef double acc_t __attribute__((ext_vector_type(4)));
+    static __device__ __forceinline__ acc_t mma(double a, double b, acc_t c) {
+        return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ int row(int lane, int q) { return (lane >> 4) + 4 * q; }
+};
+template <> struct BsrMfma<float> {
+    typedef float acc_t __attribute__((ext_vector_type(4)));
+    static __device__ __forceinline__ acc_t mma(float a, float b, acc_t c) {
+        return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ int row(int lane, int q) { return 4 * (lane >> 4) + q; }
+};
+
+template <typename R, bool CPLX, int BI, int BD, int ROWS, bool YROW, bool XROW>
+__global__ void __launch_bounds__(256) bsr_mfma_kernel(const BsrArgs p, long ntiles_n) {
+    typedef typename BsrMfmaElem<R, CPLX>::type E;
+    typedef typename BsrMfma<R>::acc_t acc_t;
     static_assert(BI <= 16 && BD % 4 == 0, "block shape");
     const E *__restrict__ v = (const E *)p.v;
     const E *__restrict__ x = (const E *)p.x;
@@ -285,22 +304,22 @@ __global__ void __launch_bounds__(256) bsr_mfma_kernel(const BsrArgs p, long nti
 #pragma unroll
             for (int r = 0; r < ROWS; ++r) {
                 if constexpr (CPLX) {
-                    accR[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[r][ks].x, bf[r][ks].x, accR[r], 0, 0, 0);
-                    accI[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[r][ks].x, bf[r][ks].y, accI[r], 0, 0, 0);
-                    accR[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(-af[r][ks].y, bf[r][ks].y, accR[r], 0, 0, 0);
-                    accI[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[r][ks].y, bf[r][ks].x, accI[r], 0, 0, 0);
+                    accR[r] = BsrMfma<R>::mma(af[r][ks].x, bf[r][ks].x, accR[r]);
+                    accI[r] = BsrMfma<R>::mma(af[r][ks].x, bf[r][ks].y, accI[r]);
+                    accR[r] = BsrMfma<R>::mma(-af[r][ks].y, bf[r][ks].y, accR[r]);
+                    accI[r] = BsrMfma<R>::mma(af[r][ks].y, bf[r][ks].x, accI[r]);
                 } else {
-                    accR[r] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[r][ks], bf[r][ks], accR[r], 0, 0, 0);
+                    accR[r] = BsrMfma<R>::mma(af[r][ks], bf[r][ks], accR[r]);
                 }
             }
     }
-    // C/D map of v_mfma_f64_16x16x4_f64: col = lane & 15, row = (lane >> 4) + 4 * q
+    // C/D map: col = lane & 15, row = BsrMfma<R>::row(lane, q)
 #pragma unroll
     for (int r = 0; r < ROWS; ++r) {
         if (i0 + r >= p.block_rows) break;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const int row = kq + 4 * q;
+            const int row = BsrMfma<R>::row(lane, q);
             if (row >= BI || !bcol_ok) continue;
             const long img = (i0 + r) * BI + row;
             E *yp = YROW ? y + img * p.ldy + bcol : y + img + bcol * p.ldy;
@@ -314,7 +333,7 @@ __global__ void __launch_bounds__(256) bsr_mfma_kernel(const BsrArgs p, long nti
     }
 }
 
-template <bool CPLX, int BI, int BD, int ROWS>
+template <typename R, bool CPLX, int BI, int BD, int ROWS>
 void launch_bsr_mfma(const BsrArgs &a, bool yrow, bool xrow, hipStream_t s) {
     const long ntn = (a.ncols + 15) / 16;
     const long waves = (a.block_rows + ROWS - 1) / ROWS * ntn;
@@ -322,13 +341,13 @@ void launch_bsr_mfma(const BsrArgs &a, bool yrow, bool xrow, hipStream_t s) {
     if (blocks >= (1L << 31)) throw Error("bsr: grid too large");
     KernelTimer timer("bsr", s);
     if (yrow && xrow)
-        hipLaunchKernelGGL((bsr_mfma_kernel<CPLX, BI, BD, ROWS, true, true>), dim3(blocks), dim3(256), 0, s, a, ntn);
+        hipLaunchKernelGGL((bsr_mfma_kernel<R, CPLX, BI, BD, ROWS, true, true>), dim3(blocks), dim3(256), 0, s, a, ntn);
     else if (yrow && !xrow)
-        hipLaunchKernelGGL((bsr_mfma_kernel<CPLX, BI, BD, ROWS, true, false>), dim3(blocks), dim3(256), 0, s, a, ntn);
+        hipLaunchKernelGGL((bsr_mfma_kernel<R, CPLX, BI, BD, ROWS, true, false>), dim3(blocks), dim3(256), 0, s, a, ntn);
     else if (!yrow && xrow)
-        hipLaunchKernelGGL((bsr_mfma_kernel<CPLX, BI, BD, ROWS, false, true>), dim3(blocks), dim3(256), 0, s, a, ntn);
+        hipLaunchKernelGGL((bsr_mfma_kernel<R, CPLX, BI, BD, ROWS, false, true>), dim3(blocks), dim3(256), 0, s, a, ntn);
     else
-        hipLaunchKernelGGL((bsr_mfma_kernel<CPLX, BI, BD, ROWS, false, false>), dim3(blocks), dim3(256), 0, s, a, ntn);
+        hipLaunchKernelGGL((bsr_mfma_kernel<R, CPLX, BI, BD, ROWS, false, false>), dim3(blocks), dim3(256), 0, s, a, ntn);
     SBX_HIP_CHECK(hipGetLastError());
 }
 
@@ -381,13 +400,14 @@ void launch_typed(const BsrArgs &a, int nnz_per_row, bool yrow, bool xrow, hipSt
     else if (a.bi == 12 && a.bd == 12) {
         // one block row per wave: interleaving 2 or 4 rows per wave measured 6 % / 25 % slower
         // (more VGPRs, fewer waves to hide the HBM latency of the value stream)
-        if constexpr (std::is_same<E, double2>::value) {
-            launch_bsr_mfma<true, 12, 12, 1>(a, yrow, xrow, s);
-        } else if constexpr (std::is_same<E, double>::value) {
-            launch_bsr_mfma<false, 12, 12, 1>(a, yrow, xrow, s);
-        } else {
-            launch_layouts<E, 12, 12>(a, yrow, xrow, blocks, s);
-        }
+        if constexpr (std::is_same<E, double2>::value)
+            launch_bsr_mfma<double, true, 12, 12, 1>(a, yrow, xrow, s);
+        else if constexpr (std::is_same<E, double>::value)
+            launch_bsr_mfma<double, false, 12, 12, 1>(a, yrow, xrow, s);
+        else if constexpr (std::is_same<E, float2>::value)
+            launch_bsr_mfma<float, true, 12, 12, 1>(a, yrow, xrow, s);
+        else
+            launch_bsr_mfma<float, false, 12, 12, 1>(a, yrow, xrow, s);
     }
     else
         launch_layouts<E, 0, 0>(a, yrow, xrow, blocks, s);

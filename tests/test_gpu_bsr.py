@@ -69,3 +69,34 @@ def test_bsr_lattice(gpu, spin, color, ncols, y_layout):
     torch.cuda.synchronize()
     assert rel_err(ty.cpu().numpy(), yref) == 0.0
     op.destroy()
+
+
+@pytest.mark.parametrize("dtype,ttype", [(np.complex64, 2), (np.float64, 1), (np.float32, 0)])
+@pytest.mark.parametrize("spin,color,ncols", [(1, 3, 5), (4, 3, 3), (4, 3, 20)])
+def test_bsr_lattice_types(gpu, dtype, ttype, spin, color, ncols):
+    """Other element types on the 3x3 (ELL) and 12x12 (MFMA) kernels, x/y row major; small
+    integer values so every type is exact."""
+    import torch
+    import superbblas_amd as sb
+    L = 4
+    dim, ii, jj, vals, nb = lattice_operator(L, spin, color)
+    vals = (vals.real if np.dtype(dtype).kind == "f" else vals).astype(dtype)
+    b = spin * color
+    vol = L ** 4
+    g = np.arange(vol * b * ncols)
+    x = ((g % 7 - 3) + (1j * (g % 5 - 2) if np.dtype(dtype).kind == "c" else 0)).astype(dtype)
+    yref = np.zeros(vol * b * ncols, dtype)
+    oracle_bsr(ttype, dim, 0, vol, b, b, ii, jj, vals, False, x, ncols, True, yref, ncols, True,
+               ncols, 1.0)
+    full = [([0] * 6, dim)]
+    op = sb.create_bsr(full, dim, full, dim, [1, 1, 1, 1, spin, color], [1, 1, 1, 1, spin, color],
+                       False, [torch.from_numpy(ii).to(gpu)], [torch.from_numpy(jj).to(gpu)],
+                       [torch.from_numpy(vals).to(gpu)])
+    dimx = [1, L, L, L, L, spin, color, ncols]
+    ty = torch.zeros(vol * b * ncols, dtype=torch.from_numpy(x).dtype, device=gpu)
+    sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", [([0] * 8, dimx)], "pXYZTSCn", [0] * 8, dimx, dimx,
+                  [torch.from_numpy(x).to(gpu)], 0.0, [([0] * 8, dimx)], "pxyztscn", [0] * 8,
+                  dimx, dimx, "p", [ty])
+    torch.cuda.synchronize()
+    assert np.array_equal(ty.cpu().numpy(), yref)
+    op.destroy()
