@@ -77,7 +77,7 @@ def cpu_baseline(threads):
             "kind": "port", "sample": "oracle xgemm_batch_strided 'T','N' 64x64x1536 batch 8"}
 
 
-def pmc_traffic(kernel_substr):
+def pmc_traffic(*kernel_substrs):
     """HBM bytes per launch of a kernel from the latest committed PMC pass (profiles/rNN_pmc.json,
     made by tools/pmc_summary.py from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of this
     bench).  PMC counters cannot be read inside a timed run, so they come from that pass."""
@@ -88,7 +88,7 @@ def pmc_traffic(kernel_substr):
     with open(files[-1]) as f:
         ks = json.load(f)["kernels"]
     for k, v in ks.items():
-        if kernel_substr in k:
+        if all(sub in k for sub in kernel_substrs):
             return v["hbm_bytes"], os.path.relpath(files[-1], ROOT) + ": " + k
     return None, None
 
@@ -196,11 +196,16 @@ def main():
     if not args.no_side:
         side.update(permute_bench(sb, dev, L, n))
         side.update(bsr_bench(sb, dev, L))
+        if world == 1:
+            try:
+                side.update(chain_bench(sb, dev))
+            except Exception as e:  # a side measurement never takes the bench down
+                side["chain_error"] = str(e)[:200]
     base = None
     if rank == 0 and not args.no_cpu:
         base = cpu_baseline(int(os.environ.get("OMP_NUM_THREADS", "16")))
 
-    traffic, traffic_src = pmc_traffic("gemm_z_dma_kernel<true, true, 128, 128, 8, 4, 2>")
+    traffic, traffic_src = pmc_traffic("dma_kernel<", "128, 128, 8, 4, 2>")
     if rank == 0:
         line = {
             "metric": "lattice contraction GFLOP/s + permute GB/s, 16^4 spin×color, 1/2/4/8 GPUs",
@@ -228,7 +233,7 @@ def main():
                          "traffic": traffic, "traffic_unit": "bytes per launch",
                          "traffic_source": traffic_src,
                          "algorithmic_bytes": 16.0 * (2 * vol(local0) + vol(gdimr)),
-                         "kernel": "gemm_z_dma_kernel<128x128x8, 8 waves> (FP64 MFMA "
+                         "kernel": "gemm_dma_kernel<complex<double>, 128x128x8, 8 waves> (FP64 MFMA "
                                    "16x16x4, complex 4M), %d launches, %.4f ms avg "
                                    "(HIP events on its launch stream)" % (gemm_calls,
                                                                           kernel_s * 1e3),
@@ -289,7 +294,112 @@ def permute_bench(sb, dev, L, n, reps=3):
     gbps = 32.0 * vol(d1) / t / 1e9
     res.update({"permute_GBps": round(gbps, 1), "permute_frac_hbm": round(gbps / PEAK_HBM_GBPS, 4),
                 "permute_ms": round(t * 1e3, 3)})
+    # the reference's second variant (tests/dist.cpp:268-300): complex<float> source copied and
+    # converted into complex<double> slices; 8 + 16 bytes per element
+    af = a.to(torch.complex64)
+
+    def run_f():
+        for k in range(n):
+            sb.copy(1.0, p0, "xyztsc", [0] * 6, d0, d0, [af], p1, "tnsxyzc", [0, k, 0, 0, 0, 0, 0],
+                    d1, [b])
+    try:
+        g2 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g2):
+            run_f()
+        t2 = timed(g2.replay)
+    except Exception:  # pragma: no cover
+        t2 = timed(run_f)
+    res["permute_cf2cd_GBps"] = round(24.0 * vol(d1) / t2 / 1e9, 1)
     return res
+
+
+def chain_bench(sb, dev, Ls=16, Lt=64, ncols=12, reps=3):
+    """configs[4] on one GPU's share (16^3 x 64 sites, = 32^3 x 64 over a 2x2x2 grid),
+    complex<float>: (1) redistribute a propagator from `tnsxyzc` into the operator's domain
+    layout `pxyztscn`, (2) apply the 9-point 12x12-block (spin 4 x color 3) BSR operator,
+    (3) contract the result with its conjugate over the lattice and color into `TSnsN`.
+    Stage times from HIP events; the ranks' exchanges are absent on one GPU."""
+    s_, c_ = 4, 3
+    dims = [Ls, Ls, Ls, Lt]
+    V = Ls * Ls * Ls * Lt
+    b = s_ * c_
+    cf = torch.complex64
+    # (1) source propagator tnsxyzc
+    dsrc = [Lt, ncols, s_, Ls, Ls, Ls, c_]
+    src = torch.empty(vol(dsrc), dtype=cf, device=dev)
+    fill_f = torch.empty(vol(dsrc), dtype=torch.complex128, device=dev)
+    fill(fill_f, 21)
+    src.copy_(fill_f)
+    del fill_f
+    dx = [1, Ls, Ls, Ls, Lt, s_, c_, ncols]
+    x = torch.empty(vol(dx), dtype=cf, device=dev)
+    y = torch.empty_like(x)
+    # (2) operator: site-major blocks, 9 neighbours (self, -+x, -+y, -+z, -+t)
+    sites = np.array(np.unravel_index(np.arange(V), dims)).T
+    jj = np.zeros((V, 9, 6), np.int32)
+    jj[:, 0, :4] = sites
+    k = 1
+    for d in range(4):
+        for sg in (-1, 1):
+            cc = sites.copy()
+            cc[:, d] = (cc[:, d] + sg) % dims[d]
+            jj[:, k, :4] = cc
+            k += 1
+    vals = torch.empty(V * 9 * b * b, dtype=cf, device=dev)
+    vals.real.uniform_(-1, 1)
+    vals.imag.uniform_(-1, 1)
+    dim = dims + [s_, c_]
+    full = [([0] * 6, dim)]
+    blk = [1, 1, 1, 1, s_, c_]
+    op = sb.create_bsr(full, dim, full, dim, blk, blk, False,
+                       [torch.full((V,), 9, dtype=torch.int32, device=dev)],
+                       [torch.from_numpy(jj.reshape(-1)).to(dev)], [vals])
+    del jj, sites
+    # (3) output of the contraction: T S n s N
+    dr = [Lt, s_, ncols, s_, ncols]
+    vr = torch.empty(vol(dr), dtype=cf, device=dev)
+    p_src, p_x, p_r = [([0] * 7, dsrc)], [([0] * 8, dx)], [([0] * 5, dr)]
+
+    def stage1():
+        sb.copy(1.0, p_src, "tnsxyzc", [0] * 7, dsrc, dsrc, [src], p_x, "pxyztscn", [0] * 8, dx,
+                [x])
+
+    def stage2():
+        sb.bsr_krylov(1.0, op, "XYZTSC", "xyztsc", p_x, "pxyztscn", [0] * 8, dx, dx, [x], 0.0,
+                      p_x, "pXYZTSCn", [0] * 8, dx, dx, "p", [y])
+
+    def stage3():
+        sb.contraction(1.0, p_x, [0] * 8, dx, dx, "pXYZTSCn", True, [y], p_x, [0] * 8, dx, dx,
+                       "pXYZTsCN", False, [y], 0.0, p_r, [0] * 5, dr, dr, "TSnsN", [vr])
+    stages = (stage1, stage2, stage3)
+    for f in stages:
+        f()
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    times = [0.0, 0.0, 0.0]
+    for _ in range(reps):
+        ev[0].record()
+        for i, f in enumerate(stages):
+            f()
+            ev[i + 1].record()
+        torch.cuda.synchronize()
+        for i in range(3):
+            times[i] += ev[i].elapsed_time(ev[i + 1]) / reps
+    op.destroy()
+    by1 = 16.0 * vol(dsrc)
+    by2 = 8.0 * (9 * b * b * V + 2 * b * V * ncols) + 4.0 * (10 * V + 1)
+    fl2 = 8.0 * 9 * b * b * V * ncols
+    fl3 = 8.0 * vol(dr) * Ls * Ls * Ls * c_
+    return {"chain_workload": "configs[4] per-GPU share: 16^3x64 sites, n=12, spin 4 x color 3, "
+                              "complex<float>; redistribute -> BSR 12x12 9-point -> contraction",
+            "chain_ms": round(sum(times), 3),
+            "chain_redistribute_ms": round(times[0], 3),
+            "chain_redistribute_GBps": round(by1 / (times[0] / 1e3) / 1e9, 1),
+            "chain_bsr_ms": round(times[1], 3),
+            "chain_bsr_GBps": round(by2 / (times[1] / 1e3) / 1e9, 1),
+            "chain_bsr_TFLOPs": round(fl2 / (times[1] / 1e3) / 1e12, 2),
+            "chain_contraction_ms": round(times[2], 3),
+            "chain_contraction_TFLOPs": round(fl3 / (times[2] / 1e3) / 1e12, 2)}
 
 
 def bsr_bench(sb, dev, L, ncols=12, reps=5):

@@ -11,12 +11,15 @@
 // Host-side normalisation (launch_box_copy):
 //   1. drop size-1 dims, sort by destination stride, merge dims contiguous on both sides;
 //   2. the leading dim contiguous on both sides becomes the run R (an "item" of R elements);
-//   3. V = the destination-fastest remaining dim, U = the chain of dims contiguous in the source
+//   3. V = the chain of dims contiguous in the destination from stride R, U = the chain of dims
+//      contiguous in the source
 //      starting at stride R; everything else is an outer dim handled by the grid;
 //   4. if U is empty the direct kernel (destination-ordered gather) is used.
 #include "sbx_internal.h"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <numeric>
 
 namespace sbx {
@@ -130,14 +133,13 @@ template <typename D> constexpr int tile_elems() { return (int)(24576 / sizeof(D
 
 struct TiledArgs {
     uint32_t R, TU, TV;     // run length, tile sizes (items)
-    uint32_t NU, NV;        // extents of the U chain (flattened) and of V
+    uint32_t NU, NV;        // extents of the U and V chains (flattened)
     FastDiv fR, fTU, fTV;   // divisors
     FastDiv fRTU, fRTV;     // R*TU, R*TV
     uint32_t ntu, ntv;      // number of tiles along U and V
-    int nu;                 // dims in the U chain
-    FastDiv usize[MAXD];
-    long usst[MAXD], udst[MAXD];
-    long vsst, vdst;        // strides of V
+    int nu, nv;             // dims in the U chain (source-contiguous) / V chain (dest-contiguous)
+    FastDiv usize[MAXD], vsize[MAXD];
+    long usst[MAXD], udst[MAXD], vsst[MAXD], vdst[MAXD];
     int nw;                 // outer dims
     FastDiv wsize[MAXD];
     long wsst[MAXD], wdst[MAXD];
@@ -146,10 +148,29 @@ struct TiledArgs {
     Alpha alpha;
 };
 
+/// Offsets of item `idx` of a chain of dims (fastest first)
+__device__ __forceinline__ void chain_offsets(uint32_t idx, int n, const FastDiv *size,
+                                              const long *sst, const long *dst, long &so,
+                                              long &doff) {
+    so = 0;
+    doff = 0;
+    for (int i = 0; i < n; ++i) {
+        const uint32_t q = size[i].div(idx);
+        const uint32_t c = idx - q * size[i].d;
+        idx = q;
+        so += (long)c * sst[i];
+        doff += (long)c * dst[i];
+    }
+}
+
+// A tile = TU items of the U chain (contiguous runs in the source) x TV items of the V chain
+// (contiguous runs in the destination), each item a run of R elements contiguous on both sides.
+// Read phase: r fastest, then u, then v (coalesced source reads); write phase: r fastest, then
+// v, then u (coalesced destination writes); the tile is transposed through LDS.
 template <typename S, typename D, bool ADD>
 __global__ void __launch_bounds__(256) copy_tiled_kernel(const TiledArgs p) {
     __shared__ D tile[tile_elems<D>() + 64];
-    __shared__ long su[256], du[256]; // per-item offsets of the U chain (TU <= 256)
+    __shared__ long su[256], du[256], sv[256], dv[256]; // per-item chain offsets of the tile
 
     const S *__restrict__ src = (const S *)p.src;
     D *__restrict__ dst = (D *)p.dstp;
@@ -170,31 +191,17 @@ __global__ void __launch_bounds__(256) copy_tiled_kernel(const TiledArgs p) {
     }
     const uint32_t u0 = tu * p.TU, v0 = tv * p.TV;
     const uint32_t nu_t = min(p.TU, p.NU - u0), nv_t = min(p.TV, p.NV - v0);
-    sbase += (long)v0 * p.vsst;
-    dbase += (long)v0 * p.vdst;
-
-    // Offsets of the U items of this tile
-    for (uint32_t u = threadIdx.x; u < nu_t; u += 256) {
-        uint32_t rem = u0 + u;
-        long so = 0, doff = 0;
-        for (int i = 0; i < p.nu; ++i) {
-            const uint32_t q = p.usize[i].div(rem);
-            const uint32_t c = rem - q * p.usize[i].d;
-            rem = q;
-            so += (long)c * p.usst[i];
-            doff += (long)c * p.udst[i];
-        }
-        su[u] = so;
-        du[u] = doff;
-    }
+    for (uint32_t u = threadIdx.x; u < nu_t; u += 256)
+        chain_offsets(u0 + u, p.nu, p.usize, p.usst, p.udst, su[u], du[u]);
+    for (uint32_t v = threadIdx.x; v < nv_t; v += 256)
+        chain_offsets(v0 + v, p.nv, p.vsize, p.vsst, p.vdst, sv[v], dv[v]);
     __syncthreads();
 
     const uint32_t ld = p.TU * p.R + 1; // padded LDS row (one row per v)
     constexpr int EPT = 4;              // elements per thread in flight
-    // Read phase: r fastest, then u (contiguous in the source), then v
     const uint32_t nread = p.R * p.TU * nv_t;
     for (uint32_t e0 = threadIdx.x; e0 < nread; e0 += 256 * EPT) {
-        D v[EPT];
+        D val[EPT];
         uint32_t li[EPT];
 #pragma unroll
         for (int q = 0; q < EPT; ++q) {
@@ -208,14 +215,13 @@ __global__ void __launch_bounds__(256) copy_tiled_kernel(const TiledArgs p) {
             // clamped (always valid) address: the loads of the EPT elements are all issued
             // before the first use instead of one branch + wait per element
             const uint32_t uc = ok ? u : 0, vc = ok ? vv : 0, rc = ok ? r : 0;
-            v[q] = conv<D, S>(src[sbase + su[uc] + (long)vc * p.vsst + rc]);
+            val[q] = conv<D, S>(src[sbase + su[uc] + sv[vc] + rc]);
         }
 #pragma unroll
         for (int q = 0; q < EPT; ++q)
-            if (li[q] != 0xffffffffu) tile[li[q]] = v[q];
+            if (li[q] != 0xffffffffu) tile[li[q]] = val[q];
     }
     __syncthreads();
-    // Write phase: r fastest, then v (contiguous in the destination), then u
     const uint32_t nwrite = p.R * p.TV * nu_t;
     for (uint32_t e0 = threadIdx.x; e0 < nwrite; e0 += 256 * EPT) {
 #pragma unroll
@@ -226,7 +232,7 @@ __global__ void __launch_bounds__(256) copy_tiled_kernel(const TiledArgs p) {
             const uint32_t vv = p.fR.div(rem);
             const uint32_t r = rem - vv * p.R;
             if (e < nwrite && vv < nv_t)
-                put<ADD, D>(dst + dbase + du[u] + (long)vv * p.vdst + r,
+                put<ADD, D>(dst + dbase + du[u] + dv[vv] + r,
                             scale<D>(tile[vv * ld + u * p.R + r], p.alpha));
         }
     }
@@ -275,7 +281,7 @@ Norm normalize(const BoxCopyDesc &d) {
 }
 
 template <typename S, typename D, bool ADD>
-void launch_pair(const BoxCopyDesc &d, const Norm &n, long total, hipStream_t stream) {
+void launch_pair(const BoxCopyDesc &d, Norm n, long total, hipStream_t stream) {
     Alpha alpha{d.alpha.re, d.alpha.im, d.alpha.is_one() ? 1 : 0};
     const S *src = (const S *)d.src;
     D *dst = (D *)d.dst;
@@ -299,30 +305,65 @@ void launch_pair(const BoxCopyDesc &d, const Norm &n, long total, hipStream_t st
         R = n.size[0];
         first = 1;
     }
-    // V: destination-fastest remaining dim; U chain: source-contiguous from stride R
-    int V = (first < nd) ? first : -1;
-    std::vector<int> U;
-    if (V >= 0 && R <= 64) {
-        long want = R;
-        std::vector<bool> used(nd, false);
-        used[V] = true;
-        for (int i = 0; i < first; ++i) used[i] = true;
-        while (true) {
+    // V chain: dims contiguous in the destination from stride R (destination order);
+    // U chain: dims contiguous in the source from stride R, not in V.  Both are capped so that a
+    // tile holds a few hundred items on each side.
+    constexpr long CHAIN_MAX = 256;
+    // a chain may take only the inner part of a dimension: split size = inner * outer
+    auto split_dim = [&](int i, long inner) {
+        n.size.push_back(n.size[i] / inner);
+        n.ss.push_back(n.ss[i] * inner);
+        n.ds.push_back(n.ds[i] * inner);
+        n.size[i] = inner;
+    };
+    auto best_divisor = [](long size, long cap) {
+        long best = 1;
+        for (long d = 2; d <= std::min(size, cap); ++d)
+            if (size % d == 0) best = d;
+        return best;
+    };
+    std::vector<int> U, Vc;
+    std::vector<bool> used(nd, false);
+    for (int i = 0; i < first; ++i) used[i] = true;
+    auto build_chain = [&](bool dst_side, std::vector<int> &chain, long start) {
+        long want = start, prod = 1;
+        while (prod < CHAIN_MAX) {
             int found = -1;
-            for (int i = 0; i < nd; ++i)
-                if (!used[i] && n.ss[i] == want) found = i;
+            for (int i = 0; i < (int)n.size.size(); ++i)
+                if (!used[i] && (dst_side ? n.ds[i] : n.ss[i]) == want) found = i;
             if (found < 0) break;
-            U.push_back(found);
+            if (prod * n.size[found] > CHAIN_MAX) {
+                const long d = best_divisor(n.size[found], CHAIN_MAX / prod);
+                if (d < 2) break;
+                split_dim(found, d);
+                used.push_back(false);
+            }
+            chain.push_back(found);
             used[found] = true;
+            prod *= n.size[found];
             want *= n.size[found];
         }
+    };
+    if (first < nd && R <= 64) {
+        build_chain(true, Vc, R);
+        if (!Vc.empty()) build_chain(false, U, R);
+        if (!Vc.empty() && U.empty()) {
+            // the source-contiguous dims went to V: start U at the smallest remaining source
+            // stride (reads of a tile then interleave across its V items, still line-complete)
+            long smin = -1;
+            for (int i = 0; i < (int)n.size.size(); ++i)
+                if (!used[i] && (smin < 0 || n.ss[i] < smin)) smin = n.ss[i];
+            if (smin > 0) build_chain(false, U, smin);
+        }
     }
-    if (V < 0 || U.empty() || n.ss[V] <= R) {
+    const int ndd = (int)n.size.size(); // dims after splits
+    if (ndd > MAXD) throw Error("copy: too many non-mergeable dimensions");
+    if (Vc.empty() || U.empty()) {
         // Direct destination-ordered gather
         DirectArgs a{};
-        a.nd = nd;
+        a.nd = ndd;
         a.total = (uint32_t)total;
-        for (int i = 0; i < nd; ++i) {
+        for (int i = 0; i < ndd; ++i) {
             a.size[i] = FastDiv((uint32_t)n.size[i]);
             a.sst[i] = n.ss[i];
             a.dst[i] = n.ds[i];
@@ -338,18 +379,20 @@ void launch_pair(const BoxCopyDesc &d, const Norm &n, long total, hipStream_t st
         return;
     }
 
+    static const bool debug = getenv("SBX_COPY_DEBUG") != nullptr; // print the tiling
     TiledArgs a{};
-    long NU = 1;
+    long NU = 1, NV = 1;
     for (int i : U) NU *= n.size[i];
-    const long NV = n.size[V];
-    // Tile sizes: contiguous runs of ~48-96 elements on both sides (>= 768 B for 16-byte
+    for (int i : Vc) NV *= n.size[i];
+    // Tile sizes: contiguous runs of >= 48 elements on both sides (>= 768 B for 16-byte
     // elements) and ~1.5K elements per workgroup so several workgroups share a CU
     const long budget = tile_elems<D>();
-    long TU = std::min(NU, std::max(1L, (48 + R - 1) / R));
-    long TV = std::min(NV, std::max(1L, budget / (R * TU)));
-    while (TU < NU && TU < 256 && R * TU * 2 * TV <= budget && R * TU < R * TV) TU *= 2;
-    TU = std::min(std::min(TU, NU), 256L);
-    TV = std::min(NV, std::max(1L, budget / (R * TU)));
+    constexpr long run_target = 48; // elements per contiguous source run of a tile row
+    // the LDS image holds TV padded rows of R*TU + 1 elements: TV * (R*TU + 1) <= budget + 64
+    const long cap = budget + 64;
+    long TU = std::min(std::min(NU, std::max(1L, (run_target + R - 1) / R)), 256L);
+    long TV = std::min(std::min(NV, std::max(1L, cap / (R * TU + 1))), 256L);
+    if (TV == NV) TU = std::min(std::min(NU, std::max(1L, (cap / TV - 1) / R)), 256L);
     if (R * TU * TV + TV > tile_elems<D>() + 64) throw Error("copy: internal tile sizing error");
     a.R = (uint32_t)R;
     a.TU = (uint32_t)TU;
@@ -369,12 +412,16 @@ void launch_pair(const BoxCopyDesc &d, const Norm &n, long total, hipStream_t st
         a.usst[k] = n.ss[U[k]];
         a.udst[k] = n.ds[U[k]];
     }
-    a.vsst = n.ss[V];
-    a.vdst = n.ds[V];
+    a.nv = (int)Vc.size();
+    for (std::size_t k = 0; k < Vc.size(); ++k) {
+        a.vsize[k] = FastDiv((uint32_t)n.size[Vc[k]]);
+        a.vsst[k] = n.ss[Vc[k]];
+        a.vdst[k] = n.ds[Vc[k]];
+    }
     long NW = 1;
     int nw = 0;
-    for (int i = first; i < nd; ++i) {
-        if (i == V || std::find(U.begin(), U.end(), i) != U.end()) continue;
+    for (int i = first; i < ndd; ++i) {
+        if (used[i]) continue;
         a.wsize[nw] = FastDiv((uint32_t)n.size[i]);
         a.wsst[nw] = n.ss[i];
         a.wdst[nw] = n.ds[i];
@@ -387,6 +434,12 @@ void launch_pair(const BoxCopyDesc &d, const Norm &n, long total, hipStream_t st
     a.alpha = alpha;
     const long blocks = (long)a.ntu * a.ntv * NW;
     if (blocks >= (1L << 31)) throw Error("copy: grid too large");
+    if (debug) {
+        std::fprintf(stderr, "copy_tiled: dims(size/ss/ds)");
+        for (int i = 0; i < ndd; ++i) std::fprintf(stderr, " %ld/%ld/%ld", n.size[i], n.ss[i], n.ds[i]);
+        std::fprintf(stderr, " | R=%ld NU=%ld NV=%ld TU=%ld TV=%ld nu=%d nv=%d nw=%d blocks=%ld\n", R,
+                     NU, NV, TU, TV, a.nu, a.nv, nw, blocks);
+    }
     KernelTimer timer("copy", stream);
     hipLaunchKernelGGL((copy_tiled_kernel<S, D, ADD>), dim3((unsigned)blocks), dim3(256), 0,
                        stream, a);

@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Time the box-copy kernel on named permutations (not part of the product):
+  slice  xyztsc -> tnsxyzc[n]        (config 2p, one slice, complex<double>)
+  big    xyztnsc -> tnsxyzc          (whole tensor, complex<double>)
+  chain  pXYZTSCn -> TSnpXYZC        (the chain's contraction operand reorder, complex<float>)
+kernel time from the library timers; SBX_COPY_DEBUG=1 prints the tiling."""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import superbblas_amd as sb  # noqa: E402
+
+
+def vol(d):
+    n = 1
+    for x in d:
+        n *= x
+    return n
+
+
+def case(name, o0, d0, o1, d1, from1, dtype, reps=10):
+    dev = torch.device("cuda:0")
+    a = torch.randn(vol(d0), dtype=dtype, device=dev)
+    b = torch.zeros(vol(d1), dtype=dtype, device=dev)
+    p0, p1 = [([0] * len(d0), d0)], [([0] * len(d1), d1)]
+
+    def f():
+        sb.copy(1.0, p0, o0, [0] * len(d0), d0, d0, [a], p1, o1, from1, d1, [b])
+    f()
+    torch.cuda.synchronize()
+    sb.timings_enable(True)
+    sb.timings_reset()
+    for _ in range(reps):
+        f()
+    torch.cuda.synchronize()
+    ms, calls = sb.timings_get("copy")
+    sb.timings_enable(False)
+    t = ms / calls / 1e3
+    es = torch.empty(0, dtype=dtype).element_size()
+    print(json.dumps({"case": name, "us": round(t * 1e6, 1),
+                      "GBps": round(2 * es * vol(d0) / t / 1e9, 1)}))
+
+
+def main():
+    L, n = 16, 64
+    case("slice", "xyztsc", [L, L, L, L, 4, 3], "tnsxyzc", [L, n, 4, L, L, L, 3],
+         [0, 5, 0, 0, 0, 0, 0], torch.complex128)
+    case("big", "xyztnsc", [L, L, L, L, n, 4, 3], "tnsxyzc", [L, n, 4, L, L, L, 3], [0] * 7,
+         torch.complex128)
+    case("redist", "tnsxyzc", [64, 12, 4, 16, 16, 16, 3], "pxyztscn",
+         [1, 16, 16, 16, 64, 4, 3, 12], [0] * 8, torch.complex64)
+    case("chain", "pXYZTSCn", [1, 16, 16, 16, 64, 4, 3, 12], "TSnpXYZC",
+         [64, 4, 12, 1, 16, 16, 16, 3], [0] * 8, torch.complex64)
+
+
+if __name__ == "__main__":
+    main()
