@@ -386,7 +386,8 @@ void launch_pair(const BoxCopyDesc &d, Norm n, long total, hipStream_t stream) {
     for (int i : Vc) NV *= n.size[i];
     // Tile sizes: contiguous runs of >= 48 elements on both sides (>= 768 B for 16-byte
     // elements) and ~1.5K elements per workgroup so several workgroups share a CU
-    const long budget = tile_elems<D>();
+    // small copies: smaller tiles so that >= ~1024 workgroups (4 per CU) share the chip
+    const long budget = std::max(256L, std::min((long)tile_elems<D>(), total / 1024));
     constexpr long run_target = 48; // elements per contiguous source run of a tile row
     // the LDS image holds TV padded rows of R*TU + 1 elements: TV * (R*TU + 1) <= budget + 64
     const long cap = budget + 64;
