@@ -26,6 +26,7 @@
 #include <complex>
 #include <cstddef>
 #include <functional>
+#include <memory>
 #include <ostream>
 #include <stdexcept>
 #include <string>
@@ -236,9 +237,77 @@ template <typename T> void deallocate(T *ptr, Context ctx) {
     sbx_context c = sbx_detail::contexts(&ctx, 1)[0];
     sbx_detail::check(sbx_deallocate((void *)ptr, c));
 }
+/// Custom allocator hooks (platform.h:117-139): assign a function to the returned reference and
+/// the library takes its device memory from it (return nullptr to fall back to hipMalloc)
+using Allocator = std::function<void *(std::size_t, enum platform)>;
+using Deallocator = std::function<void(void *, enum platform)>;
+namespace sbx_detail {
+inline Allocator &allocator_storage() {
+    static Allocator a{};
+    return a;
+}
+inline Deallocator &deallocator_storage() {
+    static Deallocator d{};
+    return d;
+}
+inline void *alloc_trampoline(unsigned long long bytes, int device, void *) {
+    Allocator &a = allocator_storage();
+    if (!a) return nullptr;
+    (void)device; // the library makes `device` current before calling
+    return a((std::size_t)bytes, GPU);
+}
+inline void free_trampoline(void *p, int, void *) {
+    Deallocator &d = deallocator_storage();
+    if (d) d(p, GPU);
+}
+inline void install_allocator_hooks() {
+    static bool done = false;
+    if (done) return;
+    done = true;
+    check(sbx_set_custom_allocator(alloc_trampoline, free_trampoline, nullptr));
+}
+} // namespace sbx_detail
+inline Allocator &getCustomAllocator() {
+    sbx_detail::install_allocator_hooks();
+    return sbx_detail::allocator_storage();
+}
+inline Deallocator &getCustomDeallocator() {
+    sbx_detail::install_allocator_hooks();
+    return sbx_detail::deallocator_storage();
+}
+
+/// A buffer of the library's scratch cache (alloc.h:428-435); returned to the cache on release
+template <typename T> std::shared_ptr<char> allocate_from_cache(std::size_t n, Context ctx) {
+    sbx_context c = sbx_detail::contexts(&ctx, 1)[0];
+    void *p = nullptr;
+    sbx_detail::check(sbx_allocate_from_cache((unsigned long long)(n * sizeof(T)), c, &p));
+    return std::shared_ptr<char>((char *)p, [c](char *q) { (void)sbx_release_to_cache(q, c); });
+}
+
+/// Scratch-cache usage per device (performance.h:436-495)
+template <typename OStream> void reportCacheUsage(OStream &s) {
+    const unsigned int n = getGpuDevicesCount();
+    for (unsigned int d = 0; d < n; ++d) {
+        unsigned long long cached = 0, live = 0;
+        sbx_detail::check(sbx_cache_usage((int)d, &cached, &live));
+        s << "superbblas_amd cache on GPU " << d << ": " << cached / 1048576.0 << " MiB idle, "
+          << live / 1048576.0 << " MiB in use" << std::endl;
+    }
+}
+/// Report scratch buffers still in use (performance.h:497-518)
+template <typename OStream> void checkForMemoryLeaks(OStream &s) {
+    const unsigned int n = getGpuDevicesCount();
+    for (unsigned int d = 0; d < n; ++d) {
+        unsigned long long cached = 0, live = 0;
+        sbx_detail::check(sbx_cache_usage((int)d, &cached, &live));
+        if (live) s << "superbblas_amd: " << live << " bytes of scratch still in use on GPU " << d
+                    << std::endl;
+    }
+}
+
 /// Kernel timings (HIP events per kernel family); enable with sbx_timings_enable(1)
 inline void resetTimings() { sbx_detail::check(sbx_timings_reset()); }
-inline void reportTimings(std::ostream &s) {
+template <typename OStream> void reportTimings(OStream &s) {
     std::vector<char> buf(1 << 16);
     sbx_detail::check(sbx_timings_report(buf.data(), (int)buf.size()));
     s << "superbblas_amd kernel timings (family calls total_ms)\n" << buf.data();

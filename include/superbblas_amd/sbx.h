@@ -78,6 +78,21 @@ int sbx_clear_handles(void);
 int sbx_allocate(unsigned long long bytes, sbx_context ctx, void **ptr);
 int sbx_deallocate(void *ptr, sbx_context ctx);
 
+/* ---- memory (getCustomAllocator / getCustomDeallocator platform.h:129-139,
+   allocate_from_cache alloc.h:428-435, reportCacheUsage / checkForMemoryLeaks
+   performance.h:436-518) ---- */
+typedef void *(*sbx_alloc_fn)(unsigned long long bytes, int device, void *user);
+typedef void (*sbx_free_fn)(void *ptr, int device, void *user);
+/* Device memory the library allocates (sbx_allocate on GPU contexts and its scratch cache) comes
+   from `alloc` / goes back to `dealloc` (both NULL: hipMalloc / hipFree).  Cached blocks of the
+   previous allocator are released first. */
+int sbx_set_custom_allocator(sbx_alloc_fn alloc, sbx_free_fn dealloc, void *user);
+/* A buffer of the library's scratch cache, ordered on the library stream of the device */
+int sbx_allocate_from_cache(unsigned long long bytes, sbx_context ctx, void **ptr);
+int sbx_release_to_cache(void *ptr, sbx_context ctx);
+/* Bytes of `device` held by the scratch cache: idle blocks and blocks in use */
+int sbx_cache_usage(int device, unsigned long long *cached, unsigned long long *live);
+
 /* ---- kernel timers (reportTimings / resetTimings, performance.h:356-518) ----
    When enabled, every GPU kernel family ("gemm", "gemm_splitk_reduce", "copy", "bsr") is
    bracketed by HIP events on the stream it is launched on; totals are summed on query. */

@@ -227,8 +227,7 @@ int sbx_clear_handles(void) {
 int sbx_allocate(unsigned long long bytes, sbx_context ctx, void **ptr) {
     return guard([&] {
         if (ctx.plat == SBX_GPU) {
-            set_device(ctx.device);
-            SBX_HIP_CHECK(hipMalloc(ptr, bytes));
+            *ptr = device_alloc(bytes, ctx.device);
         } else {
             SBX_HIP_CHECK(hipHostMalloc(ptr, bytes, hipHostMallocDefault));
         }
@@ -241,10 +240,41 @@ int sbx_deallocate(void *ptr, sbx_context ctx) {
         if (ctx.plat == SBX_GPU) {
             set_device(ctx.device);
             SBX_HIP_CHECK(hipStreamSynchronize(get_stream(ctx.device)));
-            SBX_HIP_CHECK(hipFree(ptr));
+            device_free(ptr, ctx.device);
         } else {
             SBX_HIP_CHECK(hipHostFree(ptr));
         }
+    });
+}
+
+int sbx_set_custom_allocator(sbx_alloc_fn alloc, sbx_free_fn dealloc, void *user) {
+    return guard([&] {
+        if ((alloc == nullptr) != (dealloc == nullptr))
+            throw Error("set_custom_allocator: give both functions or neither");
+        set_alloc_hooks(alloc, dealloc, user);
+    });
+}
+
+int sbx_allocate_from_cache(unsigned long long bytes, sbx_context ctx, void **ptr) {
+    return guard([&] {
+        if (ctx.plat != SBX_GPU) throw Error("allocate_from_cache: GPU contexts only");
+        *ptr = scratch_alloc(bytes, ctx.device);
+    });
+}
+
+int sbx_release_to_cache(void *ptr, sbx_context ctx) {
+    return guard([&] {
+        if (ctx.plat != SBX_GPU) throw Error("release_to_cache: GPU contexts only");
+        scratch_free(ptr, ctx.device);
+    });
+}
+
+int sbx_cache_usage(int device, unsigned long long *cached, unsigned long long *live) {
+    return guard([&] {
+        std::size_t c = 0, l = 0;
+        cache_usage(device, &c, &l);
+        if (cached) *cached = c;
+        if (live) *live = l;
     });
 }
 

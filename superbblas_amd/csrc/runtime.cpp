@@ -138,6 +138,15 @@ Cache &cache(int device) {
     if ((int)c.size() <= device) c.resize(device + 1);
     return c[device];
 }
+struct Hooks {
+    AllocHook alloc = nullptr;
+    FreeHook free = nullptr;
+    void *user = nullptr;
+};
+Hooks &hooks() {
+    static Hooks h;
+    return h;
+}
 std::size_t round_bytes(std::size_t b) {
     if (b <= 256) return 256;
     if (b < (2u << 20)) {
@@ -154,7 +163,7 @@ void release_cached(int device) {
     (void)hipDeviceSynchronize();
     for (auto &e : c.free_blocks) {
         if (e.second.ev) (void)hipEventDestroy(e.second.ev);
-        (void)hipFree(e.second.p);
+        device_free(e.second.p, device);
     }
     c.free_blocks.clear();
     c.cached_bytes = 0;
@@ -181,14 +190,81 @@ void *scratch_alloc(std::size_t bytes, int device) {
         return b.p;
     }
     void *p = nullptr;
-    if (hipMalloc(&p, rb) != hipSuccess) {
+    try {
+        p = device_alloc(rb, device);
+    } catch (const Error &) {
         // out of memory: give the cached blocks back and retry once (alloc.h:104-168)
         (void)hipGetLastError();
         release_cached(device);
-        SBX_HIP_CHECK(hipMalloc(&p, rb));
+        p = device_alloc(rb, device);
     }
     c.live[p] = rb;
     return p;
+}
+
+void set_alloc_hooks(AllocHook a, FreeHook f, void *user) {
+    std::lock_guard<std::mutex> g(g_cache_mutex);
+    // blocks obtained from the previous allocator go back to it before the switch
+    for (int d = 0; d < (int)caches().size(); ++d) {
+        (void)hipSetDevice(d);
+        release_cached(d);
+    }
+    hooks() = Hooks{a, f, user};
+}
+
+namespace {
+std::mutex g_hook_mutex;
+std::map<void *, Hooks> &hook_owned() { // blocks that came from a caller's allocator
+    static std::map<void *, Hooks> m;
+    return m;
+}
+} // namespace
+
+void *device_alloc(std::size_t bytes, int device) {
+    set_device(device);
+    const Hooks h = hooks();
+    if (h.alloc) {
+        if (void *p = h.alloc(bytes, device, h.user)) {
+            std::lock_guard<std::mutex> g(g_hook_mutex);
+            hook_owned()[p] = h;
+            return p;
+        }
+        // a null answer means "use the library's allocation" (as an empty std::function)
+    }
+    void *p = nullptr;
+    SBX_HIP_CHECK(hipMalloc(&p, bytes));
+    return p;
+}
+
+void device_free(void *p, int device) {
+    if (!p) return;
+    set_device(device);
+    Hooks h;
+    bool owned = false;
+    {
+        std::lock_guard<std::mutex> g(g_hook_mutex);
+        auto it = hook_owned().find(p);
+        if (it != hook_owned().end()) {
+            h = it->second;
+            owned = true;
+            hook_owned().erase(it);
+        }
+    }
+    if (owned) {
+        SBX_HIP_CHECK(hipDeviceSynchronize()); // the hook is not stream-ordered
+        h.free(p, device, h.user);
+        return;
+    }
+    SBX_HIP_CHECK(hipFree(p));
+}
+
+void cache_usage(int device, std::size_t *cached, std::size_t *live) {
+    std::lock_guard<std::mutex> g(g_cache_mutex);
+    Cache &c = cache(device);
+    *cached = c.cached_bytes;
+    std::size_t l = 0;
+    for (auto &e : c.live) l += e.second;
+    *live = l;
 }
 
 void scratch_free(void *p, int device) {

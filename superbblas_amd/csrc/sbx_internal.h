@@ -78,6 +78,16 @@ struct StreamOverride {
 /// Stream-ordered scratch allocation (caching allocator over hipMalloc, see runtime.cpp)
 void *scratch_alloc(std::size_t bytes, int device);
 void scratch_free(void *p, int device);
+/// Caller-provided allocator hooks (getCustomAllocator / getCustomDeallocator, platform.h:129-139):
+/// device memory the library needs comes from `alloc` when set (nullptr -> the library's own)
+typedef void *(*AllocHook)(unsigned long long bytes, int device, void *user);
+typedef void (*FreeHook)(void *p, int device, void *user);
+void set_alloc_hooks(AllocHook a, FreeHook f, void *user);
+/// Device memory through the hooks or hipMalloc / hipFree (not cached)
+void *device_alloc(std::size_t bytes, int device);
+void device_free(void *p, int device);
+/// Bytes held by the scratch cache of `device`: idle (cached) and in use (live)
+void cache_usage(int device, std::size_t *cached, std::size_t *live);
 
 /// RAII scratch buffer on a device, freed in stream order
 struct Scratch {

@@ -6,6 +6,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <sstream>
 #include <vector>
 
 using namespace superbblas;
@@ -207,6 +208,30 @@ int main() {
         deallocate(dv, gpu);
         deallocate(dii, gpu);
         deallocate(djj, gpu);
+    }
+
+    // ---- allocator hooks, cache buffers and usage reports (platform.h:129-139, alloc.h:428,
+    //      performance.h:436-518) ----
+    {
+        static int calls = 0;
+        getCustomAllocator() = [](std::size_t, enum platform) -> void * {
+            ++calls;
+            return nullptr; // fall back to the library's own device allocation
+        };
+        getCustomDeallocator() = [](void *, enum platform) {};
+        clearCaches();
+        {
+            auto buf = allocate_from_cache<Z>(1000, gpu);
+            CHECK(buf.get() != nullptr, "allocate_from_cache");
+        }
+        CHECK(calls > 0, "custom allocator consulted");
+        getCustomAllocator() = nullptr;
+        getCustomDeallocator() = nullptr;
+        std::ostringstream os;
+        reportCacheUsage(os);
+        checkForMemoryLeaks(os);
+        CHECK(os.str().find("cache on GPU 0") != std::string::npos, "reportCacheUsage output");
+        CHECK(os.str().find("still in use") == std::string::npos, "no scratch leaked");
     }
 
     // ---- error behaviour: invalid calls throw std::runtime_error (platform.h:226-243) ----
