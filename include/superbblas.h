@@ -577,6 +577,33 @@ void contraction(T alpha, const PartitionItem<Nd0> *p0, const Coor<Nd0> &from0,
         ncomponents1, o1, conj1, v1, ctx1, beta, pr, fromr, sizer, dimr, ncomponentsr, o_r, vr,
         ctxr, sbx_detail::comm_of(mpicomm, ctxr, ncomponentsr), co, request, session);
 }
+
+template <std::size_t Nd, std::size_t Ni, typename T>
+void create_bsr(const PartitionItem<Ni> *pim, const Coor<Ni> &dimi, const PartitionItem<Nd> *pdm,
+                const Coor<Nd> &dimd, int ncomponents, const Coor<Ni> &blockim,
+                const Coor<Nd> &blockdm, bool blockImFast, IndexType **ii, Coor<Nd> **jj,
+                const T **v, const Context *ctx, MPI_Comm mpicomm, CoorOrder co, BSR_handle **bsrh,
+                Session session = 0) {
+    sbx_detail::create_bsr_impl<Nd, Ni, T>(pim, dimi, pdm, dimd, ncomponents, blockim, blockdm,
+                                           blockImFast, ii, jj, v, ctx,
+                                           sbx_detail::comm_of(mpicomm, ctx, ncomponents), co,
+                                           bsrh, session);
+}
+
+template <std::size_t Nd, std::size_t Ni, std::size_t Nx, std::size_t Ny, typename T>
+void bsr_krylov(T alpha, BSR_handle *bsrh, const char *oim, const char *odm,
+                const PartitionItem<Nx> *px, int ncomponents, const char *ox,
+                const Coor<Nx> &fromx, const Coor<Nx> &sizex, const Coor<Nx> &dimx, const T **vx,
+                T beta, const PartitionItem<Ny> *py, const char *oy, const Coor<Ny> &fromy,
+                const Coor<Ny> &sizey, const Coor<Ny> &dimy, char okr, T **vy,
+                const Context *ctx, MPI_Comm mpicomm, CoorOrder co, Request *request = nullptr,
+                bool just_local = false, Session session = 0) {
+    if (just_local) throw std::runtime_error("bsr_krylov: just_local is not supported");
+    sbx_detail::bsr_krylov_impl<Nd, Ni, Nx, Ny, T>(
+        alpha, bsrh, oim, odm, px, ncomponents, ox, fromx, sizex, dimx, vx, beta, py, oy, fromy,
+        sizey, dimy, okr, vy, ctx, sbx_detail::comm_of(mpicomm, ctx, ncomponents), co, request,
+        session);
+}
 #endif // SUPERBBLAS_USE_MPI
 
 } // namespace superbblas
