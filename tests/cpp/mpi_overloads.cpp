@@ -1,0 +1,29 @@
+// Type-checks the MPI_Comm overloads of include/superbblas.h (compiled with -fsyntax-only
+// against tests/cpp/mpi_stub; see tests/test_cpu_header.py).
+#include "superbblas.h"
+
+using namespace superbblas;
+using Z = std::complex<double>;
+
+void use_mpi_overloads(MPI_Comm comm) {
+    Context gpu = createGpuContext(0);
+    const Coor<2> d{4, 4};
+    PartitionItem<2> p{Coor<2>{}, d};
+    const Z *c0 = nullptr;
+    Z *v1 = nullptr;
+    copy<2, 2, Z, Z>(1.0, &p, 1, "ab", Coor<2>{}, d, d, &c0, nullptr, &gpu, &p, 1, "ba", Coor<2>{},
+                     d, &v1, nullptr, &gpu, comm, SlowToFast, Copy);
+    const PartitionItem<1> pr{Coor<1>{}, Coor<1>{4}};
+    contraction<2, 2, 1, Z>(Z(1), &p, Coor<2>{}, d, d, 1, "ab", false, &c0, &gpu, &p, Coor<2>{},
+                            d, d, 1, "ab", true, &c0, &gpu, Z(0), &pr, Coor<1>{}, Coor<1>{4},
+                            Coor<1>{4}, 1, "a", &v1, &gpu, comm, SlowToFast);
+    IndexType *ii = nullptr;
+    Coor<2> *jj = nullptr;
+    BSR_handle *op = nullptr;
+    create_bsr<2, 2, Z>(&p, d, &p, d, 1, Coor<2>{1, 1}, Coor<2>{1, 1}, false, &ii, &jj, &c0, &gpu,
+                        comm, SlowToFast, &op);
+    const PartitionItem<3> px{Coor<3>{}, Coor<3>{4, 4, 2}};
+    bsr_krylov<2, 2, 3, 3, Z>(Z(1), op, "ab", "AB", &px, 1, "ABn", Coor<3>{}, Coor<3>{4, 4, 2},
+                              Coor<3>{4, 4, 2}, &c0, Z(0), &px, "abn", Coor<3>{}, Coor<3>{4, 4, 2},
+                              Coor<3>{4, 4, 2}, 0, &v1, &gpu, comm, SlowToFast);
+}

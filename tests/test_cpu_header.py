@@ -32,3 +32,10 @@ def test_c_abi_header_compiles_as_c():
     _compile(["gcc", "-std=c99", "-Wall", "-Werror"],
              '#include "superbblas_amd/sbx.h"\nint main(void) { return sbx_version(0, 0); }\n',
              ".c")
+
+
+def test_mpi_overloads_typecheck():
+    """The SUPERBBLAS_USE_MPI section instantiates against a declarations-only <mpi.h>."""
+    with open(os.path.join(ROOT, "tests", "cpp", "mpi_overloads.cpp")) as f:
+        _compile(["g++", "-std=c++14", "-Wall", "-DSUPERBBLAS_USE_MPI", "-I",
+                  os.path.join(ROOT, "tests", "cpp", "mpi_stub")], f.read(), ".cpp")
