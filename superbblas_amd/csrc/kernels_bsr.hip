@@ -132,7 +132,7 @@ __global__ void __launch_bounds__(256) bsr_kernel(const BsrArgs p) {
 
 constexpr int ELL_LDS_BYTES = 24576; // per workgroup: several workgroups share a CU
 
-template <typename E, int BI, int BD, bool YROW, bool XROW>
+template <typename E, int BI, int BD, int G, bool YROW, bool XROW>
 __global__ void __launch_bounds__(256) bsr_ell_kernel(const BsrArgs p, int nnz, int rb) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int BLK = BI * BD;
@@ -161,37 +161,47 @@ __global__ void __launch_bounds__(256) bsr_ell_kernel(const BsrArgs p, int nnz, 
     }
     for (int e = threadIdx.x; e < nrows * nnz; e += 256) cols[e] = p.jj[row0 * nnz + e];
     __syncthreads();
-    // 2) every thread computes the BI outputs of (block row, rhs column) pairs; the x rows of
-    //    block j+1 are fetched while block j is applied
-    const long npairs = (long)nrows * p.ncols;
+    // 2) every thread computes the BI x G outputs of a (block row, group of G rhs columns); the
+    //    x rows of block j+1 are fetched while block j is applied
+    const long ngroups = (p.ncols + G - 1) / G;
+    const long npairs = (long)nrows * ngroups;
     for (long q = threadIdx.x; q < npairs; q += 256) {
         int r;
-        long col;
+        long g;
         if (YROW) {
-            r = (int)(q / p.ncols);
-            col = q % p.ncols;
+            r = (int)(q / ngroups);
+            g = q % ngroups;
         } else {
             r = (int)(q % nrows);
-            col = q / nrows;
+            g = q / nrows;
         }
-        E acc[BI];
+        long colv[G];
 #pragma unroll
-        for (int c = 0; c < BI; ++c) acc[c] = Ops<E>::zero();
+        for (int k = 0; k < G; ++k) colv[k] = min(g * G + k, p.ncols - 1);
+        E acc[BI][G];
+#pragma unroll
+        for (int c = 0; c < BI; ++c)
+#pragma unroll
+            for (int k = 0; k < G; ++k) acc[c][k] = Ops<E>::zero();
         const int *jr = cols + r * nnz;
         const E *vr = vals + r * nnz * BLK;
-        auto fetch = [&](int d0, E *xv) {
+        auto fetch = [&](int d0, E (*xv)[G]) {
             const long d = d0 < 0 ? 0 : d0;
 #pragma unroll
             for (int e = 0; e < BD; ++e)
-                xv[e] = XROW ? x[(d + e) * p.ldx + col] : x[(d + e) + col * p.ldx];
+#pragma unroll
+                for (int k = 0; k < G; ++k)
+                    xv[e][k] = XROW ? x[(d + e) * p.ldx + colv[k]] : x[(d + e) + colv[k] * p.ldx];
         };
-        E xn[BD];
+        E xn[BD][G];
         int dn = jr[0];
         fetch(dn, xn);
         for (int j = 0; j < nnz; ++j) {
-            E xc[BD];
+            E xc[BD][G];
 #pragma unroll
-            for (int e = 0; e < BD; ++e) xc[e] = xn[e];
+            for (int e = 0; e < BD; ++e)
+#pragma unroll
+                for (int k = 0; k < G; ++k) xc[e][k] = xn[e][k];
             const int dc = dn;
             if (j + 1 < nnz) {
                 dn = jr[j + 1];
@@ -204,15 +214,21 @@ __global__ void __launch_bounds__(256) bsr_ell_kernel(const BsrArgs p, int nnz, 
 #pragma unroll
                 for (int c = 0; c < BI; ++c) {
                     const E a = p.block_im_fast ? vb[c + e * BI] : vb[c * BD + e];
-                    acc[c] = Ops<E>::fma(a, xc[e], acc[c]);
+#pragma unroll
+                    for (int k = 0; k < G; ++k) acc[c][k] = Ops<E>::fma(a, xc[e][k], acc[c][k]);
                 }
         }
 #pragma unroll
         for (int c = 0; c < BI; ++c) {
             const long img = (row0 + r) * BI + c;
-            E *yp = YROW ? y + img * p.ldy + col : y + img + col * p.ldy;
-            const E out = Ops<E>::scale(acc[c], p.alpha_re, p.alpha_im);
-            *yp = p.add ? Ops<E>::add(*yp, out) : out;
+#pragma unroll
+            for (int k = 0; k < G; ++k) {
+                const long col = g * G + k;
+                if (col >= p.ncols) break;
+                E *yp = YROW ? y + img * p.ldy + col : y + img + col * p.ldy;
+                const E out = Ops<E>::scale(acc[c][k], p.alpha_re, p.alpha_im);
+                *yp = p.add ? Ops<E>::add(*yp, out) : out;
+            }
         }
     }
 }
@@ -351,25 +367,33 @@ void launch_bsr_mfma(const BsrArgs &a, bool yrow, bool xrow, hipStream_t s) {
     SBX_HIP_CHECK(hipGetLastError());
 }
 
-template <typename E, int BI, int BD>
-void launch_ell(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_t s) {
-    const int blk_bytes = nnz * BI * BD * (int)sizeof(E);
-    int rb = std::max(1, ELL_LDS_BYTES / std::max(1, blk_bytes));
-    // about one (row, rhs) pair per thread
-    if (a.ncols <= 256) rb = (int)std::min<long>(rb, std::max(1L, 256 / a.ncols));
+template <typename E, int BI, int BD, int G>
+void launch_ell_g(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_t s, long lds_bytes) {
+    const long blk_bytes = (long)nnz * (BI * BD * (long)sizeof(E) + 4);
+    const long ngroups = (a.ncols + G - 1) / G;
+    int rb = (int)std::max(1L, lds_bytes / std::max(1L, blk_bytes));
+    // about one (row, column group) per thread
+    if (ngroups <= 256) rb = (int)std::min<long>(rb, std::max(1L, 256 / ngroups));
     const long blocks = (a.block_rows + rb - 1) / rb;
     if (blocks >= (1L << 31)) throw Error("bsr: grid too large");
-    const size_t lds = (size_t)rb * blk_bytes + (size_t)rb * nnz * sizeof(int);
+    const size_t lds = (size_t)rb * blk_bytes;
     KernelTimer timer("bsr", s);
     if (yrow && xrow)
-        hipLaunchKernelGGL((bsr_ell_kernel<E, BI, BD, true, true>), dim3(blocks), dim3(256), lds, s, a, nnz, rb);
+        hipLaunchKernelGGL((bsr_ell_kernel<E, BI, BD, G, true, true>), dim3(blocks), dim3(256), lds, s, a, nnz, rb);
     else if (yrow && !xrow)
-        hipLaunchKernelGGL((bsr_ell_kernel<E, BI, BD, true, false>), dim3(blocks), dim3(256), lds, s, a, nnz, rb);
+        hipLaunchKernelGGL((bsr_ell_kernel<E, BI, BD, G, true, false>), dim3(blocks), dim3(256), lds, s, a, nnz, rb);
     else if (!yrow && xrow)
-        hipLaunchKernelGGL((bsr_ell_kernel<E, BI, BD, false, true>), dim3(blocks), dim3(256), lds, s, a, nnz, rb);
+        hipLaunchKernelGGL((bsr_ell_kernel<E, BI, BD, G, false, true>), dim3(blocks), dim3(256), lds, s, a, nnz, rb);
     else
-        hipLaunchKernelGGL((bsr_ell_kernel<E, BI, BD, false, false>), dim3(blocks), dim3(256), lds, s, a, nnz, rb);
+        hipLaunchKernelGGL((bsr_ell_kernel<E, BI, BD, G, false, false>), dim3(blocks), dim3(256), lds, s, a, nnz, rb);
     SBX_HIP_CHECK(hipGetLastError());
+}
+
+template <typename E, int BI, int BD>
+void launch_ell(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_t s) {
+    // two rhs columns per thread (measured against 1 and 4, and 48 KB of LDS per workgroup:
+    // 16^4 3x3 n = 12: 46 us vs 51 / 61; n = 64: 191 us vs 218 / 234)
+    launch_ell_g<E, BI, BD, 2>(a, nnz, yrow, xrow, s, ELL_LDS_BYTES);
 }
 
 template <typename E, int BI, int BD>
