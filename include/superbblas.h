@@ -14,8 +14,8 @@
  *    SUPERBBLAS_USE_MPI defined, MPI_Comm overloads are provided that wrap MPI_Alltoallv.
  *  - Masks (mask0/mask1) must be null; `session` must be 0; `request` is always completed on
  *    return (as the reference's no-MPI overloads do, dist.h:3601, 3730).
- *  - Only the ContractWithDomain form of bsr_krylov and powers of one (okr size 1) are
- *    implemented; Kronecker BSR operators are not.
+ *  - Only the ContractWithDomain form of bsr_krylov is implemented (with powers over the okr
+ *    label); Kronecker BSR operators are not.
  */
 #ifndef SUPERBBLAS_AMD_SUPERBBLAS_H
 #define SUPERBBLAS_AMD_SUPERBBLAS_H

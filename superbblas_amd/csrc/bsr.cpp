@@ -9,7 +9,7 @@
 //    component runs the SpMM kernel, and the image pieces are copied/added into y.
 //  * x / y are used in place when their partition and layout already match (the common case
 //    of the lattice tests and the benchmarks); otherwise through temporaries.
-// Not yet supported (next tier): Kronecker BSR, powers > 1, contracting with
+// Not yet supported (next tier): Kronecker BSR, contracting with
 // the image side of the operator (transposed application).
 #include "plan.h"
 
@@ -220,7 +220,10 @@ void bsr_krylov(const BsrOp &op, const Scalar &alpha, const std::string &oi,
             throw Error("bsr_krylov: dimensions of the dense output tensor doesn't match");
         }
     }
-    if (power > 1) throw Error("bsr_krylov: powers larger than one are not supported yet");
+    // Powers (bsr.h:2138-2147, 2211-2247): y[.., p, ..] = alpha * A^(p+1) x; the operator must map
+    // the domain onto itself
+    if (power > 1 && (op.dimi != op.dimd || op.blocki != op.blockd))
+        throw Error("bsr_krylov: powers need an operator with the same image and domain");
     for (int i = 0; i < op.nd; ++i)
         if (op.blockd[i] > 1 && op.blockd[i] != op.dimd[i])
             throw Error("Still not supported partially blocking a dimension");
@@ -267,8 +270,9 @@ void bsr_krylov(const BsrOp &op, const Scalar &alpha, const std::string &oi,
                 ny.size.push_back(sizeC[k]);
             }
             CompPlan cp;
-            // x in place: same rank component whose range (shifted by fromx) equals nx
-            if (rk < (int)x.ranges.size())
+            // x in place: same rank component whose range (shifted by fromx) equals nx (with
+            // powers x's temporary is overwritten by every power, so x is always copied)
+            if (power == 1 && rk < (int)x.ranges.size())
                 for (int j = 0; j < (int)x.ranges[rk].size(); ++j) {
                     const Range &r = x.ranges[rk][j];
                     bool eq = true;
@@ -292,7 +296,7 @@ void bsr_krylov(const BsrOp &op, const Scalar &alpha, const std::string &oi,
                     break;
                 }
             if (!cp.xdirect) tx.ranges[rk].push_back(nx);
-            if (rk < (int)y.ranges.size())
+            if (power == 1 && rk < (int)y.ranges.size())
                 for (int j = 0; j < (int)y.ranges[rk].size(); ++j) {
                     const Range &r = y.ranges[rk][j];
                     bool eq = true;
@@ -358,39 +362,51 @@ void bsr_krylov(const BsrOp &op, const Scalar &alpha, const std::string &oi,
     if (direct_all && !beta.is_zero() && !beta.is_one())
         dist_copy(beta, y, fromy, sizey, y, fromy, false, comm);
 
-    // Local SpMM
-    for (int c = 0; c < (int)op.comps.size(); ++c) {
-        const BsrComp &bc = op.comps[c];
-        if (bc.block_rows == 0) continue;
-        BsrDesc d;
-        d.t = dtype;
-        d.block_rows = bc.block_rows;
-        d.bi = bi;
-        d.bd = bd;
-        d.ii = bc.ii;
-        d.jj = bc.jj;
-        d.v = bc.v;
-        d.block_im_fast = op.block_im_fast;
-        d.num_nnz_per_row = bc.nnz_per_row;
-        d.x = my_x[c];
-        d.x_row_major = my_lx[c].row_major;
-        d.ldx = my_lx[c].ld;
-        d.y = my_y[c];
-        d.y_row_major = my_ly[c].row_major;
-        d.ldy = my_ly[c].ld;
-        d.ncols = volC;
-        d.alpha = alpha;
-        d.add = plans[comm.rank][c].ydirect ? !beta.is_zero() : false;
-        launch_bsr(d, bc.dev);
-    }
-
-    // Copy/add the image pieces into y
-    if (need_y) {
-        if (!beta.is_zero() && !beta.is_one())
-            dist_copy(beta, y, fromy, sizey, y, fromy, false, comm);
-        Coor from0(ly.size(), 0), size0 = op.dimi;
-        size0.insert(size0.end(), sizeC.begin(), sizeC.end());
-        dist_copy(Scalar{1, 0}, ty, from0, size0, y, fromy, !beta.is_zero(), comm);
+    Coor from0(ly.size(), 0), size0 = op.dimi;
+    size0.insert(size0.end(), sizeC.begin(), sizeC.end());
+    if (need_y && !beta.is_zero() && !beta.is_one())
+        dist_copy(beta, y, fromy, sizey, y, fromy, false, comm);
+    const int power_pos = okr != 0 ? (int)y.labels.find(okr) : -1;
+    for (int pw = 0; pw < power; ++pw) {
+        // Local SpMM
+        for (int c = 0; c < (int)op.comps.size(); ++c) {
+            const BsrComp &bc = op.comps[c];
+            if (bc.block_rows == 0) continue;
+            BsrDesc d;
+            d.t = dtype;
+            d.block_rows = bc.block_rows;
+            d.bi = bi;
+            d.bd = bd;
+            d.ii = bc.ii;
+            d.jj = bc.jj;
+            d.v = bc.v;
+            d.block_im_fast = op.block_im_fast;
+            d.num_nnz_per_row = bc.nnz_per_row;
+            d.x = my_x[c];
+            d.x_row_major = my_lx[c].row_major;
+            d.ldx = my_lx[c].ld;
+            d.y = my_y[c];
+            d.y_row_major = my_ly[c].row_major;
+            d.ldy = my_ly[c].ld;
+            d.ncols = volC;
+            d.alpha = pw == 0 ? alpha : Scalar{1, 0};
+            d.add = plans[comm.rank][c].ydirect ? !beta.is_zero() : false;
+            launch_bsr(d, bc.dev);
+        }
+        // Copy/add the image pieces into y (power pw at okr = fromy[okr] + pw)
+        if (need_y) {
+            Coor fy = fromy;
+            if (power_pos >= 0)
+                fy[power_pos] = (int)normalize_coor((long)fy[power_pos] + pw, y.dim[power_pos]);
+            dist_copy(Scalar{1, 0}, ty, from0, size0, y, fy, !beta.is_zero(), comm);
+        }
+        if (pw + 1 == power) break;
+        // The next power applies the operator to this one: the image pieces, relabelled as
+        // domain coordinates, become x (with the halo of the domain partition)
+        DistTensor ty_as_x = ty;
+        ty_as_x.labels = lx;
+        Coor zx(lx.size(), 0);
+        dist_copy(Scalar{1, 0}, ty_as_x, zx, size0, tx, zx, false, comm);
     }
 }
 

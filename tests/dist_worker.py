@@ -171,6 +171,26 @@ def case_bsr(sb, comm, rank, n, dev, ncols=3):
                np.array(jg, np.int32).ravel(), allv.ravel(), False, gx, ncols, True, ref, ncols,
                True, ncols, 1.0)
     assert np.array_equal(out, ref), "bsr"
+    # powers: the second power needs the first one's halo from the neighbouring ranks
+    vx = scatter(sb, gx, dimx, px, rank, 1, dev)
+    dimy2 = [2] + dimx[1:]
+    py2 = sb.basic_partitioning("pxyztscn", dimy2, [1, 1, 1, 1, n, 1, 1, 1], "xyzt", n, 1)
+    gy2 = np.zeros(vol(dimy2), np.complex128)
+    vy2 = scatter(sb, gy2, dimy2, py2, rank, 1, dev)
+    op = sb.create_bsr(pi, dim, pd, dim, [1, 1, 1, 1, 1, 3], [1, 1, 1, 1, 1, 3], False,
+                       [torch.from_numpy(ii).to(dev)],
+                       [torch.from_numpy(np.array(jj, np.int32).ravel()).to(dev)],
+                       [torch.from_numpy(vals).to(dev)], comm=comm)
+    sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", px, "pXYZTSCn", z8, dimx, dimx, vx, 0.0, py2,
+                  "pxyztscn", z8, dimy2, dimy2, "p", vy2, comm=comm)
+    torch.cuda.synchronize()
+    op.destroy()
+    out2 = gather(gy2, dimy2, py2, 1, vy2)
+    ref2 = np.zeros_like(ref)
+    oracle_bsr(T_CDOUBLE, dim, 0, V, b, b, np.full(V, 9, np.int32),
+               np.array(jg, np.int32).ravel(), allv.ravel(), False, ref, ncols, True, ref2, ncols,
+               True, ncols, 1.0)
+    assert np.array_equal(out2, np.concatenate([ref, ref2])), "bsr powers"
 
 
 def main():

@@ -100,3 +100,40 @@ def test_bsr_lattice_types(gpu, dtype, ttype, spin, color, ncols):
     torch.cuda.synchronize()
     assert np.array_equal(ty.cpu().numpy(), yref)
     op.destroy()
+
+
+@pytest.mark.parametrize("spin,color,ncols,power", [(1, 3, 2, 3), (4, 3, 3, 2)])
+def test_bsr_powers(gpu, spin, color, ncols, power):
+    """okr powers (bsr.h:2211-2247): y[.., p, ..] = alpha A^(p+1) x + beta y[.., p, ..]."""
+    import torch
+    import superbblas_amd as sb
+    L = 4
+    dim, ii, jj, vals, nb = lattice_operator(L, spin, color)
+    b = spin * color
+    vol = L ** 4
+    g = np.arange(vol * b * ncols)
+    x = ((g % 7 - 3) + 1j * (g % 5 - 2)).astype(np.complex128)
+    y0 = ((g % 3 - 1) + 1j * (g % 2)).astype(np.complex128)
+    alpha, beta = 2.0 + 0j, -1.0 + 0j
+    # reference: repeated oracle applications; y layout pxyztscn with p = power index
+    refs, cur = [], x.copy()
+    for _ in range(power):
+        nxt = np.zeros_like(x)
+        oracle_bsr(T_CDOUBLE, dim, 0, vol, b, b, ii, jj, vals, False, cur, ncols, True, nxt, ncols,
+                   True, ncols, 1.0)
+        refs.append(nxt)
+        cur = nxt
+    yref = np.concatenate([alpha * r + beta * y0 for r in refs])
+    full = [([0] * 6, dim)]
+    op = sb.create_bsr(full, dim, full, dim, [1, 1, 1, 1, spin, color], [1, 1, 1, 1, spin, color],
+                       False, [torch.from_numpy(ii).to(gpu)], [torch.from_numpy(jj).to(gpu)],
+                       [torch.from_numpy(vals).to(gpu)])
+    dimx = [1, L, L, L, L, spin, color, ncols]
+    dimy = [power, L, L, L, L, spin, color, ncols]
+    ty = torch.from_numpy(np.concatenate([y0] * power)).to(gpu)
+    sb.bsr_krylov(alpha, op, "xyztsc", "XYZTSC", [([0] * 8, dimx)], "pXYZTSCn", [0] * 8, dimx,
+                  dimx, [torch.from_numpy(x).to(gpu)], beta, [([0] * 8, dimy)], "pxyztscn",
+                  [0] * 8, dimy, dimy, "p", [ty])
+    torch.cuda.synchronize()
+    op.destroy()
+    assert rel_err(ty.cpu().numpy(), yref) < 1e-13
