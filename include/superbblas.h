@@ -15,7 +15,7 @@
  *  - Masks (mask0/mask1) must be null; `session` must be 0; `request` is always completed on
  *    return (as the reference's no-MPI overloads do, dist.h:3601, 3730).
  *  - Only the ContractWithDomain form of bsr_krylov is implemented (with powers over the okr
- *    label); Kronecker BSR operators are not.
+ *    label, for plain and Kronecker operators).
  */
 #ifndef SUPERBBLAS_AMD_SUPERBBLAS_H
 #define SUPERBBLAS_AMD_SUPERBBLAS_H
@@ -190,6 +190,27 @@ void create_bsr_impl(const PartitionItem<Ni> *pim, const Coor<Ni> &dimi,
                          dimd.data(), ncomponents, blockim.data(), blockdm.data(),
                          blockImFast ? 1 : 0, (const int *const *)ii, jjp.data(),
                          (const void *const *)v, c.data(), comm, co_of(co), &h, 0));
+    *bsrh = reinterpret_cast<BSR_handle *>(h);
+}
+
+template <std::size_t Nd, std::size_t Ni, typename T>
+void create_kron_bsr_impl(const PartitionItem<Ni> *pim, const Coor<Ni> &dimi,
+                          const PartitionItem<Nd> *pdm, const Coor<Nd> &dimd, int ncomponents,
+                          const Coor<Ni> &blockim, const Coor<Nd> &blockdm,
+                          const Coor<Ni> &kronim, const Coor<Nd> &krondm, bool blockImFast,
+                          IndexType **ii, Coor<Nd> **jj, const T **v, const T **kronv,
+                          const Context *ctx, sbx_comm comm, CoorOrder co, BSR_handle **bsrh,
+                          Session session) {
+    check_session(session);
+    const auto c = contexts(ctx, ncomponents);
+    std::vector<const int *> jjp(ncomponents);
+    for (int i = 0; i < ncomponents; ++i) jjp[i] = reinterpret_cast<const int *>(jj[i]);
+    sbx_bsr h = nullptr;
+    check(sbx_create_kron_bsr((int)Nd, (int)Ni, dtype<T>::value, parts(pim), dimi.data(),
+                              parts(pdm), dimd.data(), ncomponents, blockim.data(),
+                              blockdm.data(), kronim.data(), krondm.data(), blockImFast ? 1 : 0,
+                              (const int *const *)ii, jjp.data(), (const void *const *)v,
+                              (const void *const *)kronv, c.data(), comm, co_of(co), &h, 0));
     *bsrh = reinterpret_cast<BSR_handle *>(h);
 }
 
@@ -448,6 +469,32 @@ void create_bsr(const PartitionItem<Ni> *pim, const Coor<Ni> &dimi, const Partit
                                            blockImFast, ii, jj, v, ctx, comm, co, bsrh, session);
 }
 
+/// create_kron_bsr (bsr.h:2476-2490): kronv[c] holds one volume(kronim) x volume(krondm) matrix
+/// per nonzero position of a block row; keep ii, jj, v and kronv allocated until destroy_bsr
+template <std::size_t Nd, std::size_t Ni, typename T>
+void create_kron_bsr(const PartitionItem<Ni> *pim, const Coor<Ni> &dimi,
+                     const PartitionItem<Nd> *pdm, const Coor<Nd> &dimd, int ncomponents,
+                     const Coor<Ni> &blockim, const Coor<Nd> &blockdm, const Coor<Ni> &kronim,
+                     const Coor<Nd> &krondm, bool blockImFast, IndexType **ii, Coor<Nd> **jj,
+                     const T **v, const T **kronv, const Context *ctx, CoorOrder co,
+                     BSR_handle **bsrh, Session session = 0) {
+    sbx_detail::create_kron_bsr_impl<Nd, Ni, T>(pim, dimi, pdm, dimd, ncomponents, blockim,
+                                                blockdm, kronim, krondm, blockImFast, ii, jj, v,
+                                                kronv, ctx, nullptr, co, bsrh, session);
+}
+
+template <std::size_t Nd, std::size_t Ni, typename T>
+void create_kron_bsr(const PartitionItem<Ni> *pim, const Coor<Ni> &dimi,
+                     const PartitionItem<Nd> *pdm, const Coor<Nd> &dimd, int ncomponents,
+                     const Coor<Ni> &blockim, const Coor<Nd> &blockdm, const Coor<Ni> &kronim,
+                     const Coor<Nd> &krondm, bool blockImFast, IndexType **ii, Coor<Nd> **jj,
+                     const T **v, const T **kronv, const Context *ctx, Communicator comm,
+                     CoorOrder co, BSR_handle **bsrh, Session session = 0) {
+    sbx_detail::create_kron_bsr_impl<Nd, Ni, T>(pim, dimi, pdm, dimd, ncomponents, blockim,
+                                                blockdm, kronim, krondm, blockImFast, ii, jj, v,
+                                                kronv, ctx, comm, co, bsrh, session);
+}
+
 inline void destroy_bsr(BSR_handle *bsrh) {
     sbx_detail::check(sbx_destroy_bsr(reinterpret_cast<sbx_bsr>(bsrh)));
 }
@@ -588,6 +635,18 @@ void create_bsr(const PartitionItem<Ni> *pim, const Coor<Ni> &dimi, const Partit
                                            blockImFast, ii, jj, v, ctx,
                                            sbx_detail::comm_of(mpicomm, ctx, ncomponents), co,
                                            bsrh, session);
+}
+
+template <std::size_t Nd, std::size_t Ni, typename T>
+void create_kron_bsr(const PartitionItem<Ni> *pim, const Coor<Ni> &dimi,
+                     const PartitionItem<Nd> *pdm, const Coor<Nd> &dimd, int ncomponents,
+                     const Coor<Ni> &blockim, const Coor<Nd> &blockdm, const Coor<Ni> &kronim,
+                     const Coor<Nd> &krondm, bool blockImFast, IndexType **ii, Coor<Nd> **jj,
+                     const T **v, const T **kronv, const Context *ctx, MPI_Comm mpicomm,
+                     CoorOrder co, BSR_handle **bsrh, Session session = 0) {
+    sbx_detail::create_kron_bsr_impl<Nd, Ni, T>(
+        pim, dimi, pdm, dimd, ncomponents, blockim, blockdm, kronim, krondm, blockImFast, ii, jj,
+        v, kronv, ctx, sbx_detail::comm_of(mpicomm, ctx, ncomponents), co, bsrh, session);
 }
 
 template <std::size_t Nd, std::size_t Ni, std::size_t Nx, std::size_t Ny, typename T>

@@ -186,6 +186,19 @@ int sbx_create_bsr(int nd, int ni, int t, const int *pim, const int *dimi, const
                    int blockImFast, const int *const *ii, const int *const *jj,
                    const void *const *v, const sbx_context *ctx, sbx_comm comm, int co,
                    sbx_bsr *bsrh, int session);
+/* create_kron_bsr (bsr.h:2476-2490 no MPI, 2322-2336 MPI): as sbx_create_bsr plus the
+   Kronecker block dimensions kronim[ni] / krondm[nd] and, per component, kronv[c]: one
+   ki x kd matrix (ki = volume(kronim), kd = volume(krondm); image index fastest if
+   blockImFast) per nonzero position of a block row; every block row must have the same number
+   of nonzero blocks and no -1 domain coordinates (get_kron_indices, bsr.h:1485-1537).
+   kronv must stay allocated until sbx_destroy_bsr.  bsr_krylov then prefers row-major x / y
+   with the Kronecker labels fastest: (D, d, C, kd) and (I, i, C, ki). */
+int sbx_create_kron_bsr(int nd, int ni, int t, const int *pim, const int *dimi, const int *pdm,
+                        const int *dimd, int ncomponents, const int *blockim, const int *blockdm,
+                        const int *kronim, const int *krondm, int blockImFast,
+                        const int *const *ii, const int *const *jj, const void *const *v,
+                        const void *const *kronv, const sbx_context *ctx, sbx_comm comm, int co,
+                        sbx_bsr *bsrh, int session);
 int sbx_bsr_krylov(sbx_bsr bsrh, int nd, int ni, int nx, int ny, int t, const double *alpha,
                    const char *oim, const char *odm, const int *px, int ncomponents,
                    const char *ox, const int *fromx, const int *sizex, const int *dimx,

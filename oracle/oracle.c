@@ -354,6 +354,69 @@ int oracle_bsr(int t, int nd, const int *dimd, int co, long block_rows, int bi, 
     return 0;
 }
 
+/*
+ * Kronecker BSR operator on one component (create_kron_bsr -> get_kron_indices
+ * bsr.h:1485-1537, builtin CPU operator bsr.h:587-648): every block row has `nnz` nonzero
+ * blocks and the nonzero at position mu of a row also carries kron[mu], a ki x kd matrix
+ * (element (a, b) at a + b*ki if block_im_fast else a*kd + b, like the blocks).
+ *   jj        nd ints per nonzero: domain coordinate of the block; the site is its linear index
+ *             over site_dim (the component's domain with blocked / Kronecker dims set to 1)
+ *   x, y      row major (site, d, col, b) and (block row, i, col, a)
+ *   y(r, i, col, a) = alpha * sum_mu sum_b K_mu(a, b) sum_d U_{r,mu}(i, d) x(site, d, col, b)
+ */
+int oracle_kron_bsr(int t, int nd, const int *site_dim, int co, long block_rows, int nnz, int bi,
+                    int bd, int ki, int kd, const int *jj, const void *v, const void *kron,
+                    int block_im_fast, const void *x, void *y, long ncols, const double *alpha,
+                    int add) {
+    long sd[64];
+    get_strides(nd, site_dim, co, sd);
+    const int cplx = is_complex(t);
+#pragma omp parallel for schedule(static)
+    for (long r = 0; r < block_rows; ++r) {
+        for (int i = 0; i < bi; ++i)
+            for (long col = 0; col < ncols; ++col)
+                for (int a = 0; a < ki; ++a) {
+                    double accr = 0, acci = 0;
+                    for (int mu = 0; mu < nnz; ++mu) {
+                        const long j = r * nnz + mu;
+                        const int *cj = jj + j * nd;
+                        long site = 0;
+                        for (int q = 0; q < nd; ++q)
+                            site += (long)normalize_coor(cj[q], site_dim[q]) * sd[q];
+                        for (int b = 0; b < kd; ++b) {
+                            double kr, kim;
+                            load(t, kron, (long)mu * ki * kd + (block_im_fast ? a + (long)b * ki
+                                                                              : (long)a * kd + b),
+                                 &kr, &kim);
+                            double sr = 0, si = 0;
+                            for (int d = 0; d < bd; ++d) {
+                                double ur, ui, xr, xi;
+                                load(t, v, j * bi * bd + (block_im_fast ? i + (long)d * bi
+                                                                        : (long)i * bd + d),
+                                     &ur, &ui);
+                                load(t, x, ((site * bd + d) * ncols + col) * kd + b, &xr, &xi);
+                                sr += ur * xr - ui * xi;
+                                si += ur * xi + ui * xr;
+                            }
+                            accr += kr * sr - kim * si;
+                            acci += kr * si + kim * sr;
+                        }
+                    }
+                    const long yi = ((r * bi + i) * ncols + col) * ki + a;
+                    double rr = alpha[0] * accr - (cplx ? alpha[1] * acci : 0);
+                    double ri = cplx ? alpha[0] * acci + alpha[1] * accr : 0;
+                    if (add) {
+                        double wr, wi;
+                        load(t, y, yi, &wr, &wi);
+                        rr += wr;
+                        ri += wi;
+                    }
+                    store(t, y, yi, rr, ri);
+                }
+    }
+    return 0;
+}
+
 int oracle_num_threads(void) {
 #ifdef _OPENMP
     return omp_get_max_threads();

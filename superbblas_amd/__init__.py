@@ -594,6 +594,27 @@ def create_bsr(pim, dimi, pdm, dimd, blockim, blockdm, block_im_fast: bool,
     return BSR(h, nd, ni, t, co, (list(ii), list(jj), list(v)))
 
 
+def create_kron_bsr(pim, dimi, pdm, dimd, blockim, blockdm, kronim, krondm, block_im_fast: bool,
+                    ii: Sequence[torch.Tensor], jj: Sequence[torch.Tensor],
+                    v: Sequence[torch.Tensor], kronv: Sequence[torch.Tensor],
+                    co: int = SlowToFast, comm: Optional[Comm] = None) -> BSR:
+    """create_kron_bsr<Nd,Ni,T> (bsr.h:2476-2490): create_bsr plus, per component, kronv[c] =
+    one volume(kronim) x volume(krondm) matrix per nonzero position of a block row."""
+    nd, ni = len(dimd), len(dimi)
+    nc = len(v)
+    h = ctypes.c_void_p()
+    t = _dtype_of(list(v) + list(kronv))
+    iip = (ctypes.c_void_p * nc)(*[x.data_ptr() for x in ii])
+    jjp = (ctypes.c_void_p * nc)(*[x.data_ptr() for x in jj])
+    _bind_stream(list(v))
+    _check(_lib.sbx_create_kron_bsr(nd, ni, t, _partition(pim, ni), _ints(dimi),
+                                    _partition(pdm, nd), _ints(dimd), nc, _ints(blockim),
+                                    _ints(blockdm), _ints(kronim), _ints(krondm),
+                                    int(block_im_fast), iip, jjp, _ptrs(v), _ptrs(kronv),
+                                    _ctxs(v), _comm(comm), co, ctypes.byref(h), 0))
+    return BSR(h, nd, ni, t, co, (list(ii), list(jj), list(v), list(kronv)))
+
+
 def bsr_krylov(alpha, bsr: BSR, oim: str, odm: str, px, ox: str, fromx, sizex, dimx, vx, beta,
                py, oy: str, fromy, sizey, dimy, okr: Optional[str], vy, co: int = SlowToFast,
                comm: Optional[Comm] = None):
@@ -621,6 +642,7 @@ def bsr_get_preferred_layout(bsr: BSR, ncomponents: int = 1, co: int = SlowToFas
 __all__ = [
     "SlowToFast", "FastToSlow", "Copy", "Add", "RowMajor", "ColumnMajor", "SuperbblasError",
     "Comm", "copy", "copy_plan", "contraction", "local_copy", "xgemm_batch_strided", "create_bsr",
+    "create_kron_bsr",
     "bsr_krylov", "bsr_get_preferred_layout", "basic_partitioning", "basic_partitioning_ext",
     "partitioning_distributed_procs", "make_hole", "sync", "stream", "set_stream",
     "clear_caches", "timings_enable", "timings_reset", "timings_get", "timings_report",

@@ -9,8 +9,11 @@
 //    component runs the SpMM kernel, and the image pieces are copied/added into y.
 //  * x / y are used in place when their partition and layout already match (the common case
 //    of the lattice tests and the benchmarks); otherwise through temporaries.
-// Not yet supported (next tier): Kronecker BSR, contracting with
-// the image side of the operator (transposed application).
+//  * Kronecker operators (create_kron_bsr, bsr.h:2476-2490) carry one ki x kd matrix per
+//    nonzero position of the block rows; x and y are then row major with the Kronecker labels
+//    fastest, (D, d, C, kd) and (I, i, C, ki), the layout the reference's planner suggests for
+//    them (bsr.h:1914-1928), and the local product runs kernels_bsr_kron.hip.
+// Not yet supported: contracting with the image side of the operator (transposed application).
 #include "plan.h"
 
 #include <algorithm>
@@ -23,12 +26,15 @@ struct BsrComp {
     int *ii = nullptr; // device CSR row pointers
     int *jj = nullptr; // device first domain index per nonzero block
     const void *v = nullptr;
+    const void *kron = nullptr; // Kronecker matrices (user memory, device)
     int nnz_per_row = -1;
 };
 
 struct BsrOp {
     int nd = 0, ni = 0, dtype = SBX_CDOUBLE;
     Coor dimi, dimd, blocki, blockd;
+    Coor kroni, krond; // all ones without Kronecker blocking
+    bool is_kron = false;
     bool block_im_fast = false;
     int nprocs = 1, rank = 0, ncomponents = 1;
     std::vector<std::vector<Range>> pi, pd; // SlowToFast, all ranks
@@ -51,8 +57,20 @@ BsrOp *bsr_create(int nd, int ni, int dtype, const std::vector<std::vector<Range
                   const Coor &blocki, const Coor &blockd, bool block_im_fast,
                   const std::vector<const int *> &ii, const std::vector<const int *> &jj,
                   const std::vector<const void *> &v, const std::vector<int> &devs, bool reverse_jj,
-                  const Comm &comm) {
+                  const Comm &comm, const Coor *kroni, const Coor *krond,
+                  const std::vector<const void *> *kronv) {
     std::unique_ptr<BsrOp> op(new BsrOp());
+    op->is_kron = kronv != nullptr;
+    op->kroni = op->is_kron ? *kroni : Coor(ni, 1);
+    op->krond = op->is_kron ? *krond : Coor(nd, 1);
+    if ((int)op->kroni.size() != ni || (int)op->krond.size() != nd)
+        throw Error("create_kron_bsr: invalid Kronecker dimensions");
+    for (int i = 0; i < nd; ++i)
+        if (blockd[i] < 1 || op->krond[i] < 1 || (blockd[i] > 1 && op->krond[i] > 1))
+            throw Error("Invalid simultaneous blocking and Kronecker blocking");
+    for (int i = 0; i < ni; ++i)
+        if (blocki[i] < 1 || op->kroni[i] < 1 || (blocki[i] > 1 && op->kroni[i] > 1))
+            throw Error("Invalid simultaneous blocking and Kronecker blocking");
     op->nd = nd;
     op->ni = ni;
     op->dtype = dtype;
@@ -66,6 +84,7 @@ BsrOp *bsr_create(int nd, int ni, int dtype, const std::vector<std::vector<Range
     op->pi = pi;
     op->pd = pd;
     const long bi = volume(blocki), bd = volume(blockd);
+    const long ki = volume(op->kroni);
     const int ncomp = (int)pi[comm.rank].size();
     op->ncomponents = ncomp;
     for (int c = 0; c < ncomp; ++c) {
@@ -73,9 +92,10 @@ BsrOp *bsr_create(int nd, int ni, int dtype, const std::vector<std::vector<Range
         bc.dev = devs[c];
         if (bc.dev < 0) throw Error("create_bsr: only GPU contexts are supported");
         const Range &ri = pi[comm.rank][c], &rd = pd[comm.rank][c];
-        const long nii = bi > 0 ? volume(ri.size) / bi : 0;
+        const long nii = bi > 0 ? volume(ri.size) / (bi * ki) : 0;
         bc.block_rows = nii;
         bc.v = v[c];
+        if (op->is_kron) bc.kron = (*kronv)[c];
         if (nii == 0 || volume(rd.size) == 0) {
             bc.block_rows = 0;
             op->comps.push_back(bc);
@@ -98,8 +118,17 @@ BsrOp *bsr_create(int nd, int ni, int dtype, const std::vector<std::vector<Range
             SBX_HIP_CHECK(hipMemcpy(hjj_coor.data(), jj[c], sizeof(int) * nnz * nd,
                                     hipMemcpyDefault));
         // linear domain index of each block (get_bsr_indices, bsr.h:1451-1459): periodic
-        // coordinates over the component's domain dims
-        const std::vector<long> st = strides_slow_to_fast(rd.size);
+        // coordinates over the component's domain dims; for Kronecker operators the index of
+        // the domain site, over the dims that are neither blocked nor Kronecker-blocked
+        // (get_kron_indices divides the linear index by bd*kd, bsr.h:1524-1527)
+        if (op->is_kron && !same)
+            throw Error("get_kron_indices: unsupported having a different number of nonzeros in "
+                        "each row");
+        Coor site_size = rd.size;
+        if (op->is_kron)
+            for (int d = 0; d < nd; ++d)
+                if (blockd[d] > 1 || op->krond[d] > 1) site_size[d] = 1;
+        const std::vector<long> st = strides_slow_to_fast(site_size);
         std::vector<int> hjj(nnz);
         bool minus_one = false;
         for (long k = 0; k < nnz; ++k) {
@@ -112,12 +141,16 @@ BsrOp *bsr_create(int nd, int ni, int dtype, const std::vector<std::vector<Range
             }
             long idx = 0;
             for (int d = 0; d < nd; ++d) {
+                if (site_size[d] == 1) continue;
                 const int coor = reverse_jj ? cc[nd - 1 - d] : cc[d];
                 idx += (long)normalize_coor(coor, rd.size[d]) * st[d];
             }
             if (idx > 0x7fffffffL) throw Error("Ups! IndexType isn't big enough");
             hjj[k] = (int)idx;
         }
+        if (minus_one && op->is_kron)
+            throw Error("get_kron_indices: unsupported nonzero pattern specification, some domain "
+                        "coordinates have -1");
         if (minus_one && !same)
             throw Error("bsr: unsupported nonzero pattern specification, some domain coordinates "
                         "have -1 but not all block rows have the same number of nonzero blocks");
@@ -222,30 +255,63 @@ void bsr_krylov(const BsrOp &op, const Scalar &alpha, const std::string &oi,
     }
     // Powers (bsr.h:2138-2147, 2211-2247): y[.., p, ..] = alpha * A^(p+1) x; the operator must map
     // the domain onto itself
-    if (power > 1 && (op.dimi != op.dimd || op.blocki != op.blockd))
-        throw Error("bsr_krylov: powers need an operator with the same image and domain");
+    if (power > 1 && (op.dimi != op.dimd || op.blocki != op.blockd || op.kroni != op.krond))
+        throw Error("When using powers the domain and the image of the sparse operator should be "
+                    "the same");
     for (int i = 0; i < op.nd; ++i)
-        if (op.blockd[i] > 1 && op.blockd[i] != op.dimd[i])
+        if ((op.blockd[i] > 1 && op.blockd[i] != op.dimd[i]) ||
+            (op.krond[i] > 1 && op.krond[i] != op.dimd[i]))
+            throw Error("Still not supported partially blocking a dimension");
+    for (int i = 0; i < op.ni; ++i)
+        if ((op.blocki[i] > 1 && op.blocki[i] != op.dimi[i]) ||
+            (op.kroni[i] > 1 && op.kroni[i] != op.dimi[i]))
             throw Error("Still not supported partially blocking a dimension");
     if (x.dtype != op.dtype || y.dtype != op.dtype) throw Error("bsr_krylov: type mismatch");
     const int dtype = op.dtype;
     const std::size_t es = dtype_size(dtype);
     const int bi = (int)volume(op.blocki), bd = (int)volume(op.blockd);
 
-    // Temporaries' layouts: row major (C fastest)
-    const std::string lx = od + C, ly = oi + C;
+    // Temporaries' layouts, row major (C fastest but for the Kronecker labels): od + C / oi + C,
+    // or (D, d, C, kd) / (I, i, C, ki) for Kronecker operators (bsr.h:1914-1928)
+    std::string lx = od + C, ly = oi + C;
+    if (op.is_kron) {
+        auto split = [&](const std::string &o, const Coor &blk, const Coor &kr) {
+            std::string S, b, k;
+            for (std::size_t i = 0; i < o.size(); ++i)
+                (blk[i] > 1 ? b : kr[i] > 1 ? k : S) += o[i];
+            return S + b + C + k;
+        };
+        lx = split(od, op.blockd, op.krond);
+        ly = split(oi, op.blocki, op.kroni);
+    }
     Coor sizeC(C.size());
     for (std::size_t k = 0; k < C.size(); ++k) sizeC[k] = sizex[x.labels.find(C[k])];
     const long volC = volume(sizeC);
+    const Coor zeroC(C.size(), 0);
+    // a coordinate in a temporary's label order from its operator-side and C-side parts
+    auto arrange = [&](const std::string &lab, const std::string &o, const Coor &opv,
+                       const Coor &cv) {
+        Coor r(lab.size());
+        for (std::size_t k = 0; k < lab.size(); ++k) {
+            const auto pos = o.find(lab[k]);
+            r[k] = pos != std::string::npos ? opv[pos] : cv[C.find(lab[k])];
+        }
+        return r;
+    };
+    // whether a user piece can be the kernel's operand as it is
+    auto operand_layout = [&](const std::string &spatial, const std::string &order,
+                              const std::string &labels, const Coor &size) {
+        if (!op.is_kron) return dense_layout(spatial, C, labels, size);
+        const Group g = group_of(order, labels, size);
+        return Layout{g.ok && (g.vol <= 1 || g.stride == 1), true, 0};
+    };
 
     // x_ / y_ in coordinates relative to the regions (domain coord d <-> x coord fromx + d)
     DistTensor tx, ty;
     tx.labels = lx;
     ty.labels = ly;
-    tx.dim = op.dimd;
-    tx.dim.insert(tx.dim.end(), sizeC.begin(), sizeC.end());
-    ty.dim = op.dimi;
-    ty.dim.insert(ty.dim.end(), sizeC.begin(), sizeC.end());
+    tx.dim = arrange(lx, od, op.dimd, sizeC);
+    ty.dim = arrange(ly, oi, op.dimi, sizeC);
     tx.dtype = ty.dtype = dtype;
     tx.ranges.resize(comm.nprocs);
     ty.ranges.resize(comm.nprocs);
@@ -262,13 +328,8 @@ void bsr_krylov(const BsrOp &op, const Scalar &alpha, const std::string &oi,
     for (int rk = 0; rk < comm.nprocs; ++rk) {
         for (int c = 0; c < (int)op.pi[rk].size(); ++c) {
             const Range &rd = op.pd[rk][c], &ri = op.pi[rk][c];
-            Range nx{rd.from, rd.size}, ny{ri.from, ri.size};
-            for (std::size_t k = 0; k < C.size(); ++k) {
-                nx.from.push_back(0);
-                nx.size.push_back(sizeC[k]);
-                ny.from.push_back(0);
-                ny.size.push_back(sizeC[k]);
-            }
+            const Range nx{arrange(lx, od, rd.from, zeroC), arrange(lx, od, rd.size, sizeC)};
+            const Range ny{arrange(ly, oi, ri.from, zeroC), arrange(ly, oi, ri.size, sizeC)};
             CompPlan cp;
             // x in place: same rank component whose range (shifted by fromx) equals nx (with
             // powers x's temporary is overwritten by every power, so x is always copied)
@@ -287,7 +348,7 @@ void bsr_krylov(const BsrOp &op, const Scalar &alpha, const std::string &oi,
                              normalize_coor((long)r.from[i] - fromx[i], x.dim[i]) == nx.from[k];
                     }
                     if (!eq) continue;
-                    Layout l = dense_layout(od, C, x.labels, r.size);
+                    Layout l = operand_layout(od, lx, x.labels, r.size);
                     if (!l.ok) continue;
                     if (comm.nprocs == 1 && rk == comm.rank && x.dev[j] != op.comps[c].dev) continue;
                     cp.xdirect = true;
@@ -311,7 +372,7 @@ void bsr_krylov(const BsrOp &op, const Scalar &alpha, const std::string &oi,
                              normalize_coor((long)r.from[i] - fromy[i], y.dim[i]) == ny.from[k];
                     }
                     if (!eq) continue;
-                    Layout l = dense_layout(oi, C, y.labels, r.size);
+                    Layout l = operand_layout(oi, ly, y.labels, r.size);
                     if (!l.ok) continue;
                     if (comm.nprocs == 1 && rk == comm.rank && y.dev[j] != op.comps[c].dev) continue;
                     // the output region must be exactly this component and no other component
@@ -362,8 +423,7 @@ void bsr_krylov(const BsrOp &op, const Scalar &alpha, const std::string &oi,
     if (direct_all && !beta.is_zero() && !beta.is_one())
         dist_copy(beta, y, fromy, sizey, y, fromy, false, comm);
 
-    Coor from0(ly.size(), 0), size0 = op.dimi;
-    size0.insert(size0.end(), sizeC.begin(), sizeC.end());
+    const Coor from0(ly.size(), 0), size0 = ty.dim;
     if (need_y && !beta.is_zero() && !beta.is_one())
         dist_copy(beta, y, fromy, sizey, y, fromy, false, comm);
     const int power_pos = okr != 0 ? (int)y.labels.find(okr) : -1;
@@ -391,7 +451,14 @@ void bsr_krylov(const BsrOp &op, const Scalar &alpha, const std::string &oi,
             d.ncols = volC;
             d.alpha = pw == 0 ? alpha : Scalar{1, 0};
             d.add = plans[comm.rank][c].ydirect ? !beta.is_zero() : false;
-            launch_bsr(d, bc.dev);
+            if (op.is_kron) {
+                d.ki = (int)volume(op.kroni);
+                d.kd = (int)volume(op.krond);
+                d.kron = bc.kron;
+                launch_bsr_kron(d, bc.dev);
+            } else {
+                launch_bsr(d, bc.dev);
+            }
         }
         // Copy/add the image pieces into y (power pw at okr = fromy[okr] + pw)
         if (need_y) {
@@ -404,7 +471,8 @@ void bsr_krylov(const BsrOp &op, const Scalar &alpha, const std::string &oi,
         // The next power applies the operator to this one: the image pieces, relabelled as
         // domain coordinates, become x (with the halo of the domain partition)
         DistTensor ty_as_x = ty;
-        ty_as_x.labels = lx;
+        for (char &ch : ty_as_x.labels)
+            if (oi.find(ch) != std::string::npos) ch = od[oi.find(ch)];
         Coor zx(lx.size(), 0);
         dist_copy(Scalar{1, 0}, ty_as_x, zx, size0, tx, zx, false, comm);
     }

@@ -16,7 +16,8 @@ BsrOp *bsr_create(int nd, int ni, int dtype, const std::vector<std::vector<Range
                   const Coor &blocki, const Coor &blockd, bool block_im_fast,
                   const std::vector<const int *> &ii, const std::vector<const int *> &jj,
                   const std::vector<const void *> &v, const std::vector<int> &devs, bool reverse_jj,
-                  const Comm &comm);
+                  const Comm &comm, const Coor *kroni = nullptr, const Coor *krond = nullptr,
+                  const std::vector<const void *> *kronv = nullptr);
 void bsr_destroy(BsrOp *op);
 void bsr_krylov(const BsrOp &op, const Scalar &alpha, const std::string &oi,
                 const std::string &od, const DistTensor &x, const Coor &fromx, const Coor &sizex,
@@ -35,6 +36,7 @@ struct sbx_bsr_s {
     sbx::BsrOp *op = nullptr;
     int co = SBX_SLOW_TO_FAST;
     int nd = 0, ni = 0, dtype = 0;
+    bool is_kron = false;
 };
 
 using namespace sbx;
@@ -530,36 +532,66 @@ int sbx_contraction(int nd0, int nd1, int ndr, int t, const double *alpha, const
     });
 }
 
-int sbx_create_bsr(int nd, int ni, int t, const int *pim, const int *dimi, const int *pdm,
+namespace {
+int create_bsr_any(int nd, int ni, int t, const int *pim, const int *dimi, const int *pdm,
                    const int *dimd, int ncomponents, const int *blockim, const int *blockdm,
-                   int blockImFast, const int *const *ii, const int *const *jj,
-                   const void *const *v, const sbx_context *ctx, sbx_comm comm, int co,
-                   sbx_bsr *bsrh, int session) {
+                   const int *kronim, const int *krondm, int blockImFast, const int *const *ii,
+                   const int *const *jj, const void *const *v, const void *const *kronv,
+                   const sbx_context *ctx, sbx_comm comm, int co, sbx_bsr *bsrh, int session) {
     return guard([&] {
         check_session(session);
+        if (!bsrh) throw Error("create_bsr: null handle output");
         const Comm c = get_comm(comm);
         const bool rev = co == SBX_FAST_TO_SLOW;
         std::vector<const int *> vii, vjj;
-        std::vector<const void *> vv;
+        std::vector<const void *> vv, vk;
         std::vector<int> devs;
         for (int i = 0; i < ncomponents; ++i) {
             vii.push_back(ii[i]);
             vjj.push_back(jj[i]);
             vv.push_back(v[i]);
+            if (kronv) vk.push_back(kronv[i]);
             if (ctx[i].plat != SBX_GPU) throw Error("create_bsr: only GPU contexts are supported");
             devs.push_back(ctx[i].device);
         }
+        const Coor ki = kronv ? to_coor(kronim, ni, rev) : Coor(), kd = kronv ? to_coor(krondm, nd, rev) : Coor();
         std::unique_ptr<sbx_bsr_s> h(new sbx_bsr_s());
         h->op = bsr_create(nd, ni, t, to_ranges(pim, ni, ncomponents, c, rev), to_coor(dimi, ni, rev),
                            to_ranges(pdm, nd, ncomponents, c, rev), to_coor(dimd, nd, rev),
                            to_coor(blockim, ni, rev), to_coor(blockdm, nd, rev), blockImFast != 0,
-                           vii, vjj, vv, devs, rev, c);
+                           vii, vjj, vv, devs, rev, c, kronv ? &ki : nullptr,
+                           kronv ? &kd : nullptr, kronv ? &vk : nullptr);
         h->co = co;
         h->nd = nd;
         h->ni = ni;
         h->dtype = t;
+        h->is_kron = kronv != nullptr;
         *bsrh = h.release();
     });
+}
+} // namespace
+
+int sbx_create_bsr(int nd, int ni, int t, const int *pim, const int *dimi, const int *pdm,
+                   const int *dimd, int ncomponents, const int *blockim, const int *blockdm,
+                   int blockImFast, const int *const *ii, const int *const *jj,
+                   const void *const *v, const sbx_context *ctx, sbx_comm comm, int co,
+                   sbx_bsr *bsrh, int session) {
+    return create_bsr_any(nd, ni, t, pim, dimi, pdm, dimd, ncomponents, blockim, blockdm, nullptr,
+                          nullptr, blockImFast, ii, jj, v, nullptr, ctx, comm, co, bsrh, session);
+}
+
+int sbx_create_kron_bsr(int nd, int ni, int t, const int *pim, const int *dimi, const int *pdm,
+                        const int *dimd, int ncomponents, const int *blockim, const int *blockdm,
+                        const int *kronim, const int *krondm, int blockImFast,
+                        const int *const *ii, const int *const *jj, const void *const *v,
+                        const void *const *kronv, const sbx_context *ctx, sbx_comm comm, int co,
+                        sbx_bsr *bsrh, int session) {
+    if (!kronv || !kronim || !krondm) {
+        g_last_error = "create_kron_bsr: null Kronecker values or dimensions";
+        return SBX_ERROR;
+    }
+    return create_bsr_any(nd, ni, t, pim, dimi, pdm, dimd, ncomponents, blockim, blockdm, kronim,
+                          krondm, blockImFast, ii, jj, v, kronv, ctx, comm, co, bsrh, session);
 }
 
 int sbx_bsr_krylov(sbx_bsr bsrh, int nd, int ni, int nx, int ny, int t, const double *alpha,

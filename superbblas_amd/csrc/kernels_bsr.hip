@@ -15,6 +15,7 @@
 //    then every thread computes all `bi` outputs of one (block row, rhs column) pair reading the
 //    blocks from LDS (broadcast across the rhs lanes) and x from global memory (contiguous along
 //    the rhs for row-major x).
+#include "elem_ops.h"
 #include "sbx_internal.h"
 
 #include <algorithm>
@@ -37,46 +38,6 @@ struct BsrArgs {
     long ncols;
     double alpha_re, alpha_im;
     int add;
-};
-
-template <typename E> struct Ops;
-template <> struct Ops<double2> {
-    static __device__ __forceinline__ double2 zero() { return double2{0, 0}; }
-    static __device__ __forceinline__ double2 fma(double2 a, double2 b, double2 c) {
-        return double2{c.x + a.x * b.x - a.y * b.y, c.y + a.x * b.y + a.y * b.x};
-    }
-    static __device__ __forceinline__ double2 scale(double2 v, double ar, double ai) {
-        return double2{ar * v.x - ai * v.y, ar * v.y + ai * v.x};
-    }
-    static __device__ __forceinline__ double2 add(double2 a, double2 b) {
-        return double2{a.x + b.x, a.y + b.y};
-    }
-};
-template <> struct Ops<float2> {
-    static __device__ __forceinline__ float2 zero() { return float2{0, 0}; }
-    static __device__ __forceinline__ float2 fma(float2 a, float2 b, float2 c) {
-        return float2{c.x + a.x * b.x - a.y * b.y, c.y + a.x * b.y + a.y * b.x};
-    }
-    static __device__ __forceinline__ float2 scale(float2 v, double ar, double ai) {
-        return float2{(float)ar * v.x - (float)ai * v.y, (float)ar * v.y + (float)ai * v.x};
-    }
-    static __device__ __forceinline__ float2 add(float2 a, float2 b) {
-        return float2{a.x + b.x, a.y + b.y};
-    }
-};
-template <> struct Ops<double> {
-    static __device__ __forceinline__ double zero() { return 0; }
-    static __device__ __forceinline__ double fma(double a, double b, double c) { return c + a * b; }
-    static __device__ __forceinline__ double scale(double v, double ar, double) { return ar * v; }
-    static __device__ __forceinline__ double add(double a, double b) { return a + b; }
-};
-template <> struct Ops<float> {
-    static __device__ __forceinline__ float zero() { return 0; }
-    static __device__ __forceinline__ float fma(float a, float b, float c) { return c + a * b; }
-    static __device__ __forceinline__ float scale(float v, double ar, double) {
-        return (float)ar * v;
-    }
-    static __device__ __forceinline__ float add(float a, float b) { return a + b; }
 };
 
 template <typename E, int BI_, int BD_, bool YROW, bool XROW>

@@ -1,0 +1,317 @@
+// Kronecker BSR operator times dense tensor (the Wilson-type stencil: a color block per
+// direction times a spin matrix shared by all sites of that direction).
+//
+// Reference: create_kron_bsr (bsr.h:2476-2490), get_kron_indices (bsr.h:1485-1537), the builtin
+// CPU operator (bsr.h:587-648) and BSR<Gpu>::contract_kron_cols + hipsparseXbsrmm
+// (bsr.h:933-998, 1001-1029):
+//   y(I, i, n, a) = alpha * sum_mu sum_b K_mu(a, b) sum_d U_{I,mu}(i, d) x(J(I,mu), d, n, b)
+// with mu the position of the nonzero within its block row (every row has the same count).
+// Layout (row major, SlowToFast): x (site, d, n, b), y (site, i, n, a): one thread per
+// (block row, rhs column) owns the bi*ki outputs of that pair, reads bd*kd contiguous x values
+// per neighbour (consecutive lanes -> consecutive rhs columns -> contiguous 16*kd-byte pieces),
+// and the spin matrix K_mu is wave-uniform (scalar loads; zero entries -- half of a Wilson
+// projector -- are skipped with a scalar branch).
+#include "elem_ops.h"
+#include "sbx_internal.h"
+
+#include <algorithm>
+
+namespace sbx {
+namespace {
+
+struct KronArgs {
+    long block_rows;
+    int nnz; ///< nonzero blocks per block row
+    int bi, bd, ki, kd;
+    const int *jj; ///< domain site of nonzero r*nnz + mu
+    const void *v;
+    const void *kron;
+    int block_im_fast;
+    const void *x;
+    void *y;
+    long ncols;
+    double alpha_re, alpha_im;
+    int add;
+};
+
+template <typename E, int BI, int BD, int KI, int KD>
+__global__ void __launch_bounds__(256) bsr_kron_kernel(const KronArgs p) {
+    const E *__restrict__ v = (const E *)p.v;
+    const E *__restrict__ kron = (const E *)p.kron;
+    const E *__restrict__ x = (const E *)p.x;
+    E *__restrict__ y = (E *)p.y;
+    const long total = p.block_rows * p.ncols;
+    const long xsite = (long)BD * p.ncols * KD, xrow = p.ncols * KD;
+    for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256L) {
+        const long c = idx % p.ncols, r = idx / p.ncols;
+        E acc[BI][KI];
+#pragma unroll
+        for (int i = 0; i < BI; ++i)
+#pragma unroll
+            for (int a = 0; a < KI; ++a) acc[i][a] = Ops<E>::zero();
+        for (int mu = 0; mu < p.nnz; ++mu) {
+            const long j = r * p.nnz + mu;
+            const E *xs = x + p.jj[j] * xsite + c * KD;
+            E xv[BD][KD];
+#pragma unroll
+            for (int d = 0; d < BD; ++d)
+#pragma unroll
+                for (int b = 0; b < KD; ++b) xv[d][b] = xs[d * xrow + b];
+            // spin first: xk(d, a) = sum_b K_mu(a, b) x(d, b)
+            const E *K = kron + (long)mu * KI * KD;
+            E xk[BD][KI];
+#pragma unroll
+            for (int d = 0; d < BD; ++d)
+#pragma unroll
+                for (int a = 0; a < KI; ++a) xk[d][a] = Ops<E>::zero();
+#pragma unroll
+            for (int a = 0; a < KI; ++a)
+#pragma unroll
+                for (int b = 0; b < KD; ++b) {
+                    const E k = p.block_im_fast ? K[a + b * KI] : K[a * KD + b];
+                    if (!Ops<E>::nonzero(k)) continue;
+#pragma unroll
+                    for (int d = 0; d < BD; ++d) xk[d][a] = Ops<E>::fma(k, xv[d][b], xk[d][a]);
+                }
+            // color: acc(i, a) += sum_d U(i, d) xk(d, a)
+            const E *U = v + j * BI * BD;
+#pragma unroll
+            for (int i = 0; i < BI; ++i)
+#pragma unroll
+                for (int d = 0; d < BD; ++d) {
+                    const E u = p.block_im_fast ? U[i + d * BI] : U[i * BD + d];
+#pragma unroll
+                    for (int a = 0; a < KI; ++a) acc[i][a] = Ops<E>::fma(u, xk[d][a], acc[i][a]);
+                }
+        }
+        E *ys = y + (r * BI * p.ncols + c) * KI;
+#pragma unroll
+        for (int i = 0; i < BI; ++i)
+#pragma unroll
+            for (int a = 0; a < KI; ++a) {
+                E o = Ops<E>::scale(acc[i][a], p.alpha_re, p.alpha_im);
+                if (p.add) o = Ops<E>::add(o, ys[i * p.ncols * KI + a]);
+                ys[i * p.ncols * KI + a] = o;
+            }
+    }
+}
+
+/// Wave-uniform element load through the constant address space (scalar loads into SGPRs)
+template <typename R> using ConstPtr = const __attribute__((address_space(4))) R *;
+template <typename E> struct Uniform {
+    static __device__ __forceinline__ E load(const E *p, long i) {
+        return ((ConstPtr<E>)p)[i];
+    }
+};
+template <> struct Uniform<double2> {
+    static __device__ __forceinline__ double2 load(const double2 *p, long i) {
+        const ConstPtr<double> q = (ConstPtr<double>)p;
+        return double2{q[2 * i], q[2 * i + 1]};
+    }
+};
+template <> struct Uniform<float2> {
+    static __device__ __forceinline__ float2 load(const float2 *p, long i) {
+        const ConstPtr<float> q = (ConstPtr<float>)p;
+        return float2{q[2 * i], q[2 * i + 1]};
+    }
+};
+
+/// Many rhs columns: a workgroup owns `S` consecutive block rows x up to 256 columns; the color
+/// blocks of its rows (S * NNZ * BI * BD values, contiguous in memory) and their domain sites are
+/// staged in LDS with coalesced loads (instead of every lane of a row fetching the same 9 blocks
+/// through L1), the spin matrices are read through the constant address space so that they live
+/// in SGPRs (wave-uniform operands of the FMAs), and the x values of the next nonzero are loaded
+/// while the current one is being applied (the loop over the NNZ nonzeros is unrolled).
+template <typename E, int BI, int BD, int KI, int KD, int NNZ>
+__global__ void __launch_bounds__(256) bsr_kron_lds_kernel(const KronArgs p, int S, int cpg) {
+    extern __shared__ char smem[];
+    constexpr int BLK = BI * BD * NNZ;
+    E *Us = (E *)smem;
+    int *Js = (int *)(Us + (long)S * BLK);
+    const E *__restrict__ v = (const E *)p.v;
+    const E *kron = (const E *)p.kron;
+    const E *__restrict__ x = (const E *)p.x;
+    E *__restrict__ y = (E *)p.y;
+    // consecutive chunks of block rows on one XCD: neighbouring sites share x lines in its L2
+    const int nwg = gridDim.x * gridDim.y, bid = blockIdx.x + blockIdx.y * gridDim.x;
+    const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    const int gx = wg % gridDim.x, gy = wg / gridDim.x;
+    const long r0 = (long)gx * S;
+    const int nrows = (int)std::min<long>(S, p.block_rows - r0);
+    {
+        const E *src = v + r0 * BLK;
+        for (int e = threadIdx.x; e < nrows * BLK; e += 256) Us[e] = src[e];
+        const int *jsrc = p.jj + r0 * NNZ;
+        for (int e = threadIdx.x; e < nrows * NNZ; e += 256) Js[e] = jsrc[e];
+    }
+    __syncthreads();
+    const int sl = threadIdx.x / cpg;
+    const long c = (long)gy * cpg + threadIdx.x % cpg;
+    if (sl >= nrows || c >= p.ncols) return;
+    const long r = r0 + sl;
+    const long xsite = (long)BD * p.ncols * KD, xrow = p.ncols * KD;
+    const E *xc = x + c * KD;
+    E acc[BI][KI];
+#pragma unroll
+    for (int i = 0; i < BI; ++i)
+#pragma unroll
+        for (int a = 0; a < KI; ++a) acc[i][a] = Ops<E>::zero();
+    const E *Ur = Us + sl * BLK;
+    const int *Jr = Js + sl * NNZ;
+    E xa[BD][KD];
+    {
+        const E *xs = xc + Jr[0] * xsite;
+#pragma unroll
+        for (int d = 0; d < BD; ++d)
+#pragma unroll
+            for (int b = 0; b < KD; ++b) xa[d][b] = xs[d * xrow + b];
+    }
+#pragma unroll 1
+    for (int mu = 0; mu < NNZ; ++mu) {
+        E xb[BD][KD];
+        if (mu + 1 < NNZ) {
+            const E *xs = xc + Jr[mu + 1] * xsite;
+#pragma unroll
+            for (int d = 0; d < BD; ++d)
+#pragma unroll
+                for (int b = 0; b < KD; ++b) xb[d][b] = xs[d * xrow + b];
+        }
+        const E *K = kron + mu * KI * KD;
+        const E *U = Ur + mu * BI * BD;
+#pragma unroll
+        for (int d = 0; d < BD; ++d) {
+            // spin: xk(a) = sum_b K_mu(a, b) x(d, b)
+            E xk[KI];
+#pragma unroll
+            for (int a = 0; a < KI; ++a) {
+                xk[a] = Ops<E>::zero();
+#pragma unroll
+                for (int b = 0; b < KD; ++b)
+                    xk[a] = Ops<E>::fma(
+                        Uniform<E>::load(K, p.block_im_fast ? a + b * KI : a * KD + b), xa[d][b],
+                        xk[a]);
+            }
+            // color: acc(i, a) += U(i, d) xk(a)
+#pragma unroll
+            for (int i = 0; i < BI; ++i) {
+                const E u = p.block_im_fast ? U[i + d * BI] : U[i * BD + d];
+#pragma unroll
+                for (int a = 0; a < KI; ++a) acc[i][a] = Ops<E>::fma(u, xk[a], acc[i][a]);
+            }
+        }
+        if (mu + 1 < NNZ) {
+#pragma unroll
+            for (int d = 0; d < BD; ++d)
+#pragma unroll
+                for (int b = 0; b < KD; ++b) xa[d][b] = xb[d][b];
+        }
+    }
+    E *ys = y + (r * BI * p.ncols + c) * KI;
+#pragma unroll
+    for (int i = 0; i < BI; ++i)
+#pragma unroll
+        for (int a = 0; a < KI; ++a) {
+            E o = Ops<E>::scale(acc[i][a], p.alpha_re, p.alpha_im);
+            if (p.add) o = Ops<E>::add(o, ys[i * p.ncols * KI + a]);
+            ys[i * p.ncols * KI + a] = o;
+        }
+}
+
+/// Any block / Kronecker sizes: one thread per output element (block row, i, column, a)
+template <typename E>
+__global__ void __launch_bounds__(256) bsr_kron_generic_kernel(const KronArgs p) {
+    const E *__restrict__ v = (const E *)p.v;
+    const E *__restrict__ kron = (const E *)p.kron;
+    const E *__restrict__ x = (const E *)p.x;
+    E *__restrict__ y = (E *)p.y;
+    const long total = p.block_rows * p.bi * p.ncols * p.ki;
+    for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256L) {
+        const int a = (int)(idx % p.ki);
+        long t = idx / p.ki;
+        const long c = t % p.ncols;
+        t /= p.ncols;
+        const int i = (int)(t % p.bi);
+        const long r = t / p.bi;
+        E acc = Ops<E>::zero();
+        for (int mu = 0; mu < p.nnz; ++mu) {
+            const long j = r * p.nnz + mu;
+            const E *xs = x + (long)p.jj[j] * p.bd * p.ncols * p.kd + c * p.kd;
+            const E *K = kron + (long)mu * p.ki * p.kd;
+            const E *U = v + j * p.bi * p.bd;
+            for (int b = 0; b < p.kd; ++b) {
+                const E k = p.block_im_fast ? K[a + b * p.ki] : K[a * p.kd + b];
+                if (!Ops<E>::nonzero(k)) continue;
+                E s = Ops<E>::zero();
+                for (int d = 0; d < p.bd; ++d) {
+                    const E u = p.block_im_fast ? U[i + d * p.bi] : U[i * p.bd + d];
+                    s = Ops<E>::fma(u, xs[d * p.ncols * p.kd + b], s);
+                }
+                acc = Ops<E>::fma(k, s, acc);
+            }
+        }
+        E o = Ops<E>::scale(acc, p.alpha_re, p.alpha_im);
+        if (p.add) o = Ops<E>::add(o, y[idx]);
+        y[idx] = o;
+    }
+}
+
+constexpr long KRON_LDS_BYTES = 64 * 1024;
+
+template <typename E> void launch_kron_typed(const KronArgs &a, hipStream_t s) {
+    KernelTimer timer("bsr", s);
+    const long row_bytes = (long)a.nnz * (a.bi * a.bd * sizeof(E) + sizeof(int));
+    if (a.bi == 3 && a.bd == 3 && a.ki == 4 && a.kd == 4 && a.nnz == 9 && a.ncols >= 4 &&
+        row_bytes * (256 / std::min<long>(a.ncols, 256)) <= KRON_LDS_BYTES) {
+        const int cpg = (int)std::min<long>(a.ncols, 256);
+        const int S = 256 / cpg;
+        const dim3 grid((unsigned)((a.block_rows + S - 1) / S), (unsigned)((a.ncols + cpg - 1) / cpg));
+        hipLaunchKernelGGL((bsr_kron_lds_kernel<E, 3, 3, 4, 4, 9>), grid, dim3(256),
+                           (size_t)(row_bytes * S), s, a, S, cpg);
+    } else if (a.bi == 3 && a.bd == 3 && a.ki == 4 && a.kd == 4) {
+        const long total = a.block_rows * a.ncols;
+        const long blocks = std::min((total + 255) / 256, 65536L);
+        hipLaunchKernelGGL((bsr_kron_kernel<E, 3, 3, 4, 4>), dim3(blocks), dim3(256), 0, s, a);
+    } else {
+        const long total = a.block_rows * a.bi * a.ncols * a.ki;
+        const long blocks = std::min((total + 255) / 256, 65536L);
+        hipLaunchKernelGGL((bsr_kron_generic_kernel<E>), dim3(blocks), dim3(256), 0, s, a);
+    }
+    SBX_HIP_CHECK(hipGetLastError());
+}
+
+} // namespace
+
+void launch_bsr_kron(const BsrDesc &d, int device) {
+    if (d.block_rows == 0 || d.ncols == 0) return;
+    if (d.num_nnz_per_row <= 0 || !d.kron || !d.x_row_major || !d.y_row_major)
+        throw Error("kron bsr: internal error (layout or pattern)");
+    set_device(device);
+    hipStream_t s = get_stream(device);
+    KronArgs a{};
+    a.block_rows = d.block_rows;
+    a.nnz = d.num_nnz_per_row;
+    a.bi = d.bi;
+    a.bd = d.bd;
+    a.ki = d.ki;
+    a.kd = d.kd;
+    a.jj = d.jj;
+    a.v = d.v;
+    a.kron = d.kron;
+    a.block_im_fast = d.block_im_fast ? 1 : 0;
+    a.x = d.x;
+    a.y = d.y;
+    a.ncols = d.ncols;
+    a.alpha_re = d.alpha.re;
+    a.alpha_im = d.alpha.im;
+    a.add = d.add ? 1 : 0;
+    switch (d.t) {
+    case SBX_CDOUBLE: return launch_kron_typed<double2>(a, s);
+    case SBX_CFLOAT: return launch_kron_typed<float2>(a, s);
+    case SBX_DOUBLE: return launch_kron_typed<double>(a, s);
+    case SBX_FLOAT: return launch_kron_typed<float>(a, s);
+    default: throw Error("kron bsr: unsupported type");
+    }
+}
+
+} // namespace sbx

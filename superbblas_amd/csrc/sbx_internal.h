@@ -192,7 +192,12 @@ struct BsrDesc {
     long ncols;
     Scalar alpha;
     bool add; ///< y += (instead of y =)
+    // Kronecker BSR (bsr.h:587-621): kron != nullptr; x is (site, bd, ncols, kd) and y is
+    // (block row, bi, ncols, ki), both row major; jj holds the domain site of each nonzero
+    int ki = 1, kd = 1;
+    const void *kron = nullptr; ///< num_nnz_per_row matrices of ki x kd
 };
 void launch_bsr(const BsrDesc &d, int device);
+void launch_bsr_kron(const BsrDesc &d, int device);
 
 } // namespace sbx

@@ -86,6 +86,22 @@ def oracle_bsr(t, dimd, co, block_rows, bi, bd, ii, jj, v, block_im_fast, x, ldx
     assert rc == 0
 
 
+def oracle_kron_bsr(t, site_dim, co, block_rows, nnz, bi, bd, ki, kd, jj, v, kron, block_im_fast,
+                    x, y, ncols, alpha, add=False):
+    """Kronecker BSR on one component, x (site, d, col, b) and y (row, i, col, a) row major."""
+    o = oracle()
+    o.oracle_kron_bsr.argtypes = [
+        ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_int,
+        ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+        ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long,
+        ctypes.c_void_p, ctypes.c_int]
+    rc = o.oracle_kron_bsr(t, len(site_dim), ctypes.cast(ints(site_dim), ctypes.c_void_p), co,
+                           block_rows, nnz, bi, bd, ki, kd, ptr(jj), ptr(v), ptr(kron),
+                           int(block_im_fast), ptr(x), ptr(y), ncols,
+                           ctypes.cast(scal(alpha), ctypes.c_void_p), int(add))
+    assert rc == 0
+
+
 def int_valued(n, dtype, seed=0):
     """Small integer-valued data (exact in every supported type)."""
     i = np.arange(n, dtype=np.int64) + seed * 7919

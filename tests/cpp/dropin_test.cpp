@@ -205,6 +205,53 @@ int main() {
         destroy_bsr(op);
         deallocate(vx, gpu);
         deallocate(vy, gpu);
+
+        // the same stencil as a Kronecker operator: color blocks times one 4x4 spin matrix per
+        // direction (create_kron_bsr, bsr.h:2476-2490); x pXYZTCnS -> y pxyztcns
+        {
+            const int sp = 4;
+            const Coor<6> kdim{L, L, L, L, sp, c};
+            std::vector<Z> hk(9 * sp * sp);
+            for (long i = 0; i < (long)hk.size(); ++i) hk[i] = val(i, 7);
+            Z *dk = upload<1>(hk, Coor<1>{(int)hk.size()}, "i");
+            const Z *ck = dk;
+            PartitionItem<6> pk{Coor<6>{}, kdim};
+            const Coor<6> kron{1, 1, 1, 1, sp, 1};
+            create_kron_bsr<6, 6, Z>(&pk, kdim, &pk, kdim, 1, block, block, kron, kron, false,
+                                     &dii, &djj, &cv, &ck, &gpu, SlowToFast, &op);
+            const Coor<8> kx{1, L, L, L, L, c, nc, sp};
+            std::vector<Z> hkx(vol(kx)), hky(vol(kx), Z(0));
+            for (long i = 0; i < vol(kx); ++i) hkx[i] = val(i, 5);
+            Z *kvx = upload<8>(hkx, kx, "pXYZTCnS"), *kvy = upload<8>(hky, kx, "pxyztcns");
+            PartitionItem<8> pkx{Coor<8>{}, kx};
+            const Z *ckx = kvx;
+            bsr_krylov<6, 6, 8, 8, Z>(Z(1), op, "xyztsc", "XYZTSC", &pkx, 1, "pXYZTCnS", {{}},
+                                      kx, kx, &ckx, Z(0), &pkx, "pxyztcns", {{}}, kx, kx, 'p',
+                                      &kvy, &gpu, SlowToFast);
+            auto kout = download<8>(kvy, kx, "pxyztcns");
+            bool kok = true;
+            for (long r = 0; r < V; ++r)
+                for (int i = 0; i < c; ++i)
+                    for (int col = 0; col < nc; ++col)
+                        for (int a = 0; a < sp; ++a) {
+                            Z acc = 0;
+                            for (int k = 0; k < 9; ++k) {
+                                const Coor<6> &q = jj[r * 9 + k];
+                                const long site = ((q[0] * L + q[1]) * L + q[2]) * L + q[3];
+                                for (int b = 0; b < sp; ++b)
+                                    for (int j = 0; j < c; ++j)
+                                        acc += hk[(k * sp + a) * sp + b] *
+                                               hv[((r * 9 + k) * c + i) * c + j] *
+                                               hkx[((site * c + j) * nc + col) * sp + b];
+                            }
+                            kok &= kout[((r * c + i) * nc + col) * sp + a] == acc;
+                        }
+            CHECK(kok, "bsr_krylov Kronecker stencil");
+            destroy_bsr(op);
+            deallocate(kvx, gpu);
+            deallocate(kvy, gpu);
+            deallocate(dk, gpu);
+        }
         deallocate(dv, gpu);
         deallocate(dii, gpu);
         deallocate(djj, gpu);

@@ -22,6 +22,9 @@ void use_mpi_overloads(MPI_Comm comm) {
     BSR_handle *op = nullptr;
     create_bsr<2, 2, Z>(&p, d, &p, d, 1, Coor<2>{1, 1}, Coor<2>{1, 1}, false, &ii, &jj, &c0, &gpu,
                         comm, SlowToFast, &op);
+    create_kron_bsr<2, 2, Z>(&p, d, &p, d, 1, Coor<2>{1, 1}, Coor<2>{1, 1}, Coor<2>{1, 1},
+                             Coor<2>{1, 1}, false, &ii, &jj, &c0, &c0, &gpu, comm, SlowToFast,
+                             &op);
     const PartitionItem<3> px{Coor<3>{}, Coor<3>{4, 4, 2}};
     bsr_krylov<2, 2, 3, 3, Z>(Z(1), op, "ab", "AB", &px, 1, "ABn", Coor<3>{}, Coor<3>{4, 4, 2},
                               Coor<3>{4, 4, 2}, &c0, Z(0), &px, "abn", Coor<3>{}, Coor<3>{4, 4, 2},

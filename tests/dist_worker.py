@@ -10,7 +10,9 @@ Cases (all multi-rank: the exchange, pack/unpack kernels and reductions run for 
             output on rank 0 (cross-rank reduction) and output split over t with beta != 0
             [dist.h:3092-3196]
   bsr    -- 9-point stencil operator split over t with a halo domain partition, x split over t,
-            y split over t  [bsr.h:2107-2266]
+            y split over t, one power and two  [bsr.h:2107-2266]
+  kron   -- the same stencil as a Kronecker operator (color blocks x spin matrices), two powers
+            [bsr.h:2476-2490, 587-648]
 """
 import os
 import sys
@@ -24,7 +26,7 @@ sys.path.insert(0, os.path.dirname(HERE))
 sys.path.insert(0, HERE)
 
 from _common import (T_CDOUBLE, oracle_bsr, oracle_contraction, oracle_copy,  # noqa: E402
-                     rel_err)
+                     oracle_kron_bsr, rel_err)
 from _golden import gen, piece, put_piece, vol  # noqa: E402
 
 
@@ -193,6 +195,73 @@ def case_bsr(sb, comm, rank, n, dev, ncols=3):
     assert np.array_equal(out2, np.concatenate([ref, ref2])), "bsr powers"
 
 
+def case_kron(sb, comm, rank, n, dev, ncols=2, power=2):
+    L, Lt, spin, color = 4, 2 * n, 4, 3
+    dim = [L, L, L, Lt, spin, color]
+    pi = sb.basic_partitioning("xyztsc", dim, [1, 1, 1, n, 1, 1], "xyzt", n, 1)
+    pd = []
+    for f, s in pi:
+        f, s = list(f), list(s)
+        for d in range(4):
+            s[d] = min(dim[d], s[d] + 2)
+            f[d] = (f[d] - 1) % dim[d] if s[d] < dim[d] else 0
+        pd.append((f, s))
+    f, s = pi[rank]
+    sites = np.array(np.unravel_index(np.arange(vol(s[:4])), s[:4])).T + np.array(f[:4])
+    dom = np.array(dim[:4])
+    dirs = [(None, 0)] + [(d, dr) for d in range(4) for dr in (-1, 1)]
+    jj = []
+    for st in sites:
+        for d, dr in dirs:
+            c = st.copy()
+            if d is not None:
+                c[d] += dr
+            jj.append(list((c - np.array(pd[rank][0][:4])) % dom) + [0, 0])
+    gsite = np.ravel_multi_index(tuple((sites % dom).T), dim[:4])
+    nb = color * color
+    allv = gen("int", vol(dim[:4]) * 9 * nb, 4, np.complex128).reshape(-1, 9 * nb)
+    vals = np.ascontiguousarray(allv[gsite]).ravel()
+    kron = gen("int", 9 * spin * spin, 7, np.complex128)
+    blk, kr = [1, 1, 1, 1, 1, color], [1, 1, 1, 1, spin, 1]
+    op = sb.create_kron_bsr(pi, dim, pd, dim, blk, blk, kr, kr, False,
+                            [torch.from_numpy(np.full(len(sites), 9, np.int32)).to(dev)],
+                            [torch.from_numpy(np.array(jj, np.int32).ravel()).to(dev)],
+                            [torch.from_numpy(vals).to(dev)], [torch.from_numpy(kron).to(dev)],
+                            comm=comm)
+    dimx = [1, L, L, L, Lt, color, ncols, spin]
+    dimy = [power] + dimx[1:]
+    px = sb.basic_partitioning("pXYZTCnS", dimx, [1, 1, 1, 1, n, 1, 1, 1], "XYZT", n, 1)
+    py = sb.basic_partitioning("pxyztcns", dimy, [1, 1, 1, 1, n, 1, 1, 1], "xyzt", n, 1)
+    gx = gen("int", vol(dimx), 5, np.complex128)
+    gy = gen("int", vol(dimy), 6, np.complex128)
+    vx = scatter(sb, gx, dimx, px, rank, 1, dev)
+    vy = scatter(sb, gy, dimy, py, rank, 1, dev)
+    z8 = [0] * 8
+    sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", px, "pXYZTCnS", z8, dimx, dimx, vx, 0.0, py,
+                  "pxyztcns", z8, dimy, dimy, "p", vy, comm=comm)
+    torch.cuda.synchronize()
+    op.destroy()
+    out = gather(np.zeros_like(gy), dimy, py, 1, vy)
+    allsites = np.array(np.unravel_index(np.arange(vol(dim[:4])), dim[:4])).T
+    jg = []
+    for st in allsites:
+        for d, dr in dirs:
+            c = st.copy()
+            if d is not None:
+                c[d] += dr
+            jg.append(list(c % dom) + [0, 0])
+    V = vol(dim[:4])
+    cur, refs = gx, []
+    for _ in range(power):
+        y = np.zeros_like(cur)
+        oracle_kron_bsr(T_CDOUBLE, dim[:4] + [1, 1], 0, V, 9, color, color, spin, spin,
+                        np.array(jg, np.int32).ravel(), allv.ravel(), kron, False, cur, y, ncols,
+                        1.0)
+        refs.append(y)
+        cur = y
+    assert np.array_equal(out, np.concatenate(refs)), "kron bsr"
+
+
 def main():
     dist.init_process_group("gloo")
     rank, n = dist.get_rank(), dist.get_world_size()
@@ -206,13 +275,15 @@ def main():
         comm = sb.Comm.from_torch_distributed(dev_idx)
     else:
         comm = sb.Comm.host_staged(dev_idx)
-    cases = os.environ.get("SBX_TEST_CASES", "copy,contr,bsr").split(",")
+    cases = os.environ.get("SBX_TEST_CASES", "copy,contr,bsr,kron").split(",")
     if "copy" in cases:
         case_copy(sb, comm, rank, n, dev)
     if "contr" in cases:
         case_contraction(sb, comm, rank, n, dev)
     if "bsr" in cases:
         case_bsr(sb, comm, rank, n, dev)
+    if "kron" in cases:
+        case_kron(sb, comm, rank, n, dev)
     dist.barrier()
     comm.close()
     dist.destroy_process_group()

@@ -16,7 +16,7 @@ def declared_symbols():
 
 def test_header_declares_api():
     syms = declared_symbols()
-    for s in ("sbx_copy", "sbx_contraction", "sbx_create_bsr", "sbx_bsr_krylov",
+    for s in ("sbx_copy", "sbx_contraction", "sbx_create_bsr", "sbx_create_kron_bsr", "sbx_bsr_krylov",
               "sbx_destroy_bsr", "sbx_comm_create", "sbx_xgemm_batch_strided"):
         assert s in syms
 

@@ -70,9 +70,10 @@ def test_golden_contraction(gpu, case):
     assert np.array_equal(out, output(case, t))
 
 
-def _bsr_component(L, spin, color, pi_c, pd_c):
-    """ii/jj/nonzeros of one component of ref_golden.cpp bsr_case (tests/bsr.cpp:169-255)."""
-    b = spin * color
+def _bsr_component(L, spin, color, pi_c, pd_c, b=None):
+    """ii/jj/nonzeros of one component of ref_golden.cpp bsr_case (tests/bsr.cpp:169-255);
+    b = the block size (spin*color, or color for the Kronecker form)."""
+    b = spin * color if b is None else b
     dimi = list(pi_c[1][:4])
     sites = np.array(np.unravel_index(np.arange(vol(dimi)), dimi)).T + np.array(pi_c[0][:4])
     dom = np.array([L, L, L, L])
@@ -108,13 +109,46 @@ def test_golden_bsr(gpu, case):
     blk = [1, 1, 1, 1, spin, color]
     op = sb.create_bsr(case["pi"], dim, case["pd"], dim, blk, blk, False, iis, jjs, vs)
     dimx = [1, L, L, L, L, spin, color, ncols]
+    dimy = [case.get("power", 1)] + dimx[1:]
     gx = gen("int", vol(dimx), 5, np.complex128)
-    gy = gen("int", vol(dimx), 6, np.complex128)
+    gy = gen("int", vol(dimy), 6, np.complex128)
     vx = [torch.from_numpy(piece(gx, dimx, f, s)).to(gpu) for f, s in case["px"]]
-    vy = [torch.from_numpy(piece(gy, dimx, f, s)).to(gpu) for f, s in case["py"]]
+    vy = [torch.from_numpy(piece(gy, dimy, f, s)).to(gpu) for f, s in case["py"]]
     sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", case["px"], "pXYZTSCn", [0] * 8, dimx, dimx, vx,
-                  0.0, case["py"], "pxyztscn", [0] * 8, dimx, dimx, "p", vy)
+                  0.0, case["py"], "pxyztscn", [0] * 8, dimy, dimy, "p", vy)
     torch.cuda.synchronize()
     op.destroy()
-    out = _gather(vy, dimx, case["py"], np.complex128)
+    out = _gather(vy, dimy, case["py"], np.complex128)
+    assert np.array_equal(out, output(case, np.complex128))
+
+
+@pytest.mark.parametrize("case", manifest("kron_bsr"), ids=lambda c: "kron%d" % c["id"])
+def test_golden_kron_bsr(gpu, case):
+    """create_kron_bsr + bsr_krylov (tests/bsr.cpp:826-852 shapes) against the reference."""
+    import torch
+    import superbblas_amd as sb
+    L, spin, color, ncols = case["L"], case["spin"], case["color"], case["ncols"]
+    dim = [L, L, L, L, spin, color]
+    kron = gen("int", 9 * spin * spin, 7, np.complex128)
+    iis, jjs, vs, ks = [], [], [], []
+    for pi_c, pd_c in zip(case["pi"], case["pd"]):
+        ii, jj, v = _bsr_component(L, spin, color, pi_c, pd_c, b=color)
+        iis.append(torch.from_numpy(ii).to(gpu))
+        jjs.append(torch.from_numpy(jj).to(gpu))
+        vs.append(torch.from_numpy(v).to(gpu))
+        ks.append(torch.from_numpy(kron).to(gpu))
+    blk, kr = [1, 1, 1, 1, 1, color], [1, 1, 1, 1, spin, 1]
+    op = sb.create_kron_bsr(case["pi"], dim, case["pd"], dim, blk, blk, kr, kr,
+                            case["block_im_fast"], iis, jjs, vs, ks)
+    dimx = [1, L, L, L, L, color, ncols, spin]
+    dimy = [case["power"]] + dimx[1:]
+    gx = gen("int", vol(dimx), 5, np.complex128)
+    gy = gen("int", vol(dimy), 6, np.complex128)
+    vx = [torch.from_numpy(piece(gx, dimx, f, s)).to(gpu) for f, s in case["px"]]
+    vy = [torch.from_numpy(piece(gy, dimy, f, s)).to(gpu) for f, s in case["py"]]
+    sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", case["px"], "pXYZTCnS", [0] * 8, dimx, dimx, vx,
+                  0.0, case["py"], "pxyztcns", [0] * 8, dimy, dimy, "p", vy)
+    torch.cuda.synchronize()
+    op.destroy()
+    out = _gather(vy, dimy, case["py"], np.complex128)
     assert np.array_equal(out, output(case, np.complex128))

@@ -1,0 +1,166 @@
+"""Kronecker BSR (create_kron_bsr, bsr.h:2476-2490; builtin operator bsr.h:587-648) on the GPU vs
+the oracle's restatement, on the 9-point lattice stencil with color blocks and one spin matrix
+per direction (tests/bsr.cpp:547-644).  Integer-valued data: exact in every type."""
+import numpy as np
+import pytest
+
+from _common import T_CDOUBLE, oracle_kron_bsr
+
+pytestmark = pytest.mark.gpu
+
+
+def kron_lattice(L, spin, color, sparse_kron=False):
+    V = L ** 4
+    sites = np.array(np.unravel_index(np.arange(V), (L, L, L, L))).T
+    jj = []
+    for s in sites:
+        jj.append(list(s) + [0, 0])
+        for d in range(4):
+            for dr in (-1, 1):
+                c = s.copy()
+                c[d] = (c[d] + dr) % L
+                jj.append(list(c) + [0, 0])
+    jj = np.array(jj, np.int32).ravel()
+    k = np.arange(V * 9 * color * color, dtype=np.int64)
+    vals = ((k * 3 + 1) % 7 - 3) + 1j * ((k * 5 + 2) % 9 - 4)
+    q = np.arange(9 * spin * spin, dtype=np.int64)
+    kron = ((q * 5 + 2) % 7 - 3) + 1j * ((q * 3 + 1) % 5 - 2)
+    if sparse_kron:
+        # Wilson-projector-like pattern: half of every spin matrix is zero (the skip path)
+        a, b = np.unravel_index(q % (spin * spin), (spin, spin))
+        kron[(a + b + q // (spin * spin)) % 2 == 1] = 0
+    return np.full(V, 9, np.int32), jj, vals, kron
+
+
+def reference(L, spin, color, ncols, vals, kron, jj, x, alpha, beta, y0, power, bif=False):
+    V = L ** 4
+    cur, out = x.astype(np.complex128), []
+    for p in range(power):
+        y = np.zeros_like(cur)
+        oracle_kron_bsr(T_CDOUBLE, [L, L, L, L, 1, 1], 0, V, 9, color, color, spin, spin, jj,
+                        vals, kron, bif, cur, y, ncols, 1.0)
+        out.append(y)
+        cur = y
+    return np.concatenate([alpha * o + beta * y0[i * len(x):(i + 1) * len(x)]
+                           for i, o in enumerate(out)])
+
+
+@pytest.mark.parametrize("dtype", [np.complex128, np.complex64, np.float64, np.float32])
+@pytest.mark.parametrize("spin,color,ncols", [(4, 3, 3), (2, 3, 2), (4, 1, 5)])
+def test_kron_types_sizes(gpu, dtype, spin, color, ncols):
+    """(4, 3) runs the specialized kernel, the others the generic one."""
+    import torch
+    import superbblas_amd as sb
+    L = 4
+    cplx = np.dtype(dtype).kind == "c"
+    ii, jj, vals, kron = kron_lattice(L, spin, color)
+    if not cplx:
+        vals, kron = vals.real.copy(), kron.real.copy()
+    V = L ** 4
+    g = np.arange(V * color * ncols * spin)
+    x = ((g % 7 - 3) + (1j * (g % 5 - 2) if cplx else 0)).astype(np.complex128)
+    ref = reference(L, spin, color, ncols, vals.astype(np.complex128),
+                    kron.astype(np.complex128), jj, x, 1.0, 0.0, np.zeros_like(x), 1)
+    dim = [L, L, L, L, spin, color]
+    full = [([0] * 6, dim)]
+    blk, kr = [1, 1, 1, 1, 1, color], [1, 1, 1, 1, spin, 1]
+    op = sb.create_kron_bsr(full, dim, full, dim, blk, blk, kr, kr, False,
+                            [torch.from_numpy(ii).to(gpu)], [torch.from_numpy(jj).to(gpu)],
+                            [torch.from_numpy(vals.astype(dtype)).to(gpu)],
+                            [torch.from_numpy(kron.astype(dtype)).to(gpu)])
+    dimx = [1, L, L, L, L, color, ncols, spin]
+    tx = torch.from_numpy((x if cplx else x.real).astype(dtype)).to(gpu)
+    ty = torch.zeros(V * color * ncols * spin, dtype=tx.dtype, device=gpu)
+    sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", [([0] * 8, dimx)], "pXYZTCnS", [0] * 8, dimx,
+                  dimx, [tx], 0.0, [([0] * 8, dimx)], "pxyztcns", [0] * 8, dimx, dimx, "p", [ty])
+    torch.cuda.synchronize()
+    op.destroy()
+    out = ty.cpu().numpy().astype(np.complex128)
+    assert np.array_equal(out, ref if cplx else ref.real.astype(np.complex128))
+
+
+@pytest.mark.parametrize("bif", [False, True])
+def test_kron_sparse_alpha_beta_power(gpu, bif):
+    """Sparse spin matrices, complex alpha, beta != 0, powers, both block orders."""
+    import torch
+    import superbblas_amd as sb
+    L, spin, color, ncols, power = 4, 4, 3, 2, 3
+    ii, jj, vals, kron = kron_lattice(L, spin, color, sparse_kron=True)
+    V = L ** 4
+    n = V * color * ncols * spin
+    g = np.arange(n)
+    x = ((g % 5 - 2) + 1j * (g % 3 - 1)).astype(np.complex128)
+    y0 = ((np.arange(n * power) % 7 - 3) + 1j).astype(np.complex128)
+    alpha, beta = 1 - 1j, 2.0
+    ref = reference(L, spin, color, ncols, vals, kron, jj, x, alpha, beta, y0, power, bif)
+    dim = [L, L, L, L, spin, color]
+    full = [([0] * 6, dim)]
+    blk, kr = [1, 1, 1, 1, 1, color], [1, 1, 1, 1, spin, 1]
+    op = sb.create_kron_bsr(full, dim, full, dim, blk, blk, kr, kr, bif,
+                            [torch.from_numpy(ii).to(gpu)], [torch.from_numpy(jj).to(gpu)],
+                            [torch.from_numpy(vals).to(gpu)], [torch.from_numpy(kron).to(gpu)])
+    dimx = [1, L, L, L, L, color, ncols, spin]
+    dimy = [power] + dimx[1:]
+    tx = torch.from_numpy(x).to(gpu)
+    ty = torch.from_numpy(y0.copy()).to(gpu)
+    sb.bsr_krylov(alpha, op, "xyztsc", "XYZTSC", [([0] * 8, dimx)], "pXYZTCnS", [0] * 8, dimx,
+                  dimx, [tx], beta, [([0] * 8, dimy)], "pxyztcns", [0] * 8, dimy, dimy, "p", [ty])
+    torch.cuda.synchronize()
+    op.destroy()
+    assert np.array_equal(ty.cpu().numpy(), ref)
+
+
+def test_kron_other_layouts(gpu):
+    """x and y in layouts other than the preferred (D, d, C, kd): through the temporaries."""
+    import torch
+    import superbblas_amd as sb
+    L, spin, color, ncols = 4, 4, 3, 3
+    ii, jj, vals, kron = kron_lattice(L, spin, color)
+    V = L ** 4
+    g = np.arange(V * color * ncols * spin)
+    x = ((g % 7 - 3) + 1j * (g % 5 - 2)).astype(np.complex128)
+    ref = reference(L, spin, color, ncols, vals, kron, jj, x, 1.0, 0.0, np.zeros_like(x), 1)
+    # preferred layouts: x pXYZTCnS and y pxyztcns; use x = nXYZTSC (column major) and
+    # y = pxyztsnc instead
+    xt = x.reshape(L, L, L, L, color, ncols, spin).transpose(5, 0, 1, 2, 3, 6, 4).copy()
+    dim = [L, L, L, L, spin, color]
+    full = [([0] * 6, dim)]
+    blk, kr = [1, 1, 1, 1, 1, color], [1, 1, 1, 1, spin, 1]
+    op = sb.create_kron_bsr(full, dim, full, dim, blk, blk, kr, kr, False,
+                            [torch.from_numpy(ii).to(gpu)], [torch.from_numpy(jj).to(gpu)],
+                            [torch.from_numpy(vals).to(gpu)], [torch.from_numpy(kron).to(gpu)])
+    dimx = [ncols, L, L, L, L, spin, color]
+    dimy = [1, L, L, L, L, spin, ncols, color]
+    tx = torch.from_numpy(xt.ravel()).to(gpu)
+    ty = torch.zeros(V * color * ncols * spin, dtype=torch.complex128, device=gpu)
+    sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", [([0] * 7, dimx)], "nXYZTSC", [0] * 7, dimx,
+                  dimx, [tx], 0.0, [([0] * 8, dimy)], "pxyztsnc", [0] * 8, dimy, dimy, "p", [ty])
+    torch.cuda.synchronize()
+    op.destroy()
+    out = ty.cpu().numpy().reshape(L, L, L, L, spin, ncols, color).transpose(0, 1, 2, 3, 6, 5, 4)
+    assert np.array_equal(out.ravel(), ref)
+
+
+def test_kron_errors(gpu):
+    import torch
+    import superbblas_amd as sb
+    L, spin, color = 4, 4, 3
+    ii, jj, vals, kron = kron_lattice(L, spin, color)
+    dim = [L, L, L, L, spin, color]
+    full = [([0] * 6, dim)]
+    blk, kr = [1, 1, 1, 1, 1, color], [1, 1, 1, 1, spin, 1]
+    t = lambda a: torch.from_numpy(a).to(gpu)  # noqa: E731
+    ii2 = ii.copy()
+    ii2[0], ii2[1] = 8, 10
+    with pytest.raises(sb.SuperbblasError, match="different number of nonzeros"):
+        sb.create_kron_bsr(full, dim, full, dim, blk, blk, kr, kr, False, [t(ii2)], [t(jj)],
+                           [t(vals)], [t(kron)])
+    jj2 = jj.copy()
+    jj2[6] = -1
+    with pytest.raises(sb.SuperbblasError, match="-1"):
+        sb.create_kron_bsr(full, dim, full, dim, blk, blk, kr, kr, False, [t(ii)], [t(jj2)],
+                           [t(vals)], [t(kron)])
+    with pytest.raises(sb.SuperbblasError, match="simultaneous blocking"):
+        sb.create_kron_bsr(full, dim, full, dim, blk, blk, [1, 1, 1, 1, spin, color],
+                           [1, 1, 1, 1, spin, color], False, [t(ii)], [t(jj)], [t(vals)],
+                           [t(kron)])

@@ -3,7 +3,7 @@ golden vectors produced by the real reference (tests/golden, oracle/ref_golden.c
 import numpy as np
 import pytest
 
-from _common import oracle_bsr, oracle_contraction, oracle_copy, T_CDOUBLE
+from _common import oracle_bsr, oracle_contraction, oracle_copy, oracle_kron_bsr, T_CDOUBLE
 from _golden import NPT, gen, manifest, output, vol
 
 
@@ -62,14 +62,37 @@ def lattice_operator(L, spin, color):
 @pytest.mark.parametrize("case", manifest("bsr"), ids=lambda c: "bsr%d" % c["id"])
 def test_oracle_bsr(case):
     L, spin, color, ncols = case["L"], case["spin"], case["color"], case["ncols"]
+    power = case.get("power", 1)
     b = spin * color
     V = L ** 4
     ii, jj, vals = lattice_operator(L, spin, color)
-    x = gen("int", V * b * ncols, 5, np.complex128)
-    y = gen("int", V * b * ncols, 6, np.complex128)
-    oracle_bsr(T_CDOUBLE, [L, L, L, L, spin, color], 0, V, b, b, ii, jj, vals, False, x, ncols,
-               True, y, ncols, True, ncols, 1.0)
-    assert np.array_equal(y, output(case, np.complex128))
+    # powers (bsr.h:2211-2247): y[p] = A^(p+1) x
+    cur, out = gen("int", V * b * ncols, 5, np.complex128), []
+    for _ in range(power):
+        y = np.zeros_like(cur)
+        oracle_bsr(T_CDOUBLE, [L, L, L, L, spin, color], 0, V, b, b, ii, jj, vals, False, cur,
+                   ncols, True, y, ncols, True, ncols, 1.0)
+        out.append(y)
+        cur = y
+    assert np.array_equal(np.concatenate(out), output(case, np.complex128))
+
+
+@pytest.mark.parametrize("case", manifest("kron_bsr"), ids=lambda c: "kron%d" % c["id"])
+def test_oracle_kron_bsr(case):
+    """Kronecker BSR (create_lattice_kron, tests/bsr.cpp:547-644) against the reference."""
+    L, spin, color, ncols = case["L"], case["spin"], case["color"], case["ncols"]
+    V = L ** 4
+    ii, jj, _ = lattice_operator(L, 1, 1)
+    vals = gen("int", V * 9 * color * color, 4, np.complex128)
+    kron = gen("int", 9 * spin * spin, 7, np.complex128)
+    cur, out = gen("int", V * color * ncols * spin, 5, np.complex128), []
+    for _ in range(case["power"]):
+        y = np.zeros_like(cur)
+        oracle_kron_bsr(T_CDOUBLE, [L, L, L, L, 1, 1], 0, V, 9, color, color, spin, spin, jj,
+                        vals, kron, case["block_im_fast"], cur, y, ncols, 1.0)
+        out.append(y)
+        cur = y
+    assert np.array_equal(np.concatenate(out), output(case, np.complex128))
 
 
 # ---- host planner (the library's C++ partitioning helpers; no GPU needed) ----
