@@ -12,7 +12,8 @@
  *  - The distributed overloads take a `superbblas::Communicator` (an sbx_comm: RCCL over xGMI,
  *    or host-staged through a user all-to-all) where the reference takes an MPI_Comm.  With
  *    SUPERBBLAS_USE_MPI defined, MPI_Comm overloads are provided that wrap MPI_Alltoallv.
- *  - Masks (mask0/mask1) must be null; `session` must be 0; `request` is always completed on
+ *  - Masks (mask0/mask1) must select the same elements (as the reference requires); `session`
+ *    must be 0; `request` is always completed on
  *    return (as the reference's no-MPI overloads do, dist.h:3601, 3730).
  *  - Only the ContractWithDomain form of bsr_krylov is implemented (with powers over the okr
  *    label, for plain and Kronecker operators).
@@ -118,10 +119,6 @@ template <std::size_t N> inline const int *parts(const PartitionItem<N> *p) {
     return reinterpret_cast<const int *>(p);
 }
 
-inline void no_masks(const MaskType **m0, const MaskType **m1) {
-    if (m0 || m1) throw std::runtime_error("superbblas_amd: masks are not supported");
-}
-
 inline void check_session(Session s) {
     if (s != 0) throw std::runtime_error("superbblas_amd: session must be 0");
 }
@@ -136,15 +133,16 @@ void copy_impl(typename elem<T>::type alpha, const PartitionItem<Nd0> *p0, int n
                const Coor<Nd1> &from1, const Coor<Nd1> &dim1, Q **v1, const MaskType **mask1,
                const Context *ctx1, sbx_comm comm, CoorOrder co, CopyAdd copyadd,
                Request *request, Session session) {
-    no_masks(mask0, mask1);
+    static_assert(std::is_same<MaskType, float>::value, "MaskType is float (tensor.h:54)");
     check_session(session);
     const auto a = scalar(alpha);
     const auto c0 = contexts(ctx0, ncomponents0), c1 = contexts(ctx1, ncomponents1);
-    check(sbx_copy((int)Nd0, (int)Nd1, a.data(), dtype<T>::value, dtype<Q>::value, parts(p0),
-                   ncomponents0, o0, from0.data(), size0.data(), dim0.data(),
-                   (const void *const *)v0, c0.data(), parts(p1), ncomponents1, o1, from1.data(),
-                   dim1.data(), (void *const *)v1, c1.data(), comm, co_of(co),
-                   copyadd == Copy ? SBX_COPY : SBX_ADD, 0));
+    check(sbx_copy_masked((int)Nd0, (int)Nd1, a.data(), dtype<T>::value, dtype<Q>::value,
+                          parts(p0), ncomponents0, o0, from0.data(), size0.data(), dim0.data(),
+                          (const void *const *)v0, (const float *const *)mask0, c0.data(),
+                          parts(p1), ncomponents1, o1, from1.data(), dim1.data(),
+                          (void *const *)v1, (const float *const *)mask1, c1.data(), comm,
+                          co_of(co), copyadd == Copy ? SBX_COPY : SBX_ADD, 0));
     if (request) *request = Request{};
 }
 

@@ -153,6 +153,20 @@ int sbx_copy(int nd0, int nd1, const double *alpha, int t0, int t1,
              void *const *v1, const sbx_context *ctx1, sbx_comm comm, int co, int copyadd,
              int session);
 
+/* copy with masks (the reference's mask0 / mask1 arguments, dist.h:3534-3602; MaskType =
+   float, tensor.h:54): mask0[c] / mask1[c] are laid out like the data of component c;
+   elements are copied (and, with SBX_COPY, the uncovered part of the region zeroed) only where
+   the masks are nonzero.  As in the reference the two masks must select the same elements
+   (tensor.h:1019-1027): the destination mask decides for pieces received from other ranks.
+   mask0 may be null (no origin mask); mask1 is required when mask0 is given. */
+int sbx_copy_masked(int nd0, int nd1, const double *alpha, int t0, int t1, const int *p0,
+                    int ncomponents0, const char *o0, const int *from0, const int *size0,
+                    const int *dim0, const void *const *v0, const float *const *mask0,
+                    const sbx_context *ctx0, const int *p1, int ncomponents1, const char *o1,
+                    const int *from1, const int *dim1, void *const *v1,
+                    const float *const *mask1, const sbx_context *ctx1, sbx_comm comm, int co,
+                    int copyadd, int session);
+
 /* Exchange plan of sbx_copy as seen by `rank` of `nprocs` (host only, no GPU work; the
    reference get_indices_to_send / get_indices_to_receive, dist.h:1789-1900, 2321-2324):
    send[q] / recv[q] = elements sent to / received from rank q, *local = elements moved within

@@ -88,9 +88,10 @@ static int normalize_coor(long c, int dim) {
  * With alpha == 1 the value is moved without a multiplication (copy_n.h:147-244 uses a plain
  * assignment for alpha == 1); Add computes w + alpha*v.
  */
-int oracle_copy(int nd0, int nd1, const double *alpha, int t0, int t1, const char *o0,
-                const int *from0, const int *size0, const int *dim0, const void *v0,
-                const char *o1, const int *from1, const int *dim1, void *v1, int co, int add) {
+int oracle_copy_masked(int nd0, int nd1, const double *alpha, int t0, int t1, const char *o0,
+                       const int *from0, const int *size0, const int *dim0, const void *v0,
+                       const float *m0, const char *o1, const int *from1, const int *dim1,
+                       void *v1, const float *m1, int co, int add) {
     long s0[64], s1[64];
     int perm[64]; /* perm[j]: position in o0 of label o1[j], or -1 */
     if (nd0 > 64 || nd1 > 64) return -1;
@@ -103,6 +104,12 @@ int oracle_copy(int nd0, int nd1, const double *alpha, int t0, int t1, const cha
     }
     const long n = vol(nd0, size0);
     const int one = alpha[0] == 1 && alpha[1] == 0;
+    /* masks (local_copy_normalize, tensor.h:1019-1027): with an origin mask, the origin indices
+       with a nonzero mask0 and the destination indices with a nonzero mask1 are selected in
+       the same element order and paired in that order; different counts are an error */
+    long *i0s = (long *)malloc(sizeof(long) * (n > 0 ? n : 1));
+    long *i1s = (long *)malloc(sizeof(long) * (n > 0 ? n : 1));
+    long n0 = 0, n1 = 0;
     int cc[64];
     for (long k = 0; k < n; ++k) {
         /* decode k in FastToSlow order of size0 (get_permutation, tensor.h:815-845) */
@@ -124,6 +131,16 @@ int oracle_copy(int nd0, int nd1, const double *alpha, int t0, int t1, const cha
             const long c = perm[j] >= 0 ? cc[perm[j]] : 0;
             i1 += (long)normalize_coor((long)from1[j] + c, dim1[j]) * s1[j];
         }
+        if (!m0 || m0[i0] != 0) i0s[n0++] = i0;
+        if (!m0 || m1[i1] != 0) i1s[n1++] = i1;
+    }
+    if (n0 != n1) {
+        free(i0s);
+        free(i1s);
+        return -2; /* "copy: non-compatible masks" */
+    }
+    for (long q = 0; q < n0; ++q) {
+        const long i0 = i0s[q], i1 = i1s[q];
         if (one && !add && t0 == t1) {
             memcpy((char *)v1 + i1 * elem_size(t1), (const char *)v0 + i0 * elem_size(t0),
                    elem_size(t0));
@@ -143,7 +160,16 @@ int oracle_copy(int nd0, int nd1, const double *alpha, int t0, int t1, const cha
         }
         store(t1, v1, i1, re, im);
     }
+    free(i0s);
+    free(i1s);
     return 0;
+}
+
+int oracle_copy(int nd0, int nd1, const double *alpha, int t0, int t1, const char *o0,
+                const int *from0, const int *size0, const int *dim0, const void *v0,
+                const char *o1, const int *from1, const int *dim1, void *v1, int co, int add) {
+    return oracle_copy_masked(nd0, nd1, alpha, t0, t1, o0, from0, size0, dim0, v0, NULL, o1,
+                              from1, dim1, v1, NULL, co, add);
 }
 
 /*

@@ -135,6 +135,9 @@ class _Pack:
 
 _lib.sbx_copy.argtypes = [_I, _I, _VP, _I, _I, _VP, _I, ctypes.c_char_p, _VP, _VP, _VP, _VP, _VP,
                           _VP, _I, ctypes.c_char_p, _VP, _VP, _VP, _VP, _VP, _I, _I, _I]
+_lib.sbx_copy_masked.argtypes = [_I, _I, _VP, _I, _I, _VP, _I, ctypes.c_char_p, _VP, _VP, _VP,
+                                 _VP, _VP, _VP, _VP, _I, ctypes.c_char_p, _VP, _VP, _VP, _VP, _VP,
+                                 _VP, _I, _I, _I]
 _lib.sbx_contraction.argtypes = (
     [_I, _I, _I, _I, _VP] +
     [_VP, _VP, _VP, _VP, _I, ctypes.c_char_p, _I, _VP, _VP] * 2 + [_VP] +
@@ -441,8 +444,11 @@ def make_hole(frm, size, hole_from, hole_size, dim):
 
 def copy(alpha, p0, o0: str, from0, size0, dim0, v0: Sequence[torch.Tensor], p1, o1: str, from1,
          dim1, v1: Sequence[torch.Tensor], co: int = SlowToFast, copyadd: int = Copy,
-         comm: Optional[Comm] = None):
-    """v1[from1 + P(c - from0)] (=|+=) alpha * v0[c]  for c in [from0, from0 + size0)."""
+         comm: Optional[Comm] = None, mask0: Optional[Sequence[torch.Tensor]] = None,
+         mask1: Optional[Sequence[torch.Tensor]] = None):
+    """v1[from1 + P(c - from0)] (=|+=) alpha * v0[c]  for c in [from0, from0 + size0);
+    with masks (float32 tensors shaped like the components, dist.h:3534-3602) only where the
+    masks are nonzero."""
     nprocs, rank = _nprocs_rank(comm)
     nd0, nd1 = len(o0), len(o1)
     nc0, nc1 = len(v0), len(v1)
@@ -465,10 +471,24 @@ def copy(alpha, p0, o0: str, from0, size0, dim0, v0: Sequence[torch.Tensor], p1,
     k.add_ctxs(v1)
     k.add_ptrs(v0)
     k.add_ptrs(v1)
+    if mask0 is None and mask1 is None:
+        a, pp = k.addrs()
+        _check(_lib.sbx_copy(nd0, nd1, _scalar(alpha), t0, t1, a[0], nc0, o0.encode(), a[1], a[2],
+                             a[3], pp[0], a[4], a[5], nc1, o1.encode(), a[6], a[7], pp[1], a[8],
+                             _comm(comm), co, copyadd, 0))
+        return
+    for m, v in ((mask0, v0), (mask1, v1)):
+        if m is not None and (len(m) != len(v) or any(
+                x.dtype != torch.float32 or x.numel() != y.numel() for x, y in zip(m, v))):
+            raise SuperbblasError("masks must be float32 tensors shaped like the components")
+    k.add_ptrs(mask0 or [])
+    k.add_ptrs(mask1 or [])
     a, pp = k.addrs()
-    _check(_lib.sbx_copy(nd0, nd1, _scalar(alpha), t0, t1, a[0], nc0, o0.encode(), a[1], a[2],
-                         a[3], pp[0], a[4], a[5], nc1, o1.encode(), a[6], a[7], pp[1], a[8],
-                         _comm(comm), co, copyadd, 0))
+    _check(_lib.sbx_copy_masked(nd0, nd1, _scalar(alpha), t0, t1, a[0], nc0, o0.encode(), a[1],
+                                a[2], a[3], pp[0], pp[2] if mask0 is not None else None, a[4],
+                                a[5], nc1, o1.encode(), a[6], a[7], pp[1],
+                                pp[3] if mask1 is not None else None, a[8], _comm(comm), co,
+                                copyadd, 0))
 
 
 def copy_plan(p0, o0: str, from0, size0, dim0, ncomponents0: int, p1, o1: str, from1, dim1,

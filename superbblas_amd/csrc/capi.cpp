@@ -157,6 +157,38 @@ DistTensor make_tensor(int nd, const char *o, const int *dim, const int *p, int 
     return t;
 }
 
+/// Masks of copy() (MaskType = float, one per component, laid out like its data); host masks
+/// are mirrored to the device like host data
+void attach_masks(DistTensor &t, const float *const *mask, int ncomponents,
+                  const sbx_context *ctx, const Comm &comm, Mirror &mirror) {
+    if (!mask) return;
+    for (int c = 0; c < ncomponents; ++c) {
+        const float *m = mask[c];
+        const std::size_t bytes = volume(t.ranges[comm.rank][c].size) * sizeof(float);
+        if (!m && bytes > 0) throw Error("copy: null mask pointer for a nonempty component");
+        if (ctx[c].plat != SBX_GPU && bytes > 0) {
+            mirror.any = true;
+            mirror.bufs.emplace_back(bytes, mirror.device);
+            set_device(mirror.device);
+            SBX_HIP_CHECK(hipMemcpyAsync(mirror.bufs.back().ptr, m, bytes, hipMemcpyHostToDevice,
+                                         get_stream(mirror.device)));
+            m = (const float *)mirror.bufs.back().ptr;
+        }
+        t.mask.push_back(m);
+    }
+}
+
+/// Element conversions of copy(): same type, real -> real, real -> complex, complex -> complex
+/// (blas.h:57-65; never complex -> real), and int <-> size_t
+void check_copy_types(int t0, int t1) {
+    auto real = [](int t) { return t == SBX_FLOAT || t == SBX_DOUBLE; };
+    auto index = [](int t) { return t == SBX_INT || t == SBX_SIZE_T; };
+    if (t0 == t1 || (real(t0) && (real(t1) || dtype_is_complex(t1))) ||
+        (dtype_is_complex(t0) && dtype_is_complex(t1)) || (index(t0) && index(t1)))
+        return;
+    throw Error("copy: unsupported type conversion");
+}
+
 void finish_mirror(Mirror &m) {
     if (!m.any) return;
     for (auto &b : m.back) {
@@ -422,13 +454,18 @@ int sbx_make_hole(int nd, const int *from, const int *size, const int *hole_from
     });
 }
 
-int sbx_copy(int nd0, int nd1, const double *alpha, int t0, int t1, const int *p0,
-             int ncomponents0, const char *o0, const int *from0, const int *size0, const int *dim0,
-             const void *const *v0, const sbx_context *ctx0, const int *p1, int ncomponents1,
-             const char *o1, const int *from1, const int *dim1, void *const *v1,
-             const sbx_context *ctx1, sbx_comm comm, int co, int copyadd, int session) {
+int sbx_copy_masked(int nd0, int nd1, const double *alpha, int t0, int t1, const int *p0,
+                    int ncomponents0, const char *o0, const int *from0, const int *size0,
+                    const int *dim0, const void *const *v0, const float *const *mask0,
+                    const sbx_context *ctx0, const int *p1, int ncomponents1, const char *o1,
+                    const int *from1, const int *dim1, void *const *v1,
+                    const float *const *mask1, const sbx_context *ctx1, sbx_comm comm, int co,
+                    int copyadd, int session) {
     return guard([&] {
         check_session(session);
+        check_copy_types(t0, t1);
+        if (mask0 && !mask1)
+            throw Error("copy: a destination mask (mask1) is required with an origin mask");
         const Comm c = get_comm(comm);
         const bool rev = co == SBX_FAST_TO_SLOW;
         check_copy_args(to_labels(o0, nd0, rev, "o0"), to_coor(from0, nd0, rev),
@@ -440,10 +477,22 @@ int sbx_copy(int nd0, int nd1, const double *alpha, int t0, int t1, const int *p
         DistTensor a = make_tensor(nd0, o0, dim0, p0, ncomponents0, v0, ctx0, t0, c, rev, m, false, "o0");
         DistTensor b = make_tensor(nd1, o1, dim1, p1, ncomponents1, (const void *const *)v1, ctx1,
                                    t1, c, rev, m, true, "o1");
+        attach_masks(a, mask0, ncomponents0, ctx0, c, m);
+        attach_masks(b, mask1, ncomponents1, ctx1, c, m);
         dist_copy(to_scalar(alpha), a, to_coor(from0, nd0, rev), to_coor(size0, nd0, rev), b,
                   to_coor(from1, nd1, rev), copyadd == SBX_ADD, c);
         finish_mirror(m);
     });
+}
+
+int sbx_copy(int nd0, int nd1, const double *alpha, int t0, int t1, const int *p0,
+             int ncomponents0, const char *o0, const int *from0, const int *size0, const int *dim0,
+             const void *const *v0, const sbx_context *ctx0, const int *p1, int ncomponents1,
+             const char *o1, const int *from1, const int *dim1, void *const *v1,
+             const sbx_context *ctx1, sbx_comm comm, int co, int copyadd, int session) {
+    return sbx_copy_masked(nd0, nd1, alpha, t0, t1, p0, ncomponents0, o0, from0, size0, dim0, v0,
+                           nullptr, ctx0, p1, ncomponents1, o1, from1, dim1, v1, nullptr, ctx1,
+                           comm, co, copyadd, session);
 }
 
 int sbx_copy_plan(int nd0, int nd1, const int *p0, int ncomponents0, const char *o0,

@@ -199,13 +199,16 @@ long offset_of(const Coor &from, const std::vector<long> &strides) {
 void local_piece_copy(const Scalar &alpha, int src_t, const void *src, const Coor &src_size,
                       const Coor &src_from, int dst_t, void *dst, const Coor &dst_size,
                       const Coor &dst_from, const Coor &box, const std::vector<int> &perm_s2d,
-                      bool add, int device) {
+                      bool add, int device, const float *src_mask = nullptr,
+                      const float *dst_mask = nullptr) {
     const std::vector<long> ss = strides_slow_to_fast(src_size), ds = strides_slow_to_fast(dst_size);
     BoxCopyDesc d;
     d.src_t = src_t;
     d.dst_t = dst_t;
     d.src = (const char *)src + dtype_size(src_t) * offset_of(src_from, ss);
     d.dst = (char *)dst + dtype_size(dst_t) * offset_of(dst_from, ds);
+    if (src_mask) d.src_mask = src_mask + offset_of(src_from, ss);
+    if (dst_mask) d.dst_mask = dst_mask + offset_of(dst_from, ds);
     d.size.resize(box.size());
     d.src_stride = ss;
     d.dst_stride.resize(box.size());
@@ -368,7 +371,7 @@ void dist_copy(const Scalar &alpha, const DistTensor &src, const Coor &from0, co
                 for (const Piece &q : ps)
                     local_piece_copy(Scalar{0, 0}, dst.dtype, dst.ptr[i], rb.size, q.dst_from,
                                      dst.dtype, dst.ptr[i], rb.size, q.dst_from, q.size, id,
-                                     false, dst.dev[i]);
+                                     false, dst.dev[i], nullptr, dst.mask_of(i));
             }
         }
     };
@@ -406,7 +409,8 @@ void dist_copy(const Scalar &alpha, const DistTensor &src, const Coor &from0, co
         const int da = src.dev[ca.idx], db = dst.dev[cb.idx];
         if (da == db) {
             local_piece_copy(alpha, src.dtype, src.ptr[ca.idx], ra.size, p.src_from, dst.dtype,
-                             dst.ptr[cb.idx], rb.size, p.dst_from, p.size, perm_s2d, add, db);
+                             dst.ptr[cb.idx], rb.size, p.dst_from, p.size, perm_s2d, add, db,
+                             src.mask_of(ca.idx), dst.mask_of(cb.idx));
         } else {
             // pack on the origin device, peer copy, unpack on the destination device
             const long n = volume(p.size);
@@ -421,7 +425,8 @@ void dist_copy(const Scalar &alpha, const DistTensor &src, const Coor &from0, co
             set_device(db);
             SBX_HIP_CHECK(hipMemcpyPeerAsync(dbuf.ptr, db, sbuf.ptr, da, bytes, get_stream(db)));
             local_piece_copy(alpha, src.dtype, dbuf.ptr, p.size, Coor(src.nd(), 0), dst.dtype,
-                             dst.ptr[cb.idx], rb.size, p.dst_from, p.size, perm_s2d, add, db);
+                             dst.ptr[cb.idx], rb.size, p.dst_from, p.size, perm_s2d, add, db,
+                             nullptr, dst.mask_of(cb.idx));
             stream_wait(db, da); // keep sbuf alive until the peer copy is done
         }
     }
@@ -500,7 +505,7 @@ void dist_copy(const Scalar &alpha, const DistTensor &src, const Coor &from0, co
             local_piece_copy(alpha, src.dtype, (char *)rbuf.ptr + cur[ca.rank], p.size,
                              Coor(src.nd(), 0), dst.dtype, dst.ptr[cb.idx],
                              dst.ranges[cb.rank][cb.idx].size, p.dst_from, p.size, perm_s2d, add,
-                             device);
+                             device, nullptr, dst.mask_of(cb.idx));
             cur[ca.rank] += volume(p.size) * es;
         }
     }

@@ -57,6 +57,11 @@ template <> __device__ __forceinline__ double2 conv<double2, float2>(float2 v) {
 template <> __device__ __forceinline__ float2 conv<float2, double2>(double2 v) {
     return float2{(float)v.x, (float)v.y};
 }
+// real -> complex (blas.h:57-65 instantiates TREAL -> QCOMPLEX, never complex -> real)
+template <> __device__ __forceinline__ double2 conv<double2, double>(double v) { return double2{v, 0}; }
+template <> __device__ __forceinline__ double2 conv<double2, float>(float v) { return double2{(double)v, 0}; }
+template <> __device__ __forceinline__ float2 conv<float2, float>(float v) { return float2{v, 0}; }
+template <> __device__ __forceinline__ float2 conv<float2, double>(double v) { return float2{(float)v, 0}; }
 
 struct Alpha {
     double re, im;
@@ -115,6 +120,31 @@ __global__ void __launch_bounds__(256) copy_direct_kernel(const DirectArgs p) {
             so += (long)c * p.sst[i];
             doff += (long)c * p.dst[i];
         }
+        put<ADD, D>(dst + doff, scale<D>(conv<D, S>(src[so]), p.alpha));
+    }
+}
+
+// Masked destination-ordered gather (copy with MaskType masks, tensor.h:1019-1027): an element
+// is moved only where the given source and destination masks are both nonzero
+template <typename S, typename D, bool ADD>
+__global__ void __launch_bounds__(256) copy_masked_kernel(const DirectArgs p,
+                                                          const float *__restrict__ smask,
+                                                          const float *__restrict__ dmask) {
+    const S *__restrict__ src = (const S *)p.src;
+    D *__restrict__ dst = (D *)p.dstp;
+    for (uint32_t idx = blockIdx.x * 256u + threadIdx.x; idx < p.total; idx += gridDim.x * 256u) {
+        uint32_t rem = idx;
+        long so = 0, doff = 0;
+#pragma unroll
+        for (int i = 0; i < MAXD; ++i) {
+            if (i >= p.nd) break;
+            const uint32_t q = p.size[i].div(rem);
+            const uint32_t c = rem - q * p.size[i].d;
+            rem = q;
+            so += (long)c * p.sst[i];
+            doff += (long)c * p.dst[i];
+        }
+        if ((smask && smask[so] == 0.f) || (dmask && dmask[doff] == 0.f)) continue;
         put<ADD, D>(dst + doff, scale<D>(conv<D, S>(src[so]), p.alpha));
     }
 }
@@ -285,6 +315,27 @@ void launch_pair(const BoxCopyDesc &d, Norm n, long total, hipStream_t stream) {
     Alpha alpha{d.alpha.re, d.alpha.im, d.alpha.is_one() ? 1 : 0};
     const S *src = (const S *)d.src;
     D *dst = (D *)d.dst;
+    if (d.src_mask || d.dst_mask) {
+        if (total >= (1L << 32) - 1) throw Error("copy: masked boxes of 2^32 elements or more are not supported");
+        if ((int)n.size.size() > MAXD) throw Error("copy: too many non-mergeable dimensions");
+        DirectArgs a{};
+        a.nd = (int)n.size.size();
+        a.total = (uint32_t)total;
+        for (int i = 0; i < a.nd; ++i) {
+            a.size[i] = FastDiv((uint32_t)n.size[i]);
+            a.sst[i] = n.ss[i];
+            a.dst[i] = n.ds[i];
+        }
+        a.src = src;
+        a.dstp = dst;
+        a.alpha = alpha;
+        const long blocks = std::min((total + 255) / 256, 8192L);
+        KernelTimer timer("copy", stream);
+        hipLaunchKernelGGL((copy_masked_kernel<S, D, ADD>), dim3((unsigned)blocks), dim3(256), 0,
+                           stream, a, d.src_mask, d.dst_mask);
+        SBX_HIP_CHECK(hipGetLastError());
+        return;
+    }
     // Fully contiguous on both sides
     if (n.size.size() == 1 && n.ss[0] == 1 && n.ds[0] == 1) {
         const long blocks = std::min((total + 255) / 256, 8192L);
@@ -479,6 +530,10 @@ void launch_box_copy(const BoxCopyDesc &d, int device) {
     if (st == SBX_DOUBLE && dt == SBX_FLOAT) return launch_sd<double, float>(d, n, total, s);
     if (st == SBX_CFLOAT && dt == SBX_CDOUBLE) return launch_sd<float2, double2>(d, n, total, s);
     if (st == SBX_CDOUBLE && dt == SBX_CFLOAT) return launch_sd<double2, float2>(d, n, total, s);
+    if (st == SBX_FLOAT && dt == SBX_CFLOAT) return launch_sd<float, float2>(d, n, total, s);
+    if (st == SBX_FLOAT && dt == SBX_CDOUBLE) return launch_sd<float, double2>(d, n, total, s);
+    if (st == SBX_DOUBLE && dt == SBX_CFLOAT) return launch_sd<double, float2>(d, n, total, s);
+    if (st == SBX_DOUBLE && dt == SBX_CDOUBLE) return launch_sd<double, double2>(d, n, total, s);
     if (st == SBX_INT && dt == SBX_SIZE_T) return launch_sd<int, unsigned long>(d, n, total, s);
     if (st == SBX_SIZE_T && dt == SBX_INT) return launch_sd<unsigned long, int>(d, n, total, s);
     throw Error("copy: unsupported type conversion");

@@ -108,7 +108,9 @@ struct DistTensor {
     std::vector<std::vector<Range>> ranges;
     std::vector<void *> ptr;
     std::vector<int> dev;
+    std::vector<const float *> mask; ///< per local component (empty: no masks), copy() only
     int nd() const { return (int)labels.size(); }
+    const float *mask_of(int i) const { return mask.empty() ? nullptr : mask[i]; }
 };
 
 /// A single-component view used by the local kernels

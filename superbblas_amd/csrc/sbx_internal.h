@@ -166,6 +166,9 @@ struct BoxCopyDesc {
     std::vector<long> size, src_stride, dst_stride; // in elements
     Scalar alpha;
     bool add;
+    // optional masks (MaskType = float, laid out like the data they mask, at the box origin):
+    // an element is written only where both given masks are nonzero (tensor.h:1019-1027)
+    const float *src_mask = nullptr, *dst_mask = nullptr;
 };
 void launch_box_copy(const BoxCopyDesc &d, int device);
 

@@ -39,12 +39,16 @@ def ptr(a: np.ndarray):
     return ctypes.c_void_p(a.ctypes.data)
 
 
-def oracle_copy(alpha, o0, from0, size0, dim0, v0, o1, from1, dim1, v1, co=0, add=False):
-    """In place on v1 (numpy)."""
-    rc = oracle().oracle_copy(len(o0), len(o1), scal(alpha), TYPE_OF[v0.dtype], TYPE_OF[v1.dtype],
-                              o0.encode(), ints(from0), ints(size0), ints(dim0), ptr(v0),
-                              o1.encode(), ints(from1), ints(dim1), ptr(v1), co, int(add))
-    assert rc == 0
+def oracle_copy(alpha, o0, from0, size0, dim0, v0, o1, from1, dim1, v1, co=0, add=False,
+                mask0=None, mask1=None):
+    """In place on v1 (numpy); optional float32 masks over the whole origin / destination."""
+    m0 = ptr(mask0) if mask0 is not None else None
+    m1 = ptr(mask1) if mask1 is not None else None
+    rc = oracle().oracle_copy_masked(len(o0), len(o1), scal(alpha), TYPE_OF[v0.dtype],
+                                     TYPE_OF[v1.dtype], o0.encode(), ints(from0), ints(size0),
+                                     ints(dim0), ptr(v0), m0, o1.encode(), ints(from1),
+                                     ints(dim1), ptr(v1), m1, co, int(add))
+    assert rc == 0, "oracle_copy_masked: %d" % rc
 
 
 def oracle_contraction(alpha, o0, from0, size0, dim0, conj0, v0, o1, from1, size1, dim1, conj1,

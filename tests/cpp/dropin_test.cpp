@@ -128,6 +128,30 @@ int main() {
         deallocate(v1, gpu);
     }
 
+    // ---- masked copy between host components (mask0 / mask1, dist.h:3583-3602) ----
+    {
+        Context cpu = createCpuContext();
+        const Coor<2> d{4, 5}, dt{5, 4};
+        std::vector<Z> a(20), b(20, Z(-1));
+        std::vector<MaskType> ma(20), mb(20);
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 5; ++j) {
+                a[i * 5 + j] = Z(i * 5 + j, 1);
+                ma[i * 5 + j] = mb[j * 4 + i] = (i + j) % 2 == 0 ? 1 : 0;
+            }
+        PartitionItem<2> pa{Coor<2>{}, d}, pb{Coor<2>{}, dt};
+        const Z *pa0 = a.data();
+        Z *pb0 = b.data();
+        const MaskType *m0 = ma.data(), *m1 = mb.data();
+        copy<2, 2, Z, Z>(1.0, &pa, 1, "ij", Coor<2>{}, d, d, &pa0, &m0, &cpu, &pb, 1, "ji",
+                         Coor<2>{}, dt, &pb0, &m1, &cpu, SlowToFast, Copy);
+        bool ok = true;
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 5; ++j)
+                ok &= b[j * 4 + i] == ((i + j) % 2 == 0 ? a[i * 5 + j] : Z(-1));
+        CHECK(ok, "masked copy ij -> ji (host components)");
+    }
+
     // ---- BSR: 9-point periodic stencil, 3x3 blocks, x pXYZTSCn -> y pxyztscn (tests/bsr.cpp) ----
     {
         const Coor<6> dim{L, L, L, L, 1, c};

@@ -66,6 +66,25 @@ def case_copy(sb, comm, rank, n, dev):
                     [2, 0, 1, 3], dim1, ref, add=add)
         # untouched destination elements live in their owner's component: compare everything
         assert np.array_equal(out.view(np.uint8), ref.view(np.uint8)), ("copy", add)
+    # masked (parity masks selecting the same elements on both sides, dist.h:3534-3602)
+    from _golden import parity_masks
+    case = {"o0": "xyzt", "o1": "tzyx", "dim0": dim0, "dim1": dim1, "from0": [1, 2, 0, 3],
+            "from1": [2, 0, 1, 3]}
+    gm0, gm1 = parity_masks(case)
+    for add in (False, True):
+        g1 = gen("int", vol(dim1), 2, np.complex128)
+        v0 = scatter(sb, g0, dim0, p0, rank, 1, dev)
+        v1 = scatter(sb, g1, dim1, p1, rank, 1, dev)
+        m0 = scatter(sb, gm0, dim0, p0, rank, 1, dev)
+        m1 = scatter(sb, gm1, dim1, p1, rank, 1, dev)
+        sb.copy(1.0, p0, "xyzt", [1, 2, 0, 3], [3, 4, 2, 5], dim0, v0, p1, "tzyx", [2, 0, 1, 3],
+                dim1, v1, copyadd=sb.Add if add else sb.Copy, comm=comm, mask0=m0, mask1=m1)
+        torch.cuda.synchronize()
+        out = gather(np.zeros_like(g1), dim1, p1, 1, v1)
+        ref = g1.copy()
+        oracle_copy(1.0, "xyzt", [1, 2, 0, 3], [3, 4, 2, 5], dim0, g0, "tzyx", [2, 0, 1, 3],
+                    dim1, ref, add=add, mask0=gm0, mask1=gm1)
+        assert np.array_equal(out.view(np.uint8), ref.view(np.uint8)), ("masked copy", add)
 
 
 def case_contraction(sb, comm, rank, n, dev):

@@ -152,3 +152,52 @@ def test_host_components(gpu):
     sb.copy(1.0, [([0, 0], [6, 4])], "ba", [0, 0], [6, 4], [6, 4], [t1], [([0, 0], dim)], "ab",
             [0, 0], dim, [back])
     assert np.array_equal(back.numpy(), v0)
+
+
+def test_copy_masked_zeroing_and_errors(gpu):
+    """Copy with masks where the origin does not cover the region: the uncovered destination
+    elements are zeroed only where mask1 is nonzero (dist.h:2356-2382 zeroes through a masked
+    local_copy); masked-out elements keep their value.  Complex -> real is rejected."""
+    import torch
+    import superbblas_amd as sb
+    n = 8
+    dim = [n, 6]
+    # origin: two components, the second empty -> rows 4..7 have no origin
+    p0 = [([0, 0], [4, 6]), ([4, 0], [0, 6])]
+    p1 = [([0, 0], dim)]
+    g0 = np.arange(n * 6, dtype=np.float64).reshape(n, 6) + 1
+    v0 = [torch.from_numpy(g0[:4].copy().ravel()).to(gpu), torch.zeros(0, dtype=torch.float64, device=gpu)]
+    m = ((np.arange(n)[:, None] + np.arange(6)[None, :]) % 3 != 0).astype(np.float32)
+    y0 = -np.ones((n, 6))
+    v1 = [torch.from_numpy(y0.ravel().copy()).to(gpu)]
+    m0 = [torch.from_numpy(m[:4].ravel().copy()).to(gpu), torch.zeros(0, dtype=torch.float32, device=gpu)]
+    m1 = [torch.from_numpy(m.ravel().copy()).to(gpu)]
+    sb.copy(1.0, p0, "ab", [0, 0], dim, dim, v0, p1, "ab", [0, 0], dim, v1, mask0=m0, mask1=m1)
+    torch.cuda.synchronize()
+    out = v1[0].cpu().numpy().reshape(n, 6)
+    ref = y0.copy()
+    ref[:4][m[:4] != 0] = g0[:4][m[:4] != 0]
+    ref[4:][m[4:] != 0] = 0
+    assert np.array_equal(out, ref)
+    # complex -> real is not a supported conversion (blas.h:57-65)
+    vc = [torch.zeros(n * 6, dtype=torch.complex128, device=gpu)]
+    with pytest.raises(sb.SuperbblasError, match="conversion"):
+        sb.copy(1.0, p1, "ab", [0, 0], dim, dim, vc, p1, "ab", [0, 0], dim, v1)
+    with pytest.raises(sb.SuperbblasError, match="mask1"):
+        sb.copy(1.0, p1, "ab", [0, 0], dim, dim, v1, p1, "ab", [0, 0], dim, v1, mask0=m1)
+
+
+@pytest.mark.parametrize("t0,t1", [(np.float32, np.complex64), (np.float32, np.complex128),
+                                   (np.float64, np.complex64), (np.float64, np.complex128)])
+def test_copy_real_to_complex(gpu, t0, t1):
+    import torch
+    import superbblas_amd as sb
+    dim0, dim1 = [5, 7, 3], [3, 5, 7]
+    g = (np.arange(105) - 50).astype(t0)
+    v0 = [torch.from_numpy(g).to(gpu)]
+    v1 = [torch.from_numpy(np.full(105, 9 + 9j, t1)).to(gpu)]
+    sb.copy(2.0, [([0, 0, 0], dim0)], "abc", [0, 0, 0], dim0, dim0, v0, [([0, 0, 0], dim1)],
+            "cab", [0, 0, 0], dim1, v1)
+    torch.cuda.synchronize()
+    ref = (2.0 * g.reshape(dim0).transpose(2, 0, 1)).astype(t1).ravel()
+    assert np.array_equal(v1[0].cpu().numpy(), ref)

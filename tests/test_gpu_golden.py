@@ -8,7 +8,7 @@ bit-exact."""
 import numpy as np
 import pytest
 
-from _golden import NPT, gen, manifest, output, piece, put_piece, vol
+from _golden import NPT, gen, manifest, output, parity_masks, piece, put_piece, vol
 
 pytestmark = pytest.mark.gpu
 
@@ -39,10 +39,15 @@ def test_golden_copy(gpu, case):
     g1 = gen(case["gen1"], vol(case["dim1"]), 2, t1)
     v0 = _scatter(g0, case["dim0"], case["p0"], gpu)
     v1 = _scatter(g1, case["dim1"], case["p1"], gpu)
+    m0 = m1 = None
+    if case.get("mask"):
+        gm0, gm1 = parity_masks(case)
+        m0 = _scatter(gm0, case["dim0"], case["p0"], gpu)
+        m1 = _scatter(gm1, case["dim1"], case["p1"], gpu)
     sb.copy(complex(*case["alpha"]) if np.dtype(t0).kind == "c" else case["alpha"][0],
             case["p0"], case["o0"], case["from0"], case["size0"], case["dim0"], v0,
             case["p1"], case["o1"], case["from1"], case["dim1"], v1,
-            copyadd=sb.Add if case["add"] else sb.Copy)
+            copyadd=sb.Add if case["add"] else sb.Copy, mask0=m0, mask1=m1)
     torch.cuda.synchronize()
     out = _gather(v1, case["dim1"], case["p1"], t1)
     ref = output(case, t1)

@@ -4,7 +4,7 @@ import numpy as np
 import pytest
 
 from _common import oracle_bsr, oracle_contraction, oracle_copy, oracle_kron_bsr, T_CDOUBLE
-from _golden import NPT, gen, manifest, output, vol
+from _golden import NPT, gen, manifest, output, parity_masks, vol
 
 
 def _is_replicated(p, dim):
@@ -17,10 +17,11 @@ def test_oracle_copy(case):
     v0 = gen(case["gen0"], vol(case["dim0"]), 1, t0)
     v1 = gen(case["gen1"], vol(case["dim1"]), 2, t1)
     reps = len(case["p0"]) if (case["add"] and _is_replicated(case["p0"], case["dim0"])) else 1
+    m0, m1 = parity_masks(case) if case.get("mask") else (None, None)
     for _ in range(reps):
         oracle_copy(complex(*case["alpha"]), case["o0"], case["from0"], case["size0"],
                     case["dim0"], v0, case["o1"], case["from1"], case["dim1"], v1,
-                    add=case["add"])
+                    add=case["add"], mask0=m0, mask1=m1)
     ref = output(case, t1)
     assert np.array_equal(v1.view(np.uint8), ref.view(np.uint8))
 
