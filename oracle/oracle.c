@@ -381,6 +381,62 @@ int oracle_bsr(int t, int nd, const int *dimd, int co, long block_rows, int bi, 
 }
 
 /*
+ * Conjugate-transposed BSR product on one component, y = alpha * A^H x (+ y if add): what the
+ * reference's GPU path asks hipsparse bsrmm for with HIPSPARSE_OPERATION_CONJUGATE_TRANSPOSE
+ * when x holds the image labels (transSp, bsr.h:1001-1029, 1942; the CPU builtin operator
+ * throws "Not implemented" for it, bsr.h:536-538, so this restatement is not pinned by
+ * reference outputs).  Same arguments as oracle_bsr; x is indexed by image rows (r*bi + c) and
+ * y by domain rows (d0 + e); y has `ydim` rows.
+ */
+int oracle_bsr_adjoint(int t, int nd, const int *dimd, int co, long block_rows, int bi, int bd,
+                       const int *ii, const int *jj, const void *v, int block_im_fast,
+                       const void *x, long ldx, int x_row_major, void *y, long ldy,
+                       int y_row_major, long ydim, long ncols, const double *alpha, int add) {
+    long sd[64];
+    get_strides(nd, dimd, co, sd);
+    const int cplx = is_complex(t);
+    double *acc = (double *)calloc((size_t)(2 * ydim * ncols), sizeof(double));
+    long j = 0;
+    for (long r = 0; r < block_rows; ++r)
+        for (int q = 0; q < ii[r]; ++q, ++j) {
+            const int *cj = jj + j * nd;
+            if (cj[0] == -1) continue;
+            long d0 = 0;
+            for (int k = 0; k < nd; ++k) d0 += (long)normalize_coor(cj[k], dimd[k]) * sd[k];
+            for (int c = 0; c < bi; ++c)
+                for (int e = 0; e < bd; ++e) {
+                    double ar, ai;
+                    load(t, v, j * bi * bd + (block_im_fast ? c + (long)e * bi : (long)c * bd + e),
+                         &ar, &ai);
+                    ai = -ai; /* conjugate */
+                    const long row = r * bi + c, d = d0 + e;
+                    for (long col = 0; col < ncols; ++col) {
+                        double xr, xi;
+                        load(t, x, x_row_major ? row * ldx + col : row + col * ldx, &xr, &xi);
+                        acc[2 * (d * ncols + col)] += ar * xr - ai * xi;
+                        acc[2 * (d * ncols + col) + 1] += ar * xi + ai * xr;
+                    }
+                }
+        }
+    for (long d = 0; d < ydim; ++d)
+        for (long col = 0; col < ncols; ++col) {
+            const double sr = acc[2 * (d * ncols + col)], si = acc[2 * (d * ncols + col) + 1];
+            double rr = alpha[0] * sr - (cplx ? alpha[1] * si : 0);
+            double ri = cplx ? alpha[0] * si + alpha[1] * sr : 0;
+            const long yi = y_row_major ? d * ldy + col : d + col * ldy;
+            if (add) {
+                double wr, wi;
+                load(t, y, yi, &wr, &wi);
+                rr += wr;
+                ri += wi;
+            }
+            store(t, y, yi, rr, ri);
+        }
+    free(acc);
+    return 0;
+}
+
+/*
  * Kronecker BSR operator on one component (create_kron_bsr -> get_kron_indices
  * bsr.h:1485-1537, builtin CPU operator bsr.h:587-648): every block row has `nnz` nonzero
  * blocks and the nonzero at position mu of a row also carries kron[mu], a ki x kd matrix

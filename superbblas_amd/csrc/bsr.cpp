@@ -13,7 +13,8 @@
 //    nonzero position of the block rows; x and y are then row major with the Kronecker labels
 //    fastest, (D, d, C, kd) and (I, i, C, ki), the layout the reference's planner suggests for
 //    them (bsr.h:1914-1928), and the local product runs kernels_bsr_kron.hip.
-// Not yet supported: contracting with the image side of the operator (transposed application).
+//  * contracting with the image side (x has the image labels) applies A^H: a conj-transposed
+//    operator built on first use (make_transposed), whose overlapping image pieces are summed.
 #include "plan.h"
 
 #include <algorithm>
@@ -28,6 +29,8 @@ struct BsrComp {
     const void *v = nullptr;
     const void *kron = nullptr; // Kronecker matrices (user memory, device)
     int nnz_per_row = -1;
+    std::vector<int> h_rowptr, h_jj; // host copies of the pattern (for the transposed operator)
+    void *owned_v = nullptr;         // values owned by the operator (transposed operator)
 };
 
 struct BsrOp {
@@ -40,6 +43,8 @@ struct BsrOp {
     std::vector<std::vector<Range>> pi, pd; // SlowToFast, all ranks
     std::vector<BsrComp> comps;             // this rank's components
     int co = SBX_SLOW_TO_FAST;
+    bool image_overlaps = false; // image ranges of different components overlap (transposed op)
+    mutable std::unique_ptr<BsrOp> transposed; // A^H, built on the first image-side contraction
     ~BsrOp() {
         for (auto &c : comps) {
             if (c.dev >= 0) {
@@ -48,6 +53,7 @@ struct BsrOp {
             }
             if (c.ii) (void)hipFree(c.ii);
             if (c.jj) (void)hipFree(c.jj);
+            if (c.owned_v) (void)hipFree(c.owned_v);
         }
     }
 };
@@ -159,10 +165,102 @@ BsrOp *bsr_create(int nd, int ni, int dtype, const std::vector<std::vector<Range
         SBX_HIP_CHECK(hipMemcpy(bc.ii, rowptr.data(), sizeof(int) * (nii + 1), hipMemcpyHostToDevice));
         if (nnz > 0)
             SBX_HIP_CHECK(hipMemcpy(bc.jj, hjj.data(), sizeof(int) * nnz, hipMemcpyHostToDevice));
+        if (!op->is_kron) {
+            bc.h_rowptr = std::move(rowptr);
+            bc.h_jj = std::move(hjj);
+        }
         op->comps.push_back(bc);
     }
     return op.release();
 }
+
+namespace {
+
+/// The conjugate transpose A^H of a (non-Kronecker) operator, for contractions with the image
+/// side of A (the reference's transSp: hipsparse bsrmm with CONJUGATE_TRANSPOSE,
+/// bsr.h:1001-1029, 1942): image partition = A's domain partition (which may overlap across
+/// components: the halos), domain partition = A's image partition, blocks conj-transposed and
+/// regrouped by block column.
+BsrOp *make_transposed(const BsrOp &a) {
+    if (a.is_kron) throw Error("bsr_krylov: contracting with the image space of a Kronecker operator is not supported");
+    std::unique_ptr<BsrOp> t(new BsrOp());
+    t->nd = a.ni;
+    t->ni = a.nd;
+    t->dtype = a.dtype;
+    t->dimi = a.dimd;
+    t->dimd = a.dimi;
+    t->blocki = a.blockd;
+    t->blockd = a.blocki;
+    t->kroni = a.krond;
+    t->krond = a.kroni;
+    t->block_im_fast = !a.block_im_fast; // the same block storage read transposed
+    t->nprocs = a.nprocs;
+    t->rank = a.rank;
+    t->ncomponents = a.ncomponents;
+    t->pi = a.pd;
+    t->pd = a.pi;
+    t->co = a.co;
+    // do image ranges (A's domain ranges) of different components overlap?
+    std::vector<Range> all;
+    for (auto &r : a.pd)
+        for (auto &q : r) all.push_back(q);
+    for (std::size_t i = 0; i < all.size() && !t->image_overlaps; ++i)
+        for (std::size_t j = i + 1; j < all.size(); ++j)
+            if (volume(all[i].size) > 0 && volume(all[j].size) > 0 &&
+                !intersection(all[i], all[j], a.dimd).empty()) {
+                t->image_overlaps = true;
+                break;
+            }
+    const long bi = volume(a.blocki), bd = volume(a.blockd);
+    const std::size_t es = dtype_size(a.dtype);
+    for (int c = 0; c < (int)a.comps.size(); ++c) {
+        const BsrComp &ac = a.comps[c];
+        BsrComp bc;
+        bc.dev = ac.dev;
+        const Range &rd = a.pd[a.rank][c];
+        const long ncb = bd > 0 ? volume(rd.size) / bd : 0; // A's block columns = A^H's block rows
+        if (ac.block_rows == 0 || ncb == 0) {
+            t->comps.push_back(bc);
+            continue;
+        }
+        bc.block_rows = ncb;
+        const std::vector<int> &rp = ac.h_rowptr, &jj = ac.h_jj;
+        std::vector<int> cnt(ncb + 1, 0);
+        for (int k = 0; k < rp.back(); ++k)
+            if (jj[k] >= 0) ++cnt[jj[k] / bd + 1];
+        for (long q = 0; q < ncb; ++q) cnt[q + 1] += cnt[q];
+        const int nnz = cnt[ncb];
+        std::vector<int> pos(cnt.begin(), cnt.end() - 1), tjj(std::max(nnz, 1)), perm(std::max(nnz, 1));
+        for (long i = 0; i < ac.block_rows; ++i)
+            for (int k = rp[i]; k < rp[i + 1]; ++k) {
+                if (jj[k] < 0) continue;
+                const int q = pos[jj[k] / bd]++;
+                tjj[q] = (int)(i * bi); // first element of A's block row i
+                perm[q] = k;
+            }
+        bool same = true;
+        for (long q = 0; q < ncb; ++q) same &= (cnt[q + 1] - cnt[q] == cnt[1] - cnt[0]);
+        bc.nnz_per_row = same ? cnt[1] - cnt[0] : -1;
+        set_device(bc.dev);
+        SBX_HIP_CHECK(hipMalloc(&bc.ii, sizeof(int) * (ncb + 1)));
+        SBX_HIP_CHECK(hipMalloc(&bc.jj, sizeof(int) * std::max(nnz, 1)));
+        SBX_HIP_CHECK(hipMemcpy(bc.ii, cnt.data(), sizeof(int) * (ncb + 1), hipMemcpyHostToDevice));
+        SBX_HIP_CHECK(hipMemcpy(bc.jj, tjj.data(), sizeof(int) * std::max(nnz, 1), hipMemcpyHostToDevice));
+        // values: block perm[q] of A, conjugated, at position q
+        SBX_HIP_CHECK(hipMalloc(&bc.owned_v, es * bi * bd * std::max(nnz, 1)));
+        Scratch dperm(sizeof(int) * std::max(nnz, 1), bc.dev);
+        SBX_HIP_CHECK(hipMemcpyAsync(dperm.ptr, perm.data(), sizeof(int) * std::max(nnz, 1),
+                                     hipMemcpyHostToDevice, get_stream(bc.dev)));
+        launch_gather_blocks(a.dtype, ac.v, (const int *)dperm.ptr, nnz, bi * bd, true,
+                             bc.owned_v, bc.dev);
+        SBX_HIP_CHECK(hipStreamSynchronize(get_stream(bc.dev)));
+        bc.v = bc.owned_v;
+        t->comps.push_back(std::move(bc));
+    }
+    return t.release();
+}
+
+} // namespace
 
 void bsr_destroy(BsrOp *op) { delete op; }
 
@@ -215,6 +313,21 @@ void bsr_krylov(const BsrOp &op, const Scalar &alpha, const std::string &oi,
     if ((int)oi.size() != op.ni || (int)od.size() != op.nd)
         throw Error("bsr_krylov: labels don't match the operator");
     if (comm.nprocs != op.nprocs) throw Error("bsr_krylov: communicator mismatch");
+    // Contraction with the image side (x has image labels, y domain labels): y = alpha A^H x,
+    // applied as the transposed operator (bsr.h:1737-1760 kinds, 1942 transSp)
+    bool x_image = false, x_domain = false;
+    for (char c : x.labels) {
+        x_image |= oi.find(c) != std::string::npos;
+        x_domain |= od.find(c) != std::string::npos;
+    }
+    if (x_image && x_domain)
+        throw Error("Unsupported to contract dense input tensor with domain and image dimensions "
+                    "of the sparse tensor");
+    if (x_image) {
+        if (!op.transposed) op.transposed.reset(make_transposed(op));
+        return bsr_krylov(*op.transposed, alpha, od, oi, x, fromx, sizex, beta, y, fromy, sizey,
+                          okr, comm);
+    }
     // Label classes (bsr.h:1722-1795): x has domain labels + C (+ okr); y image labels + C (+okr)
     std::string C;
     for (int i = 0; i < x.nd(); ++i) {
@@ -225,8 +338,6 @@ void bsr_krylov(const BsrOp &op, const Scalar &alpha, const std::string &oi,
                             "sparse tensor");
             continue;
         }
-        if (oi.find(c) != std::string::npos)
-            throw Error("bsr_krylov: contracting with the image space is not supported yet");
         if (okr != 0 && c == okr) {
             if (sizex[i] > 1)
                 throw Error("The power dimension on the input vector has a size larger than one");
@@ -426,6 +537,10 @@ void bsr_krylov(const BsrOp &op, const Scalar &alpha, const std::string &oi,
     const Coor from0(ly.size(), 0), size0 = ty.dim;
     if (need_y && !beta.is_zero() && !beta.is_one())
         dist_copy(beta, y, fromy, sizey, y, fromy, false, comm);
+    // overlapping image pieces (A^H with a halo domain) are summed: add into a zeroed output
+    const bool add_y = !beta.is_zero() || op.image_overlaps;
+    if (need_y && beta.is_zero() && op.image_overlaps)
+        dist_copy(Scalar{0, 0}, y, fromy, sizey, y, fromy, false, comm);
     const int power_pos = okr != 0 ? (int)y.labels.find(okr) : -1;
     for (int pw = 0; pw < power; ++pw) {
         // Local SpMM
@@ -465,7 +580,7 @@ void bsr_krylov(const BsrOp &op, const Scalar &alpha, const std::string &oi,
             Coor fy = fromy;
             if (power_pos >= 0)
                 fy[power_pos] = (int)normalize_coor((long)fy[power_pos] + pw, y.dim[power_pos]);
-            dist_copy(Scalar{1, 0}, ty, from0, size0, y, fy, !beta.is_zero(), comm);
+            dist_copy(Scalar{1, 0}, ty, from0, size0, y, fy, add_y, comm);
         }
         if (pw + 1 == power) break;
         // The next power applies the operator to this one: the image pieces, relabelled as
@@ -474,7 +589,12 @@ void bsr_krylov(const BsrOp &op, const Scalar &alpha, const std::string &oi,
         for (char &ch : ty_as_x.labels)
             if (oi.find(ch) != std::string::npos) ch = od[oi.find(ch)];
         Coor zx(lx.size(), 0);
-        dist_copy(Scalar{1, 0}, ty_as_x, zx, size0, tx, zx, false, comm);
+        if (op.image_overlaps) {
+            dist_copy(Scalar{0, 0}, tx, zx, tx.dim, tx, zx, false, comm);
+            dist_copy(Scalar{1, 0}, ty_as_x, zx, size0, tx, zx, true, comm);
+        } else {
+            dist_copy(Scalar{1, 0}, ty_as_x, zx, size0, tx, zx, false, comm);
+        }
     }
 }
 

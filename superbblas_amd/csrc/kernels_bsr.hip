@@ -398,7 +398,47 @@ void launch_typed(const BsrArgs &a, int nnz_per_row, bool yrow, bool xrow, hipSt
         launch_layouts<E, 0, 0>(a, yrow, xrow, blocks, s);
 }
 
+template <typename E> __device__ __forceinline__ E conj_of(E v) { return v; }
+template <> __device__ __forceinline__ double2 conj_of<double2>(double2 v) { return double2{v.x, -v.y}; }
+template <> __device__ __forceinline__ float2 conj_of<float2>(float2 v) { return float2{v.x, -v.y}; }
+
+template <typename E>
+__global__ void __launch_bounds__(256) gather_blocks_kernel(const E *__restrict__ src,
+                                                            const int *__restrict__ perm,
+                                                            long nblocks, long be, int conj,
+                                                            E *__restrict__ dst) {
+    const long total = nblocks * be;
+    for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256L) {
+        const long q = idx / be, e = idx - q * be;
+        const E v = src[(long)perm[q] * be + e];
+        dst[idx] = conj ? conj_of<E>(v) : v;
+    }
+}
+
+template <typename E>
+void gather_typed(const void *src, const int *perm, long nblocks, long be, bool cj, void *dst,
+                  hipStream_t s) {
+    const long blocks = std::min((nblocks * be + 255) / 256, 65536L);
+    hipLaunchKernelGGL(gather_blocks_kernel<E>, dim3((unsigned)blocks), dim3(256), 0, s,
+                       (const E *)src, perm, nblocks, be, cj ? 1 : 0, (E *)dst);
+    SBX_HIP_CHECK(hipGetLastError());
+}
+
 } // namespace
+
+void launch_gather_blocks(int t, const void *src, const int *perm, long nblocks, long block_elems,
+                          bool conj_values, void *dst, int device) {
+    if (nblocks == 0 || block_elems == 0) return;
+    set_device(device);
+    hipStream_t s = get_stream(device);
+    switch (t) {
+    case SBX_CDOUBLE: return gather_typed<double2>(src, perm, nblocks, block_elems, conj_values, dst, s);
+    case SBX_CFLOAT: return gather_typed<float2>(src, perm, nblocks, block_elems, conj_values, dst, s);
+    case SBX_DOUBLE: return gather_typed<double>(src, perm, nblocks, block_elems, false, dst, s);
+    case SBX_FLOAT: return gather_typed<float>(src, perm, nblocks, block_elems, false, dst, s);
+    default: throw Error("bsr: unsupported type");
+    }
+}
 
 void launch_bsr(const BsrDesc &d, int device) {
     if (d.block_rows == 0 || d.ncols == 0) return;

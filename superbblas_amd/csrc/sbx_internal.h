@@ -202,5 +202,8 @@ struct BsrDesc {
 };
 void launch_bsr(const BsrDesc &d, int device);
 void launch_bsr_kron(const BsrDesc &d, int device);
+/// dst block q = (conj if conj_values) src block perm[q], q < nblocks, blocks of block_elems
+void launch_gather_blocks(int t, const void *src, const int *perm, long nblocks, long block_elems,
+                          bool conj_values, void *dst, int device);
 
 } // namespace sbx

@@ -90,6 +90,22 @@ def oracle_bsr(t, dimd, co, block_rows, bi, bd, ii, jj, v, block_im_fast, x, ldx
     assert rc == 0
 
 
+def oracle_bsr_adjoint(t, dimd, co, block_rows, bi, bd, ii, jj, v, block_im_fast, x, ldx,
+                       x_row_major, y, ldy, y_row_major, ydim, ncols, alpha, add=False):
+    """y = alpha A^H x on one component (x by image rows, y by domain rows)."""
+    o = oracle()
+    o.oracle_bsr_adjoint.argtypes = [
+        ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_int,
+        ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+        ctypes.c_void_p, ctypes.c_long, ctypes.c_int, ctypes.c_void_p, ctypes.c_long,
+        ctypes.c_int, ctypes.c_long, ctypes.c_long, ctypes.c_void_p, ctypes.c_int]
+    rc = o.oracle_bsr_adjoint(t, len(dimd), ctypes.cast(ints(dimd), ctypes.c_void_p), co,
+                              block_rows, bi, bd, ptr(ii), ptr(jj), ptr(v), int(block_im_fast),
+                              ptr(x), ldx, int(x_row_major), ptr(y), ldy, int(y_row_major), ydim,
+                              ncols, ctypes.cast(scal(alpha), ctypes.c_void_p), int(add))
+    assert rc == 0
+
+
 def oracle_kron_bsr(t, site_dim, co, block_rows, nnz, bi, bd, ki, kd, jj, v, kron, block_im_fast,
                     x, y, ncols, alpha, add=False):
     """Kronecker BSR on one component, x (site, d, col, b) and y (row, i, col, a) row major."""

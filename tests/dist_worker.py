@@ -212,6 +212,25 @@ def case_bsr(sb, comm, rank, n, dev, ncols=3):
                np.array(jg, np.int32).ravel(), allv.ravel(), False, ref, ncols, True, ref2, ncols,
                True, ncols, 1.0)
     assert np.array_equal(out2, np.concatenate([ref, ref2])), "bsr powers"
+    # image side: y (domain labels) = A^H x (image labels); the halo contributions of every rank
+    # are summed into their owners
+    from _common import oracle_bsr_adjoint
+    op = sb.create_bsr(pi, dim, pd, dim, [1, 1, 1, 1, 1, 3], [1, 1, 1, 1, 1, 3], False,
+                       [torch.from_numpy(ii).to(dev)],
+                       [torch.from_numpy(np.array(jj, np.int32).ravel()).to(dev)],
+                       [torch.from_numpy(vals).to(dev)], comm=comm)
+    vx = scatter(sb, gx, dimx, px, rank, 1, dev)
+    vy = scatter(sb, gy, dimx, px, rank, 1, dev)
+    sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", px, "pxyztscn", z8, dimx, dimx, vx, 0.0, px,
+                  "pXYZTSCn", z8, dimx, dimx, None, vy, comm=comm)
+    torch.cuda.synchronize()
+    op.destroy()
+    out3 = gather(np.zeros_like(gy), dimx, px, 1, vy)
+    ref3 = np.zeros_like(gy)
+    oracle_bsr_adjoint(T_CDOUBLE, dim, 0, V, b, b, np.full(V, 9, np.int32),
+                       np.array(jg, np.int32).ravel(), allv.ravel(), False, gx, ncols, True, ref3,
+                       ncols, True, V * b, ncols, 1.0)
+    assert np.array_equal(out3, ref3), "bsr image side"
 
 
 def case_kron(sb, comm, rank, n, dev, ncols=2, power=2):

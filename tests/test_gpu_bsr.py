@@ -137,3 +137,44 @@ def test_bsr_powers(gpu, spin, color, ncols, power):
     torch.cuda.synchronize()
     op.destroy()
     assert rel_err(ty.cpu().numpy(), yref) < 1e-13
+
+
+@pytest.mark.parametrize("spin,color,ncols,beta,power", [(1, 3, 2, 0.0, 1), (4, 3, 3, 0.5, 1),
+                                                        (1, 3, 2, 1.0, 2)])
+def test_bsr_image_side(gpu, spin, color, ncols, beta, power):
+    """x with the image labels, y with the domain labels: y = alpha A^H x + beta y (the
+    reference's transSp, bsr.h:1942, hipsparse CONJUGATE_TRANSPOSE)."""
+    import torch
+    import superbblas_amd as sb
+    from _common import oracle_bsr_adjoint
+    L = 4
+    dim, ii, jj, vals, nb = lattice_operator(L, spin, color)
+    b = spin * color
+    vol = L ** 4
+    n = vol * b * ncols
+    g = np.arange(n)
+    x = ((g % 7 - 3) + 1j * (g % 5 - 2)).astype(np.complex128)
+    y0 = ((np.arange(n * power) % 3 - 1) + 1j).astype(np.complex128)
+    alpha = 1 - 1j
+    refs, cur = [], x
+    for _ in range(power):
+        nxt = np.zeros_like(x)
+        oracle_bsr_adjoint(T_CDOUBLE, dim, 0, vol, b, b, ii, jj, vals, False, cur, ncols, True,
+                           nxt, ncols, True, vol * b, ncols, 1.0)
+        refs.append(nxt)
+        cur = nxt
+    yref = np.concatenate([alpha * r + beta * y0[p * n:(p + 1) * n] for p, r in enumerate(refs)])
+    full = [([0] * 6, dim)]
+    blk = [1, 1, 1, 1, spin, color]
+    op = sb.create_bsr(full, dim, full, dim, blk, blk, False, [torch.from_numpy(ii).to(gpu)],
+                       [torch.from_numpy(jj).to(gpu)], [torch.from_numpy(vals).to(gpu)])
+    dimx = [1, L, L, L, L, spin, color, ncols]
+    dimy = [power] + dimx[1:]
+    tx = torch.from_numpy(x).to(gpu)
+    ty = torch.from_numpy(y0.copy()).to(gpu)
+    sb.bsr_krylov(alpha, op, "xyztsc", "XYZTSC", [([0] * 8, dimx)], "pxyztscn", [0] * 8, dimx,
+                  dimx, [tx], beta, [([0] * 8, dimy)], "pXYZTSCn", [0] * 8, dimy, dimy,
+                  "p" if power > 1 else None, [ty])
+    torch.cuda.synchronize()
+    op.destroy()
+    assert np.array_equal(ty.cpu().numpy(), yref)

@@ -125,3 +125,22 @@ def test_make_hole():
     for c in manifest("hole"):
         r = sb.make_hole(c["from"], c["size"], c["hfrom"], c["hsize"], c["dim"])
         assert [[list(f), list(s)] for f, s in r] == c["r"], c
+
+
+def test_oracle_bsr_adjoint_identity():
+    """The A^H restatement (the reference's CPU path has none: bsr.h:536-538) is pinned through
+    the golden-pinned forward product: <y, A x> = <A^H y, x> on the lattice operator."""
+    from _common import oracle_bsr_adjoint
+    L, spin, color, ncols = 4, 1, 3, 2
+    b = spin * color
+    V = L ** 4
+    ii, jj, vals = lattice_operator(L, spin, color)
+    x = gen("int", V * b * ncols, 5, np.complex128)
+    y = gen("int", V * b * ncols, 6, np.complex128)
+    ax = np.zeros_like(x)
+    oracle_bsr(T_CDOUBLE, [L, L, L, L, spin, color], 0, V, b, b, ii, jj, vals, False, x, ncols,
+               True, ax, ncols, True, ncols, 1.0)
+    ahy = np.zeros_like(y)
+    oracle_bsr_adjoint(T_CDOUBLE, [L, L, L, L, spin, color], 0, V, b, b, ii, jj, vals, False, y,
+                       ncols, True, ahy, ncols, True, V * b, ncols, 1.0)
+    assert np.vdot(y, ax) == np.vdot(ahy, x)
