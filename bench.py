@@ -77,6 +77,26 @@ def cpu_baseline(threads):
             "kind": "port", "sample": "oracle xgemm_batch_strided 'T','N' 64x64x1536 batch 8"}
 
 
+def cpu_side_baselines(threads):
+    """The reference's CPU path for the side measurements (permute config 2p, BSR config 3),
+    bounded samples of the same workloads, timed beside the GPU numbers (rank 0, N = 1)."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "ref_bench")
+    if not os.path.exists(exe):
+        return {}
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads), OPENBLAS_NUM_THREADS="1")
+    out = {}
+    for key, args in (("permute", ["permute", "16", "64", "1"]), ("bsr", ["bsr", "16", "12", "2"])):
+        try:
+            r = subprocess.run([exe] + args, env=env, timeout=300, capture_output=True, text=True,
+                               check=True).stdout
+            r = json.loads(r.strip().splitlines()[-1])
+            out["%s_cpu_reference_GBps" % key] = round(r["gbps"], 3)
+        except Exception as e:  # pragma: no cover
+            out["%s_cpu_reference_error" % key] = str(e)[:200]
+    out["cpu_reference_threads"] = threads
+    return out
+
+
 def pmc_traffic(*kernel_substrs):
     """HBM bytes per launch of a kernel from the latest committed PMC pass (profiles/rNN_pmc.json,
     made by tools/pmc_summary.py from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of this
@@ -204,6 +224,8 @@ def main():
     base = None
     if rank == 0 and not args.no_cpu:
         base = cpu_baseline(int(os.environ.get("OMP_NUM_THREADS", "16")))
+        if world == 1 and not args.no_side:
+            side.update(cpu_side_baselines(int(os.environ.get("OMP_NUM_THREADS", "16"))))
 
     traffic, traffic_src = pmc_traffic("dma_kernel<", "128, 128, 8, 4, 2>")
     if rank == 0:

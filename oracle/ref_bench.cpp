@@ -97,6 +97,56 @@ int main(int argc, char **argv) {
         std::printf("{\"op\": \"permute\", \"L\": %d, \"n\": %d, \"seconds\": %.6g, "
                     "\"gbps\": %.6g, \"threads\": %d}\n",
                     L, n, t, bytes / t / 1e9, threads());
+    } else if (what == "bsr") {
+        // config 3: 16^4 periodic 9-point stencil (tests/bsr.cpp:169-255), 3x3 color blocks,
+        // n = the number of rhs, x pXYZTSCn -> y pxyztscn, the builtin CPU operator
+        // (bsr.h:535-650: OpenMP over block rows, one small GEMM per nonzero block)
+        const Coor<6> dim{L, L, L, L, 1, 3};
+        const std::size_t V = (std::size_t)L * L * L * L;
+        std::vector<IndexType> ii(V, 9);
+        std::vector<Coor<6>> jj;
+        for (std::size_t i = 0; i < V; ++i) {
+            Coor<6> c{(int)(i / (L * L * L)), (int)(i / (L * L) % L), (int)(i / L % L),
+                      (int)(i % L), 0, 0};
+            jj.push_back(c);
+            for (int d = 0; d < 4; ++d)
+                for (int dir = -1; dir < 2; dir += 2) {
+                    Coor<6> q = c;
+                    q[d] = (q[d] + dir + L) % L;
+                    jj.push_back(q);
+                }
+        }
+        std::vector<Z> v(V * 9 * 9);
+        for (std::size_t i = 0; i < v.size(); ++i) v[i] = Z(std::sin(0.1 * i), std::cos(0.3 * i));
+        std::vector<PartitionItem<6>> pop(1, PartitionItem<6>{Coor<6>{}, dim});
+        IndexType *iip = ii.data();
+        Coor<6> *jjp = jj.data();
+        const Z *vp = v.data();
+        const Coor<6> block{1, 1, 1, 1, 1, 3};
+        BSR_handle *op = nullptr;
+        create_bsr<6, 6, Z>(pop.data(), dim, pop.data(), dim, 1, block, block, false, &iip, &jjp,
+                            &vp, &cpu, SlowToFast, &op);
+        const Coor<8> dx{1, L, L, L, L, 1, 3, n};
+        std::vector<Z> x(detail::volume(dx)), y(detail::volume(dx));
+        for (std::size_t i = 0; i < x.size(); ++i) x[i] = Z(std::cos(0.2 * i), std::sin(0.7 * i));
+        std::vector<PartitionItem<8>> px(1, PartitionItem<8>{Coor<8>{}, dx});
+        const Z *pxp = x.data();
+        Z *pyp = y.data();
+        auto run = [&] {
+            bsr_krylov<6, 6, 8, 8, Z>(Z{1}, op, "xyztsc", "XYZTSC", px.data(), 1, "pXYZTSCn",
+                                      Coor<8>{}, dx, dx, &pxp, Z{0}, px.data(), "pxyztscn",
+                                      Coor<8>{}, dx, dx, 'p', &pyp, &cpu, SlowToFast);
+        };
+        run();
+        double t = now();
+        for (int r = 0; r < reps; ++r) run();
+        t = (now() - t) / reps;
+        destroy_bsr(op);
+        // the library's algorithmic bytes of one application
+        const double bytes = 16.0 * (81.0 * V + 2.0 * 3 * V * n) + 4.0 * (9.0 * V + V + 1);
+        std::printf("{\"op\": \"bsr\", \"L\": %d, \"n\": %d, \"seconds\": %.6g, "
+                    "\"gbps\": %.6g, \"gflops\": %.6g, \"threads\": %d}\n",
+                    L, n, t, bytes / t / 1e9, 8.0 * 81 * V * n / t / 1e9, threads());
     } else {
         std::fprintf(stderr, "unknown op\n");
         return 1;
