@@ -541,6 +541,123 @@ void bsr_get_preferred_layout(BSR_handle *bsrh, int ncomponents, const Context *
     }
 }
 
+// ---- dense batched solvers (dense.h:1160-1290) ----
+
+namespace sbx_detail {
+template <std::size_t N, typename T, typename F>
+void inplace_dense_impl(F fn, const PartitionItem<N> *p, const Coor<N> &dim, int ncomponents,
+                        const char *o, T **v, const char *orows, const char *ocols,
+                        const Context *ctx, sbx_comm comm, CoorOrder co, Session session) {
+    check_session(session);
+    const auto c = contexts(ctx, ncomponents);
+    check(fn((int)N, dtype<T>::value, parts(p), dim.data(), ncomponents, o, (void *const *)v,
+             orows, ocols, c.data(), comm, co_of(co), 0));
+}
+
+template <std::size_t Nc, std::size_t Nx, std::size_t Ny, typename T, typename F>
+void solve_dense_impl(F fn, T alpha, const PartitionItem<Nc> *pc, const Coor<Nc> &dimc,
+                      int ncomponentsc, const char *oc, const T **vc, const char *orows,
+                      const char *ocols, const Context *ctxc, const PartitionItem<Nx> *px,
+                      const Coor<Nx> &dimx, int ncomponentsx, const char *ox, const T **vx,
+                      const Context *ctxx, const PartitionItem<Ny> *py, const Coor<Ny> &dimy,
+                      int ncomponentsy, const char *oy, T **vy, const Context *ctxy, sbx_comm comm,
+                      CoorOrder co, Session session) {
+    check_session(session);
+    const auto a = scalar(alpha);
+    const auto c0 = contexts(ctxc, ncomponentsc), c1 = contexts(ctxx, ncomponentsx),
+               c2 = contexts(ctxy, ncomponentsy);
+    check(fn((int)Nc, (int)Nx, (int)Ny, dtype<T>::value, a.data(), parts(pc), dimc.data(),
+             ncomponentsc, oc, (const void *const *)vc, orows, ocols, c0.data(), parts(px),
+             dimx.data(), ncomponentsx, ox, (const void *const *)vx, c1.data(), parts(py),
+             dimy.data(), ncomponentsy, oy, (void *const *)vy, c2.data(), comm, co_of(co), 0));
+}
+} // namespace sbx_detail
+
+/// cholesky: every matrix (rows orows x columns ocols, batch = the other labels) <- its upper
+/// Cholesky factor U (A = U^H U), dense.h:1160-1175
+template <std::size_t N, typename T>
+void cholesky(const PartitionItem<N> *p, const Coor<N> &dim, int ncomponents, const char *o,
+              T **v, const char *orows, const char *ocols, const Context *ctx, CoorOrder co,
+              Session session = 0) {
+    sbx_detail::inplace_dense_impl<N, T>(sbx_cholesky, p, dim, ncomponents, o, v, orows, ocols,
+                                         ctx, nullptr, co, session);
+}
+template <std::size_t N, typename T>
+void cholesky(const PartitionItem<N> *p, const Coor<N> &dim, int ncomponents, const char *o,
+              T **v, const char *orows, const char *ocols, const Context *ctx, Communicator comm,
+              CoorOrder co, Session session = 0) {
+    sbx_detail::inplace_dense_impl<N, T>(sbx_cholesky, p, dim, ncomponents, o, v, orows, ocols,
+                                         ctx, comm, co, session);
+}
+
+/// inversion: every matrix <- its inverse, dense.h:1274-1287
+template <std::size_t N, typename T>
+void inversion(const PartitionItem<N> *p, const Coor<N> &dim, int ncomponents, const char *o,
+               T **v, const char *orows, const char *ocols, const Context *ctx, CoorOrder co,
+               Session session = 0) {
+    sbx_detail::inplace_dense_impl<N, T>(sbx_inversion, p, dim, ncomponents, o, v, orows, ocols,
+                                         ctx, nullptr, co, session);
+}
+template <std::size_t N, typename T>
+void inversion(const PartitionItem<N> *p, const Coor<N> &dim, int ncomponents, const char *o,
+               T **v, const char *orows, const char *ocols, const Context *ctx,
+               Communicator comm, CoorOrder co, Session session = 0) {
+    sbx_detail::inplace_dense_impl<N, T>(sbx_inversion, p, dim, ncomponents, o, v, orows, ocols,
+                                         ctx, comm, co, session);
+}
+
+/// trsm: y = alpha C^-1 x or alpha x C^-1 with C upper triangular, dense.h:1195-1222
+template <std::size_t Nc, std::size_t Nx, std::size_t Ny, typename T>
+void trsm(T alpha, const PartitionItem<Nc> *pc, const Coor<Nc> &dimc, int ncomponentsc,
+          const char *oc, const T **vc, const char *orows, const char *ocols, const Context *ctxc,
+          const PartitionItem<Nx> *px, const Coor<Nx> &dimx, int ncomponentsx, const char *ox,
+          const T **vx, const Context *ctxx, const PartitionItem<Ny> *py, const Coor<Ny> &dimy,
+          int ncomponentsy, const char *oy, T **vy, const Context *ctxy, CoorOrder co,
+          Session session = 0) {
+    sbx_detail::solve_dense_impl<Nc, Nx, Ny, T>(sbx_trsm, alpha, pc, dimc, ncomponentsc, oc, vc,
+                                                orows, ocols, ctxc, px, dimx, ncomponentsx, ox,
+                                                vx, ctxx, py, dimy, ncomponentsy, oy, vy, ctxy,
+                                                nullptr, co, session);
+}
+template <std::size_t Nc, std::size_t Nx, std::size_t Ny, typename T>
+void trsm(T alpha, const PartitionItem<Nc> *pc, const Coor<Nc> &dimc, int ncomponentsc,
+          const char *oc, const T **vc, const char *orows, const char *ocols, const Context *ctxc,
+          const PartitionItem<Nx> *px, const Coor<Nx> &dimx, int ncomponentsx, const char *ox,
+          const T **vx, const Context *ctxx, const PartitionItem<Ny> *py, const Coor<Ny> &dimy,
+          int ncomponentsy, const char *oy, T **vy, const Context *ctxy, Communicator comm,
+          CoorOrder co, Session session = 0) {
+    sbx_detail::solve_dense_impl<Nc, Nx, Ny, T>(sbx_trsm, alpha, pc, dimc, ncomponentsc, oc, vc,
+                                                orows, ocols, ctxc, px, dimx, ncomponentsx, ox,
+                                                vx, ctxx, py, dimy, ncomponentsy, oy, vy, ctxy,
+                                                comm, co, session);
+}
+
+/// gesm: y = alpha C^-1 x for general C, dense.h:1239-1266
+template <std::size_t Nc, std::size_t Nx, std::size_t Ny, typename T>
+void gesm(T alpha, const PartitionItem<Nc> *pc, const Coor<Nc> &dimc, int ncomponentsc,
+          const char *oc, const T **vc, const char *orows, const char *ocols, const Context *ctxc,
+          const PartitionItem<Nx> *px, const Coor<Nx> &dimx, int ncomponentsx, const char *ox,
+          const T **vx, const Context *ctxx, const PartitionItem<Ny> *py, const Coor<Ny> &dimy,
+          int ncomponentsy, const char *oy, T **vy, const Context *ctxy, CoorOrder co,
+          Session session = 0) {
+    sbx_detail::solve_dense_impl<Nc, Nx, Ny, T>(sbx_gesm, alpha, pc, dimc, ncomponentsc, oc, vc,
+                                                orows, ocols, ctxc, px, dimx, ncomponentsx, ox,
+                                                vx, ctxx, py, dimy, ncomponentsy, oy, vy, ctxy,
+                                                nullptr, co, session);
+}
+template <std::size_t Nc, std::size_t Nx, std::size_t Ny, typename T>
+void gesm(T alpha, const PartitionItem<Nc> *pc, const Coor<Nc> &dimc, int ncomponentsc,
+          const char *oc, const T **vc, const char *orows, const char *ocols, const Context *ctxc,
+          const PartitionItem<Nx> *px, const Coor<Nx> &dimx, int ncomponentsx, const char *ox,
+          const T **vx, const Context *ctxx, const PartitionItem<Ny> *py, const Coor<Ny> &dimy,
+          int ncomponentsy, const char *oy, T **vy, const Context *ctxy, Communicator comm,
+          CoorOrder co, Session session = 0) {
+    sbx_detail::solve_dense_impl<Nc, Nx, Ny, T>(sbx_gesm, alpha, pc, dimc, ncomponentsc, oc, vc,
+                                                orows, ocols, ctxc, px, dimx, ncomponentsx, ox,
+                                                vx, ctxx, py, dimy, ncomponentsy, oy, vy, ctxy,
+                                                comm, co, session);
+}
+
 // ---- MPI overloads: a host-staged communicator over MPI_Alltoallv (dist.h:1426-1500) ----
 #ifdef SUPERBBLAS_USE_MPI
 namespace sbx_detail {
@@ -660,6 +777,46 @@ void bsr_krylov(T alpha, BSR_handle *bsrh, const char *oim, const char *odm,
         alpha, bsrh, oim, odm, px, ncomponents, ox, fromx, sizex, dimx, vx, beta, py, oy, fromy,
         sizey, dimy, okr, vy, ctx, sbx_detail::comm_of(mpicomm, ctx, ncomponents), co, request,
         session);
+}
+template <std::size_t N, typename T>
+void cholesky(const PartitionItem<N> *p, const Coor<N> &dim, int ncomponents, const char *o,
+              T **v, const char *orows, const char *ocols, const Context *ctx, MPI_Comm mpicomm,
+              CoorOrder co, Session session = 0) {
+    sbx_detail::inplace_dense_impl<N, T>(sbx_cholesky, p, dim, ncomponents, o, v, orows, ocols,
+                                         ctx, sbx_detail::comm_of(mpicomm, ctx, ncomponents), co,
+                                         session);
+}
+template <std::size_t N, typename T>
+void inversion(const PartitionItem<N> *p, const Coor<N> &dim, int ncomponents, const char *o,
+               T **v, const char *orows, const char *ocols, const Context *ctx, MPI_Comm mpicomm,
+               CoorOrder co, Session session = 0) {
+    sbx_detail::inplace_dense_impl<N, T>(sbx_inversion, p, dim, ncomponents, o, v, orows, ocols,
+                                         ctx, sbx_detail::comm_of(mpicomm, ctx, ncomponents), co,
+                                         session);
+}
+template <std::size_t Nc, std::size_t Nx, std::size_t Ny, typename T>
+void trsm(T alpha, const PartitionItem<Nc> *pc, const Coor<Nc> &dimc, int ncomponentsc,
+          const char *oc, const T **vc, const char *orows, const char *ocols, const Context *ctxc,
+          const PartitionItem<Nx> *px, const Coor<Nx> &dimx, int ncomponentsx, const char *ox,
+          const T **vx, const Context *ctxx, const PartitionItem<Ny> *py, const Coor<Ny> &dimy,
+          int ncomponentsy, const char *oy, T **vy, const Context *ctxy, MPI_Comm mpicomm,
+          CoorOrder co, Session session = 0) {
+    sbx_detail::solve_dense_impl<Nc, Nx, Ny, T>(
+        sbx_trsm, alpha, pc, dimc, ncomponentsc, oc, vc, orows, ocols, ctxc, px, dimx,
+        ncomponentsx, ox, vx, ctxx, py, dimy, ncomponentsy, oy, vy, ctxy,
+        sbx_detail::comm_of(mpicomm, ctxc, ncomponentsc), co, session);
+}
+template <std::size_t Nc, std::size_t Nx, std::size_t Ny, typename T>
+void gesm(T alpha, const PartitionItem<Nc> *pc, const Coor<Nc> &dimc, int ncomponentsc,
+          const char *oc, const T **vc, const char *orows, const char *ocols, const Context *ctxc,
+          const PartitionItem<Nx> *px, const Coor<Nx> &dimx, int ncomponentsx, const char *ox,
+          const T **vx, const Context *ctxx, const PartitionItem<Ny> *py, const Coor<Ny> &dimy,
+          int ncomponentsy, const char *oy, T **vy, const Context *ctxy, MPI_Comm mpicomm,
+          CoorOrder co, Session session = 0) {
+    sbx_detail::solve_dense_impl<Nc, Nx, Ny, T>(
+        sbx_gesm, alpha, pc, dimc, ncomponentsc, oc, vc, orows, ocols, ctxc, px, dimx,
+        ncomponentsx, ox, vx, ctxx, py, dimy, ncomponentsy, oy, vy, ctxy,
+        sbx_detail::comm_of(mpicomm, ctxc, ncomponentsc), co, session);
 }
 #endif // SUPERBBLAS_USE_MPI
 

@@ -223,6 +223,33 @@ int sbx_bsr_get_preferred_layout(sbx_bsr bsrh, int ncomponents, const sbx_contex
                                  sbx_comm comm, int co, int *layout_x, int *layout_y);
 int sbx_destroy_bsr(sbx_bsr bsrh);
 
+/* ---- dense batched solvers (dense.h:1160-1290 no MPI, 1007-1157 MPI) ----
+   The labels of `o` split into row labels `orows`, column labels `ocols` and batch labels (the
+   rest); every batch entry is a square matrix (rows index = orows labels, last label fastest for
+   SLOW_TO_FAST).  cholesky: A <- U with A = U^H U (upper triangle; the strict lower part is left
+   untouched); inversion: A <- A^-1; trsm: y = alpha C^-1 x (x holds the column labels of the
+   upper triangular C) or y = alpha x C^-1 (x holds its row labels); gesm: y = alpha C^-1 x for a
+   general C (x holds the column labels).  A failed factorization returns an error carrying the
+   LAPACK info ("Error in lapack routine: i"). */
+int sbx_cholesky(int nd, int t, const int *p, const int *dim, int ncomponents, const char *o,
+                 void *const *v, const char *orows, const char *ocols, const sbx_context *ctx,
+                 sbx_comm comm, int co, int session);
+int sbx_inversion(int nd, int t, const int *p, const int *dim, int ncomponents, const char *o,
+                  void *const *v, const char *orows, const char *ocols, const sbx_context *ctx,
+                  sbx_comm comm, int co, int session);
+int sbx_trsm(int ndc, int ndx, int ndy, int t, const double *alpha, const int *pc, const int *dimc,
+             int ncomponentsc, const char *oc, const void *const *vc, const char *orows,
+             const char *ocols, const sbx_context *ctxc, const int *px, const int *dimx,
+             int ncomponentsx, const char *ox, const void *const *vx, const sbx_context *ctxx,
+             const int *py, const int *dimy, int ncomponentsy, const char *oy, void *const *vy,
+             const sbx_context *ctxy, sbx_comm comm, int co, int session);
+int sbx_gesm(int ndc, int ndx, int ndy, int t, const double *alpha, const int *pc, const int *dimc,
+             int ncomponentsc, const char *oc, const void *const *vc, const char *orows,
+             const char *ocols, const sbx_context *ctxc, const int *px, const int *dimx,
+             int ncomponentsx, const char *ox, const void *const *vx, const sbx_context *ctxx,
+             const int *py, const int *dimy, int ncomponentsy, const char *oy, void *const *vy,
+             const sbx_context *ctxy, sbx_comm comm, int co, int session);
+
 /* ---- kernel-level entry points (the local hot path, for direct callers and benchmarks) ---- */
 
 /* xgemm_batch_strided (blas.h:662-810; CPU blas_cpu_tmpl.hpp:376-478): BLAS column-major,

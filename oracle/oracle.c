@@ -13,6 +13,7 @@
  * Types: 0 float, 1 double, 2 complex<float>, 3 complex<double>, 4 int, 5 size_t
  */
 #include <stdint.h>
+#include <math.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -495,6 +496,147 @@ int oracle_kron_bsr(int t, int nd, const int *site_dim, int co, long block_rows,
                     }
                     store(t, y, yi, rr, ri);
                 }
+    }
+    return 0;
+}
+
+/*
+ * Dense batched solvers on k column-major n x n matrices (element (r, c) of matrix b at
+ * b*n*n + r + c*n), the local operations of dense.h (local_cholesky 56-95 -> xpotrf('U'),
+ * local_gesm 253-300 -> xgetrf + xgetrs('N'), local_inversion 335-385 -> xgetrf + xgetri,
+ * local_trsm 136-156 -> xtrsm(side, 'U', 'N', 'N')), restated with the unblocked LAPACK /
+ * BLAS algorithms (zpotf2, zgetf2 with izamax pivoting on |re|+|im|, zgetrs, ztrsm).
+ * Complex arithmetic in doubles through load/store.  Return 0, or the LAPACK info (> 0).
+ */
+typedef struct { double r, i; } cx;
+static cx cmul(cx a, cx b) { cx c = {a.r * b.r - a.i * b.i, a.r * b.i + a.i * b.r}; return c; }
+static cx csub(cx a, cx b) { cx c = {a.r - b.r, a.i - b.i}; return c; }
+static cx cconj(cx a) { cx c = {a.r, -a.i}; return c; }
+static cx cdivz(cx a, cx b) {
+    const double d = b.r * b.r + b.i * b.i;
+    cx c = {(a.r * b.r + a.i * b.i) / d, (a.i * b.r - a.r * b.i) / d};
+    return c;
+}
+static cx ld(int t, const void *p, long i) { cx v; load(t, p, i, &v.r, &v.i); return v; }
+static void st(int t, void *p, long i, cx v) { store(t, p, i, v.r, is_complex(t) ? v.i : 0); }
+
+int oracle_potrf_upper(int t, long n, long k, void *a) {
+    for (long b = 0; b < k; ++b) {
+        const long o = b * n * n;
+        for (long j = 0; j < n; ++j) {
+            /* U(j, j) = sqrt(A(j, j) - sum_p |U(p, j)|^2) */
+            double d = ld(t, a, o + j + j * n).r;
+            for (long q = 0; q < j; ++q) {
+                const cx u = ld(t, a, o + q + j * n);
+                d -= u.r * u.r + u.i * u.i;
+            }
+            if (!(d > 0)) return (int)(j + 1);
+            d = sqrt(d);
+            const cx dj = {d, 0};
+            st(t, a, o + j + j * n, dj);
+            /* U(j, c) = (A(j, c) - sum_p conj(U(p, j)) U(p, c)) / U(j, j), c > j */
+            for (long c = j + 1; c < n; ++c) {
+                cx v = ld(t, a, o + j + c * n);
+                for (long q = 0; q < j; ++q)
+                    v = csub(v, cmul(cconj(ld(t, a, o + q + j * n)), ld(t, a, o + q + c * n)));
+                v.r /= d;
+                v.i /= d;
+                st(t, a, o + j + c * n, v);
+            }
+        }
+    }
+    return 0;
+}
+
+int oracle_getrf(int t, long n, long k, void *a, int *ipiv) {
+    for (long b = 0; b < k; ++b) {
+        const long o = b * n * n;
+        for (long j = 0; j < n; ++j) {
+            long p = j;
+            double best = -1;
+            for (long r = j; r < n; ++r) {
+                const cx v = ld(t, a, o + r + j * n);
+                const double m = fabs(v.r) + fabs(v.i);
+                if (m > best) {
+                    best = m;
+                    p = r;
+                }
+            }
+            ipiv[b * n + j] = (int)p + 1;
+            if (best == 0) return (int)(j + 1);
+            if (p != j)
+                for (long c = 0; c < n; ++c) {
+                    const cx x = ld(t, a, o + j + c * n), y = ld(t, a, o + p + c * n);
+                    st(t, a, o + j + c * n, y);
+                    st(t, a, o + p + c * n, x);
+                }
+            const cx piv = ld(t, a, o + j + j * n);
+            for (long r = j + 1; r < n; ++r) st(t, a, o + r + j * n, cdivz(ld(t, a, o + r + j * n), piv));
+            for (long c = j + 1; c < n; ++c) {
+                const cx ujc = ld(t, a, o + j + c * n);
+                for (long r = j + 1; r < n; ++r)
+                    st(t, a, o + r + c * n,
+                       csub(ld(t, a, o + r + c * n), cmul(ld(t, a, o + r + j * n), ujc)));
+            }
+        }
+    }
+    return 0;
+}
+
+/* B (n x m, column-major, ld n) <- A^-1 B from the getrf factors */
+int oracle_getrs(int t, long n, long k, const void *a, const int *ipiv, long m, void *bm) {
+    for (long b = 0; b < k; ++b) {
+        const long o = b * n * n, ob = b * n * m;
+        for (long col = 0; col < m; ++col) {
+            for (long j = 0; j < n; ++j) {
+                const long p = ipiv[b * n + j] - 1;
+                if (p != j) {
+                    const cx x = ld(t, bm, ob + j + col * n), y = ld(t, bm, ob + p + col * n);
+                    st(t, bm, ob + j + col * n, y);
+                    st(t, bm, ob + p + col * n, x);
+                }
+            }
+            for (long r = 0; r < n; ++r) { /* L y = b, unit diagonal */
+                cx v = ld(t, bm, ob + r + col * n);
+                for (long q = 0; q < r; ++q)
+                    v = csub(v, cmul(ld(t, a, o + r + q * n), ld(t, bm, ob + q + col * n)));
+                st(t, bm, ob + r + col * n, v);
+            }
+            for (long r = n - 1; r >= 0; --r) { /* U x = y */
+                cx v = ld(t, bm, ob + r + col * n);
+                for (long q = r + 1; q < n; ++q)
+                    v = csub(v, cmul(ld(t, a, o + r + q * n), ld(t, bm, ob + q + col * n)));
+                st(t, bm, ob + r + col * n, cdivz(v, ld(t, a, o + r + r * n)));
+            }
+        }
+    }
+    return 0;
+}
+
+/* upper triangular solves: left  X (n x m, ld n) <- alpha U^-1 X;
+                            right X (m x n, ld m) <- alpha X U^-1 */
+int oracle_trsm_upper(int t, int left, long n, long k, long m, const double *alpha,
+                      const void *a, void *x) {
+    const cx al = {alpha[0], is_complex(t) ? alpha[1] : 0};
+    for (long b = 0; b < k; ++b) {
+        const long o = b * n * n, ox = b * n * m;
+        if (left) {
+            for (long col = 0; col < m; ++col)
+                for (long r = n - 1; r >= 0; --r) {
+                    cx v = cmul(al, ld(t, x, ox + r + col * n));
+                    for (long q = r + 1; q < n; ++q)
+                        v = csub(v, cmul(ld(t, a, o + r + q * n), ld(t, x, ox + q + col * n)));
+                    st(t, x, ox + r + col * n, cdivz(v, ld(t, a, o + r + r * n)));
+                }
+        } else {
+            for (long row = 0; row < m; ++row)
+                for (long c = 0; c < n; ++c) {
+                    cx v = cmul(al, ld(t, x, ox + row + c * m));
+                    for (long q = 0; q < c; ++q)
+                        v = csub(v, cmul(ld(t, x, ox + row + q * m), ld(t, a, o + q + c * n)));
+                    st(t, x, ox + row + c * m, cdivz(v, ld(t, a, o + c + c * n)));
+                }
+        }
     }
     return 0;
 }

@@ -650,6 +650,55 @@ def bsr_krylov(alpha, bsr: BSR, oim: str, odm: str, px, ox: str, fromx, sizex, d
         ctypes.c_char((okr or "\0").encode()), _ptrs(vy), _ctxs(vx), _comm(comm), co, 0))
 
 
+def _inplace_dense(fn, p, dim, o: str, v, orows: str, ocols: str, co, comm):
+    nd = len(o)
+    nc = len(v)
+    t = _dtype_of(v)
+    _bind_stream(list(v))
+    _check(fn(nd, t, _partition(p, nd), _ints(dim), nc, o.encode(), _ptrs(v), orows.encode(),
+              ocols.encode(), _ctxs(v), _comm(comm), co, 0))
+
+
+def cholesky(p, dim, o: str, v: Sequence[torch.Tensor], orows: str, ocols: str,
+             co: int = SlowToFast, comm: Optional[Comm] = None):
+    """cholesky<N,T> (dense.h:1160-1175): every batch matrix (rows orows x columns ocols) is
+    replaced by U with A = U^H U (upper triangle; the strict lower part is left as is)."""
+    _inplace_dense(_lib.sbx_cholesky, p, dim, o, v, orows, ocols, co, comm)
+
+
+def inversion(p, dim, o: str, v: Sequence[torch.Tensor], orows: str, ocols: str,
+              co: int = SlowToFast, comm: Optional[Comm] = None):
+    """inversion<N,T> (dense.h:1274-1287): every batch matrix is replaced by its inverse."""
+    _inplace_dense(_lib.sbx_inversion, p, dim, o, v, orows, ocols, co, comm)
+
+
+def _solve_dense(fn, alpha, pc, dimc, oc, vc, orows, ocols, px, dimx, ox, vx, py, dimy, oy, vy,
+                 co, comm):
+    t = _dtype_of(list(vc) + list(vx) + list(vy))
+    _bind_stream(list(vc) + list(vx) + list(vy))
+    _check(fn(len(oc), len(ox), len(oy), t, _scalar(alpha), _partition(pc, len(oc)), _ints(dimc),
+              len(vc), oc.encode(), _ptrs(vc), orows.encode(), ocols.encode(), _ctxs(vc),
+              _partition(px, len(ox)), _ints(dimx), len(vx), ox.encode(), _ptrs(vx), _ctxs(vx),
+              _partition(py, len(oy)), _ints(dimy), len(vy), oy.encode(), _ptrs(vy), _ctxs(vy),
+              _comm(comm), co, 0))
+
+
+def trsm(alpha, pc, dimc, oc: str, vc, orows: str, ocols: str, px, dimx, ox: str, vx, py, dimy,
+         oy: str, vy, co: int = SlowToFast, comm: Optional[Comm] = None):
+    """trsm<Nc,Nx,Ny,T> (dense.h:1195-1222): y = alpha C^-1 x (x holds C's column labels) or
+    y = alpha x C^-1 (x holds its row labels), C upper triangular (a Cholesky factor)."""
+    _solve_dense(_lib.sbx_trsm, alpha, pc, dimc, oc, vc, orows, ocols, px, dimx, ox, vx, py,
+                 dimy, oy, vy, co, comm)
+
+
+def gesm(alpha, pc, dimc, oc: str, vc, orows: str, ocols: str, px, dimx, ox: str, vx, py, dimy,
+         oy: str, vy, co: int = SlowToFast, comm: Optional[Comm] = None):
+    """gesm<Nc,Nx,Ny,T> (dense.h:1239-1266): y = alpha C^-1 x for general C (LU with partial
+    pivoting), x holding C's column labels."""
+    _solve_dense(_lib.sbx_gesm, alpha, pc, dimc, oc, vc, orows, ocols, px, dimx, ox, vx, py,
+                 dimy, oy, vy, co, comm)
+
+
 def bsr_get_preferred_layout(bsr: BSR, ncomponents: int = 1, co: int = SlowToFast,
                              comm: Optional[Comm] = None):
     lx, ly = _ints([0] * ncomponents), _ints([0] * ncomponents)
@@ -662,7 +711,7 @@ def bsr_get_preferred_layout(bsr: BSR, ncomponents: int = 1, co: int = SlowToFas
 __all__ = [
     "SlowToFast", "FastToSlow", "Copy", "Add", "RowMajor", "ColumnMajor", "SuperbblasError",
     "Comm", "copy", "copy_plan", "contraction", "local_copy", "xgemm_batch_strided", "create_bsr",
-    "create_kron_bsr",
+    "create_kron_bsr", "cholesky", "inversion", "trsm", "gesm",
     "bsr_krylov", "bsr_get_preferred_layout", "basic_partitioning", "basic_partitioning_ext",
     "partitioning_distributed_procs", "make_hole", "sync", "stream", "set_stream",
     "clear_caches", "timings_enable", "timings_reset", "timings_get", "timings_report",

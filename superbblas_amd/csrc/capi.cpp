@@ -63,6 +63,14 @@ Coor to_coor(const int *p, int n, bool rev) {
     return c;
 }
 
+/// Row / column label subsets of the dense solvers (reversed with the tensor for FastToSlow)
+std::string sub_labels(const char *s, bool rev, const char *what) {
+    if (!s) throw Error(std::string(what) + ": null labels");
+    std::string r(s);
+    if (rev) std::reverse(r.begin(), r.end());
+    return r;
+}
+
 std::string to_labels(const char *o, int n, bool rev, const char *what) {
     if (!o) throw Error(std::string(what) + ": null labels");
     if ((int)std::strlen(o) != n)
@@ -692,6 +700,87 @@ int sbx_destroy_bsr(sbx_bsr bsrh) {
         bsr_destroy(bsrh->op);
         delete bsrh;
     });
+}
+
+/* ---- dense batched solvers (dense.h) ---- */
+
+int sbx_cholesky(int nd, int t, const int *p, const int *dim, int ncomponents, const char *o,
+                 void *const *v, const char *orows, const char *ocols, const sbx_context *ctx,
+                 sbx_comm comm, int co, int session) {
+    return guard([&] {
+        check_session(session);
+        const Comm c = get_comm(comm);
+        const bool rev = co == SBX_FAST_TO_SLOW;
+        Mirror m;
+        m.device = pick_device({{ctx, ncomponents}}, c);
+        DistTensor a = make_tensor(nd, o, dim, p, ncomponents, (const void *const *)v, ctx, t, c,
+                                   rev, m, true, "o");
+        dense_cholesky(a, sub_labels(orows, rev, "orows"), sub_labels(ocols, rev, "ocols"), c);
+        finish_mirror(m);
+    });
+}
+
+int sbx_inversion(int nd, int t, const int *p, const int *dim, int ncomponents, const char *o,
+                  void *const *v, const char *orows, const char *ocols, const sbx_context *ctx,
+                  sbx_comm comm, int co, int session) {
+    return guard([&] {
+        check_session(session);
+        const Comm c = get_comm(comm);
+        const bool rev = co == SBX_FAST_TO_SLOW;
+        Mirror m;
+        m.device = pick_device({{ctx, ncomponents}}, c);
+        DistTensor a = make_tensor(nd, o, dim, p, ncomponents, (const void *const *)v, ctx, t, c,
+                                   rev, m, true, "o");
+        dense_inversion(a, sub_labels(orows, rev, "orows"), sub_labels(ocols, rev, "ocols"), c);
+        finish_mirror(m);
+    });
+}
+
+namespace {
+int solve_any(bool gesm, int ndc, int ndx, int ndy, int t, const double *alpha, const int *pc,
+              const int *dimc, int ncomponentsc, const char *oc, const void *const *vc,
+              const char *orows, const char *ocols, const sbx_context *ctxc, const int *px,
+              const int *dimx, int ncomponentsx, const char *ox, const void *const *vx,
+              const sbx_context *ctxx, const int *py, const int *dimy, int ncomponentsy,
+              const char *oy, void *const *vy, const sbx_context *ctxy, sbx_comm comm, int co,
+              int session) {
+    return guard([&] {
+        check_session(session);
+        const Comm c = get_comm(comm);
+        const bool rev = co == SBX_FAST_TO_SLOW;
+        Mirror m;
+        m.device = pick_device({{ctxc, ncomponentsc}, {ctxx, ncomponentsx}, {ctxy, ncomponentsy}}, c);
+        DistTensor a = make_tensor(ndc, oc, dimc, pc, ncomponentsc, vc, ctxc, t, c, rev, m, false, "oc");
+        DistTensor x = make_tensor(ndx, ox, dimx, px, ncomponentsx, vx, ctxx, t, c, rev, m, false, "ox");
+        DistTensor y = make_tensor(ndy, oy, dimy, py, ncomponentsy, (const void *const *)vy, ctxy,
+                                   t, c, rev, m, true, "oy");
+        dense_solve(gesm, to_scalar(alpha), a, sub_labels(orows, rev, "orows"),
+                    sub_labels(ocols, rev, "ocols"), x, y, c);
+        finish_mirror(m);
+    });
+}
+} // namespace
+
+int sbx_trsm(int ndc, int ndx, int ndy, int t, const double *alpha, const int *pc, const int *dimc,
+             int ncomponentsc, const char *oc, const void *const *vc, const char *orows,
+             const char *ocols, const sbx_context *ctxc, const int *px, const int *dimx,
+             int ncomponentsx, const char *ox, const void *const *vx, const sbx_context *ctxx,
+             const int *py, const int *dimy, int ncomponentsy, const char *oy, void *const *vy,
+             const sbx_context *ctxy, sbx_comm comm, int co, int session) {
+    return solve_any(false, ndc, ndx, ndy, t, alpha, pc, dimc, ncomponentsc, oc, vc, orows, ocols,
+                     ctxc, px, dimx, ncomponentsx, ox, vx, ctxx, py, dimy, ncomponentsy, oy, vy,
+                     ctxy, comm, co, session);
+}
+
+int sbx_gesm(int ndc, int ndx, int ndy, int t, const double *alpha, const int *pc, const int *dimc,
+             int ncomponentsc, const char *oc, const void *const *vc, const char *orows,
+             const char *ocols, const sbx_context *ctxc, const int *px, const int *dimx,
+             int ncomponentsx, const char *ox, const void *const *vx, const sbx_context *ctxx,
+             const int *py, const int *dimy, int ncomponentsy, const char *oy, void *const *vy,
+             const sbx_context *ctxy, sbx_comm comm, int co, int session) {
+    return solve_any(true, ndc, ndx, ndy, t, alpha, pc, dimc, ncomponentsc, oc, vc, orows, ocols,
+                     ctxc, px, dimx, ncomponentsx, ox, vx, ctxx, py, dimy, ncomponentsy, oy, vy,
+                     ctxy, comm, co, session);
 }
 
 int sbx_xgemm_batch_strided(int t, char transa, char transb, int m, int n, int k,

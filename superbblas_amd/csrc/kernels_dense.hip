@@ -1,0 +1,345 @@
+// Dense batched solvers on small column-major matrices: Cholesky (upper), LU with partial
+// pivoting + solve, triangular solve -- the local steps of superbblas's dense.h
+// (local_cholesky dense.h:56-123 -> potrf('U'), local_gesm 253-330 -> getrf + getrs('N'),
+// local_inversion 335-440 -> getrf + getri, local_trsm 136-200 -> trsm(side, 'U', 'N', 'N')),
+// where the reference calls rocsolver / rocblas batched routines.
+//
+// One 256-thread workgroup per matrix.  The matrix is staged in LDS when it fits
+// (n*n*sizeof(E) <= 64 KB: n <= 64 for complex<double>) and updated in place in global memory
+// otherwise; every step is a right-looking rank-1 update spread over the threads of the
+// workgroup.  Pivoting follows LAPACK's i?amax (largest |re| + |im|, first index on ties), so
+// pivot sequences match the reference's.  Right-hand sides are solved one column (or row) per
+// thread against the factor in LDS (wave-uniform reads).  A non-positive pivot (Cholesky) or a
+// zero pivot (LU) stops the factorization of that matrix and is reported as the LAPACK info.
+#include "elem_ops.h"
+#include "sbx_internal.h"
+
+#include <algorithm>
+
+namespace sbx {
+namespace {
+
+constexpr int DTH = 256;
+constexpr long DENSE_LDS_BYTES = 64 * 1024;
+
+template <typename E> struct DOps;
+template <> struct DOps<double> {
+    static __device__ __forceinline__ double re(double v) { return v; }
+    static __device__ __forceinline__ double abs1(double v) { return fabs(v); }
+    static __device__ __forceinline__ double conj(double v) { return v; }
+    static __device__ __forceinline__ double mul(double a, double b) { return a * b; }
+    static __device__ __forceinline__ double sub(double a, double b) { return a - b; }
+    static __device__ __forceinline__ double div(double a, double b) { return a / b; }
+    static __device__ __forceinline__ double divr(double a, double b) { return a / b; }
+    static __device__ __forceinline__ double real(double r) { return r; }
+    static __device__ __forceinline__ double one() { return 1; }
+};
+template <> struct DOps<float> {
+    static __device__ __forceinline__ double re(float v) { return v; }
+    static __device__ __forceinline__ double abs1(float v) { return fabsf(v); }
+    static __device__ __forceinline__ float conj(float v) { return v; }
+    static __device__ __forceinline__ float mul(float a, float b) { return a * b; }
+    static __device__ __forceinline__ float sub(float a, float b) { return a - b; }
+    static __device__ __forceinline__ float div(float a, float b) { return a / b; }
+    static __device__ __forceinline__ float divr(float a, double b) { return a / (float)b; }
+    static __device__ __forceinline__ float real(double r) { return (float)r; }
+    static __device__ __forceinline__ float one() { return 1; }
+};
+template <typename E, typename R> struct CplxOps {
+    static __device__ __forceinline__ double re(E v) { return v.x; }
+    static __device__ __forceinline__ double abs1(E v) { return fabs((double)v.x) + fabs((double)v.y); }
+    static __device__ __forceinline__ E conj(E v) { return E{v.x, -v.y}; }
+    static __device__ __forceinline__ E mul(E a, E b) {
+        return E{a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x};
+    }
+    static __device__ __forceinline__ E sub(E a, E b) { return E{a.x - b.x, a.y - b.y}; }
+    static __device__ __forceinline__ E div(E a, E b) {
+        // Smith's algorithm (robust against overflow, as LAPACK's zladiv family)
+        if (fabs((double)b.y) <= fabs((double)b.x)) {
+            const R r = b.y / b.x, d = b.x + b.y * r;
+            return E{(a.x + a.y * r) / d, (a.y - a.x * r) / d};
+        }
+        const R r = b.x / b.y, d = b.y + b.x * r;
+        return E{(a.x * r + a.y) / d, (a.y * r - a.x) / d};
+    }
+    static __device__ __forceinline__ E divr(E a, double b) { return E{(R)(a.x / b), (R)(a.y / b)}; }
+    static __device__ __forceinline__ E real(double r) { return E{(R)r, 0}; }
+    static __device__ __forceinline__ E one() { return E{1, 0}; }
+};
+template <> struct DOps<double2> : CplxOps<double2, double> {};
+template <> struct DOps<float2> : CplxOps<float2, float> {};
+
+template <typename E> __device__ __forceinline__ E scale_by(E v, double ar, double ai);
+template <> __device__ __forceinline__ double scale_by<double>(double v, double ar, double) { return ar * v; }
+template <> __device__ __forceinline__ float scale_by<float>(float v, double ar, double) { return (float)ar * v; }
+template <> __device__ __forceinline__ double2 scale_by<double2>(double2 v, double ar, double ai) {
+    return double2{ar * v.x - ai * v.y, ar * v.y + ai * v.x};
+}
+template <> __device__ __forceinline__ float2 scale_by<float2>(float2 v, double ar, double ai) {
+    return float2{(float)ar * v.x - (float)ai * v.y, (float)ar * v.y + (float)ai * v.x};
+}
+
+/// The matrix of this workgroup: staged in LDS when it fits, else the global copy
+template <typename E>
+__device__ __forceinline__ E *stage_in(E *g, long nn, bool lds, E *smem) {
+    if (!lds) return g;
+    for (long e = threadIdx.x; e < nn; e += DTH) smem[e] = g[e];
+    __syncthreads();
+    return smem;
+}
+template <typename E> __device__ __forceinline__ void stage_out(E *g, const E *m, long nn, bool lds) {
+    __syncthreads();
+    if (!lds) return;
+    for (long e = threadIdx.x; e < nn; e += DTH) g[e] = m[e];
+}
+
+// Cholesky, upper: A = U^H U, U over the upper triangle, the strict lower part untouched
+template <typename E>
+__global__ void __launch_bounds__(DTH) potrf_kernel(E *a, long n, int lds, int *info) {
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    typedef DOps<E> O;
+    E *g = a + (long)blockIdx.x * n * n;
+    E *M = stage_in(g, n * n, lds != 0, (E *)smem_raw);
+    int bad = 0;
+    for (long j = 0; j < n; ++j) {
+        __syncthreads();
+        double d = O::re(M[j + j * n]);
+        if (!(d > 0)) {
+            bad = (int)j + 1;
+            break;
+        }
+        d = sqrt(d);
+        __syncthreads();
+        if (threadIdx.x == 0) M[j + j * n] = O::real(d);
+        for (long c = j + 1 + threadIdx.x; c < n; c += DTH) M[j + c * n] = O::divr(M[j + c * n], d);
+        __syncthreads();
+        const long w = n - j - 1;
+        for (long e = threadIdx.x; e < w * w; e += DTH) {
+            const long r = j + 1 + e % w, c = j + 1 + e / w;
+            if (r <= c) M[r + c * n] = O::sub(M[r + c * n], O::mul(O::conj(M[j + r * n]), M[j + c * n]));
+        }
+    }
+    stage_out(g, M, n * n, lds != 0);
+    if (threadIdx.x == 0) info[blockIdx.x] = bad;
+}
+
+// LU with partial pivoting (getrf), then B <- alpha A^-1 B for the n x m column-major panel of
+// this matrix (getrs 'N'); identity != 0 makes B the identity first (the inverse, getri)
+template <typename E>
+__global__ void __launch_bounds__(DTH) gesv_kernel(E *a, long n, E *b, long m, int identity,
+                                                   double alpha_re, double alpha_im, int lds,
+                                                   int *ipiv_g, int *info) {
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    __shared__ double best_v[DTH];
+    __shared__ int best_i[DTH];
+    typedef DOps<E> O;
+    E *g = a + (long)blockIdx.x * n * n;
+    E *M = stage_in(g, n * n, lds != 0, (E *)smem_raw);
+    int *piv = ipiv_g + (long)blockIdx.x * n;
+    int bad = 0;
+    for (long j = 0; j < n; ++j) {
+        // pivot: the largest |re| + |im| in column j at or below the diagonal, first on ties
+        double bv = -1;
+        int bi = (int)j;
+        for (long r = j + threadIdx.x; r < n; r += DTH) {
+            const double v = O::abs1(M[r + j * n]);
+            if (v > bv) {
+                bv = v;
+                bi = (int)r;
+            }
+        }
+        best_v[threadIdx.x] = bv;
+        best_i[threadIdx.x] = bi;
+        __syncthreads();
+        for (int s = DTH / 2; s > 0; s >>= 1) {
+            if ((int)threadIdx.x < s) {
+                const double ov = best_v[threadIdx.x + s];
+                const int oi = best_i[threadIdx.x + s];
+                if (ov > best_v[threadIdx.x] || (ov == best_v[threadIdx.x] && oi < best_i[threadIdx.x])) {
+                    best_v[threadIdx.x] = ov;
+                    best_i[threadIdx.x] = oi;
+                }
+            }
+            __syncthreads();
+        }
+        const long p = best_i[0];
+        const double pv = best_v[0];
+        if (threadIdx.x == 0) piv[j] = (int)p;
+        __syncthreads();
+        if (!(pv > 0)) {
+            bad = (int)j + 1;
+            break;
+        }
+        if (p != j)
+            for (long c = threadIdx.x; c < n; c += DTH) {
+                const E t = M[j + c * n];
+                M[j + c * n] = M[p + c * n];
+                M[p + c * n] = t;
+            }
+        __syncthreads();
+        const E d = M[j + j * n];
+        for (long r = j + 1 + threadIdx.x; r < n; r += DTH) M[r + j * n] = O::div(M[r + j * n], d);
+        __syncthreads();
+        const long w = n - j - 1;
+        for (long e = threadIdx.x; e < w * w; e += DTH) {
+            const long r = j + 1 + e % w, c = j + 1 + e / w;
+            M[r + c * n] = O::sub(M[r + c * n], O::mul(M[r + j * n], M[j + c * n]));
+        }
+        __syncthreads();
+    }
+    if (!bad && b) {
+        // one right-hand side per thread: P, L (unit), U
+        E *B = b + (long)blockIdx.x * n * m;
+        for (long col = threadIdx.x; col < m; col += DTH) {
+            E *x = B + col * n;
+            if (identity)
+                for (long r = 0; r < n; ++r) x[r] = r == col ? O::one() : O::real(0);
+            for (long j = 0; j < n; ++j) {
+                const long p = piv[j];
+                if (p != j) {
+                    const E t = x[j];
+                    x[j] = x[p];
+                    x[p] = t;
+                }
+            }
+            for (long r = 0; r < n; ++r) {
+                E v = x[r];
+                for (long q = 0; q < r; ++q) v = O::sub(v, O::mul(M[r + q * n], x[q]));
+                x[r] = v;
+            }
+            for (long r = n - 1; r >= 0; --r) {
+                E v = x[r];
+                for (long q = r + 1; q < n; ++q) v = O::sub(v, O::mul(M[r + q * n], x[q]));
+                x[r] = O::div(v, M[r + r * n]);
+            }
+            if (alpha_re != 1 || alpha_im != 0)
+                for (long r = 0; r < n; ++r) x[r] = scale_by<E>(x[r], alpha_re, alpha_im);
+        }
+    }
+    stage_out(g, M, n * n, lds != 0);
+    if (threadIdx.x == 0) info[blockIdx.x] = bad;
+}
+
+// Upper triangular solve: left  X (n x m, ld n) <- alpha U^-1 X;  right X (m x n, ld m) <- alpha X U^-1
+template <typename E>
+__global__ void __launch_bounds__(DTH) trsm_kernel(const E *a, long n, E *x, long m, int left,
+                                                   double alpha_re, double alpha_im, int lds) {
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    typedef DOps<E> O;
+    const E *U = a + (long)blockIdx.x * n * n;
+    if (lds) {
+        E *s = (E *)smem_raw;
+        for (long e = threadIdx.x; e < n * n; e += DTH) s[e] = U[e];
+        __syncthreads();
+        U = s;
+    }
+    E *X = x + (long)blockIdx.x * n * m;
+    for (long t = threadIdx.x; t < m; t += DTH) {
+        if (left) {
+            E *col = X + t * n;
+            for (long r = n - 1; r >= 0; --r) {
+                E v = scale_by<E>(col[r], alpha_re, alpha_im);
+                for (long q = r + 1; q < n; ++q) v = O::sub(v, O::mul(U[r + q * n], col[q]));
+                col[r] = O::div(v, U[r + r * n]);
+            }
+        } else {
+            for (long c = 0; c < n; ++c) {
+                E v = scale_by<E>(X[t + c * m], alpha_re, alpha_im);
+                for (long q = 0; q < c; ++q) v = O::sub(v, O::mul(X[t + q * m], U[q + c * n]));
+                X[t + c * m] = O::div(v, U[c + c * n]);
+            }
+        }
+    }
+}
+
+template <typename E> bool fits_lds(long n) { return n * n * (long)sizeof(E) <= DENSE_LDS_BYTES; }
+
+template <typename E> void potrf_typed(void *a, long n, long k, int *info, hipStream_t s) {
+    const bool lds = fits_lds<E>(n);
+    hipLaunchKernelGGL(potrf_kernel<E>, dim3((unsigned)k), dim3(DTH),
+                       lds ? (size_t)(n * n * sizeof(E)) : 0, s, (E *)a, n, lds ? 1 : 0, info);
+    SBX_HIP_CHECK(hipGetLastError());
+}
+template <typename E>
+void gesv_typed(void *a, long n, long k, void *b, long m, bool identity, const Scalar &alpha,
+                int *ipiv, int *info, hipStream_t s) {
+    const bool lds = fits_lds<E>(n);
+    hipLaunchKernelGGL(gesv_kernel<E>, dim3((unsigned)k), dim3(DTH),
+                       lds ? (size_t)(n * n * sizeof(E)) : 0, s, (E *)a, n, (E *)b, m,
+                       identity ? 1 : 0, alpha.re, alpha.im, lds ? 1 : 0, ipiv, info);
+    SBX_HIP_CHECK(hipGetLastError());
+}
+template <typename E>
+void trsm_typed(const void *a, long n, long k, void *x, long m, bool left, const Scalar &alpha,
+                hipStream_t s) {
+    const bool lds = fits_lds<E>(n);
+    hipLaunchKernelGGL(trsm_kernel<E>, dim3((unsigned)k), dim3(DTH),
+                       lds ? (size_t)(n * n * sizeof(E)) : 0, s, (const E *)a, n, (E *)x, m,
+                       left ? 1 : 0, alpha.re, alpha.im, lds ? 1 : 0);
+    SBX_HIP_CHECK(hipGetLastError());
+}
+
+/// The first nonzero LAPACK info of the batch (synchronises the stream)
+int first_info(const int *info_d, long k, hipStream_t s) {
+    std::vector<int> h(k);
+    SBX_HIP_CHECK(hipMemcpyAsync(h.data(), info_d, sizeof(int) * k, hipMemcpyDeviceToHost, s));
+    SBX_HIP_CHECK(hipStreamSynchronize(s));
+    for (int v : h)
+        if (v) return v;
+    return 0;
+}
+
+/// Calls f(E{}) with the element type of `t`
+template <typename F> void dispatch(int t, F &&f) {
+    switch (t) {
+    case SBX_CDOUBLE: return f(double2{});
+    case SBX_CFLOAT: return f(float2{});
+    case SBX_DOUBLE: return f(double{});
+    case SBX_FLOAT: return f(float{});
+    default: throw Error("dense: unsupported type");
+    }
+}
+
+} // namespace
+
+int launch_potrf(int t, void *a, long n, long k, int device) {
+    if (n == 0 || k == 0) return 0;
+    if (k >= (1L << 31)) throw Error("dense: too many matrices");
+    set_device(device);
+    hipStream_t s = get_stream(device);
+    Scratch info(sizeof(int) * k, device);
+    {
+        KernelTimer timer("dense", s);
+        dispatch(t, [&](auto z) { potrf_typed<decltype(z)>(a, n, k, (int *)info.ptr, s); });
+    }
+    return first_info((const int *)info.ptr, k, s);
+}
+
+int launch_gesv(int t, void *a, long n, long k, void *b, long m, bool identity,
+                const Scalar &alpha, int device) {
+    if (n == 0 || k == 0) return 0;
+    if (k >= (1L << 31)) throw Error("dense: too many matrices");
+    set_device(device);
+    hipStream_t s = get_stream(device);
+    Scratch info(sizeof(int) * k, device), ipiv(sizeof(int) * k * n, device);
+    {
+        KernelTimer timer("dense", s);
+        dispatch(t, [&](auto z) {
+            gesv_typed<decltype(z)>(a, n, k, b, m, identity, alpha, (int *)ipiv.ptr,
+                                    (int *)info.ptr, s);
+        });
+    }
+    return first_info((const int *)info.ptr, k, s);
+}
+
+void launch_trsm(int t, const void *a, long n, long k, void *x, long m, bool left,
+                 const Scalar &alpha, int device) {
+    if (n == 0 || k == 0 || m == 0) return;
+    if (k >= (1L << 31)) throw Error("dense: too many matrices");
+    set_device(device);
+    hipStream_t s = get_stream(device);
+    KernelTimer timer("dense", s);
+    dispatch(t, [&](auto z) { trsm_typed<decltype(z)>(a, n, k, x, m, left, alpha, s); });
+}
+
+} // namespace sbx

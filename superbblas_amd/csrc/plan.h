@@ -156,4 +156,15 @@ void dist_contraction(const Scalar &alpha, const DistTensor &v0, const Coor &fro
 void local_contraction(const Scalar &alpha, const Local &x, bool conjx, const Local &y,
                        bool conjy, const Scalar &beta, const Local &r);
 
+//
+// Dense batched solvers (dense.cpp, reference dense.h)
+//
+void dense_cholesky(const DistTensor &v, const std::string &orows, const std::string &ocols,
+                    const Comm &comm);
+void dense_inversion(const DistTensor &v, const std::string &orows, const std::string &ocols,
+                     const Comm &comm);
+void dense_solve(bool gesm, const Scalar &alpha, const DistTensor &c, const std::string &orows,
+                 const std::string &ocols, const DistTensor &x, const DistTensor &y,
+                 const Comm &comm);
+
 } // namespace sbx

@@ -202,6 +202,15 @@ struct BsrDesc {
 };
 void launch_bsr(const BsrDesc &d, int device);
 void launch_bsr_kron(const BsrDesc &d, int device);
+/// Dense batched solvers on k column-major n x n matrices (kernels_dense.hip); the int results
+/// are the first nonzero LAPACK info of the batch (0: success)
+int launch_potrf(int t, void *a, long n, long k, int device);
+/// LU + solve: B (n x m per matrix) <- alpha A^-1 B (identity: B starts as I); A gets the LU
+int launch_gesv(int t, void *a, long n, long k, void *b, long m, bool identity,
+                const Scalar &alpha, int device);
+/// left: X (n x m) <- alpha U^-1 X;  right: X (m x n) <- alpha X U^-1  (U upper, non-unit)
+void launch_trsm(int t, const void *a, long n, long k, void *x, long m, bool left,
+                 const Scalar &alpha, int device);
 /// dst block q = (conj if conj_values) src block perm[q], q < nblocks, blocks of block_elems
 void launch_gather_blocks(int t, const void *src, const int *perm, long nblocks, long block_elems,
                           bool conj_values, void *dst, int device);

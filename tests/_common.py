@@ -122,6 +122,26 @@ def oracle_kron_bsr(t, site_dim, co, block_rows, nnz, bi, bd, ki, kd, jj, v, kro
     assert rc == 0
 
 
+def oracle_potrf(a, n, k):
+    return oracle().oracle_potrf_upper(TYPE_OF[a.dtype], ctypes.c_long(n), ctypes.c_long(k), ptr(a))
+
+
+def oracle_getrf(a, n, k, ipiv):
+    return oracle().oracle_getrf(TYPE_OF[a.dtype], ctypes.c_long(n), ctypes.c_long(k), ptr(a),
+                                 ptr(ipiv))
+
+
+def oracle_getrs(a, n, k, ipiv, m, b):
+    return oracle().oracle_getrs(TYPE_OF[a.dtype], ctypes.c_long(n), ctypes.c_long(k), ptr(a),
+                                 ptr(ipiv), ctypes.c_long(m), ptr(b))
+
+
+def oracle_trsm(left, n, k, m, alpha, a, x):
+    return oracle().oracle_trsm_upper(TYPE_OF[a.dtype], int(left), ctypes.c_long(n),
+                                      ctypes.c_long(k), ctypes.c_long(m),
+                                      ctypes.cast(scal(alpha), ctypes.c_void_p), ptr(a), ptr(x))
+
+
 def int_valued(n, dtype, seed=0):
     """Small integer-valued data (exact in every supported type)."""
     i = np.arange(n, dtype=np.int64) + seed * 7919

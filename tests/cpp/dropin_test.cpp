@@ -152,6 +152,65 @@ int main() {
         CHECK(ok, "masked copy ij -> ji (host components)");
     }
 
+    // ---- dense: Cholesky of HPD matrices, then trsm / gesm solves (dense.h:1160-1266) ----
+    {
+        Context cpu = createCpuContext();
+        const int n = 5, nt = 3;
+        const Coor<3> d{nt, n, n}, dx{nt, n, 2};
+        std::vector<Z> a(nt * n * n), u, g(nt * n * n), x(nt * n * 2), y(nt * n * 2);
+        for (int t = 0; t < nt; ++t)
+            for (int i = 0; i < n; ++i)
+                for (int j = 0; j < n; ++j) {
+                    Z s = 0;
+                    for (int q = 0; q < n; ++q)
+                        s += std::conj(val(t * 25 + q * 5 + i, 3)) * val(t * 25 + q * 5 + j, 3);
+                    a[(t * n + i) * n + j] = s + (i == j ? Z(n) : Z(0));
+                    g[(t * n + i) * n + j] = val(t * 25 + i * 5 + j, 4) + (i == j ? Z(20) : Z(0));
+                }
+        for (long i = 0; i < (long)x.size(); ++i) x[i] = val(i, 5);
+        u = a;
+        PartitionItem<3> p{Coor<3>{}, d}, px{Coor<3>{}, dx};
+        Z *up = u.data();
+        cholesky<3, Z>(&p, d, 1, "tij", &up, "i", "j", &cpu, SlowToFast);
+        bool ok = true;
+        for (int t = 0; t < nt; ++t)
+            for (int i = 0; i < n; ++i)
+                for (int j = i; j < n; ++j) {
+                    Z s = 0; // (U^H U)(i, j), U(r, c) at (t, r, c)
+                    for (int q = 0; q <= i; ++q)
+                        s += std::conj(u[(t * n + q) * n + i]) * u[(t * n + q) * n + j];
+                    ok &= std::abs(s - a[(t * n + i) * n + j]) < 1e-10 * std::abs(a[(t * n + i) * n + i]);
+                }
+        CHECK(ok, "cholesky: U^H U == A");
+        // trsm: y = U^-1 x, then U y == x
+        const Z *cu = u.data(), *cx = x.data();
+        Z *py = y.data();
+        trsm<3, 3, 3, Z>(Z(1), &p, d, 1, "tij", &cu, "i", "j", &cpu, &px, dx, 1, "tjn", &cx, &cpu,
+                         &px, dx, 1, "tin", &py, &cpu, SlowToFast);
+        ok = true;
+        for (int t = 0; t < nt; ++t)
+            for (int i = 0; i < n; ++i)
+                for (int c = 0; c < 2; ++c) {
+                    Z s = 0;
+                    for (int q = i; q < n; ++q) s += u[(t * n + i) * n + q] * y[(t * n + q) * 2 + c];
+                    ok &= std::abs(s - x[(t * n + i) * 2 + c]) < 1e-10;
+                }
+        CHECK(ok, "trsm: U y == x");
+        // gesm: y = G^-1 x, then G y == x
+        const Z *cg = g.data();
+        gesm<3, 3, 3, Z>(Z(1), &p, d, 1, "tij", &cg, "i", "j", &cpu, &px, dx, 1, "tjn", &cx, &cpu,
+                         &px, dx, 1, "tin", &py, &cpu, SlowToFast);
+        ok = true;
+        for (int t = 0; t < nt; ++t)
+            for (int i = 0; i < n; ++i)
+                for (int c = 0; c < 2; ++c) {
+                    Z s = 0;
+                    for (int q = 0; q < n; ++q) s += g[(t * n + i) * n + q] * y[(t * n + q) * 2 + c];
+                    ok &= std::abs(s - x[(t * n + i) * 2 + c]) < 1e-10;
+                }
+        CHECK(ok, "gesm: G y == x");
+    }
+
     // ---- BSR: 9-point periodic stencil, 3x3 blocks, x pXYZTSCn -> y pxyztscn (tests/bsr.cpp) ----
     {
         const Coor<6> dim{L, L, L, L, 1, c};

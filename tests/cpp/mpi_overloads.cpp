@@ -25,6 +25,12 @@ void use_mpi_overloads(MPI_Comm comm) {
     create_kron_bsr<2, 2, Z>(&p, d, &p, d, 1, Coor<2>{1, 1}, Coor<2>{1, 1}, Coor<2>{1, 1},
                              Coor<2>{1, 1}, false, &ii, &jj, &c0, &c0, &gpu, comm, SlowToFast,
                              &op);
+    cholesky<2, Z>(&p, d, 1, "ab", &v1, "a", "b", &gpu, comm, SlowToFast);
+    inversion<2, Z>(&p, d, 1, "ab", &v1, "a", "b", &gpu, comm, SlowToFast);
+    trsm<2, 2, 2, Z>(Z(1), &p, d, 1, "ab", &c0, "a", "b", &gpu, &p, d, 1, "bn", &c0, &gpu, &p, d,
+                     1, "an", &v1, &gpu, comm, SlowToFast);
+    gesm<2, 2, 2, Z>(Z(1), &p, d, 1, "ab", &c0, "a", "b", &gpu, &p, d, 1, "bn", &c0, &gpu, &p, d,
+                     1, "an", &v1, &gpu, comm, SlowToFast);
     const PartitionItem<3> px{Coor<3>{}, Coor<3>{4, 4, 2}};
     bsr_krylov<2, 2, 3, 3, Z>(Z(1), op, "ab", "AB", &px, 1, "ABn", Coor<3>{}, Coor<3>{4, 4, 2},
                               Coor<3>{4, 4, 2}, &c0, Z(0), &px, "abn", Coor<3>{}, Coor<3>{4, 4, 2},

@@ -300,6 +300,52 @@ def case_kron(sb, comm, rank, n, dev, ncols=2, power=2):
     assert np.array_equal(out, np.concatenate(refs)), "kron bsr"
 
 
+def case_dense(sb, comm, rank, n, dev):
+    """cholesky / gesm with the matrices split over ranks along a row label (the working copy
+    gathers whole matrices: a redistribution), and the batch label split too."""
+    from _common import oracle_getrf, oracle_getrs, oracle_potrf
+    from _dense import dense_input, from_matrices, to_matrices, to_panel, from_panel
+    nt, ni = 4, 6
+    dim = [nt, ni, ni]
+    p = sb.basic_partitioning("tij", dim, [1, n, 1], "i", n, 1)  # rows split over ranks
+    a = dense_input("hpd", nt, ni, np.complex128)
+    g = from_matrices(a, "tij", dim, "i", "j")
+    v = scatter(sb, g, dim, p, rank, 1, dev)
+    sb.cholesky(p, dim, "tij", v, "i", "j", comm=comm)
+    torch.cuda.synchronize()
+    out = gather(np.zeros_like(g), dim, p, 1, v)
+    w = np.ascontiguousarray(a.transpose(0, 2, 1)).ravel()
+    assert oracle_potrf(w, ni, nt) == 0
+    ref = from_matrices(w.reshape(nt, ni, ni).transpose(0, 2, 1), "tij", dim, "i", "j")
+    assert np.allclose(out, ref, rtol=0, atol=1e-12 * np.abs(ref).max()), "dense cholesky"
+    # gesm: C split over t, x (another label order) split over t too -- the right-hand-side
+    # labels of x must be whole in each component, as in the reference (dense.h:565-598) --,
+    # y split over its rows
+    c = dense_input("gen", nt, ni, np.complex128)
+    gc = from_matrices(c, "tij", dim, "i", "j")
+    pc = sb.basic_partitioning("tij", dim, [n, 1, 1], "t", n, 1)
+    dimx = [nt, ni, 4]
+    dimxp = [4, nt, ni]  # "ntj"
+    px = sb.basic_partitioning("ntj", dimxp, [1, n, 1], "t", n, 1)
+    py = sb.basic_partitioning("tin", dimx, [1, n, 1], "i", n, 1)
+    gx = gen("int", vol(dimx), 5, np.complex128)
+    gxp = np.ascontiguousarray(gx.reshape(dimx).transpose(2, 0, 1)).ravel()
+    vc = scatter(sb, gc, dim, pc, rank, 1, dev)
+    vx = scatter(sb, gxp, dimxp, px, rank, 1, dev)
+    vy = scatter(sb, np.zeros_like(gx), dimx, py, rank, 1, dev)
+    sb.gesm(2.0, pc, dim, "tij", vc, "i", "j", px, dimxp, "ntj", vx, py, dimx, "tin", vy,
+            comm=comm)
+    torch.cuda.synchronize()
+    out = gather(np.zeros_like(gx), dimx, py, 1, vy)
+    w = np.ascontiguousarray(c.transpose(0, 2, 1)).ravel()
+    piv = np.zeros(nt * ni, np.int32)
+    assert oracle_getrf(w, ni, nt, piv) == 0
+    xm = np.ascontiguousarray(to_panel(gx, "tjn", dimx, "n", "j")).ravel()
+    oracle_getrs(w, ni, nt, piv, 4, xm)
+    ref = 2.0 * from_panel(xm.reshape(nt, 4, ni), "tin", dimx, "n", "i")
+    assert np.allclose(out, ref, rtol=0, atol=1e-12 * np.abs(ref).max()), "dense gesm"
+
+
 def main():
     dist.init_process_group("gloo")
     rank, n = dist.get_rank(), dist.get_world_size()
@@ -313,7 +359,7 @@ def main():
         comm = sb.Comm.from_torch_distributed(dev_idx)
     else:
         comm = sb.Comm.host_staged(dev_idx)
-    cases = os.environ.get("SBX_TEST_CASES", "copy,contr,bsr,kron").split(",")
+    cases = os.environ.get("SBX_TEST_CASES", "copy,contr,bsr,kron,dense").split(",")
     if "copy" in cases:
         case_copy(sb, comm, rank, n, dev)
     if "contr" in cases:
@@ -322,6 +368,8 @@ def main():
         case_bsr(sb, comm, rank, n, dev)
     if "kron" in cases:
         case_kron(sb, comm, rank, n, dev)
+    if "dense" in cases:
+        case_dense(sb, comm, rank, n, dev)
     dist.barrier()
     comm.close()
     dist.destroy_process_group()

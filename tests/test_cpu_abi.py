@@ -17,6 +17,7 @@ def declared_symbols():
 def test_header_declares_api():
     syms = declared_symbols()
     for s in ("sbx_copy", "sbx_contraction", "sbx_create_bsr", "sbx_create_kron_bsr", "sbx_bsr_krylov",
+              "sbx_copy_masked", "sbx_cholesky", "sbx_trsm", "sbx_gesm", "sbx_inversion",
               "sbx_destroy_bsr", "sbx_comm_create", "sbx_xgemm_batch_strided"):
         assert s in syms
 

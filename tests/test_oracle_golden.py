@@ -144,3 +144,86 @@ def test_oracle_bsr_adjoint_identity():
     oracle_bsr_adjoint(T_CDOUBLE, [L, L, L, L, spin, color], 0, V, b, b, ii, jj, vals, False, y,
                        ncols, True, ahy, ncols, True, V * b, ncols, 1.0)
     assert np.vdot(y, ax) == np.vdot(ahy, x)
+
+
+# ---- dense batched solvers (dense.h) ----
+
+def _cm(m):
+    """(nb, n, n) [b, r, c] -> column-major data per matrix"""
+    return np.ascontiguousarray(m.transpose(0, 2, 1)).ravel()
+
+
+def _from_cm(d, nb, r, c):
+    return d.reshape(nb, c, r).transpose(0, 2, 1)
+
+
+def _dense_tol(t):
+    return 1e-12 if np.dtype(t) in (np.float64, np.complex128) else 1e-5
+
+
+@pytest.mark.parametrize("case", manifest("cholesky") + manifest("inversion"),
+                         ids=lambda c: "%s%d" % (c["kind"], c["id"]))
+def test_oracle_dense_inplace(case):
+    from _common import oracle_getrf, oracle_getrs, oracle_potrf
+    from _dense import dense_input, from_matrices, to_matrices
+    t = NPT[case["t"]]
+    o, dim, n = case["o"], case["dim"], case["n"]
+    nt = dim[0]
+    a = dense_input(case["input"], nt, n, t)  # [t, r, c]
+    # lay the input out as the tensor o (t + rows + cols), as the golden generator did
+    g = from_matrices(a, "t" + case["orows"] + case["ocols"],
+                      [dim[o.index(c)] for c in "t" + case["orows"] + case["ocols"]],
+                      case["orows"], case["ocols"])
+    g = to_matrices(g, "t" + case["orows"] + case["ocols"],
+                    [dim[o.index(c)] for c in "t" + case["orows"] + case["ocols"]],
+                    case["orows"], case["ocols"])
+    w = _cm(g).astype(t)
+    if case["kind"] == "cholesky":
+        assert oracle_potrf(w, n, nt) == 0
+    else:
+        piv = np.zeros(nt * n, np.int32)
+        assert oracle_getrf(w, n, nt, piv) == 0
+        eye = np.tile(np.eye(n, dtype=t).ravel(), nt)
+        assert oracle_getrs(w, n, nt, piv, n, eye) == 0
+        w = eye
+    res = _from_cm(w, nt, n, n)
+    ref = to_matrices(output(case, t), o, dim, case["orows"], case["ocols"])
+    assert np.allclose(res, ref, rtol=0, atol=_dense_tol(t) * np.abs(ref).max())
+
+
+@pytest.mark.parametrize("case", manifest("trsm") + manifest("gesm"),
+                         ids=lambda c: "%s%d" % (c["kind"], c["id"]))
+def test_oracle_dense_solve(case):
+    from _common import oracle_getrf, oracle_getrs, oracle_trsm
+    from _dense import dense_input, from_panel, to_panel
+    t = NPT[case["t"]]
+    oc, n = case["oc"], case["n"]
+    nt = case["dimc"][0]
+    c = dense_input("tri" if case["kind"] == "trsm" else "gen", nt, n, t)
+    ox, oy, dimx, dimy = case["ox"], case["oy"], case["dimx"], case["dimy"]
+    x = gen("int", vol(dimx), 5, t)
+    alpha = complex(*case["alpha"]) if np.dtype(t).kind == "c" else case["alpha"][0]
+    rows, cols = case["orows"], case["ocols"]
+    on = [l for l in ox if l not in oc]
+    contract_rows = any(l in rows for l in ox)
+    cw = _cm(c)
+    if not contract_rows:  # C \\ X: X (n x m), rows = column labels
+        xm = to_panel(x, ox, dimx, on, cols)  # [b, m, n] = column-major (n x m)
+        m = xm.shape[1]
+        xw = np.ascontiguousarray(xm).ravel().astype(t)
+        if case["kind"] == "trsm":
+            oracle_trsm(True, n, nt, m, alpha, cw, xw)
+        else:
+            piv = np.zeros(nt * n, np.int32)
+            assert oracle_getrf(cw, n, nt, piv) == 0
+            oracle_getrs(cw, n, nt, piv, m, xw)
+            xw = xw * alpha
+        res = from_panel(xw.reshape(nt, m, n), oy, dimy, on, rows)
+    else:  # X / C: X (m x n), columns = row labels
+        xm = to_panel(x, ox, dimx, rows, on)  # [b, n, m] = column-major (m x n)
+        m = xm.shape[2]
+        xw = np.ascontiguousarray(xm).ravel().astype(t)
+        oracle_trsm(False, n, nt, m, alpha, cw, xw)
+        res = from_panel(xw.reshape(nt, n, m), oy, dimy, cols, on)
+    ref = output(case, t)
+    assert np.allclose(res, ref, rtol=0, atol=_dense_tol(t) * np.abs(ref).max())
