@@ -75,8 +75,14 @@ inline Context createCudaContext(int) {
 
 struct BSR_handle; // opaque (sbx_bsr)
 
+/// elem<T>::type is T's element type if T is an array, otherwise T (blas.h:98-108)
 template <typename T> struct elem { using type = T; };
-template <typename T> struct elem<std::complex<T>> { using type = T; };
+template <typename T, std::size_t N> struct elem<std::array<T, N>> {
+    using type = typename elem<T>::type;
+};
+template <typename T, std::size_t N> struct elem<const std::array<T, N>> {
+    using type = typename elem<T>::type;
+};
 
 /// Communicator of the distributed overloads (replaces MPI_Comm)
 using Communicator = sbx_comm;
@@ -658,6 +664,241 @@ void gesm(T alpha, const PartitionItem<Nc> *pc, const Coor<Nc> &dimc, int ncompo
                                                 comm, co, session);
 }
 
+// ---- tensor storage, the S3T file format (storage.h:2374-2617) ----
+
+/// Type of the values (storage.h:63) and of checksum (storage.h:66-70)
+enum values_datatype { FLOAT = 0, DOUBLE = 1, CFLOAT = 2, CDOUBLE = 3, CHAR = 4, INT = 5 };
+enum checksum_type { NoChecksum = 0, GlobalChecksum = 1, BlockChecksum = 2 };
+
+/// Handle to a tensor storage (storage.h:2127)
+using Storage_handle = sbx_storage;
+
+namespace sbx_detail {
+/// get_storage_context (storage.h:1630-1645): the template parameters must match the file
+template <std::size_t Nd, typename T> inline sbx_storage storage_of(Storage_handle stoh) {
+    int nd = 0, t = 0;
+    check(sbx_storage_info(stoh, &nd, &t));
+    if (t != dtype<T>::value)
+        throw std::runtime_error(
+            "The template parameter T does not match with the datatype of the storage");
+    if (nd != (int)Nd)
+        throw std::runtime_error("The template parameter Nd does not match with the number of "
+                                 "dimensions of the storage");
+    return stoh;
+}
+template <typename T> inline int storage_dtype() {
+    static_assert(!std::is_same<T, std::size_t>::value, "storage: unsupported type");
+    return dtype<T>::value;
+}
+template <std::size_t Nd0, std::size_t Nd1, typename T, typename Q>
+void save_impl(typename elem<T>::type alpha, const PartitionItem<Nd0> *p0, int ncomponents0,
+               const char *o0, const Coor<Nd0> &from0, const Coor<Nd0> &size0,
+               const Coor<Nd0> &dim0, const T **v0, const Context *ctx0, const char *o1,
+               const Coor<Nd1> &from1, Storage_handle stoh, sbx_comm comm, CoorOrder co,
+               Session session) {
+    check_session(session);
+    const auto a = scalar(alpha);
+    const auto c = contexts(ctx0, ncomponents0);
+    check(sbx_storage_save((int)Nd0, (int)Nd1, a.data(), dtype<T>::value, parts(p0),
+                           ncomponents0, o0, from0.data(), size0.data(), dim0.data(),
+                           (const void *const *)v0, c.data(), o1, from1.data(),
+                           storage_of<Nd1, Q>(stoh), comm, co_of(co), 0));
+}
+template <std::size_t Nd0, std::size_t Nd1, typename T, typename Q>
+void load_impl(typename elem<T>::type alpha, Storage_handle stoh, const char *o0,
+               const Coor<Nd0> &from0, const Coor<Nd0> &size0, const PartitionItem<Nd1> *p1,
+               int ncomponents1, const char *o1, const Coor<Nd1> &from1, const Coor<Nd1> &dim1,
+               Q **v1, const Context *ctx1, sbx_comm comm, CoorOrder co, CopyAdd copyadd,
+               Session session) {
+    check_session(session);
+    const auto a = scalar(alpha);
+    const auto c = contexts(ctx1, ncomponents1);
+    check(sbx_storage_load((int)Nd0, (int)Nd1, a.data(), storage_of<Nd0, T>(stoh), o0,
+                           from0.data(), size0.data(), dtype<Q>::value, parts(p1), ncomponents1,
+                           o1, from1.data(), dim1.data(), (void *const *)v1, c.data(), comm,
+                           co_of(co), copyadd == Add ? SBX_ADD : SBX_COPY, 0));
+}
+template <std::size_t Nd0, std::size_t Nd1, typename Q>
+void append_impl(const PartitionItem<Nd0> *p0, int num_blocks, const char *o0,
+                 const Coor<Nd0> &from0, const Coor<Nd0> &size0, const Coor<Nd0> &dim0,
+                 const char *o1, const Coor<Nd1> &from1, Storage_handle stoh, sbx_comm comm,
+                 CoorOrder co) {
+    check(sbx_storage_append_blocks((int)Nd0, (int)Nd1, parts(p0), num_blocks, o0, from0.data(),
+                                    size0.data(), dim0.data(), o1, from1.data(),
+                                    storage_of<Nd1, Q>(stoh), comm, co_of(co)));
+}
+template <std::size_t N> inline std::string trivial_order() {
+    std::string o(N, 'a');
+    for (std::size_t i = 0; i < N; ++i) o[i] = (char)('a' + i);
+    return o;
+}
+inline void read_header_impl(const char *filename, CoorOrder co, values_datatype &values_dtype,
+                             std::vector<char> &metadata, std::vector<IndexType> &size) {
+    int t = 0, ml = 0, nd = 0;
+    check(sbx_storage_read_header(filename, co_of(co), &t, nullptr, 0, &ml, &nd, nullptr, 0));
+    metadata.resize(ml);
+    size.resize(nd);
+    check(sbx_storage_read_header(filename, co_of(co), &t, metadata.data(), ml, &ml, &nd,
+                                  size.data(), nd));
+    switch (t) {
+    case SBX_FLOAT: values_dtype = FLOAT; break;
+    case SBX_DOUBLE: values_dtype = DOUBLE; break;
+    case SBX_CFLOAT: values_dtype = CFLOAT; break;
+    case SBX_CDOUBLE: values_dtype = CDOUBLE; break;
+    default: values_dtype = INT; break;
+    }
+}
+} // namespace sbx_detail
+
+/// create_storage: a new file for a tensor of dims `dim` (its content, if any, is lost),
+/// storage.h:2386-2395
+template <std::size_t Nd, typename T>
+void create_storage(const Coor<Nd> &dim, CoorOrder co, const char *filename,
+                    const char *metadata, int metadata_length, checksum_type checksum,
+                    Storage_handle *stoh) {
+    sbx_detail::check(sbx_storage_create((int)Nd, dim.data(), sbx_detail::co_of(co), filename,
+                                         metadata, metadata_length, (int)checksum,
+                                         sbx_detail::storage_dtype<T>(), nullptr, stoh));
+}
+template <std::size_t Nd, typename T>
+void create_storage(const Coor<Nd> &dim, CoorOrder co, const char *filename,
+                    const char *metadata, int metadata_length, checksum_type checksum,
+                    Communicator comm, Storage_handle *stoh) {
+    sbx_detail::check(sbx_storage_create((int)Nd, dim.data(), sbx_detail::co_of(co), filename,
+                                         metadata, metadata_length, (int)checksum,
+                                         sbx_detail::storage_dtype<T>(), comm, stoh));
+}
+
+/// read_storage_header: values type, metadata and dims of a file, storage.h:2405-2421
+inline void read_storage_header(const char *filename, CoorOrder co,
+                                values_datatype &values_dtype, std::vector<char> &metadata,
+                                std::vector<IndexType> &size) {
+    sbx_detail::read_header_impl(filename, co, values_dtype, metadata, size);
+}
+
+/// open_storage: open an existing file, storage.h:2469-2476
+template <std::size_t Nd, typename T>
+void open_storage(const char *filename, bool allow_writing, Storage_handle *stoh) {
+    sbx_detail::check(sbx_storage_open((int)Nd, sbx_detail::storage_dtype<T>(), filename,
+                                       allow_writing ? 1 : 0, nullptr, stoh));
+}
+template <std::size_t Nd, typename T>
+void open_storage(const char *filename, bool allow_writing, Communicator comm,
+                  Storage_handle *stoh) {
+    sbx_detail::check(sbx_storage_open((int)Nd, sbx_detail::storage_dtype<T>(), filename,
+                                       allow_writing ? 1 : 0, comm, stoh));
+}
+
+/// append_blocks: declare blocks as stored (in the storage's coordinates), storage.h:2484-2495
+template <std::size_t Nd1, typename Q>
+void append_blocks(const PartitionItem<Nd1> *p, int num_blocks, const Coor<Nd1> &dim,
+                   Storage_handle stoh, CoorOrder co) {
+    const std::string o = sbx_detail::trivial_order<Nd1>();
+    sbx_detail::append_impl<Nd1, Nd1, Q>(p, num_blocks, o.c_str(), Coor<Nd1>{{}}, dim, dim,
+                                         o.c_str(), Coor<Nd1>{{}}, stoh, nullptr, co);
+}
+template <std::size_t Nd1, typename Q>
+void append_blocks(const PartitionItem<Nd1> *p, int num_blocks, const Coor<Nd1> &dim,
+                   Storage_handle stoh, Communicator comm, CoorOrder co) {
+    const std::string o = sbx_detail::trivial_order<Nd1>();
+    sbx_detail::append_impl<Nd1, Nd1, Q>(p, num_blocks, o.c_str(), Coor<Nd1>{{}}, dim, dim,
+                                         o.c_str(), Coor<Nd1>{{}}, stoh, comm, co);
+}
+/// append_blocks: blocks of a tensor (labels o0) restricted to [from0, from0+size0) and placed
+/// at from1 on the storage (labels o1), storage.h:2509-2521
+template <std::size_t Nd0, std::size_t Nd1, typename Q>
+void append_blocks(const PartitionItem<Nd0> *p0, int num_blocks, const char *o0,
+                   const Coor<Nd0> &from0, const Coor<Nd0> &size0, const Coor<Nd0> dim0,
+                   const char *o1, const Coor<Nd1> &from1, Storage_handle stoh, CoorOrder co) {
+    sbx_detail::append_impl<Nd0, Nd1, Q>(p0, num_blocks, o0, from0, size0, dim0, o1, from1, stoh,
+                                         nullptr, co);
+}
+template <std::size_t Nd0, std::size_t Nd1, typename Q>
+void append_blocks(const PartitionItem<Nd0> *p0, int num_blocks, const char *o0,
+                   const Coor<Nd0> &from0, const Coor<Nd0> &size0, const Coor<Nd0> dim0,
+                   const char *o1, const Coor<Nd1> &from1, Storage_handle stoh,
+                   Communicator comm, CoorOrder co) {
+    sbx_detail::append_impl<Nd0, Nd1, Q>(p0, num_blocks, o0, from0, size0, dim0, o1, from1, stoh,
+                                         comm, co);
+}
+
+/// save: alpha * v0[from0:from0+size0] into the stored blocks at from1, storage.h:2539-2554
+template <std::size_t Nd0, std::size_t Nd1, typename T, typename Q>
+void save(typename elem<T>::type alpha, const PartitionItem<Nd0> *p0, int ncomponents0,
+          const char *o0, const Coor<Nd0> &from0, const Coor<Nd0> &size0, const Coor<Nd0> &dim0,
+          const T **v0, const Context *ctx0, const char *o1, const Coor<Nd1> &from1,
+          Storage_handle stoh, CoorOrder co, Session session = 0) {
+    sbx_detail::save_impl<Nd0, Nd1, T, Q>(alpha, p0, ncomponents0, o0, from0, size0, dim0, v0,
+                                          ctx0, o1, from1, stoh, nullptr, co, session);
+}
+template <std::size_t Nd0, std::size_t Nd1, typename T, typename Q>
+void save(typename elem<T>::type alpha, const PartitionItem<Nd0> *p0, int ncomponents0,
+          const char *o0, const Coor<Nd0> &from0, const Coor<Nd0> &size0, const Coor<Nd0> &dim0,
+          const T **v0, const Context *ctx0, const char *o1, const Coor<Nd1> &from1,
+          Storage_handle stoh, Communicator comm, CoorOrder co, Session session = 0) {
+    sbx_detail::save_impl<Nd0, Nd1, T, Q>(alpha, p0, ncomponents0, o0, from0, size0, dim0, v0,
+                                          ctx0, o1, from1, stoh, comm, co, session);
+}
+
+/// load: v1[from1 + P(c - from0)] = alpha * sto[c] for the stored c in [from0, from0+size0)
+/// (Add copies as well, as the reference's local_load does), storage.h:2571-2595
+template <std::size_t Nd0, std::size_t Nd1, typename T, typename Q>
+void load(typename elem<T>::type alpha, Storage_handle stoh, const char *o0,
+          const Coor<Nd0> from0, const Coor<Nd0> size0, const PartitionItem<Nd1> *p1,
+          int ncomponents1, const char *o1, const Coor<Nd1> &from1, const Coor<Nd1> &dim1,
+          Q **v1, const Context *ctx1, CoorOrder co, CopyAdd copyadd, Session session = 0) {
+    sbx_detail::load_impl<Nd0, Nd1, T, Q>(alpha, stoh, o0, from0, size0, p1, ncomponents1, o1,
+                                          from1, dim1, v1, ctx1, nullptr, co, copyadd, session);
+}
+template <std::size_t Nd0, std::size_t Nd1, typename T, typename Q>
+void load(typename elem<T>::type alpha, Storage_handle stoh, const char *o0,
+          const Coor<Nd0> &from0, const Coor<Nd0> &size0, const PartitionItem<Nd1> *p1,
+          int ncomponents1, const char *o1, const Coor<Nd1> &from1, const Coor<Nd1> &dim1,
+          Q **v1, const Context *ctx1, Communicator comm, CoorOrder co, CopyAdd copyadd,
+          Session session = 0) {
+    sbx_detail::load_impl<Nd0, Nd1, T, Q>(alpha, stoh, o0, from0, size0, p1, ncomponents1, o1,
+                                          from1, dim1, v1, ctx1, comm, co, copyadd, session);
+}
+
+/// get_blocks: stored boxes overlapping [from1, from1+size1) of a tensor with labels o1,
+/// relative to from1, storage.h:2608-2617
+template <std::size_t Nd0, std::size_t Nd1, typename T>
+void get_blocks(Storage_handle stoh, const char *o0, const char *o1, const Coor<Nd1> from1,
+                const Coor<Nd1> size1, std::vector<PartitionItem<Nd1>> &blocks, CoorOrder co) {
+    sbx_storage s = sbx_detail::storage_of<Nd0, T>(stoh);
+    int n = 0;
+    sbx_detail::check(sbx_storage_get_blocks(s, (int)Nd0, (int)Nd1, o0, o1, from1.data(),
+                                             size1.data(), sbx_detail::co_of(co), nullptr, 0,
+                                             &n));
+    const std::size_t first = blocks.size();
+    blocks.resize(first + n);
+    sbx_detail::check(sbx_storage_get_blocks(
+        s, (int)Nd0, (int)Nd1, o0, o1, from1.data(), size1.data(), sbx_detail::co_of(co),
+        reinterpret_cast<int *>(blocks.data() + first), n, &n));
+}
+
+/// check_storage: verify the checksums, storage.h:2439-2446
+template <std::size_t Nd1, typename Q> void check_storage(Storage_handle stoh) {
+    sbx_detail::check(sbx_storage_check(sbx_detail::storage_of<Nd1, Q>(stoh), nullptr));
+}
+template <std::size_t Nd1, typename Q> void check_storage(Storage_handle stoh, Communicator comm) {
+    sbx_detail::check(sbx_storage_check(sbx_detail::storage_of<Nd1, Q>(stoh), comm));
+}
+
+/// close_storage: write the pending checksums and release the handle, storage.h:2451-2460
+template <std::size_t Nd1, typename Q> void close_storage(Storage_handle stoh) {
+    sbx_detail::check(sbx_storage_close(sbx_detail::storage_of<Nd1, Q>(stoh), nullptr));
+}
+template <std::size_t Nd1, typename Q> void close_storage(Storage_handle stoh, Communicator comm) {
+    sbx_detail::check(sbx_storage_close(sbx_detail::storage_of<Nd1, Q>(stoh), comm));
+}
+
+/// preallocate_storage / flush_storage, storage.h:2427-2434
+inline void preallocate_storage(Storage_handle stoh, std::size_t size) {
+    sbx_detail::check(sbx_storage_preallocate(stoh, (unsigned long long)size));
+}
+inline void flush_storage(Storage_handle stoh) { sbx_detail::check(sbx_storage_flush(stoh)); }
+
 // ---- MPI overloads: a host-staged communicator over MPI_Alltoallv (dist.h:1426-1500) ----
 #ifdef SUPERBBLAS_USE_MPI
 namespace sbx_detail {
@@ -818,6 +1059,71 @@ void gesm(T alpha, const PartitionItem<Nc> *pc, const Coor<Nc> &dimc, int ncompo
         ncomponentsx, ox, vx, ctxx, py, dimy, ncomponentsy, oy, vy, ctxy,
         sbx_detail::comm_of(mpicomm, ctxc, ncomponentsc), co, session);
 }
+// storage over MPI (storage.h:2142-2370)
+template <std::size_t Nd, typename T>
+void create_storage(const Coor<Nd> &dim, CoorOrder co, const char *filename,
+                    const char *metadata, int metadata_length, checksum_type checksum,
+                    MPI_Comm mpicomm, Storage_handle *stoh) {
+    create_storage<Nd, T>(dim, co, filename, metadata, metadata_length, checksum,
+                          sbx_detail::comm_of(mpicomm, nullptr, 0), stoh);
+}
+inline void read_storage_header(const char *filename, CoorOrder co,
+                                values_datatype &values_dtype, std::vector<char> &metadata,
+                                std::vector<IndexType> &size, MPI_Comm) {
+    sbx_detail::read_header_impl(filename, co, values_dtype, metadata, size);
+}
+template <std::size_t Nd, typename T>
+void open_storage(const char *filename, bool allow_writing, MPI_Comm mpicomm,
+                  Storage_handle *stoh) {
+    open_storage<Nd, T>(filename, allow_writing, sbx_detail::comm_of(mpicomm, nullptr, 0), stoh);
+}
+template <std::size_t Nd1, typename Q>
+void append_blocks(const PartitionItem<Nd1> *p, int num_blocks, const Coor<Nd1> &dim,
+                   Storage_handle stoh, MPI_Comm mpicomm, CoorOrder co) {
+    append_blocks<Nd1, Q>(p, num_blocks, dim, stoh, sbx_detail::comm_of(mpicomm, nullptr, 0), co);
+}
+template <std::size_t Nd0, std::size_t Nd1, typename Q>
+void append_blocks(const PartitionItem<Nd0> *p0, int num_blocks, const char *o0,
+                   const Coor<Nd0> &from0, const Coor<Nd0> &size0, const Coor<Nd0> &dim0,
+                   const char *o1, const Coor<Nd1> &from1, Storage_handle stoh,
+                   MPI_Comm mpicomm, CoorOrder co) {
+    append_blocks<Nd0, Nd1, Q>(p0, num_blocks, o0, from0, size0, dim0, o1, from1, stoh,
+                               sbx_detail::comm_of(mpicomm, nullptr, 0), co);
+}
+template <std::size_t Nd0, std::size_t Nd1, typename T, typename Q>
+void save(typename elem<T>::type alpha, const PartitionItem<Nd0> *p0, int ncomponents0,
+          const char *o0, const Coor<Nd0> &from0, const Coor<Nd0> &size0, const Coor<Nd0> &dim0,
+          const T **v0, const Context *ctx0, const char *o1, const Coor<Nd1> &from1,
+          Storage_handle stoh, MPI_Comm mpicomm, CoorOrder co, Session session = 0) {
+    sbx_detail::save_impl<Nd0, Nd1, T, Q>(alpha, p0, ncomponents0, o0, from0, size0, dim0, v0,
+                                          ctx0, o1, from1, stoh,
+                                          sbx_detail::comm_of(mpicomm, ctx0, ncomponents0), co,
+                                          session);
+}
+template <std::size_t Nd0, std::size_t Nd1, typename T, typename Q>
+void load(typename elem<T>::type alpha, Storage_handle stoh, const char *o0,
+          const Coor<Nd0> &from0, const Coor<Nd0> &size0, const PartitionItem<Nd1> *p1,
+          int ncomponents1, const char *o1, const Coor<Nd1> &from1, const Coor<Nd1> &dim1,
+          Q **v1, const Context *ctx1, MPI_Comm mpicomm, CoorOrder co, CopyAdd copyadd,
+          Session session = 0) {
+    sbx_detail::load_impl<Nd0, Nd1, T, Q>(alpha, stoh, o0, from0, size0, p1, ncomponents1, o1,
+                                          from1, dim1, v1, ctx1,
+                                          sbx_detail::comm_of(mpicomm, ctx1, ncomponents1), co,
+                                          copyadd, session);
+}
+template <std::size_t Nd0, std::size_t Nd1, typename T>
+void get_blocks(Storage_handle stoh, const char *o0, const char *o1, const Coor<Nd1> from1,
+                const Coor<Nd1> size1, std::vector<PartitionItem<Nd1>> &blocks, MPI_Comm,
+                CoorOrder co) {
+    get_blocks<Nd0, Nd1, T>(stoh, o0, o1, from1, size1, blocks, co);
+}
+template <std::size_t Nd1, typename Q> void check_storage(Storage_handle stoh, MPI_Comm mpicomm) {
+    check_storage<Nd1, Q>(stoh, sbx_detail::comm_of(mpicomm, nullptr, 0));
+}
+template <std::size_t Nd1, typename Q> void close_storage(Storage_handle stoh, MPI_Comm mpicomm) {
+    close_storage<Nd1, Q>(stoh, sbx_detail::comm_of(mpicomm, nullptr, 0));
+}
+
 #endif // SUPERBBLAS_USE_MPI
 
 } // namespace superbblas

@@ -53,6 +53,7 @@ typedef struct sbx_context {
 
 typedef struct sbx_comm_s *sbx_comm; /* replaces MPI_Comm (dist.h:120-149) */
 typedef struct sbx_bsr_s *sbx_bsr;   /* replaces BSR_handle* (bsr.h:34-52) */
+typedef struct sbx_storage_s *sbx_storage; /* replaces Storage_handle (storage.h:2127) */
 
 /* ---- errors / runtime (platform.h:757-841, blas.h:965-988, alloc.h:398-443) ---- */
 
@@ -249,6 +250,52 @@ int sbx_gesm(int ndc, int ndx, int ndy, int t, const double *alpha, const int *p
              int ncomponentsx, const char *ox, const void *const *vx, const sbx_context *ctxx,
              const int *py, const int *dimy, int ncomponentsy, const char *oy, void *const *vy,
              const sbx_context *ctxy, sbx_comm comm, int co, int session);
+
+/* ---- tensor storage, the S3T file format (storage.h:19-54) ----
+   Values types: SBX_FLOAT, SBX_DOUBLE, SBX_CFLOAT, SBX_CDOUBLE, SBX_INT (the file's
+   values_datatype 0, 1, 2, 3, 5); checksum: 0 none, 1 global, 2 per block (checksum_type,
+   storage.h:70).  Every rank of `comm` opens the same file; rank 0 writes the headers and
+   checksums, all ranks write their own values.  comm may be NULL (one process). */
+int sbx_storage_create(int nd, const int *dim, int co, const char *filename,
+                       const char *metadata, int metadata_length, int checksum, int t,
+                       sbx_comm comm, sbx_storage *sto);                  /* storage.h:2143, 2387 */
+/* metadata is copied up to metadata_cap bytes; *metadata_length and *nd are the file's values;
+   dim receives up to dim_cap dimensions (reversed for SBX_FAST_TO_SLOW) */
+int sbx_storage_read_header(const char *filename, int co, int *t, char *metadata,
+                            int metadata_cap, int *metadata_length, int *nd, int *dim,
+                            int dim_cap);                                 /* storage.h:2161, 2405 */
+int sbx_storage_open(int nd, int t, const char *filename, int allow_writing, sbx_comm comm,
+                     sbx_storage *sto);                                   /* storage.h:2187, 2470 */
+/* append the blocks p0 (num_blocks from/size pairs on a tensor with labels o0, dims dim0),
+   restricted to [from0, from0+size0) and placed at from1 on the storage (labels o1); the simple
+   form append_blocks(p, n, dim, ...) is o0 = o1 = trivial labels, from0 = from1 = 0 */
+int sbx_storage_append_blocks(int nd0, int nd1, const int *p0, int num_blocks, const char *o0,
+                              const int *from0, const int *size0, const int *dim0,
+                              const char *o1, const int *from1, sbx_storage sto, sbx_comm comm,
+                              int co);                                    /* storage.h:2230, 2510 */
+int sbx_storage_save(int nd0, int nd1, const double *alpha, int t0, const int *p0,
+                     int ncomponents0, const char *o0, const int *from0, const int *size0,
+                     const int *dim0, const void *const *v0, const sbx_context *ctx0,
+                     const char *o1, const int *from1, sbx_storage sto, sbx_comm comm, int co,
+                     int session);                                        /* storage.h:2261, 2540 */
+/* the values always replace the destination's, for Copy and Add alike (storage.h:1149-1150) */
+int sbx_storage_load(int nd0, int nd1, const double *alpha, sbx_storage sto, const char *o0,
+                     const int *from0, const int *size0, int t1, const int *p1, int ncomponents1,
+                     const char *o1, const int *from1, const int *dim1, void *const *v1,
+                     const sbx_context *ctx1, sbx_comm comm, int co, int copyadd,
+                     int session);                                        /* storage.h:2292, 2572 */
+/* stored blocks overlapping [from1, from1+size1) of a tensor with labels o1: up to cap from/size
+   pairs (2*nd1 ints each) relative to from1; *nblocks is the total */
+int sbx_storage_get_blocks(sbx_storage sto, int nd0, int nd1, const char *o0, const char *o1,
+                           const int *from1, const int *size1, int co, int *blocks, int cap,
+                           int *nblocks);                                 /* storage.h:2330, 2609 */
+/* rank and values type of an open storage (the template checks of get_storage_context) */
+int sbx_storage_info(sbx_storage sto, int *nd, int *t);
+int sbx_storage_check(sbx_storage sto, sbx_comm comm);                    /* storage.h:2347, 2439 */
+int sbx_storage_flush(sbx_storage sto);                                   /* storage.h:2434 */
+int sbx_storage_preallocate(sbx_storage sto, unsigned long long size);    /* storage.h:2427 */
+/* writes the pending checksums and releases the handle (also on error) */
+int sbx_storage_close(sbx_storage sto, sbx_comm comm);                    /* storage.h:2361, 2451 */
 
 /* ---- kernel-level entry points (the local hot path, for direct callers and benchmarks) ---- */
 

@@ -708,6 +708,183 @@ def bsr_get_preferred_layout(bsr: BSR, ncomponents: int = 1, co: int = SlowToFas
     return list(lx[:ncomponents]), list(ly[:ncomponents])
 
 
+# ---------------------------------------------------------------------------------------------
+# tensor storage, the S3T file format (storage.h:2374-2617)
+# ---------------------------------------------------------------------------------------------
+
+NoChecksum, GlobalChecksum, BlockChecksum = 0, 1, 2
+_STORAGE_TYPES = {torch.float32: FLOAT, torch.float64: DOUBLE, torch.complex64: CFLOAT,
+                  torch.complex128: CDOUBLE, torch.int32: INT}
+_STORAGE_TORCH = {v: k for k, v in _STORAGE_TYPES.items()}
+
+
+class Storage:
+    """Handle of an S3T tensor storage (Storage_handle, storage.h:2127)."""
+
+    def __init__(self, handle, nd, dtype):
+        self._h, self.nd, self.dtype = handle, nd, dtype
+
+    @property
+    def handle(self):
+        if not self._h:
+            raise SuperbblasError("storage: the handle is closed")
+        return self._h
+
+    @property
+    def torch_dtype(self):
+        return _STORAGE_TORCH[self.dtype]
+
+    def close(self, comm: Optional[Comm] = None):
+        if self._h:
+            h, self._h = self._h, None
+            _check(_lib.sbx_storage_close(h, _comm(comm)))
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _storage_type(dtype) -> int:
+    if isinstance(dtype, int):
+        return dtype
+    if dtype not in _STORAGE_TYPES:
+        raise SuperbblasError("storage: unsupported type %s" % dtype)
+    return _STORAGE_TYPES[dtype]
+
+
+def create_storage(dim, co: int, filename: str, metadata: bytes = b"",
+                   checksum: int = NoChecksum, dtype=torch.complex128,
+                   comm: Optional[Comm] = None) -> Storage:
+    """create_storage<Nd,T> (storage.h:2386-2395): a new file (its content, if any, is lost)."""
+    h = ctypes.c_void_p()
+    t = _storage_type(dtype)
+    meta = bytes(metadata)
+    _check(_lib.sbx_storage_create(len(dim), _ints(dim), co, os.fsencode(filename), meta,
+                                   len(meta), checksum, t, _comm(comm), ctypes.byref(h)))
+    return Storage(h, len(dim), t)
+
+
+def read_storage_header(filename: str, co: int = SlowToFast):
+    """read_storage_header (storage.h:2405-2421): (values type, metadata bytes, dims)."""
+    t, ml, nd = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    _check(_lib.sbx_storage_read_header(os.fsencode(filename), co, ctypes.byref(t), None, 0,
+                                        ctypes.byref(ml), ctypes.byref(nd), None, 0))
+    meta = ctypes.create_string_buffer(max(1, ml.value))
+    dim = _ints([0] * nd.value)
+    _check(_lib.sbx_storage_read_header(os.fsencode(filename), co, ctypes.byref(t), meta,
+                                        ml.value, ctypes.byref(ml), ctypes.byref(nd), dim,
+                                        nd.value))
+    return t.value, meta.raw[:ml.value], list(dim[:nd.value])
+
+
+def open_storage(filename: str, allow_writing: bool = False, nd: Optional[int] = None,
+                 dtype=None, comm: Optional[Comm] = None) -> Storage:
+    """open_storage<Nd,T> (storage.h:2469-2476); nd/dtype default to the file's own."""
+    if nd is None or dtype is None:
+        t0, _, d0 = read_storage_header(filename)
+        nd = len(d0) if nd is None else nd
+        dtype = t0 if dtype is None else dtype
+    h = ctypes.c_void_p()
+    t = _storage_type(dtype)
+    _check(_lib.sbx_storage_open(nd, t, os.fsencode(filename), int(allow_writing), _comm(comm),
+                                 ctypes.byref(h)))
+    return Storage(h, nd, t)
+
+
+def append_blocks(sto: Storage, p0, dim0, o0: Optional[str] = None, from0=None, size0=None,
+                  o1: Optional[str] = None, from1=None, co: int = SlowToFast,
+                  comm: Optional[Comm] = None):
+    """append_blocks (storage.h:2484-2521): declare the blocks p0 (from/size pairs) stored; the
+    short form (o0/o1 omitted) takes them in the storage's own coordinates."""
+    nd0 = len(dim0)
+    if o0 is None:
+        o0 = "".join(chr(ord("a") + i) for i in range(nd0))
+    if o1 is None:
+        o1 = "".join(chr(ord("a") + i) for i in range(sto.nd))
+    from0 = [0] * nd0 if from0 is None else from0
+    size0 = list(dim0) if size0 is None else size0
+    from1 = [0] * sto.nd if from1 is None else from1
+    _check(_lib.sbx_storage_append_blocks(nd0, sto.nd, _partition(p0, nd0), len(p0), o0.encode(),
+                                          _ints(from0), _ints(size0), _ints(dim0), o1.encode(),
+                                          _ints(from1), sto.handle, _comm(comm), co))
+
+
+def save(alpha, p0, o0: str, from0, size0, dim0, v0: Sequence[torch.Tensor], o1: str, from1,
+         sto: Storage, co: int = SlowToFast, comm: Optional[Comm] = None):
+    """save<Nd0,Nd1,T,Q> (storage.h:2539-2554): write alpha * v0[from0:from0+size0] into the
+    stored blocks at from1 (labels o1); values outside the stored blocks are dropped."""
+    nprocs, rank = _nprocs_rank(comm)
+    nd0 = len(o0)
+    nc0 = len(v0)
+    if len(p0) != nprocs * nc0:
+        raise SuperbblasError("partition is incompatible with the communicator/components")
+    _check_sizes(p0, rank, nc0, v0, "save origin")
+    t0 = _dtype_of(v0)
+    _bind_stream(v0)
+    _check(_lib.sbx_storage_save(nd0, sto.nd, _scalar(alpha), t0, _partition(p0, nd0), nc0,
+                                 o0.encode(), _ints(from0), _ints(size0), _ints(dim0), _ptrs(v0),
+                                 _ctxs(v0), o1.encode(), _ints(from1), sto.handle, _comm(comm),
+                                 co, 0))
+
+
+def load(alpha, sto: Storage, o0: str, from0, size0, p1, o1: str, from1, dim1,
+         v1: Sequence[torch.Tensor], co: int = SlowToFast, copyadd: int = Copy,
+         comm: Optional[Comm] = None):
+    """load<Nd0,Nd1,T,Q> (storage.h:2571-2595): v1[from1 + P(c - from0)] = alpha * sto[c] for
+    the stored c in [from0, from0+size0); the rest of v1 is untouched (Add copies as well, as
+    the reference's local_load does)."""
+    nprocs, rank = _nprocs_rank(comm)
+    nd1 = len(o1)
+    nc1 = len(v1)
+    if len(p1) != nprocs * nc1:
+        raise SuperbblasError("partition is incompatible with the communicator/components")
+    _check_sizes(p1, rank, nc1, v1, "load destination")
+    t1 = _dtype_of(v1)
+    _bind_stream(v1)
+    _check(_lib.sbx_storage_load(sto.nd, nd1, _scalar(alpha), sto.handle, o0.encode(),
+                                 _ints(from0), _ints(size0), t1, _partition(p1, nd1), nc1,
+                                 o1.encode(), _ints(from1), _ints(dim1), _ptrs(v1), _ctxs(v1),
+                                 _comm(comm), co, copyadd, 0))
+
+
+def get_blocks(sto: Storage, o0: str, o1: str, from1, size1, co: int = SlowToFast):
+    """get_blocks<Nd0,Nd1,T> (storage.h:2608-2617): the stored boxes overlapping
+    [from1, from1+size1) of a tensor with labels o1, as (from, size) relative to from1."""
+    nd1 = len(o1)
+    n = ctypes.c_int()
+    _check(_lib.sbx_storage_get_blocks(sto.handle, sto.nd, nd1, o0.encode(), o1.encode(),
+                                       _ints(from1), _ints(size1), co, None, 0, ctypes.byref(n)))
+    out = _ints([0] * (2 * nd1 * n.value))
+    _check(_lib.sbx_storage_get_blocks(sto.handle, sto.nd, nd1, o0.encode(), o1.encode(),
+                                       _ints(from1), _ints(size1), co, out, n.value,
+                                       ctypes.byref(n)))
+    flat = list(out[:2 * nd1 * n.value])
+    return [(flat[i * 2 * nd1:i * 2 * nd1 + nd1], flat[i * 2 * nd1 + nd1:(i + 1) * 2 * nd1])
+            for i in range(n.value)]
+
+
+def check_storage(sto: Storage, comm: Optional[Comm] = None):
+    """check_storage (storage.h:2439-2446): verify the checksums; raises on a mismatch."""
+    _check(_lib.sbx_storage_check(sto.handle, _comm(comm)))
+
+
+def flush_storage(sto: Storage):
+    """flush_storage (storage.h:2434)."""
+    _check(_lib.sbx_storage_flush(sto.handle))
+
+
+def preallocate_storage(sto: Storage, size: int):
+    """preallocate_storage (storage.h:2427-2429): extend the file to `size` bytes."""
+    _check(_lib.sbx_storage_preallocate(sto.handle, ctypes.c_ulonglong(size)))
+
+
+def close_storage(sto: Storage, comm: Optional[Comm] = None):
+    """close_storage (storage.h:2451-2460): write the pending checksums and release."""
+    sto.close(comm)
+
+
 __all__ = [
     "SlowToFast", "FastToSlow", "Copy", "Add", "RowMajor", "ColumnMajor", "SuperbblasError",
     "Comm", "copy", "copy_plan", "contraction", "local_copy", "xgemm_batch_strided", "create_bsr",
@@ -715,5 +892,8 @@ __all__ = [
     "bsr_krylov", "bsr_get_preferred_layout", "basic_partitioning", "basic_partitioning_ext",
     "partitioning_distributed_procs", "make_hole", "sync", "stream", "set_stream",
     "clear_caches", "timings_enable", "timings_reset", "timings_get", "timings_report",
-    "get_gpu_devices_count", "version", "LIB_PATH",
+    "get_gpu_devices_count", "version", "LIB_PATH", "Storage", "NoChecksum", "GlobalChecksum",
+    "BlockChecksum", "create_storage", "read_storage_header", "open_storage", "append_blocks",
+    "save", "load", "get_blocks", "check_storage", "flush_storage", "preallocate_storage",
+    "close_storage",
 ]

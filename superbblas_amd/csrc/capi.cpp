@@ -39,6 +39,12 @@ struct sbx_bsr_s {
     bool is_kron = false;
 };
 
+struct sbx_storage_s {
+    sbx::StorageCtx *s = nullptr;
+    int dtype = SBX_CDOUBLE;
+    int nd = 0;
+};
+
 using namespace sbx;
 
 namespace {
@@ -212,6 +218,11 @@ Scalar to_scalar(const double *a) { return a ? Scalar{a[0], a[1]} : Scalar{1, 0}
 
 void check_session(int session) {
     if (session != 0) throw Error("only session 0 is supported");
+}
+
+sbx_storage_s &storage_of(sbx_storage sto) {
+    if (!sto || !sto->s) throw Error("storage: invalid handle");
+    return *sto;
 }
 
 } // namespace
@@ -821,4 +832,171 @@ int sbx_xgemm_batch_strided(int t, char transa, char transb, int m, int n, int k
     });
 }
 
+//
+// Tensor storage (storage.cpp)
+//
+
+
+int sbx_storage_create(int nd, const int *dim, int co, const char *filename,
+                       const char *metadata, int metadata_length, int checksum, int t,
+                       sbx_comm comm, sbx_storage *sto) {
+    return guard([&] {
+        if (!filename || !sto) throw Error("storage: null argument");
+        std::unique_ptr<sbx_storage_s> h(new sbx_storage_s());
+        h->dtype = t;
+        h->nd = nd;
+        h->s = storage_create(t, to_coor(dim, nd, co == SBX_FAST_TO_SLOW), filename, metadata,
+                              metadata_length, checksum, get_comm(comm));
+        *sto = h.release();
+    });
+}
+
+int sbx_storage_read_header(const char *filename, int co, int *t, char *metadata,
+                            int metadata_cap, int *metadata_length, int *nd, int *dim,
+                            int dim_cap) {
+    return guard([&] {
+        if (!filename) throw Error("storage: null file name");
+        int dt;
+        std::string meta;
+        Coor d;
+        storage_read_header(filename, dt, meta, d);
+        if (co == SBX_FAST_TO_SLOW) std::reverse(d.begin(), d.end());
+        if (t) *t = dt;
+        if (metadata && metadata_cap > 0)
+            std::memcpy(metadata, meta.data(), std::min<std::size_t>(metadata_cap, meta.size()));
+        if (metadata_length) *metadata_length = (int)meta.size();
+        if (nd) *nd = (int)d.size();
+        if (dim)
+            for (int i = 0; i < std::min(dim_cap, (int)d.size()); ++i) dim[i] = d[i];
+    });
+}
+
+int sbx_storage_open(int nd, int t, const char *filename, int allow_writing, sbx_comm comm,
+                     sbx_storage *sto) {
+    return guard([&] {
+        if (!filename || !sto) throw Error("storage: null argument");
+        std::unique_ptr<sbx_storage_s> h(new sbx_storage_s());
+        h->dtype = t;
+        h->nd = nd;
+        h->s = storage_open(nd, t, filename, allow_writing != 0, get_comm(comm));
+        *sto = h.release();
+    });
+}
+
+int sbx_storage_append_blocks(int nd0, int nd1, const int *p0, int num_blocks, const char *o0,
+                              const int *from0, const int *size0, const int *dim0,
+                              const char *o1, const int *from1, sbx_storage sto, sbx_comm comm,
+                              int co) {
+    return guard([&] {
+        sbx_storage_s &h = storage_of(sto);
+        if (nd1 != h.nd) throw Error("storage: invalid number of dimensions");
+        if (num_blocks < 0 || (num_blocks > 0 && !p0)) throw Error("storage: invalid blocks");
+        const bool rev = co == SBX_FAST_TO_SLOW;
+        std::vector<Range> blocks;
+        for (int i = 0; i < num_blocks; ++i)
+            blocks.push_back(Range{to_coor(p0 + (std::size_t)i * 2 * nd0, nd0, rev),
+                                   to_coor(p0 + (std::size_t)i * 2 * nd0 + nd0, nd0, rev)});
+        storage_append_blocks(*h.s, blocks, to_labels(o0, nd0, rev, "o0"),
+                              to_coor(from0, nd0, rev), to_coor(size0, nd0, rev),
+                              to_coor(dim0, nd0, rev), to_labels(o1, nd1, rev, "o1"),
+                              to_coor(from1, nd1, rev), get_comm(comm));
+    });
+}
+
+int sbx_storage_save(int nd0, int nd1, const double *alpha, int t0, const int *p0,
+                     int ncomponents0, const char *o0, const int *from0, const int *size0,
+                     const int *dim0, const void *const *v0, const sbx_context *ctx0,
+                     const char *o1, const int *from1, sbx_storage sto, sbx_comm comm, int co,
+                     int session) {
+    return guard([&] {
+        check_session(session);
+        sbx_storage_s &h = storage_of(sto);
+        if (nd1 != h.nd) throw Error("storage: invalid number of dimensions");
+        check_copy_types(t0, h.dtype);
+        const Comm c = get_comm(comm);
+        const bool rev = co == SBX_FAST_TO_SLOW;
+        Mirror m;
+        m.device = pick_device({{ctx0, ncomponents0}}, c);
+        DistTensor a = make_tensor(nd0, o0, dim0, p0, ncomponents0, v0, ctx0, t0, c, rev, m, false,
+                                   "o0");
+        storage_save(*h.s, to_scalar(alpha), a, to_coor(from0, nd0, rev), to_coor(size0, nd0, rev),
+                     to_labels(o1, nd1, rev, "o1"), to_coor(from1, nd1, rev), c);
+        finish_mirror(m);
+    });
+}
+
+int sbx_storage_load(int nd0, int nd1, const double *alpha, sbx_storage sto, const char *o0,
+                     const int *from0, const int *size0, int t1, const int *p1, int ncomponents1,
+                     const char *o1, const int *from1, const int *dim1, void *const *v1,
+                     const sbx_context *ctx1, sbx_comm comm, int co, int copyadd, int session) {
+    return guard([&] {
+        check_session(session);
+        (void)copyadd;
+        sbx_storage_s &h = storage_of(sto);
+        if (nd0 != h.nd) throw Error("storage: invalid number of dimensions");
+        check_copy_types(h.dtype, t1);
+        const Comm c = get_comm(comm);
+        const bool rev = co == SBX_FAST_TO_SLOW;
+        Mirror m;
+        m.device = pick_device({{ctx1, ncomponents1}}, c);
+        DistTensor b = make_tensor(nd1, o1, dim1, p1, ncomponents1, (const void *const *)v1, ctx1,
+                                   t1, c, rev, m, true, "o1");
+        storage_load(*h.s, to_scalar(alpha), to_labels(o0, nd0, rev, "o0"),
+                     to_coor(from0, nd0, rev), to_coor(size0, nd0, rev), b,
+                     to_coor(from1, nd1, rev), c);
+        finish_mirror(m);
+    });
+}
+
+int sbx_storage_get_blocks(sbx_storage sto, int nd0, int nd1, const char *o0, const char *o1,
+                           const int *from1, const int *size1, int co, int *blocks, int cap,
+                           int *nblocks) {
+    return guard([&] {
+        sbx_storage_s &h = storage_of(sto);
+        if (nd0 != h.nd) throw Error("storage: invalid number of dimensions");
+        // only the storage labels follow `co` (storage.h:1404)
+        const std::vector<Range> r =
+            storage_get_blocks(*h.s, to_labels(o0, nd0, co == SBX_FAST_TO_SLOW, "o0"),
+                               to_labels(o1, nd1, false, "o1"), to_coor(from1, nd1, false),
+                               to_coor(size1, nd1, false));
+        if (nblocks) *nblocks = (int)r.size();
+        for (int i = 0; blocks && i < std::min(cap, (int)r.size()); ++i)
+            for (int k = 0; k < nd1; ++k) {
+                blocks[(std::size_t)i * 2 * nd1 + k] = r[i].from[k];
+                blocks[(std::size_t)i * 2 * nd1 + nd1 + k] = r[i].size[k];
+            }
+    });
+}
+
+int sbx_storage_info(sbx_storage sto, int *nd, int *t) {
+    return guard([&] {
+        const sbx_storage_s &h = storage_of(sto);
+        if (nd) *nd = h.nd;
+        if (t) *t = h.dtype;
+    });
+}
+
+int sbx_storage_check(sbx_storage sto, sbx_comm comm) {
+    return guard([&] { storage_checksums(*storage_of(sto).s, get_comm(comm), false); });
+}
+
+int sbx_storage_flush(sbx_storage sto) {
+    return guard([&] { storage_flush(*storage_of(sto).s); });
+}
+
+int sbx_storage_preallocate(sbx_storage sto, unsigned long long size) {
+    return guard([&] { storage_preallocate(*storage_of(sto).s, (std::size_t)size); });
+}
+
+int sbx_storage_close(sbx_storage sto, sbx_comm comm) {
+    return guard([&] {
+        std::unique_ptr<sbx_storage_s> h(sto);
+        if (!h) throw Error("storage: invalid handle");
+        StorageCtx *s = h->s;
+        h->s = nullptr;
+        storage_close(s, get_comm(comm));
+    });
+}
+
 } // extern "C"
+

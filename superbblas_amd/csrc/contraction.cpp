@@ -41,24 +41,6 @@ GroupStride group_stride(const std::string &group, const std::string &labels, co
     return g;
 }
 
-Range translate(const Range &r, const std::string &la, const Coor &fromA, const Coor &dimA,
-                const std::string &lb, const Coor &fromB, const Coor &dimB) {
-    Range o{Coor(lb.size()), Coor(lb.size())};
-    for (std::size_t j = 0; j < lb.size(); ++j) {
-        auto i = la.find(lb[j]);
-        if (i == std::string::npos) {
-            o.from[j] = fromB[j];
-            o.size[j] = 1;
-        } else {
-            o.from[j] = normalize_coor(
-                (long)normalize_coor((long)r.from[i] - fromA[i] + dimA[i], dimA[i]) + fromB[j],
-                dimB[j]);
-            o.size[j] = r.size[i];
-        }
-    }
-    return o;
-}
-
 /// Reorder the entries of `c` (labels `from`) into labels `to`
 Coor reorder(const Coor &c, const std::string &from, const std::string &to) {
     Coor r(to.size());

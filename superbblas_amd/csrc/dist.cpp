@@ -35,27 +35,6 @@ namespace {
 // Helpers
 //
 
-/// Map coordinates of the copy region from tensor A (labels la) to tensor B (labels lb):
-/// cB = fromB + (cA - fromA) for common labels, fromB for labels only in B
-Range translate(const Range &r, const std::string &la, const Coor &fromA, const Coor &dimA,
-                const std::string &lb, const Coor &fromB, const Coor &dimB) {
-    Range o{Coor(lb.size()), Coor(lb.size())};
-    for (std::size_t j = 0; j < lb.size(); ++j) {
-        auto i = la.find(lb[j]);
-        if (i == std::string::npos) {
-            o.from[j] = fromB[j];
-            o.size[j] = 1;
-        } else {
-            o.from[j] = normalize_coor(
-                (long)normalize_coor((long)r.from[i] - fromA[i] + dimA[i], dimA[i]) + fromB[j],
-                dimB[j]);
-            o.size[j] = r.size[i];
-        }
-    }
-    if (volume(o.size) == 0) o.size.assign(lb.size(), 0);
-    return o;
-}
-
 /// One box to copy between two local arrays
 struct Piece {
     int a, b;      // global component index of the origin / destination
@@ -508,6 +487,31 @@ void dist_copy(const Scalar &alpha, const DistTensor &src, const Coor &from0, co
                              device, nullptr, dst.mask_of(cb.idx));
             cur[ca.rank] += volume(p.size) * es;
         }
+    }
+}
+
+void comm_barrier(const Comm &comm) {
+    if (comm.nprocs <= 1) return;
+    if (comm.nccl) {
+        // a one-element all-reduce on the communicator's device, waited for on the host
+        set_device(comm.device);
+        hipStream_t s = get_stream(comm.device);
+        Scratch one(sizeof(int), comm.device);
+        SBX_HIP_CHECK(hipMemsetAsync(one.ptr, 0, sizeof(int), s));
+        nccl_check(ncclAllReduce(one.ptr, one.ptr, 1, ncclInt, ncclSum, (ncclComm_t)comm.nccl, s),
+                   "ncclAllReduce");
+        SBX_HIP_CHECK(hipStreamSynchronize(s));
+    } else if (comm.host_fn) {
+        // one byte to and from every peer through the caller's all-to-all
+        std::vector<unsigned long long> n(comm.nprocs, 1), d(comm.nprocs);
+        for (int q = 0; q < comm.nprocs; ++q) d[q] = q;
+        n[comm.rank] = 0;
+        std::vector<char> sbuf(comm.nprocs, 0), rbuf(comm.nprocs, 0);
+        const int rc = comm.host_fn(sbuf.data(), n.data(), d.data(), rbuf.data(), n.data(),
+                                    d.data(), comm.host_user);
+        if (rc != 0) throw Error("the host all-to-all callback failed (" + std::to_string(rc) + ")");
+    } else {
+        throw Error("the communicator has no transport");
     }
 }
 

@@ -267,4 +267,26 @@ std::vector<Range> basic_partitioning_ext(const Coor &dim, const Coor &procs, in
     return fs;
 }
 
+/// Map coordinates of the copy region from tensor A (labels la) to tensor B (labels lb):
+/// cB = fromB + (cA - fromA) for common labels, fromB for labels only in B
+Range translate(const Range &r, const std::string &la, const Coor &fromA, const Coor &dimA,
+                const std::string &lb, const Coor &fromB, const Coor &dimB) {
+    Range o{Coor(lb.size()), Coor(lb.size())};
+    for (std::size_t j = 0; j < lb.size(); ++j) {
+        auto i = la.find(lb[j]);
+        if (i == std::string::npos) {
+            o.from[j] = fromB[j];
+            o.size[j] = 1;
+        } else {
+            o.from[j] = normalize_coor(
+                (long)normalize_coor((long)r.from[i] - fromA[i] + dimA[i], dimA[i]) + fromB[j],
+                dimB[j]);
+            o.size[j] = r.size[i];
+        }
+    }
+    if (volume(o.size) == 0) o.size.assign(lb.size(), 0);
+    return o;
+}
+
+
 } // namespace sbx

@@ -56,6 +56,11 @@ std::vector<Range> intersection(const Range &a, const Range &b, const Coor &dim)
 /// Intersect a list of ranges with a range
 std::vector<Range> intersection(const std::vector<Range> &as, const Range &b, const Coor &dim);
 
+/// Map a range of tensor A (labels la) to tensor B (labels lb) (translate_range, dist.h:612-634):
+/// cB = fromB + (cA - fromA) for common labels, fromB for labels only in B
+Range translate(const Range &r, const std::string &la, const Coor &fromA, const Coor &dimA,
+                const std::string &lb, const Coor &fromB, const Coor &dimB);
+
 /// Subranges of `r` after removing `hole` (dist.h:3744-3825)
 std::vector<Range> make_hole(const Range &r, const Range &hole, const Coor &dim);
 
@@ -126,6 +131,9 @@ struct Local {
 // Distributed operations (dist.cpp)
 //
 
+/// Every rank of `comm` reaches this point before any leaves it (MPI_Barrier)
+void comm_barrier(const Comm &comm);
+
 /// copy: dst[from1 + P(c - from0)] (=|+=) alpha * src[c] for c in [from0, from0+size0)
 void dist_copy(const Scalar &alpha, const DistTensor &src, const Coor &from0, const Coor &size0,
                const DistTensor &dst, const Coor &from1, bool add, const Comm &comm);
@@ -166,5 +174,31 @@ void dense_inversion(const DistTensor &v, const std::string &orows, const std::s
 void dense_solve(bool gesm, const Scalar &alpha, const DistTensor &c, const std::string &orows,
                  const std::string &ocols, const DistTensor &x, const DistTensor &y,
                  const Comm &comm);
+
+//
+// Tensor storage, the S3T format (storage.cpp, reference storage.h); storage dims SlowToFast
+//
+struct StorageCtx;
+StorageCtx *storage_create(int dtype, const Coor &dim, const char *filename, const char *meta,
+                           int meta_len, int checksum, const Comm &comm);
+void storage_read_header(const char *filename, int &dtype, std::string &meta, Coor &dim);
+StorageCtx *storage_open(int nd, int dtype, const char *filename, bool allow_writing,
+                         const Comm &comm);
+void storage_append_blocks(StorageCtx &s, const std::vector<Range> &p0, const std::string &o0,
+                           const Coor &from0, const Coor &size0, const Coor &dim0,
+                           const std::string &o1, const Coor &from1, const Comm &comm);
+void storage_save(StorageCtx &s, const Scalar &alpha, const DistTensor &v, const Coor &from0,
+                  const Coor &size0, const std::string &o1, const Coor &from1, const Comm &comm);
+void storage_load(StorageCtx &s, const Scalar &alpha, const std::string &o0, const Coor &from0,
+                  const Coor &size0, const DistTensor &v, const Coor &from1, const Comm &comm);
+std::vector<Range> storage_get_blocks(const StorageCtx &s, const std::string &o0,
+                                      const std::string &o1, const Coor &from1,
+                                      const Coor &size1);
+/// do_write: write the pending checksums; otherwise verify them (check_or_write_checksums)
+void storage_checksums(StorageCtx &s, const Comm &comm, bool do_write);
+void storage_flush(StorageCtx &s);
+void storage_preallocate(StorageCtx &s, std::size_t size);
+/// write the pending checksums and free the context
+void storage_close(StorageCtx *s, const Comm &comm);
 
 } // namespace sbx

@@ -364,6 +364,65 @@ int main() {
         CHECK(os.str().find("still in use") == std::string::npos, "no scratch leaked");
     }
 
+    // ---- storage: save a tensor to an S3T file and load it back (storage.h:2374-2617) ----
+    {
+        const char *fn = "/tmp/sbx_dropin_storage.s3t";
+        const Coor<3> d{4, 3, 5};
+        Storage_handle sto = nullptr;
+        const char meta[] = "dropin";
+        create_storage<3, Z>(d, SlowToFast, fn, meta, 6, BlockChecksum, &sto);
+        PartitionItem<3> whole{Coor<3>{}, d};
+        PartitionItem<3> halves[2] = {PartitionItem<3>{Coor<3>{0, 0, 0}, Coor<3>{2, 3, 5}},
+                                      PartitionItem<3>{Coor<3>{2, 0, 0}, Coor<3>{2, 3, 5}}};
+        append_blocks<3, Z>(halves, 2, d, sto, SlowToFast);
+        std::vector<std::complex<float>> h(60);
+        for (int i = 0; i < 60; ++i) h[i] = std::complex<float>((float)i, (float)-i);
+        const std::complex<float> *src = h.data();
+        Context cpu = createCpuContext();
+        save<3, 3, std::complex<float>, Z>(std::complex<float>(2), &whole, 1, "abc", Coor<3>{}, d,
+                                           d, &src, &cpu, "abc", Coor<3>{}, sto, SlowToFast);
+        std::vector<PartitionItem<3>> blocks;
+        get_blocks<3, 3, Z>(sto, "abc", "abc", Coor<3>{}, d, blocks, SlowToFast);
+        CHECK(blocks.size() == 2, "storage get_blocks");
+        close_storage<3, Z>(sto);
+        values_datatype vt;
+        std::vector<char> md;
+        std::vector<IndexType> dims;
+        read_storage_header(fn, SlowToFast, vt, md, dims);
+        CHECK(vt == CDOUBLE && md.size() == 6 && dims.size() == 3 && dims[2] == 5,
+              "read_storage_header");
+        open_storage<3, Z>(fn, false, &sto);
+        check_storage<3, Z>(sto);
+        const Coor<3> dt{5, 3, 4};
+        PartitionItem<3> pt{Coor<3>{}, dt};
+        auto dbuf = allocate_from_cache<Z>(60, gpu);
+        Z *dst = (Z *)dbuf.get();
+        load<3, 3, Z, Z>(1.0, sto, "abc", Coor<3>{}, d, &pt, 1, "cba", Coor<3>{}, dt, &dst, &gpu,
+                         SlowToFast, Copy);
+        std::vector<Z> back(60);
+        Z *bp = back.data();
+        const Z *dsrc = dst;
+        copy<3, 3, Z, Z>(1.0, &pt, 1, "cba", Coor<3>{}, dt, dt, &dsrc, nullptr, &gpu, &pt, 1,
+                         "cba", Coor<3>{}, dt, &bp, nullptr, &cpu, SlowToFast, Copy);
+        bool ok = true;
+        for (int a = 0; a < 4; ++a)
+            for (int b = 0; b < 3; ++b)
+                for (int c = 0; c < 5; ++c) {
+                    const int g = (a * 3 + b) * 5 + c;
+                    ok = ok && back[(c * 3 + b) * 4 + a] == Z(2.0 * g, -2.0 * g);
+                }
+        CHECK(ok, "storage save/load round trip");
+        bool thrown = false;
+        try {
+            check_storage<3, double>(sto);
+        } catch (const std::runtime_error &) {
+            thrown = true;
+        }
+        CHECK(thrown, "storage template type mismatch must throw");
+        close_storage<3, Z>(sto);
+        std::remove(fn);
+    }
+
     // ---- error behaviour: invalid calls throw std::runtime_error (platform.h:226-243) ----
     {
         bool thrown = false;

@@ -35,4 +35,21 @@ void use_mpi_overloads(MPI_Comm comm) {
     bsr_krylov<2, 2, 3, 3, Z>(Z(1), op, "ab", "AB", &px, 1, "ABn", Coor<3>{}, Coor<3>{4, 4, 2},
                               Coor<3>{4, 4, 2}, &c0, Z(0), &px, "abn", Coor<3>{}, Coor<3>{4, 4, 2},
                               Coor<3>{4, 4, 2}, 0, &v1, &gpu, comm, SlowToFast);
+    Storage_handle sto = nullptr;
+    create_storage<2, Z>(d, SlowToFast, "f", "", 0, NoChecksum, comm, &sto);
+    open_storage<2, Z>("f", true, comm, &sto);
+    append_blocks<2, Z>(&p, 1, d, sto, comm, SlowToFast);
+    append_blocks<2, 2, Z>(&p, 1, "ab", Coor<2>{}, d, d, "ba", Coor<2>{}, sto, comm, SlowToFast);
+    save<2, 2, Z, Z>(Z(1), &p, 1, "ab", Coor<2>{}, d, d, &c0, &gpu, "ab", Coor<2>{}, sto, comm,
+                     SlowToFast);
+    load<2, 2, Z, Z>(Z(1), sto, "ab", Coor<2>{}, d, &p, 1, "ab", Coor<2>{}, d, &v1, &gpu, comm,
+                     SlowToFast, Copy);
+    std::vector<PartitionItem<2>> blocks;
+    get_blocks<2, 2, Z>(sto, "ab", "ab", Coor<2>{}, d, blocks, comm, SlowToFast);
+    values_datatype vt;
+    std::vector<char> md;
+    std::vector<IndexType> dims;
+    read_storage_header("f", SlowToFast, vt, md, dims, comm);
+    check_storage<2, Z>(sto, comm);
+    close_storage<2, Z>(sto, comm);
 }

@@ -13,6 +13,10 @@ Cases (all multi-rank: the exchange, pack/unpack kernels and reductions run for 
             y split over t, one power and two  [bsr.h:2107-2266]
   kron   -- the same stencil as a Kronecker operator (color blocks x spin matrices), two powers
             [bsr.h:2476-2490, 587-648]
+  dense  -- cholesky / gesm with the matrices split over ranks  [dense.h:1007-1157]
+  storage -- every rank saves its part of a tensor into one shared S3T file (global and block
+            checksums), the file is checked by the S3T restatement, then loaded back into
+            another distribution  [storage.h:1198-1385, 2142-2370]
 """
 import os
 import sys
@@ -346,6 +350,55 @@ def case_dense(sb, comm, rank, n, dev):
     assert np.allclose(out, ref, rtol=0, atol=1e-12 * np.abs(ref).max()), "dense gesm"
 
 
+def case_storage(sb, comm, rank, n, dev):
+    from oracle import s3t
+    dim = [6, 5, 5]  # storage "abc"
+    dim0 = [5, 6, 5]  # tensor "cab", split over a
+    p0 = sb.basic_partitioning("cab", dim0, [1, n, 1], "a", n, 1)
+    g0 = gen("index", vol(dim0), 1, np.complex128)
+    blocks = [([0, 0, 0], [3, 5, 5]), ([3, 1, 0], [3, 2, 5]), ([3, 4, 0], [3, 2, 5])]  # wraps b
+    stored = np.zeros(dim, bool)
+    stored[0:3] = True
+    stored[3:6, [1, 2, 4, 0]] = True  # b = 3 is never stored for a >= 3
+    S = (2.0 - 1.0j) * g0.reshape(dim0).transpose(1, 2, 0)  # S[a, b, c] = alpha * v0[c, a, b]
+    fn = os.path.join("/tmp", "sbx_dist_storage_%s.s3t" % os.environ.get("MASTER_PORT", "0"))
+    for checksum in (sb.GlobalChecksum, sb.BlockChecksum):
+        sto = sb.create_storage(dim, sb.SlowToFast, fn, b"dist", checksum, torch.complex128,
+                                comm=comm)
+        sb.append_blocks(sto, blocks, dim, comm=comm)
+        v0 = scatter(sb, g0, dim0, p0, rank, 1, dev)
+        sb.save(2.0 - 1.0j, p0, "cab", [0, 0, 0], dim0, dim0, v0, "abc", [0, 0, 0], sto,
+                comm=comm)
+        sto.close(comm)
+        if rank == 0:
+            with open(fn, "rb") as f:
+                st = s3t.parse(f.read())  # verifies every checksum
+            got = [(b["from"], b["size"]) for ch in st["chunks"] for b in ch]
+            assert got == [(list(f), list(sz)) for f, sz in blocks], ("storage blocks", got)
+            for ch in st["chunks"]:
+                for b in ch:
+                    assert np.array_equal(b["values"], piece(S.ravel(), dim, b["from"],
+                                                             b["size"])), "storage values"
+        dist.barrier()
+        # load back into "bca" split over c, with the unstored elements untouched
+        diml = [5, 5, 6]
+        pl = sb.basic_partitioning("bca", diml, [1, n, 1], "c", n, 1)
+        gl = gen("int", vol(diml), 2, np.complex128)
+        vl = scatter(sb, gl, diml, pl, rank, 1, dev)
+        sto = sb.open_storage(fn, False, comm=comm)
+        sb.check_storage(sto, comm)
+        sb.load(1.0, sto, "abc", [0, 0, 0], dim, pl, "bca", [0, 0, 0], diml, vl, comm=comm)
+        torch.cuda.synchronize()
+        sto.close(comm)
+        out = gather(np.zeros_like(gl), diml, pl, 1, vl)
+        ref = np.where(stored.transpose(1, 2, 0), S.transpose(1, 2, 0),
+                       gl.reshape(diml)).ravel()
+        assert np.array_equal(out, ref), "storage load"
+        dist.barrier()
+    if rank == 0:
+        os.remove(fn)
+
+
 def main():
     dist.init_process_group("gloo")
     rank, n = dist.get_rank(), dist.get_world_size()
@@ -359,7 +412,7 @@ def main():
         comm = sb.Comm.from_torch_distributed(dev_idx)
     else:
         comm = sb.Comm.host_staged(dev_idx)
-    cases = os.environ.get("SBX_TEST_CASES", "copy,contr,bsr,kron,dense").split(",")
+    cases = os.environ.get("SBX_TEST_CASES", "copy,contr,bsr,kron,dense,storage").split(",")
     if "copy" in cases:
         case_copy(sb, comm, rank, n, dev)
     if "contr" in cases:
@@ -370,6 +423,8 @@ def main():
         case_kron(sb, comm, rank, n, dev)
     if "dense" in cases:
         case_dense(sb, comm, rank, n, dev)
+    if "storage" in cases:
+        case_storage(sb, comm, rank, n, dev)
     dist.barrier()
     comm.close()
     dist.destroy_process_group()

@@ -18,7 +18,9 @@ def test_header_declares_api():
     syms = declared_symbols()
     for s in ("sbx_copy", "sbx_contraction", "sbx_create_bsr", "sbx_create_kron_bsr", "sbx_bsr_krylov",
               "sbx_copy_masked", "sbx_cholesky", "sbx_trsm", "sbx_gesm", "sbx_inversion",
-              "sbx_destroy_bsr", "sbx_comm_create", "sbx_xgemm_batch_strided"):
+              "sbx_destroy_bsr", "sbx_comm_create", "sbx_xgemm_batch_strided", "sbx_storage_create",
+              "sbx_storage_open", "sbx_storage_append_blocks", "sbx_storage_save",
+              "sbx_storage_load", "sbx_storage_get_blocks", "sbx_storage_close"):
         assert s in syms
 
 
