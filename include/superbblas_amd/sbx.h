@@ -104,6 +104,11 @@ int sbx_timings_get(const char *name, double *ms, long long *calls);
 /* "name calls total_ms" per line into buf (truncated to len-1 chars) */
 int sbx_timings_report(char *buf, int len);
 
+/* ---- tuning hook (no reference counterpart) ----
+   Override a kernel-shape choice of the library for tuning runs; value 0 restores the default.
+   Keys: "copy.budget", "copy.run", "copy.kernel", "bsr.variant". */
+int sbx_tune_set(const char *key, long long value);
+
 /* ---- communicator (replaces MPI; dist.h:1426-1773 send_receive) ---- */
 
 /* Fill `id` (128 bytes) with a fresh RCCL unique id; call on one rank and broadcast it */

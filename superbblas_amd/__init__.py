@@ -260,6 +260,11 @@ def timings_reset():
     _check(_lib.sbx_timings_reset())
 
 
+def tune_set(key: str, value: int):
+    """Override a kernel-shape choice for tuning runs (sbx_tune_set; 0 restores the default)."""
+    _check(_lib.sbx_tune_set(key.encode(), ctypes.c_longlong(value)))
+
+
 def timings_get(name: str) -> Tuple[float, int]:
     """(total milliseconds, launches) of a kernel family: gemm, gemm_splitk_reduce, copy, bsr."""
     ms, calls = ctypes.c_double(), ctypes.c_longlong()

@@ -331,6 +331,18 @@ int sbx_cache_usage(int device, unsigned long long *cached, unsigned long long *
     });
 }
 
+int sbx_tune_set(const char *key, long long value) {
+    return guard([&] {
+        if (!key) throw Error("tune_set: null key");
+        const std::string k(key);
+        if (k == "copy.budget") g_copy_tune.budget = (long)value;
+        else if (k == "copy.run") g_copy_tune.run = (long)value;
+        else if (k == "copy.kernel") g_copy_tune.kernel = (int)value;
+        else if (k == "bsr.variant") g_bsr_tune.variant = (int)value;
+        else throw Error("tune_set: unknown key " + k);
+    });
+}
+
 int sbx_timings_enable(int on) {
     return guard([&] { timings_enable(on != 0); });
 }

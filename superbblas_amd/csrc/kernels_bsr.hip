@@ -22,6 +22,7 @@
 #include <type_traits>
 
 namespace sbx {
+BsrTune g_bsr_tune;
 namespace {
 
 struct BsrArgs {
@@ -310,8 +311,206 @@ __global__ void __launch_bounds__(256) bsr_mfma_kernel(const BsrArgs p, long nti
     }
 }
 
+// One block row per wave, the fragments of nonzero block t+1 loaded while block t is applied
+// (twice the bytes in flight per wave; 985 -> 880 us on the chain's complex<float> operator).
+// Mapping consecutive block rows to one XCD was measured no faster.
+template <typename R, bool CPLX, int BI, int BD, bool YROW, bool XROW>
+__global__ void __launch_bounds__(256) bsr_mfma_pf_kernel(const BsrArgs p, long ntiles_n) {
+    typedef typename BsrMfmaElem<R, CPLX>::type E;
+    typedef typename BsrMfma<R>::acc_t acc_t;
+    static_assert(BI <= 16 && BD % 4 == 0, "block shape");
+    constexpr int KS = BD / 4;
+    const E *__restrict__ v = (const E *)p.v;
+    const E *__restrict__ x = (const E *)p.x;
+    E *__restrict__ y = (E *)p.y;
+    const int lane = threadIdx.x & 63;
+    const long wave = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (wave >= p.block_rows * ntiles_n) return; // whole waves only: MFMA needs all 64 lanes
+    const long i = wave / ntiles_n;
+    const long col0 = (wave % ntiles_n) * 16;
+    const int ar = lane & 15, kq = lane >> 4;
+    const bool arow_ok = ar < BI;
+    const int arc = arow_ok ? ar : 0;
+    const long bcol = col0 + (lane & 15);
+    const bool bcol_ok = bcol < p.ncols;
+    const long bcc = bcol_ok ? bcol : 0;
+    acc_t accR = acc_t{0, 0, 0, 0}, accI = acc_t{0, 0, 0, 0};
+    const int jb = p.ii[i], je = p.ii[i + 1];
+    E an[KS], bn[KS];
+    auto fetch = [&](int j) {
+        const int dj = p.jj[j];
+        const bool ok = dj >= 0;
+        const long d0 = ok ? dj : 0;
+        const E *vb = v + (long)j * BI * BD;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const int e = ks * 4 + kq;
+            const E a = p.block_im_fast ? vb[arc + e * BI] : vb[arc * BD + e];
+            const E b = XROW ? x[(d0 + e) * p.ldx + bcc] : x[(d0 + e) + bcc * p.ldx];
+            an[ks] = (arow_ok && ok) ? a : E{};
+            bn[ks] = bcol_ok ? b : E{};
+        }
+    };
+    if (jb < je) fetch(jb);
+    for (int j = jb; j < je; ++j) {
+        E af[KS], bf[KS];
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            af[ks] = an[ks];
+            bf[ks] = bn[ks];
+        }
+        if (j + 1 < je) fetch(j + 1);
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            if constexpr (CPLX) {
+                accR = BsrMfma<R>::mma(af[ks].x, bf[ks].x, accR);
+                accI = BsrMfma<R>::mma(af[ks].x, bf[ks].y, accI);
+                accR = BsrMfma<R>::mma(-af[ks].y, bf[ks].y, accR);
+                accI = BsrMfma<R>::mma(af[ks].y, bf[ks].x, accI);
+            } else {
+                accR = BsrMfma<R>::mma(af[ks], bf[ks], accR);
+            }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int row = BsrMfma<R>::row(lane, q);
+        if (row >= BI || !bcol_ok) continue;
+        const long img = i * BI + row;
+        E *yp = YROW ? y + img * p.ldy + bcol : y + img + bcol * p.ldy;
+        E out;
+        if constexpr (CPLX)
+            out = Ops<E>::scale(E{accR[q], accI[q]}, p.alpha_re, p.alpha_im);
+        else
+            out = Ops<E>::scale(accR[q], p.alpha_re, p.alpha_im);
+        *yp = p.add ? Ops<E>::add(*yp, out) : out;
+    }
+}
+
+// ELL form with a compile-time number of nonzero blocks per row (the 9-point stencils): the
+// row's block columns are read first (scalar loads), then the fragments of NB blocks at a time
+// are loaded one group ahead of the MFMAs, so no load waits on another load and NB blocks' bytes
+// are in flight per wave.
+template <typename R, bool CPLX, int BI, int BD, bool YROW, bool XROW, int NNZ, int NB>
+__global__ void __launch_bounds__(256) bsr_mfma_ell_kernel(const BsrArgs p, long ntiles_n) {
+    typedef typename BsrMfmaElem<R, CPLX>::type E;
+    typedef typename BsrMfma<R>::acc_t acc_t;
+    static_assert(BI <= 16 && BD % 4 == 0 && NNZ % NB == 0, "block shape");
+    constexpr int KS = BD / 4, NG = NNZ / NB;
+    const E *__restrict__ v = (const E *)p.v;
+    const E *__restrict__ x = (const E *)p.x;
+    E *__restrict__ y = (E *)p.y;
+    const int lane = threadIdx.x & 63;
+    const long wave = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (wave >= p.block_rows * ntiles_n) return; // whole waves only: MFMA needs all 64 lanes
+    const long i = wave / ntiles_n;
+    const long col0 = (wave % ntiles_n) * 16;
+    const int ar = lane & 15, kq = lane >> 4;
+    const bool arow_ok = ar < BI;
+    const int arc = arow_ok ? ar : 0;
+    const long bcol = col0 + (lane & 15);
+    const bool bcol_ok = bcol < p.ncols;
+    const long bcc = bcol_ok ? bcol : 0;
+    const long jb = i * NNZ;
+    int dj[NNZ];
+#pragma unroll
+    for (int k = 0; k < NNZ; ++k) dj[k] = p.jj[jb + k];
+    E af[2][NB][KS], bf[2][NB][KS];
+    auto fetch = [&](int g, E (*a_)[KS], E (*b_)[KS]) {
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+            const int k = g * NB + u;
+            const bool ok = dj[k] >= 0;
+            const long d0 = ok ? dj[k] : 0;
+            const E *vb = v + (jb + k) * (BI * BD);
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const int e = ks * 4 + kq;
+                const E a = p.block_im_fast ? vb[arc + e * BI] : vb[arc * BD + e];
+                const E b = XROW ? x[(d0 + e) * p.ldx + bcc] : x[(d0 + e) + bcc * p.ldx];
+                a_[u][ks] = (arow_ok && ok) ? a : E{};
+                b_[u][ks] = bcol_ok ? b : E{};
+            }
+        }
+    };
+    acc_t accR = acc_t{0, 0, 0, 0}, accI = acc_t{0, 0, 0, 0};
+    fetch(0, af[0], bf[0]);
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+        if (g + 1 < NG) fetch(g + 1, af[(g + 1) & 1], bf[(g + 1) & 1]);
+#pragma unroll
+        for (int u = 0; u < NB; ++u)
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const E a = af[g & 1][u][ks], b = bf[g & 1][u][ks];
+                if constexpr (CPLX) {
+                    accR = BsrMfma<R>::mma(a.x, b.x, accR);
+                    accI = BsrMfma<R>::mma(a.x, b.y, accI);
+                    accR = BsrMfma<R>::mma(-a.y, b.y, accR);
+                    accI = BsrMfma<R>::mma(a.y, b.x, accI);
+                } else {
+                    accR = BsrMfma<R>::mma(a, b, accR);
+                }
+            }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int row = BsrMfma<R>::row(lane, q);
+        if (row >= BI || !bcol_ok) continue;
+        const long img = i * BI + row;
+        E *yp = YROW ? y + img * p.ldy + bcol : y + img + bcol * p.ldy;
+        E out;
+        if constexpr (CPLX)
+            out = Ops<E>::scale(E{accR[q], accI[q]}, p.alpha_re, p.alpha_im);
+        else
+            out = Ops<E>::scale(accR[q], p.alpha_re, p.alpha_im);
+        *yp = p.add ? Ops<E>::add(*yp, out) : out;
+    }
+}
+
+template <typename R, bool CPLX, int BI, int BD, int NNZ, int NB>
+void launch_bsr_mfma_ell(const BsrArgs &a, bool yrow, bool xrow, hipStream_t s) {
+    const long ntn = (a.ncols + 15) / 16;
+    const long waves = a.block_rows * ntn;
+    const long blocks = (waves + 3) / 4;
+    if (blocks >= (1L << 31)) throw Error("bsr: grid too large");
+    KernelTimer timer("bsr", s);
+    if (yrow && xrow)
+        hipLaunchKernelGGL((bsr_mfma_ell_kernel<R, CPLX, BI, BD, true, true, NNZ, NB>), dim3(blocks), dim3(256), 0, s, a, ntn);
+    else if (yrow && !xrow)
+        hipLaunchKernelGGL((bsr_mfma_ell_kernel<R, CPLX, BI, BD, true, false, NNZ, NB>), dim3(blocks), dim3(256), 0, s, a, ntn);
+    else if (!yrow && xrow)
+        hipLaunchKernelGGL((bsr_mfma_ell_kernel<R, CPLX, BI, BD, false, true, NNZ, NB>), dim3(blocks), dim3(256), 0, s, a, ntn);
+    else
+        hipLaunchKernelGGL((bsr_mfma_ell_kernel<R, CPLX, BI, BD, false, false, NNZ, NB>), dim3(blocks), dim3(256), 0, s, a, ntn);
+    SBX_HIP_CHECK(hipGetLastError());
+}
+
+template <typename R, bool CPLX, int BI, int BD>
+void launch_bsr_mfma_pf(const BsrArgs &a, bool yrow, bool xrow, hipStream_t s) {
+    const long ntn = (a.ncols + 15) / 16;
+    const long waves = a.block_rows * ntn;
+    const long blocks = (waves + 3) / 4;
+    if (blocks >= (1L << 31)) throw Error("bsr: grid too large");
+    KernelTimer timer("bsr", s);
+    if (yrow && xrow)
+        hipLaunchKernelGGL((bsr_mfma_pf_kernel<R, CPLX, BI, BD, true, true>), dim3(blocks), dim3(256), 0, s, a, ntn);
+    else if (yrow && !xrow)
+        hipLaunchKernelGGL((bsr_mfma_pf_kernel<R, CPLX, BI, BD, true, false>), dim3(blocks), dim3(256), 0, s, a, ntn);
+    else if (!yrow && xrow)
+        hipLaunchKernelGGL((bsr_mfma_pf_kernel<R, CPLX, BI, BD, false, true>), dim3(blocks), dim3(256), 0, s, a, ntn);
+    else
+        hipLaunchKernelGGL((bsr_mfma_pf_kernel<R, CPLX, BI, BD, false, false>), dim3(blocks), dim3(256), 0, s, a, ntn);
+    SBX_HIP_CHECK(hipGetLastError());
+}
+
 template <typename R, bool CPLX, int BI, int BD, int ROWS>
-void launch_bsr_mfma(const BsrArgs &a, bool yrow, bool xrow, hipStream_t s) {
+void launch_bsr_mfma(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_t s) {
+    // the 9-point stencils: columns preloaded, one block ahead (16^4 complex<double> n = 12:
+    // 426 -> 350 us; complex<float> 16^3 x 64: 985 -> 797 us); a 3- or 9-block lookahead, the
+    // XCD-grouped row order and non-temporal value loads were all measured slower
+    if (g_bsr_tune.variant == 0 && nnz == 9) return launch_bsr_mfma_ell<R, CPLX, BI, BD, 9, 1>(a, yrow, xrow, s);
+    if (g_bsr_tune.variant == 0) return launch_bsr_mfma_pf<R, CPLX, BI, BD>(a, yrow, xrow, s);
     const long ntn = (a.ncols + 15) / 16;
     const long waves = (a.block_rows + ROWS - 1) / ROWS * ntn;
     const long blocks = (waves + 3) / 4;
@@ -386,13 +585,13 @@ void launch_typed(const BsrArgs &a, int nnz_per_row, bool yrow, bool xrow, hipSt
         // one block row per wave: interleaving 2 or 4 rows per wave measured 6 % / 25 % slower
         // (more VGPRs, fewer waves to hide the HBM latency of the value stream)
         if constexpr (std::is_same<E, double2>::value)
-            launch_bsr_mfma<double, true, 12, 12, 1>(a, yrow, xrow, s);
+            launch_bsr_mfma<double, true, 12, 12, 1>(a, nnz_per_row, yrow, xrow, s);
         else if constexpr (std::is_same<E, double>::value)
-            launch_bsr_mfma<double, false, 12, 12, 1>(a, yrow, xrow, s);
+            launch_bsr_mfma<double, false, 12, 12, 1>(a, nnz_per_row, yrow, xrow, s);
         else if constexpr (std::is_same<E, float2>::value)
-            launch_bsr_mfma<float, true, 12, 12, 1>(a, yrow, xrow, s);
+            launch_bsr_mfma<float, true, 12, 12, 1>(a, nnz_per_row, yrow, xrow, s);
         else
-            launch_bsr_mfma<float, false, 12, 12, 1>(a, yrow, xrow, s);
+            launch_bsr_mfma<float, false, 12, 12, 1>(a, nnz_per_row, yrow, xrow, s);
     }
     else
         launch_layouts<E, 0, 0>(a, yrow, xrow, blocks, s);

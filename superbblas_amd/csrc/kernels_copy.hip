@@ -23,6 +23,7 @@
 #include <numeric>
 
 namespace sbx {
+CopyTune g_copy_tune;
 namespace {
 
 /// Unsigned 32-bit division by a runtime constant (mul-hi + shift)
@@ -167,6 +168,7 @@ struct TiledArgs {
     FastDiv fR, fTU, fTV;   // divisors
     FastDiv fRTU, fRTV;     // R*TU, R*TV
     uint32_t ntu, ntv;      // number of tiles along U and V
+    uint32_t lr, lw;        // log2 of the lanes per tile row in the read / write phase
     int nu, nv;             // dims in the U chain (source-contiguous) / V chain (dest-contiguous)
     FastDiv usize[MAXD], vsize[MAXD];
     long usst[MAXD], udst[MAXD], vsst[MAXD], vdst[MAXD];
@@ -264,6 +266,103 @@ __global__ void __launch_bounds__(256) copy_tiled_kernel(const TiledArgs p) {
             if (e < nwrite && vv < nv_t)
                 put<ADD, D>(dst + dbase + du[u] + dv[vv] + r,
                             scale<D>(tile[vv * ld + u * p.R + r], p.alpha));
+        }
+    }
+}
+
+/// Offsets of item `idx` of a chain of dims (fastest first), unrolled for short chains
+__device__ __forceinline__ void chain_offsets4(uint32_t idx, int n, const FastDiv *size,
+                                               const long *sst, const long *dst, long &so,
+                                               long &doff) {
+    so = 0;
+    doff = 0;
+#pragma unroll
+    for (int i = 0; i < MAXD; ++i) {
+        if (i >= n) break;
+        const uint32_t q = size[i].div(idx);
+        const uint32_t c = idx - q * size[i].d;
+        idx = q;
+        so += (long)c * sst[i];
+        doff += (long)c * dst[i];
+    }
+}
+
+// Row-mapped single-pass form: in the read phase lane l of a wave owns the positions l, l+64, ...
+// of a tile row (a source-contiguous run of R*TU elements) and the wave walks the rows v = wave,
+// wave+4, ...; the write phase does the same over destination rows.  A lane's (u, r) split and
+// offset base are computed once, so an element costs one LDS offset read (wave-uniform), one
+// global access and one LDS access.  The u and v offset tables are filled by different waves.
+template <typename S, typename D, bool ADD, int KR>
+__global__ void __launch_bounds__(256) copy_tiled3_kernel(const TiledArgs p) {
+    __shared__ D tile[tile_elems<D>() + 64];
+    __shared__ long su[256], du[256], sv[256], dv[256];
+    const S *__restrict__ src = (const S *)p.src;
+    D *__restrict__ dst = (D *)p.dstp;
+    uint32_t b = blockIdx.x;
+    const uint32_t tu = b % p.ntu;
+    b /= p.ntu;
+    const uint32_t tv = b % p.ntv;
+    uint32_t w = b / p.ntv;
+    long sbase = 0, dbase = 0;
+#pragma unroll
+    for (int i = 0; i < MAXD; ++i) {
+        if (i >= p.nw) break;
+        const uint32_t q = p.wsize[i].div(w);
+        const uint32_t c = w - q * p.wsize[i].d;
+        w = q;
+        sbase += (long)c * p.wsst[i];
+        dbase += (long)c * p.wdst[i];
+    }
+    const uint32_t u0 = tu * p.TU, v0 = tv * p.TV;
+    const uint32_t nu_t = min(p.TU, p.NU - u0), nv_t = min(p.TV, p.NV - v0);
+    const uint32_t t = threadIdx.x;
+    if (t < 128) {
+        if (t < nu_t) chain_offsets4(u0 + t, p.nu, p.usize, p.usst, p.udst, su[t], du[t]);
+        if (t + 128 < nu_t) chain_offsets4(u0 + t + 128, p.nu, p.usize, p.usst, p.udst, su[t + 128], du[t + 128]);
+    } else {
+        const uint32_t v = t - 128;
+        if (v < nv_t) chain_offsets4(v0 + v, p.nv, p.vsize, p.vsst, p.vdst, sv[v], dv[v]);
+        if (v + 128 < nv_t) chain_offsets4(v0 + v + 128, p.nv, p.vsize, p.vsst, p.vdst, sv[v + 128], dv[v + 128]);
+    }
+    __syncthreads();
+    const uint32_t lane = t & 63, wave = t >> 6;
+    const uint32_t ld = p.TU * p.R + 1;
+    // read phase: rows = v (nv_t of them), row width R*nu_t; 2^lr lanes per row, so a wave
+    // covers 64 >> lr rows per step and a thread keeps KR rows' loads in flight
+    {
+        const uint32_t wr = p.R * nu_t, lpr = 1u << p.lr;
+        const uint32_t step = 4u * (64u >> p.lr);
+        const uint32_t vfirst = wave * (64u >> p.lr) + (lane >> p.lr);
+        for (uint32_t pos = lane & (lpr - 1); pos < wr; pos += lpr) {
+            const uint32_t u = p.fR.div(pos), r = pos - u * p.R;
+            const long base = sbase + su[u] + r;
+            for (uint32_t vb = vfirst; vb < nv_t; vb += step * KR) {
+                D val[KR];
+#pragma unroll
+                for (int k = 0; k < KR; ++k) {
+                    const uint32_t v = vb + step * k;
+                    val[k] = conv<D, S>(src[base + sv[v < nv_t ? v : vb]]);
+                }
+#pragma unroll
+                for (int k = 0; k < KR; ++k) {
+                    const uint32_t v = vb + step * k;
+                    if (v < nv_t) tile[v * ld + pos] = val[k];
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // write phase: rows = u (nu_t of them), row width R*nv_t
+    {
+        const uint32_t ww = p.R * nv_t, lpr = 1u << p.lw;
+        const uint32_t step = 4u * (64u >> p.lw);
+        const uint32_t ufirst = wave * (64u >> p.lw) + (lane >> p.lw);
+        for (uint32_t pos = lane & (lpr - 1); pos < ww; pos += lpr) {
+            const uint32_t v = p.fR.div(pos), r = pos - v * p.R;
+            const long base = dbase + dv[v] + r;
+            const uint32_t lb = v * ld + r;
+            for (uint32_t u = ufirst; u < nu_t; u += step)
+                put<ADD, D>(dst + base + du[u], scale<D>(tile[lb + u * p.R], p.alpha));
         }
     }
 }
@@ -438,8 +537,9 @@ void launch_pair(const BoxCopyDesc &d, Norm n, long total, hipStream_t stream) {
     // Tile sizes: contiguous runs of >= 48 elements on both sides (>= 768 B for 16-byte
     // elements) and ~1.5K elements per workgroup so several workgroups share a CU
     // small copies: smaller tiles so that >= ~1024 workgroups (4 per CU) share the chip
-    const long budget = std::max(256L, std::min((long)tile_elems<D>(), total / 1024));
-    constexpr long run_target = 48; // elements per contiguous source run of a tile row
+    long budget = std::max(256L, std::min((long)tile_elems<D>(), total / 1024));
+    if (g_copy_tune.budget > 0) budget = std::min((long)tile_elems<D>(), g_copy_tune.budget);
+    const long run_target = g_copy_tune.run > 0 ? g_copy_tune.run : 48; // elements per contiguous source run of a tile row
     // the LDS image holds TV padded rows of R*TU + 1 elements: TV * (R*TU + 1) <= budget + 64
     const long cap = budget + 64;
     long TU = std::min(std::min(NU, std::max(1L, (run_target + R - 1) / R)), 256L);
@@ -456,6 +556,14 @@ void launch_pair(const BoxCopyDesc &d, Norm n, long total, hipStream_t stream) {
     a.fTV = FastDiv((uint32_t)TV);
     a.fRTU = FastDiv((uint32_t)(R * TU));
     a.fRTV = FastDiv((uint32_t)(R * TV));
+    // lanes per tile row: the smallest power of two >= the row width, at most a wave
+    auto lanes_log2 = [](long width) {
+        uint32_t l = 0;
+        while (l < 6 && (1L << l) < width) ++l;
+        return l;
+    };
+    a.lr = lanes_log2(R * TU);
+    a.lw = lanes_log2(R * TV);
     a.ntu = (uint32_t)((NU + TU - 1) / TU);
     a.ntv = (uint32_t)((NV + TV - 1) / TV);
     a.nu = (int)U.size();
@@ -493,8 +601,12 @@ void launch_pair(const BoxCopyDesc &d, Norm n, long total, hipStream_t stream) {
                      NU, NV, TU, TV, a.nu, a.nv, nw, blocks);
     }
     KernelTimer timer("copy", stream);
-    hipLaunchKernelGGL((copy_tiled_kernel<S, D, ADD>), dim3((unsigned)blocks), dim3(256), 0,
-                       stream, a);
+    if (g_copy_tune.kernel == 1)
+        hipLaunchKernelGGL((copy_tiled_kernel<S, D, ADD>), dim3((unsigned)blocks), dim3(256), 0,
+                           stream, a);
+    else
+        hipLaunchKernelGGL((copy_tiled3_kernel<S, D, ADD, 4>), dim3((unsigned)blocks), dim3(256),
+                           0, stream, a);
     SBX_HIP_CHECK(hipGetLastError());
 }
 

@@ -171,6 +171,17 @@ struct BoxCopyDesc {
     const float *src_mask = nullptr, *dst_mask = nullptr;
 };
 void launch_box_copy(const BoxCopyDesc &d, int device);
+/// Kernel-shape overrides for tuning runs (0 = the library's choice); set through sbx_tune_set
+struct CopyTune {
+    long budget = 0; ///< elements per LDS tile
+    long run = 0;    ///< target elements of a tile row's contiguous source run
+    int kernel = 0;  ///< 1: the round-1 tiled kernel (element-indexed phases) instead of the row-mapped one
+};
+extern CopyTune g_copy_tune;
+struct BsrTune {
+    int variant = 0; ///< 12x12 MFMA kernel: 0 = the library's choice, 1 = the round-1 kernel
+};
+extern BsrTune g_bsr_tune;
 
 /// Fill `n` elements of type `t` with zeros
 void launch_zero(void *p, std::size_t bytes, int device);

@@ -71,6 +71,45 @@ def test_bsr_lattice(gpu, spin, color, ncols, y_layout):
     op.destroy()
 
 
+@pytest.mark.parametrize("spin,color,ncols", [(1, 3, 3), (4, 3, 2), (4, 3, 17)])
+@pytest.mark.parametrize("variant", [0, 1])
+def test_bsr_ragged_rows(gpu, spin, color, ncols, variant):
+    """Rows with 0..9 nonzero blocks (a CSR operator, not ELL): the general-row kernels (12x12:
+    the one-block-ahead MFMA kernel, variant 0, and the round-1 kernel, variant 1), exact."""
+    import torch
+    import superbblas_amd as sb
+    L = 4
+    dim, ii, jj, vals, nb = lattice_operator(L, spin, color)
+    b = spin * color
+    vol = L ** 4
+    keep = np.arange(vol) % (nb + 1)  # row r keeps its first r % 10 blocks
+    sel = np.concatenate([np.arange(r * nb, r * nb + keep[r]) for r in range(vol)])
+    ii2 = keep.astype(np.int32)
+    jj2 = jj.reshape(vol * nb, 6)[sel].reshape(-1).astype(np.int32)
+    vals2 = vals.reshape(vol * nb, b * b)[sel].reshape(-1)
+    x = (np.arange(vol * b * ncols) % 13 - 6 + 1j * (np.arange(vol * b * ncols) % 3)).astype(
+        np.complex128)
+    yref = np.zeros(vol * b * ncols, np.complex128)
+    oracle_bsr(T_CDOUBLE, dim, 0, vol, b, b, ii2, jj2, vals2, False, x, ncols, True, yref, ncols,
+               True, ncols, 1.0)
+    full = [([0] * 6, dim)]
+    sb.tune_set("bsr.variant", variant)
+    try:
+        op = sb.create_bsr(full, dim, full, dim, [1, 1, 1, 1, spin, color],
+                           [1, 1, 1, 1, spin, color], False, [torch.from_numpy(ii2).to(gpu)],
+                           [torch.from_numpy(jj2).to(gpu)], [torch.from_numpy(vals2).to(gpu)])
+        dimx = [1, L, L, L, L, spin, color, ncols]
+        ty = torch.full((vol * b * ncols,), 7.0, dtype=torch.complex128, device=gpu)
+        sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", [([0] * 8, dimx)], "pXYZTSCn", [0] * 8, dimx,
+                      dimx, [torch.from_numpy(x).to(gpu)], 0.0, [([0] * 8, dimx)], "pxyztscn",
+                      [0] * 8, dimx, dimx, "p", [ty])
+        torch.cuda.synchronize()
+        op.destroy()
+    finally:
+        sb.tune_set("bsr.variant", 0)
+    assert np.array_equal(ty.cpu().numpy(), yref)
+
+
 @pytest.mark.parametrize("dtype,ttype", [(np.complex64, 2), (np.float64, 1), (np.float32, 0)])
 @pytest.mark.parametrize("spin,color,ncols", [(1, 3, 5), (4, 3, 3), (4, 3, 20)])
 def test_bsr_lattice_types(gpu, dtype, ttype, spin, color, ncols):

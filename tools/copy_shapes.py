@@ -45,6 +45,14 @@ def case(name, o0, d0, o1, d1, from1, dtype, reps=10):
 
 
 def main():
+    for kern in (0, 1):
+        sb.tune_set("copy.kernel", kern)
+        print(json.dumps({"copy.kernel": kern}))
+        shapes()
+    sb.tune_set("copy.kernel", 0)
+
+
+def shapes():
     L, n = 16, 64
     case("slice", "xyztsc", [L, L, L, L, 4, 3], "tnsxyzc", [L, n, 4, L, L, L, 3],
          [0, 5, 0, 0, 0, 0, 0], torch.complex128)
