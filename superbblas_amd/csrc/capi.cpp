@@ -338,6 +338,7 @@ int sbx_tune_set(const char *key, long long value) {
         if (k == "copy.budget") g_copy_tune.budget = (long)value;
         else if (k == "copy.run") g_copy_tune.run = (long)value;
         else if (k == "copy.kernel") g_copy_tune.kernel = (int)value;
+        else if (k == "copy.nt") g_copy_tune.nt = (int)value;
         else if (k == "bsr.variant") g_bsr_tune.variant = (int)value;
         else throw Error("tune_set: unknown key " + k);
     });

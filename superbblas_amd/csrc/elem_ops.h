@@ -1,4 +1,4 @@
-// Element arithmetic shared by the BSR kernels: complex (double2 / float2, interleaved re/im
+// Element arithmetic shared by the BSR and copy kernels: complex (double2 / float2, interleaved re/im
 // as std::complex) and real types.  Alpha is passed as doubles (the ABI's scalar).
 #pragma once
 
@@ -50,6 +50,25 @@ template <> struct Ops<float> {
     static __device__ __forceinline__ float add(float a, float b) { return a + b; }
     static __device__ __forceinline__ bool nonzero(float a) { return a != 0; }
 };
+
+/// Non-temporal (streaming) store of one element: the line is written through without being
+/// kept in the caches (outputs written once and not re-read by the same kernel)
+template <typename D> __device__ __forceinline__ void store_nt(D *p, D v) {
+    if constexpr (sizeof(D) == 16) {
+        typedef double v2 __attribute__((ext_vector_type(2)));
+        v2 t;
+        __builtin_memcpy(&t, &v, 16);
+        __builtin_nontemporal_store(t, (v2 *)p);
+    } else if constexpr (sizeof(D) == 8) {
+        double t;
+        __builtin_memcpy(&t, &v, 8);
+        __builtin_nontemporal_store(t, (double *)p);
+    } else {
+        float t;
+        __builtin_memcpy(&t, &v, 4);
+        __builtin_nontemporal_store(t, (float *)p);
+    }
+}
 
 } // namespace
 } // namespace sbx

@@ -508,7 +508,8 @@ template <typename R, bool CPLX, int BI, int BD, int ROWS>
 void launch_bsr_mfma(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_t s) {
     // the 9-point stencils: columns preloaded, one block ahead (16^4 complex<double> n = 12:
     // 426 -> 350 us; complex<float> 16^3 x 64: 985 -> 797 us); a 3- or 9-block lookahead, the
-    // XCD-grouped row order and non-temporal value loads were all measured slower
+    // XCD-grouped row order and non-temporal value loads were all measured slower, and
+    // non-temporal stores of y no faster
     if (g_bsr_tune.variant == 0 && nnz == 9) return launch_bsr_mfma_ell<R, CPLX, BI, BD, 9, 1>(a, yrow, xrow, s);
     if (g_bsr_tune.variant == 0) return launch_bsr_mfma_pf<R, CPLX, BI, BD>(a, yrow, xrow, s);
     const long ntn = (a.ncols + 15) / 16;
@@ -552,7 +553,8 @@ void launch_ell_g(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_t s
 template <typename E, int BI, int BD>
 void launch_ell(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_t s) {
     // two rhs columns per thread (measured against 1 and 4, and 48 KB of LDS per workgroup:
-    // 16^4 3x3 n = 12: 46 us vs 51 / 61; n = 64: 191 us vs 218 / 234)
+    // 16^4 3x3 n = 12: 46 us vs 51 / 61; n = 64: 191 us vs 218 / 234; one column per thread
+    // over all 256 threads with the x rows of all 9 blocks in flight: 56-60 us)
     launch_ell_g<E, BI, BD, 2>(a, nnz, yrow, xrow, s, ELL_LDS_BYTES);
 }
 

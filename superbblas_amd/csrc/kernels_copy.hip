@@ -15,6 +15,7 @@
 //      contiguous in the source
 //      starting at stride R; everything else is an outer dim handled by the grid;
 //   4. if U is empty the direct kernel (destination-ordered gather) is used.
+#include "elem_ops.h"
 #include "sbx_internal.h"
 
 #include <algorithm>
@@ -150,13 +151,18 @@ __global__ void __launch_bounds__(256) copy_masked_kernel(const DirectArgs p,
     }
 }
 
-// Contiguous copy of `total` elements (both sides dense)
+// Contiguous copy of `total` elements (both sides dense); streaming stores when `nt`
 template <typename S, typename D, bool ADD>
 __global__ void __launch_bounds__(256) copy_contig_kernel(const S *__restrict__ src,
                                                            D *__restrict__ dst, long total,
-                                                           Alpha alpha) {
-    for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256L)
-        put<ADD, D>(dst + idx, scale<D>(conv<D, S>(src[idx]), alpha));
+                                                           Alpha alpha, int nt) {
+    for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256L) {
+        const D v = scale<D>(conv<D, S>(src[idx]), alpha);
+        if (!ADD && nt)
+            store_nt(dst + idx, v);
+        else
+            put<ADD, D>(dst + idx, v);
+    }
 }
 
 /// LDS tile capacity in elements: 24 KB of tile per workgroup whatever the element size
@@ -169,6 +175,7 @@ struct TiledArgs {
     FastDiv fRTU, fRTV;     // R*TU, R*TV
     uint32_t ntu, ntv;      // number of tiles along U and V
     uint32_t lr, lw;        // log2 of the lanes per tile row in the read / write phase
+    int nt;                 // non-temporal stores
     int nu, nv;             // dims in the U chain (source-contiguous) / V chain (dest-contiguous)
     FastDiv usize[MAXD], vsize[MAXD];
     long usst[MAXD], udst[MAXD], vsst[MAXD], vdst[MAXD];
@@ -362,7 +369,13 @@ __global__ void __launch_bounds__(256) copy_tiled3_kernel(const TiledArgs p) {
             const long base = dbase + dv[v] + r;
             const uint32_t lb = v * ld + r;
             for (uint32_t u = ufirst; u < nu_t; u += step)
-                put<ADD, D>(dst + base + du[u], scale<D>(tile[lb + u * p.R], p.alpha));
+            {
+                const D val = scale<D>(tile[lb + u * p.R], p.alpha);
+                if (!ADD && p.nt)
+                    store_nt(dst + base + du[u], val);
+                else
+                    put<ADD, D>(dst + base + du[u], val);
+            }
         }
     }
 }
@@ -439,8 +452,9 @@ void launch_pair(const BoxCopyDesc &d, Norm n, long total, hipStream_t stream) {
     if (n.size.size() == 1 && n.ss[0] == 1 && n.ds[0] == 1) {
         const long blocks = std::min((total + 255) / 256, 8192L);
         KernelTimer timer("copy", stream);
+        const int nt = g_copy_tune.nt > 0 || (g_copy_tune.nt == 0 && total * (long)sizeof(D) >= (8L << 20));
         hipLaunchKernelGGL((copy_contig_kernel<S, D, ADD>), dim3((unsigned)blocks), dim3(256), 0,
-                           stream, src, dst, total, alpha);
+                           stream, src, dst, total, alpha, nt);
         SBX_HIP_CHECK(hipGetLastError());
         return;
     }
@@ -562,6 +576,9 @@ void launch_pair(const BoxCopyDesc &d, Norm n, long total, hipStream_t stream) {
         while (l < 6 && (1L << l) < width) ++l;
         return l;
     };
+    // streaming stores for large destinations (written once, not re-read by this kernel):
+    // the config-2p slice loop 6.8 -> 4.9 us per slice, the 1.6 GB permute 5.0 -> 5.2 TB/s
+    a.nt = g_copy_tune.nt > 0 || (g_copy_tune.nt == 0 && total * (long)sizeof(D) >= (8L << 20));
     a.lr = lanes_log2(R * TU);
     a.lw = lanes_log2(R * TV);
     a.ntu = (uint32_t)((NU + TU - 1) / TU);

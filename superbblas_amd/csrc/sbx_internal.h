@@ -176,6 +176,7 @@ struct CopyTune {
     long budget = 0; ///< elements per LDS tile
     long run = 0;    ///< target elements of a tile row's contiguous source run
     int kernel = 0;  ///< 1: the round-1 tiled kernel (element-indexed phases) instead of the row-mapped one
+    int nt = 0;      ///< row-mapped kernel stores: 0 = non-temporal for large outputs, 1 = always, -1 = never
 };
 extern CopyTune g_copy_tune;
 struct BsrTune {

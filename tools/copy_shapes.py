@@ -45,11 +45,13 @@ def case(name, o0, d0, o1, d1, from1, dtype, reps=10):
 
 
 def main():
-    for kern in (0, 1):
+    for kern, nt in ((0, 0), (1, 0), (0, -1)):
         sb.tune_set("copy.kernel", kern)
-        print(json.dumps({"copy.kernel": kern}))
+        sb.tune_set("copy.nt", nt)
+        print(json.dumps({"copy.kernel": kern, "copy.nt": nt}))
         shapes()
     sb.tune_set("copy.kernel", 0)
+    sb.tune_set("copy.nt", 0)
 
 
 def shapes():

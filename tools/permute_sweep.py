@@ -56,9 +56,9 @@ def main():
     print(json.dumps({"case": "torch contiguous copy x64 slices", "GBps": round(by / t / 1e9, 1),
                       "us_per_slice": round(t / n * 1e6, 2)}), flush=True)
     ref = None
-    configs = [dict(), dict(kernel=1)]
+    configs = [dict(), dict(kernel=1), dict(nt=-1)]
     for cfg in configs:
-        for k in ("budget", "run", "kernel"):
+        for k in ("budget", "run", "kernel", "nt"):
             sb.tune_set("copy." + k, cfg.get(k, 0))
         b.zero_()
 
