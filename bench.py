@@ -210,7 +210,12 @@ def main():
     # flops of one launch (a step's GEMM is split in T chunks when a cross-rank reduction is
     # pipelined behind it) / the launch's average duration
     flops_launch = flops_rank * args.steps / max(gemm_calls, 1)
-    achieved = flops_launch / kernel_s / 1e12
+    # executed MFMA flops: complex products in the 3-multiplication (Gauss) form issue 3 real
+    # multiply-adds per complex MAC (6 flops), the 4-multiplication form 4 (8 flops)
+    m3 = sb.tune_get("gemm.m3") >= 0
+    exec_per_alg = 6.0 / 8.0 if m3 else 1.0
+    algorithmic = flops_launch / kernel_s / 1e12
+    achieved = algorithmic * exec_per_alg
 
     side = {}
     if not args.no_side:
@@ -222,12 +227,12 @@ def main():
             except Exception as e:  # a side measurement never takes the bench down
                 side["chain_error"] = str(e)[:200]
     base = None
-    if rank == 0 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu:
         base = cpu_baseline(int(os.environ.get("OMP_NUM_THREADS", "16")))
         if world == 1 and not args.no_side:
             side.update(cpu_side_baselines(int(os.environ.get("OMP_NUM_THREADS", "16"))))
 
-    traffic, traffic_src = pmc_traffic("dma_kernel<", "128, 128, 8, 4, 2>")
+    traffic, traffic_src = pmc_traffic("dma_kernel<", "128, 128, 8, 4, 2")
     if rank == 0:
         line = {
             "metric": "lattice contraction GFLOP/s + permute GB/s, 16^4 spin×color, 1/2/4/8 GPUs",
@@ -256,10 +261,16 @@ def main():
                          "traffic_source": traffic_src,
                          "algorithmic_bytes": 16.0 * (2 * vol(local0) + vol(gdimr)),
                          "kernel": "gemm_dma_kernel<complex<double>, 128x128x8, 8 waves> (FP64 MFMA "
-                                   "16x16x4, complex 4M), %d launches, %.4f ms avg "
-                                   "(HIP events on its launch stream)" % (gemm_calls,
+                                   "16x16x4, complex %s), %d launches, %.4f ms avg "
+                                   "(HIP events on its launch stream)" % ("3M" if m3 else "4M",
+                                                                          gemm_calls,
                                                                           kernel_s * 1e3),
                          "flops_per_launch": flops_launch,
+                         "executed_flops_per_launch": flops_launch * exec_per_alg,
+                         "algorithmic_TFLOPs": round(algorithmic, 3),
+                         "complex_product": ("3-multiplication form (6 executed real flops per "
+                                             "complex MAC; value and algorithmic_TFLOPs count 8)"
+                                             if m3 else "4-multiplication form"),
                          "step_TFLOPs": round(flops_rank / step_s / 1e12, 3),
                          "splitk_reduce_ms_avg": round(red_ms / max(red_calls, 1), 4)},
             "cpu_baseline": base,

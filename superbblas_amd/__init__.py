@@ -265,6 +265,12 @@ def tune_set(key: str, value: int):
     _check(_lib.sbx_tune_set(key.encode(), ctypes.c_longlong(value)))
 
 
+def tune_get(key: str) -> int:
+    v = ctypes.c_longlong()
+    _check(_lib.sbx_tune_get(key.encode(), ctypes.byref(v)))
+    return v.value
+
+
 def timings_get(name: str) -> Tuple[float, int]:
     """(total milliseconds, launches) of a kernel family: gemm, gemm_splitk_reduce, copy, bsr."""
     ms, calls = ctypes.c_double(), ctypes.c_longlong()

@@ -340,7 +340,22 @@ int sbx_tune_set(const char *key, long long value) {
         else if (k == "copy.kernel") g_copy_tune.kernel = (int)value;
         else if (k == "copy.nt") g_copy_tune.nt = (int)value;
         else if (k == "bsr.variant") g_bsr_tune.variant = (int)value;
+        else if (k == "gemm.m3") g_gemm_tune.m3 = (int)value;
         else throw Error("tune_set: unknown key " + k);
+    });
+}
+
+int sbx_tune_get(const char *key, long long *value) {
+    return guard([&] {
+        if (!key || !value) throw Error("tune_get: null argument");
+        const std::string k(key);
+        if (k == "copy.budget") *value = g_copy_tune.budget;
+        else if (k == "copy.run") *value = g_copy_tune.run;
+        else if (k == "copy.kernel") *value = g_copy_tune.kernel;
+        else if (k == "copy.nt") *value = g_copy_tune.nt;
+        else if (k == "bsr.variant") *value = g_bsr_tune.variant;
+        else if (k == "gemm.m3") *value = g_gemm_tune.m3;
+        else throw Error("tune_get: unknown key " + k);
     });
 }
 

@@ -179,6 +179,10 @@ struct CopyTune {
     int nt = 0;      ///< row-mapped kernel stores: 0 = non-temporal for large outputs, 1 = always, -1 = never
 };
 extern CopyTune g_copy_tune;
+struct GemmTune {
+    int m3 = 0; ///< complex GEMMs (LDS-DMA kernel): -1 the 4-multiplication form, else the 3-multiplication form
+};
+extern GemmTune g_gemm_tune;
 struct BsrTune {
     int variant = 0; ///< 12x12 MFMA kernel: 0 = the library's choice, 1 = the round-1 kernel
 };
