@@ -23,10 +23,12 @@ struct GroupStride {
     long stride, vol;
 };
 
-/// Stride/volume of a label group in a dense array; !ok if the group labels (in the given
-/// order, size-1 labels ignored) are not one contiguous run of memory
-GroupStride group_stride(const std::string &group, const std::string &labels, const Coor &size) {
-    const std::vector<long> st = strides_slow_to_fast(size);
+/// Stride/volume of a label group of a box of extents `size` inside a dense array of extents
+/// `dims` (empty: the box is the array); !ok if the group labels (in the given order, size-1
+/// labels ignored) are not one contiguous run of memory
+GroupStride group_stride(const std::string &group, const std::string &labels, const Coor &size,
+                         const Coor &dims = Coor()) {
+    const std::vector<long> st = strides_slow_to_fast(dims.empty() ? size : dims);
     GroupStride g{true, 0, 1};
     int prev = -1;
     for (char c : group) {
@@ -77,12 +79,15 @@ void local_contraction(const Scalar &alpha, const Local &x, bool conjx, const Lo
     }
     if (r.labels.size() != T.size() + M.size() + N.size())
         throw Error("o_r has unmatched dimensions");
-    const auto gx_t = group_stride(T, x.labels, x.size), gx_k = group_stride(K, x.labels, x.size),
-               gx_m = group_stride(M, x.labels, x.size);
-    const auto gy_t = group_stride(T, y.labels, y.size), gy_k = group_stride(K, y.labels, y.size),
-               gy_n = group_stride(N, y.labels, y.size);
-    const auto gr_t = group_stride(T, r.labels, r.size), gr_m = group_stride(M, r.labels, r.size),
-               gr_n = group_stride(N, r.labels, r.size);
+    const auto gx_t = group_stride(T, x.labels, x.size, x.dims),
+               gx_k = group_stride(K, x.labels, x.size, x.dims),
+               gx_m = group_stride(M, x.labels, x.size, x.dims);
+    const auto gy_t = group_stride(T, y.labels, y.size, y.dims),
+               gy_k = group_stride(K, y.labels, y.size, y.dims),
+               gy_n = group_stride(N, y.labels, y.size, y.dims);
+    const auto gr_t = group_stride(T, r.labels, r.size, r.dims),
+               gr_m = group_stride(M, r.labels, r.size, r.dims),
+               gr_n = group_stride(N, r.labels, r.size, r.dims);
     if (!(gx_t.ok && gx_k.ok && gx_m.ok && gy_t.ok && gy_k.ok && gy_n.ok && gr_t.ok && gr_m.ok &&
           gr_n.ok))
         throw Error("local_contraction: operands need reordering");
@@ -152,13 +157,36 @@ void check_contraction_args(const std::string &l0, const Coor &size0, const std:
             throw Error("o1 has unmatched directions");
 }
 
-/// A sub-slab [c0, c0+n) of the slowest label of a dense local array
+/// A sub-slab [c0, c0+n) of the slowest label of a local box
 Local slab(const Local &l, long c0, long n, std::size_t es) {
     Local r = l;
-    const long inner = volume(l.size) / std::max(1, l.size[0]);
+    const Coor &d = l.dims.empty() ? l.size : l.dims;
+    const long inner = volume(d) / std::max(1, d[0]);
     r.ptr = (char *)l.ptr + (std::size_t)(c0 * inner) * es;
     r.size[0] = (int)n;
     return r;
+}
+
+/// Offsets of box `f` inside component range `rc` (periodic coordinates), or empty if `f` is not
+/// a non-wrapping sub-box of `rc`
+Coor offset_in(const Range &f, const Range &rc, const Coor &dim) {
+    Coor off(f.from.size());
+    for (std::size_t j = 0; j < off.size(); ++j) {
+        const long o = normalize_coor((long)f.from[j] - rc.from[j], dim[j]);
+        if (o + f.size[j] > rc.size[j]) return Coor();
+        off[j] = (int)o;
+    }
+    return off;
+}
+
+/// View of the box `f` of component `ptr` (range `rc`, dense in its own extents)
+Local sub_view(void *ptr, int dev, const Range &rc, const Range &f, const Coor &off,
+               const std::string &labels, int dtype) {
+    const std::vector<long> st = strides_slow_to_fast(rc.size);
+    long o = 0;
+    for (std::size_t j = 0; j < off.size(); ++j) o += off[j] * st[j];
+    return Local{(char *)ptr + (std::size_t)o * dtype_size(dtype), dev, f.size, labels, dtype,
+                 rc.size};
 }
 
 void dist_contraction(const Scalar &alpha, const DistTensor &v0, const Coor &from0,
@@ -195,21 +223,22 @@ void dist_contraction(const Scalar &alpha, const DistTensor &v0, const Coor &fro
         if (X.labels.find(c) == std::string::npos) N += c;
     const std::string lX = T + M + K, lY = T + N + K, lR = T + N + M; // temporaries' layouts
 
-    auto layout_ok = [&](const std::string &labels, const Coor &size,
+    // every group of the box `size` inside an array of extents `dims` is one contiguous run
+    auto layout_ok = [&](const std::string &labels, const Coor &size, const Coor &dims,
                          std::initializer_list<const std::string *> groups) {
         for (const std::string *g : groups)
-            if (!group_stride(*g, labels, size).ok) return false;
+            if (!group_stride(*g, labels, size, dims).ok) return false;
         return true;
     };
-    auto same = [](const Range &a, const Range &b) { return a.from == b.from && a.size == b.size; };
 
     // Pieces of the work: X's ranges restricted to the box, repetitions removed (dist.h:3001-3028)
     struct WorkPiece {
         int rank, comp;
         Range px;        // in X coordinates (global)
         Range py, pr;    // needed ranges of Y and of the output (global coordinates)
-        int ydirect = -1; // local Y component usable in place
+        int ydirect = -1; // local Y component usable in place (the piece's box inside it)
         bool xdirect = false;
+        Coor xoff, yoff;  // offsets of the piece's boxes inside those components
     };
     std::vector<WorkPiece> work;
     {
@@ -252,16 +281,18 @@ void dist_contraction(const Scalar &alpha, const DistTensor &v0, const Coor &fro
                             w.pr.from[j] = fromr[j];
                             w.pr.size[j] = sizeY[k];
                         }
-                    // in-place use of X's component
-                    w.xdirect = same(f, rx) &&
-                                layout_ok(X.labels, rx.size, {&T, &M, &K});
+                    // in-place use of X's component (the piece may be a sub-box of it)
+                    w.xoff = offset_in(f, rx, X.dim);
+                    w.xdirect = !w.xoff.empty() &&
+                                layout_ok(X.labels, f.size, rx.size, {&T, &M, &K});
                     // in-place use of a Y component on the same rank
                     for (int j = 0; j < (int)Y.ranges[rk].size(); ++j) {
                         const Range &ry = Y.ranges[rk][j];
-                        if (same(w.py, ry) &&
-                            layout_ok(Y.labels, ry.size, {&T, &N, &K}) &&
+                        const Coor yo = offset_in(w.py, ry, Y.dim);
+                        if (!yo.empty() && layout_ok(Y.labels, w.py.size, ry.size, {&T, &N, &K}) &&
                             (comm.nprocs > 1 || rk != comm.rank || Y.dev[j] == X.dev[i])) {
                             w.ydirect = j;
+                            w.yoff = yo;
                             break;
                         }
                     }
@@ -272,14 +303,18 @@ void dist_contraction(const Scalar &alpha, const DistTensor &v0, const Coor &fro
     }
 
     // Single-process, single piece whose output is exactly one component: GEMM in place with beta
+    // (boxes may be sub-boxes of the components: contracting a slice runs in place too)
     if (comm.nprocs == 1 && work.size() == 1 && work[0].xdirect && work[0].ydirect >= 0 &&
-        vr.ranges[0].size() == 1 && same(work[0].pr, vr.ranges[0][0]) &&
-        layout_ok(vr.labels, vr.ranges[0][0].size, {&T, &N, &M}) &&
+        vr.ranges[0].size() == 1 && !offset_in(work[0].pr, vr.ranges[0][0], vr.dim).empty() &&
+        layout_ok(vr.labels, work[0].pr.size, vr.ranges[0][0].size, {&T, &N, &M}) &&
         vr.dev[0] == X.dev[work[0].comp]) {
         const WorkPiece &w = work[0];
-        Local lx{X.ptr[w.comp], X.dev[w.comp], X.ranges[0][w.comp].size, X.labels, dtype};
-        Local ly{Y.ptr[w.ydirect], Y.dev[w.ydirect], Y.ranges[0][w.ydirect].size, Y.labels, dtype};
-        Local lr{vr.ptr[0], vr.dev[0], vr.ranges[0][0].size, vr.labels, dtype};
+        const Local lx = sub_view(X.ptr[w.comp], X.dev[w.comp], X.ranges[0][w.comp], w.px, w.xoff,
+                                  X.labels, dtype);
+        const Local ly = sub_view(Y.ptr[w.ydirect], Y.dev[w.ydirect], Y.ranges[0][w.ydirect],
+                                  w.py, w.yoff, Y.labels, dtype);
+        const Local lr = sub_view(vr.ptr[0], vr.dev[0], vr.ranges[0][0], w.pr,
+                                  offset_in(w.pr, vr.ranges[0][0], vr.dim), vr.labels, dtype);
         local_contraction(alpha, lx, conjX, ly, conjY, beta, lr);
         return;
     }
@@ -319,7 +354,8 @@ void dist_contraction(const Scalar &alpha, const DistTensor &v0, const Coor &fro
                 l.x = Local{bufs.back().ptr, dev, r.size, lX, dtype};
             }
         } else if (mine) {
-            l.x = Local{X.ptr[w.comp], dev, X.ranges[w.rank][w.comp].size, X.labels, dtype};
+            l.x = sub_view(X.ptr[w.comp], dev, X.ranges[w.rank][w.comp], w.px, w.xoff, X.labels,
+                           dtype);
         }
         if (w.ydirect < 0) {
             Range r{reorder(w.py.from, Y.labels, lY), reorder(w.py.size, Y.labels, lY)};
@@ -331,8 +367,8 @@ void dist_contraction(const Scalar &alpha, const DistTensor &v0, const Coor &fro
                 l.y = Local{bufs.back().ptr, dev, r.size, lY, dtype};
             }
         } else if (mine) {
-            l.y = Local{Y.ptr[w.ydirect], Y.dev[w.ydirect], Y.ranges[w.rank][w.ydirect].size,
-                        Y.labels, dtype};
+            l.y = sub_view(Y.ptr[w.ydirect], Y.dev[w.ydirect], Y.ranges[w.rank][w.ydirect], w.py,
+                           w.yoff, Y.labels, dtype);
         }
         {
             Range r{reorder(w.pr.from, vr.labels, lR), reorder(w.pr.size, vr.labels, lR)};

@@ -554,7 +554,8 @@ template <typename E, int BI, int BD>
 void launch_ell(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_t s) {
     // two rhs columns per thread (measured against 1 and 4, and 48 KB of LDS per workgroup:
     // 16^4 3x3 n = 12: 46 us vs 51 / 61; n = 64: 191 us vs 218 / 234; one column per thread
-    // over all 256 threads with the x rows of all 9 blocks in flight: 56-60 us)
+    // over all 256 threads with the x rows of all 9 blocks in flight: 56-60 us; non-temporal
+    // loads of the value stream: 50 us)
     launch_ell_g<E, BI, BD, 2>(a, nnz, yrow, xrow, s, ELL_LDS_BYTES);
 }
 

@@ -122,9 +122,10 @@ struct DistTensor {
 struct Local {
     void *ptr;
     int dev;
-    Coor size; // local dims
+    Coor size; // extents of the box (the view)
     std::string labels;
     int dtype;
+    Coor dims; // extents of the dense array the box lies in (empty: the box is the array)
 };
 
 //

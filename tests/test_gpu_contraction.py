@@ -138,3 +138,46 @@ def test_multicomponent_contraction(gpu):
                    False, c1, 1.0, _single(dr), z(dr), dr, dr, "tNSns", cr)
     torch.cuda.synchronize()
     assert rel_err(cr[0].cpu().numpy(), ref) < 1e-10
+
+
+@pytest.mark.parametrize("case", ["tslice", "nslice", "xbox", "twrap", "all_t_in_r"])
+def test_subbox_contraction(gpu, case):
+    """contraction() on boxes smaller than the tensors (from/size): t slices and n slices run
+    in place on views of the components; an x box and a periodic t box that wraps go through
+    temporaries.  Elements of vr outside the box stay untouched."""
+    L, n = 4, 4
+    d0, d1, dr = _lattice(L, n, "tnsxyzc", "tNSxyzc")
+    v0 = random_valued(_vol(d0), np.complex128, 11)
+    v1 = random_valued(_vol(d1), np.complex128, 12)
+    vr = random_valued(_vol(dr), np.complex128, 13)
+    f0, s0 = [0] * 7, list(d0)
+    f1, s1 = [0] * 7, list(d1)
+    fr, sr = [0] * 5, list(dr)
+    if case == "tslice":
+        f0[0] = f1[0] = fr[0] = 1
+        s0[0] = s1[0] = sr[0] = 2
+    elif case == "nslice":
+        f0[1], s0[1] = 1, 2   # n in v0 and vr
+        fr[3], sr[3] = 2, 2   # vr's n (label 3 of tNSns) from 2
+        f1[1], s1[1] = 3, 1   # N in v1 and vr
+        fr[1], sr[1] = 0, 1
+    elif case == "xbox":
+        f0[3] = f1[3] = 1
+        s0[3] = s1[3] = 2
+    elif case == "twrap":
+        f0[0] = f1[0] = fr[0] = 3
+        s0[0] = s1[0] = sr[0] = 2
+    elif case == "all_t_in_r":
+        f0[0] = f1[0] = 1
+        s0[0] = s1[0] = sr[0] = 2
+        fr[0] = 2
+    ref = vr.copy()
+    oracle_contraction(1.5 - 0.5j, "tnsxyzc", f0, s0, d0, False, v0, "tNSxyzc", f1, s1, d1, True,
+                       v1, 0.5, "tNSns", fr, sr, dr, ref)
+    out = _gpu_contraction(gpu, 1.5 - 0.5j, "tnsxyzc", f0, s0, d0, False, v0, "tNSxyzc", f1, s1,
+                           d1, True, v1, 0.5, "tNSns", fr, sr, dr, vr.copy())
+    assert rel_err(out, ref) < 1e-10
+    untouched = np.ones(dr, bool)
+    idx = [np.arange(f, f + s) % d for f, s, d in zip(fr, sr, dr)]
+    untouched[np.ix_(*idx)] = False
+    assert np.array_equal(out.reshape(dr)[untouched], vr.reshape(dr)[untouched])
