@@ -116,8 +116,8 @@ def pmc_traffic(*kernel_substrs):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--L", type=int, default=16)
     ap.add_argument("--n", type=int, default=64)
     ap.add_argument("--no-side", action="store_true", help="skip permute/BSR side measurements")
@@ -173,6 +173,22 @@ def main():
         if world > 1:
             torch.distributed.barrier()
 
+    # side measurements first: they also bring the GPU clocks up before the contraction is timed
+    # (the first ~10 GEMM launches on an idle GPU run ~12 % slower)
+    side = {}
+    if not args.no_side:
+        side.update(permute_bench(sb, dev, L, n))
+        side.update(bsr_bench(sb, dev, L))
+        if world == 1:
+            try:
+                side.update(chain_bench(sb, dev))
+            except Exception as e:  # a side measurement never takes the bench down
+                side["chain_error"] = str(e)[:200]
+    if not args.no_side:
+        # the same contraction with complex products in the 4-multiplication form (the reference
+        # / rocBLAS ZGEMM arithmetic): a comparison point, and ~20 ms of MFMA load right before
+        # the timed region (the clocks ramp over the first ~15 GEMM launches on an idle GPU)
+        side.update(form4m_bench(sb, step, flops_rank_of(L, n)))
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -204,7 +220,7 @@ def main():
     sb.timings_enable(False)
     kernel_s = gemm_ms / max(gemm_calls, 1) / 1e3  # average launch of the MFMA GEMM kernel
 
-    flops_rank = 8.0 * L * (L ** 3 * 3) * (n * 4) ** 2  # 8 * volT * volA * volB * volC
+    flops_rank = flops_rank_of(L, n)
     total_flops = flops_rank * world * args.steps
     value = total_flops / elapsed / 1e9
     # flops of one launch (a step's GEMM is split in T chunks when a cross-rank reduction is
@@ -217,15 +233,6 @@ def main():
     algorithmic = flops_launch / kernel_s / 1e12
     achieved = algorithmic * exec_per_alg
 
-    side = {}
-    if not args.no_side:
-        side.update(permute_bench(sb, dev, L, n))
-        side.update(bsr_bench(sb, dev, L))
-        if world == 1:
-            try:
-                side.update(chain_bench(sb, dev))
-            except Exception as e:  # a side measurement never takes the bench down
-                side["chain_error"] = str(e)[:200]
     base = None
     if rank == 0 and world == 1 and not args.no_cpu:
         base = cpu_baseline(int(os.environ.get("OMP_NUM_THREADS", "16")))
@@ -272,6 +279,7 @@ def main():
                                              "complex MAC; value and algorithmic_TFLOPs count 8)"
                                              if m3 else "4-multiplication form"),
                          "step_TFLOPs": round(flops_rank / step_s / 1e12, 3),
+                         "step_ms_each": [round(x, 3) for x in step_ms],
                          "splitk_reduce_ms_avg": round(red_ms / max(red_calls, 1), 4)},
             "cpu_baseline": base,
         }
@@ -283,6 +291,28 @@ def main():
     if comm is not None:
         comm.close()
         torch.distributed.destroy_process_group()
+
+
+def flops_rank_of(L, n):
+    return 8.0 * L * (L ** 3 * 3) * (n * 4) ** 2  # 8 * volT * volA * volB * volC
+
+
+def form4m_bench(sb, step, flops, reps=15):
+    prev = sb.tune_get("gemm.m3")
+    sb.tune_set("gemm.m3", -1)
+    try:
+        step()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            step()
+        e.record()
+        torch.cuda.synchronize()
+        t = s.elapsed_time(e) / reps
+    finally:
+        sb.tune_set("gemm.m3", prev)
+    return {"contraction_4M_ms": round(t, 4), "contraction_4M_TFLOPs": round(flops / t / 1e9, 2)}
 
 
 def permute_bench(sb, dev, L, n, reps=3):

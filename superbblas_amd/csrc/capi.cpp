@@ -341,6 +341,7 @@ int sbx_tune_set(const char *key, long long value) {
         else if (k == "copy.nt") g_copy_tune.nt = (int)value;
         else if (k == "bsr.variant") g_bsr_tune.variant = (int)value;
         else if (k == "gemm.m3") g_gemm_tune.m3 = (int)value;
+        else if (k == "gemm.splits") g_gemm_tune.splits = (int)value;
         else throw Error("tune_set: unknown key " + k);
     });
 }
@@ -355,6 +356,7 @@ int sbx_tune_get(const char *key, long long *value) {
         else if (k == "copy.nt") *value = g_copy_tune.nt;
         else if (k == "bsr.variant") *value = g_bsr_tune.variant;
         else if (k == "gemm.m3") *value = g_gemm_tune.m3;
+        else if (k == "gemm.splits") *value = g_gemm_tune.splits;
         else throw Error("tune_get: unknown key " + k);
     });
 }

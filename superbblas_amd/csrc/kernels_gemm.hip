@@ -640,6 +640,7 @@ void launch_dma_cfg(const GemmKArgs &p0, int device, hipStream_t stream, long sp
     const bool m3 = CPLX && g_gemm_tune.m3 >= 0;
     GemmKArgs p = p0;
     Scratch work;
+    if (g_gemm_tune.splits > 0) splits = g_gemm_tune.splits;
     const long nwg = prepare_launch<typename Elem<R, CPLX>::type>(p, BM, BN, BKK, splits,
                                                                    target_wgs, work, device);
     {
@@ -681,6 +682,8 @@ void launch_tiled(const GemmKArgs &p, int device, hipStream_t stream) {
         launch_tiled_cfg<R, CPLX, AK, BK, 64, 64, 16, 2, 2>(p, device, stream);
     } else if constexpr (std::is_same<R, double>::value && CPLX) {
         // (16-deep slabs: same time in the 3-multiplication form, 1.68 -> 1.51 ms in the 4-)
+        // split-K to one workgroup per CU (config 2: 4 splits 1.19 ms, 8 / 16 splits 1.20 /
+        // 1.23 ms once the clocks have ramped up, tools/gemm_chunks.py)
         if (p.m >= 128 && p.n >= 128)
             launch_dma_cfg<R, CPLX, AK, BK, 128, 128, 8, 4, 2>(p, device, stream, 0, 256);
         else

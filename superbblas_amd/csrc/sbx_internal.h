@@ -181,6 +181,7 @@ struct CopyTune {
 extern CopyTune g_copy_tune;
 struct GemmTune {
     int m3 = 0; ///< complex GEMMs (LDS-DMA kernel): -1 the 4-multiplication form, else the 3-multiplication form
+    int splits = 0; ///< LDS-DMA kernel split-K factor (0 = the library's choice)
 };
 extern GemmTune g_gemm_tune;
 struct BsrTune {

@@ -28,7 +28,8 @@ def main():
     v1 = torch.randn(vol(d0), dtype=torch.complex128, device=dev)
     vr = torch.zeros(vol(dr), dtype=torch.complex128, device=dev)
     z7, z5 = [0] * 7, [0] * 5
-    for nch in (1, 2, 4):
+    for nch, splits in ((1, 0), (2, 0), (4, 0), (1, 4), (1, 8), (1, 16)):
+        sb.tune_set("gemm.splits", splits)
         tl = L // nch
 
         def f():
@@ -53,7 +54,7 @@ def main():
         ms, calls = sb.timings_get("gemm")
         rms, _ = sb.timings_get("gemm_splitk_reduce")
         sb.timings_enable(False)
-        print(json.dumps({"chunks": nch, "step_ms": round(s.elapsed_time(e) / 10, 4),
+        print(json.dumps({"chunks": nch, "splits": splits, "step_ms": round(s.elapsed_time(e) / 10, 4),
                           "gemm_ms_per_step": round(ms / 10, 4),
                           "reduce_ms_per_step": round(rms / 10, 4)}), flush=True)
 
