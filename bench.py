@@ -184,6 +184,14 @@ def main():
                 side.update(chain_bench(sb, dev))
             except Exception as e:  # a side measurement never takes the bench down
                 side["chain_error"] = str(e)[:200]
+    if not args.no_side and world > 1:
+        # configs[3] "4b": the second operand distributed over t only, so the contraction first
+        # redistributes it to the first operand's xyz partition (an all-to-all over RCCL)
+        try:
+            side.update(redistribution_bench(sb, dev, comm, world, rank, gdim0, p0, v0, v1, pr, vr,
+                                             barrier))
+        except Exception as e:  # a side measurement never takes the bench down
+            side["redistribution_error"] = str(e)[:200]
     if not args.no_side:
         # the same contraction with complex products in the 4-multiplication form (the reference
         # / rocBLAS ZGEMM arithmetic): a comparison point, and ~20 ms of MFMA load right before
@@ -291,6 +299,49 @@ def main():
     if comm is not None:
         comm.close()
         torch.distributed.destroy_process_group()
+
+
+def redistribution_bench(sb, dev, comm, world, rank, gdim0, p0, v0, v1, pr, vr, barrier, reps=5):
+    """configs[3] with redistribution (N > 1): v1 partitioned over t across the ranks (16/N t
+    slices of the whole lattice each) is (a) copied into v0's xyz partition -- the MPI_Alltoallv
+    of the reference's copy_request, here RCCL grouped send/recv -- and (b) contracted with v0
+    as is, which makes the library redistribute it before the GEMMs (dist.h:3150-3159).
+    Bytes moved per rank = the part of v1 that changes owner."""
+    pt = sb.basic_partitioning("tNSxyzc", gdim0, [world, 1, 1, 1, 1, 1, 1], "t", world, 1)
+    v1t = torch.empty(vol(pt[rank][1]), dtype=torch.complex128, device=dev)
+    z7, z5 = [0] * 7, [0] * 5
+    gdimr = [gdim0[0], gdim0[1], 4, gdim0[1], 4]
+    # t-partitioned copy of v1 (itself an all-to-all), then the timed redistribution back
+    sb.copy(1.0, p0, "tNSxyzc", z7, gdim0, gdim0, [v1], pt, "tNSxyzc", z7, gdim0, [v1t], comm=comm)
+    tmp = torch.empty_like(v1)
+
+    def redist():
+        sb.copy(1.0, pt, "tNSxyzc", z7, gdim0, gdim0, [v1t], p0, "tNSxyzc", z7, gdim0, [tmp],
+                comm=comm)
+
+    def contract():
+        sb.contraction(1.0, p0, z7, gdim0, gdim0, "tnsxyzc", False, [v0], pt, z7, gdim0, gdim0,
+                       "tNSxyzc", False, [v1t], 0.0, pr, z5, gdimr, gdimr, "tNSns", [vr],
+                       comm=comm)
+
+    out = {}
+    for name, fn in (("redistribute", redist), ("contraction_redistributed", contract)):
+        fn()
+        torch.cuda.synchronize()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        barrier()
+        out[name + "_ms"] = round((time.perf_counter() - t0) / reps * 1e3, 4)
+    ok = bool(torch.equal(tmp, v1))
+    # bytes this rank receives: its xyz block minus the t slices it already owned
+    moved = 16.0 * vol(p0[rank][1]) * (world - 1) / world
+    out["redistribute_GBps_per_rank"] = round(moved / out["redistribute_ms"] / 1e6, 1)
+    out["redistribute_exact"] = ok
+    del v1t, tmp
+    return out
 
 
 def flops_rank_of(L, n):
