@@ -386,14 +386,13 @@ void dist_contraction(const Scalar &alpha, const DistTensor &v0, const Coor &fro
     bool need_x = false, need_y = false;
     for (auto &rk : tx.ranges) need_x |= !rk.empty();
     for (auto &rk : ty.ranges) need_y |= !rk.empty();
-    if (need_x) dist_copy(Scalar{1, 0}, X, fromX, sizeX, tx, tfromX, false, comm);
-    if (need_y) dist_copy(Scalar{1, 0}, Y, fromY, sizeY, ty, tfromY, false, comm);
 
     const Coor tfromr = reorder(fromr, vr.labels, lR), tsizer = reorder(sizer, vr.labels, lR);
 
-    // 3+4 pipelined: with other ranks in the reduction, split the leading T label into chunks;
-    // chunk c's partial output is reduced into vr (pack, RCCL exchange, Add unpack) on the
-    // side stream while the GEMMs of chunk c+1 run on the main stream
+    // 2+3+4 pipelined: with other ranks in the reduction, split the leading T label into chunks;
+    // on the side stream, the operands of chunk c+1 are redistributed into the temporaries
+    // (all-to-all) and chunk c's partial output is reduced into vr (pack, RCCL exchange, Add
+    // unpack) while the GEMMs of chunk c run on the main stream.
     // The decision uses only information every rank holds (the global work list), so all ranks
     // issue the same sequence of collective copies.
     int nchunks = 1;
@@ -412,13 +411,58 @@ void dist_contraction(const Scalar &alpha, const DistTensor &v0, const Coor &fro
         const int dev = !lw.empty() ? lw[0].r.dev : (comm.device >= 0 ? comm.device : vr.dev.empty() ? 0 : vr.dev[0]);
         const hipStream_t main_s = get_stream(dev), side_s = get_side_stream(dev);
         const long tn = tsizer[0];
+        // operands of the T range [c0, c1) into the temporaries (box restricted along T[0])
+        auto copy_operands = [&](long c0, long c1) {
+            if (need_x) {
+                Coor f = fromX, sz = sizeX, tf = tfromX;
+                const int j = (int)X.labels.find(T[0]);
+                f[j] = normalize_coor((long)f[j] + c0, X.dim[j]);
+                sz[j] = (int)(c1 - c0);
+                tf[0] = normalize_coor((long)tf[0] + c0, tx.dim[0]);
+                dist_copy(Scalar{1, 0}, X, f, sz, tx, tf, false, comm);
+            }
+            if (need_y) {
+                Coor f = fromY, sz = sizeY, tf = tfromY;
+                const int j = (int)Y.labels.find(T[0]);
+                f[j] = normalize_coor((long)f[j] + c0, Y.dim[j]);
+                sz[j] = (int)(c1 - c0);
+                tf[0] = normalize_coor((long)tf[0] + c0, ty.dim[0]);
+                dist_copy(Scalar{1, 0}, Y, f, sz, ty, tf, false, comm);
+            }
+        };
+        auto chunk = [&](int c) { return std::make_pair(tn * c / nchunks, tn * (c + 1) / nchunks); };
+        // event after the side stream's copy of the next chunk's operands
+        hipEvent_t ready = nullptr;
+        auto record_ready = [&]() {
+            SBX_HIP_CHECK(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+            SBX_HIP_CHECK(hipEventRecord(ready, side_s));
+        };
+        stream_after(side_s, main_s);
+        if (need_x || need_y) {
+            StreamOverride so(dev, side_s);
+            copy_operands(chunk(0).first, chunk(0).second);
+            record_ready();
+        }
         for (int c = 0; c < nchunks; ++c) {
-            const long c0 = tn * c / nchunks, c1 = tn * (c + 1) / nchunks;
+            const long c0 = chunk(c).first, c1 = chunk(c).second;
+            if (ready) {
+                SBX_HIP_CHECK(hipStreamWaitEvent(main_s, ready, 0));
+                SBX_HIP_CHECK(hipEventDestroy(ready));
+                ready = nullptr;
+            }
+            if (c1 > c0)
+                for (const LocalWork &l : lw)
+                    local_contraction(alpha, slab(l.x, c0, c1 - c0, es), conjX,
+                                      slab(l.y, c0, c1 - c0, es), conjY, Scalar{0, 0},
+                                      slab(l.r, c0, c1 - c0, es));
+            {
+                StreamOverride so(dev, side_s);
+                if ((need_x || need_y) && c + 1 < nchunks) {
+                    copy_operands(chunk(c + 1).first, chunk(c + 1).second);
+                    record_ready();
+                }
+            }
             if (c1 == c0) continue;
-            for (const LocalWork &l : lw)
-                local_contraction(alpha, slab(l.x, c0, c1 - c0, es), conjX,
-                                  slab(l.y, c0, c1 - c0, es), conjY, Scalar{0, 0},
-                                  slab(l.r, c0, c1 - c0, es));
             stream_after(side_s, main_s);
             {
                 StreamOverride so(dev, side_s);
@@ -433,6 +477,9 @@ void dist_contraction(const Scalar &alpha, const DistTensor &v0, const Coor &fro
         stream_after(main_s, side_s); // join: vr complete, temporaries free in order
         return;
     }
+
+    if (need_x) dist_copy(Scalar{1, 0}, X, fromX, sizeX, tx, tfromX, false, comm);
+    if (need_y) dist_copy(Scalar{1, 0}, Y, fromY, sizeY, ty, tfromY, false, comm);
 
     // 3) local contractions into the partial outputs
     for (const LocalWork &l : lw) local_contraction(alpha, l.x, conjX, l.y, conjY, Scalar{0, 0}, l.r);
