@@ -550,12 +550,140 @@ void launch_ell_g(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_t s
     SBX_HIP_CHECK(hipGetLastError());
 }
 
+// 9-point ELL form of bsr_ell_kernel: each thread reads its block row's 9 block columns straight
+// from global memory into registers and issues the x rows of its first PD blocks before the
+// workgroup streams the values into LDS, so the x gathers, the column reads and the value stream
+// are in flight together (bsr_ell_kernel: value stream, then the columns, then one x block at a
+// time); blocks j+PD are fetched while block j is applied.
+template <typename E, int BI, int BD, int G, int PD, bool YROW, bool XROW>
+__global__ void __launch_bounds__(256) bsr_ell9_kernel(const BsrArgs p, int rb) {
+    constexpr int NNZ = 9, BLK = BI * BD, NB = PD + 1;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    E *vals = (E *)smem;
+    const E *__restrict__ v = (const E *)p.v;
+    const E *__restrict__ x = (const E *)p.x;
+    E *__restrict__ y = (E *)p.y;
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int chunk = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    const long row0 = (long)chunk * rb;
+    const int nrows = (int)min((long)rb, p.block_rows - row0);
+    const long ngroups = (p.ncols + G - 1) / G;
+    const long npairs = (long)nrows * ngroups; // <= 256 (launcher)
+    const long q = threadIdx.x;
+    const bool active = q < npairs;
+    int r;
+    long g;
+    if (YROW) {
+        r = (int)(q / ngroups);
+        g = q % ngroups;
+    } else {
+        r = (int)(q % nrows);
+        g = q / nrows;
+    }
+    if (!active) {
+        r = 0;
+        g = 0;
+    }
+    long colv[G];
+#pragma unroll
+    for (int k = 0; k < G; ++k) colv[k] = min(g * G + k, p.ncols - 1);
+    int dj[NNZ];
+#pragma unroll
+    for (int j = 0; j < NNZ; ++j) dj[j] = p.jj[(row0 + r) * NNZ + j];
+    E xb[NB][BD][G];
+    auto fetch = [&](int d0, E (*xv)[G]) {
+        const long d = d0 < 0 ? 0 : d0;
+#pragma unroll
+        for (int e = 0; e < BD; ++e)
+#pragma unroll
+            for (int k = 0; k < G; ++k)
+                xv[e][k] = XROW ? x[(d + e) * p.ldx + colv[k]] : x[(d + e) + colv[k] * p.ldx];
+    };
+#pragma unroll
+    for (int j = 0; j < PD; ++j) fetch(dj[j], xb[j]);
+    const long vbase = row0 * NNZ * BLK;
+    const int nv = nrows * NNZ * BLK;
+    for (int e0 = threadIdx.x; e0 < nv; e0 += 256 * 8) {
+        E t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] = v[vbase + min(e0 + 256 * u, nv - 1)];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (e0 + 256 * u < nv) vals[e0 + 256 * u] = t[u];
+    }
+    __syncthreads();
+    if (!active) return;
+    E acc[BI][G];
+#pragma unroll
+    for (int c = 0; c < BI; ++c)
+#pragma unroll
+        for (int k = 0; k < G; ++k) acc[c][k] = Ops<E>::zero();
+    const E *vr = vals + r * NNZ * BLK;
+#pragma unroll
+    for (int j = 0; j < NNZ; ++j) {
+        if (j + PD < NNZ) fetch(dj[j + PD], xb[(j + PD) % NB]);
+        if (dj[j] < 0) continue;
+        const E *vb = vr + j * BLK;
+#pragma unroll
+        for (int e = 0; e < BD; ++e)
+#pragma unroll
+            for (int c = 0; c < BI; ++c) {
+                const E a = p.block_im_fast ? vb[c + e * BI] : vb[c * BD + e];
+#pragma unroll
+                for (int k = 0; k < G; ++k)
+                    acc[c][k] = Ops<E>::fma(a, xb[j % NB][e][k], acc[c][k]);
+            }
+    }
+#pragma unroll
+    for (int c = 0; c < BI; ++c) {
+        const long img = (row0 + r) * BI + c;
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            const long col = g * G + k;
+            if (col >= p.ncols) break;
+            E *yp = YROW ? y + img * p.ldy + col : y + img + col * p.ldy;
+            const E out = Ops<E>::scale(acc[c][k], p.alpha_re, p.alpha_im);
+            *yp = p.add ? Ops<E>::add(*yp, out) : out;
+        }
+    }
+}
+
+template <typename E, int BI, int BD, int G, int PD>
+void launch_ell9(const BsrArgs &a, bool yrow, bool xrow, hipStream_t s, long lds_bytes) {
+    const long blk_bytes = 9L * BI * BD * (long)sizeof(E);
+    const long ngroups = (a.ncols + G - 1) / G;
+    if (ngroups > 256) throw Error("bsr: internal ELL9 sizing error");
+    int rb = (int)std::max(1L, lds_bytes / blk_bytes);
+    rb = (int)std::min<long>(rb, std::max(1L, 256 / ngroups));
+    const long blocks = (a.block_rows + rb - 1) / rb;
+    if (blocks >= (1L << 31)) throw Error("bsr: grid too large");
+    const size_t lds = (size_t)rb * blk_bytes;
+    KernelTimer timer("bsr", s);
+    if (yrow && xrow)
+        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, true, true>), dim3(blocks), dim3(256), lds, s, a, rb);
+    else if (yrow && !xrow)
+        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, true, false>), dim3(blocks), dim3(256), lds, s, a, rb);
+    else if (!yrow && xrow)
+        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, false, true>), dim3(blocks), dim3(256), lds, s, a, rb);
+    else
+        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, false, false>), dim3(blocks), dim3(256), lds, s, a, rb);
+    SBX_HIP_CHECK(hipGetLastError());
+}
+
 template <typename E, int BI, int BD>
 void launch_ell(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_t s) {
     // two rhs columns per thread (measured against 1 and 4, and 48 KB of LDS per workgroup:
     // 16^4 3x3 n = 12: 46 us vs 51 / 61; n = 64: 191 us vs 218 / 234; one column per thread
     // over all 256 threads with the x rows of all 9 blocks in flight: 56-60 us; non-temporal
     // loads of the value stream: 50 us)
+    // the 9-point stencils: ell9 with 12 KB of values per workgroup from 8 rhs columns on, else
+    // 24 KB (16^4 3x3: n = 1 30.6 -> 26.5 us, n = 4 33.3 -> 28.1, n = 12 47.3 -> 42.9, n = 64
+    // 190 -> 181-188; at n = 12 6 / 8 / 16 / 24 KB: 72 / 52 / 48 / 45 us; one or four columns
+    // per thread, or the x rows of two blocks ahead: 46-82 us).  The x gathers are the bound:
+    // without them the value stream and y run at 5.5 TB/s (22 us at n = 12).
+    if (nnz == 9 && g_bsr_tune.variant != 1)
+        return launch_ell9<E, BI, BD, 2, 1>(a, yrow, xrow, s, a.ncols >= 8 ? 12288 : 24576);
     launch_ell_g<E, BI, BD, 2>(a, nnz, yrow, xrow, s, ELL_LDS_BYTES);
 }
 

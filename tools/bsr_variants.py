@@ -42,10 +42,13 @@ def op_and_vectors(dims, spin, color, ncols, dtype, dev):
 
 def main():
     dev = torch.device("cuda:0")
-    for name, dims, dtype, spin in (("16^4 cdouble 3x3", (16, 16, 16, 16), torch.complex128, 1),
-                                    ("16^4 cdouble", (16, 16, 16, 16), torch.complex128, 4),
-                                    ("16^3x64 cfloat", (16, 16, 16, 64), torch.complex64, 4)):
-        ncols = 12
+    for name, dims, dtype, spin, ncols in (
+            ("16^4 cdouble 3x3 n=1", (16, 16, 16, 16), torch.complex128, 1, 1),
+            ("16^4 cdouble 3x3 n=4", (16, 16, 16, 16), torch.complex128, 1, 4),
+            ("16^4 cdouble 3x3", (16, 16, 16, 16), torch.complex128, 1, 12),
+            ("16^4 cdouble 3x3 n=64", (16, 16, 16, 16), torch.complex128, 1, 64),
+            ("16^4 cdouble", (16, 16, 16, 16), torch.complex128, 4, 12),
+            ("16^3x64 cfloat", (16, 16, 16, 64), torch.complex64, 4, 12)):
         op, x, y, dimx, V, b = op_and_vectors(dims, spin, 3, ncols, dtype, dev)
         px = [([0] * 8, dimx)]
         es = 16 if dtype == torch.complex128 else 8
@@ -54,7 +57,7 @@ def main():
             sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", px, "pXYZTSCn", [0] * 8, dimx, dimx, [x],
                           0.0, px, "pxyztscn", [0] * 8, dimx, dimx, "p", [y])
         ref = None
-        for var in ((0,) if spin == 1 else (1, 0)):
+        for var in (1, 0):
             sb.tune_set("bsr.variant", var)
             f()
             torch.cuda.synchronize()
