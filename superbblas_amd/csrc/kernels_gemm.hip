@@ -401,7 +401,11 @@ __global__ void __launch_bounds__(WM *WN * 64) gemm_dma_kernel(const GemmKArgs p
 
     const int wm = wave / WN, wn = wave % WN;
     const int frow = wm * WTM + (lane & 15), fcol = wn * WTN + (lane & 15), kq = lane >> 4;
-    const R sa = p.conja ? R(-1) : R(1), sb = p.conjb ? R(-1) : R(1);
+    // conjugation: the imaginary parts' sign bit flipped with an integer xor (no FP64 multiply)
+    typedef typename std::conditional<sizeof(R) == 8, unsigned long long, unsigned>::type U;
+    const U sign = (U)1 << (sizeof(R) * 8 - 1);
+    const U ma = p.conja ? sign : 0, mb = p.conjb ? sign : 0;
+    auto flip = [](R v, U m) { return __builtin_bit_cast(R, __builtin_bit_cast(U, v) ^ m); };
 
     constexpr bool G3 = CPLX && M3;
     acc_t accR[MT][NT], accI[MT][NT], acc3[G3 ? MT : 1][G3 ? NT : 1];
@@ -444,12 +448,12 @@ __global__ void __launch_bounds__(WM *WN * 64) gemm_dma_kernel(const GemmKArgs p
                 R as[MT], bs[NT];
 #pragma unroll
                 for (int i = 0; i < MT; ++i) {
-                    af[i].y *= sa;
+                    af[i].y = flip(af[i].y, ma);
                     as[i] = af[i].x + af[i].y;
                 }
 #pragma unroll
                 for (int j = 0; j < NT; ++j) {
-                    bf[j].y *= sb;
+                    bf[j].y = flip(bf[j].y, mb);
                     bs[j] = bf[j].x + bf[j].y;
                 }
 #pragma unroll
@@ -462,9 +466,9 @@ __global__ void __launch_bounds__(WM *WN * 64) gemm_dma_kernel(const GemmKArgs p
                     }
             } else if constexpr (CPLX) {
 #pragma unroll
-                for (int i = 0; i < MT; ++i) af[i].y *= sa;
+                for (int i = 0; i < MT; ++i) af[i].y = flip(af[i].y, ma);
 #pragma unroll
-                for (int j = 0; j < NT; ++j) bf[j].y *= sb;
+                for (int j = 0; j < NT; ++j) bf[j].y = flip(bf[j].y, mb);
 #pragma unroll
                 for (int i = 0; i < MT; ++i)
 #pragma unroll
