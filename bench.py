@@ -568,7 +568,8 @@ def bsr_bench(sb, dev, L, ncols=12, reps=5):
     tk = bms / max(bcalls, 1) / 1e3
     return {"bsr_GFLOPs": round(flops / t / 1e9, 1), "bsr_GBps": round(bytes_ / t / 1e9, 1),
             "bsr_ncols": ncols, "bsr_ms": round(t * 1e3, 4),
-            "bsr_kernel_GBps": round(bytes_ / tk / 1e9, 1), "bsr_kernel_ms": round(tk * 1e3, 4)}
+            "bsr_kernel_GBps": round(bytes_ / tk / 1e9, 1), "bsr_kernel_ms": round(tk * 1e3, 4),
+            "bsr_kernel_frac_hbm": round(bytes_ / tk / 1e9 / PEAK_HBM_GBPS, 4)}
 
 
 if __name__ == "__main__":
