@@ -185,6 +185,11 @@ def main():
             except Exception as e:  # a side measurement never takes the bench down
                 side["chain_error"] = str(e)[:200]
     if not args.no_side and world > 1:
+        try:
+            side.update(chain_dist_bench(sb, dev, comm, world, rank, grid, barrier))
+        except Exception as e:  # a side measurement never takes the bench down
+            side["chain_dist_error"] = str(e)[:200]
+    if not args.no_side and world > 1:
         # configs[3] "4b": the second operand distributed over t only, so the contraction first
         # redistributes it to the first operand's xyz partition (an all-to-all over RCCL)
         try:
@@ -514,6 +519,117 @@ def chain_bench(sb, dev, Ls=16, Lt=64, ncols=12, reps=3):
             "chain_bsr_TFLOPs": round(fl2 / (times[1] / 1e3) / 1e12, 2),
             "chain_contraction_ms": round(times[2], 3),
             "chain_contraction_TFLOPs": round(fl3 / (times[2] / 1e3) / 1e12, 2)}
+
+
+def chain_dist_bench(sb, dev, comm, world, rank, grid, barrier, Ls=16, Lt=64, ncols=12, reps=3):
+    """configs[4] on N ranks (weak scaling, 16^3 x 64 sites per rank; N = 8: the 32^3 x 64
+    lattice over a 2x2x2 grid), complex<float>: (1) redistribute the propagator from a t
+    partition (source `tnsxyzc`, Lt/N t slices per rank) into the operator's xyz partition
+    `pxyztscn` (all-to-all), (2) apply the 9-point 12x12-block operator, whose domain partition
+    is the image partition plus a one-site halo in x, y, z (halo exchange inside bsr_krylov),
+    (3) contract the result with its conjugate over x, y, z and color into `TSnsN` on rank 0
+    (partial outputs reduced across the ranks).  Stage times are max-over-ranks wall times."""
+    s_, c_ = 4, 3
+    b = s_ * c_
+    cf = torch.complex64
+    G = [Ls * grid[0], Ls * grid[1], Ls * grid[2], Lt]
+    dim = G + [s_, c_]
+    dsrc = [Lt, ncols, s_, G[0], G[1], G[2], c_]
+    psrc = sb.basic_partitioning("tnsxyzc", dsrc, [world, 1, 1, 1, 1, 1, 1], "t", world, 1)
+    dx = [1] + G + [s_, c_, ncols]
+    px = sb.basic_partitioning("pxyztscn", dx, [1] + grid + [1, 1, 1, 1], "xyz", world, 1)
+    src = torch.empty(vol(psrc[rank][1]), dtype=cf, device=dev)
+    src.real.uniform_(-1, 1)
+    src.imag.uniform_(-1, 1)
+    x = torch.empty(vol(px[rank][1]), dtype=cf, device=dev)
+    y = torch.empty_like(x)
+    # operator: image = the rank's xyz block, domain = image + one-site halo in x, y, z
+    pi = sb.basic_partitioning("xyztsc", dim, grid + [1, 1, 1], "xyz", world, 1)
+    pd = []
+    for f, sz in pi:
+        f, sz = list(f), list(sz)
+        for d in range(3):
+            if sz[d] + 2 <= dim[d]:
+                sz[d] += 2
+                f[d] = (f[d] - 1) % dim[d]
+            else:
+                sz[d], f[d] = dim[d], 0
+        pd.append((f, sz))
+    f0, s0 = pi[rank]
+    V = vol(s0[:4])
+    sites = np.array(np.unravel_index(np.arange(V), s0[:4])).T + np.array(f0[:4])
+    gdim = np.array(G)
+    jj = np.zeros((V, 9, 6), np.int32)
+    dfrom = np.array(pd[rank][0][:4])
+    jj[:, 0, :4] = (sites - dfrom) % gdim
+    k = 1
+    for d in range(4):
+        for sg in (-1, 1):
+            c = sites.copy()
+            c[:, d] = (c[:, d] + sg) % gdim[d]
+            jj[:, k, :4] = (c - dfrom) % gdim
+            k += 1
+    vals = torch.empty(V * 9 * b * b, dtype=cf, device=dev)
+    vals.real.uniform_(-1, 1)
+    vals.imag.uniform_(-1, 1)
+    blk = [1, 1, 1, 1, s_, c_]
+    op = sb.create_bsr(pi, dim, pd, dim, blk, blk, False,
+                       [torch.full((V,), 9, dtype=torch.int32, device=dev)],
+                       [torch.from_numpy(jj.reshape(-1)).to(dev)], [vals], comm=comm)
+    del jj, sites
+    dr = [Lt, s_, ncols, s_, ncols]
+    pr = [([0] * 5, dr)] + [([0] * 5, [0] * 5)] * (world - 1)
+    vr = torch.empty(vol(dr) if rank == 0 else 1, dtype=cf, device=dev)
+    z7, z8, z5 = [0] * 7, [0] * 8, [0] * 5
+
+    def stage1():
+        sb.copy(1.0, psrc, "tnsxyzc", z7, dsrc, dsrc, [src], px, "pxyztscn", z8, dx, [x],
+                comm=comm)
+
+    def stage2():
+        sb.bsr_krylov(1.0, op, "XYZTSC", "xyztsc", px, "pxyztscn", z8, dx, dx, [x], 0.0, px,
+                      "pXYZTSCn", z8, dx, dx, "p", [y], comm=comm)
+
+    def stage3():
+        sb.contraction(1.0, px, z8, dx, dx, "pXYZTSCn", True, [y], px, z8, dx, dx, "pXYZTsCN",
+                       False, [y], 0.0, pr, z5, dr, dr, "TSnsN", [vr], comm=comm)
+    stages = (stage1, stage2, stage3)
+    for fn in stages:
+        fn()
+    torch.cuda.synchronize()
+    barrier()
+    times = [0.0, 0.0, 0.0]
+    t_all = time.perf_counter()
+    for _ in range(reps):
+        for i, fn in enumerate(stages):
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            barrier()
+            times[i] += (time.perf_counter() - t0) / reps
+    t_all = (time.perf_counter() - t_all) / reps
+    op.destroy()
+    out = {"chain_dist_workload": "configs[4]: %dx%dx%dx%d lattice over an xyz grid %s, n=%d, "
+                                  "spin 4 x color 3, complex<float>" % (G[0], G[1], G[2], G[3],
+                                                                        grid, ncols),
+           "chain_dist_ms": t_all * 1e3}
+    for i, name in enumerate(("redistribute", "bsr", "contraction")):
+        out["chain_dist_%s_ms" % name] = times[i] * 1e3
+    if world > 1 and dist_available():
+        on_cpu = torch.distributed.get_backend() == "gloo"
+        t = torch.tensor([out[k] for k in sorted(out) if k.endswith("_ms")], dtype=torch.float64,
+                         device="cpu" if on_cpu else dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        for k, v in zip(sorted(k for k in out if k.endswith("_ms")), t.tolist()):
+            out[k] = v
+    for k in list(out):
+        if k.endswith("_ms"):
+            out[k] = round(out[k], 3)
+    return out
+
+
+def dist_available():
+    return torch.distributed.is_available() and torch.distributed.is_initialized()
 
 
 def bsr_bench(sb, dev, L, ncols=12, reps=5):
