@@ -70,15 +70,32 @@ struct Alpha {
     int one; // alpha == 1: no multiplication (bit-exact data movement)
 };
 
-template <typename D> __device__ __forceinline__ D scale(D v, const Alpha &a) { return a.one ? v : (D)(v * (D)a.re); }
+// alpha * v in the SOURCE type, then converted (the reference's copy_n computes alpha * v[i]
+// with alpha of type elem<T>::type and v of the source type T, copy_n.h:147-244): a real source
+// is scaled by the real part of alpha, so a real -> complex copy has a +0 imaginary part; the
+// complex product is formed with separately rounded products (no FMA contraction), as the
+// reference's C-complex multiply on the CPU
+template <typename S> __device__ __forceinline__ S scale(S v, const Alpha &a) {
+    return a.one ? v : (S)(v * (S)a.re);
+}
 template <> __device__ __forceinline__ double2 scale<double2>(double2 v, const Alpha &a) {
+#pragma clang fp contract(off)
     if (a.one) return v;
     return double2{a.re * v.x - a.im * v.y, a.re * v.y + a.im * v.x};
 }
 template <> __device__ __forceinline__ float2 scale<float2>(float2 v, const Alpha &a) {
+#pragma clang fp contract(off)
     if (a.one) return v;
     const float ar = (float)a.re, ai = (float)a.im;
     return float2{ar * v.x - ai * v.y, ar * v.y + ai * v.x};
+}
+template <> __device__ __forceinline__ int scale<int>(int v, const Alpha &a) { return v; }
+template <> __device__ __forceinline__ unsigned long scale<unsigned long>(unsigned long v, const Alpha &a) {
+    return v;
+}
+/// the element written for source value v
+template <typename D, typename S> __device__ __forceinline__ D xform(S v, const Alpha &a) {
+    return conv<D, S>(scale<S>(v, a));
 }
 template <typename D> __device__ __forceinline__ D add(D a, D b) { return a + b; }
 template <> __device__ __forceinline__ double2 add<double2>(double2 a, double2 b) {
@@ -122,7 +139,7 @@ __global__ void __launch_bounds__(256) copy_direct_kernel(const DirectArgs p) {
             so += (long)c * p.sst[i];
             doff += (long)c * p.dst[i];
         }
-        put<ADD, D>(dst + doff, scale<D>(conv<D, S>(src[so]), p.alpha));
+        put<ADD, D>(dst + doff, xform<D, S>(src[so], p.alpha));
     }
 }
 
@@ -147,7 +164,7 @@ __global__ void __launch_bounds__(256) copy_masked_kernel(const DirectArgs p,
             doff += (long)c * p.dst[i];
         }
         if ((smask && smask[so] == 0.f) || (dmask && dmask[doff] == 0.f)) continue;
-        put<ADD, D>(dst + doff, scale<D>(conv<D, S>(src[so]), p.alpha));
+        put<ADD, D>(dst + doff, xform<D, S>(src[so], p.alpha));
     }
 }
 
@@ -157,7 +174,7 @@ __global__ void __launch_bounds__(256) copy_contig_kernel(const S *__restrict__ 
                                                            D *__restrict__ dst, long total,
                                                            Alpha alpha, int nt) {
     for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256L) {
-        const D v = scale<D>(conv<D, S>(src[idx]), alpha);
+        const D v = xform<D, S>(src[idx], alpha);
         if (!ADD && nt)
             store_nt(dst + idx, v);
         else
@@ -254,7 +271,7 @@ __global__ void __launch_bounds__(256) copy_tiled_kernel(const TiledArgs p) {
             // clamped (always valid) address: the loads of the EPT elements are all issued
             // before the first use instead of one branch + wait per element
             const uint32_t uc = ok ? u : 0, vc = ok ? vv : 0, rc = ok ? r : 0;
-            val[q] = conv<D, S>(src[sbase + su[uc] + sv[vc] + rc]);
+            val[q] = xform<D, S>(src[sbase + su[uc] + sv[vc] + rc], p.alpha);
         }
 #pragma unroll
         for (int q = 0; q < EPT; ++q)
@@ -272,7 +289,7 @@ __global__ void __launch_bounds__(256) copy_tiled_kernel(const TiledArgs p) {
             const uint32_t r = rem - vv * p.R;
             if (e < nwrite && vv < nv_t)
                 put<ADD, D>(dst + dbase + du[u] + dv[vv] + r,
-                            scale<D>(tile[vv * ld + u * p.R + r], p.alpha));
+                            tile[vv * ld + u * p.R + r]);
         }
     }
 }
@@ -348,7 +365,7 @@ __global__ void __launch_bounds__(256) copy_tiled3_kernel(const TiledArgs p) {
 #pragma unroll
                 for (int k = 0; k < KR; ++k) {
                     const uint32_t v = vb + step * k;
-                    val[k] = conv<D, S>(src[base + sv[v < nv_t ? v : vb]]);
+                    val[k] = xform<D, S>(src[base + sv[v < nv_t ? v : vb]], p.alpha);
                 }
 #pragma unroll
                 for (int k = 0; k < KR; ++k) {
@@ -370,7 +387,7 @@ __global__ void __launch_bounds__(256) copy_tiled3_kernel(const TiledArgs p) {
             const uint32_t lb = v * ld + r;
             for (uint32_t u = ufirst; u < nu_t; u += step)
             {
-                const D val = scale<D>(tile[lb + u * p.R], p.alpha);
+                const D val = tile[lb + u * p.R];
                 if (!ADD && p.nt)
                     store_nt(dst + base + du[u], val);
                 else

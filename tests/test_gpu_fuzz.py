@@ -1,0 +1,138 @@
+"""Seeded random parity sweep of contraction() and copy() on the GPU against the oracle
+(oracle/oracle.c, pinned to the reference by tests/test_oracle_golden.py).
+
+Every case draws label groups (T batch, A summed, B / C free), extents, label orders, boxes
+(from/size, periodic, possibly wrapping), conjugation, alpha/beta and a split of the operands
+into components, so the planner's in-place / sub-box / temporary paths and the GEMM's stride
+forms are all crossed.  Bars: contraction <= 1e-10 relative (complex<double>, random values) and
+untouched elements outside the output box bit-identical; copy bit-exact (integer-valued data)."""
+import numpy as np
+import pytest
+
+from _common import int_valued, oracle_contraction, oracle_copy, random_valued, rel_err
+
+pytestmark = pytest.mark.gpu
+
+_LETTERS = "abcdefghij"
+
+
+def _vol(d):
+    n = 1
+    for x in d:
+        n *= x
+    return n
+
+
+def _split(sb, gpu, v, labels, dims, rng):
+    """The tensor as 1 or 2 components (split along a random label of extent >= 2)."""
+    import torch
+    cand = [i for i, d in enumerate(dims) if d >= 2]
+    if not cand or rng.random() < 0.5:
+        return [([0] * len(dims), list(dims))], [torch.from_numpy(v.copy()).to(gpu)]
+    i = int(rng.choice(cand))
+    procs = [1] * len(dims)
+    procs[i] = 2
+    p = sb.basic_partitioning(labels, dims, procs, labels[i], 2, 1)
+    full = v.reshape(dims)
+    comps = []
+    for frm, size in p:
+        sl = tuple(slice(f, f + s) for f, s in zip(frm, size))
+        comps.append(torch.from_numpy(np.ascontiguousarray(full[sl]).ravel()).to(gpu))
+    return p, comps
+
+
+def _gather(p, comps, dims, dtype):
+    out = np.zeros(dims, dtype)
+    for (frm, size), t in zip(p, comps):
+        sl = tuple(slice(f, f + s) for f, s in zip(frm, size))
+        out[sl] = t.cpu().numpy().reshape(size)
+    return out.ravel()
+
+
+def _box(rng, dims):
+    frm = [int(rng.integers(0, d)) for d in dims]
+    size = [int(rng.integers(1, d + 1)) if rng.random() < 0.5 else d for d in dims]
+    return frm, size
+
+
+@pytest.mark.parametrize("seed", range(48))
+def test_fuzz_contraction(gpu, seed):
+    import torch
+    import superbblas_amd as sb
+    rng = np.random.default_rng(1000 + seed)
+    counts = [int(rng.integers(0, 3)) for _ in range(4)]  # T, A, B, C
+    if counts[0] + counts[2] + counts[3] == 0:
+        counts[2] = 1
+    letters = list(rng.permutation(list(_LETTERS)))
+    T = "".join(letters[:counts[0]])
+    A = "".join(letters[counts[0]:sum(counts[:2])])
+    B = "".join(letters[sum(counts[:2]):sum(counts[:3])])
+    C = "".join(letters[sum(counts[:3]):sum(counts)])
+    ext = {c: int(rng.integers(1, 5)) for c in T + A + B + C}
+    o0 = "".join(rng.permutation(list(T + A + B)))
+    o1 = "".join(rng.permutation(list(T + A + C)))
+    o_r = "".join(rng.permutation(list(T + B + C)))
+    d0, d1, dr = ([ext[c] for c in o] for o in (o0, o1, o_r))
+    # boxes: shared labels have the same box size; origins differ per tensor
+    bsize = {c: (int(rng.integers(1, ext[c] + 1)) if rng.random() < 0.4 else ext[c]) for c in ext}
+    f0 = [int(rng.integers(0, ext[c])) if bsize[c] < ext[c] or rng.random() < 0.3 else 0 for c in o0]
+    f1 = [int(rng.integers(0, ext[c])) if bsize[c] < ext[c] or rng.random() < 0.3 else 0 for c in o1]
+    fr = [int(rng.integers(0, ext[c])) if bsize[c] < ext[c] or rng.random() < 0.3 else 0 for c in o_r]
+    s0, s1, sr = ([bsize[c] for c in o] for o in (o0, o1, o_r))
+    conj0, conj1 = bool(rng.integers(0, 2)), bool(rng.integers(0, 2))
+    alpha = complex(rng.uniform(-2, 2), rng.uniform(-2, 2))
+    beta = [0.0, 1.0, complex(rng.uniform(-1, 1), rng.uniform(-1, 1))][int(rng.integers(0, 3))]
+    v0 = random_valued(_vol(d0), np.complex128, 3 * seed + 1)
+    v1 = random_valued(_vol(d1), np.complex128, 3 * seed + 2)
+    vr = random_valued(_vol(dr), np.complex128, 3 * seed + 3)
+    ref = vr.copy()
+    oracle_contraction(alpha, o0, f0, s0, d0, conj0, v0, o1, f1, s1, d1, conj1, v1, beta, o_r,
+                       fr, sr, dr, ref)
+    p0, c0 = _split(sb, gpu, v0, o0, d0, rng)
+    p1, c1 = _split(sb, gpu, v1, o1, d1, rng)
+    pr, cr = _split(sb, gpu, vr, o_r, dr, rng)
+    sb.contraction(alpha, p0, f0, s0, d0, o0, conj0, c0, p1, f1, s1, d1, o1, conj1, c1, beta, pr,
+                   fr, sr, dr, o_r, cr)
+    torch.cuda.synchronize()
+    out = _gather(pr, cr, dr, np.complex128)
+    case = (o0, o1, o_r, d0, d1, dr, f0, f1, fr, s0, conj0, conj1, alpha, beta)
+    assert rel_err(out, ref) < 1e-10, case
+    inside = np.zeros(dr, bool)
+    idx = [np.arange(f, f + s) % d for f, s, d in zip(fr, sr, dr)]
+    inside[np.ix_(*idx)] = True
+    assert np.array_equal(out.reshape(dr)[~inside], vr.reshape(dr)[~inside]), case
+
+
+@pytest.mark.parametrize("seed", range(48))
+def test_fuzz_copy(gpu, seed):
+    import torch
+    import superbblas_amd as sb
+    rng = np.random.default_rng(5000 + seed)
+    nd = int(rng.integers(1, 7))
+    labels = "".join(rng.permutation(list(_LETTERS))[:nd])
+    ext = {c: int(rng.integers(1, 6)) for c in labels}
+    o0 = labels
+    o1 = "".join(rng.permutation(list(labels)))
+    d0 = [ext[c] for c in o0]
+    d1 = [ext[c] for c in o1]
+    f0, s0 = _box(rng, d0)
+    f1 = [int(rng.integers(0, d)) for d in d1]
+    t0, t1 = [(np.complex128, np.complex128), (np.complex64, np.complex128),
+              (np.float64, np.float64), (np.float32, np.complex64),
+              (np.int32, np.int32)][int(rng.integers(0, 5))]
+    add = bool(rng.integers(0, 2)) and np.dtype(t1).kind != "i"
+    alpha = 1.0 if np.dtype(t0).kind == "i" else [1.0, 2.0, -0.5][int(rng.integers(0, 3))]
+    v0 = int_valued(_vol(d0), t0, seed) if np.dtype(t0).kind != "i" else \
+        np.arange(_vol(d0), dtype=t0)
+    v1 = int_valued(_vol(d1), t1, seed + 1) if np.dtype(t1).kind != "i" else \
+        -np.arange(_vol(d1), dtype=t1)
+    ref = v1.copy()
+    oracle_copy(alpha, o0, f0, s0, d0, v0, o1, f1, d1, ref, add=add)
+    p0, c0 = _split(sb, gpu, v0, o0, d0, rng)
+    p1, c1 = _split(sb, gpu, v1, o1, d1, rng)
+    sb.copy(alpha, p0, o0, f0, s0, d0, c0, p1, o1, f1, d1, c1,
+            copyadd=sb.Add if add else sb.Copy)
+    torch.cuda.synchronize()
+    out = _gather(p1, c1, d1, t1)
+    assert np.array_equal(out.view(np.uint8), ref.view(np.uint8)), (o0, o1, d0, f0, s0, f1, t0,
+                                                                     t1, add, alpha)
