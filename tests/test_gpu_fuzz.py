@@ -1,11 +1,12 @@
-"""Seeded random parity sweep of contraction() and copy() on the GPU against the oracle
+"""Seeded random parity sweep of contraction(), copy() and bsr_krylov() on the GPU against the oracle
 (oracle/oracle.c, pinned to the reference by tests/test_oracle_golden.py).
 
 Every case draws label groups (T batch, A summed, B / C free), extents, label orders, boxes
 (from/size, periodic, possibly wrapping), conjugation, alpha/beta and a split of the operands
 into components, so the planner's in-place / sub-box / temporary paths and the GEMM's stride
-forms are all crossed.  Bars: contraction <= 1e-10 relative (complex<double>, random values) and
-untouched elements outside the output box bit-identical; copy bit-exact (integer-valued data)."""
+forms are all crossed.  Bars: contraction <= 1e-10 relative (complex<double>, random values;
+1e-12 double, 2e-5 single precision) and untouched elements outside the output box
+bit-identical; copy and BSR bit-exact (integer-valued data)."""
 import numpy as np
 import pytest
 
@@ -57,6 +58,17 @@ def _box(rng, dims):
 
 @pytest.mark.parametrize("seed", range(48))
 def test_fuzz_contraction(gpu, seed):
+    _fuzz_contraction(gpu, seed, np.complex128, 1e-10)
+
+
+@pytest.mark.parametrize("seed", range(12))
+@pytest.mark.parametrize("dtype,tol", [(np.complex64, 2e-5), (np.float64, 1e-12),
+                                       (np.float32, 2e-5)])
+def test_fuzz_contraction_types(gpu, seed, dtype, tol):
+    _fuzz_contraction(gpu, 100 + seed, dtype, tol)
+
+
+def _fuzz_contraction(gpu, seed, dtype, tol):
     import torch
     import superbblas_amd as sb
     rng = np.random.default_rng(1000 + seed)
@@ -80,11 +92,13 @@ def test_fuzz_contraction(gpu, seed):
     fr = [int(rng.integers(0, ext[c])) if bsize[c] < ext[c] or rng.random() < 0.3 else 0 for c in o_r]
     s0, s1, sr = ([bsize[c] for c in o] for o in (o0, o1, o_r))
     conj0, conj1 = bool(rng.integers(0, 2)), bool(rng.integers(0, 2))
-    alpha = complex(rng.uniform(-2, 2), rng.uniform(-2, 2))
-    beta = [0.0, 1.0, complex(rng.uniform(-1, 1), rng.uniform(-1, 1))][int(rng.integers(0, 3))]
-    v0 = random_valued(_vol(d0), np.complex128, 3 * seed + 1)
-    v1 = random_valued(_vol(d1), np.complex128, 3 * seed + 2)
-    vr = random_valued(_vol(dr), np.complex128, 3 * seed + 3)
+    cplx = np.dtype(dtype).kind == "c"
+    alpha = complex(rng.uniform(-2, 2), rng.uniform(-2, 2)) if cplx else float(rng.uniform(-2, 2))
+    beta = [0.0, 1.0, complex(rng.uniform(-1, 1), rng.uniform(-1, 1)) if cplx else
+            float(rng.uniform(-1, 1))][int(rng.integers(0, 3))]
+    v0 = random_valued(_vol(d0), dtype, 3 * seed + 1)
+    v1 = random_valued(_vol(d1), dtype, 3 * seed + 2)
+    vr = random_valued(_vol(dr), dtype, 3 * seed + 3)
     ref = vr.copy()
     oracle_contraction(alpha, o0, f0, s0, d0, conj0, v0, o1, f1, s1, d1, conj1, v1, beta, o_r,
                        fr, sr, dr, ref)
@@ -94,9 +108,9 @@ def test_fuzz_contraction(gpu, seed):
     sb.contraction(alpha, p0, f0, s0, d0, o0, conj0, c0, p1, f1, s1, d1, o1, conj1, c1, beta, pr,
                    fr, sr, dr, o_r, cr)
     torch.cuda.synchronize()
-    out = _gather(pr, cr, dr, np.complex128)
+    out = _gather(pr, cr, dr, dtype)
     case = (o0, o1, o_r, d0, d1, dr, f0, f1, fr, s0, conj0, conj1, alpha, beta)
-    assert rel_err(out, ref) < 1e-10, case
+    assert rel_err(out, ref) < tol, case
     inside = np.zeros(dr, bool)
     idx = [np.arange(f, f + s) % d for f, s, d in zip(fr, sr, dr)]
     inside[np.ix_(*idx)] = True
@@ -136,3 +150,63 @@ def test_fuzz_copy(gpu, seed):
     out = _gather(p1, c1, d1, t1)
     assert np.array_equal(out.view(np.uint8), ref.view(np.uint8)), (o0, o1, d0, f0, s0, f1, t0,
                                                                      t1, add, alpha)
+
+
+@pytest.mark.parametrize("seed", range(32))
+def test_fuzz_bsr(gpu, seed):
+    """bsr_krylov on random stencils: lattice extents 1-4, spin x color blocks (1-4 x 1-3),
+    ragged or constant neighbour counts, either block order, row- or column-major x and y,
+    alpha/beta; integer-valued data, exact against the oracle's builtin loop."""
+    import torch
+    import superbblas_amd as sb
+    from _common import T_CDOUBLE, oracle_bsr
+    rng = np.random.default_rng(9000 + seed)
+    L = [int(rng.integers(1, 5)) for _ in range(4)]
+    spin, color = int(rng.choice([1, 2, 4])), int(rng.integers(1, 4))
+    b = spin * color
+    V = _vol(L)
+    dim = L + [spin, color]
+    sites = np.array(np.unravel_index(np.arange(V), L)).T
+    dirs = [(None, 0)] + [(d, s) for d in range(4) for s in (-1, 1)]
+    ragged = rng.random() < 0.5
+    jj, ii = [], []
+    for st in sites:
+        k = int(rng.integers(0, 10)) if ragged else 9
+        for d, sg in dirs[:k]:
+            c = st.copy()
+            if d is not None:
+                c[d] = (c[d] + sg) % L[d]
+            jj.append(list(c) + [0, 0])
+        ii.append(k)
+    ii = np.array(ii, np.int32)
+    jj = np.array(jj, np.int32).reshape(-1, 6) if jj else np.zeros((0, 6), np.int32)
+    nnz = int(ii.sum())
+    vals = int_valued(nnz * b * b, np.complex128, seed)
+    bif = bool(rng.integers(0, 2))
+    ncols = int(rng.integers(1, 18))
+    x = int_valued(V * b * ncols, np.complex128, seed + 1)
+    y0 = int_valued(V * b * ncols, np.complex128, seed + 2)
+    xrow, yrow = bool(rng.integers(0, 2)), bool(rng.integers(0, 2))
+    alpha = [1.0, 2.0, -1.0 + 1.0j][int(rng.integers(0, 3))]
+    beta = [0.0, 1.0, 0.5][int(rng.integers(0, 3))]
+    ax = np.zeros(V * b * ncols, np.complex128)
+    oracle_bsr(T_CDOUBLE, dim, 0, V, b, b, ii, jj.ravel(), vals, bif, x,
+               ncols if xrow else V * b, xrow, ax, ncols if yrow else V * b, yrow, ncols, 1.0)
+    ref = alpha * ax + beta * y0
+    full = [([0] * 6, dim)]
+    blk = [1, 1, 1, 1, spin, color]
+    op = sb.create_bsr(full, dim, full, dim, blk, blk, bif, [torch.from_numpy(ii).to(gpu)],
+                       [torch.from_numpy(jj.ravel().copy()).to(gpu)],
+                       [torch.from_numpy(vals).to(gpu)])
+    ox = "pXYZTSCn" if xrow else "pnXYZTSC"
+    dx = [1] + L + [spin, color, ncols] if xrow else [1, ncols] + L + [spin, color]
+    oy = "pxyztscn" if yrow else "pnxyztsc"
+    dy = [1] + L + [spin, color, ncols] if yrow else [1, ncols] + L + [spin, color]
+    ty = torch.from_numpy(y0.copy()).to(gpu)
+    sb.bsr_krylov(alpha, op, "xyztsc", "XYZTSC", [([0] * 8, dx)], ox, [0] * 8, dx, dx,
+                  [torch.from_numpy(x).to(gpu)], beta, [([0] * 8, dy)], oy, [0] * 8, dy, dy, "p",
+                  [ty])
+    torch.cuda.synchronize()
+    op.destroy()
+    assert np.array_equal(ty.cpu().numpy(), ref), (L, spin, color, ragged, bif, ncols, xrow, yrow,
+                                                   alpha, beta)
