@@ -17,6 +17,9 @@ Cases (all multi-rank: the exchange, pack/unpack kernels and reductions run for 
   storage -- every rank saves its part of a tensor into one shared S3T file (global and block
             checksums), the file is checked by the S3T restatement, then loaded back into
             another distribution  [storage.h:1198-1385, 2142-2370]
+  fuzz   -- seeded random copies (permutation, wrapping box, Copy/Add, type pairs) and
+            contractions (label groups, orders, boxes, conj, alpha/beta) between random
+            distributions over the ranks (some ranks may own nothing)
 """
 import os
 import sys
@@ -399,6 +402,88 @@ def case_storage(sb, comm, rank, n, dev):
         os.remove(fn)
 
 
+def _rand_partition(sb, rng, labels, dims, n):
+    i = int(rng.integers(0, len(dims)))
+    procs = [1] * len(dims)
+    procs[i] = n
+    return sb.basic_partitioning(labels, dims, procs, labels[i], n, 1)
+
+
+def _nonempty(ts, dev):
+    """A rank that owns no element still passes a valid (1-element) buffer."""
+    return [t if t.numel() else torch.zeros(1, dtype=t.dtype, device=dev) for t in ts]
+
+
+def case_fuzz(sb, comm, rank, n, dev, ncases=12):
+    letters = "abcdefgh"
+    for seed in range(ncases):
+        rng = np.random.default_rng(777 + seed)
+        # copy
+        nd = int(rng.integers(1, 6))
+        o0 = "".join(rng.permutation(list(letters))[:nd])
+        o1 = "".join(rng.permutation(list(o0)))
+        ext = {c: int(rng.integers(1, 6)) for c in o0}
+        d0, d1 = [ext[c] for c in o0], [ext[c] for c in o1]
+        f0 = [int(rng.integers(0, d)) for d in d0]
+        s0 = [int(rng.integers(1, d + 1)) for d in d0]
+        f1 = [int(rng.integers(0, d)) for d in d1]
+        t0, t1 = [(np.complex128, np.complex128), (np.complex64, np.complex128),
+                  (np.float64, np.complex128)][int(rng.integers(0, 3))]
+        add = bool(rng.integers(0, 2))
+        p0 = _rand_partition(sb, rng, o0, d0, n)
+        p1 = _rand_partition(sb, rng, o1, d1, n)
+        g0 = gen("int", vol(d0), seed, t0)
+        g1 = gen("int", vol(d1), seed + 1, t1)
+        v0 = _nonempty(scatter(sb, g0, d0, p0, rank, 1, dev), dev)
+        v1 = _nonempty(scatter(sb, g1, d1, p1, rank, 1, dev), dev)
+        sb.copy(1.0, p0, o0, f0, s0, d0, v0, p1, o1, f1, d1, v1,
+                copyadd=sb.Add if add else sb.Copy, comm=comm)
+        torch.cuda.synchronize()
+        out = gather(np.zeros_like(g1), d1, p1, 1, [v1[0][:vol(p1[rank][1])]])
+        ref = g1.copy()
+        oracle_copy(1.0, o0, f0, s0, d0, g0, o1, f1, d1, ref, add=add)
+        assert np.array_equal(out.view(np.uint8), ref.view(np.uint8)), ("fuzz copy", seed)
+        # contraction
+        cnt = [int(rng.integers(0, 3)) for _ in range(4)]
+        if cnt[0] + cnt[1] + cnt[2] == 0:
+            cnt[2] = 1  # every tensor has a label (a partition needs a dimension)
+        if cnt[0] + cnt[1] + cnt[3] == 0:
+            cnt[3] = 1
+        ls = list(rng.permutation(list(letters)))
+        T, A = "".join(ls[:cnt[0]]), "".join(ls[cnt[0]:sum(cnt[:2])])
+        B, C = "".join(ls[sum(cnt[:2]):sum(cnt[:3])]), "".join(ls[sum(cnt[:3]):sum(cnt)])
+        ext = {c: int(rng.integers(1, 5)) for c in T + A + B + C}
+        o0 = "".join(rng.permutation(list(T + A + B)))
+        o1 = "".join(rng.permutation(list(T + A + C)))
+        o_r = "".join(rng.permutation(list(T + B + C)))
+        d0, d1, dr = ([ext[c] for c in o] for o in (o0, o1, o_r))
+        bs = {c: int(rng.integers(1, ext[c] + 1)) if rng.random() < 0.4 else ext[c] for c in ext}
+        f0 = [int(rng.integers(0, ext[c])) for c in o0]
+        f1 = [int(rng.integers(0, ext[c])) for c in o1]
+        fr = [int(rng.integers(0, ext[c])) for c in o_r]
+        s0, s1, sr = ([bs[c] for c in o] for o in (o0, o1, o_r))
+        alpha = complex(rng.uniform(-1, 1), rng.uniform(-1, 1))
+        beta = [0.0, 1.0, 0.5 - 0.25j][int(rng.integers(0, 3))]
+        conj0, conj1 = bool(rng.integers(0, 2)), bool(rng.integers(0, 2))
+        p0 = _rand_partition(sb, rng, o0, d0, n)
+        p1 = _rand_partition(sb, rng, o1, d1, n)
+        pr = _rand_partition(sb, rng, o_r, dr, n)
+        g0 = gen("int", vol(d0), 10 + seed, np.complex128)
+        g1 = gen("int", vol(d1), 20 + seed, np.complex128)
+        gr = gen("int", vol(dr), 30 + seed, np.complex128)
+        v0 = _nonempty(scatter(sb, g0, d0, p0, rank, 1, dev), dev)
+        v1 = _nonempty(scatter(sb, g1, d1, p1, rank, 1, dev), dev)
+        vr = _nonempty(scatter(sb, gr, dr, pr, rank, 1, dev), dev)
+        sb.contraction(alpha, p0, f0, s0, d0, o0, conj0, v0, p1, f1, s1, d1, o1, conj1, v1, beta,
+                       pr, fr, sr, dr, o_r, vr, comm=comm)
+        torch.cuda.synchronize()
+        out = gather(np.zeros_like(gr), dr, pr, 1, [vr[0][:vol(pr[rank][1])]])
+        ref = gr.copy()
+        oracle_contraction(alpha, o0, f0, s0, d0, conj0, g0, o1, f1, s1, d1, conj1, g1, beta, o_r,
+                           fr, sr, dr, ref)
+        assert rel_err(out, ref) < 1e-10, ("fuzz contraction", seed, o0, o1, o_r, d0, d1, dr)
+
+
 def main():
     dist.init_process_group("gloo")
     rank, n = dist.get_rank(), dist.get_world_size()
@@ -412,7 +497,7 @@ def main():
         comm = sb.Comm.from_torch_distributed(dev_idx)
     else:
         comm = sb.Comm.host_staged(dev_idx)
-    cases = os.environ.get("SBX_TEST_CASES", "copy,contr,bsr,kron,dense,storage").split(",")
+    cases = os.environ.get("SBX_TEST_CASES", "copy,contr,bsr,kron,dense,storage,fuzz").split(",")
     if "copy" in cases:
         case_copy(sb, comm, rank, n, dev)
     if "contr" in cases:
@@ -425,6 +510,8 @@ def main():
         case_dense(sb, comm, rank, n, dev)
     if "storage" in cases:
         case_storage(sb, comm, rank, n, dev)
+    if "fuzz" in cases:
+        case_fuzz(sb, comm, rank, n, dev)
     dist.barrier()
     comm.close()
     dist.destroy_process_group()
