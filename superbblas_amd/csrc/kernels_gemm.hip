@@ -687,7 +687,8 @@ void launch_tiled(const GemmKArgs &p, int device, hipStream_t stream) {
     } else if constexpr (std::is_same<R, double>::value && CPLX) {
         // (16-deep slabs: same time in the 3-multiplication form, 1.68 -> 1.51 ms in the 4-)
         // split-K to one workgroup per CU (config 2: 4 splits 1.19 ms, 8 / 16 splits 1.20 /
-        // 1.23 ms once the clocks have ramped up, tools/gemm_chunks.py)
+        // 1.23 ms once the clocks have ramped up, tools/gemm_chunks.py); 16 waves of 32x32
+        // (125 VGPRs, 4 waves/SIMD) measured 1.19-1.22 ms in the 3M form (8 waves: 1.16-1.18)
         if (p.m >= 128 && p.n >= 128)
             launch_dma_cfg<R, CPLX, AK, BK, 128, 128, 8, 4, 2>(p, device, stream, 0, 256);
         else
