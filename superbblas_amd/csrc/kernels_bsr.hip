@@ -468,6 +468,110 @@ __global__ void __launch_bounds__(256) bsr_mfma_ell_kernel(const BsrArgs p, long
     }
 }
 
+// Contiguous-block form (row-major x with ldx == ncols <= 16, ELL with NNZ blocks per row): the
+// nonzero block A_ij and the x block of its domain rows are each one contiguous run of
+// BI*BD (BD*ncols) elements, so a wave fetches them with lane-linear 16-byte loads (every lane a
+// distinct 16 bytes, 1 KB per instruction) instead of 12-row fragment gathers, stages them in a
+// wave-private LDS slot and reads the MFMA fragments from there.  Block j+1 is fetched into
+// registers while block j is applied.
+template <typename R, bool CPLX, int BI, int BD, bool YROW, int NNZ, int PD>
+__global__ void __launch_bounds__(256) bsr_mfma_blk_kernel(const BsrArgs p) {
+    typedef typename BsrMfmaElem<R, CPLX>::type E;
+    typedef typename BsrMfma<R>::acc_t acc_t;
+    static_assert(BI <= 16 && BD % 4 == 0, "block shape");
+    constexpr int KS = BD / 4;
+    constexpr int EPL = 16 / (int)sizeof(E);            // elements per 16-byte lane load
+    constexpr int ABLK = BI * BD, XBLK = BD * 16;        // staged elements (x: up to 16 cols)
+    constexpr int NA = (ABLK + 64 * EPL - 1) / (64 * EPL), NX = (XBLK + 64 * EPL - 1) / (64 * EPL);
+    typedef __attribute__((ext_vector_type(4))) unsigned u4;
+    __shared__ __attribute__((aligned(16))) E lds[4][ABLK + XBLK];
+    const E *__restrict__ v = (const E *)p.v;
+    const E *__restrict__ x = (const E *)p.x;
+    E *__restrict__ y = (E *)p.y;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const long i = (long)blockIdx.x * 4 + w;
+    if (i >= p.block_rows) return;
+    const int nc = (int)p.ncols, xblk = BD * nc;
+    const long jb = i * NNZ;
+    int dj[NNZ];
+#pragma unroll
+    for (int k = 0; k < NNZ; ++k) dj[k] = p.jj[jb + k];
+    u4 ra[PD][NA], rx[PD][NX];
+    auto fetch = [&](int k, u4 *ra_, u4 *rx_) {
+        const u4 *ap = (const u4 *)(v + (jb + k) * ABLK);
+        const u4 *xp = (const u4 *)(x + (long)(dj[k] < 0 ? 0 : dj[k]) * nc);
+#pragma unroll
+        for (int q = 0; q < NA; ++q) {
+            const int g = lane + 64 * q; // 16-byte granule of the block
+            ra_[q] = g * EPL < ABLK ? ap[g] : u4{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int q = 0; q < NX; ++q) {
+            const int g = lane + 64 * q;
+            rx_[q] = g * EPL < xblk ? xp[g] : u4{0, 0, 0, 0};
+        }
+    };
+    E *const sa = lds[w], *const sx = lds[w] + ABLK;
+    const int ar = lane & 15, kq = lane >> 4;
+    const bool arow_ok = ar < BI, bcol_ok = ar < nc;
+    acc_t accR = acc_t{0, 0, 0, 0}, accI = acc_t{0, 0, 0, 0}, acc3 = acc_t{0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < PD && k < NNZ; ++k) fetch(k, ra[k], rx[k]);
+#pragma unroll
+    for (int k = 0; k < NNZ; ++k) {
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int q = 0; q < NA; ++q)
+            if ((lane + 64 * q) * EPL < ABLK) ((u4 *)sa)[lane + 64 * q] = ra[k % PD][q];
+#pragma unroll
+        for (int q = 0; q < NX; ++q)
+            if ((lane + 64 * q) * EPL < xblk) ((u4 *)sx)[lane + 64 * q] = rx[k % PD][q];
+        __builtin_amdgcn_wave_barrier();
+        if (k + PD < NNZ) fetch(k + PD, ra[k % PD], rx[k % PD]);
+        if (dj[k] < 0) continue;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const int e = ks * 4 + kq;
+            E a = arow_ok ? (p.block_im_fast ? sa[ar + e * BI] : sa[ar * BD + e]) : E{};
+            E b = bcol_ok ? sx[e * nc + ar] : E{};
+            if constexpr (CPLX) {
+                // 3-multiplication form: P1 = ar*br, P2 = ai*bi, P3 = (ar+ai)(br+bi)
+                accR = BsrMfma<R>::mma(a.x, b.x, accR);
+                accI = BsrMfma<R>::mma(a.y, b.y, accI);
+                acc3 = BsrMfma<R>::mma(a.x + a.y, b.x + b.y, acc3);
+            } else {
+                accR = BsrMfma<R>::mma(a, b, accR);
+            }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int row = BsrMfma<R>::row(lane, q);
+        if (row >= BI || !bcol_ok) continue;
+        const long img = i * BI + row;
+        E *yp = YROW ? y + img * p.ldy + ar : y + img + ar * p.ldy;
+        E out;
+        if constexpr (CPLX)
+            out = Ops<E>::scale(E{accR[q] - accI[q], acc3[q] - accR[q] - accI[q]}, p.alpha_re,
+                                p.alpha_im);
+        else
+            out = Ops<E>::scale(accR[q], p.alpha_re, p.alpha_im);
+        *yp = p.add ? Ops<E>::add(*yp, out) : out;
+    }
+}
+
+template <typename R, bool CPLX, int BI, int BD, int NNZ, int PD>
+void launch_bsr_mfma_blk(const BsrArgs &a, bool yrow, hipStream_t s) {
+    const long blocks = (a.block_rows + 3) / 4;
+    if (blocks >= (1L << 31)) throw Error("bsr: grid too large");
+    KernelTimer timer("bsr", s);
+    if (yrow)
+        hipLaunchKernelGGL((bsr_mfma_blk_kernel<R, CPLX, BI, BD, true, NNZ, PD>), dim3(blocks), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL((bsr_mfma_blk_kernel<R, CPLX, BI, BD, false, NNZ, PD>), dim3(blocks), dim3(256), 0, s, a);
+    SBX_HIP_CHECK(hipGetLastError());
+}
+
 template <typename R, bool CPLX, int BI, int BD, int NNZ, int NB>
 void launch_bsr_mfma_ell(const BsrArgs &a, bool yrow, bool xrow, hipStream_t s) {
     const long ntn = (a.ncols + 15) / 16;
@@ -510,8 +614,14 @@ void launch_bsr_mfma(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_
     // 426 -> 350 us; complex<float> 16^3 x 64: 985 -> 797 us); a 3- or 9-block lookahead, the
     // XCD-grouped row order and non-temporal value loads were all measured slower, and
     // non-temporal stores of y no faster
-    if (g_bsr_tune.variant == 0 && nnz == 9) return launch_bsr_mfma_ell<R, CPLX, BI, BD, 9, 1>(a, yrow, xrow, s);
-    if (g_bsr_tune.variant == 0) return launch_bsr_mfma_pf<R, CPLX, BI, BD>(a, yrow, xrow, s);
+    // contiguous x blocks (row-major x, ldx == ncols <= 16): lane-linear block loads staged
+    // through LDS (16^4 complex<double> n = 12: 372 -> 348-355 us; the chain's complex<float>
+    // operator 843-922 -> 722 us; two or three blocks of lookahead: 359-377 / 739-772 us)
+    if (g_bsr_tune.variant != 1 && g_bsr_tune.variant != 2 && nnz == 9 && xrow &&
+        a.ldx == a.ncols && a.ncols <= 16)
+        return launch_bsr_mfma_blk<R, CPLX, BI, BD, 9, 1>(a, yrow, s);
+    if (g_bsr_tune.variant != 1 && nnz == 9) return launch_bsr_mfma_ell<R, CPLX, BI, BD, 9, 1>(a, yrow, xrow, s);
+    if (g_bsr_tune.variant != 1) return launch_bsr_mfma_pf<R, CPLX, BI, BD>(a, yrow, xrow, s);
     const long ntn = (a.ncols + 15) / 16;
     const long waves = (a.block_rows + ROWS - 1) / ROWS * ntn;
     const long blocks = (waves + 3) / 4;

@@ -185,7 +185,7 @@ struct GemmTune {
 };
 extern GemmTune g_gemm_tune;
 struct BsrTune {
-    int variant = 0; ///< ELL kernels (3x3 and 12x12): 0 = the library's choice, 1 = the round-1 kernels
+    int variant = 0; ///< BSR kernels: 0 = the library's choice, 1 = the round-1 kernels, 2 = no 12x12 block-staged kernel
 };
 extern BsrTune g_bsr_tune;
 

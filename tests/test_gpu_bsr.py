@@ -217,3 +217,40 @@ def test_bsr_image_side(gpu, spin, color, ncols, beta, power):
     torch.cuda.synchronize()
     op.destroy()
     assert np.array_equal(ty.cpu().numpy(), yref)
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("ncols,dtype", [(3, np.complex128), (16, np.complex64), (20, np.complex128),
+                                         (5, np.float64)])
+def test_bsr_12x12_kernel_forms(gpu, variant, ncols, dtype):
+    """The 12x12 (spin x color) 9-point operator through every kernel form: the block-staged
+    MFMA kernel (variant 0, row-major x with ncols <= 16), the column-preloading MFMA kernel
+    (variant 2, and variant 0 beyond 16 columns) and the round-1 kernel (variant 1); exact."""
+    import torch
+    import superbblas_amd as sb
+    from _common import TYPE_OF
+    L, spin, color = 4, 4, 3
+    dim, ii, jj, vals, nb = lattice_operator(L, spin, color, dtype)
+    b = spin * color
+    vol = L ** 4
+    g = np.arange(vol * b * ncols)
+    x = ((g % 9 - 4) + (1j * (g % 5 - 2) if np.dtype(dtype).kind == "c" else 0)).astype(dtype)
+    yref = np.zeros(vol * b * ncols, dtype)
+    oracle_bsr(TYPE_OF[np.dtype(dtype)], dim, 0, vol, b, b, ii, jj, vals, False, x, ncols, True,
+               yref, ncols, True, ncols, 1.0)
+    full = [([0] * 6, dim)]
+    blk = [1, 1, 1, 1, spin, color]
+    sb.tune_set("bsr.variant", variant)
+    try:
+        op = sb.create_bsr(full, dim, full, dim, blk, blk, False, [torch.from_numpy(ii).to(gpu)],
+                           [torch.from_numpy(jj).to(gpu)], [torch.from_numpy(vals).to(gpu)])
+        dimx = [1, L, L, L, L, spin, color, ncols]
+        ty = torch.zeros(vol * b * ncols, dtype=getattr(torch, np.dtype(dtype).name), device=gpu)
+        sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", [([0] * 8, dimx)], "pXYZTSCn", [0] * 8, dimx,
+                      dimx, [torch.from_numpy(x).to(gpu)], 0.0, [([0] * 8, dimx)], "pxyztscn",
+                      [0] * 8, dimx, dimx, "p", [ty])
+        torch.cuda.synchronize()
+        op.destroy()
+    finally:
+        sb.tune_set("bsr.variant", 0)
+    assert np.array_equal(ty.cpu().numpy(), yref)

@@ -57,7 +57,7 @@ def main():
             sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", px, "pXYZTSCn", [0] * 8, dimx, dimx, [x],
                           0.0, px, "pxyztscn", [0] * 8, dimx, dimx, "p", [y])
         ref = None
-        for var in (1, 0):
+        for var in ((1, 0) if spin == 1 else (1, 2, 0)):
             sb.tune_set("bsr.variant", var)
             f()
             torch.cuda.synchronize()
