@@ -35,6 +35,8 @@ def lattice_operator(L, spin, color, dtype=np.complex128):
     nnz = vol * nb
     k = np.arange(nnz * b * b, dtype=np.int64)
     vals = ((k * 3 + 1) % 7 - 3) + 1j * ((k * 5 + 2) % 9 - 4)
+    if np.dtype(dtype).kind != "c":
+        vals = vals.real
     return dim, ii, jj, vals.astype(dtype), nb
 
 
