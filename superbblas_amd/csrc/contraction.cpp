@@ -43,6 +43,50 @@ GroupStride group_stride(const std::string &group, const std::string &labels, co
     return g;
 }
 
+/// Labels of `group` (in the given order, size-1 labels ignored) that start a new run of memory
+/// in a box of extents `size` inside an array of extents `dims`: at most one such label lets the
+/// GEMM address the group as two runs (outer index, inner index)
+std::string group_breaks(const std::string &group, const std::string &labels, const Coor &size,
+                         const Coor &dims = Coor()) {
+    const std::vector<long> st = strides_slow_to_fast(dims.empty() ? size : dims);
+    std::string br;
+    int prev = -1;
+    for (char c : group) {
+        auto i = labels.find(c);
+        if (i == std::string::npos) throw Error("contraction: internal label error");
+        if (size[i] == 1) continue;
+        if (prev >= 0 && st[prev] != st[i] * (long)size[i]) br += c;
+        prev = (int)i;
+    }
+    return br;
+}
+
+/// Split form of a group in one tensor: inner run starting at label `brk` (0: one run)
+struct GroupSplit {
+    long vol = 1, lo = 1;   // group volume, inner extent
+    long s = 0, s_hi = 0;   // inner / outer strides
+};
+GroupSplit group_split(const std::string &group, char brk, const std::string &labels,
+                       const Coor &size, const Coor &dims = Coor()) {
+    const std::vector<long> st = strides_slow_to_fast(dims.empty() ? size : dims);
+    GroupSplit g;
+    bool inner = brk == 0;
+    int last = -1, last_outer = -1;
+    for (char c : group) {
+        const auto i = labels.find(c);
+        if (c == brk) inner = true;
+        if (size[i] == 1) continue;
+        g.vol *= size[i];
+        if (inner) g.lo *= size[i];
+        else last_outer = (int)i;
+        last = (int)i;
+    }
+    g.s = last >= 0 ? st[last] : 0;
+    g.s_hi = last_outer >= 0 ? st[last_outer] : g.s * g.lo;
+    if (brk == 0) g.lo = g.vol;
+    return g;
+}
+
 /// Reorder the entries of `c` (labels `from`) into labels `to`
 Coor reorder(const Coor &c, const std::string &from, const std::string &to) {
     Coor r(to.size());
@@ -79,18 +123,36 @@ void local_contraction(const Scalar &alpha, const Local &x, bool conjx, const Lo
     }
     if (r.labels.size() != T.size() + M.size() + N.size())
         throw Error("o_r has unmatched dimensions");
-    const auto gx_t = group_stride(T, x.labels, x.size, x.dims),
-               gx_k = group_stride(K, x.labels, x.size, x.dims),
-               gx_m = group_stride(M, x.labels, x.size, x.dims);
-    const auto gy_t = group_stride(T, y.labels, y.size, y.dims),
-               gy_k = group_stride(K, y.labels, y.size, y.dims),
-               gy_n = group_stride(N, y.labels, y.size, y.dims);
-    const auto gr_t = group_stride(T, r.labels, r.size, r.dims),
-               gr_m = group_stride(M, r.labels, r.size, r.dims),
-               gr_n = group_stride(N, r.labels, r.size, r.dims);
-    if (!(gx_t.ok && gx_k.ok && gx_m.ok && gy_t.ok && gy_k.ok && gy_n.ok && gr_t.ok && gr_m.ok &&
-          gr_n.ok))
-        throw Error("local_contraction: operands need reordering");
+    const auto gx_t = group_stride(T, x.labels, x.size, x.dims);
+    const auto gy_t = group_stride(T, y.labels, y.size, y.dims);
+    const auto gr_t = group_stride(T, r.labels, r.size, r.dims);
+    // M, N and K may each be two runs of memory, split at the same label in every tensor that
+    // holds the group (e.g. the summed xyz and c of pXYZTSCn); T must be one run
+    auto common_break = [](std::initializer_list<std::string> brs, char &brk) {
+        std::string all;
+        for (const std::string &b : brs)
+            for (char c : b)
+                if (all.find(c) == std::string::npos) all += c;
+        if (all.size() > 1) return false;
+        brk = all.empty() ? 0 : all[0];
+        return true;
+    };
+    char bm = 0, bn = 0, bk = 0;
+    const bool groups_ok =
+        gx_t.ok && gy_t.ok && gr_t.ok &&
+        common_break({group_breaks(M, x.labels, x.size, x.dims),
+                      group_breaks(M, r.labels, r.size, r.dims)}, bm) &&
+        common_break({group_breaks(N, y.labels, y.size, y.dims),
+                      group_breaks(N, r.labels, r.size, r.dims)}, bn) &&
+        common_break({group_breaks(K, x.labels, x.size, x.dims),
+                      group_breaks(K, y.labels, y.size, y.dims)}, bk);
+    if (!groups_ok) throw Error("local_contraction: operands need reordering");
+    const GroupSplit gx_k = group_split(K, bk, x.labels, x.size, x.dims),
+                     gx_m = group_split(M, bm, x.labels, x.size, x.dims),
+                     gy_k = group_split(K, bk, y.labels, y.size, y.dims),
+                     gy_n = group_split(N, bn, y.labels, y.size, y.dims),
+                     gr_m = group_split(M, bm, r.labels, r.size, r.dims),
+                     gr_n = group_split(N, bn, r.labels, r.size, r.dims);
     if (gx_t.vol != gy_t.vol || gx_t.vol != gr_t.vol || gx_k.vol != gy_k.vol ||
         gx_m.vol != gr_m.vol || gy_n.vol != gr_n.vol)
         throw Error("some dimension does not match");
@@ -103,21 +165,30 @@ void local_contraction(const Scalar &alpha, const Local &x, bool conjx, const Lo
     d.k = gx_k.vol;
     d.batch = gx_t.vol;
     d.a = x.ptr;
-    d.sa_m = gx_m.stride;
-    d.sa_k = gx_k.stride;
+    d.sa_m = gx_m.s;
+    d.sa_k = gx_k.s;
     d.sa_b = gx_t.stride;
     d.conja = conjx;
     d.b = y.ptr;
-    d.sb_k = gy_k.stride;
-    d.sb_n = gy_n.stride;
+    d.sb_k = gy_k.s;
+    d.sb_n = gy_n.s;
     d.sb_b = gy_t.stride;
     d.conjb = conjy;
     d.c = r.ptr;
-    d.sc_m = gr_m.stride;
-    d.sc_n = gr_n.stride;
+    d.sc_m = gr_m.s;
+    d.sc_n = gr_n.s;
     d.sc_b = gr_t.stride;
     d.alpha = alpha;
     d.beta = beta;
+    d.m_lo = gx_m.lo;
+    d.n_lo = gy_n.lo;
+    d.k_lo = gx_k.lo;
+    d.sa_m_hi = gx_m.s_hi;
+    d.sa_k_hi = gx_k.s_hi;
+    d.sb_k_hi = gy_k.s_hi;
+    d.sb_n_hi = gy_n.s_hi;
+    d.sc_m_hi = gr_m.s_hi;
+    d.sc_n_hi = gr_n.s_hi;
     if (volume(x.size) == 0 || volume(y.size) == 0) d.k = 0;
     launch_gemm(d, x.dev);
 }
@@ -223,12 +294,18 @@ void dist_contraction(const Scalar &alpha, const DistTensor &v0, const Coor &fro
         if (X.labels.find(c) == std::string::npos) N += c;
     const std::string lX = T + M + K, lY = T + N + K, lR = T + N + M; // temporaries' layouts
 
-    // every group of the box `size` inside an array of extents `dims` is one contiguous run
+    // T of the box `size` inside an array of extents `dims` is one contiguous run and the other
+    // groups at most two runs each (the GEMM's split groups)
     auto layout_ok = [&](const std::string &labels, const Coor &size, const Coor &dims,
                          std::initializer_list<const std::string *> groups) {
+        if (!group_stride(T, labels, size, dims).ok) return false;
         for (const std::string *g : groups)
-            if (!group_stride(*g, labels, size, dims).ok) return false;
+            if (g != &T && group_breaks(*g, labels, size, dims).size() > 1) return false;
         return true;
+    };
+    // the split points of a group in two tensors agree (at most one label in their union)
+    auto same_break = [](const std::string &a, const std::string &b) {
+        return a.empty() || b.empty() || a == b;
     };
 
     // Pieces of the work: X's ranges restricted to the box, repetitions removed (dist.h:3001-3028)
@@ -290,6 +367,9 @@ void dist_contraction(const Scalar &alpha, const DistTensor &v0, const Coor &fro
                         const Range &ry = Y.ranges[rk][j];
                         const Coor yo = offset_in(w.py, ry, Y.dim);
                         if (!yo.empty() && layout_ok(Y.labels, w.py.size, ry.size, {&T, &N, &K}) &&
+                            (!w.xdirect ||
+                             same_break(group_breaks(K, X.labels, f.size, rx.size),
+                                        group_breaks(K, Y.labels, w.py.size, ry.size))) &&
                             (comm.nprocs > 1 || rk != comm.rank || Y.dev[j] == X.dev[i])) {
                             w.ydirect = j;
                             w.yoff = yo;
@@ -307,6 +387,10 @@ void dist_contraction(const Scalar &alpha, const DistTensor &v0, const Coor &fro
     if (comm.nprocs == 1 && work.size() == 1 && work[0].xdirect && work[0].ydirect >= 0 &&
         vr.ranges[0].size() == 1 && !offset_in(work[0].pr, vr.ranges[0][0], vr.dim).empty() &&
         layout_ok(vr.labels, work[0].pr.size, vr.ranges[0][0].size, {&T, &N, &M}) &&
+        same_break(group_breaks(M, X.labels, work[0].px.size, X.ranges[0][work[0].comp].size),
+                   group_breaks(M, vr.labels, work[0].pr.size, vr.ranges[0][0].size)) &&
+        same_break(group_breaks(N, Y.labels, work[0].py.size, Y.ranges[0][work[0].ydirect].size),
+                   group_breaks(N, vr.labels, work[0].pr.size, vr.ranges[0][0].size)) &&
         vr.dev[0] == X.dev[work[0].comp]) {
         const WorkPiece &w = work[0];
         const Local lx = sub_view(X.ptr[w.comp], X.dev[w.comp], X.ranges[0][w.comp], w.px, w.xoff,

@@ -94,7 +94,22 @@ struct GemmKArgs {
     void *work;
     int tm, tn;
     unsigned a_bytes, b_bytes; // extent of one batch entry of A / B (buffer descriptor range)
+    // split label groups: index i of M (N, K) is (i / m_lo, i % m_lo) with strides (sa_m_hi,
+    // sa_m), ...; split == 0 when every group is one run (m_lo == m, ...)
+    int split;
+    long m_lo, n_lo, k_lo;
+    long sa_m_hi, sa_k_hi, sb_k_hi, sb_n_hi, sc_m_hi, sc_n_hi;
 };
+
+/// Offset of index i of a split group: (i / lo) * s_hi + (i % lo) * s (i < 2^31)
+__device__ __forceinline__ long split_off(long i, long lo, long s, long s_hi) {
+    const unsigned q = (unsigned)i / (unsigned)lo;
+    return (long)q * s_hi + (long)((unsigned)i - q * (unsigned)lo) * s;
+}
+__device__ __forceinline__ long c_off(const GemmKArgs &p, long gi, long gj) {
+    return p.split ? split_off(gi, p.m_lo, p.sc_m, p.sc_m_hi) + split_off(gj, p.n_lo, p.sc_n, p.sc_n_hi)
+                   : gi * p.sc_m + gj * p.sc_n;
+}
 
 // out = alpha*v (+ beta*old)
 template <typename R>
@@ -169,7 +184,10 @@ __global__ void __launch_bounds__(WM *WN * 64) gemm_kernel(const GemmKArgs p) {
             const int kk = AK ? e % BKK : e / BM;
             const long gi = m0 + row, gk = k0 + kk;
             const bool ok = gi < p.m && gk < k_end;
-            const unsigned off = ok ? (unsigned)((gi * p.sa_m + gk * p.sa_k) * sizeof(E)) : OOB;
+            const long o = p.split ? split_off(gi, p.m_lo, p.sa_m, p.sa_m_hi) +
+                                         split_off(gk, p.k_lo, p.sa_k, p.sa_k_hi)
+                                   : gi * p.sa_m + gk * p.sa_k;
+            const unsigned off = ok ? (unsigned)(o * sizeof(E)) : OOB;
             ra[i] = buf_load<E>(rsA, off);
         }
 #pragma unroll
@@ -179,7 +197,10 @@ __global__ void __launch_bounds__(WM *WN * 64) gemm_kernel(const GemmKArgs p) {
             const int kk = BK ? e % BKK : e / BN;
             const long gj = n0 + col, gk = k0 + kk;
             const bool ok = gj < p.n && gk < k_end;
-            const unsigned off = ok ? (unsigned)((gk * p.sb_k + gj * p.sb_n) * sizeof(E)) : OOB;
+            const long o = p.split ? split_off(gk, p.k_lo, p.sb_k, p.sb_k_hi) +
+                                         split_off(gj, p.n_lo, p.sb_n, p.sb_n_hi)
+                                   : gk * p.sb_k + gj * p.sb_n;
+            const unsigned off = ok ? (unsigned)(o * sizeof(E)) : OOB;
             rb[i] = buf_load<E>(rsB, off);
         }
     };
@@ -268,7 +289,7 @@ __global__ void __launch_bounds__(WM *WN * 64) gemm_kernel(const GemmKArgs p) {
                 const R vr = accR[i][j][r];
                 const R vi = CPLX ? accI[i][j][r] : R(0);
                 if (p.splits == 1) {
-                    R *cptr = (R *)((E *)p.c + bb * p.sc_b + gi * p.sc_m + gj * p.sc_n);
+                    R *cptr = (R *)((E *)p.c + bb * p.sc_b + c_off(p, gi, gj));
                     epilogue_store<R>(cptr, vr, vi, p, CPLX);
                 } else {
                     E *w = (E *)p.work + (((long)split * p.batch + bb) * p.n + gj) * p.m + gi;
@@ -311,7 +332,8 @@ struct DmaOperand {
     // K-major image: granule swizzle so that 16 consecutive rows read at one k hit distinct
     // 16-B bank groups (a 256-B bank row holds 16/GR image rows)
     static __device__ __forceinline__ int swz(int row) { return (row / (16 / GR)) & (GR - 1); }
-    __device__ __forceinline__ void init(int tid, long r0, long nrows, long s_r, long s_k) {
+    __device__ __forceinline__ void init(int tid, long r0, long nrows, long s_r, long s_k,
+                                         bool split = false, long r_lo = 1, long s_r_hi = 0) {
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
             const int slot = tid + NTH * i; // lane-linear granule slot of this lane
@@ -326,16 +348,22 @@ struct DmaOperand {
             const long gr = r0 + r;
             rok[i] = gr < nrows;
             kl[i] = k;
-            roff[i] = (unsigned)(((rok[i] ? gr : 0) * s_r + (long)k * s_k) * ES);
+            // split groups: the row part only; the k part is added per slab in issue()
+            roff[i] = split ? (unsigned)(split_off(rok[i] ? gr : 0, r_lo, s_r, s_r_hi) * ES)
+                            : (unsigned)(((rok[i] ? gr : 0) * s_r + (long)k * s_k) * ES);
         }
     }
     // issue the DMA of slab [k0, k0+BKK) into the image at `lds_base`
     __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, const char *lds_base,
-                                          int wave, long k0, long k_end, long s_k) const {
+                                          int wave, long k0, long k_end, long s_k,
+                                          bool split = false, long k_lo = 1,
+                                          long s_k_hi = 0) const {
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
             const bool ok = rok[i] && (k0 + kl[i] < k_end);
-            const unsigned off = ok ? roff[i] + (unsigned)(k0 * s_k * ES) : 0x80000000u;
+            const unsigned kpart = split ? (unsigned)(split_off(k0 + kl[i], k_lo, s_k, s_k_hi) * ES)
+                                         : (unsigned)(k0 * s_k * ES);
+            const unsigned off = ok ? roff[i] + kpart : 0x80000000u;
             // inline asm so that hipcc does not wait vmcnt(0) before every ds_read of the
             // other buffer (it cannot tell the DMA target from the buffer being read); the
             // kernel retires the DMA itself with an explicit vmcnt(0) before its barrier
@@ -396,8 +424,9 @@ __global__ void __launch_bounds__(WM *WN * 64) gemm_dma_kernel(const GemmKArgs p
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     OpA da;
     OpB db;
-    da.init(tid, m0, p.m, p.sa_m, p.sa_k);
-    db.init(tid, n0, p.n, p.sb_n, p.sb_k);
+    const bool spl = p.split != 0;
+    da.init(tid, m0, p.m, p.sa_m, p.sa_k, spl, p.m_lo, p.sa_m_hi);
+    db.init(tid, n0, p.n, p.sb_n, p.sb_k, spl, p.n_lo, p.sb_n_hi);
 
     const int wm = wave / WN, wn = wave % WN;
     const int frow = wm * WTM + (lane & 15), fcol = wn * WTN + (lane & 15), kq = lane >> 4;
@@ -421,8 +450,8 @@ __global__ void __launch_bounds__(WM *WN * 64) gemm_dma_kernel(const GemmKArgs p
     const long nslab = (k_end - k_begin + BKK - 1) / BKK;
     const char *const base = (const char *)lds;
     if (nslab > 0) {
-        da.issue(rsA, base, wave, k_begin, k_end, p.sa_k);
-        db.issue(rsB, base + BM * BKK * ES, wave, k_begin, k_end, p.sb_k);
+        da.issue(rsA, base, wave, k_begin, k_end, p.sa_k, spl, p.k_lo, p.sa_k_hi);
+        db.issue(rsB, base + BM * BKK * ES, wave, k_begin, k_end, p.sb_k, spl, p.k_lo, p.sb_k_hi);
     }
     for (long s = 0; s < nslab; ++s) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // this wave's DMA of slab s landed
@@ -431,8 +460,8 @@ __global__ void __launch_bounds__(WM *WN * 64) gemm_dma_kernel(const GemmKArgs p
         if (s + 1 < nslab) {
             const char *nb = base + (size_t)(cur ^ 1) * SLAB * ES;
             const long kn = k_begin + (s + 1) * BKK;
-            da.issue(rsA, nb, wave, kn, k_end, p.sa_k);
-            db.issue(rsB, nb + BM * BKK * ES, wave, kn, k_end, p.sb_k);
+            da.issue(rsA, nb, wave, kn, k_end, p.sa_k, spl, p.k_lo, p.sa_k_hi);
+            db.issue(rsB, nb + BM * BKK * ES, wave, kn, k_end, p.sb_k, spl, p.k_lo, p.sb_k_hi);
         }
         const E *As = lds + cur * SLAB;
         const E *Bs = As + BM * BKK;
@@ -510,7 +539,7 @@ __global__ void __launch_bounds__(WM *WN * 64) gemm_dma_kernel(const GemmKArgs p
                     vi = acc3[i][j][r] - p1 - p2;
                 }
                 if (p.splits == 1) {
-                    R *cptr = (R *)((E *)p.c + bb * p.sc_b + gi * p.sc_m + gj * p.sc_n);
+                    R *cptr = (R *)((E *)p.c + bb * p.sc_b + c_off(p, gi, gj));
                     epilogue_store<R>(cptr, vr, vi, p, CPLX);
                 } else {
                     E *w = (E *)p.work + (((long)split * p.batch + bb) * p.n + gj) * p.m + gi;
@@ -544,7 +573,7 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const GemmKArgs p) {
                 sr += w[s * slab];
             }
         }
-        R *cptr = (R *)((E *)p.c + bb * p.sc_b + gi * p.sc_m + gj * p.sc_n);
+        R *cptr = (R *)((E *)p.c + bb * p.sc_b + c_off(p, gi, gj));
         epilogue_store<R>(cptr, sr, si, p, CPLX);
     }
 }
@@ -559,7 +588,7 @@ __global__ void __launch_bounds__(256) scale_c_kernel(const GemmKArgs p) {
         const long gi = idx % p.m;
         const long gj = (idx / p.m) % p.n;
         const long bb = idx / (p.m * p.n);
-        R *cptr = (R *)((E *)p.c + bb * p.sc_b + gi * p.sc_m + gj * p.sc_n);
+        R *cptr = (R *)((E *)p.c + bb * p.sc_b + c_off(p, gi, gj));
         GemmKArgs q = p;
         q.alpha_re = 0;
         q.alpha_im = 0;
@@ -583,12 +612,20 @@ long prepare_launch(GemmKArgs &p, int BM, int BN, int BKK, long splits, long tar
             splits = std::min(splits, max_splits);
         }
     }
-    const long ea = ((p.m - 1) * std::labs(p.sa_m) + (p.k - 1) * std::labs(p.sa_k) + 1) *
-                    (long)sizeof(E);
-    const long eb = ((p.k - 1) * std::labs(p.sb_k) + (p.n - 1) * std::labs(p.sb_n) + 1) *
-                    (long)sizeof(E);
+    // largest element offset of a split (or plain) group index
+    auto ext = [](long n, long lo, long st, long st_hi) {
+        return (n / lo - 1) * std::labs(st_hi) + (lo - 1) * std::labs(st);
+    };
+    const long ea = p.split ? (ext(p.m, p.m_lo, p.sa_m, p.sa_m_hi) +
+                               ext(p.k, p.k_lo, p.sa_k, p.sa_k_hi) + 1) * (long)sizeof(E)
+                            : ((p.m - 1) * std::labs(p.sa_m) + (p.k - 1) * std::labs(p.sa_k) + 1) *
+                                  (long)sizeof(E);
+    const long eb = p.split ? (ext(p.k, p.k_lo, p.sb_k, p.sb_k_hi) +
+                               ext(p.n, p.n_lo, p.sb_n, p.sb_n_hi) + 1) * (long)sizeof(E)
+                            : ((p.k - 1) * std::labs(p.sb_k) + (p.n - 1) * std::labs(p.sb_n) + 1) *
+                                  (long)sizeof(E);
     if (ea >= 0x7fffffffL || eb >= 0x7fffffffL || p.sa_m < 0 || p.sa_k < 0 || p.sb_k < 0 ||
-        p.sb_n < 0)
+        p.sb_n < 0 || p.sa_m_hi < 0 || p.sa_k_hi < 0 || p.sb_k_hi < 0 || p.sb_n_hi < 0)
         throw Error("gemm: operand batch entries of 2 GiB or more are not supported yet");
     p.a_bytes = (unsigned)ea;
     p.b_bytes = (unsigned)eb;
@@ -667,6 +704,12 @@ template <typename E> bool dma_ok(const GemmKArgs &p, bool ak, bool bk) {
     if (EPG == 1) return true;
     auto aligned = [](const void *ptr) { return ((std::uintptr_t)ptr & 15) == 0; };
     if (!aligned(p.a) || !aligned(p.b)) return false;
+    // split groups: the inner extent of the contiguous dimension and every outer stride are
+    // granule multiples (a granule never straddles two runs)
+    if (p.split) {
+        if ((ak ? p.k_lo : p.m_lo) % EPG || (bk ? p.k_lo : p.n_lo) % EPG) return false;
+        if (p.sa_m_hi % EPG || p.sa_k_hi % EPG || p.sb_k_hi % EPG || p.sb_n_hi % EPG) return false;
+    }
     // K-major operand: k extent and the row/batch strides are granule multiples
     if (ak && (p.k % EPG || p.sa_m % EPG || p.sa_b % EPG)) return false;
     if (bk && (p.k % EPG || p.sb_n % EPG || p.sb_b % EPG)) return false;
@@ -751,6 +794,19 @@ GemmKArgs make_args(const GemmDesc &d) {
     p.conjb = d.conjb;
     p.splits = 1;
     p.kchunk = d.k;
+    p.m_lo = d.m_lo > 0 ? d.m_lo : d.m;
+    p.n_lo = d.n_lo > 0 ? d.n_lo : d.n;
+    p.k_lo = d.k_lo > 0 ? d.k_lo : d.k;
+    p.sa_m_hi = d.sa_m_hi;
+    p.sa_k_hi = d.sa_k_hi;
+    p.sb_k_hi = d.sb_k_hi;
+    p.sb_n_hi = d.sb_n_hi;
+    p.sc_m_hi = d.sc_m_hi;
+    p.sc_n_hi = d.sc_n_hi;
+    p.split = (p.m_lo != p.m || p.n_lo != p.n || p.k_lo != p.k) ? 1 : 0;
+    if (p.split && (p.m_lo < 1 || p.n_lo < 1 || p.k_lo < 1 || p.m % p.m_lo || p.n % p.n_lo ||
+                    p.k % p.k_lo))
+        throw Error("gemm: invalid split groups");
     return p;
 }
 

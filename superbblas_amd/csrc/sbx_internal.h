@@ -152,6 +152,11 @@ struct GemmDesc {
     void *c;
     long sc_m, sc_n, sc_b;
     Scalar alpha, beta;
+    // optional split label groups (two runs of memory each): index i of M is (i / m_lo, i % m_lo)
+    // with strides (sa_m_hi, sa_m) in A and (sc_m_hi, sc_m) in C; likewise N and K.  0 (or the
+    // full extent) = one run.
+    long m_lo = 0, n_lo = 0, k_lo = 0;
+    long sa_m_hi = 0, sa_k_hi = 0, sb_k_hi = 0, sb_n_hi = 0, sc_m_hi = 0, sc_n_hi = 0;
 };
 void launch_gemm(const GemmDesc &d, int device);
 

@@ -181,3 +181,47 @@ def test_subbox_contraction(gpu, case):
     idx = [np.arange(f, f + s) % d for f, s, d in zip(fr, sr, dr)]
     untouched[np.ix_(*idx)] = False
     assert np.array_equal(out.reshape(dr)[untouched], vr.reshape(dr)[untouched])
+
+
+@pytest.mark.parametrize("dtype,tol", [(np.complex128, 1e-10), (np.complex64, 2e-5)])
+def test_split_groups_in_place(gpu, dtype, tol):
+    """Label groups that are two runs of memory are contracted in place (no operand reorder):
+    the chain's y^dagger y over x, y, z and color (K = XYZ + C, M = S + n, N = s + N in
+    pXYZTSCn / pXYZTsCN) and the row-major lattice form tsxyzcn x tSxyzcN -> tNSns."""
+    import torch
+    import superbblas_amd as sb
+    L, Lt, nc = 3, 4, 5
+    dx = [1, L, L, L, Lt, 4, 3, nc]
+    y = random_valued(_vol(dx), dtype, 41)
+    dr = [Lt, 4, nc, 4, nc]
+    ref = np.zeros(_vol(dr), dtype)
+    z8, z5 = [0] * 8, [0] * 5
+    oracle_contraction(1.0, "pXYZTSCn", z8, dx, dx, True, y, "pXYZTsCN", z8, dx, dx, False, y, 0.0,
+                       "TSnsN", z5, dr, dr, ref)
+    ty = torch.from_numpy(y).to(gpu)
+    tr = torch.zeros(_vol(dr), dtype=ty.dtype, device=gpu)
+    sb.timings_enable(True)
+    sb.timings_reset()
+    sb.contraction(1.0, _single(dx), z8, dx, dx, "pXYZTSCn", True, [ty], _single(dx), z8, dx, dx,
+                   "pXYZTsCN", False, [ty], 0.0, _single(dr), z5, dr, dr, "TSnsN", [tr])
+    torch.cuda.synchronize()
+    copies = sb.timings_get("copy")[1]
+    sb.timings_enable(False)
+    assert copies == 0, "operands were reordered"
+    assert rel_err(tr.cpu().numpy(), ref) < tol
+    # row-major lattice contraction (dist.cpp:393-415)
+    d0, d1, dr2 = _lattice(4, 3, "tsxyzcn", "tSxyzcN")
+    v0 = random_valued(_vol(d0), dtype, 42)
+    v1 = random_valued(_vol(d1), dtype, 43)
+    ref2 = np.zeros(_vol(dr2), dtype)
+    z7 = [0] * 7
+    oracle_contraction(1.0, "tsxyzcn", z7, d0, d0, False, v0, "tSxyzcN", z7, d1, d1, False, v1,
+                       0.0, "tNSns", z5, dr2, dr2, ref2)
+    sb.timings_enable(True)
+    sb.timings_reset()
+    out = _gpu_contraction(gpu, 1.0, "tsxyzcn", z7, d0, d0, False, v0, "tSxyzcN", z7, d1, d1,
+                           False, v1, 0.0, "tNSns", z5, dr2, dr2, np.zeros(_vol(dr2), dtype))
+    copies = sb.timings_get("copy")[1]
+    sb.timings_enable(False)
+    assert copies == 0, "operands were reordered"
+    assert rel_err(out, ref2) < tol
