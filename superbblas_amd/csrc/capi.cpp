@@ -339,6 +339,8 @@ int sbx_tune_set(const char *key, long long value) {
         else if (k == "copy.run") g_copy_tune.run = (long)value;
         else if (k == "copy.kernel") g_copy_tune.kernel = (int)value;
         else if (k == "copy.nt") g_copy_tune.nt = (int)value;
+        else if (k == "copy.max_elems") g_copy_tune.max_elems = (long)value;
+        else if (k == "gemm.max_bytes") g_gemm_tune.max_bytes = (long)value;
         else if (k == "bsr.variant") g_bsr_tune.variant = (int)value;
         else if (k == "gemm.m3") g_gemm_tune.m3 = (int)value;
         else if (k == "gemm.splits") g_gemm_tune.splits = (int)value;
@@ -354,6 +356,8 @@ int sbx_tune_get(const char *key, long long *value) {
         else if (k == "copy.run") *value = g_copy_tune.run;
         else if (k == "copy.kernel") *value = g_copy_tune.kernel;
         else if (k == "copy.nt") *value = g_copy_tune.nt;
+        else if (k == "copy.max_elems") *value = g_copy_tune.max_elems;
+        else if (k == "gemm.max_bytes") *value = g_gemm_tune.max_bytes;
         else if (k == "bsr.variant") *value = g_bsr_tune.variant;
         else if (k == "gemm.m3") *value = g_gemm_tune.m3;
         else if (k == "gemm.splits") *value = g_gemm_tune.splits;

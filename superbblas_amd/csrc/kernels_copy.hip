@@ -658,6 +658,27 @@ void launch_box_copy(const BoxCopyDesc &d, int device) {
     long total = 1;
     for (long s : d.size) total *= s;
     if (total == 0) return;
+    // boxes beyond the kernels' 32-bit element indexing (2^31 elements and more -- 32 GB of
+    // complex<double> fit in 288 GB of HBM) are copied as slabs of the dimension with the
+    // largest destination stride, each slab a separate launch on shifted base pointers
+    const long max_elems = g_copy_tune.max_elems > 0 ? g_copy_tune.max_elems : (1L << 31) - 1;
+    if (total > max_elems) {
+        int k = -1;
+        for (int i = 0; i < (int)d.size.size(); ++i)
+            if (d.size[i] > 1 && (k < 0 || d.dst_stride[i] > d.dst_stride[k])) k = i;
+        const long inner = total / d.size[k];
+        const long rows = std::max(1L, max_elems / inner);
+        for (long r0 = 0; r0 < d.size[k]; r0 += rows) {
+            BoxCopyDesc c = d;
+            c.size[k] = std::min(rows, d.size[k] - r0);
+            c.src = (const char *)d.src + dtype_size(d.src_t) * r0 * d.src_stride[k];
+            c.dst = (char *)d.dst + dtype_size(d.dst_t) * r0 * d.dst_stride[k];
+            if (d.src_mask) c.src_mask = d.src_mask + r0 * d.src_stride[k];
+            if (d.dst_mask) c.dst_mask = d.dst_mask + r0 * d.dst_stride[k];
+            launch_box_copy(c, device);
+        }
+        return;
+    }
     set_device(device);
     hipStream_t s = get_stream(device);
     const Norm n = normalize(d);

@@ -814,6 +814,82 @@ GemmKArgs make_args(const GemmDesc &d) {
 
 void launch_gemm(const GemmDesc &d, int device) {
     if (d.m == 0 || d.n == 0 || d.batch == 0) return;
+    // operands beyond the 32-bit buffer descriptors (2 GiB per batch entry): cut K (the later
+    // pieces accumulate with beta = 1), or M / N when one K index alone is too large
+    if (d.k > 0 && (d.alpha.re != 0 || d.alpha.im != 0)) {
+        const long es = (long)dtype_size(d.t);
+        const long max_bytes = g_gemm_tune.max_bytes > 0 ? g_gemm_tune.max_bytes : (1L << 31) - 1;
+        auto ext = [&](long n, long lo, long st, long st_hi) {
+            return lo > 0 && lo < n ? (n / lo - 1) * std::labs(st_hi) + (lo - 1) * std::labs(st)
+                                    : (n - 1) * std::labs(st);
+        };
+        const long ea = (ext(d.m, d.m_lo, d.sa_m, d.sa_m_hi) + ext(d.k, d.k_lo, d.sa_k, d.sa_k_hi) + 1) * es;
+        const long eb = (ext(d.k, d.k_lo, d.sb_k, d.sb_k_hi) + ext(d.n, d.n_lo, d.sb_n, d.sb_n_hi) + 1) * es;
+        if (ea > max_bytes || eb > max_bytes) {
+            // cut a group of extent n (inner extent lo, 0 = one run) in two: split groups only
+            // between outer indices; returns the first part's extent and the second's offset
+            // (in elements, per stride pair)
+            struct Cut {
+                long n1, lo1, n2, lo2, o_outer;
+                bool ok;
+            };
+            auto cut = [](long n, long lo) {
+                Cut c{};
+                const bool spl = lo > 0 && lo < n;
+                if (spl) {
+                    const long outer = n / lo, o1 = outer / 2;
+                    c = Cut{o1 * lo, lo, n - o1 * lo, lo, o1, true};
+                } else {
+                    c = Cut{n / 2, 0, n - n / 2, 0, n / 2, n > 1};
+                }
+                return c;
+            };
+            // element offset of the second part for one operand's strides
+            auto off = [](long n, long lo, long st, long st_hi, long o) {
+                return lo > 0 && lo < n ? o * st_hi : o * st;
+            };
+            const Cut ck = cut(d.k, d.k_lo);
+            if (ck.ok) {
+                GemmDesc a = d, b = d;
+                a.k = ck.n1;
+                a.k_lo = ck.lo1;
+                b.k = ck.n2;
+                b.k_lo = ck.lo2;
+                b.a = (const char *)d.a + es * off(d.k, d.k_lo, d.sa_k, d.sa_k_hi, ck.o_outer);
+                b.b = (const char *)d.b + es * off(d.k, d.k_lo, d.sb_k, d.sb_k_hi, ck.o_outer);
+                b.beta = Scalar{1, 0};
+                launch_gemm(a, device);
+                launch_gemm(b, device);
+                return;
+            }
+            const Cut cm = cut(d.m, d.m_lo), cn = cut(d.n, d.n_lo);
+            if (cm.ok && (ea > max_bytes || !cn.ok)) {
+                GemmDesc a = d, b = d;
+                a.m = cm.n1;
+                a.m_lo = cm.lo1;
+                b.m = cm.n2;
+                b.m_lo = cm.lo2;
+                b.a = (const char *)d.a + es * off(d.m, d.m_lo, d.sa_m, d.sa_m_hi, cm.o_outer);
+                b.c = (char *)d.c + es * off(d.m, d.m_lo, d.sc_m, d.sc_m_hi, cm.o_outer);
+                launch_gemm(a, device);
+                launch_gemm(b, device);
+                return;
+            }
+            if (cn.ok) {
+                GemmDesc a = d, b = d;
+                a.n = cn.n1;
+                a.n_lo = cn.lo1;
+                b.n = cn.n2;
+                b.n_lo = cn.lo2;
+                b.b = (const char *)d.b + es * off(d.n, d.n_lo, d.sb_n, d.sb_n_hi, cn.o_outer);
+                b.c = (char *)d.c + es * off(d.n, d.n_lo, d.sc_n, d.sc_n_hi, cn.o_outer);
+                launch_gemm(a, device);
+                launch_gemm(b, device);
+                return;
+            }
+            throw Error("gemm: operand batch entries of 2 GiB or more are not supported");
+        }
+    }
     set_device(device);
     hipStream_t s = get_stream(device);
     GemmKArgs p = make_args(d);

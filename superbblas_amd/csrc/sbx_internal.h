@@ -182,11 +182,13 @@ struct CopyTune {
     long run = 0;    ///< target elements of a tile row's contiguous source run
     int kernel = 0;  ///< 1: the round-1 tiled kernel (element-indexed phases) instead of the row-mapped one
     int nt = 0;      ///< row-mapped kernel stores: 0 = non-temporal for large outputs, 1 = always, -1 = never
+    long max_elems = 0; ///< elements per launch before a box is cut into slabs (0 = 2^31 - 1)
 };
 extern CopyTune g_copy_tune;
 struct GemmTune {
     int m3 = 0; ///< complex GEMMs (LDS-DMA kernel): -1 the 4-multiplication form, else the 3-multiplication form
     int splits = 0; ///< LDS-DMA kernel split-K factor (0 = the library's choice)
+    long max_bytes = 0; ///< operand bytes per batch entry before a GEMM is cut (0 = 2^31 - 1)
 };
 extern GemmTune g_gemm_tune;
 struct BsrTune {

@@ -210,3 +210,19 @@ def test_fuzz_bsr(gpu, seed):
     op.destroy()
     assert np.array_equal(ty.cpu().numpy(), ref), (L, spin, color, ragged, bif, ncols, xrow, yrow,
                                                    alpha, beta)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_fuzz_oversize_paths(gpu, seed):
+    """The paths for operands beyond 32-bit indexing (copies cut into slabs of the outermost
+    destination dimension, GEMMs cut along K / M / N with beta = 1 accumulation), exercised by
+    lowering their thresholds (sbx_tune_set copy.max_elems / gemm.max_bytes) on small cases."""
+    import superbblas_amd as sb
+    sb.tune_set("copy.max_elems", 37)
+    sb.tune_set("gemm.max_bytes", 3000)
+    try:
+        test_fuzz_copy(gpu, seed)
+        _fuzz_contraction(gpu, 200 + seed, np.complex128, 1e-10)
+    finally:
+        sb.tune_set("copy.max_elems", 0)
+        sb.tune_set("gemm.max_bytes", 0)
