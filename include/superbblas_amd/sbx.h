@@ -107,7 +107,7 @@ int sbx_timings_report(char *buf, int len);
 /* ---- tuning hook (no reference counterpart) ----
    Override a kernel-shape choice of the library for tuning runs; value 0 restores the default.
    Keys: "copy.budget", "copy.run", "copy.kernel", "copy.nt", "bsr.variant", "gemm.m3",
-   "gemm.splits". */
+   "gemm.splits", "copy.max_elems", "gemm.max_bytes". */
 int sbx_tune_set(const char *key, long long value);
 int sbx_tune_get(const char *key, long long *value);
 
