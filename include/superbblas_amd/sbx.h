@@ -99,6 +99,9 @@ int sbx_cache_usage(int device, unsigned long long *cached, unsigned long long *
    bracketed by HIP events on the stream it is launched on; totals are summed on query. */
 int sbx_timings_enable(int on);
 int sbx_timings_reset(void);
+/* time only these kernel families ("gemm,copy"; NULL or "" = all): each timed launch adds two
+   event records to its stream */
+int sbx_timings_filter(const char *names);
 /* total milliseconds and launch count of one kernel family (synchronizes its events) */
 int sbx_timings_get(const char *name, double *ms, long long *calls);
 /* "name calls total_ms" per line into buf (truncated to len-1 chars) */

@@ -260,6 +260,11 @@ def timings_reset():
     _check(_lib.sbx_timings_reset())
 
 
+def timings_filter(names: Optional[str] = None):
+    """Time only these kernel families (comma-separated; None = all)."""
+    _check(_lib.sbx_timings_filter(names.encode() if names else None))
+
+
 def tune_set(key: str, value: int):
     """Override a kernel-shape choice for tuning runs (sbx_tune_set; 0 restores the default)."""
     _check(_lib.sbx_tune_set(key.encode(), ctypes.c_longlong(value)))

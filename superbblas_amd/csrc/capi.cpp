@@ -369,6 +369,10 @@ int sbx_timings_enable(int on) {
     return guard([&] { timings_enable(on != 0); });
 }
 
+int sbx_timings_filter(const char *names) {
+    return guard([&] { timings_filter(names && *names ? names : nullptr); });
+}
+
 int sbx_timings_reset(void) {
     return guard([&] { timings_reset(); });
 }

@@ -320,6 +320,7 @@ int pointer_device(const void *p) {
 namespace {
 struct TimerState {
     bool on = false;
+    std::string only; // comma-separated kernel families to time (empty: all)
     struct Pending {
         std::string name;
         hipEvent_t a, b;
@@ -374,8 +375,15 @@ std::string timings_report() {
              std::to_string(e.second.first) + "\n";
     return r;
 }
+void timings_filter(const char *names) {
+    std::lock_guard<std::mutex> g(g_timer_mutex);
+    timers().only = names ? std::string(",") + names + "," : std::string();
+}
 KernelTimer::KernelTimer(const char *n, hipStream_t s) : name(n), stream(s) {
     if (!timers().on) return;
+    // each timed launch adds two event records to the stream (~4 us of stream time each)
+    if (!timers().only.empty() && timers().only.find(std::string(",") + n + ",") == std::string::npos)
+        return;
     hipEvent_t a;
     SBX_HIP_CHECK(hipEventCreate(&a));
     SBX_HIP_CHECK(hipEventRecord(a, s));

@@ -123,6 +123,8 @@ void timings_reset();
 void timings_get(const char *name, double *ms, long long *calls);
 /// "name calls total_ms" lines of every timed family
 std::string timings_report();
+/// Time only the named kernel families (comma-separated; null or empty: all)
+void timings_filter(const char *names);
 struct KernelTimer {
     const char *name;
     hipStream_t stream;
