@@ -1,20 +1,25 @@
 #!/usr/bin/env python3
 """Benchmark: lattice contraction GFLOP/s (+ permute GB/s) -- BASELINE.json metric.
 
-Workload (N = 1): BASELINE.json configs[1], the 16^4 lattice spin x color contraction
+Workload (N = 1, default): BASELINE.json configs[1], the 16^4 lattice spin x color contraction
   v0 `tnsxyzc` {16,64,4,16,16,16,3} x v1 `tNSxyzc` -> vr `tNSns` {16,64,4,64,4},
   complex<double>, through superbblas_amd.contraction (the drop-in C-ABI).  One step = one
   contraction call (= one strided batched complex GEMM m = n = 256, k = 12288, batch 16 on MFMA,
   1.031e11 flop).  Inputs are resident in HBM before the timed region.
-N > 1 (one process per GPU, RCCL): weak scaling -- every rank owns a 16^4 block of a lattice of
-  16*px x 16*py x 16*pz x 16 sites (xyz grid 2x1x1 / 2x2x1 / 2x2x2), the contraction sums over
-  xyz so each rank runs the same local GEMM and the partial tNSns outputs are reduced into rank
-  0's output through the library's remap communicator (RCCL over xGMI).
-Side measurements on the same run (reported as extra fields): the dist.cpp permute
-  xyztsc -> tnsxyzc (64 slices, GB/s) and the 16^4 3x3-block BSR SpMM (config 3).
-cpu_baseline: the real reference (oracle/_ref/ref_bench: header-only superbblas + OpenBLAS,
-  OpenMP over the batch) timed on this box's host cores on a bounded sample (the 16^4, n = 16
-  contraction), or the oracle restatement when the reference build is absent.
+N > 1 (one process per GPU, RCCL; --config 4a, the default): configs[3], STRONG scaling -- one
+  32^4, n = 64 problem (1.649e12 flop per step) split over an xyzt grid 2x1x1x1 / 2x2x1x1 /
+  2x2x2x1; xyz is summed, so every rank runs its local batched GEMM and the partial tNSns outputs
+  are reduced into rank 0's output through the library's remap communicator (RCCL over xGMI),
+  pipelined over t chunks behind the GEMMs.  value = global flops / max-over-ranks time; rank 0
+  then runs the same global problem alone (strong_scaling_vs_1gpu).  --config 4b: v1 split over
+  t only, redistributed by an all-to-all inside the contraction.
+Side measurements (extra fields): N = 1 -- the dist.cpp permute xyztsc -> tnsxyzc (64 slices),
+  the 16^4 3x3-block BSR SpMM at n = 1 / 12 / 64 (config 3), the configs[4] chain on one GPU's
+  share, the opt-in 3M complex form; N > 1 -- the configs[4] chain over the ranks, the 4b
+  redistribution.
+cpu_baseline: the real reference (oracle/_ref/ref_bench[_mkl]: header-only superbblas compiled
+  here, linked with the image's OpenBLAS or MKL) timed on this box's host cores at configs[1]'s
+  exact shape; the oracle restatement when the reference build is absent.
 """
 import argparse
 import json
@@ -47,21 +52,77 @@ def fill(t, seed):
     t.copy_(torch.view_as_complex(r))
 
 
-def cpu_baseline(threads):
-    """Time the reference CPU path on a bounded sample."""
-    exe = os.path.join(ROOT, "oracle", "_ref", "ref_bench")
-    env = dict(os.environ, OMP_NUM_THREADS=str(threads), OPENBLAS_NUM_THREADS="1")
-    if os.path.exists(exe):
-        try:
-            out = subprocess.run([exe, "contraction", "16", "16", "3"], env=env, timeout=300,
-                                 capture_output=True, text=True, check=True).stdout
-            r = json.loads(out.strip().splitlines()[-1])
-            return {"value": round(r["gflops"], 2), "unit": "GFLOP/s", "cores": r["threads"],
-                    "kind": "reference",
-                    "sample": "superbblas::contraction tnsxyzc x tNSxyzc -> tNSns, 16^4, n=16, "
-                              "complex<double>, 3 reps (OpenMP over t, OpenBLAS zgemm per t)"}
-        except Exception as e:  # pragma: no cover
-            print("cpu_baseline: reference run failed: %s" % e, file=sys.stderr)
+def host_cpu():
+    """Host cores this process may use (its affinity mask, capped by OMP_NUM_THREADS when the box
+    sets one), the machine's logical CPU count and the CPU model."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        avail = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    threads = min(avail, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else avail
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:  # pragma: no cover
+        pass
+    return {"threads": threads, "affinity_cpus": avail, "nproc": os.cpu_count(), "model": model}
+
+
+REF_EXES = (("openblas", "ref_bench"), ("mkl", "ref_bench_mkl"))
+
+
+def run_ref(args, threads, blas):
+    """One run of the reference's CPU path (oracle/_ref, the real superbblas headers compiled here)
+    with `threads` OpenMP threads; returns its JSON line or None."""
+    exe = os.path.join(ROOT, "oracle", "_ref", dict(REF_EXES)[blas])
+    if not os.path.exists(exe):
+        return None
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads), OPENBLAS_NUM_THREADS="1",
+               MKL_NUM_THREADS="1")
+    try:
+        out = subprocess.run([exe] + [str(a) for a in args], env=env, timeout=300,
+                             capture_output=True, text=True, check=True).stdout
+        return json.loads(out.strip().splitlines()[-1])
+    except Exception as e:  # pragma: no cover
+        print("cpu baseline: %s %s failed: %s" % (blas, args, e), file=sys.stderr)
+        return None
+
+
+def best_ref(args, thread_counts, key):
+    """The reference's best configuration over the BLAS libraries of the image and thread counts
+    (higher `key` is better); returns (best run, {"blas/threads": value})."""
+    best, tried = None, {}
+    for blas, _ in REF_EXES:
+        for t in thread_counts:
+            r = run_ref(args, t, blas)
+            if r is None:
+                continue
+            tried["%s/%d" % (blas, t)] = round(r[key], 3)
+            if best is None or r[key] > best[key]:
+                best = dict(r, blas=blas)
+    return best, tried
+
+
+def cpu_baseline():
+    """The reference's CPU contraction at configs[1]'s exact shape (16^4, n = 64, complex<double>;
+    OpenMP over t with one zgemm per t, blas_cpu_tmpl.hpp:468-476) on this box's host cores,
+    with the faster of the image's two BLAS libraries; the oracle restatement when the reference
+    build is absent."""
+    cpu = host_cpu()
+    best, tried = best_ref(["contraction", 16, 64, 2], [cpu["threads"]], "gflops")
+    if best is not None:
+        return {"value": round(best["gflops"], 2), "unit": "GFLOP/s", "cores": best["threads"],
+                "kind": "reference",
+                "sample": "superbblas::contraction tnsxyzc x tNSxyzc -> tNSns, 16^4, n=64, "
+                          "complex<double>, 2 timed reps after 1 warm-up (OpenMP over t, one "
+                          "zgemm per t; BLAS %s)" % best["blas"],
+                "blas_tried_GFLOPs": tried, "cpu_model": cpu["model"], "nproc": cpu["nproc"],
+                "affinity_cpus": cpu["affinity_cpus"]}
     # restatement (oracle/oracle.c) on a small sample
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from _common import oracle_gemm, random_valued
@@ -73,27 +134,32 @@ def cpu_baseline(threads):
     t = time.perf_counter()
     oracle_gemm("T", "N", m, n, k, 1.0, a, k, m * k, bb, k, n * k, 0.0, c, m, m * n, b)
     t = time.perf_counter() - t
-    return {"value": round(8.0 * m * n * k * b / t / 1e9, 2), "unit": "GFLOP/s", "cores": threads,
-            "kind": "port", "sample": "oracle xgemm_batch_strided 'T','N' 64x64x1536 batch 8"}
+    return {"value": round(8.0 * m * n * k * b / t / 1e9, 2), "unit": "GFLOP/s",
+            "cores": cpu["threads"], "kind": "port",
+            "sample": "oracle xgemm_batch_strided 'T','N' 64x64x1536 batch 8",
+            "cpu_model": cpu["model"], "nproc": cpu["nproc"]}
 
 
-def cpu_side_baselines(threads):
-    """The reference's CPU path for the side measurements (permute config 2p, BSR config 3),
-    bounded samples of the same workloads, timed beside the GPU numbers (rank 0, N = 1)."""
-    exe = os.path.join(ROOT, "oracle", "_ref", "ref_bench")
-    if not os.path.exists(exe):
-        return {}
-    env = dict(os.environ, OMP_NUM_THREADS=str(threads), OPENBLAS_NUM_THREADS="1")
-    out = {}
-    for key, args in (("permute", ["permute", "16", "64", "1"]), ("bsr", ["bsr", "16", "12", "2"])):
-        try:
-            r = subprocess.run([exe] + args, env=env, timeout=300, capture_output=True, text=True,
-                               check=True).stdout
-            r = json.loads(r.strip().splitlines()[-1])
-            out["%s_cpu_reference_GBps" % key] = round(r["gbps"], 3)
-        except Exception as e:  # pragma: no cover
-            out["%s_cpu_reference_error" % key] = str(e)[:200]
-    out["cpu_reference_threads"] = threads
+def cpu_side_baselines():
+    """The reference's CPU path for the side measurements (permute config 2p; BSR config 3 at
+    n = 1, 12, 64), timed beside the GPU numbers (rank 0, N = 1).  The BSR builtin loop issues
+    one tiny zgemm (zgemv at n = 1) per nonzero block (bsr.h:535-650): both BLAS libraries of the
+    image lose time to per-call overhead and get SLOWER with more threads at n = 12 (OpenBLAS
+    serialises concurrent calls on its buffer lock), so every (BLAS, threads in {1, all}) pair is
+    timed and the best is reported."""
+    cpu = host_cpu()
+    threads = sorted({1, cpu["threads"]})
+    out = {"cpu_reference_threads": cpu["threads"], "cpu_model": cpu["model"]}
+    best, tried = best_ref(["permute", 16, 64, 1], [cpu["threads"]], "gbps")
+    if best is not None:
+        out["permute_cpu_reference_GBps"] = round(best["gbps"], 3)
+    for ncols in (1, 12, 64):
+        best, tried = best_ref(["bsr", 16, ncols, 2], threads, "gbps")
+        if best is not None:
+            out["bsr_n%d_cpu_reference_GBps" % ncols] = round(best["gbps"], 3)
+            out["bsr_n%d_cpu_reference_best" % ncols] = "%s/%d threads" % (best["blas"],
+                                                                           best["threads"])
+            out["bsr_n%d_cpu_reference_tried_GBps" % ncols] = tried
     return out
 
 
@@ -113,23 +179,38 @@ def pmc_traffic(*kernel_substrs):
     return None, None
 
 
+# lattice grids of configs[3] (x, y, z, t split factors)
+GRIDS = {1: [1, 1, 1, 1], 2: [2, 1, 1, 1], 4: [2, 2, 1, 1], 8: [2, 2, 2, 1]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--L", type=int, default=16)
+    ap.add_argument("--config", choices=["1", "4a", "4b"], default=None,
+                    help="1: configs[1] (16^4 on one GPU, the default at N = 1); 4a: configs[3], "
+                         "the 32^4 problem over an xyz grid (the default at N > 1); 4b: the same "
+                         "with the second operand over t only (redistributed)")
+    ap.add_argument("--L", type=int, default=None)
     ap.add_argument("--n", type=int, default=64)
-    ap.add_argument("--no-side", action="store_true", help="skip permute/BSR side measurements")
+    ap.add_argument("--no-side", action="store_true", help="skip the side measurements")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
-    ap.add_argument("--share-gpu", action="store_true",
+    ap.add_argument("--no-1gpu", action="store_true",
+                    help="N > 1: skip the same global problem on rank 0's GPU alone")
+    ap.add_argument("--share-gpu", choices=["host", "rccl"], nargs="?", const="host", default=None,
                     help="rehearsal of the N>1 path on a box with fewer GPUs than ranks: ranks "
-                         "share GPUs, gloo process group, host-staged exchanges (not a bench)")
+                         "share GPUs; 'host': host-staged exchanges over gloo, 'rccl': RCCL "
+                         "with one host id per rank (socket transport) -- not a bench")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.share_gpu == "rccl":
+        os.environ["NCCL_HOSTID"] = "sbx-bench-rank-%d" % rank
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("NCCL_IB_DISABLE", "1")
     if args.share_gpu:
         local_rank %= torch.cuda.device_count()
     torch.cuda.set_device(local_rank)
@@ -141,31 +222,37 @@ def main():
         import torch.distributed as dist
         if args.share_gpu:
             dist.init_process_group("gloo")
-            comm = sb.Comm.host_staged(local_rank)
+            comm = (sb.Comm.host_staged(local_rank) if args.share_gpu == "host"
+                    else sb.Comm.from_torch_distributed(local_rank))
         else:
             dist.init_process_group("nccl", device_id=dev)
             comm = sb.Comm.from_torch_distributed(local_rank)
 
-    L, n = args.L, args.n
-    grid = {1: [1, 1, 1], 2: [2, 1, 1], 4: [2, 2, 1], 8: [2, 2, 2]}.get(world)
+    config = args.config or ("1" if world == 1 else "4a")
+    if config == "1" and world > 1:
+        raise SystemExit("configs[1] is the single-GPU workload; use --config 4a/4b at N > 1")
+    grid = GRIDS.get(world)
     if grid is None:
         raise SystemExit("unsupported --gpus %d" % world)
-    # global lattice (weak scaling over x, y, z)
-    gdim0 = [L, n, 4, L * grid[0], L * grid[1], L * grid[2], 3]  # tnsxyzc
+    L = args.L or (16 if config == "1" else 32)
+    n = args.n
+    # one global problem (strong scaling), split over the lattice grid
+    gdim0 = [L, n, 4, L, L, L, 3]  # tnsxyzc
     gdimr = [L, n, 4, n, 4]  # tNSns
-    procs = [1, 1, 1] + grid + [1]
-    p0 = sb.basic_partitioning("tnsxyzc", gdim0, procs, "xyz", world, 1)
+    procs = [grid[3], 1, 1, grid[0], grid[1], grid[2], 1]
+    p0 = sb.basic_partitioning("tnsxyzc", gdim0, procs, "xyzt", world, 1)
+    p1 = p0 if config != "4b" else sb.basic_partitioning("tNSxyzc", gdim0,
+                                                         [world, 1, 1, 1, 1, 1, 1], "t", world, 1)
     pr = [([0] * 5, gdimr)] + [([0] * 5, [0] * 5)] * (world - 1)  # output on rank 0
-    local0 = p0[rank][1]
-    v0 = torch.empty(vol(local0), dtype=torch.complex128, device=dev)
-    v1 = torch.empty(vol(local0), dtype=torch.complex128, device=dev)
-    vr = torch.zeros(vol(pr[rank][1]) if rank == 0 else 1, dtype=torch.complex128, device=dev)
+    v0 = torch.empty(vol(p0[rank][1]), dtype=torch.complex128, device=dev)
+    v1 = torch.empty(vol(p1[rank][1]), dtype=torch.complex128, device=dev)
+    vr = torch.zeros(vol(gdimr) if rank == 0 else 1, dtype=torch.complex128, device=dev)
     fill(v0, 1 + rank)
     fill(v1, 101 + rank)
     z7, z5 = [0] * 7, [0] * 5
 
     def step():
-        sb.contraction(1.0, p0, z7, gdim0, gdim0, "tnsxyzc", False, [v0], p0, z7, gdim0, gdim0,
+        sb.contraction(1.0, p0, z7, gdim0, gdim0, "tnsxyzc", False, [v0], p1, z7, gdim0, gdim0,
                        "tNSxyzc", False, [v1], 0.0, pr, z5, gdimr, gdimr, "tNSns", [vr],
                        comm=comm)
 
@@ -176,32 +263,32 @@ def main():
     # side measurements first: they also bring the GPU clocks up before the contraction is timed
     # (the first ~10 GEMM launches on an idle GPU run ~12 % slower)
     side = {}
-    if not args.no_side:
-        side.update(permute_bench(sb, dev, L, n))
-        side.update(bsr_bench(sb, dev, L))
-        if world == 1:
-            try:
-                side.update(chain_bench(sb, dev))
-            except Exception as e:  # a side measurement never takes the bench down
-                side["chain_error"] = str(e)[:200]
+    if not args.no_side and world == 1:
+        side.update(permute_bench(sb, dev, 16, 64))
+        side.update(bsr_bench(sb, dev, 16))
+        try:
+            side.update(chain_bench(sb, dev))
+        except Exception as e:  # a side measurement never takes the bench down
+            side["chain_error"] = str(e)[:200]
     if not args.no_side and world > 1:
         try:
-            side.update(chain_dist_bench(sb, dev, comm, world, rank, grid, barrier))
+            side.update(chain_dist_bench(sb, dev, comm, world, rank, grid[:3], barrier))
         except Exception as e:  # a side measurement never takes the bench down
             side["chain_dist_error"] = str(e)[:200]
-    if not args.no_side and world > 1:
-        # configs[3] "4b": the second operand distributed over t only, so the contraction first
-        # redistributes it to the first operand's xyz partition (an all-to-all over RCCL)
+    if not args.no_side and world > 1 and config == "4a":
+        # configs[3] "4b" beside the 4a headline: v1 over t only, (a) its all-to-all
+        # redistribution alone, (b) the contraction that pipelines it behind the GEMMs
         try:
-            side.update(redistribution_bench(sb, dev, comm, world, rank, gdim0, p0, v0, v1, pr, vr,
-                                             barrier))
+            side.update(redistribution_bench(sb, dev, comm, world, rank, gdim0, p0, v0, v1, pr,
+                                             vr, barrier))
         except Exception as e:  # a side measurement never takes the bench down
             side["redistribution_error"] = str(e)[:200]
-    if not args.no_side:
-        # the same contraction with complex products in the 4-multiplication form (the reference
-        # / rocBLAS ZGEMM arithmetic): a comparison point, and ~20 ms of MFMA load right before
-        # the timed region (the clocks ramp over the first ~15 GEMM launches on an idle GPU)
-        side.update(form4m_bench(sb, step, flops_rank_of(L, n)))
+    flops_step = flops_of(L, n)
+    if not args.no_side and world == 1:
+        # the same contraction with complex products in the opt-in 3-multiplication form: a
+        # comparison point (not the headline: only a normwise error bound), and ~20 ms of MFMA
+        # load right before the timed region
+        side.update(form3m_bench(sb, step, flops_step))
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -209,7 +296,7 @@ def main():
     torch.cuda.synchronize()
     # kernel timers: HIP events around every launch on the library's (= torch's current) stream
     sb.timings_enable(True)
-    sb.timings_filter("gemm")  # only the dominant kernel: every timed launch adds two events
+    sb.timings_filter("gemm,gemm_splitk_reduce")  # the dominant kernel and its split-K reduce
     sb.timings_reset()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
@@ -228,34 +315,59 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     step_ms = [a.elapsed_time(b) for a, b in ev]
-    step_s = float(np.mean(step_ms)) / 1e3
     gemm_ms, gemm_calls = sb.timings_get("gemm")
     red_ms, red_calls = sb.timings_get("gemm_splitk_reduce")
     sb.timings_enable(False)
     sb.timings_filter(None)
-    kernel_s = gemm_ms / max(gemm_calls, 1) / 1e3  # average launch of the MFMA GEMM kernel
+    # one GEMM = the MFMA kernel launch + its split-K reduce (the reduce is part of the GEMM)
+    kernel_s = (gemm_ms + red_ms) / max(gemm_calls, 1) / 1e3
 
-    flops_rank = flops_rank_of(L, n)
-    total_flops = flops_rank * world * args.steps
-    value = total_flops / elapsed / 1e9
-    # flops of one launch (a step's GEMM is split in T chunks when a cross-rank reduction is
-    # pipelined behind it) / the launch's average duration
-    flops_launch = flops_rank * args.steps / max(gemm_calls, 1)
-    # executed MFMA flops: complex products in the 3-multiplication (Gauss) form issue 3 real
-    # multiply-adds per complex MAC (6 flops), the 4-multiplication form 4 (8 flops)
-    m3 = sb.tune_get("gemm.m3") >= 0
+    value = flops_step * args.steps / elapsed / 1e9  # whole-job: global flops / max-rank time
+    # this rank's flops per GEMM launch (a step's GEMM is cut in T chunks when a cross-rank
+    # reduction is pipelined behind it) / the launch's average duration
+    local_flops = flops_step * vol(p0[rank][1]) / vol(gdim0)
+    flops_launch = local_flops * args.steps / max(gemm_calls, 1)
+    # executed MFMA flops: the 4-multiplication form (default) issues 4 real multiply-adds per
+    # complex MAC (8 flops); the opt-in 3-multiplication form 3 (6 flops)
+    m3 = sb.tune_get("gemm.m3") > 0
     exec_per_alg = 6.0 / 8.0 if m3 else 1.0
     algorithmic = flops_launch / kernel_s / 1e12
     achieved = algorithmic * exec_per_alg
 
+    # strong scaling: the same global problem on rank 0's GPU alone (outside the timed region)
+    scaling_fields = {}
+    if world > 1 and not args.no_1gpu:
+        barrier()
+        if rank == 0:
+            try:
+                t1 = single_gpu_time(sb, dev, gdim0, gdimr)
+                scaling_fields = {"value_1gpu_same_problem": round(flops_step / t1 / 1e9, 2),
+                                  "ms_per_step_1gpu": round(t1 * 1e3, 4),
+                                  "strong_scaling_vs_1gpu": round(t1 / (elapsed / args.steps), 3)}
+            except Exception as e:  # pragma: no cover
+                scaling_fields = {"single_gpu_error": str(e)[:200]}
+        barrier()
+
     base = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        base = cpu_baseline(int(os.environ.get("OMP_NUM_THREADS", "16")))
-        if world == 1 and not args.no_side:
-            side.update(cpu_side_baselines(int(os.environ.get("OMP_NUM_THREADS", "16"))))
+        base = cpu_baseline()
+        if not args.no_side:
+            side.update(cpu_side_baselines())
 
-    traffic, traffic_src = pmc_traffic("dma_kernel<", "128, 128, 8, 4, 2")
+    traffic, traffic_src = pmc_traffic("dma_kernel<", "128, 128, 16, 4, 2")
     if rank == 0:
+        if config == "1":
+            workload = ("configs[1]: 16^4 lattice spin x color contraction tnsxyzc x tNSxyzc -> "
+                        "tNSns, n=64, complex<double>")
+        else:
+            workload = ("configs[3] %s: %d^4 lattice contraction tnsxyzc x tNSxyzc -> tNSns, n=%d, "
+                        "complex<double>, one global problem, v0 split x%d y%d z%d t%d, v1 %s, "
+                        "output on rank 0 (partial outputs reduced over %s)"
+                        % (config, L, n, grid[0], grid[1], grid[2], grid[3],
+                           "the same" if config == "4a" else "split over t (redistributed to "
+                           "v0's partition by an all-to-all)",
+                           "RCCL" if not args.share_gpu or args.share_gpu == "rccl" else
+                           "host staging"))
         line = {
             "metric": "lattice contraction GFLOP/s + permute GB/s, 16^4 spin×color, 1/2/4/8 GPUs",
             "value": round(value, 2),
@@ -265,47 +377,78 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if world > 1 else "weak",
             "vs_baseline": None,
             "dtype": "complex<f64>",
             "data": "synthetic (uniform [-1,1) complex, seeded)",
-            "config": {"workload": "configs[1]: 16^4 lattice spin x color contraction "
-                                   "tnsxyzc x tNSxyzc -> tNSns, n=64, complex<double>"
-                                   + ("" if world == 1 else
-                                      "; weak scaling, xyz grid %s, 16^4 sites per GPU, "
-                                      "partial outputs reduced to rank 0 over RCCL" % grid),
-                       "L": L, "n": n, "gemm": "T,N m=n=%d k=%d batch=%d" % (4 * n, L ** 3 * 3, L),
-                       "parallelism": "xyz domain decomposition" if world > 1 else "single GPU"},
+            "config": {"workload": workload, "L": L, "n": n,
+                       "gemm": "T,N m=n=%d k=%d batch=%d per rank" % (
+                           4 * n, vol(p0[rank][1][3:]), p0[rank][1][0]),
+                       "parallelism": ("xyzt grid %s" % "x".join(map(str, grid))
+                                       if world > 1 else "single GPU")},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 3),
                          "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_FP64_TFLOPS, 4),
                          "traffic": traffic, "traffic_unit": "bytes per launch",
                          "traffic_source": traffic_src,
-                         "algorithmic_bytes": 16.0 * (2 * vol(local0) + vol(gdimr)),
-                         "kernel": "gemm_dma_kernel<complex<double>, 128x128x8, 8 waves> (FP64 MFMA "
-                                   "16x16x4, complex %s), %d launches, %.4f ms avg "
-                                   "(HIP events on its launch stream)" % ("3M" if m3 else "4M",
-                                                                          gemm_calls,
-                                                                          kernel_s * 1e3),
+                         "algorithmic_bytes": 16.0 * (vol(p0[rank][1]) + vol(p1[rank][1]) +
+                                                      vol(gdimr)),
+                         "kernel": "gemm_dma_kernel<complex<double>, 128x128x%d, 8 waves> (FP64 "
+                                   "MFMA 16x16x4, complex %s) + split-K reduce, %d launches, %.4f "
+                                   "ms avg (HIP events on its launch stream)" % (
+                                       8 if m3 else 16, "3M" if m3 else "4M", gemm_calls,
+                                       kernel_s * 1e3),
                          "flops_per_launch": flops_launch,
                          "executed_flops_per_launch": flops_launch * exec_per_alg,
                          "algorithmic_TFLOPs": round(algorithmic, 3),
                          "complex_product": ("3-multiplication form (6 executed real flops per "
                                              "complex MAC; value and algorithmic_TFLOPs count 8)"
-                                             if m3 else "4-multiplication form"),
-                         "step_TFLOPs": round(flops_rank / step_s / 1e12, 3),
+                                             if m3 else "4-multiplication form (BLAS rounding)"),
+                         "step_TFLOPs": round(flops_step / (float(np.mean(step_ms)) / 1e3) / 1e12,
+                                              3),
                          "step_ms_each": [round(x, 3) for x in step_ms],
+                         "gemm_ms_avg": round(gemm_ms / max(gemm_calls, 1), 4),
                          "splitk_reduce_ms_avg": round(red_ms / red_calls, 4) if red_calls else None},
             "cpu_baseline": base,
         }
+        line.update(scaling_fields)
         line.update(side)
         if args.share_gpu:
-            line["rehearsal"] = ("ranks shared %d GPU(s) with host-staged exchanges: a test of the "
-                                 "N>1 path, not a measurement" % torch.cuda.device_count())
-        print(json.dumps(line))
+            line["rehearsal"] = ("ranks shared %d GPU(s) (%s exchanges): a test of the N>1 path, "
+                                 "not a measurement" % (torch.cuda.device_count(),
+                                                        args.share_gpu))
+        print(json.dumps(line), flush=True)
     if comm is not None:
         comm.close()
         torch.distributed.destroy_process_group()
+
+
+def single_gpu_time(sb, dev, gdim0, gdimr, reps=3):
+    """The global contraction on this GPU alone (one component per tensor): the denominator of
+    the strong-scaling figure, timed with HIP events on torch's current stream."""
+    a = torch.empty(vol(gdim0), dtype=torch.complex128, device=dev)
+    b = torch.empty_like(a)
+    fill(a, 11)
+    fill(b, 12)
+    c = torch.empty(vol(gdimr), dtype=torch.complex128, device=dev)
+    z7, z5 = [0] * 7, [0] * 5
+    q0, qr = [(z7, gdim0)], [(z5, gdimr)]
+
+    def run():
+        sb.contraction(1.0, q0, z7, gdim0, gdim0, "tnsxyzc", False, [a], q0, z7, gdim0, gdim0,
+                       "tNSxyzc", False, [b], 0.0, qr, z5, gdimr, gdimr, "tNSns", [c])
+    run()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        run()
+    e.record()
+    torch.cuda.synchronize()
+    t = s.elapsed_time(e) / 1e3 / reps
+    del a, b, c
+    torch.cuda.empty_cache()
+    return t
 
 
 def redistribution_bench(sb, dev, comm, world, rank, gdim0, p0, v0, v1, pr, vr, barrier, reps=5):
@@ -351,13 +494,13 @@ def redistribution_bench(sb, dev, comm, world, rank, gdim0, p0, v0, v1, pr, vr, 
     return out
 
 
-def flops_rank_of(L, n):
+def flops_of(L, n):
     return 8.0 * L * (L ** 3 * 3) * (n * 4) ** 2  # 8 * volT * volA * volB * volC
 
 
-def form4m_bench(sb, step, flops, reps=15):
+def form3m_bench(sb, step, flops, reps=15):
     prev = sb.tune_get("gemm.m3")
-    sb.tune_set("gemm.m3", -1)
+    sb.tune_set("gemm.m3", 1)
     try:
         step()
         torch.cuda.synchronize()
@@ -370,7 +513,7 @@ def form4m_bench(sb, step, flops, reps=15):
         t = s.elapsed_time(e) / reps
     finally:
         sb.tune_set("gemm.m3", prev)
-    return {"contraction_4M_ms": round(t, 4), "contraction_4M_TFLOPs": round(flops / t / 1e9, 2)}
+    return {"contraction_3M_ms": round(t, 4), "contraction_3M_TFLOPs": round(flops / t / 1e9, 2)}
 
 
 def permute_bench(sb, dev, L, n, reps=3):
@@ -507,6 +650,11 @@ def chain_bench(sb, dev, Ls=16, Lt=64, ncols=12, reps=3):
         for i in range(3):
             times[i] += ev[i].elapsed_time(ev[i + 1]) / reps
     op.destroy()
+    # full-size property check of the chain's result: vr[T,S,n,s,N] = sum conj(y[..S..n]) y[..s..N]
+    # is Hermitian under (S n) <-> (s N)
+    h = vr.view(Lt, s_ * ncols, s_ * ncols)
+    herm = (torch.linalg.vector_norm(h - h.conj().transpose(1, 2)) /
+            torch.linalg.vector_norm(h)).item()
     by1 = 16.0 * vol(dsrc)
     by2 = 8.0 * (9 * b * b * V + 2 * b * V * ncols) + 4.0 * (10 * V + 1)
     fl2 = 8.0 * 9 * b * b * V * ncols
@@ -520,7 +668,8 @@ def chain_bench(sb, dev, Ls=16, Lt=64, ncols=12, reps=3):
             "chain_bsr_GBps": round(by2 / (times[1] / 1e3) / 1e9, 1),
             "chain_bsr_TFLOPs": round(fl2 / (times[1] / 1e3) / 1e12, 2),
             "chain_contraction_ms": round(times[2], 3),
-            "chain_contraction_TFLOPs": round(fl3 / (times[2] / 1e3) / 1e12, 2)}
+            "chain_contraction_TFLOPs": round(fl3 / (times[2] / 1e3) / 1e12, 2),
+            "chain_hermitian_rel_err": herm}
 
 
 def chain_dist_bench(sb, dev, comm, world, rank, grid, barrier, Ls=16, Lt=64, ncols=12, reps=3):
@@ -634,8 +783,10 @@ def dist_available():
     return torch.distributed.is_available() and torch.distributed.is_initialized()
 
 
-def bsr_bench(sb, dev, L, ncols=12, reps=5):
-    """config 3: 16^4 periodic 9-point stencil, 3x3 blocks, complex<double>."""
+def bsr_bench(sb, dev, L, ncols_list=(1, 12, 64), reps=5):
+    """config 3: 16^4 periodic 9-point stencil, 3x3 blocks, complex<double>, n = 1 / 12 / 64 rhs.
+    Kernel time from the library's HIP-event timers on the launch stream; algorithmic bytes
+    16 (81 V + 2 3 V n) + 4 (9 V + V + 1) per application."""
     dim = [L, L, L, L, 1, 3]
     V = L ** 4
     sites = np.array(np.unravel_index(np.arange(V), (L, L, L, L))).T
@@ -655,39 +806,47 @@ def bsr_bench(sb, dev, L, ncols=12, reps=5):
     op = sb.create_bsr(full, dim, full, dim, [1, 1, 1, 1, 1, 3], [1, 1, 1, 1, 1, 3], False,
                        [torch.from_numpy(ii).to(dev)], [torch.from_numpy(jj.reshape(-1)).to(dev)],
                        [vals])
-    dimx = [1, L, L, L, L, 1, 3, ncols]
-    x = torch.empty(vol(dimx), dtype=torch.complex128, device=dev)
-    fill(x, 10)
-    y = torch.empty_like(x)
-    px = [([0] * 8, dimx)]
+    out = {}
+    for ncols in ncols_list:
+        dimx = [1, L, L, L, L, 1, 3, ncols]
+        x = torch.empty(vol(dimx), dtype=torch.complex128, device=dev)
+        fill(x, 10)
+        y = torch.empty_like(x)
+        px = [([0] * 8, dimx)]
 
-    def run():
-        sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", px, "pXYZTSCn", [0] * 8, dimx, dimx, [x], 0.0,
-                      px, "pxyztscn", [0] * 8, dimx, dimx, "p", [y])
-    run()  # first launch loads the code object
-    torch.cuda.synchronize()
-    sb.timings_enable(True)
-    sb.timings_reset()
-    run()
-    torch.cuda.synchronize()
-    bms, bcalls = sb.timings_get("bsr")
-    sb.timings_enable(False)
-    torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(reps):
-        run()
-    e.record()
-    torch.cuda.synchronize()
-    t = s.elapsed_time(e) / 1e3 / reps
-    flops = 8.0 * 81 * V * ncols
-    bytes_ = 16.0 * (81 * V + 2 * 3 * V * ncols) + 4.0 * (9 * V + V + 1)
+        def run():
+            sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", px, "pXYZTSCn", [0] * 8, dimx, dimx, [x],
+                          0.0, px, "pxyztscn", [0] * 8, dimx, dimx, "p", [y])
+        run()  # first launch loads the code object
+        torch.cuda.synchronize()
+        sb.timings_enable(True)
+        sb.timings_filter("bsr")
+        sb.timings_reset()
+        for _ in range(reps):
+            run()
+        torch.cuda.synchronize()
+        bms, bcalls = sb.timings_get("bsr")
+        sb.timings_enable(False)
+        sb.timings_filter(None)
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            run()
+        e.record()
+        torch.cuda.synchronize()
+        t = s.elapsed_time(e) / 1e3 / reps
+        flops = 8.0 * 81 * V * ncols
+        bytes_ = 16.0 * (81 * V + 2 * 3 * V * ncols) + 4.0 * (9 * V + V + 1)
+        tk = bms / max(bcalls, 1) / 1e3
+        p = "bsr_n%d_" % ncols
+        out.update({p + "GFLOPs": round(flops / t / 1e9, 1), p + "GBps": round(bytes_ / t / 1e9, 1),
+                    p + "ms": round(t * 1e3, 4), p + "kernel_ms": round(tk * 1e3, 4),
+                    p + "kernel_GBps": round(bytes_ / tk / 1e9, 1),
+                    p + "kernel_frac_hbm": round(bytes_ / tk / 1e9 / PEAK_HBM_GBPS, 4),
+                    p + "algorithmic_bytes": bytes_})
+        del x, y
     op.destroy()
-    tk = bms / max(bcalls, 1) / 1e3
-    return {"bsr_GFLOPs": round(flops / t / 1e9, 1), "bsr_GBps": round(bytes_ / t / 1e9, 1),
-            "bsr_ncols": ncols, "bsr_ms": round(t * 1e3, 4),
-            "bsr_kernel_GBps": round(bytes_ / tk / 1e9, 1), "bsr_kernel_ms": round(tk * 1e3, 4),
-            "bsr_kernel_frac_hbm": round(bytes_ / tk / 1e9 / PEAK_HBM_GBPS, 4)}
+    return out
 
 
 if __name__ == "__main__":

@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <iostream>
 #include <vector>
 
 #ifdef _OPENMP
@@ -151,5 +152,7 @@ int main(int argc, char **argv) {
         std::fprintf(stderr, "unknown op\n");
         return 1;
     }
+    // SB_TRACK_TIME=1: the reference's own per-function timings (performance.h:356-518)
+    reportTimings(std::cerr);
     return 0;
 }

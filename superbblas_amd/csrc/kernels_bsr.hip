@@ -474,7 +474,7 @@ __global__ void __launch_bounds__(256) bsr_mfma_ell_kernel(const BsrArgs p, long
 // distinct 16 bytes, 1 KB per instruction) instead of 12-row fragment gathers, stages them in a
 // wave-private LDS slot and reads the MFMA fragments from there.  Block j+1 is fetched into
 // registers while block j is applied.
-template <typename R, bool CPLX, int BI, int BD, bool YROW, int NNZ, int PD>
+template <typename R, bool CPLX, int BI, int BD, bool YROW, int NNZ, int PD, bool M3>
 __global__ void __launch_bounds__(256) bsr_mfma_blk_kernel(const BsrArgs p) {
     typedef typename BsrMfmaElem<R, CPLX>::type E;
     typedef typename BsrMfma<R>::acc_t acc_t;
@@ -534,11 +534,17 @@ __global__ void __launch_bounds__(256) bsr_mfma_blk_kernel(const BsrArgs p) {
             const int e = ks * 4 + kq;
             E a = arow_ok ? (p.block_im_fast ? sa[ar + e * BI] : sa[ar * BD + e]) : E{};
             E b = bcol_ok ? sx[e * nc + ar] : E{};
-            if constexpr (CPLX) {
-                // 3-multiplication form: P1 = ar*br, P2 = ai*bi, P3 = (ar+ai)(br+bi)
+            if constexpr (CPLX && M3) {
+                // 3-multiplication form (opt-in): P1 = ar*br, P2 = ai*bi, P3 = (ar+ai)(br+bi)
                 accR = BsrMfma<R>::mma(a.x, b.x, accR);
                 accI = BsrMfma<R>::mma(a.y, b.y, accI);
                 acc3 = BsrMfma<R>::mma(a.x + a.y, b.x + b.y, acc3);
+            } else if constexpr (CPLX) {
+                // 4-multiplication form (BLAS rounding): re += ar*br - ai*bi, im += ar*bi + ai*br
+                accR = BsrMfma<R>::mma(a.x, b.x, accR);
+                accI = BsrMfma<R>::mma(a.x, b.y, accI);
+                accR = BsrMfma<R>::mma(-a.y, b.y, accR);
+                accI = BsrMfma<R>::mma(a.y, b.x, accI);
             } else {
                 accR = BsrMfma<R>::mma(a, b, accR);
             }
@@ -551,9 +557,11 @@ __global__ void __launch_bounds__(256) bsr_mfma_blk_kernel(const BsrArgs p) {
         const long img = i * BI + row;
         E *yp = YROW ? y + img * p.ldy + ar : y + img + ar * p.ldy;
         E out;
-        if constexpr (CPLX)
+        if constexpr (CPLX && M3)
             out = Ops<E>::scale(E{accR[q] - accI[q], acc3[q] - accR[q] - accI[q]}, p.alpha_re,
                                 p.alpha_im);
+        else if constexpr (CPLX)
+            out = Ops<E>::scale(E{accR[q], accI[q]}, p.alpha_re, p.alpha_im);
         else
             out = Ops<E>::scale(accR[q], p.alpha_re, p.alpha_im);
         *yp = p.add ? Ops<E>::add(*yp, out) : out;
@@ -565,10 +573,15 @@ void launch_bsr_mfma_blk(const BsrArgs &a, bool yrow, hipStream_t s) {
     const long blocks = (a.block_rows + 3) / 4;
     if (blocks >= (1L << 31)) throw Error("bsr: grid too large");
     KernelTimer timer("bsr", s);
-    if (yrow)
-        hipLaunchKernelGGL((bsr_mfma_blk_kernel<R, CPLX, BI, BD, true, NNZ, PD>), dim3(blocks), dim3(256), 0, s, a);
+    const bool m3 = CPLX && g_gemm_tune.m3 > 0;
+    if (yrow && m3)
+        hipLaunchKernelGGL((bsr_mfma_blk_kernel<R, CPLX, BI, BD, true, NNZ, PD, true>), dim3(blocks), dim3(256), 0, s, a);
+    else if (yrow)
+        hipLaunchKernelGGL((bsr_mfma_blk_kernel<R, CPLX, BI, BD, true, NNZ, PD, false>), dim3(blocks), dim3(256), 0, s, a);
+    else if (m3)
+        hipLaunchKernelGGL((bsr_mfma_blk_kernel<R, CPLX, BI, BD, false, NNZ, PD, true>), dim3(blocks), dim3(256), 0, s, a);
     else
-        hipLaunchKernelGGL((bsr_mfma_blk_kernel<R, CPLX, BI, BD, false, NNZ, PD>), dim3(blocks), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((bsr_mfma_blk_kernel<R, CPLX, BI, BD, false, NNZ, PD, false>), dim3(blocks), dim3(256), 0, s, a);
     SBX_HIP_CHECK(hipGetLastError());
 }
 

@@ -5,8 +5,12 @@
 // hand-written MFMA kernel:
 //  * f64 / complex<f64>: v_mfma_f64_16x16x4_f64; f32 / complex<f32>: v_mfma_f32_16x16x4_f32.
 //    There is no complex MFMA, so a complex tile product issues 4 real MFMAs
-//    (re*re - im*im, re*im + im*re; the 4M form, not Gauss' 3M, to stay close to BLAS
-//    rounding).  Conjugation flips the sign of the imaginary part when the tile is staged.
+//    (re*re - im*im, re*im + im*re: the 4-multiplication form, which keeps each component's
+//    rounding at the level of BLAS zgemm -- pinned against the reference's OpenBLAS output on
+//    near-real and wide-range operands, tests/test_gpu_golden.py).  The 3-multiplication (Gauss)
+//    form is an opt-in (sbx_tune_set("gemm.m3", 1)): 25 % fewer MFMAs, but a small imaginary
+//    part inherits the rounding of the large real products.  Conjugation flips the sign of the
+//    imaginary part when the fragment is read.
 //  * Operands are staged global -> registers -> LDS (async-stage split: the next K-slab is
 //    loaded into registers while the current one is consumed from LDS), in a [row][k] image
 //    padded by one element so that the 16-byte fragment reads are bank-conflict free.
@@ -673,12 +677,14 @@ void launch_tiled_cfg(const GemmKArgs &p0, int device, hipStream_t stream, long 
 }
 
 /// Launch one tile configuration of the LDS-DMA kernel
-template <typename R, bool CPLX, bool AK, bool BK, int BM, int BN, int BKK, int WM, int WN>
+template <typename R, bool CPLX, bool AK, bool BK, int BM, int BN, int BKK, int WM, int WN,
+          bool ALLOW_M3 = true>
 void launch_dma_cfg(const GemmKArgs &p0, int device, hipStream_t stream, long splits = 0,
                     long target_wgs = 1024) {
-    // complex: the 3-multiplication form unless disabled (config 2: 1.70 -> 1.20 ms; results
-    // within 5e-15 relative of the 4-multiplication form on random complex<double> inputs)
-    const bool m3 = CPLX && g_gemm_tune.m3 >= 0;
+    // complex: the 4-multiplication form unless the 3-multiplication form is asked for (config
+    // 2: 1.53 -> 1.20 ms, but only a normwise error bound: near-real products lose the imaginary
+    // part's relative accuracy, ADVICE r1 / tests/test_gpu_golden.py)
+    const bool m3 = CPLX && g_gemm_tune.m3 > 0;
     GemmKArgs p = p0;
     Scratch work;
     if (g_gemm_tune.splits > 0) splits = g_gemm_tune.splits;
@@ -686,10 +692,14 @@ void launch_dma_cfg(const GemmKArgs &p0, int device, hipStream_t stream, long sp
                                                                    target_wgs, work, device);
     {
         KernelTimer timer("gemm", stream);
-        if (m3)
-            hipLaunchKernelGGL((gemm_dma_kernel<R, CPLX, AK, BK, BM, BN, BKK, WM, WN, CPLX>),
-                               dim3((unsigned)nwg), dim3(WM * WN * 64), 0, stream, p);
-        else
+        if constexpr (ALLOW_M3) {
+            if (m3)
+                hipLaunchKernelGGL((gemm_dma_kernel<R, CPLX, AK, BK, BM, BN, BKK, WM, WN, CPLX>),
+                                   dim3((unsigned)nwg), dim3(WM * WN * 64), 0, stream, p);
+            else
+                hipLaunchKernelGGL((gemm_dma_kernel<R, CPLX, AK, BK, BM, BN, BKK, WM, WN>),
+                                   dim3((unsigned)nwg), dim3(WM * WN * 64), 0, stream, p);
+        } else
             hipLaunchKernelGGL((gemm_dma_kernel<R, CPLX, AK, BK, BM, BN, BKK, WM, WN>),
                                dim3((unsigned)nwg), dim3(WM * WN * 64), 0, stream, p);
         SBX_HIP_CHECK(hipGetLastError());
@@ -732,10 +742,18 @@ void launch_tiled(const GemmKArgs &p, int device, hipStream_t stream) {
         // split-K to one workgroup per CU (config 2: 4 splits 1.19 ms, 8 / 16 splits 1.20 /
         // 1.23 ms once the clocks have ramped up, tools/gemm_chunks.py); 16 waves of 32x32
         // (125 VGPRs, 4 waves/SIMD) measured 1.19-1.22 ms in the 3M form (8 waves: 1.16-1.18)
-        if (p.m >= 128 && p.n >= 128)
-            launch_dma_cfg<R, CPLX, AK, BK, 128, 128, 8, 4, 2>(p, device, stream, 0, 256);
-        else
+        // The 4-multiplication form (default) streams 16-deep slabs (half the barriers per MFMA;
+        // 128 KB of LDS double buffer), the 3-multiplication form 8-deep ones (its third
+        // accumulator set leaves no VGPRs for deeper fragment prefetch)
+        const bool m3 = g_gemm_tune.m3 > 0;
+        if (p.m >= 128 && p.n >= 128) {
+            if (m3)
+                launch_dma_cfg<R, CPLX, AK, BK, 128, 128, 8, 4, 2>(p, device, stream, 0, 256);
+            else
+                launch_dma_cfg<R, CPLX, AK, BK, 128, 128, 16, 4, 2, false>(p, device, stream, 0, 256);
+        } else {
             launch_dma_cfg<R, CPLX, AK, BK, 64, 64, 8, 2, 2>(p, device, stream, 0, 1024);
+        }
     } else {
         // 8-byte and 4-byte elements: 32-deep slabs (fewer barriers per MFMA; measured against
         // 16 and 64 on the lattice shape: double 50.5, complex<float> 116, float 107 TFLOP/s)

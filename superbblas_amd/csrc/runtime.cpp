@@ -353,7 +353,10 @@ void timings_enable(bool on) {
     std::lock_guard<std::mutex> g(g_timer_mutex);
     timers().on = on;
 }
-bool timings_enabled() { return timers().on; }
+bool timings_enabled() {
+    std::lock_guard<std::mutex> g(g_timer_mutex);
+    return timers().on;
+}
 void timings_reset() {
     std::lock_guard<std::mutex> g(g_timer_mutex);
     drain_timers();
@@ -380,10 +383,15 @@ void timings_filter(const char *names) {
     timers().only = names ? std::string(",") + names + "," : std::string();
 }
 KernelTimer::KernelTimer(const char *n, hipStream_t s) : name(n), stream(s) {
-    if (!timers().on) return;
-    // each timed launch adds two event records to the stream (~4 us of stream time each)
-    if (!timers().only.empty() && timers().only.find(std::string(",") + n + ",") == std::string::npos)
-        return;
+    {
+        // the switch and the family filter are written under the lock (timings_enable/filter)
+        std::lock_guard<std::mutex> g(g_timer_mutex);
+        if (!timers().on) return;
+        // each timed launch adds two event records to the stream (~4 us of stream time each)
+        if (!timers().only.empty() &&
+            timers().only.find(std::string(",") + n + ",") == std::string::npos)
+            return;
+    }
     hipEvent_t a;
     SBX_HIP_CHECK(hipEventCreate(&a));
     SBX_HIP_CHECK(hipEventRecord(a, s));

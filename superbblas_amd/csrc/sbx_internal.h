@@ -188,7 +188,8 @@ struct CopyTune {
 };
 extern CopyTune g_copy_tune;
 struct GemmTune {
-    int m3 = 0; ///< complex GEMMs (LDS-DMA kernel): -1 the 4-multiplication form, else the 3-multiplication form
+    int m3 = 0; ///< complex products on the matrix cores (GEMM LDS-DMA and 12x12 BSR kernels): > 0 the
+               ///< 3-multiplication (Gauss) form, else the 4-multiplication form (the default: BLAS rounding)
     int splits = 0; ///< LDS-DMA kernel split-K factor (0 = the library's choice)
     long max_bytes = 0; ///< operand bytes per batch entry before a GEMM is cut (0 = 2^31 - 1)
 };

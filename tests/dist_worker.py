@@ -17,6 +17,10 @@ Cases (all multi-rank: the exchange, pack/unpack kernels and reductions run for 
   storage -- every rank saves its part of a tensor into one shared S3T file (global and block
             checksums), the file is checked by the S3T restatement, then loaded back into
             another distribution  [storage.h:1198-1385, 2142-2370]
+  golden -- the reference's random-valued golden contractions (configs[0] 8^4 n=16, near-real,
+            41-binade range; tests/golden cases 51-55) with the lattice split over the ranks as
+            the bench's configs[3] shapes: v0 and v1 on an xyz grid (2x1x1, 2x2x1, ...; "4a") or
+            v1 over t only ("4b", redistributed), output on rank 0; within 1e-10 per component
   fuzz   -- seeded random copies (permutation, wrapping box, Copy/Add, type pairs) and
             contractions (label groups, orders, boxes, conj, alpha/beta) between random
             distributions over the ranks (some ranks may own nothing)
@@ -34,7 +38,8 @@ sys.path.insert(0, HERE)
 
 from _common import (T_CDOUBLE, oracle_bsr, oracle_contraction, oracle_copy,  # noqa: E402
                      oracle_kron_bsr, rel_err)
-from _golden import gen, piece, put_piece, vol  # noqa: E402
+from _golden import (component_errors, contraction_inputs, gen, manifest, output,  # noqa: E402
+                     piece, put_piece, vol)
 
 
 def scatter(sb, glob, dim, p, rank, nc, dev):
@@ -402,6 +407,39 @@ def case_storage(sb, comm, rank, n, dev):
         os.remove(fn)
 
 
+LATTICE_GRID = {1: [1, 1, 1], 2: [2, 1, 1], 3: [3, 1, 1], 4: [2, 2, 1], 8: [2, 2, 2]}
+
+
+def case_golden(sb, comm, rank, n, dev):
+    grid = LATTICE_GRID.get(n, [n, 1, 1])
+    for case in manifest("contraction"):
+        if case.get("gen", "int") == "int" or case["o0"] != "tnsxyzc" or len(case["p0"]) != 1:
+            continue
+        g0, g1, gr = contraction_inputs(case)
+        d0, d1, dr = case["dim0"], case["dim1"], case["dimr"]
+        p0 = sb.basic_partitioning("tnsxyzc", d0, [1, 1, 1] + grid + [1], "xyz", n, 1)
+        for shape in ("4a", "4b"):
+            if shape == "4a":
+                p1 = sb.basic_partitioning(case["o1"], d1, [1, 1, 1] + grid + [1], "xyz", n, 1)
+            else:
+                p1 = sb.basic_partitioning(case["o1"], d1, [n, 1, 1, 1, 1, 1, 1], "t", n, 1)
+            pr = [([0] * len(dr), dr)] + [([0] * len(dr), [0] * len(dr))] * (n - 1)
+            v0 = scatter(sb, g0, d0, p0, rank, 1, dev)
+            v1 = scatter(sb, g1, d1, p1, rank, 1, dev)
+            vr = scatter(sb, gr, dr, pr, rank, 1, dev)
+            if vr[0].numel() == 0:
+                vr = [torch.zeros(1, dtype=torch.complex128, device=dev)]
+            beta = complex(*case["beta"])
+            sb.contraction(complex(*case["alpha"]), p0, case["from0"], case["size0"], d0,
+                           case["o0"], case["conj0"], v0, p1, case["from1"], case["size1"], d1,
+                           case["o1"], case["conj1"], v1, beta, pr, case["fromr"], case["sizer"],
+                           dr, case["o_r"], vr, comm=comm)
+            torch.cuda.synchronize()
+            out = gather(np.zeros_like(gr), dr, pr, 1, vr[:1] if rank == 0 else [vr[0][:0]])
+            errs = component_errors(out, output(case, np.complex128))
+            assert max(errs) < 1e-10, ("golden", case["id"], shape, errs)
+
+
 def _rand_partition(sb, rng, labels, dims, n):
     i = int(rng.integers(0, len(dims)))
     procs = [1] * len(dims)
@@ -485,6 +523,15 @@ def case_fuzz(sb, comm, rank, n, dev, ncases=12):
 
 
 def main():
+    transport = os.environ.get("SBX_TEST_TRANSPORT", "host")
+    if transport == "rccl" and os.environ.get("SBX_RCCL_SHARED_GPU") == "1":
+        # several RCCL ranks on one GPU (a 1-GPU test box): RCCL refuses two ranks of one host on
+        # one device, so every rank declares its own host id; the ranks then exchange through
+        # RCCL's network transport over loopback sockets.  The library's RCCL code path (grouped
+        # ncclSend/ncclRecv on its streams, the side-stream pipeline) is the one that runs.
+        os.environ["NCCL_HOSTID"] = "sbx-test-rank-%s" % os.environ.get("RANK", "0")
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("NCCL_IB_DISABLE", "1")
     dist.init_process_group("gloo")
     rank, n = dist.get_rank(), dist.get_world_size()
     ndev = torch.cuda.device_count()
@@ -492,12 +539,11 @@ def main():
     torch.cuda.set_device(dev_idx)
     dev = torch.device("cuda", dev_idx)
     import superbblas_amd as sb
-    transport = os.environ.get("SBX_TEST_TRANSPORT", "host")
     if transport == "rccl":
         comm = sb.Comm.from_torch_distributed(dev_idx)
     else:
         comm = sb.Comm.host_staged(dev_idx)
-    cases = os.environ.get("SBX_TEST_CASES", "copy,contr,bsr,kron,dense,storage,fuzz").split(",")
+    cases = os.environ.get("SBX_TEST_CASES", "copy,contr,bsr,kron,dense,storage,fuzz,golden").split(",")
     if "copy" in cases:
         case_copy(sb, comm, rank, n, dev)
     if "contr" in cases:
@@ -512,6 +558,8 @@ def main():
         case_storage(sb, comm, rank, n, dev)
     if "fuzz" in cases:
         case_fuzz(sb, comm, rank, n, dev)
+    if "golden" in cases:
+        case_golden(sb, comm, rank, n, dev)
     dist.barrier()
     comm.close()
     dist.destroy_process_group()

@@ -1,9 +1,12 @@
 """Multi-process GPU parity: copy / contraction / BSR with the data really split across ranks
 (tests/dist_worker.py, one process per rank, launched with torch.distributed.run).
 
-The host-staged transport lets the ranks share the one GPU of a test box (RCCL refuses two ranks
-on one device); the RCCL transport runs when there is a GPU per rank.  The planner, pack/unpack
-kernels, cross-rank reductions and halo exchange are the same code for both transports."""
+The host-staged transport lets the ranks share the one GPU of a test box.  The RCCL transport runs
+with a GPU per rank, or -- on a 1-GPU box -- with every rank declaring its own RCCL host id
+(NCCL_HOSTID; RCCL refuses two ranks of one host on one device), so the ranks exchange through
+RCCL's socket transport: the library's RCCL path (grouped ncclSend/ncclRecv on the library and
+side streams, the T-chunk pipeline) runs for real, only the wire differs from xGMI.  The planner,
+pack/unpack kernels, cross-rank reductions and halo exchange are the same code for both."""
 import os
 import socket
 import subprocess
@@ -22,8 +25,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run(nprocs, transport):
+def _run(nprocs, transport, cases=None, shared=False):
     env = dict(os.environ, SBX_TEST_TRANSPORT=transport, OMP_NUM_THREADS="2")
+    if cases:
+        env["SBX_TEST_CASES"] = cases
+    if shared:
+        env["SBX_RCCL_SHARED_GPU"] = "1"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            "--nproc-per-node", str(nprocs), "--master-addr", "127.0.0.1", "--master-port",
            str(_free_port()), os.path.join(HERE, "dist_worker.py")]
@@ -36,9 +43,12 @@ def test_dist_host_staged(gpu, nprocs):
     _run(nprocs, "host")
 
 
-def test_dist_rccl(gpu):
+def test_dist_host_staged_grid4(gpu):
+    """4 ranks on a 2x2x1 lattice grid (bench configs[3] at N=4), golden contractions only"""
+    _run(4, "host", cases="golden")
+
+
+@pytest.mark.parametrize("nprocs", [2, 3])
+def test_dist_rccl(gpu, nprocs):
     import torch
-    if torch.cuda.device_count() < 2:
-        pytest.skip("RCCL transport needs one GPU per rank (this box has %d)"
-                    % torch.cuda.device_count())
-    _run(2, "rccl")
+    _run(nprocs, "rccl", shared=torch.cuda.device_count() < nprocs)

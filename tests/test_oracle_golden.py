@@ -4,7 +4,8 @@ import numpy as np
 import pytest
 
 from _common import oracle_bsr, oracle_contraction, oracle_copy, oracle_kron_bsr, T_CDOUBLE
-from _golden import NPT, gen, manifest, output, parity_masks, vol
+from _golden import (CONTRACTION_RTOL, NPT, component_errors, contraction_inputs, gen, manifest,
+                     output, parity_masks, vol)
 
 
 def _is_replicated(p, dim):
@@ -29,16 +30,19 @@ def test_oracle_copy(case):
 @pytest.mark.parametrize("case", manifest("contraction"), ids=lambda c: "contr%d" % c["id"])
 def test_oracle_contraction(case):
     t = NPT[case["t"]]
-    v0 = gen("int", vol(case["dim0"]), 1, t)
-    v1 = gen("int", vol(case["dim1"]), 2, t)
-    vr = gen("int", vol(case["dimr"]), 3, t)
+    v0, v1, vr = contraction_inputs(case)
     oracle_contraction(complex(*case["alpha"]), case["o0"], case["from0"], case["size0"],
                        case["dim0"], case["conj0"], v0, case["o1"], case["from1"], case["size1"],
                        case["dim1"], case["conj1"], v1, complex(*case["beta"]), case["o_r"],
                        case["fromr"], case["sizer"], case["dimr"], vr)
     ref = output(case, t)
-    # integer-valued inputs: the sums are exact in f64, so the restatement must match exactly
-    assert np.array_equal(vr, ref)
+    if case.get("gen", "int") == "int":
+        # integer-valued inputs: the sums are exact in f64, so the restatement must match exactly
+        assert np.array_equal(vr, ref)
+    else:
+        # random values: the restatement sums in another order than OpenBLAS
+        tol = CONTRACTION_RTOL[case["t"]]
+        assert max(component_errors(vr, ref)) < tol
 
 
 def lattice_operator(L, spin, color):
