@@ -574,6 +574,19 @@ def permute_bench(sb, dev, L, n, reps=3):
     except Exception:  # pragma: no cover
         t2 = timed(run_f)
     res["permute_cf2cd_GBps"] = round(24.0 * vol(d1) / t2 / 1e9, 1)
+    # the same 64-slice loop called eagerly from C++ through the C ABI (tests/dist.cpp's loop;
+    # no Python between calls): the host cost per sbx_copy with the plan / launch caches warm
+    exe = os.path.join(ROOT, "tools", "capi_overhead")
+    if os.path.exists(exe):
+        try:
+            r = subprocess.run([exe, "permute", str(L), str(n), "5"], timeout=120,
+                               capture_output=True, text=True, check=True).stdout
+            r = json.loads(r.strip().splitlines()[-1])
+            res["permute_eager_cpp_GBps"] = r["GBps"]
+            res["permute_eager_cpp_frac_hbm"] = round(r["GBps"] / PEAK_HBM_GBPS, 4)
+            res["capi_host_us_per_copy"] = r["host_us_per_copy"]
+        except Exception as e:  # pragma: no cover
+            res["permute_eager_cpp_error"] = str(e)[:200]
     return res
 
 

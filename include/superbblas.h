@@ -32,6 +32,7 @@
 #include <stdexcept>
 #include <string>
 #include <type_traits>
+#include <cstdlib>
 #include <vector>
 
 #ifdef SUPERBBLAS_USE_MPI
@@ -899,7 +900,7 @@ inline void preallocate_storage(Storage_handle stoh, std::size_t size) {
 }
 inline void flush_storage(Storage_handle stoh) { sbx_detail::check(sbx_storage_flush(stoh)); }
 
-// ---- MPI overloads: a host-staged communicator over MPI_Alltoallv (dist.h:1426-1500) ----
+// ---- MPI overloads: RCCL (one GPU per rank) or host staging over MPI_Alltoallv ----
 #ifdef SUPERBBLAS_USE_MPI
 namespace sbx_detail {
 inline int mpi_alltoallv(const void *sbuf, const unsigned long long *sbytes,
@@ -924,8 +925,30 @@ inline int mpi_alltoallv(const void *sbuf, const unsigned long long *sbytes,
                ? 0
                : 1;
 }
-/// One host-staged communicator per MPI_Comm, created on first use (device = the first GPU
-/// context's device), kept until clearHandles-like teardown at exit
+/// Whether every rank of `mpicomm` drives its own GPU: ranks on one node (MPI_COMM_TYPE_SHARED)
+/// must hold distinct device ids (RCCL runs one rank per device, like the reference's GPU-aware
+/// MPI path, dist.h:1626-1641)
+inline bool ranks_own_devices(MPI_Comm mpicomm, int device) {
+    MPI_Comm node;
+    if (MPI_Comm_split_type(mpicomm, MPI_COMM_TYPE_SHARED, 0, MPI_INFO_NULL, &node) != MPI_SUCCESS)
+        return false;
+    int n = 1;
+    MPI_Comm_size(node, &n);
+    std::vector<int> devs(n);
+    MPI_Allgather(&device, 1, MPI_INT, devs.data(), 1, MPI_INT, node);
+    MPI_Comm_free(&node);
+    for (int i = 0; i < n; ++i)
+        for (int j = i + 1; j < n; ++j)
+            if (devs[i] == devs[j]) return false;
+    return true;
+}
+
+/// One communicator per MPI_Comm, created on first use (device = the first GPU context's
+/// device) and kept for the life of the process.  Transport: RCCL over xGMI when every rank
+/// drives its own GPU -- the unique id is made by rank 0 and broadcast with MPI_Bcast, so device
+/// buffers travel directly (the reference's GPU-aware MPI path, dist.h:1626-1641, 1702-1773) --
+/// otherwise (ranks sharing a GPU) the host-staged transport over MPI_Alltoallv
+/// (dist.h:1426-1500).  SUPERBBLAS_AMD_MPI_TRANSPORT=host|rccl forces one.
 inline sbx_comm comm_of(MPI_Comm mpicomm, const Context *ctx, int ncomponents) {
     struct Entry {
         std::unique_ptr<MPI_Comm> c;
@@ -945,8 +968,19 @@ inline sbx_comm comm_of(MPI_Comm mpicomm, const Context *ctx, int ncomponents) {
             device = ctx[i].device;
             break;
         }
+    const char *force = std::getenv("SUPERBBLAS_AMD_MPI_TRANSPORT");
+    bool rccl = ranks_own_devices(mpicomm, device); // collective: every rank decides alike
+    if (force && std::string(force) == "host") rccl = false;
+    if (force && std::string(force) == "rccl") rccl = true;
     Entry e{std::unique_ptr<MPI_Comm>(new MPI_Comm(mpicomm)), nullptr};
-    check(sbx_comm_create_host(n, rank, device, mpi_alltoallv, e.c.get(), &e.h));
+    if (rccl) {
+        unsigned char id[128] = {0};
+        if (rank == 0) check(sbx_comm_unique_id(id));
+        MPI_Bcast(id, 128, MPI_BYTE, 0, mpicomm);
+        check(sbx_comm_create(n, rank, id, device, &e.h));
+    } else {
+        check(sbx_comm_create_host(n, rank, device, mpi_alltoallv, e.c.get(), &e.h));
+    }
     cache.push_back(std::move(e));
     return cache.back().h;
 }

@@ -87,7 +87,9 @@ static int normalize_coor(long c, int dim) {
  *   v1[(from1 + P(c - from0)) mod dim1] (=|+=) alpha * v0[(from0 + c) mod dim0],
  *   c in [0, size0); labels of o1 missing in o0 take from1.
  * With alpha == 1 the value is moved without a multiplication (copy_n.h:147-244 uses a plain
- * assignment for alpha == 1); Add computes w + alpha*v.
+ * assignment for alpha == 1); Add computes w + alpha*v.  With alpha == 0 a Copy writes +0 to the
+ * destination region and an Add does nothing (dist.h:2383, copy_n.h:92 and 435-438: no
+ * 0 * v products, so no -0.0).
  */
 int oracle_copy_masked(int nd0, int nd1, const double *alpha, int t0, int t1, const char *o0,
                        const int *from0, const int *size0, const int *dim0, const void *v0,
@@ -140,8 +142,13 @@ int oracle_copy_masked(int nd0, int nd1, const double *alpha, int t0, int t1, co
         free(i1s);
         return -2; /* "copy: non-compatible masks" */
     }
+    const int zero = alpha[0] == 0 && alpha[1] == 0;
     for (long q = 0; q < n0; ++q) {
         const long i0 = i0s[q], i1 = i1s[q];
+        if (zero) {
+            if (!add) store(t1, v1, i1, 0.0, 0.0);
+            continue;
+        }
         if (one && !add && t0 == t1) {
             memcpy((char *)v1 + i1 * elem_size(t1), (const char *)v0 + i0 * elem_size(t0),
                    elem_size(t0));

@@ -4,6 +4,9 @@
 // mirrors host (CPU-context) components through device scratch so that every data movement
 // and every flop runs on the GPU, and turns C++ exceptions into status codes.
 #include "plan.h"
+#include <algorithm>
+#include <memory>
+#include <unordered_map>
 
 #include <rccl/rccl.h>
 
@@ -227,6 +230,59 @@ sbx_storage_s &storage_of(sbx_storage sto) {
 
 } // namespace
 
+namespace {
+//
+// copy() fast path: single process, device components, no masks.  The first call of a shape
+// runs the planner with a launch tape on; later calls of the same shape (every argument but the
+// data pointers and a nonzero alpha) replay the tape on the new pointers -- no planning, no
+// allocations (the reference's copy-plan cache, dist.h:2303-2353).
+//
+struct TapeKeyHash {
+    std::size_t operator()(const std::vector<long> &k) const {
+        std::size_t h = 1469598103934665603ull;
+        for (long v : k) h = (h ^ (std::size_t)v) * 1099511628211ull;
+        return h;
+    }
+};
+std::mutex g_tape_mutex;
+std::unordered_map<std::vector<long>, std::shared_ptr<const CopyTape>, TapeKeyHash> &tapes() {
+    static std::unordered_map<std::vector<long>, std::shared_ptr<const CopyTape>, TapeKeyHash> m;
+    return m;
+}
+
+void key_ints(std::vector<long> &k, const int *p, long n) {
+    for (long i = 0; i < n; ++i) k.push_back(p ? p[i] : 0);
+}
+void key_str(std::vector<long> &k, const char *o, int n) {
+    for (int i = 0; i < n; ++i) k.push_back(o[i]);
+}
+
+/// Resolve a recorded pointer to (argument, component, byte offset) among the call's components;
+/// false when it lies in none or in more than one (aliasing: not replayable)
+bool resolve(const void *ptr, const void *const *v0, const int *p0, int nc0, int nd0, int t0,
+             const void *const *v1, const int *p1, int nc1, int nd1, int t1, int &arg, int &comp,
+             long &off) {
+    int found = 0;
+    auto scan = [&](const void *const *v, const int *p, int nc, int nd, int t, int a) {
+        for (int c = 0; c < nc; ++c) {
+            long vol = 1;
+            for (int i = 0; i < nd; ++i) vol *= p[(long)c * 2 * nd + nd + i];
+            const char *b = (const char *)v[c];
+            const long bytes = vol * (long)dtype_size(t);
+            if (b && (const char *)ptr >= b && (const char *)ptr < b + std::max(bytes, 1L)) {
+                ++found;
+                arg = a;
+                comp = c;
+                off = (long)((const char *)ptr - b);
+            }
+        }
+    };
+    scan(v0, p0, nc0, nd0, t0, 0);
+    scan(v1, p1, nc1, nd1, t1, 1);
+    return found == 1;
+}
+} // namespace
+
 extern "C" {
 
 const char *sbx_last_error(void) { return g_last_error.c_str(); }
@@ -270,7 +326,13 @@ int sbx_stream_reset(int device) {
 }
 
 int sbx_clear_caches(void) {
-    return guard([&] { trim_pools(); });
+    return guard([&] {
+        trim_pools();
+        clear_copy_plan_cache();
+        clear_copy_launch_cache();
+        std::lock_guard<std::mutex> g(g_tape_mutex);
+        tapes().clear();
+    });
 }
 
 int sbx_clear_handles(void) {
@@ -524,6 +586,48 @@ int sbx_copy_masked(int nd0, int nd1, const double *alpha, int t0, int t1, const
         if (mask0 && !mask1)
             throw Error("copy: a destination mask (mask1) is required with an origin mask");
         const Comm c = get_comm(comm);
+        const Scalar a_call = to_scalar(alpha);
+        // fast path (see above): the shape key excludes the data pointers and alpha's value
+        bool fast = !mask0 && !mask1 && c.nprocs == 1 && p0 && p1 && v0 && v1 && o0 && o1 &&
+                    ncomponents0 >= 1 && ncomponents1 >= 1 && ctx0 && ctx1 &&
+                    (int)std::strlen(o0) == nd0 && (int)std::strlen(o1) == nd1;
+        for (int i = 0; fast && i < ncomponents0; ++i) fast = ctx0[i].plat == SBX_GPU;
+        for (int i = 0; fast && i < ncomponents1; ++i) fast = ctx1[i].plat == SBX_GPU;
+        std::vector<long> key;
+        if (fast) {
+            key.reserve(32 + 6 * (nd0 + nd1) + 2 * (ncomponents0 * nd0 + ncomponents1 * nd1));
+            key.insert(key.end(), {nd0, nd1, t0, t1, ncomponents0, ncomponents1, co, copyadd,
+                                   (long)a_call.is_zero(), comm ? 1L : 0L, c.device,
+                                   g_copy_tune.budget, g_copy_tune.run, g_copy_tune.kernel,
+                                   g_copy_tune.nt, g_copy_tune.max_elems});
+            key_str(key, o0, nd0);
+            key_str(key, o1, nd1);
+            key_ints(key, p0, 2L * nd0 * ncomponents0);
+            key_ints(key, p1, 2L * nd1 * ncomponents1);
+            key_ints(key, from0, nd0);
+            key_ints(key, size0, nd0);
+            key_ints(key, dim0, nd0);
+            key_ints(key, from1, nd1);
+            key_ints(key, dim1, nd1);
+            for (int i = 0; i < ncomponents0; ++i) key.push_back(ctx0[i].device);
+            for (int i = 0; i < ncomponents1; ++i) key.push_back(ctx1[i].device);
+            std::shared_ptr<const CopyTape> tape;
+            {
+                std::lock_guard<std::mutex> g(g_tape_mutex);
+                auto it = tapes().find(key);
+                if (it != tapes().end()) tape = it->second;
+            }
+            if (tape) {
+                for (const TapeLaunch &l : tape->launches) {
+                    const char *sb = l.src_arg == 0 ? (const char *)v0[l.src_comp]
+                                                    : (const char *)v1[l.src_comp];
+                    char *db = l.dst_arg == 0 ? (char *)const_cast<void *>(v0[l.dst_comp])
+                                              : (char *)v1[l.dst_comp];
+                    replay_launch(l, sb + l.src_off, db + l.dst_off, l.alpha_is_call ? a_call : l.alpha);
+                }
+                return;
+            }
+        }
         const bool rev = co == SBX_FAST_TO_SLOW;
         check_copy_args(to_labels(o0, nd0, rev, "o0"), to_coor(from0, nd0, rev),
                         to_coor(size0, nd0, rev), to_coor(dim0, nd0, rev),
@@ -536,9 +640,40 @@ int sbx_copy_masked(int nd0, int nd1, const double *alpha, int t0, int t1, const
                                    t1, c, rev, m, true, "o1");
         attach_masks(a, mask0, ncomponents0, ctx0, c, m);
         attach_masks(b, mask1, ncomponents1, ctx1, c, m);
-        dist_copy(to_scalar(alpha), a, to_coor(from0, nd0, rev), to_coor(size0, nd0, rev), b,
-                  to_coor(from1, nd1, rev), copyadd == SBX_ADD, c);
+        auto tape = fast ? std::make_shared<CopyTape>() : nullptr;
+        set_copy_tape(tape.get());
+        try {
+            dist_copy(a_call, a, to_coor(from0, nd0, rev), to_coor(size0, nd0, rev), b,
+                      to_coor(from1, nd1, rev), copyadd == SBX_ADD, c);
+        } catch (...) {
+            set_copy_tape(nullptr);
+            throw;
+        }
+        set_copy_tape(nullptr);
         finish_mirror(m);
+        if (tape && tape->valid) {
+            // resolve the recorded pointers against the components (p0/p1 in the caller's
+            // order; the byte extents do not depend on it)
+            for (TapeLaunch &l : tape->launches) {
+                bool ok = resolve(l.src, v0, p0, ncomponents0, nd0, t0, (const void *const *)v1, p1,
+                                  ncomponents1, nd1, t1, l.src_arg, l.src_comp, l.src_off) &&
+                          resolve(l.dst, v0, p0, ncomponents0, nd0, t0, (const void *const *)v1, p1,
+                                  ncomponents1, nd1, t1, l.dst_arg, l.dst_comp, l.dst_off);
+                const bool is_call = l.alpha.re == a_call.re && l.alpha.im == a_call.im;
+                // a launch whose alpha matches neither the call nor zero would be ambiguous
+                if (!is_call && !l.alpha.is_zero()) ok = false;
+                l.alpha_is_call = is_call;
+                if (!ok) {
+                    tape->valid = false;
+                    break;
+                }
+            }
+            if (tape->valid) {
+                std::lock_guard<std::mutex> g(g_tape_mutex);
+                if (tapes().size() >= 4096) tapes().clear();
+                tapes().emplace(std::move(key), tape);
+            }
+        }
     });
 }
 

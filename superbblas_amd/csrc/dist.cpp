@@ -26,6 +26,9 @@
 #include <algorithm>
 #include <cassert>
 #include <map>
+#include <memory>
+#include <mutex>
+#include <unordered_map>
 
 namespace sbx {
 
@@ -255,7 +258,87 @@ void host_exchange(const Comm &comm, const void *sdev, const std::vector<std::si
     if (nr) SBX_HIP_CHECK(hipMemcpyAsync(rdev, st.recv, nr, hipMemcpyHostToDevice, s));
 }
 
+/// The planner's result for one copy shape: the pieces and whether they cover this rank's
+/// destination region (no zero-fill needed).  Cached by shape (the reference caches its copy
+/// plans the same way, dist.h:2303-2353), so a repeated copy skips the interval algebra.
+struct CopyPlan {
+    std::vector<Piece> pieces;
+    bool full = true;
+};
+
+struct PlanKeyHash {
+    std::size_t operator()(const std::vector<long> &k) const {
+        std::size_t h = 1469598103934665603ull;
+        for (long v : k) h = (h ^ (std::size_t)v) * 1099511628211ull;
+        return h;
+    }
+};
+
+std::mutex g_plan_mutex;
+std::unordered_map<std::vector<long>, std::shared_ptr<const CopyPlan>, PlanKeyHash> &plan_cache() {
+    static std::unordered_map<std::vector<long>, std::shared_ptr<const CopyPlan>, PlanKeyHash> c;
+    return c;
+}
+
+void key_tensor(std::vector<long> &k, const DistTensor &t) {
+    k.push_back(t.nd());
+    for (char c : t.labels) k.push_back(c);
+    for (int d : t.dim) k.push_back(d);
+    k.push_back((long)t.ranges.size());
+    for (const auto &rk : t.ranges) {
+        k.push_back((long)rk.size());
+        for (const Range &r : rk) {
+            for (int v : r.from) k.push_back(v);
+            for (int v : r.size) k.push_back(v);
+        }
+    }
+}
+
+std::shared_ptr<const CopyPlan> get_copy_plan(const DistTensor &src, const Coor &from0,
+                                              const Coor &size0, const DistTensor &dst,
+                                              const Coor &from1, const Range &region1, bool add,
+                                              int rank) {
+    std::vector<long> key;
+    key.reserve(64);
+    key.push_back(rank);
+    key.push_back(add);
+    key_tensor(key, src);
+    key_tensor(key, dst);
+    for (int v : from0) key.push_back(v);
+    for (int v : size0) key.push_back(v);
+    for (int v : from1) key.push_back(v);
+    {
+        std::lock_guard<std::mutex> g(g_plan_mutex);
+        auto it = plan_cache().find(key);
+        if (it != plan_cache().end()) return it->second;
+    }
+    auto plan = std::make_shared<CopyPlan>();
+    plan->pieces = plan_copy(src, from0, size0, dst, from1, add, rank);
+    if (!add) {
+        // covered volume per local destination component vs. the region's volume
+        const std::vector<CompRef> dc = flatten_components(dst);
+        std::vector<long> need(dst.ranges[rank].size(), 0), got(need.size(), 0);
+        for (int i = 0; i < (int)need.size(); ++i) {
+            const Range &rb = dst.ranges[rank][i];
+            if (volume(rb.size) == 0) continue;
+            for (const Range &z : intersection(region1, rb, dst.dim)) need[i] += volume(z.size);
+        }
+        for (const Piece &p : plan->pieces)
+            if (dc[p.b].rank == rank) got[dc[p.b].idx] += volume(p.size);
+        for (std::size_t i = 0; i < need.size(); ++i) plan->full &= (need[i] == got[i]);
+    }
+    std::lock_guard<std::mutex> g(g_plan_mutex);
+    if (plan_cache().size() >= 4096) plan_cache().clear();
+    plan_cache().emplace(std::move(key), plan);
+    return plan;
+}
+
 } // namespace
+
+void clear_copy_plan_cache() {
+    std::lock_guard<std::mutex> g(g_plan_mutex);
+    plan_cache().clear();
+}
 
 HostStage::~HostStage() {
     if (send) (void)hipHostFree(send);
@@ -359,25 +442,11 @@ void dist_copy(const Scalar &alpha, const DistTensor &src, const Coor &from0, co
         return;
     }
 
-    const std::vector<Piece> pieces = plan_copy(src, from0, size0, dst, from1, add, comm.rank);
-
-    if (!add) {
-        // Zero the part of the local destination not covered by any piece
-        bool full = true;
-        {
-            // covered volume per local destination component vs. region volume
-            std::vector<long> need(dst.ranges[comm.rank].size(), 0), got(need.size(), 0);
-            for (int i = 0; i < (int)need.size(); ++i) {
-                const Range &rb = dst.ranges[comm.rank][i];
-                if (volume(rb.size) == 0) continue;
-                for (const Range &z : intersection(region1, rb, dst.dim)) need[i] += volume(z.size);
-            }
-            for (const Piece &p : pieces)
-                if (dc[p.b].rank == comm.rank) got[dc[p.b].idx] += volume(p.size);
-            for (std::size_t i = 0; i < need.size(); ++i) full &= (need[i] == got[i]);
-        }
-        if (!full) zero_region();
-    }
+    const std::shared_ptr<const CopyPlan> plan =
+        get_copy_plan(src, from0, size0, dst, from1, region1, add, comm.rank);
+    const std::vector<Piece> &pieces = plan->pieces;
+    // Zero the part of the local destination not covered by any piece
+    if (!add && !plan->full) zero_region();
 
     // Local pieces
     for (const Piece &p : pieces) {
@@ -392,6 +461,7 @@ void dist_copy(const Scalar &alpha, const DistTensor &src, const Coor &from0, co
                              src.mask_of(ca.idx), dst.mask_of(cb.idx));
         } else {
             // pack on the origin device, peer copy, unpack on the destination device
+            if (CopyTape *t = current_copy_tape()) t->valid = false; // not replayable
             const long n = volume(p.size);
             const std::size_t bytes = n * dtype_size(src.dtype);
             Scratch sbuf(bytes, da);

@@ -21,7 +21,9 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
 #include <numeric>
+#include <unordered_map>
 
 namespace sbx {
 CopyTune g_copy_tune;
@@ -439,15 +441,70 @@ Norm normalize(const BoxCopyDesc &d) {
     return n;
 }
 
+/// A prepared box-copy launch: everything but the pointers and alpha, which are patched per call
+/// (the launch cache below keys it on the box shape, element types and tuning switches; the
+/// reference caches its permutation index vectors the same way, tensor.h:919-961)
+struct CopyLaunch {
+    enum Kind { MASKED, CONTIG, DIRECT, TILED1, TILED3 } kind = DIRECT;
+    DirectArgs da{};
+    TiledArgs ta{};
+    long total = 0, blocks = 0;
+    int nt = 0;
+    void (*run)(const CopyLaunch &, const void *, void *, const Alpha &, const float *,
+                const float *, hipStream_t) = nullptr;
+};
+
 template <typename S, typename D, bool ADD>
-void launch_pair(const BoxCopyDesc &d, Norm n, long total, hipStream_t stream) {
-    Alpha alpha{d.alpha.re, d.alpha.im, d.alpha.is_one() ? 1 : 0};
-    const S *src = (const S *)d.src;
-    D *dst = (D *)d.dst;
-    if (d.src_mask || d.dst_mask) {
+void run_launch(const CopyLaunch &l, const void *src, void *dst, const Alpha &alpha,
+                const float *smask, const float *dmask, hipStream_t stream) {
+    KernelTimer timer("copy", stream);
+    const dim3 grid((unsigned)l.blocks), block(256);
+    switch (l.kind) {
+    case CopyLaunch::MASKED: {
+        DirectArgs a = l.da;
+        a.src = src;
+        a.dstp = dst;
+        a.alpha = alpha;
+        hipLaunchKernelGGL((copy_masked_kernel<S, D, ADD>), grid, block, 0, stream, a, smask, dmask);
+        break;
+    }
+    case CopyLaunch::CONTIG:
+        hipLaunchKernelGGL((copy_contig_kernel<S, D, ADD>), grid, block, 0, stream, (const S *)src,
+                           (D *)dst, l.total, alpha, l.nt);
+        break;
+    case CopyLaunch::DIRECT: {
+        DirectArgs a = l.da;
+        a.src = src;
+        a.dstp = dst;
+        a.alpha = alpha;
+        hipLaunchKernelGGL((copy_direct_kernel<S, D, ADD>), grid, block, 0, stream, a);
+        break;
+    }
+    case CopyLaunch::TILED1:
+    case CopyLaunch::TILED3: {
+        TiledArgs a = l.ta;
+        a.src = src;
+        a.dstp = dst;
+        a.alpha = alpha;
+        if (l.kind == CopyLaunch::TILED1)
+            hipLaunchKernelGGL((copy_tiled_kernel<S, D, ADD>), grid, block, 0, stream, a);
+        else
+            hipLaunchKernelGGL((copy_tiled3_kernel<S, D, ADD, 4>), grid, block, 0, stream, a);
+        break;
+    }
+    }
+    SBX_HIP_CHECK(hipGetLastError());
+}
+
+template <typename S, typename D, bool ADD>
+CopyLaunch prepare_pair(bool masked, Norm n, long total) {
+    CopyLaunch l;
+    l.run = run_launch<S, D, ADD>;
+    l.total = total;
+    if (masked) {
         if (total >= (1L << 32) - 1) throw Error("copy: masked boxes of 2^32 elements or more are not supported");
         if ((int)n.size.size() > MAXD) throw Error("copy: too many non-mergeable dimensions");
-        DirectArgs a{};
+        DirectArgs &a = l.da;
         a.nd = (int)n.size.size();
         a.total = (uint32_t)total;
         for (int i = 0; i < a.nd; ++i) {
@@ -455,25 +512,16 @@ void launch_pair(const BoxCopyDesc &d, Norm n, long total, hipStream_t stream) {
             a.sst[i] = n.ss[i];
             a.dst[i] = n.ds[i];
         }
-        a.src = src;
-        a.dstp = dst;
-        a.alpha = alpha;
-        const long blocks = std::min((total + 255) / 256, 8192L);
-        KernelTimer timer("copy", stream);
-        hipLaunchKernelGGL((copy_masked_kernel<S, D, ADD>), dim3((unsigned)blocks), dim3(256), 0,
-                           stream, a, d.src_mask, d.dst_mask);
-        SBX_HIP_CHECK(hipGetLastError());
-        return;
+        l.kind = CopyLaunch::MASKED;
+        l.blocks = std::min((total + 255) / 256, 8192L);
+        return l;
     }
     // Fully contiguous on both sides
     if (n.size.size() == 1 && n.ss[0] == 1 && n.ds[0] == 1) {
-        const long blocks = std::min((total + 255) / 256, 8192L);
-        KernelTimer timer("copy", stream);
-        const int nt = g_copy_tune.nt > 0 || (g_copy_tune.nt == 0 && total * (long)sizeof(D) >= (8L << 20));
-        hipLaunchKernelGGL((copy_contig_kernel<S, D, ADD>), dim3((unsigned)blocks), dim3(256), 0,
-                           stream, src, dst, total, alpha, nt);
-        SBX_HIP_CHECK(hipGetLastError());
-        return;
+        l.kind = CopyLaunch::CONTIG;
+        l.blocks = std::min((total + 255) / 256, 8192L);
+        l.nt = g_copy_tune.nt > 0 || (g_copy_tune.nt == 0 && total * (long)sizeof(D) >= (8L << 20));
+        return l;
     }
     if (total >= (1L << 32) - 1) throw Error("copy: boxes with 2^32 elements or more are not supported yet");
     const int nd = (int)n.size.size();
@@ -541,7 +589,7 @@ void launch_pair(const BoxCopyDesc &d, Norm n, long total, hipStream_t stream) {
     if (ndd > MAXD) throw Error("copy: too many non-mergeable dimensions");
     if (Vc.empty() || U.empty()) {
         // Direct destination-ordered gather
-        DirectArgs a{};
+        DirectArgs &a = l.da;
         a.nd = ndd;
         a.total = (uint32_t)total;
         for (int i = 0; i < ndd; ++i) {
@@ -549,19 +597,13 @@ void launch_pair(const BoxCopyDesc &d, Norm n, long total, hipStream_t stream) {
             a.sst[i] = n.ss[i];
             a.dst[i] = n.ds[i];
         }
-        a.src = src;
-        a.dstp = dst;
-        a.alpha = alpha;
-        const long blocks = std::min((total + 255) / 256, 8192L);
-        KernelTimer timer("copy", stream);
-        hipLaunchKernelGGL((copy_direct_kernel<S, D, ADD>), dim3((unsigned)blocks), dim3(256), 0,
-                           stream, a);
-        SBX_HIP_CHECK(hipGetLastError());
-        return;
+        l.kind = CopyLaunch::DIRECT;
+        l.blocks = std::min((total + 255) / 256, 8192L);
+        return l;
     }
 
     static const bool debug = getenv("SBX_COPY_DEBUG") != nullptr; // print the tiling
-    TiledArgs a{};
+    TiledArgs &a = l.ta;
     long NU = 1, NV = 1;
     for (int i : U) NU *= n.size[i];
     for (int i : Vc) NV *= n.size[i];
@@ -589,9 +631,9 @@ void launch_pair(const BoxCopyDesc &d, Norm n, long total, hipStream_t stream) {
     a.fRTV = FastDiv((uint32_t)(R * TV));
     // lanes per tile row: the smallest power of two >= the row width, at most a wave
     auto lanes_log2 = [](long width) {
-        uint32_t l = 0;
-        while (l < 6 && (1L << l) < width) ++l;
-        return l;
+        uint32_t l2 = 0;
+        while (l2 < 6 && (1L << l2) < width) ++l2;
+        return l2;
     };
     // streaming stores for large destinations (written once, not re-read by this kernel):
     // the config-2p slice loop 6.8 -> 4.9 us per slice, the 1.6 GB permute 5.0 -> 5.2 TB/s
@@ -623,9 +665,6 @@ void launch_pair(const BoxCopyDesc &d, Norm n, long total, hipStream_t stream) {
         ++nw;
     }
     a.nw = nw;
-    a.src = src;
-    a.dstp = dst;
-    a.alpha = alpha;
     const long blocks = (long)a.ntu * a.ntv * NW;
     if (blocks >= (1L << 31)) throw Error("copy: grid too large");
     if (debug) {
@@ -634,25 +673,78 @@ void launch_pair(const BoxCopyDesc &d, Norm n, long total, hipStream_t stream) {
         std::fprintf(stderr, " | R=%ld NU=%ld NV=%ld TU=%ld TV=%ld nu=%d nv=%d nw=%d blocks=%ld\n", R,
                      NU, NV, TU, TV, a.nu, a.nv, nw, blocks);
     }
-    KernelTimer timer("copy", stream);
-    if (g_copy_tune.kernel == 1)
-        hipLaunchKernelGGL((copy_tiled_kernel<S, D, ADD>), dim3((unsigned)blocks), dim3(256), 0,
-                           stream, a);
-    else
-        hipLaunchKernelGGL((copy_tiled3_kernel<S, D, ADD, 4>), dim3((unsigned)blocks), dim3(256),
-                           0, stream, a);
-    SBX_HIP_CHECK(hipGetLastError());
+    l.kind = g_copy_tune.kernel == 1 ? CopyLaunch::TILED1 : CopyLaunch::TILED3;
+    l.blocks = blocks;
+    return l;
 }
 
 template <typename S, typename D>
-void launch_sd(const BoxCopyDesc &d, const Norm &n, long total, hipStream_t s) {
-    if (d.add)
-        launch_pair<S, D, true>(d, n, total, s);
-    else
-        launch_pair<S, D, false>(d, n, total, s);
+CopyLaunch prepare_sd(bool add, bool masked, const Norm &n, long total) {
+    return add ? prepare_pair<S, D, true>(masked, n, total)
+               : prepare_pair<S, D, false>(masked, n, total);
+}
+
+CopyLaunch prepare_launch(const BoxCopyDesc &d, long total) {
+    const Norm n = normalize(d);
+    const bool m = d.src_mask || d.dst_mask, a = d.add;
+    const int st = d.src_t, dt = d.dst_t;
+    if (st == dt) {
+        switch (st) {
+        case SBX_FLOAT: return prepare_sd<float, float>(a, m, n, total);
+        case SBX_DOUBLE: return prepare_sd<double, double>(a, m, n, total);
+        case SBX_CFLOAT: return prepare_sd<float2, float2>(a, m, n, total);
+        case SBX_CDOUBLE: return prepare_sd<double2, double2>(a, m, n, total);
+        case SBX_INT: return prepare_sd<int, int>(a, m, n, total);
+        case SBX_SIZE_T: return prepare_sd<unsigned long, unsigned long>(a, m, n, total);
+        }
+    }
+    if (st == SBX_FLOAT && dt == SBX_DOUBLE) return prepare_sd<float, double>(a, m, n, total);
+    if (st == SBX_DOUBLE && dt == SBX_FLOAT) return prepare_sd<double, float>(a, m, n, total);
+    if (st == SBX_CFLOAT && dt == SBX_CDOUBLE) return prepare_sd<float2, double2>(a, m, n, total);
+    if (st == SBX_CDOUBLE && dt == SBX_CFLOAT) return prepare_sd<double2, float2>(a, m, n, total);
+    if (st == SBX_FLOAT && dt == SBX_CFLOAT) return prepare_sd<float, float2>(a, m, n, total);
+    if (st == SBX_FLOAT && dt == SBX_CDOUBLE) return prepare_sd<float, double2>(a, m, n, total);
+    if (st == SBX_DOUBLE && dt == SBX_CFLOAT) return prepare_sd<double, float2>(a, m, n, total);
+    if (st == SBX_DOUBLE && dt == SBX_CDOUBLE) return prepare_sd<double, double2>(a, m, n, total);
+    if (st == SBX_INT && dt == SBX_SIZE_T) return prepare_sd<int, unsigned long>(a, m, n, total);
+    if (st == SBX_SIZE_T && dt == SBX_INT) return prepare_sd<unsigned long, int>(a, m, n, total);
+    throw Error("copy: unsupported type conversion");
+}
+
+/// Launch cache: prepared launches by box shape, bounded (cleared when it reaches 4096 shapes;
+/// the reference caps its plan caches at a fraction of memory, cache.h:21-305)
+struct LaunchKeyHash {
+    std::size_t operator()(const std::vector<long> &k) const {
+        std::size_t h = 1469598103934665603ull;
+        for (long v : k) h = (h ^ (std::size_t)v) * 1099511628211ull;
+        return h;
+    }
+};
+std::mutex g_launch_mutex;
+std::unordered_map<std::vector<long>, CopyLaunch, LaunchKeyHash> &launch_cache() {
+    static std::unordered_map<std::vector<long>, CopyLaunch, LaunchKeyHash> c;
+    return c;
 }
 
 } // namespace
+
+void clear_copy_launch_cache() {
+    std::lock_guard<std::mutex> g(g_launch_mutex);
+    launch_cache().clear();
+}
+
+namespace {
+thread_local CopyTape *t_tape = nullptr;
+}
+void set_copy_tape(CopyTape *t) { t_tape = t; }
+CopyTape *current_copy_tape() { return t_tape; }
+
+void replay_launch(const TapeLaunch &tl, const void *src, void *dst, const Scalar &alpha) {
+    const CopyLaunch &l = *(const CopyLaunch *)tl.launch.get();
+    set_device(tl.device);
+    const Alpha a{alpha.re, alpha.im, alpha.is_one() ? 1 : 0};
+    l.run(l, src, dst, a, nullptr, nullptr, get_stream(tl.device));
+}
 
 void launch_box_copy(const BoxCopyDesc &d, int device) {
     long total = 1;
@@ -681,29 +773,45 @@ void launch_box_copy(const BoxCopyDesc &d, int device) {
     }
     set_device(device);
     hipStream_t s = get_stream(device);
-    const Norm n = normalize(d);
-    const int st = d.src_t, dt = d.dst_t;
-    if (st == dt) {
-        switch (st) {
-        case SBX_FLOAT: return launch_sd<float, float>(d, n, total, s);
-        case SBX_DOUBLE: return launch_sd<double, double>(d, n, total, s);
-        case SBX_CFLOAT: return launch_sd<float2, float2>(d, n, total, s);
-        case SBX_CDOUBLE: return launch_sd<double2, double2>(d, n, total, s);
-        case SBX_INT: return launch_sd<int, int>(d, n, total, s);
-        case SBX_SIZE_T: return launch_sd<unsigned long, unsigned long>(d, n, total, s);
+    // key: types, Copy/Add, masks, the box (sizes and both strides), the tuning switches
+    const std::size_t nd = d.size.size();
+    std::vector<long> key;
+    key.reserve(4 + 3 * nd);
+    key.push_back(d.src_t | (d.dst_t << 8) | ((long)d.add << 16) |
+                  ((long)(d.src_mask != nullptr) << 17) | ((long)(d.dst_mask != nullptr) << 18));
+    key.push_back(g_copy_tune.budget);
+    key.push_back(g_copy_tune.run);
+    key.push_back(g_copy_tune.kernel + 16L * g_copy_tune.nt);
+    for (std::size_t i = 0; i < nd; ++i) {
+        key.push_back(d.size[i]);
+        key.push_back(d.src_stride[i]);
+        key.push_back(d.dst_stride[i]);
+    }
+    CopyLaunch l;
+    bool hit = false;
+    {
+        std::lock_guard<std::mutex> g(g_launch_mutex);
+        auto it = launch_cache().find(key);
+        if (it != launch_cache().end()) {
+            l = it->second;
+            hit = true;
         }
     }
-    if (st == SBX_FLOAT && dt == SBX_DOUBLE) return launch_sd<float, double>(d, n, total, s);
-    if (st == SBX_DOUBLE && dt == SBX_FLOAT) return launch_sd<double, float>(d, n, total, s);
-    if (st == SBX_CFLOAT && dt == SBX_CDOUBLE) return launch_sd<float2, double2>(d, n, total, s);
-    if (st == SBX_CDOUBLE && dt == SBX_CFLOAT) return launch_sd<double2, float2>(d, n, total, s);
-    if (st == SBX_FLOAT && dt == SBX_CFLOAT) return launch_sd<float, float2>(d, n, total, s);
-    if (st == SBX_FLOAT && dt == SBX_CDOUBLE) return launch_sd<float, double2>(d, n, total, s);
-    if (st == SBX_DOUBLE && dt == SBX_CFLOAT) return launch_sd<double, float2>(d, n, total, s);
-    if (st == SBX_DOUBLE && dt == SBX_CDOUBLE) return launch_sd<double, double2>(d, n, total, s);
-    if (st == SBX_INT && dt == SBX_SIZE_T) return launch_sd<int, unsigned long>(d, n, total, s);
-    if (st == SBX_SIZE_T && dt == SBX_INT) return launch_sd<unsigned long, int>(d, n, total, s);
-    throw Error("copy: unsupported type conversion");
+    if (!hit) {
+        l = prepare_launch(d, total);
+        std::lock_guard<std::mutex> g(g_launch_mutex);
+        if (launch_cache().size() >= 4096) launch_cache().clear();
+        launch_cache().emplace(std::move(key), l);
+    }
+    if (CopyTape *t = t_tape) {
+        if (d.src_mask || d.dst_mask)
+            t->valid = false;
+        else
+            t->launches.push_back(TapeLaunch{std::make_shared<CopyLaunch>(l), d.src, d.dst,
+                                             device, d.alpha});
+    }
+    const Alpha alpha{d.alpha.re, d.alpha.im, d.alpha.is_one() ? 1 : 0};
+    l.run(l, d.src, d.dst, alpha, d.src_mask, d.dst_mask, s);
 }
 
 void launch_zero(void *p, std::size_t bytes, int device) {

@@ -178,6 +178,36 @@ struct BoxCopyDesc {
     const float *src_mask = nullptr, *dst_mask = nullptr;
 };
 void launch_box_copy(const BoxCopyDesc &d, int device);
+/// Drop the prepared box-copy launches (clearCaches)
+void clear_copy_launch_cache();
+
+/// Launch tape of one copy() call: the box-copy launches it issued, so that a later call of the
+/// same shape on other pointers replays them without planning (the C ABI's copy fast path;
+/// the reference's plan caches, dist.h:2303-2353).  While a tape is set on the calling thread,
+/// launch_box_copy appends to it; work that is not a plain box-copy launch (masks, peer copies)
+/// marks it invalid.
+struct TapeLaunch {
+    std::shared_ptr<const void> launch; // the prepared launch (kernels_copy.hip)
+    const void *src;                    // pointers and alpha as recorded
+    void *dst;
+    int device;
+    Scalar alpha;
+    // resolved by the recorder's owner: argument (0: origin, 1: destination), component, byte
+    // offset; alpha_is_call: alpha is the call's alpha (else the recorded constant)
+    int src_arg = -1, src_comp = -1, dst_arg = -1, dst_comp = -1;
+    long src_off = 0, dst_off = 0;
+    bool alpha_is_call = false;
+};
+struct CopyTape {
+    std::vector<TapeLaunch> launches;
+    bool valid = true;
+};
+void set_copy_tape(CopyTape *t);
+CopyTape *current_copy_tape();
+/// Issue a recorded launch on new pointers / alpha (library stream of its device)
+void replay_launch(const TapeLaunch &l, const void *src, void *dst, const Scalar &alpha);
+/// Drop the cached copy plans (dist.cpp; clearCaches)
+void clear_copy_plan_cache();
 /// Kernel-shape overrides for tuning runs (0 = the library's choice); set through sbx_tune_set
 struct CopyTune {
     long budget = 0; ///< elements per LDS tile

@@ -413,7 +413,8 @@ LATTICE_GRID = {1: [1, 1, 1], 2: [2, 1, 1], 3: [3, 1, 1], 4: [2, 2, 1], 8: [2, 2
 def case_golden(sb, comm, rank, n, dev):
     grid = LATTICE_GRID.get(n, [n, 1, 1])
     for case in manifest("contraction"):
-        if case.get("gen", "int") == "int" or case["o0"] != "tnsxyzc" or len(case["p0"]) != 1:
+        if (case.get("gen", "int") == "int" or case["o0"] != "tnsxyzc" or len(case["p0"]) != 1
+                or case["t"] != "cdouble"):
             continue
         g0, g1, gr = contraction_inputs(case)
         d0, d1, dr = case["dim0"], case["dim1"], case["dimr"]

@@ -35,6 +35,12 @@ def _run(nprocs, transport, cases=None, shared=False):
            "--nproc-per-node", str(nprocs), "--master-addr", "127.0.0.1", "--master-port",
            str(_free_port()), os.path.join(HERE, "dist_worker.py")]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=420)
+    if r.returncode != 0 or "DIST OK" not in r.stdout:
+        # keep the whole output of a failed multi-rank run (pytest shows only its tail)
+        out = os.path.join(os.path.dirname(HERE), "gpurun_out")
+        if os.path.isdir(out):
+            with open(os.path.join(out, "dist_fail_%s_%d.log" % (transport, nprocs)), "w") as f:
+                f.write(r.stdout + "\n---- stderr ----\n" + r.stderr)
     assert r.returncode == 0 and "DIST OK" in r.stdout, (r.stdout[-3000:], r.stderr[-6000:])
 
 

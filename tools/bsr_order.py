@@ -1,0 +1,88 @@
+#!/usr/bin/env python3
+"""Row-order experiment for the 3x3 lattice BSR (config 3, 16^4, complex<double>; not part of the
+product): the same 9-point operator with its block rows (sites) listed in
+  natural  -- lexicographic x, y, z, t (t fastest), the order of the bench operator;
+  blocked  -- the lattice cut into 8 blocks of 8x8x8x16 (one per XCD: the kernel deals
+              consecutive row chunks to one XCD), each block swept along t with its 8x8x8 plane
+              fastest, so a site's 8 neighbours' x rows are touched within ~3 planes (~2 MB of
+              L2 traffic) instead of 4096 sites apart.
+Only the row order changes (y comes out permuted); the kernel time shows how much of the x
+re-fetch traffic the order removes.  Prints one JSON line per (order, n)."""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import superbblas_amd as sb  # noqa: E402
+
+
+def sites_in_order(L, order):
+    idx = np.arange(L ** 4)
+    if order == "natural":
+        return np.array(np.unravel_index(idx, (L, L, L, L))).T
+    h = L // 2
+    out = []
+    for bx in range(2):
+        for by in range(2):
+            for bz in range(2):
+                t, x, y, z = np.meshgrid(np.arange(L), np.arange(h), np.arange(h), np.arange(h),
+                                         indexing="ij")
+                out.append(np.stack([x.ravel() + bx * h, y.ravel() + by * h, z.ravel() + bz * h,
+                                     t.ravel()], 1))
+    return np.concatenate(out)
+
+
+def main():
+    dev = torch.device("cuda:0")
+    L = 16
+    V = L ** 4
+    for order in ("natural", "blocked"):
+        sites = sites_in_order(L, order)
+        jj = np.zeros((V, 9, 6), np.int32)
+        jj[:, 0, :4] = sites
+        k = 1
+        for d in range(4):
+            for s in (-1, 1):
+                c = sites.copy()
+                c[:, d] = (c[:, d] + s) % L
+                jj[:, k, :4] = c
+                k += 1
+        dim = [L, L, L, L, 1, 3]
+        full = [([0] * 6, dim)]
+        vals = torch.randn(V * 81, dtype=torch.complex128, device=dev)
+        op = sb.create_bsr(full, dim, full, dim, [1, 1, 1, 1, 1, 3], [1, 1, 1, 1, 1, 3], False,
+                           [torch.full((V,), 9, dtype=torch.int32, device=dev)],
+                           [torch.from_numpy(jj.reshape(-1)).to(dev)], [vals])
+        for ncols in (1, 12, 64):
+            dimx = [1, L, L, L, L, 1, 3, ncols]
+            x = torch.randn(V * 3 * ncols, dtype=torch.complex128, device=dev)
+            y = torch.empty_like(x)
+            px = [([0] * 8, dimx)]
+
+            def run():
+                sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", px, "pXYZTSCn", [0] * 8, dimx, dimx,
+                              [x], 0.0, px, "pxyztscn", [0] * 8, dimx, dimx, "p", [y])
+            run()
+            torch.cuda.synchronize()
+            sb.timings_enable(True)
+            sb.timings_filter("bsr")
+            sb.timings_reset()
+            for _ in range(10):
+                run()
+            torch.cuda.synchronize()
+            ms, calls = sb.timings_get("bsr")
+            sb.timings_enable(False)
+            sb.timings_filter(None)
+            t = ms / calls / 1e3
+            by = 16.0 * (81 * V + 2 * 3 * V * ncols) + 4.0 * (9 * V + V + 1)
+            print(json.dumps({"order": order, "n": ncols, "kernel_us": round(t * 1e6, 2),
+                              "GBps": round(by / t / 1e9, 1),
+                              "frac_hbm": round(by / t / 8e12, 4)}), flush=True)
+        op.destroy()
+
+
+if __name__ == "__main__":
+    main()

@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
+#include <string>
 
 static double now() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -14,7 +16,61 @@ __global__ void empty_kernel(double *p) {
     if (threadIdx.x == 1000000) p[0] = 1;
 }
 
-int main() {
+// The reference's dist.cpp permute loop (tests/dist.cpp:237-266) called eagerly from C++: copy
+// an xyztsc field into each of the n slices of tnsxyzc, one sbx_copy per slice, timed with HIP
+// events on the library stream.  Prints one JSON line.
+static int permute(int L, int n4, int reps) {
+    const long vol0 = (long)L * L * L * L * 4 * 3, vol1 = vol0 * n4;
+    void *a, *b;
+    if (hipMalloc(&a, 16 * vol0) != hipSuccess || hipMalloc(&b, 16 * vol1) != hipSuccess) return 1;
+    (void)hipMemset(a, 0, 16 * vol0);
+    int p0[12] = {0, 0, 0, 0, 0, 0, L, L, L, L, 4, 3};
+    int d0[6] = {L, L, L, L, 4, 3}, f0[6] = {0, 0, 0, 0, 0, 0};
+    int p1[14] = {0, 0, 0, 0, 0, 0, 0, L, n4, 4, L, L, L, 3};
+    int d1[7] = {L, n4, 4, L, L, L, 3};
+    sbx_context ctx{SBX_GPU, 0};
+    const void *v0[1] = {a};
+    void *v1[1] = {b};
+    double alpha[2] = {1, 0};
+    hipStream_t s;
+    (void)sbx_stream_get(0, (void **)&s);
+    auto loop = [&]() {
+        for (int k = 0; k < n4; ++k) {
+            int f1[7] = {0, k, 0, 0, 0, 0, 0};
+            if (sbx_copy(6, 7, alpha, SBX_CDOUBLE, SBX_CDOUBLE, p0, 1, "xyztsc", f0, d0, d0, v0,
+                         &ctx, p1, 1, "tnsxyzc", f1, d1, v1, &ctx, nullptr, SBX_SLOW_TO_FAST,
+                         SBX_COPY, 0))
+                return false;
+        }
+        return true;
+    };
+    if (!loop()) {
+        std::printf("{\"error\": \"%s\"}\n", sbx_last_error());
+        return 1;
+    }
+    (void)hipStreamSynchronize(s);
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    const double t0 = now();
+    (void)hipEventRecord(e0, s);
+    for (int r = 0; r < reps; ++r) loop();
+    (void)hipEventRecord(e1, s);
+    const double host = (now() - t0) / reps / n4;
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    const double t = ms / 1e3 / reps;
+    std::printf("{\"op\": \"permute_eager\", \"L\": %d, \"n\": %d, \"ms\": %.4f, \"GBps\": %.1f, "
+                "\"host_us_per_copy\": %.3f}\n",
+                L, n4, t * 1e3, 32.0 * vol1 / t / 1e9, host * 1e6);
+    return 0;
+}
+
+int main(int argc, char **argv) {
+    if (argc >= 2 && std::string(argv[1]) == "permute")
+        return permute(argc > 2 ? std::atoi(argv[2]) : 16, argc > 3 ? std::atoi(argv[3]) : 64,
+                       argc > 4 ? std::atoi(argv[4]) : 5);
     double *a, *b;
     const int L = 4, n4 = 8;
     const long vol0 = (long)L * L * L * L * 4 * 3, vol1 = vol0 * n4;
