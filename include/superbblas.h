@@ -11,12 +11,12 @@
  * Differences from the reference (documented in INTEGRATION.md):
  *  - The distributed overloads take a `superbblas::Communicator` (an sbx_comm: RCCL over xGMI,
  *    or host-staged through a user all-to-all) where the reference takes an MPI_Comm.  With
- *    SUPERBBLAS_USE_MPI defined, MPI_Comm overloads are provided that wrap MPI_Alltoallv.
+ *    SUPERBBLAS_USE_MPI defined, MPI_Comm overloads are provided (RCCL when every rank drives
+ *    its own GPU, else host staging over MPI_Alltoallv).
  *  - Masks (mask0/mask1) must select the same elements (as the reference requires); `session`
- *    must be 0; `request` is always completed on
- *    return (as the reference's no-MPI overloads do, dist.h:3601, 3730).
- *  - Only the ContractWithDomain form of bsr_krylov is implemented (with powers over the okr
- *    label, for plain and Kronecker operators).
+ *    must be 0.  `request` is deferred for distributed copy() and bsr_krylov() (the exchange
+ *    is started; wait() finishes it), complete on return otherwise (as the reference's no-MPI
+ *    overloads, dist.h:3601, 3730).
  */
 #ifndef SUPERBBLAS_AMD_SUPERBBLAS_H
 #define SUPERBBLAS_AMD_SUPERBBLAS_H
@@ -98,6 +98,17 @@ inline void check(int rc) {
     if (rc != SBX_OK) throw std::runtime_error(sbx_last_error());
 }
 
+/// A Request over a C-ABI handle (sbx_wait once; copies of the Request share the handle)
+inline Request request_of(sbx_request h) {
+    if (!h) return Request{};
+    auto shared = std::make_shared<sbx_request>(h);
+    return [shared]() {
+        sbx_request r = *shared;
+        *shared = nullptr;
+        if (r) check(sbx_wait(r));
+    };
+}
+
 template <typename T> struct dtype;
 template <> struct dtype<float> { static constexpr int value = SBX_FLOAT; };
 template <> struct dtype<double> { static constexpr int value = SBX_DOUBLE; };
@@ -144,13 +155,15 @@ void copy_impl(typename elem<T>::type alpha, const PartitionItem<Nd0> *p0, int n
     check_session(session);
     const auto a = scalar(alpha);
     const auto c0 = contexts(ctx0, ncomponents0), c1 = contexts(ctx1, ncomponents1);
-    check(sbx_copy_masked((int)Nd0, (int)Nd1, a.data(), dtype<T>::value, dtype<Q>::value,
-                          parts(p0), ncomponents0, o0, from0.data(), size0.data(), dim0.data(),
-                          (const void *const *)v0, (const float *const *)mask0, c0.data(),
-                          parts(p1), ncomponents1, o1, from1.data(), dim1.data(),
-                          (void *const *)v1, (const float *const *)mask1, c1.data(), comm,
-                          co_of(co), copyadd == Copy ? SBX_COPY : SBX_ADD, 0));
-    if (request) *request = Request{};
+    sbx_request h = nullptr;
+    check(sbx_copy_req((int)Nd0, (int)Nd1, a.data(), dtype<T>::value, dtype<Q>::value,
+                       parts(p0), ncomponents0, o0, from0.data(), size0.data(), dim0.data(),
+                       (const void *const *)v0, (const float *const *)mask0, c0.data(),
+                       parts(p1), ncomponents1, o1, from1.data(), dim1.data(),
+                       (void *const *)v1, (const float *const *)mask1, c1.data(), comm,
+                       co_of(co), copyadd == Copy ? SBX_COPY : SBX_ADD, 0,
+                       request ? &h : nullptr));
+    if (request) *request = request_of(h);
 }
 
 template <std::size_t Nd0, std::size_t Nd1, std::size_t Ndo, typename T>
@@ -226,16 +239,18 @@ void bsr_krylov_impl(T alpha, BSR_handle *bsrh, const char *oim, const char *odm
                      const T **vx, T beta, const PartitionItem<Ny> *py, const char *oy,
                      const Coor<Ny> &fromy, const Coor<Ny> &sizey, const Coor<Ny> &dimy,
                      char okr, T **vy, const Context *ctx, sbx_comm comm, CoorOrder co,
-                     Request *request, Session session) {
+                     Request *request, Session session, bool just_local = false) {
     check_session(session);
     const auto a = scalar(alpha), b = scalar(beta);
     const auto c = contexts(ctx, ncomponents);
-    check(sbx_bsr_krylov(reinterpret_cast<sbx_bsr>(bsrh), (int)Nd, (int)Ni, (int)Nx, (int)Ny,
-                         dtype<T>::value, a.data(), oim, odm, parts(px), ncomponents, ox,
-                         fromx.data(), sizex.data(), dimx.data(), (const void *const *)vx,
-                         b.data(), parts(py), oy, fromy.data(), sizey.data(), dimy.data(), okr,
-                         (void *const *)vy, c.data(), comm, co_of(co), 0));
-    if (request) *request = Request{};
+    sbx_request h = nullptr;
+    check(sbx_bsr_krylov_req(reinterpret_cast<sbx_bsr>(bsrh), (int)Nd, (int)Ni, (int)Nx, (int)Ny,
+                             dtype<T>::value, a.data(), oim, odm, parts(px), ncomponents, ox,
+                             fromx.data(), sizex.data(), dimx.data(), (const void *const *)vx,
+                             b.data(), parts(py), oy, fromy.data(), sizey.data(), dimy.data(),
+                             okr, (void *const *)vy, c.data(), comm, co_of(co), 0,
+                             just_local ? 1 : 0, request ? &h : nullptr));
+    if (request) *request = request_of(h);
 }
 
 } // namespace sbx_detail
@@ -526,11 +541,10 @@ void bsr_krylov(T alpha, BSR_handle *bsrh, const char *oim, const char *odm,
                 const Coor<Ny> &sizey, const Coor<Ny> &dimy, char okr, T **vy,
                 const Context *ctx, Communicator comm, CoorOrder co, Request *request = nullptr,
                 bool just_local = false, Session session = 0) {
-    if (just_local) throw std::runtime_error("bsr_krylov: just_local is not supported");
     sbx_detail::bsr_krylov_impl<Nd, Ni, Nx, Ny, T>(alpha, bsrh, oim, odm, px, ncomponents, ox,
                                                    fromx, sizex, dimx, vx, beta, py, oy, fromy,
                                                    sizey, dimy, okr, vy, ctx, comm, co, request,
-                                                   session);
+                                                   session, just_local);
 }
 
 template <std::size_t Nd, std::size_t Ni, typename T>
@@ -1047,11 +1061,10 @@ void bsr_krylov(T alpha, BSR_handle *bsrh, const char *oim, const char *odm,
                 const Coor<Ny> &sizey, const Coor<Ny> &dimy, char okr, T **vy,
                 const Context *ctx, MPI_Comm mpicomm, CoorOrder co, Request *request = nullptr,
                 bool just_local = false, Session session = 0) {
-    if (just_local) throw std::runtime_error("bsr_krylov: just_local is not supported");
     sbx_detail::bsr_krylov_impl<Nd, Ni, Nx, Ny, T>(
         alpha, bsrh, oim, odm, px, ncomponents, ox, fromx, sizex, dimx, vx, beta, py, oy, fromy,
         sizey, dimy, okr, vy, ctx, sbx_detail::comm_of(mpicomm, ctx, ncomponents), co, request,
-        session);
+        session, just_local);
 }
 template <std::size_t N, typename T>
 void cholesky(const PartitionItem<N> *p, const Coor<N> &dim, int ncomponents, const char *o,

@@ -178,6 +178,25 @@ int sbx_copy_masked(int nd0, int nd1, const double *alpha, int t0, int t1, const
                     const float *const *mask1, const sbx_context *ctx1, sbx_comm comm, int co,
                     int copyadd, int session);
 
+/* ---- deferred completion (the reference's Request, dist.h:54-61, 2386-2437) ----
+   The _req entry points take the same arguments as their plain forms plus `request`.  When the
+   operation exchanges data with other ranks, the call returns once the exchange is started --
+   RCCL: packed and sent / received on the library's side stream, so later library-stream work
+   (e.g. the product of another operator piece) overlaps the transfer; host-staged: packed --
+   and *request receives a handle whose sbx_wait finishes it (unpack, and for bsr_krylov the
+   local product and the output copies).  Otherwise the call completes and *request is NULL.
+   As in the reference every rank must wait its requests, in the same order; the outputs are
+   defined only after sbx_wait (then, as always, stream-ordered on the library stream). */
+typedef struct sbx_request_s *sbx_request;
+int sbx_wait(sbx_request request); /* NULL: no-op; the handle is freed */
+int sbx_copy_req(int nd0, int nd1, const double *alpha, int t0, int t1, const int *p0,
+                 int ncomponents0, const char *o0, const int *from0, const int *size0,
+                 const int *dim0, const void *const *v0, const float *const *mask0,
+                 const sbx_context *ctx0, const int *p1, int ncomponents1, const char *o1,
+                 const int *from1, const int *dim1, void *const *v1, const float *const *mask1,
+                 const sbx_context *ctx1, sbx_comm comm, int co, int copyadd, int session,
+                 sbx_request *request);
+
 /* Exchange plan of sbx_copy as seen by `rank` of `nprocs` (host only, no GPU work; the
    reference get_indices_to_send / get_indices_to_receive, dist.h:1789-1900, 2321-2324):
    send[q] / recv[q] = elements sent to / received from rank q, *local = elements moved within
@@ -230,6 +249,16 @@ int sbx_bsr_krylov(sbx_bsr bsrh, int nd, int ni, int nx, int ny, int t, const do
                    const void *const *vx, const double *beta, const int *py, const char *oy,
                    const int *fromy, const int *sizey, const int *dimy, char okr,
                    void *const *vy, const sbx_context *ctx, sbx_comm comm, int co, int session);
+/* bsr_krylov with the reference's `just_local` (bsr.h:2352-2359: only this rank's part of the
+   product, no exchange; the other ranks' components are ignored) and deferred completion (the
+   halo exchange started, the local product queued at sbx_wait; see sbx_request above) */
+int sbx_bsr_krylov_req(sbx_bsr bsrh, int nd, int ni, int nx, int ny, int t, const double *alpha,
+                       const char *oim, const char *odm, const int *px, int ncomponents,
+                       const char *ox, const int *fromx, const int *sizex, const int *dimx,
+                       const void *const *vx, const double *beta, const int *py, const char *oy,
+                       const int *fromy, const int *sizey, const int *dimy, char okr,
+                       void *const *vy, const sbx_context *ctx, sbx_comm comm, int co,
+                       int session, int just_local, sbx_request *request);
 int sbx_bsr_get_preferred_layout(sbx_bsr bsrh, int ncomponents, const sbx_context *ctx,
                                  sbx_comm comm, int co, int *layout_x, int *layout_y);
 int sbx_destroy_bsr(sbx_bsr bsrh);

@@ -138,6 +138,35 @@ _lib.sbx_copy.argtypes = [_I, _I, _VP, _I, _I, _VP, _I, ctypes.c_char_p, _VP, _V
 _lib.sbx_copy_masked.argtypes = [_I, _I, _VP, _I, _I, _VP, _I, ctypes.c_char_p, _VP, _VP, _VP,
                                  _VP, _VP, _VP, _VP, _I, ctypes.c_char_p, _VP, _VP, _VP, _VP, _VP,
                                  _VP, _I, _I, _I]
+_lib.sbx_copy_req.argtypes = _lib.sbx_copy_masked.argtypes + [_VP]
+_lib.sbx_wait.argtypes = [_VP]
+
+
+class Request:
+    """Deferred completion of a distributed copy / bsr_krylov (the reference's Request,
+    dist.h:54-61): the exchange is started; wait() finishes it.  Every rank waits its requests in
+    the same order."""
+
+    def __init__(self, handle):
+        self._h = handle
+
+    def wait(self):
+        if self._h:
+            h, self._h = self._h, None
+            _check(_lib.sbx_wait(h))
+
+    def __del__(self):  # a dropped request is still completed (in this process's call order)
+        try:
+            self.wait()
+        except Exception:
+            pass
+
+
+def wait(request: Optional["Request"]):
+    if request is not None:
+        request.wait()
+
+
 _lib.sbx_contraction.argtypes = (
     [_I, _I, _I, _I, _VP] +
     [_VP, _VP, _VP, _VP, _I, ctypes.c_char_p, _I, _VP, _VP] * 2 + [_VP] +
@@ -461,10 +490,11 @@ def make_hole(frm, size, hole_from, hole_size, dim):
 def copy(alpha, p0, o0: str, from0, size0, dim0, v0: Sequence[torch.Tensor], p1, o1: str, from1,
          dim1, v1: Sequence[torch.Tensor], co: int = SlowToFast, copyadd: int = Copy,
          comm: Optional[Comm] = None, mask0: Optional[Sequence[torch.Tensor]] = None,
-         mask1: Optional[Sequence[torch.Tensor]] = None):
+         mask1: Optional[Sequence[torch.Tensor]] = None, request: bool = False):
     """v1[from1 + P(c - from0)] (=|+=) alpha * v0[c]  for c in [from0, from0 + size0);
     with masks (float32 tensors shaped like the components, dist.h:3534-3602) only where the
-    masks are nonzero."""
+    masks are nonzero.  request=True: returns a Request (the exchange of a distributed copy
+    started, finished by its wait()) or None when the copy completed."""
     nprocs, rank = _nprocs_rank(comm)
     nd0, nd1 = len(o0), len(o1)
     nc0, nc1 = len(v0), len(v1)
@@ -487,7 +517,7 @@ def copy(alpha, p0, o0: str, from0, size0, dim0, v0: Sequence[torch.Tensor], p1,
     k.add_ctxs(v1)
     k.add_ptrs(v0)
     k.add_ptrs(v1)
-    if mask0 is None and mask1 is None:
+    if mask0 is None and mask1 is None and not request:
         a, pp = k.addrs()
         _check(_lib.sbx_copy(nd0, nd1, _scalar(alpha), t0, t1, a[0], nc0, o0.encode(), a[1], a[2],
                              a[3], pp[0], a[4], a[5], nc1, o1.encode(), a[6], a[7], pp[1], a[8],
@@ -500,11 +530,14 @@ def copy(alpha, p0, o0: str, from0, size0, dim0, v0: Sequence[torch.Tensor], p1,
     k.add_ptrs(mask0 or [])
     k.add_ptrs(mask1 or [])
     a, pp = k.addrs()
-    _check(_lib.sbx_copy_masked(nd0, nd1, _scalar(alpha), t0, t1, a[0], nc0, o0.encode(), a[1],
-                                a[2], a[3], pp[0], pp[2] if mask0 is not None else None, a[4],
-                                a[5], nc1, o1.encode(), a[6], a[7], pp[1],
-                                pp[3] if mask1 is not None else None, a[8], _comm(comm), co,
-                                copyadd, 0))
+    h = ctypes.c_void_p()
+    _check(_lib.sbx_copy_req(nd0, nd1, _scalar(alpha), t0, t1, a[0], nc0, o0.encode(), a[1],
+                             a[2], a[3], pp[0], pp[2] if mask0 is not None else None, a[4],
+                             a[5], nc1, o1.encode(), a[6], a[7], pp[1],
+                             pp[3] if mask1 is not None else None, a[8], _comm(comm), co,
+                             copyadd, 0, ctypes.byref(h) if request else None))
+    if request:
+        return Request(h.value) if h.value else None
 
 
 def copy_plan(p0, o0: str, from0, size0, dim0, ncomponents0: int, p1, o1: str, from1, dim1,
@@ -653,17 +686,23 @@ def create_kron_bsr(pim, dimi, pdm, dimd, blockim, blockdm, kronim, krondm, bloc
 
 def bsr_krylov(alpha, bsr: BSR, oim: str, odm: str, px, ox: str, fromx, sizex, dimx, vx, beta,
                py, oy: str, fromy, sizey, dimy, okr: Optional[str], vy, co: int = SlowToFast,
-               comm: Optional[Comm] = None):
-    """y = alpha * A x (+ beta y) (bsr.h:2516-2543)."""
+               comm: Optional[Comm] = None, request: bool = False, just_local: bool = False):
+    """y = alpha * A x (+ beta y) (bsr.h:2516-2543; MPI form 2352-2383).  just_local: only this
+    rank's part, no exchange.  request=True: returns a Request when the halo exchange is left in
+    flight (the local product runs at its wait()), else None."""
     nx, ny = len(ox), len(oy)
     nc = len(vx)
     t = _dtype_of(list(vx) + list(vy))
     _bind_stream(list(vx) + list(vy))
-    _check(_lib.sbx_bsr_krylov(
+    h = ctypes.c_void_p()
+    _check(_lib.sbx_bsr_krylov_req(
         bsr.handle, bsr.nd, bsr.ni, nx, ny, t, _scalar(alpha), oim.encode(), odm.encode(),
         _partition(px, nx), nc, ox.encode(), _ints(fromx), _ints(sizex), _ints(dimx), _ptrs(vx),
         _scalar(beta), _partition(py, ny), oy.encode(), _ints(fromy), _ints(sizey), _ints(dimy),
-        ctypes.c_char((okr or "\0").encode()), _ptrs(vy), _ctxs(vx), _comm(comm), co, 0))
+        ctypes.c_char((okr or "\0").encode()), _ptrs(vy), _ctxs(vx), _comm(comm), co, 0,
+        int(just_local), ctypes.byref(h) if request else None))
+    if request:
+        return Request(h.value) if h.value else None
 
 
 def _inplace_dense(fn, p, dim, o: str, v, orows: str, ocols: str, co, comm):
@@ -905,7 +944,7 @@ __all__ = [
     "SlowToFast", "FastToSlow", "Copy", "Add", "RowMajor", "ColumnMajor", "SuperbblasError",
     "Comm", "copy", "copy_plan", "contraction", "local_copy", "xgemm_batch_strided", "create_bsr",
     "create_kron_bsr", "cholesky", "inversion", "trsm", "gesm",
-    "bsr_krylov", "bsr_get_preferred_layout", "basic_partitioning", "basic_partitioning_ext",
+    "bsr_krylov", "bsr_get_preferred_layout", "Request", "wait", "basic_partitioning", "basic_partitioning_ext",
     "partitioning_distributed_procs", "make_hole", "sync", "stream", "set_stream",
     "clear_caches", "timings_enable", "timings_reset", "timings_get", "timings_report",
     "get_gpu_devices_count", "version", "LIB_PATH", "Storage", "NoChecksum", "GlobalChecksum",

@@ -18,6 +18,8 @@
 #include "plan.h"
 
 #include <algorithm>
+#include <functional>
+#include <memory>
 
 namespace sbx {
 
@@ -307,12 +309,29 @@ Layout dense_layout(const std::string &spatial, const std::string &cl, const std
 } // namespace
 
 void bsr_krylov(const BsrOp &op, const Scalar &alpha, const std::string &oi,
-                const std::string &od, const DistTensor &x, const Coor &fromx, const Coor &sizex,
-                const Scalar &beta, const DistTensor &y, const Coor &fromy, const Coor &sizey,
-                char okr, const Comm &comm) {
+                const std::string &od, const DistTensor &x_in, const Coor &fromx,
+                const Coor &sizex, const Scalar &beta, const DistTensor &y_in, const Coor &fromy,
+                const Coor &sizey, char okr, const Comm &comm_in, bool just_local,
+                std::function<void()> *deferred) {
+    if (deferred) *deferred = nullptr;
     if ((int)oi.size() != op.ni || (int)od.size() != op.nd)
         throw Error("bsr_krylov: labels don't match the operator");
-    if (comm.nprocs != op.nprocs) throw Error("bsr_krylov: communicator mismatch");
+    if (comm_in.nprocs != op.nprocs) throw Error("bsr_krylov: communicator mismatch");
+    // just_local (bsr.h:2020-2075, 2188): only this rank's part of the product, no exchange --
+    // the other ranks' components are ignored and every copy stays on this process
+    const bool local_only = just_local && comm_in.nprocs > 1;
+    Comm comm = comm_in;
+    DistTensor x = x_in, y = y_in;
+    const int base = local_only ? op.rank : 0; // op.pi / op.pd index of rank 0 of `comm`
+    if (local_only) {
+        comm.nprocs = 1;
+        comm.rank = 0;
+        comm.nccl = nullptr;
+        comm.host_fn = nullptr;
+        comm.stage = nullptr;
+        x.ranges = {x_in.ranges[comm_in.rank]};
+        y.ranges = {y_in.ranges[comm_in.rank]};
+    }
     // Contraction with the image side (x has image labels, y domain labels): y = alpha A^H x,
     // applied as the transposed operator (bsr.h:1737-1760 kinds, 1942 transSp)
     bool x_image = false, x_domain = false;
@@ -325,8 +344,8 @@ void bsr_krylov(const BsrOp &op, const Scalar &alpha, const std::string &oi,
                     "of the sparse tensor");
     if (x_image) {
         if (!op.transposed) op.transposed.reset(make_transposed(op));
-        return bsr_krylov(*op.transposed, alpha, od, oi, x, fromx, sizex, beta, y, fromy, sizey,
-                          okr, comm);
+        return bsr_krylov(*op.transposed, alpha, od, oi, x_in, fromx, sizex, beta, y_in, fromy,
+                          sizey, okr, comm_in, just_local, deferred);
     }
     // Label classes (bsr.h:1722-1795): x has domain labels + C (+ okr); y image labels + C (+okr)
     std::string C;
@@ -433,12 +452,14 @@ void bsr_krylov(const BsrOp &op, const Scalar &alpha, const std::string &oi,
         Layout lxl{}, lyl{};
     };
     std::vector<std::vector<CompPlan>> plans(comm.nprocs);
-    std::vector<Scratch> bufs;
+    auto bufs_p = std::make_shared<std::vector<Scratch>>(); // temporaries (live until the end)
+    std::vector<Scratch> &bufs = *bufs_p;
+    bufs.reserve(4 * op.pi[op.rank].size());
     std::vector<void *> my_x, my_y;
     std::vector<Layout> my_lx, my_ly;
     for (int rk = 0; rk < comm.nprocs; ++rk) {
-        for (int c = 0; c < (int)op.pi[rk].size(); ++c) {
-            const Range &rd = op.pd[rk][c], &ri = op.pi[rk][c];
+        for (int c = 0; c < (int)op.pi[base + rk].size(); ++c) {
+            const Range &rd = op.pd[base + rk][c], &ri = op.pi[base + rk][c];
             const Range nx{arrange(lx, od, rd.from, zeroC), arrange(lx, od, rd.size, sizeC)};
             const Range ny{arrange(ly, oi, ri.from, zeroC), arrange(ly, oi, ri.size, sizeC)};
             CompPlan cp;
@@ -525,77 +546,93 @@ void bsr_krylov(const BsrOp &op, const Scalar &alpha, const std::string &oi,
     bool need_x = false, need_y = false;
     for (auto &r : tx.ranges) need_x |= !r.empty();
     for (auto &r : ty.ranges) need_y |= !r.empty();
+    std::function<void()> x_pending; // the halo exchange's unpack, when deferred
     if (need_x) {
         Coor from1(lx.size(), 0);
-        dist_copy(Scalar{1, 0}, x, fromx, sizex, tx, from1, false, comm);
+        dist_copy(Scalar{1, 0}, x, fromx, sizex, tx, from1, false, comm,
+                  deferred ? &x_pending : nullptr);
     }
-    // Output scaling for the in-place path
+    // Output scaling (before the product, on the library stream)
     const bool direct_all = !need_y;
     if (direct_all && !beta.is_zero() && !beta.is_one())
         dist_copy(beta, y, fromy, sizey, y, fromy, false, comm);
-
-    const Coor from0(ly.size(), 0), size0 = ty.dim;
     if (need_y && !beta.is_zero() && !beta.is_one())
         dist_copy(beta, y, fromy, sizey, y, fromy, false, comm);
     // overlapping image pieces (A^H with a halo domain) are summed: add into a zeroed output
     const bool add_y = !beta.is_zero() || op.image_overlaps;
     if (need_y && beta.is_zero() && op.image_overlaps)
         dist_copy(Scalar{0, 0}, y, fromy, sizey, y, fromy, false, comm);
-    const int power_pos = okr != 0 ? (int)y.labels.find(okr) : -1;
-    for (int pw = 0; pw < power; ++pw) {
-        // Local SpMM
-        for (int c = 0; c < (int)op.comps.size(); ++c) {
-            const BsrComp &bc = op.comps[c];
-            if (bc.block_rows == 0) continue;
-            BsrDesc d;
-            d.t = dtype;
-            d.block_rows = bc.block_rows;
-            d.bi = bi;
-            d.bd = bd;
-            d.ii = bc.ii;
-            d.jj = bc.jj;
-            d.v = bc.v;
-            d.block_im_fast = op.block_im_fast;
-            d.num_nnz_per_row = bc.nnz_per_row;
-            d.x = my_x[c];
-            d.x_row_major = my_lx[c].row_major;
-            d.ldx = my_lx[c].ld;
-            d.y = my_y[c];
-            d.y_row_major = my_ly[c].row_major;
-            d.ldy = my_ly[c].ld;
-            d.ncols = volC;
-            d.alpha = pw == 0 ? alpha : Scalar{1, 0};
-            d.add = plans[comm.rank][c].ydirect ? !beta.is_zero() : false;
-            if (op.is_kron) {
-                d.ki = (int)volume(op.kroni);
-                d.kd = (int)volume(op.krond);
-                d.kron = bc.kron;
-                launch_bsr_kron(d, bc.dev);
+
+    // the local products and the output copies; deferred behind the halo exchange when asked
+    // (the reference's bsr_req, bsr.h:2199-2257)
+    const BsrOp *opp = &op;
+    auto product = [=]() {
+        const BsrOp &op = *opp;
+        std::vector<Scratch> &keep = *bufs_p; // temporaries stay alive through the product
+        (void)keep;
+        if (x_pending) x_pending();
+        const Coor from0(ly.size(), 0), size0 = ty.dim;
+        const int power_pos = okr != 0 ? (int)y.labels.find(okr) : -1;
+        for (int pw = 0; pw < power; ++pw) {
+            // Local SpMM
+            for (int c = 0; c < (int)op.comps.size(); ++c) {
+                const BsrComp &bc = op.comps[c];
+                if (bc.block_rows == 0) continue;
+                BsrDesc d;
+                d.t = dtype;
+                d.block_rows = bc.block_rows;
+                d.bi = bi;
+                d.bd = bd;
+                d.ii = bc.ii;
+                d.jj = bc.jj;
+                d.v = bc.v;
+                d.block_im_fast = op.block_im_fast;
+                d.num_nnz_per_row = bc.nnz_per_row;
+                d.x = my_x[c];
+                d.x_row_major = my_lx[c].row_major;
+                d.ldx = my_lx[c].ld;
+                d.y = my_y[c];
+                d.y_row_major = my_ly[c].row_major;
+                d.ldy = my_ly[c].ld;
+                d.ncols = volC;
+                d.alpha = pw == 0 ? alpha : Scalar{1, 0};
+                d.add = plans[comm.rank][c].ydirect ? !beta.is_zero() : false;
+                if (op.is_kron) {
+                    d.ki = (int)volume(op.kroni);
+                    d.kd = (int)volume(op.krond);
+                    d.kron = bc.kron;
+                    launch_bsr_kron(d, bc.dev);
+                } else {
+                    launch_bsr(d, bc.dev);
+                }
+            }
+            // Copy/add the image pieces into y (power pw at okr = fromy[okr] + pw)
+            if (need_y) {
+                Coor fy = fromy;
+                if (power_pos >= 0)
+                    fy[power_pos] = (int)normalize_coor((long)fy[power_pos] + pw, y.dim[power_pos]);
+                dist_copy(Scalar{1, 0}, ty, from0, size0, y, fy, add_y, comm);
+            }
+            if (pw + 1 == power) break;
+            // The next power applies the operator to this one: the image pieces, relabelled as
+            // domain coordinates, become x (with the halo of the domain partition)
+            DistTensor ty_as_x = ty;
+            for (char &ch : ty_as_x.labels)
+                if (oi.find(ch) != std::string::npos) ch = od[oi.find(ch)];
+            Coor zx(lx.size(), 0);
+            if (op.image_overlaps) {
+                dist_copy(Scalar{0, 0}, tx, zx, tx.dim, tx, zx, false, comm);
+                dist_copy(Scalar{1, 0}, ty_as_x, zx, size0, tx, zx, true, comm);
             } else {
-                launch_bsr(d, bc.dev);
+                dist_copy(Scalar{1, 0}, ty_as_x, zx, size0, tx, zx, false, comm);
             }
         }
-        // Copy/add the image pieces into y (power pw at okr = fromy[okr] + pw)
-        if (need_y) {
-            Coor fy = fromy;
-            if (power_pos >= 0)
-                fy[power_pos] = (int)normalize_coor((long)fy[power_pos] + pw, y.dim[power_pos]);
-            dist_copy(Scalar{1, 0}, ty, from0, size0, y, fy, add_y, comm);
-        }
-        if (pw + 1 == power) break;
-        // The next power applies the operator to this one: the image pieces, relabelled as
-        // domain coordinates, become x (with the halo of the domain partition)
-        DistTensor ty_as_x = ty;
-        for (char &ch : ty_as_x.labels)
-            if (oi.find(ch) != std::string::npos) ch = od[oi.find(ch)];
-        Coor zx(lx.size(), 0);
-        if (op.image_overlaps) {
-            dist_copy(Scalar{0, 0}, tx, zx, tx.dim, tx, zx, false, comm);
-            dist_copy(Scalar{1, 0}, ty_as_x, zx, size0, tx, zx, true, comm);
-        } else {
-            dist_copy(Scalar{1, 0}, ty_as_x, zx, size0, tx, zx, false, comm);
-        }
-    }
+
+    };
+    if (deferred && x_pending)
+        *deferred = product;
+    else
+        product();
 }
 
 } // namespace sbx

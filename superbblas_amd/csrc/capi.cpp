@@ -5,6 +5,7 @@
 // and every flop runs on the GPU, and turns C++ exceptions into status codes.
 #include "plan.h"
 #include <algorithm>
+#include <functional>
 #include <memory>
 #include <unordered_map>
 
@@ -25,7 +26,8 @@ void bsr_destroy(BsrOp *op);
 void bsr_krylov(const BsrOp &op, const Scalar &alpha, const std::string &oi,
                 const std::string &od, const DistTensor &x, const Coor &fromx, const Coor &sizex,
                 const Scalar &beta, const DistTensor &y, const Coor &fromy, const Coor &sizey,
-                char okr, const Comm &comm);
+                char okr, const Comm &comm, bool just_local = false,
+                std::function<void()> *deferred = nullptr);
 void set_user_stream(int device, hipStream_t s, bool has_user);
 void destroy_streams();
 void trim_pools();
@@ -229,6 +231,10 @@ sbx_storage_s &storage_of(sbx_storage sto) {
 }
 
 } // namespace
+
+struct sbx_request_s {
+    std::function<void()> fn; // the pending part of the operation
+};
 
 namespace {
 //
@@ -573,6 +579,14 @@ int sbx_make_hole(int nd, const int *from, const int *size, const int *hole_from
     });
 }
 
+int sbx_wait(sbx_request request) {
+    return guard([&] {
+        if (!request) return;
+        std::unique_ptr<sbx_request_s> r(request);
+        if (r->fn) r->fn();
+    });
+}
+
 int sbx_copy_masked(int nd0, int nd1, const double *alpha, int t0, int t1, const int *p0,
                     int ncomponents0, const char *o0, const int *from0, const int *size0,
                     const int *dim0, const void *const *v0, const float *const *mask0,
@@ -580,6 +594,19 @@ int sbx_copy_masked(int nd0, int nd1, const double *alpha, int t0, int t1, const
                     const int *from1, const int *dim1, void *const *v1,
                     const float *const *mask1, const sbx_context *ctx1, sbx_comm comm, int co,
                     int copyadd, int session) {
+    return sbx_copy_req(nd0, nd1, alpha, t0, t1, p0, ncomponents0, o0, from0, size0, dim0, v0,
+                        mask0, ctx0, p1, ncomponents1, o1, from1, dim1, v1, mask1, ctx1, comm, co,
+                        copyadd, session, nullptr);
+}
+
+int sbx_copy_req(int nd0, int nd1, const double *alpha, int t0, int t1, const int *p0,
+                 int ncomponents0, const char *o0, const int *from0, const int *size0,
+                 const int *dim0, const void *const *v0, const float *const *mask0,
+                 const sbx_context *ctx0, const int *p1, int ncomponents1, const char *o1,
+                 const int *from1, const int *dim1, void *const *v1, const float *const *mask1,
+                 const sbx_context *ctx1, sbx_comm comm, int co, int copyadd, int session,
+                 sbx_request *request) {
+    if (request) *request = nullptr;
     return guard([&] {
         check_session(session);
         check_copy_types(t0, t1);
@@ -642,14 +669,17 @@ int sbx_copy_masked(int nd0, int nd1, const double *alpha, int t0, int t1, const
         attach_masks(b, mask1, ncomponents1, ctx1, c, m);
         auto tape = fast ? std::make_shared<CopyTape>() : nullptr;
         set_copy_tape(tape.get());
+        std::function<void()> pending;
         try {
             dist_copy(a_call, a, to_coor(from0, nd0, rev), to_coor(size0, nd0, rev), b,
-                      to_coor(from1, nd1, rev), copyadd == SBX_ADD, c);
+                      to_coor(from1, nd1, rev), copyadd == SBX_ADD, c,
+                      request && !m.any ? &pending : nullptr);
         } catch (...) {
             set_copy_tape(nullptr);
             throw;
         }
         set_copy_tape(nullptr);
+        if (pending) *request = new sbx_request_s{pending};
         finish_mirror(m);
         if (tape && tape->valid) {
             // resolve the recorded pointers against the components (p0/p1 in the caller's
@@ -841,6 +871,19 @@ int sbx_bsr_krylov(sbx_bsr bsrh, int nd, int ni, int nx, int ny, int t, const do
                    const void *const *vx, const double *beta, const int *py, const char *oy,
                    const int *fromy, const int *sizey, const int *dimy, char okr,
                    void *const *vy, const sbx_context *ctx, sbx_comm comm, int co, int session) {
+    return sbx_bsr_krylov_req(bsrh, nd, ni, nx, ny, t, alpha, oim, odm, px, ncomponents, ox,
+                              fromx, sizex, dimx, vx, beta, py, oy, fromy, sizey, dimy, okr, vy,
+                              ctx, comm, co, session, 0, nullptr);
+}
+
+int sbx_bsr_krylov_req(sbx_bsr bsrh, int nd, int ni, int nx, int ny, int t, const double *alpha,
+                       const char *oim, const char *odm, const int *px, int ncomponents,
+                       const char *ox, const int *fromx, const int *sizex, const int *dimx,
+                       const void *const *vx, const double *beta, const int *py, const char *oy,
+                       const int *fromy, const int *sizey, const int *dimy, char okr,
+                       void *const *vy, const sbx_context *ctx, sbx_comm comm, int co,
+                       int session, int just_local, sbx_request *request) {
+    if (request) *request = nullptr;
     return guard([&] {
         check_session(session);
         if (!bsrh || !bsrh->op) throw Error("bsr_krylov: invalid handle");
@@ -856,10 +899,13 @@ int sbx_bsr_krylov(sbx_bsr bsrh, int nd, int ni, int nx, int ny, int t, const do
         DistTensor x = make_tensor(nx, ox, dimx, px, ncomponents, vx, ctx, t, c, rev, m, false, "ox");
         DistTensor y = make_tensor(ny, oy, dimy, py, ncomponents, (const void *const *)vy, ctx, t,
                                    c, rev, m, true, "oy");
+        std::function<void()> pending;
         bsr_krylov(*bsrh->op, to_scalar(alpha), to_labels(oim, ni, rev, "oim"),
                    to_labels(odm, nd, rev, "odm"), x, to_coor(fromx, nx, rev),
                    to_coor(sizex, nx, rev), to_scalar(beta), y, to_coor(fromy, ny, rev),
-                   to_coor(sizey, ny, rev), okr, c);
+                   to_coor(sizey, ny, rev), okr, c, just_local != 0,
+                   request && !m.any ? &pending : nullptr);
+        if (pending) *request = new sbx_request_s{pending};
         finish_mirror(m);
     });
 }

@@ -385,7 +385,9 @@ void copy_plan_counts(const DistTensor &src, const Coor &from0, const Coor &size
 }
 
 void dist_copy(const Scalar &alpha, const DistTensor &src, const Coor &from0, const Coor &size0,
-               const DistTensor &dst, const Coor &from1, bool add, const Comm &comm) {
+               const DistTensor &dst, const Coor &from1, bool add, const Comm &comm,
+               std::function<void()> *deferred) {
+    if (deferred) *deferred = nullptr;
     if ((int)src.ranges.size() != comm.nprocs || (int)dst.ranges.size() != comm.nprocs)
         throw Error("copy: partition is incompatible with the communicator");
     if (src.nd() != (int)from0.size() || src.nd() != (int)size0.size() ||
@@ -441,6 +443,8 @@ void dist_copy(const Scalar &alpha, const DistTensor &src, const Coor &from0, co
         zero_region();
         return;
     }
+    // Add with alpha == 0 leaves the destination untouched (copy_n.h:92, dist.h:2383)
+    if (add && alpha.is_zero()) return;
 
     const std::shared_ptr<const CopyPlan> plan =
         get_copy_plan(src, from0, size0, dst, from1, region1, add, comm.rank);
@@ -497,13 +501,22 @@ void dist_copy(const Scalar &alpha, const DistTensor &src, const Coor &from0, co
         send_off[q + 1] = send_off[q] + (send_bytes[q] + 255) / 256 * 256;
         recv_off[q + 1] = recv_off[q] + (recv_bytes[q] + 255) / 256 * 256;
     }
-    if (send_off[comm.nprocs] == 0 && recv_off[comm.nprocs] == 0) {
-        // nothing to exchange for this rank, but peers may still exchange among themselves
-    }
-    Scratch sbuf(send_off[comm.nprocs], device), rbuf(recv_off[comm.nprocs], device);
+    if (!comm.nccl && !(comm.host_fn && comm.stage))
+        throw Error("copy: the communicator has no transport");
     std::vector<int> id(src.nd());
     for (int k = 0; k < src.nd(); ++k) id[k] = k;
+    set_device(device);
+    const hipStream_t main_s = get_stream(device);
+    // deferred RCCL exchange: pack, send and receive on the side stream (after the work queued so
+    // far on the library stream), so that later library-stream work overlaps the transfer
+    const bool side = deferred && comm.nccl;
+    const hipStream_t ex_s = side ? get_side_stream(device) : main_s;
+    if (side) stream_after(ex_s, main_s);
+    auto sbuf = std::make_shared<Scratch>(), rbuf = std::make_shared<Scratch>();
     {
+        std::unique_ptr<StreamOverride> so(side ? new StreamOverride(device, ex_s) : nullptr);
+        *sbuf = Scratch(send_off[comm.nprocs], device);
+        *rbuf = Scratch(recv_off[comm.nprocs], device);
         std::vector<std::size_t> cur(send_off.begin(), send_off.end() - 1);
         for (const Piece &p : pieces) {
             const CompRef &ca = sc[p.a], &cb = dc[p.b];
@@ -513,51 +526,71 @@ void dist_copy(const Scalar &alpha, const DistTensor &src, const Coor &from0, co
                             "communicator's device");
             local_piece_copy(Scalar{1, 0}, src.dtype, src.ptr[ca.idx],
                              src.ranges[ca.rank][ca.idx].size, p.src_from, src.dtype,
-                             (char *)sbuf.ptr + cur[cb.rank], p.size, Coor(src.nd(), 0), p.size,
+                             (char *)sbuf->ptr + cur[cb.rank], p.size, Coor(src.nd(), 0), p.size,
                              id, false, device);
             cur[cb.rank] += volume(p.size) * es;
         }
-    }
-    set_device(device);
-    hipStream_t s = get_stream(device);
-    if (comm.nccl) {
-        // RCCL: grouped point-to-point send/recv straight from/to device memory (xGMI)
-        ncclComm_t nc = (ncclComm_t)comm.nccl;
-        nccl_check(ncclGroupStart(), "ncclGroupStart");
-        for (int q = 0; q < comm.nprocs; ++q) {
-            if (q == comm.rank) continue;
-            if (send_bytes[q] > 0)
-                nccl_check(ncclSend((char *)sbuf.ptr + send_off[q], send_bytes[q], ncclChar, q,
-                                    nc, s),
-                           "ncclSend");
-            if (recv_bytes[q] > 0)
-                nccl_check(ncclRecv((char *)rbuf.ptr + recv_off[q], recv_bytes[q], ncclChar, q,
-                                    nc, s),
-                           "ncclRecv");
+        if (comm.nccl) {
+            // RCCL: grouped point-to-point send/recv straight from/to device memory (xGMI)
+            ncclComm_t nc = (ncclComm_t)comm.nccl;
+            nccl_check(ncclGroupStart(), "ncclGroupStart");
+            for (int q = 0; q < comm.nprocs; ++q) {
+                if (q == comm.rank) continue;
+                if (send_bytes[q] > 0)
+                    nccl_check(ncclSend((char *)sbuf->ptr + send_off[q], send_bytes[q], ncclChar,
+                                        q, nc, ex_s),
+                               "ncclSend");
+                if (recv_bytes[q] > 0)
+                    nccl_check(ncclRecv((char *)rbuf->ptr + recv_off[q], recv_bytes[q], ncclChar,
+                                        q, nc, ex_s),
+                               "ncclRecv");
+            }
+            nccl_check(ncclGroupEnd(), "ncclGroupEnd");
         }
-        nccl_check(ncclGroupEnd(), "ncclGroupEnd");
-    } else if (comm.host_fn && comm.stage) {
-        // Host-staged: device -> pinned host, the caller's all-to-all, pinned host -> device
-        // (the reference's non-GPU-aware MPI path, dist.h:1426-1500)
-        host_exchange(comm, sbuf.ptr, send_bytes, send_off, rbuf.ptr, recv_bytes, recv_off, s);
-    } else {
-        throw Error("copy: the communicator has no transport");
     }
-    {
+    // completion of the side-stream exchange (shared by the copies of the closure; consumed once)
+    auto done = std::make_shared<hipEvent_t>(nullptr);
+    if (side) {
+        SBX_HIP_CHECK(hipEventCreateWithFlags(done.get(), hipEventDisableTiming));
+        SBX_HIP_CHECK(hipEventRecord(*done, ex_s));
+    }
+    // the rest: (host-staged) exchange through the caller's all-to-all, then the unpack with the
+    // destination permutation, alpha and Copy/Add fused, on the library stream
+    auto plan_ref = plan;
+    const DistTensor src_c = src, dst_c = dst;
+    auto finish = [=]() {
+        set_device(device);
+        const hipStream_t s = get_stream(device);
+        if (*done) {
+            // the unpack (and the later free of the pack buffers, recorded on this stream)
+            // follow the exchange
+            SBX_HIP_CHECK(hipStreamWaitEvent(s, *done, 0));
+            SBX_HIP_CHECK(hipEventDestroy(*done));
+            *done = nullptr;
+        }
+        if (!comm.nccl)
+            // Host-staged: device -> pinned host, the caller's all-to-all, pinned host -> device
+            // (the reference's non-GPU-aware MPI path, dist.h:1426-1500)
+            host_exchange(comm, sbuf->ptr, send_bytes, send_off, rbuf->ptr, recv_bytes, recv_off, s);
+        const std::vector<CompRef> sc2 = flatten_components(src_c), dc2 = flatten_components(dst_c);
         std::vector<std::size_t> cur(recv_off.begin(), recv_off.end() - 1);
-        for (const Piece &p : pieces) {
-            const CompRef &ca = sc[p.a], &cb = dc[p.b];
+        for (const Piece &p : plan_ref->pieces) {
+            const CompRef &ca = sc2[p.a], &cb = dc2[p.b];
             if (cb.rank != comm.rank || ca.rank == comm.rank) continue;
-            if (dst.dev[cb.idx] != device)
+            if (dst_c.dev[cb.idx] != device)
                 throw Error("copy: with a communicator every component must be on the "
                             "communicator's device");
-            local_piece_copy(alpha, src.dtype, (char *)rbuf.ptr + cur[ca.rank], p.size,
-                             Coor(src.nd(), 0), dst.dtype, dst.ptr[cb.idx],
-                             dst.ranges[cb.rank][cb.idx].size, p.dst_from, p.size, perm_s2d, add,
-                             device, nullptr, dst.mask_of(cb.idx));
+            local_piece_copy(alpha, src_c.dtype, (char *)rbuf->ptr + cur[ca.rank], p.size,
+                             Coor(src_c.nd(), 0), dst_c.dtype, dst_c.ptr[cb.idx],
+                             dst_c.ranges[cb.rank][cb.idx].size, p.dst_from, p.size, perm_s2d,
+                             add, device, nullptr, dst_c.mask_of(cb.idx));
             cur[ca.rank] += volume(p.size) * es;
         }
-    }
+    };
+    if (deferred)
+        *deferred = finish;
+    else
+        finish();
 }
 
 void comm_barrier(const Comm &comm) {

@@ -69,7 +69,8 @@ template <> __device__ __forceinline__ float2 conv<float2, double>(double v) { r
 
 struct Alpha {
     double re, im;
-    int one; // alpha == 1: no multiplication (bit-exact data movement)
+    int one; // 1: alpha == 1, no multiplication (bit-exact data movement); 2: alpha == 0, the
+             // element is +0 (the reference zero-fills, copy_n.h:435-438: no 0 * v, no -0.0)
 };
 
 // alpha * v in the SOURCE type, then converted (the reference's copy_n computes alpha * v[i]
@@ -78,22 +79,26 @@ struct Alpha {
 // complex product is formed with separately rounded products (no FMA contraction), as the
 // reference's C-complex multiply on the CPU
 template <typename S> __device__ __forceinline__ S scale(S v, const Alpha &a) {
-    return a.one ? v : (S)(v * (S)a.re);
+    return a.one == 1 ? v : a.one == 2 ? S{} : (S)(v * (S)a.re);
 }
 template <> __device__ __forceinline__ double2 scale<double2>(double2 v, const Alpha &a) {
 #pragma clang fp contract(off)
-    if (a.one) return v;
+    if (a.one == 1) return v;
+    if (a.one == 2) return double2{0, 0};
     return double2{a.re * v.x - a.im * v.y, a.re * v.y + a.im * v.x};
 }
 template <> __device__ __forceinline__ float2 scale<float2>(float2 v, const Alpha &a) {
 #pragma clang fp contract(off)
-    if (a.one) return v;
+    if (a.one == 1) return v;
+    if (a.one == 2) return float2{0, 0};
     const float ar = (float)a.re, ai = (float)a.im;
     return float2{ar * v.x - ai * v.y, ar * v.y + ai * v.x};
 }
-template <> __device__ __forceinline__ int scale<int>(int v, const Alpha &a) { return v; }
+template <> __device__ __forceinline__ int scale<int>(int v, const Alpha &a) {
+    return a.one == 2 ? 0 : v;
+}
 template <> __device__ __forceinline__ unsigned long scale<unsigned long>(unsigned long v, const Alpha &a) {
-    return v;
+    return a.one == 2 ? 0ul : v;
 }
 /// the element written for source value v
 template <typename D, typename S> __device__ __forceinline__ D xform(S v, const Alpha &a) {
@@ -742,7 +747,7 @@ CopyTape *current_copy_tape() { return t_tape; }
 void replay_launch(const TapeLaunch &tl, const void *src, void *dst, const Scalar &alpha) {
     const CopyLaunch &l = *(const CopyLaunch *)tl.launch.get();
     set_device(tl.device);
-    const Alpha a{alpha.re, alpha.im, alpha.is_one() ? 1 : 0};
+    const Alpha a{alpha.re, alpha.im, alpha.is_one() ? 1 : alpha.is_zero() ? 2 : 0};
     l.run(l, src, dst, a, nullptr, nullptr, get_stream(tl.device));
 }
 
@@ -810,7 +815,7 @@ void launch_box_copy(const BoxCopyDesc &d, int device) {
             t->launches.push_back(TapeLaunch{std::make_shared<CopyLaunch>(l), d.src, d.dst,
                                              device, d.alpha});
     }
-    const Alpha alpha{d.alpha.re, d.alpha.im, d.alpha.is_one() ? 1 : 0};
+    const Alpha alpha{d.alpha.re, d.alpha.im, d.alpha.is_one() ? 1 : d.alpha.is_zero() ? 2 : 0};
     l.run(l, d.src, d.dst, alpha, d.src_mask, d.dst_mask, s);
 }
 

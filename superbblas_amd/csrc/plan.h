@@ -135,9 +135,15 @@ struct Local {
 /// Every rank of `comm` reaches this point before any leaves it (MPI_Barrier)
 void comm_barrier(const Comm &comm);
 
-/// copy: dst[from1 + P(c - from0)] (=|+=) alpha * src[c] for c in [from0, from0+size0)
+/// copy: dst[from1 + P(c - from0)] (=|+=) alpha * src[c] for c in [from0, from0+size0).
+/// With `deferred` and other ranks in the exchange, the call returns once the local pieces are
+/// issued and the exchange is started (RCCL: packed and sent / received on the side stream;
+/// host-staged: packed); *deferred then finishes it (unpack on the library stream after the
+/// exchange) -- the reference's Request (dist.h:54-61, 2386-2437).  *deferred stays empty when
+/// nothing is left to do.
 void dist_copy(const Scalar &alpha, const DistTensor &src, const Coor &from0, const Coor &size0,
-               const DistTensor &dst, const Coor &from1, bool add, const Comm &comm);
+               const DistTensor &dst, const Coor &from1, bool add, const Comm &comm,
+               std::function<void()> *deferred = nullptr);
 
 /// Host-only argument checks, run before any device work (the reference validates first:
 /// tensor.h:495-507 check_isomorphic, tensor.h:623-646 check_dimensions)

@@ -21,6 +21,9 @@ Cases (all multi-rank: the exchange, pack/unpack kernels and reductions run for 
             41-binade range; tests/golden cases 51-55) with the lattice split over the ranks as
             the bench's configs[3] shapes: v0 and v1 on an xyz grid (2x1x1, 2x2x1, ...; "4a") or
             v1 over t only ("4b", redistributed), output on rank 0; within 1e-10 per component
+  split  -- the reference's split operator: a halo piece applied with a deferred request (its
+            exchange in flight) and a core piece with just_local, then wait; a deferred copy
+            [tests/bsr.cpp:402-545, 779-818; bsr.h:2199-2257, 2352-2359; dist.h:54-61]
   fuzz   -- seeded random copies (permutation, wrapping box, Copy/Add, type pairs) and
             contractions (label groups, orders, boxes, conj, alpha/beta) between random
             distributions over the ranks (some ranks may own nothing)
@@ -407,6 +410,97 @@ def case_storage(sb, comm, rank, n, dev):
         os.remove(fn)
 
 
+def case_split(sb, comm, rank, n, dev, ncols=3):
+    """The reference's split operator (tests/bsr.cpp:402-545, 779-818): the 9-point operator as a
+    core piece (domain = the rank's own sites, no exchange, applied with just_local) plus a halo
+    piece (the blocks reaching other ranks' sites, domain = image + halo).  The halo piece is
+    applied first with a deferred request (its exchange in flight), the core piece runs, then
+    the request is waited: y = core x + halo x must equal the whole operator's product."""
+    L = 4
+    Lt = 2 * n
+    dim = [L, L, L, Lt, 1, 3]
+    b = 3
+    pi = sb.basic_partitioning("xyztsc", dim, [1, 1, 1, n, 1, 1], "xyzt", n, 1)
+    pd = []
+    for f, s in pi:
+        f, s = list(f), list(s)
+        for d in range(4):
+            s[d] = min(dim[d], s[d] + 2)
+            f[d] = (f[d] - 1) % dim[d] if s[d] < dim[d] else 0
+        pd.append((f, s))
+    f, s = pi[rank]
+    sites = np.array(np.unravel_index(np.arange(vol(s[:4])), s[:4])).T + np.array(f[:4])
+    dom = np.array(dim[:4])
+    lo, sz = np.array(f[:4]), np.array(s[:4])
+    jj_core, jj_halo = [], []
+    for st in sites:
+        for d, dr in [(None, 0)] + [(d, dr) for d in range(4) for dr in (-1, 1)]:
+            c = st.copy()
+            if d is not None:
+                c[d] += dr
+            inside = np.all((c - lo) % dom < sz)
+            jj_core.append(list((c - lo) % dom) + [0, 0] if inside else [-1] * 6)
+            jj_halo.append([-1] * 6 if inside else list((c - np.array(pd[rank][0][:4])) % dom)
+                           + [0, 0])
+    gsite = np.ravel_multi_index(tuple((sites % dom).T), dim[:4])
+    allv = gen("int", vol(dim[:4]) * 9 * b * b, 4, np.complex128).reshape(-1, 9 * b * b)
+    vals = torch.from_numpy(np.ascontiguousarray(allv[gsite]).ravel()).to(dev)
+    ii = torch.from_numpy(np.full(len(sites), 9, np.int32)).to(dev)
+    blk = [1, 1, 1, 1, 1, 3]
+    core = sb.create_bsr(pi, dim, pi, dim, blk, blk, False, [ii],
+                         [torch.from_numpy(np.array(jj_core, np.int32).ravel()).to(dev)], [vals],
+                         comm=comm)
+    halo = sb.create_bsr(pi, dim, pd, dim, blk, blk, False, [ii],
+                         [torch.from_numpy(np.array(jj_halo, np.int32).ravel()).to(dev)], [vals],
+                         comm=comm)
+    dimx = [1, L, L, L, Lt, 1, 3, ncols]
+    px = sb.basic_partitioning("pXYZTSCn", dimx, [1, 1, 1, 1, n, 1, 1, 1], "XYZT", n, 1)
+    gx = gen("int", vol(dimx), 5, np.complex128)
+    vx = scatter(sb, gx, dimx, px, rank, 1, dev)
+    vy = scatter(sb, np.zeros(vol(dimx), np.complex128), dimx, px, rank, 1, dev)
+    z8 = [0] * 8
+    req = sb.bsr_krylov(1.0, halo, "xyztsc", "XYZTSC", px, "pXYZTSCn", z8, dimx, dimx, vx, 1.0,
+                        px, "pxyztscn", z8, dimx, dimx, "p", vy, comm=comm, request=True)
+    assert req is not None, "the halo piece's exchange should be left in flight"
+    assert sb.bsr_krylov(1.0, core, "xyztsc", "XYZTSC", px, "pXYZTSCn", z8, dimx, dimx, vx, 1.0,
+                         px, "pxyztscn", z8, dimx, dimx, "p", vy, comm=comm, request=True,
+                         just_local=True) is None
+    req.wait()
+    torch.cuda.synchronize()
+    core.destroy()
+    halo.destroy()
+    out = gather(np.zeros(vol(dimx), np.complex128), dimx, px, 1, vy)
+    allsites = np.array(np.unravel_index(np.arange(vol(dim[:4])), dim[:4])).T
+    jg = []
+    for st in allsites:
+        for d, dr in [(None, 0)] + [(d, dr) for d in range(4) for dr in (-1, 1)]:
+            c = st.copy()
+            if d is not None:
+                c[d] += dr
+            jg.append(list(c % dom) + [0, 0])
+    ref = np.zeros(vol(dimx), np.complex128)
+    V = vol(dim[:4])
+    oracle_bsr(T_CDOUBLE, dim, 0, V, b, b, np.full(V, 9, np.int32), np.array(jg, np.int32).ravel(),
+               allv.ravel(), False, gx, ncols, True, ref, ncols, True, ncols, 1.0)
+    assert np.array_equal(out, ref), "split operator"
+    # a deferred distributed copy: the exchange in flight, finished by wait()
+    dim0, dim1 = [4, 4, 2, 2 * n], [2 * n, 2, 4, 4]
+    p0 = sb.basic_partitioning("xyzt", dim0, [1, 1, 1, n], "t", n, 1)
+    p1 = sb.basic_partitioning("tzyx", dim1, [1, 1, 1, n], "x", n, 1)
+    g0 = gen("index", vol(dim0), 1, np.complex128)
+    g1 = gen("int", vol(dim1), 2, np.complex128)
+    v0 = scatter(sb, g0, dim0, p0, rank, 1, dev)
+    v1 = scatter(sb, g1, dim1, p1, rank, 1, dev)
+    r = sb.copy(1.0, p0, "xyzt", [0] * 4, dim0, dim0, v0, p1, "tzyx", [0] * 4, dim1, v1,
+                comm=comm, request=True)
+    sb.wait(r)
+    torch.cuda.synchronize()
+    out = gather(np.zeros_like(g1), dim1, p1, 1, v1)
+    ref = g1.copy()
+    oracle_copy(1.0, "xyzt", [0] * 4, dim0, dim0, g0, "tzyx", [0] * 4, dim1, ref)
+    assert np.array_equal(out.view(np.uint8), ref.view(np.uint8)), "deferred copy"
+
+
 LATTICE_GRID = {1: [1, 1, 1], 2: [2, 1, 1], 3: [3, 1, 1], 4: [2, 2, 1], 8: [2, 2, 2]}
 
 
@@ -544,7 +638,7 @@ def main():
         comm = sb.Comm.from_torch_distributed(dev_idx)
     else:
         comm = sb.Comm.host_staged(dev_idx)
-    cases = os.environ.get("SBX_TEST_CASES", "copy,contr,bsr,kron,dense,storage,fuzz,golden").split(",")
+    cases = os.environ.get("SBX_TEST_CASES", "copy,contr,bsr,kron,dense,storage,fuzz,golden,split").split(",")
     if "copy" in cases:
         case_copy(sb, comm, rank, n, dev)
     if "contr" in cases:
@@ -561,6 +655,8 @@ def main():
         case_fuzz(sb, comm, rank, n, dev)
     if "golden" in cases:
         case_golden(sb, comm, rank, n, dev)
+    if "split" in cases:
+        case_split(sb, comm, rank, n, dev)
     dist.barrier()
     comm.close()
     dist.destroy_process_group()

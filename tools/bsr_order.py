@@ -19,10 +19,30 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import superbblas_amd as sb  # noqa: E402
 
 
+def morton_key(c, bits):
+    """interleave the bits of the 4 coordinates (t lowest)"""
+    k = np.zeros(len(c), np.int64)
+    for b in range(bits):
+        for d in range(4):
+            k |= ((c[:, d] >> b) & 1).astype(np.int64) << (4 * b + (3 - d))
+    return k
+
+
 def sites_in_order(L, order):
     idx = np.arange(L ** 4)
+    nat = np.array(np.unravel_index(idx, (L, L, L, L))).T
     if order == "natural":
-        return np.array(np.unravel_index(idx, (L, L, L, L))).T
+        return nat
+    if order == "morton":
+        return nat[np.argsort(morton_key(nat, int(np.log2(L))), kind="stable")]
+    if order == "tile4":
+        # XCD blocks of (L/2)^3 x L, inside: 4^4 tiles in Morton order, sites natural in a tile
+        blk = (nat[:, 0] // (L // 2)) * 4 + (nat[:, 1] // (L // 2)) * 2 + nat[:, 2] // (L // 2)
+        tile = nat // 4
+        tkey = morton_key(tile, int(np.log2(L // 4)) + 1)
+        inner = ((nat[:, 0] % 4 * 4 + nat[:, 1] % 4) * 4 + nat[:, 2] % 4) * 4 + nat[:, 3] % 4
+        key = (blk.astype(np.int64) << 40) | (tkey << 8) | inner
+        return nat[np.argsort(key, kind="stable")]
     h = L // 2
     out = []
     for bx in range(2):
@@ -39,7 +59,7 @@ def main():
     dev = torch.device("cuda:0")
     L = 16
     V = L ** 4
-    for order in ("natural", "blocked"):
+    for order in sys.argv[1:] or ("natural", "blocked", "morton", "tile4"):
         sites = sites_in_order(L, order)
         jj = np.zeros((V, 9, 6), np.int32)
         jj[:, 0, :4] = sites
