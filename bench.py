@@ -737,10 +737,35 @@ def chain_dist_bench(sb, dev, comm, world, rank, grid, barrier, Ls=16, Lt=64, nc
     vals.real.uniform_(-1, 1)
     vals.imag.uniform_(-1, 1)
     blk = [1, 1, 1, 1, s_, c_]
-    op = sb.create_bsr(pi, dim, pd, dim, blk, blk, False,
-                       [torch.full((V,), 9, dtype=torch.int32, device=dev)],
+    iiv = torch.full((V,), 9, dtype=torch.int32, device=dev)
+    op = sb.create_bsr(pi, dim, pd, dim, blk, blk, False, [iiv],
                        [torch.from_numpy(jj.reshape(-1)).to(dev)], [vals], comm=comm)
-    del jj, sites
+    # the same operator split as the reference's create_lattice_split (tests/bsr.cpp:402-545):
+    # a core piece (blocks whose column is one of this rank's sites: domain = image, no
+    # exchange) and a halo piece (the other blocks: domain = image + halo); the halo piece's
+    # exchange runs on the side stream while the core piece's product runs (bsr_krylov request +
+    # just_local), then the halo product is added
+    nb = np.zeros((V, 9, 4), np.int64)
+    nb[:, 0] = sites
+    k = 1
+    for d in range(4):
+        for sg in (-1, 1):
+            c = sites.copy()
+            c[:, d] = (c[:, d] + sg) % gdim[d]
+            nb[:, k] = c
+            k += 1
+    lo, sz = np.array(f0[:4]), np.array(s0[:4])
+    inside = np.all((nb - lo) % gdim < sz, axis=2)
+    jj_core = np.full((V, 9, 6), -1, np.int32)
+    jj_core[:, :, :4] = np.where(inside[:, :, None], (nb - lo) % gdim, -1)
+    jj_core[:, :, 4:] = np.where(inside[:, :, None], 0, -1)
+    jj_halo = jj.copy()
+    jj_halo[inside] = -1
+    core = sb.create_bsr(pi, dim, pi, dim, blk, blk, False, [iiv],
+                         [torch.from_numpy(jj_core.reshape(-1)).to(dev)], [vals], comm=comm)
+    halo = sb.create_bsr(pi, dim, pd, dim, blk, blk, False, [iiv],
+                         [torch.from_numpy(jj_halo.reshape(-1)).to(dev)], [vals], comm=comm)
+    del jj, sites, nb, jj_core, jj_halo
     dr = [Lt, s_, ncols, s_, ncols]
     pr = [([0] * 5, dr)] + [([0] * 5, [0] * 5)] * (world - 1)
     vr = torch.empty(vol(dr) if rank == 0 else 1, dtype=cf, device=dev)
@@ -750,13 +775,37 @@ def chain_dist_bench(sb, dev, comm, world, rank, grid, barrier, Ls=16, Lt=64, nc
         sb.copy(1.0, psrc, "tnsxyzc", z7, dsrc, dsrc, [src], px, "pxyztscn", z8, dx, [x],
                 comm=comm)
 
-    def stage2():
+    def stage2_whole():
         sb.bsr_krylov(1.0, op, "XYZTSC", "xyztsc", px, "pxyztscn", z8, dx, dx, [x], 0.0, px,
                       "pXYZTSCn", z8, dx, dx, "p", [y], comm=comm)
+
+    def stage2():
+        # halo piece first (exchange in flight, product deferred and added), core piece now
+        r = sb.bsr_krylov(1.0, halo, "XYZTSC", "xyztsc", px, "pxyztscn", z8, dx, dx, [x], 1.0,
+                          px, "pXYZTSCn", z8, dx, dx, "p", [y], comm=comm, request=True)
+        sb.bsr_krylov(1.0, core, "XYZTSC", "xyztsc", px, "pxyztscn", z8, dx, dx, [x], 0.0, px,
+                      "pXYZTSCn", z8, dx, dx, "p", [y], comm=comm, just_local=True)
+        sb.wait(r)
 
     def stage3():
         sb.contraction(1.0, px, z8, dx, dx, "pXYZTSCn", True, [y], px, z8, dx, dx, "pXYZTsCN",
                        False, [y], 0.0, pr, z5, dr, dr, "TSnsN", [vr], comm=comm)
+    # the split application must equal the whole operator's
+    stage1()
+    stage2_whole()
+    y_whole = y.clone()
+    stage2()
+    torch.cuda.synchronize()
+    split_err = (torch.linalg.vector_norm(y - y_whole) / torch.linalg.vector_norm(y_whole)).item()
+    del y_whole
+    t_whole = 0.0
+    for _ in range(reps):
+        barrier()
+        t0 = time.perf_counter()
+        stage2_whole()
+        torch.cuda.synchronize()
+        barrier()
+        t_whole += (time.perf_counter() - t0) / reps
     stages = (stage1, stage2, stage3)
     for fn in stages:
         fn()
@@ -773,10 +822,14 @@ def chain_dist_bench(sb, dev, comm, world, rank, grid, barrier, Ls=16, Lt=64, nc
             times[i] += (time.perf_counter() - t0) / reps
     t_all = (time.perf_counter() - t_all) / reps
     op.destroy()
+    core.destroy()
+    halo.destroy()
     out = {"chain_dist_workload": "configs[4]: %dx%dx%dx%d lattice over an xyz grid %s, n=%d, "
                                   "spin 4 x color 3, complex<float>" % (G[0], G[1], G[2], G[3],
                                                                         grid, ncols),
-           "chain_dist_ms": t_all * 1e3}
+           "chain_dist_ms": t_all * 1e3,
+           "chain_dist_bsr_unsplit_ms": t_whole * 1e3,
+           "chain_dist_bsr_split_rel_diff": split_err}
     for i, name in enumerate(("redistribute", "bsr", "contraction")):
         out["chain_dist_%s_ms" % name] = times[i] * 1e3
     if world > 1 and dist_available():

@@ -498,17 +498,20 @@ __global__ void __launch_bounds__(256) bsr_mfma_blk_kernel(const BsrArgs p) {
     for (int k = 0; k < NNZ; ++k) dj[k] = p.jj[jb + k];
     u4 ra[PD][NA], rx[PD][NX];
     auto fetch = [&](int k, u4 *ra_, u4 *rx_) {
+        // a skipped block (column -1: e.g. the other piece's blocks of a split core / halo
+        // operator) is not read at all
+        const bool live = dj[k] >= 0;
         const u4 *ap = (const u4 *)(v + (jb + k) * ABLK);
-        const u4 *xp = (const u4 *)(x + (long)(dj[k] < 0 ? 0 : dj[k]) * nc);
+        const u4 *xp = (const u4 *)(x + (long)(live ? dj[k] : 0) * nc);
 #pragma unroll
         for (int q = 0; q < NA; ++q) {
             const int g = lane + 64 * q; // 16-byte granule of the block
-            ra_[q] = g * EPL < ABLK ? ap[g] : u4{0, 0, 0, 0};
+            ra_[q] = live && g * EPL < ABLK ? ap[g] : u4{0, 0, 0, 0};
         }
 #pragma unroll
         for (int q = 0; q < NX; ++q) {
             const int g = lane + 64 * q;
-            rx_[q] = g * EPL < xblk ? xp[g] : u4{0, 0, 0, 0};
+            rx_[q] = live && g * EPL < xblk ? xp[g] : u4{0, 0, 0, 0};
         }
     };
     E *const sa = lds[w], *const sx = lds[w] + ABLK;

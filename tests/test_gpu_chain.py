@@ -1,0 +1,91 @@
+"""The configs[4] propagator chain (bench.py chain_bench) checked stage by stage against the
+oracle at a reduced lattice: (1) redistribute a complex<float> propagator `tnsxyzc` into the
+operator's domain layout `pxyztscn` (copy, bit-exact), (2) apply the 9-point 12x12-block
+(spin x color) BSR operator (bsr_krylov, bsr.h:2516-2543), (3) contract the result with its
+conjugate over the lattice and color into `TSnsN` (contraction, dist.h:3701-3731).  Tolerances
+are single precision (sums of <= 108 and <= 768 products).  The full-size run in bench.py
+checks the Hermitian property of stage 3 instead."""
+import numpy as np
+import pytest
+
+from _common import T_CFLOAT, oracle_bsr, oracle_contraction, oracle_copy, rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def _vol(d):
+    n = 1
+    for x in d:
+        n *= x
+    return n
+
+
+def test_chain_reduced(gpu):
+    import torch
+    import superbblas_amd as sb
+    rng = np.random.default_rng(11)
+    Ls, Lt, ncols, s_, c_ = 4, 8, 3, 4, 3
+    b = s_ * c_
+    dims = [Ls, Ls, Ls, Lt]
+    V = _vol(dims)
+    cf = np.complex64
+
+    def rand(n):
+        return (rng.uniform(-1, 1, n) + 1j * rng.uniform(-1, 1, n)).astype(cf)
+
+    # (1) tnsxyzc -> pxyztscn
+    dsrc = [Lt, ncols, s_, Ls, Ls, Ls, c_]
+    dx = [1, Ls, Ls, Ls, Lt, s_, c_, ncols]
+    src = rand(_vol(dsrc))
+    x_ref = np.zeros(_vol(dx), cf)
+    oracle_copy(1.0, "tnsxyzc", [0] * 7, dsrc, dsrc, src, "pxyztscn", [0] * 8, dx, x_ref)
+    t_src = torch.from_numpy(src).to(gpu)
+    t_x = torch.zeros(_vol(dx), dtype=torch.complex64, device=gpu)
+    sb.copy(1.0, [([0] * 7, dsrc)], "tnsxyzc", [0] * 7, dsrc, dsrc, [t_src], [([0] * 8, dx)],
+            "pxyztscn", [0] * 8, dx, [t_x])
+    torch.cuda.synchronize()
+    assert np.array_equal(t_x.cpu().numpy().view(np.uint8), x_ref.view(np.uint8))
+
+    # (2) y = A x, A the 9-point operator with 12x12 blocks
+    sites = np.array(np.unravel_index(np.arange(V), dims)).T
+    jj = np.zeros((V, 9, 6), np.int32)
+    jj[:, 0, :4] = sites
+    k = 1
+    for d in range(4):
+        for sg in (-1, 1):
+            c = sites.copy()
+            c[:, d] = (c[:, d] + sg) % dims[d]
+            jj[:, k, :4] = c
+            k += 1
+    vals = rand(V * 9 * b * b)
+    dim = dims + [s_, c_]
+    full = [([0] * 6, dim)]
+    blk = [1, 1, 1, 1, s_, c_]
+    op = sb.create_bsr(full, dim, full, dim, blk, blk, False,
+                       [torch.full((V,), 9, dtype=torch.int32, device=gpu)],
+                       [torch.from_numpy(jj.reshape(-1)).to(gpu)], [torch.from_numpy(vals).to(gpu)])
+    t_y = torch.empty_like(t_x)
+    p_x = [([0] * 8, dx)]
+    sb.bsr_krylov(1.0, op, "XYZTSC", "xyztsc", p_x, "pxyztscn", [0] * 8, dx, dx, [t_x], 0.0, p_x,
+                  "pXYZTSCn", [0] * 8, dx, dx, "p", [t_y])
+    torch.cuda.synchronize()
+    op.destroy()
+    y_ref = np.zeros(_vol(dx), cf)
+    oracle_bsr(T_CFLOAT, dim, 0, V, b, b, np.full(V, 9, np.int32), jj.reshape(-1), vals, False,
+               x_ref, ncols, True, y_ref, ncols, True, ncols, 1.0)
+    y = t_y.cpu().numpy()
+    assert rel_err(y, y_ref) < 2e-6
+
+    # (3) TSnsN = sum_{XYZC} conj(y[XYZT S C n]) y[XYZT s C N]
+    dr = [Lt, s_, ncols, s_, ncols]
+    t_r = torch.empty(_vol(dr), dtype=torch.complex64, device=gpu)
+    sb.contraction(1.0, p_x, [0] * 8, dx, dx, "pXYZTSCn", True, [t_y], p_x, [0] * 8, dx, dx,
+                   "pXYZTsCN", False, [t_y], 0.0, [([0] * 5, dr)], [0] * 5, dr, dr, "TSnsN", [t_r])
+    torch.cuda.synchronize()
+    r_ref = np.zeros(_vol(dr), cf)
+    oracle_contraction(1.0, "pXYZTSCn", [0] * 8, dx, dx, True, y_ref, "pXYZTsCN", [0] * 8, dx, dx,
+                       False, y_ref, 0.0, "TSnsN", [0] * 5, dr, dr, r_ref)
+    r = t_r.cpu().numpy()
+    assert rel_err(r, r_ref) < 2e-5
+    h = r.reshape(Lt, s_ * ncols, s_ * ncols)
+    assert rel_err(h, np.conj(np.transpose(h, (0, 2, 1)))) < 1e-5
