@@ -354,7 +354,7 @@ def main():
         if not args.no_side:
             side.update(cpu_side_baselines())
 
-    traffic, traffic_src = pmc_traffic("dma_kernel<", "128, 128, 16, 4, 2")
+    traffic, traffic_src = pmc_traffic("dma_kernel<", "128, 128, 16, 4, 4")
     if rank == 0:
         if config == "1":
             workload = ("configs[1]: 16^4 lattice spin x color contraction tnsxyzc x tNSxyzc -> "
@@ -393,11 +393,11 @@ def main():
                          "traffic_source": traffic_src,
                          "algorithmic_bytes": 16.0 * (vol(p0[rank][1]) + vol(p1[rank][1]) +
                                                       vol(gdimr)),
-                         "kernel": "gemm_dma_kernel<complex<double>, 128x128x%d, 8 waves> (FP64 "
+                         "kernel": "gemm_dma_kernel<complex<double>, 128x128x%d, %d waves> (FP64 "
                                    "MFMA 16x16x4, complex %s) + split-K reduce, %d launches, %.4f "
                                    "ms avg (HIP events on its launch stream)" % (
-                                       8 if m3 else 16, "3M" if m3 else "4M", gemm_calls,
-                                       kernel_s * 1e3),
+                                       8 if m3 else 16, 8 if m3 else 16, "3M" if m3 else "4M",
+                                       gemm_calls, kernel_s * 1e3),
                          "flops_per_launch": flops_launch,
                          "executed_flops_per_launch": flops_launch * exec_per_alg,
                          "algorithmic_TFLOPs": round(algorithmic, 3),

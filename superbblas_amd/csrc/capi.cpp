@@ -410,6 +410,8 @@ int sbx_tune_set(const char *key, long long value) {
         else if (k == "copy.max_elems") g_copy_tune.max_elems = (long)value;
         else if (k == "gemm.max_bytes") g_gemm_tune.max_bytes = (long)value;
         else if (k == "bsr.variant") g_bsr_tune.variant = (int)value;
+        else if (k == "bsr.ell9") g_bsr_tune.ell9 = (int)value;
+        else if (k == "bsr.ell9_lds") g_bsr_tune.ell9_lds = (long)value;
         else if (k == "gemm.m3") g_gemm_tune.m3 = (int)value;
         else if (k == "gemm.splits") g_gemm_tune.splits = (int)value;
         else throw Error("tune_set: unknown key " + k);
@@ -427,6 +429,8 @@ int sbx_tune_get(const char *key, long long *value) {
         else if (k == "copy.max_elems") *value = g_copy_tune.max_elems;
         else if (k == "gemm.max_bytes") *value = g_gemm_tune.max_bytes;
         else if (k == "bsr.variant") *value = g_bsr_tune.variant;
+        else if (k == "bsr.ell9") *value = g_bsr_tune.ell9;
+        else if (k == "bsr.ell9_lds") *value = g_bsr_tune.ell9_lds;
         else if (k == "gemm.m3") *value = g_gemm_tune.m3;
         else if (k == "gemm.splits") *value = g_gemm_tune.splits;
         else throw Error("tune_get: unknown key " + k);

@@ -681,8 +681,8 @@ void launch_ell_g(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_t s
 // workgroup streams the values into LDS, so the x gathers, the column reads and the value stream
 // are in flight together (bsr_ell_kernel: value stream, then the columns, then one x block at a
 // time); blocks j+PD are fetched while block j is applied.
-template <typename E, int BI, int BD, int G, int PD, bool YROW, bool XROW>
-__global__ void __launch_bounds__(256) bsr_ell9_kernel(const BsrArgs p, int rb) {
+template <typename E, int BI, int BD, int G, int PD, bool YROW, bool XROW, int NT = 256>
+__global__ void __launch_bounds__(NT) bsr_ell9_kernel(const BsrArgs p, int rb) {
     constexpr int NNZ = 9, BLK = BI * BD, NB = PD + 1;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     E *vals = (E *)smem;
@@ -730,13 +730,13 @@ __global__ void __launch_bounds__(256) bsr_ell9_kernel(const BsrArgs p, int rb) 
     for (int j = 0; j < PD; ++j) fetch(dj[j], xb[j]);
     const long vbase = row0 * NNZ * BLK;
     const int nv = nrows * NNZ * BLK;
-    for (int e0 = threadIdx.x; e0 < nv; e0 += 256 * 8) {
+    for (int e0 = threadIdx.x; e0 < nv; e0 += NT * 8) {
         E t[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) t[u] = v[vbase + min(e0 + 256 * u, nv - 1)];
+        for (int u = 0; u < 8; ++u) t[u] = v[vbase + min(e0 + NT * u, nv - 1)];
 #pragma unroll
         for (int u = 0; u < 8; ++u)
-            if (e0 + 256 * u < nv) vals[e0 + 256 * u] = t[u];
+            if (e0 + NT * u < nv) vals[e0 + NT * u] = t[u];
     }
     __syncthreads();
     if (!active) return;
@@ -775,25 +775,25 @@ __global__ void __launch_bounds__(256) bsr_ell9_kernel(const BsrArgs p, int rb) 
     }
 }
 
-template <typename E, int BI, int BD, int G, int PD>
+template <typename E, int BI, int BD, int G, int PD, int NT = 256>
 void launch_ell9(const BsrArgs &a, bool yrow, bool xrow, hipStream_t s, long lds_bytes) {
     const long blk_bytes = 9L * BI * BD * (long)sizeof(E);
     const long ngroups = (a.ncols + G - 1) / G;
-    if (ngroups > 256) throw Error("bsr: internal ELL9 sizing error");
+    if (ngroups > NT) throw Error("bsr: internal ELL9 sizing error");
     int rb = (int)std::max(1L, lds_bytes / blk_bytes);
-    rb = (int)std::min<long>(rb, std::max(1L, 256 / ngroups));
+    rb = (int)std::min<long>(rb, std::max(1L, NT / ngroups));
     const long blocks = (a.block_rows + rb - 1) / rb;
     if (blocks >= (1L << 31)) throw Error("bsr: grid too large");
     const size_t lds = (size_t)rb * blk_bytes;
     KernelTimer timer("bsr", s);
     if (yrow && xrow)
-        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, true, true>), dim3(blocks), dim3(256), lds, s, a, rb);
+        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, true, true, NT>), dim3(blocks), dim3(NT), lds, s, a, rb);
     else if (yrow && !xrow)
-        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, true, false>), dim3(blocks), dim3(256), lds, s, a, rb);
+        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, true, false, NT>), dim3(blocks), dim3(NT), lds, s, a, rb);
     else if (!yrow && xrow)
-        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, false, true>), dim3(blocks), dim3(256), lds, s, a, rb);
+        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, false, true, NT>), dim3(blocks), dim3(NT), lds, s, a, rb);
     else
-        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, false, false>), dim3(blocks), dim3(256), lds, s, a, rb);
+        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, false, false, NT>), dim3(blocks), dim3(NT), lds, s, a, rb);
     SBX_HIP_CHECK(hipGetLastError());
 }
 
@@ -808,8 +808,21 @@ void launch_ell(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_t s) 
     // 190 -> 181-188; at n = 12 6 / 8 / 16 / 24 KB: 72 / 52 / 48 / 45 us; one or four columns
     // per thread, or the x rows of two blocks ahead: 46-82 us).  The x gathers are the bound:
     // without them the value stream and y run at 5.5 TB/s (22 us at n = 12).
-    if (nnz == 9 && g_bsr_tune.variant != 1)
-        return launch_ell9<E, BI, BD, 2, 1>(a, yrow, xrow, s, a.ncols >= 8 ? 12288 : 24576);
+    if (nnz == 9 && g_bsr_tune.variant != 1) {
+        const long lds = g_bsr_tune.ell9_lds > 0 ? g_bsr_tune.ell9_lds : a.ncols >= 8 ? 12288 : 24576;
+        // experiments (sbx_tune_set "bsr.ell9"): workgroup size 64 / 128 / 256 threads x one or
+        // two blocks of x lookahead, 1 or 2 rhs columns per thread
+        switch (g_bsr_tune.ell9) {
+        case 1: return launch_ell9<E, BI, BD, 2, 1, 64>(a, yrow, xrow, s, lds);
+        case 2: return launch_ell9<E, BI, BD, 2, 1, 128>(a, yrow, xrow, s, lds);
+        case 3: return launch_ell9<E, BI, BD, 2, 2, 64>(a, yrow, xrow, s, lds);
+        case 4: return launch_ell9<E, BI, BD, 2, 2, 128>(a, yrow, xrow, s, lds);
+        case 5: return launch_ell9<E, BI, BD, 1, 1, 64>(a, yrow, xrow, s, lds);
+        case 6: return launch_ell9<E, BI, BD, 1, 2, 128>(a, yrow, xrow, s, lds);
+        case 7: return launch_ell9<E, BI, BD, 2, 2, 256>(a, yrow, xrow, s, lds);
+        default: return launch_ell9<E, BI, BD, 2, 1>(a, yrow, xrow, s, lds);
+        }
+    }
     launch_ell_g<E, BI, BD, 2>(a, nnz, yrow, xrow, s, ELL_LDS_BYTES);
 }
 

@@ -96,6 +96,7 @@ struct GemmKArgs {
     int splits;
     long kchunk;
     void *work;
+    unsigned long long *probe; // tools only: workgroup 0 stores s_memtime / s_memrealtime at its start and end
     int tm, tn;
     unsigned a_bytes, b_bytes; // extent of one batch entry of A / B (buffer descriptor range)
     // split label groups: index i of M (N, K) is (i / m_lo, i % m_lo) with strides (sa_m_hi,
@@ -389,8 +390,11 @@ struct DmaOperand {
 // M3: complex products in the 3-multiplication (Gauss) form, P1 = ar*br, P2 = ai*bi,
 // P3 = (ar+ai)*(br+bi), re = P1 - P2, im = P3 - P1 - P2: 3 real MFMAs per complex k-step instead
 // of 4 (a third accumulator per tile; the operand sums are one VALU add per fragment element)
+// PF: the 4-multiplication path reads the fragments of k-step kk+4 from LDS before issuing the
+// MFMAs of k-step kk (a register double buffer), so a wave's LDS latency hides behind its own
+// MFMAs, not only behind the other wave of its SIMD
 template <typename R, bool CPLX, bool AK, bool BK, int BM, int BN, int BKK, int WM, int WN,
-          bool M3 = false>
+          bool M3 = false, bool PF = false>
 __global__ void __launch_bounds__(WM *WN * 64) gemm_dma_kernel(const GemmKArgs p) {
     typedef typename Elem<R, CPLX>::type E;
     typedef typename Mfma<R>::acc_t acc_t;
@@ -426,6 +430,11 @@ __global__ void __launch_bounds__(WM *WN * 64) gemm_dma_kernel(const GemmKArgs p
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    unsigned long long clk0 = 0, rt0 = 0;
+    if (p.probe && bid == 0) {
+        clk0 = __builtin_amdgcn_s_memtime();
+        rt0 = __builtin_amdgcn_s_memrealtime();
+    }
     OpA da;
     OpB db;
     const bool spl = p.split != 0;
@@ -469,6 +478,41 @@ __global__ void __launch_bounds__(WM *WN * 64) gemm_dma_kernel(const GemmKArgs p
         }
         const E *As = lds + cur * SLAB;
         const E *Bs = As + BM * BKK;
+        if constexpr (PF && CPLX && !M3) {
+            E af[2][MT], bf[2][NT];
+            auto frag = [&](int kk, E *a_, E *b_) {
+#pragma unroll
+                for (int i = 0; i < MT; ++i) a_[i] = As[OpA::slot(frow + 16 * i, kk + kq)];
+#pragma unroll
+                for (int j = 0; j < NT; ++j) b_[j] = Bs[OpB::slot(fcol + 16 * j, kk + kq)];
+            };
+            frag(0, af[0], bf[0]);
+#pragma unroll
+            for (int kk = 0; kk < BKK; kk += 4) {
+                const int c = (kk / 4) & 1;
+                if (kk + 4 < BKK) frag(kk + 4, af[c ^ 1], bf[c ^ 1]);
+                E *a = af[c], *b = bf[c];
+#pragma unroll
+                for (int i = 0; i < MT; ++i) a[i].y = flip(a[i].y, ma);
+#pragma unroll
+                for (int j = 0; j < NT; ++j) b[j].y = flip(b[j].y, mb);
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+#pragma unroll
+                    for (int j = 0; j < NT; ++j) {
+                        accR[i][j] = Mfma<R>::mma(a[i].x, b[j].x, accR[i][j]);
+                        accI[i][j] = Mfma<R>::mma(a[i].x, b[j].y, accI[i][j]);
+                    }
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+#pragma unroll
+                    for (int j = 0; j < NT; ++j) {
+                        accR[i][j] = Mfma<R>::mma(-a[i].y, b[j].y, accR[i][j]);
+                        accI[i][j] = Mfma<R>::mma(a[i].y, b[j].x, accI[i][j]);
+                    }
+            }
+            continue;
+        }
 #pragma unroll
         for (int kk = 0; kk < BKK; kk += 4) {
             E af[MT], bf[NT];
@@ -525,6 +569,12 @@ __global__ void __launch_bounds__(WM *WN * 64) gemm_dma_kernel(const GemmKArgs p
         }
     }
 
+    if (p.probe && bid == 0 && tid == 0) {
+        const unsigned long long clk1 = __builtin_amdgcn_s_memtime();
+        const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
+        p.probe[0] = clk1 - clk0; // shader clock cycles
+        p.probe[1] = rt1 - rt0;   // 100 MHz reference ticks
+    }
     const int ccol = lane & 15;
 #pragma unroll
     for (int i = 0; i < MT; ++i)
@@ -678,7 +728,7 @@ void launch_tiled_cfg(const GemmKArgs &p0, int device, hipStream_t stream, long 
 
 /// Launch one tile configuration of the LDS-DMA kernel
 template <typename R, bool CPLX, bool AK, bool BK, int BM, int BN, int BKK, int WM, int WN,
-          bool ALLOW_M3 = true>
+          bool ALLOW_M3 = true, bool PF = false>
 void launch_dma_cfg(const GemmKArgs &p0, int device, hipStream_t stream, long splits = 0,
                     long target_wgs = 1024) {
     // complex: the 4-multiplication form unless the 3-multiplication form is asked for (config
@@ -700,7 +750,7 @@ void launch_dma_cfg(const GemmKArgs &p0, int device, hipStream_t stream, long sp
                 hipLaunchKernelGGL((gemm_dma_kernel<R, CPLX, AK, BK, BM, BN, BKK, WM, WN>),
                                    dim3((unsigned)nwg), dim3(WM * WN * 64), 0, stream, p);
         } else
-            hipLaunchKernelGGL((gemm_dma_kernel<R, CPLX, AK, BK, BM, BN, BKK, WM, WN>),
+            hipLaunchKernelGGL((gemm_dma_kernel<R, CPLX, AK, BK, BM, BN, BKK, WM, WN, false, PF>),
                                dim3((unsigned)nwg), dim3(WM * WN * 64), 0, stream, p);
         SBX_HIP_CHECK(hipGetLastError());
     }
@@ -742,15 +792,17 @@ void launch_tiled(const GemmKArgs &p, int device, hipStream_t stream) {
         // split-K to one workgroup per CU (config 2: 4 splits 1.19 ms, 8 / 16 splits 1.20 /
         // 1.23 ms once the clocks have ramped up, tools/gemm_chunks.py); 16 waves of 32x32
         // (125 VGPRs, 4 waves/SIMD) measured 1.19-1.22 ms in the 3M form (8 waves: 1.16-1.18)
-        // The 4-multiplication form (default) streams 16-deep slabs (half the barriers per MFMA;
-        // 128 KB of LDS double buffer), the 3-multiplication form 8-deep ones (its third
-        // accumulator set leaves no VGPRs for deeper fragment prefetch)
+        // The 4-multiplication form (default): 16-deep slabs (half the barriers per MFMA; 128 KB
+        // of LDS double buffer) and 16 waves of 32x32 (4 waves per SIMD, <= 128 VGPRs): config 2
+        // in 1.503-1.510 ms against 1.562-1.570 with 8 waves of 32x64 and 1.523-1.530 with
+        // 8-deep slabs (tools/gemm_tune.hip, profiles/r02_gemm_tune.txt).  The 3-multiplication
+        // form keeps 8 waves and 8-deep slabs (its third accumulator set needs the VGPRs).
         const bool m3 = g_gemm_tune.m3 > 0;
         if (p.m >= 128 && p.n >= 128) {
             if (m3)
                 launch_dma_cfg<R, CPLX, AK, BK, 128, 128, 8, 4, 2>(p, device, stream, 0, 256);
             else
-                launch_dma_cfg<R, CPLX, AK, BK, 128, 128, 16, 4, 2, false>(p, device, stream, 0, 256);
+                launch_dma_cfg<R, CPLX, AK, BK, 128, 128, 16, 4, 4, false>(p, device, stream, 0, 256);
         } else {
             launch_dma_cfg<R, CPLX, AK, BK, 64, 64, 8, 2, 2>(p, device, stream, 0, 1024);
         }

@@ -226,6 +226,8 @@ struct GemmTune {
 extern GemmTune g_gemm_tune;
 struct BsrTune {
     int variant = 0; ///< BSR kernels: 0 = the library's choice, 1 = the round-1 kernels, 2 = no 12x12 block-staged kernel
+    int ell9 = 0;    ///< 9-point ELL kernel shape (workgroup size / lookahead / columns per thread), 0 = default
+    long ell9_lds = 0; ///< 9-point ELL kernel: bytes of block values staged per workgroup (0 = default)
 };
 extern BsrTune g_bsr_tune;
 

@@ -75,6 +75,13 @@ void run(const char *name, F launch, const GemmKArgs &p, int reps, double flops,
         },                                                                                       \
         p, reps, flops, &ref, C, nc)
 
+#define DMAP(BM, BN, BKK, WM, WN, SPL, TGT)                                                     \
+    run("dma-pf " #BM "x" #BN "x" #BKK " w" #WM "x" #WN " s" #SPL " t" #TGT,                      \
+        [&](const GemmKArgs &q, hipStream_t s) {                                                 \
+            launch_dma_cfg<double, true, true, true, BM, BN, BKK, WM, WN, false, true>(q, 0, s, SPL, TGT); \
+        },                                                                                       \
+        p, reps, flops, &ref, C, nc)
+
 int main(int argc, char **argv) {
     const long L = 16, n = 64;
     const long m = 4 * n, nn = 4 * n, k = L * L * L * 3;
@@ -104,6 +111,22 @@ int main(int argc, char **argv) {
     (void)hipStreamSynchronize(get_stream(0));
     (void)hipMemcpy(ref.data(), C, nc * sizeof(double), hipMemcpyDeviceToHost);
 
+    if (getenv("PROBE")) {
+        // shader clock of workgroup 0 during the default 4M GEMM (s_memtime / s_memrealtime)
+        unsigned long long *probe;
+        (void)hipMalloc(&probe, 16);
+        GemmKArgs q = p;
+        q.probe = probe;
+        for (int r = 0; r < 30; ++r) {
+            launch_dma_cfg<double, true, true, true, 128, 128, 16, 4, 4, false>(q, 0, get_stream(0), 0, 256);
+            (void)hipStreamSynchronize(get_stream(0));
+            unsigned long long h[2];
+            (void)hipMemcpy(h, probe, 16, hipMemcpyDeviceToHost);
+            std::printf("probe rep %2d: wg0 %.1f us, clock %.3f GHz\n", r, h[1] / 100.0,
+                        (double)h[0] / (h[1] / 100e6) / 1e9);
+        }
+        return 0;
+    }
     const char *only = getenv("ONLY");
     for (int rep = 0; rep < 3; ++rep) {
         if (!only || std::string(only) == "a") DMA(128, 128, 8, 4, 2, 0, 256);
@@ -111,6 +134,23 @@ int main(int argc, char **argv) {
         if (!only || std::string(only) == "c") DMA(128, 64, 8, 2, 2, 0, 512);
         if (!only || std::string(only) == "d") REG(64, 64, 16, 2, 2, 0, 1024);
         if (only && std::string(only) == "e") DMA(128, 128, 8, 4, 2, 1, 1);
+        if (only && std::string(only) == "w16") {
+            DMA(128, 128, 16, 4, 4, 0, 256);
+            DMA(128, 128, 8, 4, 4, 0, 256);
+            DMAP(128, 128, 8, 4, 4, 0, 256);
+            DMA(128, 128, 16, 8, 2, 0, 256);
+            DMA(128, 128, 16, 2, 8, 0, 256);
+            DMA(128, 128, 16, 4, 4, 0, 512);
+            DMA(128, 128, 8, 4, 4, 0, 512);
+            DMA(128, 128, 8, 4, 2, 0, 256);
+            continue;
+        }
+        if (!only || std::string(only) == "p") DMAP(128, 128, 16, 4, 2, 0, 256);
+        if (!only || std::string(only) == "g") DMA(128, 128, 16, 4, 4, 0, 256);
+        if (!only || std::string(only) == "gp") DMAP(128, 128, 16, 4, 4, 0, 256);
+        if (!only || std::string(only) == "f") DMAP(128, 128, 16, 2, 2, 0, 256);
+        if (!only || std::string(only) == "p8") DMAP(128, 128, 8, 4, 2, 0, 256);
+        if (!only || std::string(only) == "s8") DMAP(128, 128, 16, 4, 2, 8, 256);
     }
     return 0;
 }
