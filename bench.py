@@ -195,6 +195,9 @@ def main():
     ap.add_argument("--L", type=int, default=None)
     ap.add_argument("--n", type=int, default=64)
     ap.add_argument("--no-side", action="store_true", help="skip the side measurements")
+    ap.add_argument("--skip", default="",
+                    help="comma-separated side measurements to skip (permute, bsr, chain, 3m, "
+                         "chain_dist, redistribution)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--no-1gpu", action="store_true",
                     help="N > 1: skip the same global problem on rank 0's GPU alone")
@@ -263,19 +266,24 @@ def main():
     # side measurements first: they also bring the GPU clocks up before the contraction is timed
     # (the first ~10 GEMM launches on an idle GPU run ~12 % slower)
     side = {}
-    if not args.no_side and world == 1:
+    skip = set(x for x in args.skip.split(",") if x)
+    if args.no_side:
+        skip |= {"permute", "bsr", "chain", "3m", "chain_dist", "redistribution"}
+    if world == 1 and "permute" not in skip:
         side.update(permute_bench(sb, dev, 16, 64))
+    if world == 1 and "bsr" not in skip:
         side.update(bsr_bench(sb, dev, 16))
+    if world == 1 and "chain" not in skip:
         try:
             side.update(chain_bench(sb, dev))
         except Exception as e:  # a side measurement never takes the bench down
             side["chain_error"] = str(e)[:200]
-    if not args.no_side and world > 1:
+    if world > 1 and "chain_dist" not in skip:
         try:
             side.update(chain_dist_bench(sb, dev, comm, world, rank, grid[:3], barrier))
         except Exception as e:  # a side measurement never takes the bench down
             side["chain_dist_error"] = str(e)[:200]
-    if not args.no_side and world > 1 and config == "4a":
+    if world > 1 and config == "4a" and "redistribution" not in skip:
         # configs[3] "4b" beside the 4a headline: v1 over t only, (a) its all-to-all
         # redistribution alone, (b) the contraction that pipelines it behind the GEMMs
         try:
@@ -284,7 +292,7 @@ def main():
         except Exception as e:  # a side measurement never takes the bench down
             side["redistribution_error"] = str(e)[:200]
     flops_step = flops_of(L, n)
-    if not args.no_side and world == 1:
+    if world == 1 and "3m" not in skip:
         # the same contraction with complex products in the opt-in 3-multiplication form: a
         # comparison point (not the headline: only a normwise error bound), and ~20 ms of MFMA
         # load right before the timed region
@@ -351,7 +359,7 @@ def main():
     base = None
     if rank == 0 and world == 1 and not args.no_cpu:
         base = cpu_baseline()
-        if not args.no_side:
+        if not {"permute", "bsr"} <= skip:
             side.update(cpu_side_baselines())
 
     traffic, traffic_src = pmc_traffic("dma_kernel<", "128, 128, 16, 4, 4")

@@ -412,6 +412,7 @@ int sbx_tune_set(const char *key, long long value) {
         else if (k == "bsr.variant") g_bsr_tune.variant = (int)value;
         else if (k == "bsr.ell9") g_bsr_tune.ell9 = (int)value;
         else if (k == "bsr.ell9_lds") g_bsr_tune.ell9_lds = (long)value;
+        else if (k == "bsr.colsplit") g_bsr_tune.colsplit = (long)value;
         else if (k == "gemm.m3") g_gemm_tune.m3 = (int)value;
         else if (k == "gemm.splits") g_gemm_tune.splits = (int)value;
         else throw Error("tune_set: unknown key " + k);
@@ -431,6 +432,7 @@ int sbx_tune_get(const char *key, long long *value) {
         else if (k == "bsr.variant") *value = g_bsr_tune.variant;
         else if (k == "bsr.ell9") *value = g_bsr_tune.ell9;
         else if (k == "bsr.ell9_lds") *value = g_bsr_tune.ell9_lds;
+        else if (k == "bsr.colsplit") *value = g_bsr_tune.colsplit;
         else if (k == "gemm.m3") *value = g_gemm_tune.m3;
         else if (k == "gemm.splits") *value = g_gemm_tune.splits;
         else throw Error("tune_get: unknown key " + k);

@@ -70,5 +70,22 @@ template <typename D> __device__ __forceinline__ void store_nt(D *p, D v) {
     }
 }
 
+/// Non-temporal (streaming) load of one element (data read once by the kernel)
+template <typename D> __device__ __forceinline__ D load_nt(const D *p) {
+    D v;
+    if constexpr (sizeof(D) == 16) {
+        typedef double v2 __attribute__((ext_vector_type(2)));
+        const v2 t = __builtin_nontemporal_load((const v2 *)p);
+        __builtin_memcpy(&v, &t, 16);
+    } else if constexpr (sizeof(D) == 8) {
+        const double t = __builtin_nontemporal_load((const double *)p);
+        __builtin_memcpy(&v, &t, 8);
+    } else {
+        const float t = __builtin_nontemporal_load((const float *)p);
+        __builtin_memcpy(&v, &t, 4);
+    }
+    return v;
+}
+
 } // namespace
 } // namespace sbx

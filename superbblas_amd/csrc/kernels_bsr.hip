@@ -681,8 +681,11 @@ void launch_ell_g(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_t s
 // workgroup streams the values into LDS, so the x gathers, the column reads and the value stream
 // are in flight together (bsr_ell_kernel: value stream, then the columns, then one x block at a
 // time); blocks j+PD are fetched while block j is applied.
-template <typename E, int BI, int BD, int G, int PD, bool YROW, bool XROW, int NT = 256>
+template <typename E, int BI, int BD, int G, int PD, bool YROW, bool XROW, int NT = 256,
+          int NTF = 0>
 __global__ void __launch_bounds__(NT) bsr_ell9_kernel(const BsrArgs p, int rb) {
+    // NTF (experiments): bit 0 = non-temporal value loads, bit 1 = non-temporal y stores
+    constexpr bool NTV = (NTF & 1) != 0, NTY = (NTF & 2) != 0;
     constexpr int NNZ = 9, BLK = BI * BD, NB = PD + 1;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     E *vals = (E *)smem;
@@ -733,7 +736,10 @@ __global__ void __launch_bounds__(NT) bsr_ell9_kernel(const BsrArgs p, int rb) {
     for (int e0 = threadIdx.x; e0 < nv; e0 += NT * 8) {
         E t[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) t[u] = v[vbase + min(e0 + NT * u, nv - 1)];
+        for (int u = 0; u < 8; ++u) {
+            const E *vp = v + vbase + min(e0 + NT * u, nv - 1);
+            t[u] = NTV ? load_nt(vp) : *vp;
+        }
 #pragma unroll
         for (int u = 0; u < 8; ++u)
             if (e0 + NT * u < nv) vals[e0 + NT * u] = t[u];
@@ -770,12 +776,17 @@ __global__ void __launch_bounds__(NT) bsr_ell9_kernel(const BsrArgs p, int rb) {
             if (col >= p.ncols) break;
             E *yp = YROW ? y + img * p.ldy + col : y + img + col * p.ldy;
             const E out = Ops<E>::scale(acc[c][k], p.alpha_re, p.alpha_im);
-            *yp = p.add ? Ops<E>::add(*yp, out) : out;
+            if (p.add)
+                *yp = Ops<E>::add(*yp, out);
+            else if constexpr (NTY)
+                store_nt(yp, out);
+            else
+                *yp = out;
         }
     }
 }
 
-template <typename E, int BI, int BD, int G, int PD, int NT = 256>
+template <typename E, int BI, int BD, int G, int PD, int NT = 256, int NTF = 0>
 void launch_ell9(const BsrArgs &a, bool yrow, bool xrow, hipStream_t s, long lds_bytes) {
     const long blk_bytes = 9L * BI * BD * (long)sizeof(E);
     const long ngroups = (a.ncols + G - 1) / G;
@@ -787,13 +798,13 @@ void launch_ell9(const BsrArgs &a, bool yrow, bool xrow, hipStream_t s, long lds
     const size_t lds = (size_t)rb * blk_bytes;
     KernelTimer timer("bsr", s);
     if (yrow && xrow)
-        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, true, true, NT>), dim3(blocks), dim3(NT), lds, s, a, rb);
+        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, true, true, NT, NTF>), dim3(blocks), dim3(NT), lds, s, a, rb);
     else if (yrow && !xrow)
-        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, true, false, NT>), dim3(blocks), dim3(NT), lds, s, a, rb);
+        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, true, false, NT, NTF>), dim3(blocks), dim3(NT), lds, s, a, rb);
     else if (!yrow && xrow)
-        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, false, true, NT>), dim3(blocks), dim3(NT), lds, s, a, rb);
+        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, false, true, NT, NTF>), dim3(blocks), dim3(NT), lds, s, a, rb);
     else
-        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, false, false, NT>), dim3(blocks), dim3(NT), lds, s, a, rb);
+        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, false, false, NT, NTF>), dim3(blocks), dim3(NT), lds, s, a, rb);
     SBX_HIP_CHECK(hipGetLastError());
 }
 
@@ -820,6 +831,11 @@ void launch_ell(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_t s) 
         case 5: return launch_ell9<E, BI, BD, 1, 1, 64>(a, yrow, xrow, s, lds);
         case 6: return launch_ell9<E, BI, BD, 1, 2, 128>(a, yrow, xrow, s, lds);
         case 7: return launch_ell9<E, BI, BD, 2, 2, 256>(a, yrow, xrow, s, lds);
+        case 8: return launch_ell9<E, BI, BD, 2, 1, 256, 2>(a, yrow, xrow, s, lds);
+        case 9: return launch_ell9<E, BI, BD, 2, 1, 256, 1>(a, yrow, xrow, s, lds);
+        case 10: return launch_ell9<E, BI, BD, 2, 1, 256, 3>(a, yrow, xrow, s, lds);
+        case 11: return launch_ell9<E, BI, BD, 2, 2, 256, 2>(a, yrow, xrow, s, lds);
+        case 12: return launch_ell9<E, BI, BD, 2, 2, 256, 3>(a, yrow, xrow, s, lds);
         default: return launch_ell9<E, BI, BD, 2, 1>(a, yrow, xrow, s, lds);
         }
     }
@@ -929,6 +945,28 @@ void launch_bsr(const BsrDesc &d, int device) {
     a.alpha_re = d.alpha.re;
     a.alpha_im = d.alpha.im;
     a.add = d.add ? 1 : 0;
+    // column passes (experiment, sbx_tune_set "bsr.colsplit"): with row-major x and y a launch
+    // over a column slice is the same product on shifted base pointers; fewer columns per pass
+    // shrink the x rows that must stay in L2 between a site's neighbours
+    const long cs = g_bsr_tune.colsplit;
+    if (cs > 0 && d.ncols > cs && d.x_row_major && d.y_row_major) {
+        const std::size_t es = dtype_size(d.t);
+        for (long c0 = 0; c0 < d.ncols; c0 += cs) {
+            BsrDesc q = d;
+            q.ncols = std::min(cs, d.ncols - c0);
+            q.x = (const char *)d.x + es * c0;
+            q.y = (char *)d.y + es * c0;
+            g_bsr_tune.colsplit = 0;
+            try {
+                launch_bsr(q, device);
+            } catch (...) {
+                g_bsr_tune.colsplit = cs;
+                throw;
+            }
+            g_bsr_tune.colsplit = cs;
+        }
+        return;
+    }
     switch (d.t) {
     case SBX_CDOUBLE: return launch_typed<double2>(a, d.num_nnz_per_row, d.y_row_major, d.x_row_major, s);
     case SBX_CFLOAT: return launch_typed<float2>(a, d.num_nnz_per_row, d.y_row_major, d.x_row_major, s);

@@ -228,6 +228,7 @@ struct BsrTune {
     int variant = 0; ///< BSR kernels: 0 = the library's choice, 1 = the round-1 kernels, 2 = no 12x12 block-staged kernel
     int ell9 = 0;    ///< 9-point ELL kernel shape (workgroup size / lookahead / columns per thread), 0 = default
     long ell9_lds = 0; ///< 9-point ELL kernel: bytes of block values staged per workgroup (0 = default)
+    long colsplit = 0; ///< rhs columns per launch (row-major x and y), 0 = all at once
 };
 extern BsrTune g_bsr_tune;
 

@@ -14,7 +14,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import superbblas_amd as sb  # noqa: E402
 
 VARIANTS = {0: "nt256 pd1 g2", 1: "nt64 pd1 g2", 2: "nt128 pd1 g2", 3: "nt64 pd2 g2",
-            4: "nt128 pd2 g2", 5: "nt64 pd1 g1", 6: "nt128 pd2 g1", 7: "nt256 pd2 g2"}
+            4: "nt128 pd2 g2", 5: "nt64 pd1 g1", 6: "nt128 pd2 g1", 7: "nt256 pd2 g2",
+            8: "nt256 pd1 g2 ntY", 9: "nt256 pd1 g2 ntV", 10: "nt256 pd1 g2 ntVY",
+            11: "nt256 pd2 g2 ntY", 12: "nt256 pd2 g2 ntVY"}
 
 
 def main():
@@ -48,7 +50,9 @@ def main():
                           0.0, px, "pxyztscn", [0] * 8, dimx, dimx, "p", [y])
         ref = None
         by = 16.0 * (81 * V + 2 * 3 * V * ncols) + 4.0 * (9 * V + V + 1)
-        for var, lds in [(v, l) for v in VARIANTS for l in (0, 6144, 12288, 24576, 49152)]:
+        vs = [int(v) for v in os.environ.get("VARIANTS", "").split(",") if v] or list(VARIANTS)
+        ls = [int(v) for v in os.environ.get("LDS", "0,6144,12288,24576,49152").split(",")]
+        for var, lds in [(v, l) for v in [0] + [v for v in vs if v != 0] for l in ls]:
             sb.tune_set("bsr.ell9", var)
             sb.tune_set("bsr.ell9_lds", lds)
             try:
