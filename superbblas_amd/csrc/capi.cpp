@@ -413,6 +413,12 @@ int sbx_tune_set(const char *key, long long value) {
         else if (k == "bsr.ell9") g_bsr_tune.ell9 = (int)value;
         else if (k == "bsr.ell9_lds") g_bsr_tune.ell9_lds = (long)value;
         else if (k == "bsr.colsplit") g_bsr_tune.colsplit = (long)value;
+        else if (k == "bsr.tile") g_bsr_tune.tile = (int)value;
+        else if (k == "bsr.tile_min_cols") g_bsr_tune.tile_min_cols = (long)value;
+        else if (k == "bsr.tile_slab") g_bsr_tune.tile_slab = (long)value;
+        else if (k == "bsr.tile_max_cols") g_bsr_tune.tile_max_cols = (long)value;
+        else if (k == "bsr.tile_rows") g_bsr_tune.tile_rows = (int)value;
+        else if (k == "bsr.probe") g_bsr_tune.probe = value;
         else if (k == "gemm.m3") g_gemm_tune.m3 = (int)value;
         else if (k == "gemm.splits") g_gemm_tune.splits = (int)value;
         else throw Error("tune_set: unknown key " + k);
@@ -433,6 +439,12 @@ int sbx_tune_get(const char *key, long long *value) {
         else if (k == "bsr.ell9") *value = g_bsr_tune.ell9;
         else if (k == "bsr.ell9_lds") *value = g_bsr_tune.ell9_lds;
         else if (k == "bsr.colsplit") *value = g_bsr_tune.colsplit;
+        else if (k == "bsr.tile") *value = g_bsr_tune.tile;
+        else if (k == "bsr.tile_min_cols") *value = g_bsr_tune.tile_min_cols;
+        else if (k == "bsr.tile_slab") *value = g_bsr_tune.tile_slab;
+        else if (k == "bsr.tile_max_cols") *value = g_bsr_tune.tile_max_cols;
+        else if (k == "bsr.tile_rows") *value = g_bsr_tune.tile_rows;
+        else if (k == "bsr.probe") *value = g_bsr_tune.probe;
         else if (k == "gemm.m3") *value = g_gemm_tune.m3;
         else if (k == "gemm.splits") *value = g_gemm_tune.splits;
         else throw Error("tune_get: unknown key " + k);

@@ -39,7 +39,15 @@ struct BsrArgs {
     long ncols;
     double alpha_re, alpha_im;
     int add;
+    unsigned long long *probe; // tools only (sbx_tune_set "bsr.probe"): per-workgroup time stamps
 };
+
+// tools only: 8 stamps per workgroup -- 100 MHz real time at start and end, then shader-clock
+// deltas of the kernel's phases
+__device__ __forceinline__ void probe_stamp(unsigned long long *probe, int slot,
+                                            unsigned long long v) {
+    if (probe && threadIdx.x == 0) probe[(long)blockIdx.x * 8 + slot] = v;
+}
 
 template <typename E, int BI_, int BD_, bool YROW, bool XROW>
 __global__ void __launch_bounds__(256) bsr_kernel(const BsrArgs p) {
@@ -682,9 +690,11 @@ void launch_ell_g(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_t s
 // are in flight together (bsr_ell_kernel: value stream, then the columns, then one x block at a
 // time); blocks j+PD are fetched while block j is applied.
 template <typename E, int BI, int BD, int G, int PD, bool YROW, bool XROW, int NT = 256,
-          int NTF = 0>
+          int NTF = 0, bool SC = false>
 __global__ void __launch_bounds__(NT) bsr_ell9_kernel(const BsrArgs p, int rb) {
     // NTF (experiments): bit 0 = non-temporal value loads, bit 1 = non-temporal y stores
+    // SC: a thread's G columns are g, g + ngroups, ... (the lanes of one row read consecutive
+    // columns in each load) instead of g*G .. g*G + G-1
     constexpr bool NTV = (NTF & 1) != 0, NTY = (NTF & 2) != 0;
     constexpr int NNZ = 9, BLK = BI * BD, NB = PD + 1;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -695,6 +705,8 @@ __global__ void __launch_bounds__(NT) bsr_ell9_kernel(const BsrArgs p, int rb) {
     const int nwg = gridDim.x, bid = blockIdx.x;
     const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
     const int chunk = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    const unsigned long long rt0 = p.probe ? __builtin_amdgcn_s_memrealtime() : 0;
+    const unsigned long long c0 = p.probe ? __builtin_amdgcn_s_memtime() : 0;
     const long row0 = (long)chunk * rb;
     const int nrows = (int)min((long)rb, p.block_rows - row0);
     const long ngroups = (p.ncols + G - 1) / G;
@@ -716,7 +728,7 @@ __global__ void __launch_bounds__(NT) bsr_ell9_kernel(const BsrArgs p, int rb) {
     }
     long colv[G];
 #pragma unroll
-    for (int k = 0; k < G; ++k) colv[k] = min(g * G + k, p.ncols - 1);
+    for (int k = 0; k < G; ++k) colv[k] = min(SC ? g + k * ngroups : g * G + k, p.ncols - 1);
     int dj[NNZ];
 #pragma unroll
     for (int j = 0; j < NNZ; ++j) dj[j] = p.jj[(row0 + r) * NNZ + j];
@@ -745,6 +757,11 @@ __global__ void __launch_bounds__(NT) bsr_ell9_kernel(const BsrArgs p, int rb) {
             if (e0 + NT * u < nv) vals[e0 + NT * u] = t[u];
     }
     __syncthreads();
+    const unsigned long long c1 = p.probe ? __builtin_amdgcn_s_memtime() : 0;
+    if (p.probe) {
+        probe_stamp(p.probe, 0, rt0);
+        probe_stamp(p.probe, 3, c1 - c0);
+    }
     if (!active) return;
     E acc[BI][G];
 #pragma unroll
@@ -772,7 +789,7 @@ __global__ void __launch_bounds__(NT) bsr_ell9_kernel(const BsrArgs p, int rb) {
         const long img = (row0 + r) * BI + c;
 #pragma unroll
         for (int k = 0; k < G; ++k) {
-            const long col = g * G + k;
+            const long col = SC ? g + k * ngroups : g * G + k;
             if (col >= p.ncols) break;
             E *yp = YROW ? y + img * p.ldy + col : y + img + col * p.ldy;
             const E out = Ops<E>::scale(acc[c][k], p.alpha_re, p.alpha_im);
@@ -784,9 +801,13 @@ __global__ void __launch_bounds__(NT) bsr_ell9_kernel(const BsrArgs p, int rb) {
                 *yp = out;
         }
     }
+    if (p.probe) {
+        probe_stamp(p.probe, 5, __builtin_amdgcn_s_memtime() - c1);
+        probe_stamp(p.probe, 1, __builtin_amdgcn_s_memrealtime());
+    }
 }
 
-template <typename E, int BI, int BD, int G, int PD, int NT = 256, int NTF = 0>
+template <typename E, int BI, int BD, int G, int PD, int NT = 256, int NTF = 0, bool SC = false>
 void launch_ell9(const BsrArgs &a, bool yrow, bool xrow, hipStream_t s, long lds_bytes) {
     const long blk_bytes = 9L * BI * BD * (long)sizeof(E);
     const long ngroups = (a.ncols + G - 1) / G;
@@ -798,13 +819,13 @@ void launch_ell9(const BsrArgs &a, bool yrow, bool xrow, hipStream_t s, long lds
     const size_t lds = (size_t)rb * blk_bytes;
     KernelTimer timer("bsr", s);
     if (yrow && xrow)
-        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, true, true, NT, NTF>), dim3(blocks), dim3(NT), lds, s, a, rb);
+        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, true, true, NT, NTF, SC>), dim3(blocks), dim3(NT), lds, s, a, rb);
     else if (yrow && !xrow)
-        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, true, false, NT, NTF>), dim3(blocks), dim3(NT), lds, s, a, rb);
+        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, true, false, NT, NTF, SC>), dim3(blocks), dim3(NT), lds, s, a, rb);
     else if (!yrow && xrow)
-        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, false, true, NT, NTF>), dim3(blocks), dim3(NT), lds, s, a, rb);
+        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, false, true, NT, NTF, SC>), dim3(blocks), dim3(NT), lds, s, a, rb);
     else
-        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, false, false, NT, NTF>), dim3(blocks), dim3(NT), lds, s, a, rb);
+        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, false, false, NT, NTF, SC>), dim3(blocks), dim3(NT), lds, s, a, rb);
     SBX_HIP_CHECK(hipGetLastError());
 }
 
@@ -836,10 +857,224 @@ void launch_ell(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_t s) 
         case 10: return launch_ell9<E, BI, BD, 2, 1, 256, 3>(a, yrow, xrow, s, lds);
         case 11: return launch_ell9<E, BI, BD, 2, 2, 256, 2>(a, yrow, xrow, s, lds);
         case 12: return launch_ell9<E, BI, BD, 2, 2, 256, 3>(a, yrow, xrow, s, lds);
+        case 13: return launch_ell9<E, BI, BD, 2, 1, 256, 0, true>(a, yrow, xrow, s, lds);
+        case 14: return launch_ell9<E, BI, BD, 2, 2, 256, 0, true>(a, yrow, xrow, s, lds);
+        case 15: return launch_ell9<E, BI, BD, 4, 1, 256, 0, true>(a, yrow, xrow, s, lds);
         default: return launch_ell9<E, BI, BD, 2, 1>(a, yrow, xrow, s, lds);
         }
     }
     launch_ell_g<E, BI, BD, 2>(a, nnz, yrow, xrow, s, ELL_LDS_BYTES);
+}
+
+// Lattice-tiled 9-point 3x3 product, complex<double> (plan: bsr.cpp build_tile_plan).  A
+// workgroup owns one tile of R block rows and one slab of at most 32 rhs columns, one column per
+// thread:
+//   0) the tile's block-row and staged-row ids into LDS, beside the per-row entry loads;
+//   1) the gathers of each row's direct (halo) x rows into registers;
+//   2) the tile's values and its staged x rows (the domain rows two or more of its rows use)
+//      into LDS by LDS-DMA (buffer_load_dwordx4 ... lds: one 16-B element per lane, no VGPRs,
+//      all in flight at once; ids of -1 read zero through the buffer descriptor);
+//   3) the products: direct blocks from registers, staged ones from LDS.
+// Each interior x row of a tile is fetched once instead of once per block that uses it: the
+// chunked kernel (bsr_ell9_kernel) is bound by those fetches in the vector-memory pipeline and
+// by the latency of its one-block-ahead gathers (tools/bsr_timeline.py).
+struct TileArgs {
+    const int *rows;
+    const unsigned *ent;
+    const int *staged;
+    int R, S;
+    int c0, nc;          // the column slab
+    int uv, ux;          // DMA instructions per wave: values, staged x
+    unsigned v_bytes, x_bytes;
+    unsigned div81_m, rowlen_m, nc_m; // magic multipliers (n / d = (umulhi(n, m) + n) >> s)
+    int rowlen_s, nc_s;
+};
+
+__device__ __forceinline__ unsigned fdiv(unsigned n, unsigned m, int s) {
+    return (unsigned)(((unsigned long long)__umulhi(n, m) + n) >> s);
+}
+
+static void magic(unsigned d, unsigned &m, int &s) {
+    s = 0;
+    while ((1ull << s) < d) ++s;
+    m = (unsigned)((((1ull << 32) * ((1ull << s) - d)) / d) + 1);
+}
+
+__device__ __forceinline__ unsigned lds_u32(const void *p) {
+    return (unsigned)(size_t)(const __attribute__((address_space(3))) void *)p;
+}
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, unsigned off, unsigned dst) {
+    // inline asm: hipcc does not order its ds_reads against an LDS-DMA it cannot see; the kernel
+    // retires the DMA with an explicit vmcnt(0) before its barrier
+    asm volatile("s_mov_b32 m0, %1\n\t"
+                 "s_nop 0\n\t"
+                 "buffer_load_dwordx4 %0, %2, 0 offen lds"
+                 :
+                 : "v"(off), "s"(dst), "s"(rs)
+                 : "memory", "m0");
+}
+
+template <int ND, bool YROW, bool XROW>
+__global__ void __launch_bounds__(512) bsr_tile_kernel(const BsrArgs p, const TileArgs t) {
+    typedef double2 E;
+    constexpr int NNZ = 9, BI = 3, BD = 3, BLK = 9, NE = ND + NNZ, VB = NNZ * BLK;
+    constexpr unsigned NONE = 15u, OOB = 0x80000000u;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int R = t.R, S = t.S, nc = t.nc, nt = blockDim.x, tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    E *vals = (E *)smem;
+    E *xs = vals + t.uv * nt;
+    int *ids = (int *)(xs + t.ux * nt);
+    const E *__restrict__ x = (const E *)p.x;
+    E *__restrict__ y = (E *)p.y;
+    // consecutive tiles on one XCD (neighbouring tiles share halo rows in its L2)
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const long chunk = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    const unsigned long long rt0 = p.probe ? __builtin_amdgcn_s_memrealtime() : 0;
+    const unsigned long long c0 = p.probe ? __builtin_amdgcn_s_memtime() : 0;
+    const int *__restrict__ rows = t.rows + chunk * R;
+    const int *__restrict__ staged = t.staged + chunk * S;
+    const int i = tid / nc, g = tid - i * nc, col = t.c0 + g;
+    const int row = i < R ? rows[i] : -1;
+    const bool active = row >= 0;
+    // 0) the tile's block rows and staged domain rows (ids) into LDS, beside the entry loads
+    for (int q = tid; q < R + S; q += nt) ids[q] = q < R ? rows[q] : staged[q - R];
+    unsigned ent[NE];
+#pragma unroll
+    for (int q = 0; q < NE; ++q) ent[q] = active ? t.ent[(chunk * R + i) * NE + q] : NONE << 28;
+    // 1) the direct (halo) x rows into registers
+    E xg[ND][BD];
+#pragma unroll
+    for (int q = 0; q < ND; ++q) {
+        const long d = (ent[q] >> 28) != NONE ? (long)(ent[q] & 0x0fffffffu) : 0;
+#pragma unroll
+        for (int e = 0; e < BD; ++e) xg[q][e] = XROW ? x[(d + e) * p.ldx + col] : x[(d + e) + (long)col * p.ldx];
+    }
+    __syncthreads();
+    const unsigned long long c1 = p.probe ? __builtin_amdgcn_s_memtime() : 0;
+    // 2) values and staged x rows by LDS-DMA (lane-linear LDS destination)
+    const __amdgpu_buffer_rsrc_t rsv =
+        __builtin_amdgcn_make_buffer_rsrc((void *)p.v, (short)0, (int)t.v_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsx =
+        __builtin_amdgcn_make_buffer_rsrc((void *)p.x, (short)0, (int)t.x_bytes, 0x00020000);
+    const unsigned vbase = lds_u32(vals) + (unsigned)wave * 1024u;
+    const int nv = R * VB;
+    for (int u = 0; u < t.uv; ++u) {
+        const unsigned e = (unsigned)(u * nt + tid), r = fdiv(e, t.div81_m, 7);
+        const int rr = (int)e < nv ? ids[r] : -1;
+        const unsigned off = rr >= 0 ? ((unsigned)rr * VB + (e - r * VB)) * 16u : OOB;
+        dma16(rsv, off, __builtin_amdgcn_readfirstlane(vbase + (unsigned)(u * nt) * 16u));
+    }
+    const unsigned xbase = lds_u32(xs) + (unsigned)wave * 1024u;
+    const int rowlen = BD * nc, nx = S * rowlen;
+    for (int u = 0; u < t.ux; ++u) {
+        const unsigned f = (unsigned)(u * nt + tid), q = fdiv(f, t.rowlen_m, t.rowlen_s);
+        const unsigned rem = f - q * (unsigned)rowlen, er = fdiv(rem, t.nc_m, t.nc_s);
+        const unsigned cl = rem - er * (unsigned)nc;
+        const int d = (int)f < nx ? ids[R + q] : -1;
+        const long el = XROW ? ((long)d + er) * p.ldx + t.c0 + cl
+                             : ((long)d + er) + (long)(t.c0 + cl) * p.ldx;
+        const unsigned off = d >= 0 ? (unsigned)(el * 16) : OOB;
+        dma16(rsx, off, __builtin_amdgcn_readfirstlane(xbase + (unsigned)(u * nt) * 16u));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned long long c2 = p.probe ? __builtin_amdgcn_s_memtime() : 0;
+    __syncthreads();
+    const unsigned long long c3 = p.probe ? __builtin_amdgcn_s_memtime() : 0;
+    if (p.probe) {
+        probe_stamp(p.probe, 0, rt0);
+        probe_stamp(p.probe, 2, c1 - c0);
+        probe_stamp(p.probe, 3, c2 - c1);
+        probe_stamp(p.probe, 4, c3 - c2);
+    }
+    if (!active) {
+        if (p.probe) probe_stamp(p.probe, 1, __builtin_amdgcn_s_memrealtime());
+        return;
+    }
+    // 3) the products: direct blocks from registers, staged ones from LDS
+    E acc[BI];
+#pragma unroll
+    for (int c = 0; c < BI; ++c) acc[c] = Ops<E>::zero();
+    const E *vr = vals + i * VB;
+    auto apply = [&](const E *vb, const E *xv) {
+#pragma unroll
+        for (int e = 0; e < BD; ++e)
+#pragma unroll
+            for (int c = 0; c < BI; ++c) {
+                const E a = p.block_im_fast ? vb[c + e * BI] : vb[c * BD + e];
+                acc[c] = Ops<E>::fma(a, xv[e], acc[c]);
+            }
+    };
+#pragma unroll
+    for (int q = 0; q < ND; ++q) {
+        const unsigned j = ent[q] >> 28;
+        if (j == NONE) continue;
+        apply(vr + j * BLK, xg[q]);
+    }
+#pragma unroll
+    for (int q = ND; q < NE; ++q) {
+        const unsigned j = ent[q] >> 28;
+        if (j == NONE) continue;
+        const E *xr = xs + (ent[q] & 0x0fffffffu) * rowlen + g;
+        E xv[BD];
+#pragma unroll
+        for (int e = 0; e < BD; ++e) xv[e] = xr[e * nc];
+        apply(vr + j * BLK, xv);
+    }
+#pragma unroll
+    for (int c = 0; c < BI; ++c) {
+        const long img = (long)row * BI + c;
+        E *yp = YROW ? y + img * p.ldy + col : y + img + (long)col * p.ldy;
+        const E out = Ops<E>::scale(acc[c], p.alpha_re, p.alpha_im);
+        *yp = p.add ? Ops<E>::add(*yp, out) : out;
+    }
+    if (p.probe) {
+        probe_stamp(p.probe, 5, __builtin_amdgcn_s_memtime() - c3);
+        probe_stamp(p.probe, 1, __builtin_amdgcn_s_memrealtime());
+    }
+}
+
+constexpr int TILE_ND = 4;           // direct entries per row (bsr.cpp: build_tile_plan nd)
+constexpr long TILE_LDS_MAX = 65536; // two or more workgroups per CU
+constexpr int TILE_MAX_SLAB = 32;    // rhs columns per workgroup (one per thread)
+
+/// complex<double> operators with a tile plan: column slabs of at most 32 (false: not this shape)
+bool launch_tile(const BsrArgs &a, TileArgs t, long nchunks, long x_rows, bool yrow, bool xrow,
+                 hipStream_t s) {
+    if (a.ncols < g_bsr_tune.tile_min_cols || a.ncols > g_bsr_tune.tile_max_cols ||
+        nchunks >= (1L << 31))
+        return false;
+    const long v_bytes = a.block_rows * 81L * 16;
+    const long x_bytes = (xrow ? x_rows * a.ldx : a.ldx * a.ncols) * 16;
+    if (v_bytes >= (1L << 31) || x_bytes >= (1L << 31)) return false;
+    const long max_slab = g_bsr_tune.tile_slab > 0 ? g_bsr_tune.tile_slab : TILE_MAX_SLAB;
+    const long nslab = (a.ncols + max_slab - 1) / max_slab;
+    const int ncs = (int)((a.ncols + nslab - 1) / nslab);
+    const int nt = (t.R * ncs + 63) / 64 * 64;
+    if (nt > 512) return false;
+    t.uv = (t.R * 81 + nt - 1) / nt;
+    const long max_ux = ((long)t.S * 3 * ncs + nt - 1) / nt;
+    const size_t lds = (size_t)(t.uv + max_ux) * nt * 16 + 4 * (size_t)(t.R + t.S);
+    if ((long)lds > TILE_LDS_MAX) return false;
+    t.v_bytes = (unsigned)v_bytes;
+    t.x_bytes = (unsigned)x_bytes;
+    KernelTimer timer("bsr", s);
+    for (long c0 = 0; c0 < a.ncols; c0 += ncs) {
+        t.c0 = (int)c0;
+        t.nc = (int)std::min<long>(ncs, a.ncols - c0);
+        t.ux = (t.S * 3 * t.nc + nt - 1) / nt;
+        magic((unsigned)(3 * t.nc), t.rowlen_m, t.rowlen_s);
+        magic((unsigned)t.nc, t.nc_m, t.nc_s);
+        int s81;
+        magic(81, t.div81_m, s81); // s81 == 7 (the kernel's constant)
+        auto kern = yrow ? (xrow ? bsr_tile_kernel<TILE_ND, true, true> : bsr_tile_kernel<TILE_ND, true, false>)
+                         : (xrow ? bsr_tile_kernel<TILE_ND, false, true> : bsr_tile_kernel<TILE_ND, false, false>);
+        hipLaunchKernelGGL(kern, dim3(nchunks), dim3(nt), lds, s, a, t);
+        SBX_HIP_CHECK(hipGetLastError());
+    }
+    return true;
 }
 
 template <typename E, int BI, int BD>
@@ -945,6 +1180,7 @@ void launch_bsr(const BsrDesc &d, int device) {
     a.alpha_re = d.alpha.re;
     a.alpha_im = d.alpha.im;
     a.add = d.add ? 1 : 0;
+    a.probe = (unsigned long long *)g_bsr_tune.probe;
     // column passes (experiment, sbx_tune_set "bsr.colsplit"): with row-major x and y a launch
     // over a column slice is the same product on shifted base pointers; fewer columns per pass
     // shrink the x rows that must stay in L2 between a site's neighbours
@@ -966,6 +1202,16 @@ void launch_bsr(const BsrDesc &d, int device) {
             g_bsr_tune.colsplit = cs;
         }
         return;
+    }
+    if (d.tile_R > 0 && g_bsr_tune.tile && g_bsr_tune.variant != 1 && d.t == SBX_CDOUBLE &&
+        d.bi == 3 && d.bd == 3 && d.num_nnz_per_row == 9) {
+        TileArgs t{};
+        t.rows = d.tile_rows;
+        t.ent = d.tile_ent;
+        t.staged = d.tile_staged;
+        t.R = d.tile_R;
+        t.S = d.tile_S;
+        if (launch_tile(a, t, d.tile_chunks, d.x_rows, d.y_row_major, d.x_row_major, s)) return;
     }
     switch (d.t) {
     case SBX_CDOUBLE: return launch_typed<double2>(a, d.num_nnz_per_row, d.y_row_major, d.x_row_major, s);

@@ -229,6 +229,12 @@ struct BsrTune {
     int ell9 = 0;    ///< 9-point ELL kernel shape (workgroup size / lookahead / columns per thread), 0 = default
     long ell9_lds = 0; ///< 9-point ELL kernel: bytes of block values staged per workgroup (0 = default)
     long colsplit = 0; ///< rhs columns per launch (row-major x and y), 0 = all at once
+    int tile = 1;      ///< 9-point 3x3 operators: lattice-tiled kernel with x reuse in LDS (0 = off)
+    long tile_min_cols = 8;  ///< ... for this many rhs columns ...
+    long tile_max_cols = 16; ///< ... up to this many (measured: the chunked kernel is as fast or faster outside)
+    long tile_slab = 0;      ///< ... rhs columns per workgroup (0 = default, 32)
+    int tile_rows = 16;     ///< ... block rows per tile (the plan, built by create_bsr)
+    long long probe = 0;    ///< tools only: device buffer for per-workgroup time stamps
 };
 extern BsrTune g_bsr_tune;
 
@@ -248,6 +254,7 @@ struct BsrDesc {
     int num_nnz_per_row; ///< >0 if all rows have the same count (ELL), else -1
     const void *x;
     long ldx;
+    long x_rows = 0; ///< domain rows of x (the component's domain volume)
     bool x_row_major; ///< x(d, col) = x[d*ldx + col] if row major, else x[d + col*ldx]
     void *y;
     long ldy;
@@ -259,6 +266,16 @@ struct BsrDesc {
     // (block row, bi, ncols, ki), both row major; jj holds the domain site of each nonzero
     int ki = 1, kd = 1;
     const void *kron = nullptr; ///< num_nnz_per_row matrices of ki x kd
+    // lattice-tile plan of a 9-nonzero 3x3 operator (bsr.cpp build_tile_plan), or tile_R = 0:
+    // chunks of tile_R block rows (tile_rows, -1 = padding), per row tile_nd direct entries then
+    // num_nnz_per_row staged entries ((j << 28) | index, j = 15: none; index = domain block row
+    // for direct entries, slot in the chunk's staged list for staged ones), and per chunk tile_S
+    // staged domain block rows (-1 = padding), read into LDS once and shared by the chunk's rows
+    int tile_R = 0, tile_S = 0, tile_nd = 0;
+    long tile_chunks = 0;
+    const int *tile_rows = nullptr;
+    const unsigned *tile_ent = nullptr;
+    const int *tile_staged = nullptr;
 };
 void launch_bsr(const BsrDesc &d, int device);
 void launch_bsr_kron(const BsrDesc &d, int device);

@@ -16,7 +16,8 @@ import superbblas_amd as sb  # noqa: E402
 VARIANTS = {0: "nt256 pd1 g2", 1: "nt64 pd1 g2", 2: "nt128 pd1 g2", 3: "nt64 pd2 g2",
             4: "nt128 pd2 g2", 5: "nt64 pd1 g1", 6: "nt128 pd2 g1", 7: "nt256 pd2 g2",
             8: "nt256 pd1 g2 ntY", 9: "nt256 pd1 g2 ntV", 10: "nt256 pd1 g2 ntVY",
-            11: "nt256 pd2 g2 ntY", 12: "nt256 pd2 g2 ntVY"}
+            11: "nt256 pd2 g2 ntY", 12: "nt256 pd2 g2 ntVY",
+            13: "nt256 pd1 g2 sc", 14: "nt256 pd2 g2 sc", 15: "nt256 pd1 g4 sc"}
 
 
 def main():
