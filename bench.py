@@ -913,10 +913,10 @@ def bsr_bench(sb, dev, L, ncols_list=(1, 12, 64), reps=5):
         bytes_ = 16.0 * (81 * V + 2 * 3 * V * ncols) + 4.0 * (9 * V + V + 1)
         tk = bms / max(bcalls, 1) / 1e3
         p = "bsr_n%d_" % ncols
-        tiled = (sb.tune_get("bsr.tile") and sb.tune_get("bsr.tile_min_cols") <= ncols
-                 <= sb.tune_get("bsr.tile_max_cols"))
-        out[p + "kernel"] = ("bsr_tile_kernel (2x2x2x2 lattice tiles, x rows shared in LDS)"
-                             if tiled else "bsr_ell9_kernel (row chunks)")
+        if ncols <= sb.tune_get("bsr.row_max_cols"):
+            out[p + "kernel"] = "bsr_ell9_row_kernel (one thread per nonzero block, values by LDS-DMA)"
+        else:
+            out[p + "kernel"] = "bsr_ell9_kernel (row chunks, values by LDS-DMA)"
         out.update({p + "GFLOPs": round(flops / t / 1e9, 1), p + "GBps": round(bytes_ / t / 1e9, 1),
                     p + "ms": round(t * 1e3, 4), p + "kernel_ms": round(tk * 1e3, 4),
                     p + "kernel_GBps": round(bytes_ / tk / 1e9, 1),

@@ -319,7 +319,7 @@ BsrOp *bsr_create(int nd, int ni, int dtype, const std::vector<std::vector<Range
                 std::vector<long> site;
                 for (int d = 0; d < ni; ++d)
                     if (ri.size[d] / blocki[d] > 1) site.push_back(ri.size[d] / blocki[d]);
-                if (g_bsr_tune.tile_rows >= 2 && g_bsr_tune.tile_rows <= 128)
+                if (g_bsr_tune.tile && g_bsr_tune.tile_rows >= 2 && g_bsr_tune.tile_rows <= 128)
                     build_tile_plan(bc, site, 9, g_bsr_tune.tile_rows, 4);
             }
         }

@@ -416,6 +416,8 @@ int sbx_tune_set(const char *key, long long value) {
         else if (k == "bsr.tile") g_bsr_tune.tile = (int)value;
         else if (k == "bsr.tile_min_cols") g_bsr_tune.tile_min_cols = (long)value;
         else if (k == "bsr.tile_slab") g_bsr_tune.tile_slab = (long)value;
+        else if (k == "bsr.row_max_cols") g_bsr_tune.row_max_cols = (long)value;
+        else if (k == "bsr.row_dma") g_bsr_tune.row_dma = (int)value;
         else if (k == "bsr.tile_max_cols") g_bsr_tune.tile_max_cols = (long)value;
         else if (k == "bsr.tile_rows") g_bsr_tune.tile_rows = (int)value;
         else if (k == "bsr.probe") g_bsr_tune.probe = value;
@@ -442,6 +444,8 @@ int sbx_tune_get(const char *key, long long *value) {
         else if (k == "bsr.tile") *value = g_bsr_tune.tile;
         else if (k == "bsr.tile_min_cols") *value = g_bsr_tune.tile_min_cols;
         else if (k == "bsr.tile_slab") *value = g_bsr_tune.tile_slab;
+        else if (k == "bsr.row_max_cols") *value = g_bsr_tune.row_max_cols;
+        else if (k == "bsr.row_dma") *value = g_bsr_tune.row_dma;
         else if (k == "bsr.tile_max_cols") *value = g_bsr_tune.tile_max_cols;
         else if (k == "bsr.tile_rows") *value = g_bsr_tune.tile_rows;
         else if (k == "bsr.probe") *value = g_bsr_tune.probe;

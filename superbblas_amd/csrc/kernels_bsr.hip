@@ -684,6 +684,21 @@ void launch_ell_g(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_t s
     SBX_HIP_CHECK(hipGetLastError());
 }
 
+__device__ __forceinline__ unsigned lds_u32(const void *p) {
+    return (unsigned)(size_t)(const __attribute__((address_space(3))) void *)p;
+}
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, unsigned off, unsigned dst) {
+    // inline asm: hipcc does not order its ds_reads against an LDS-DMA it cannot see; the kernel
+    // retires the DMA with an explicit vmcnt(0) before its barrier
+    asm volatile("s_mov_b32 m0, %1\n\t"
+                 "s_nop 0\n\t"
+                 "buffer_load_dwordx4 %0, %2, 0 offen lds"
+                 :
+                 : "v"(off), "s"(dst), "s"(rs)
+                 : "memory", "m0");
+}
+
 // 9-point ELL form of bsr_ell_kernel: each thread reads its block row's 9 block columns straight
 // from global memory into registers and issues the x rows of its first PD blocks before the
 // workgroup streams the values into LDS, so the x gathers, the column reads and the value stream
@@ -695,7 +710,9 @@ __global__ void __launch_bounds__(NT) bsr_ell9_kernel(const BsrArgs p, int rb) {
     // NTF (experiments): bit 0 = non-temporal value loads, bit 1 = non-temporal y stores
     // SC: a thread's G columns are g, g + ngroups, ... (the lanes of one row read consecutive
     // columns in each load) instead of g*G .. g*G + G-1
-    constexpr bool NTV = (NTF & 1) != 0, NTY = (NTF & 2) != 0;
+    // NTF bit 2: the values staged by LDS-DMA (16-byte elements; launcher: 32-bit offsets)
+    constexpr bool NTV = (NTF & 1) != 0, NTY = (NTF & 2) != 0, DMAV = (NTF & 4) != 0;
+    static_assert(!DMAV || sizeof(E) == 16, "LDS-DMA staging takes 16-byte elements");
     constexpr int NNZ = 9, BLK = BI * BD, NB = PD + 1;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     E *vals = (E *)smem;
@@ -745,16 +762,28 @@ __global__ void __launch_bounds__(NT) bsr_ell9_kernel(const BsrArgs p, int rb) {
     for (int j = 0; j < PD; ++j) fetch(dj[j], xb[j]);
     const long vbase = row0 * NNZ * BLK;
     const int nv = nrows * NNZ * BLK;
-    for (int e0 = threadIdx.x; e0 < nv; e0 += NT * 8) {
-        E t[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const E *vp = v + vbase + min(e0 + NT * u, nv - 1);
-            t[u] = NTV ? load_nt(vp) : *vp;
+    if constexpr (DMAV) {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)p.v, (short)0, (int)(p.block_rows * NNZ * BLK * 16), 0x00020000);
+        const unsigned base = lds_u32(vals) + (unsigned)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * 1024u;
+        for (int u = 0; u * NT < nv; ++u) {
+            const int e = u * NT + (int)threadIdx.x;
+            const unsigned off = e < nv ? (unsigned)((vbase + e) * 16) : 0x80000000u;
+            dma16(rs, off, __builtin_amdgcn_readfirstlane(base + (unsigned)(u * NT) * 16u));
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+        for (int e0 = threadIdx.x; e0 < nv; e0 += NT * 8) {
+            E t[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-            if (e0 + NT * u < nv) vals[e0 + NT * u] = t[u];
+            for (int u = 0; u < 8; ++u) {
+                const E *vp = v + vbase + min(e0 + NT * u, nv - 1);
+                t[u] = NTV ? load_nt(vp) : *vp;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (e0 + NT * u < nv) vals[e0 + NT * u] = t[u];
+        }
     }
     __syncthreads();
     const unsigned long long c1 = p.probe ? __builtin_amdgcn_s_memtime() : 0;
@@ -816,7 +845,11 @@ void launch_ell9(const BsrArgs &a, bool yrow, bool xrow, hipStream_t s, long lds
     rb = (int)std::min<long>(rb, std::max(1L, NT / ngroups));
     const long blocks = (a.block_rows + rb - 1) / rb;
     if (blocks >= (1L << 31)) throw Error("bsr: grid too large");
-    const size_t lds = (size_t)rb * blk_bytes;
+    if constexpr ((NTF & 4) != 0)
+        if (a.block_rows * blk_bytes >= (1L << 31)) return launch_ell9<E, BI, BD, G, PD, NT, NTF & 3, SC>(a, yrow, xrow, s, lds_bytes);
+    // the DMA form fills whole workgroup-wide rows of 16-byte lanes
+    const size_t lds = (NTF & 4) != 0 ? (size_t)((rb * 9L * BI * BD + NT - 1) / NT * NT) * sizeof(E)
+                                      : (size_t)rb * blk_bytes;
     KernelTimer timer("bsr", s);
     if (yrow && xrow)
         hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, true, true, NT, NTF, SC>), dim3(blocks), dim3(NT), lds, s, a, rb);
@@ -826,6 +859,122 @@ void launch_ell9(const BsrArgs &a, bool yrow, bool xrow, hipStream_t s, long lds
         hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, false, true, NT, NTF, SC>), dim3(blocks), dim3(NT), lds, s, a, rb);
     else
         hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, false, false, NT, NTF, SC>), dim3(blocks), dim3(NT), lds, s, a, rb);
+    SBX_HIP_CHECK(hipGetLastError());
+}
+
+
+
+// Few rhs columns (n <= NC <= 4), 3x3 blocks, 9 per row: one thread per (block row, nonzero
+// block).  The value stream is read by 9 x more threads than in the row-chunk kernel, without
+// an LDS staging pass, and every thread has a single x gather (its block's domain rows) in
+// flight beside its 9 values; the 9 partial products of a row are summed through LDS in block
+// order.  At n = 1 the row-chunk kernel keeps one thread per row busy through 9 dependent
+// gathers (18 of 256 threads of a workgroup active).
+template <typename E, int NC, bool YROW, bool XROW, bool DMA>
+__global__ void __launch_bounds__(256) bsr_ell9_row_kernel(const BsrArgs p, unsigned v_bytes) {
+    constexpr int NNZ = 9, BI = 3, BD = 3, BLK = 9, RW = 28; // 28 rows x 9 blocks = 252 threads
+    constexpr int NV = RW * NNZ * BLK, NP = RW * NNZ * BI * NC;
+    constexpr int NS = (DMA ? (NV + 255) / 256 * 256 : 0) > NP ? (NV + 255) / 256 * 256 : NP;
+    __shared__ __attribute__((aligned(16))) E sh[NS]; // values (DMA), then the partial products
+    const E *__restrict__ v = (const E *)p.v;
+    const E *__restrict__ x = (const E *)p.x;
+    E *__restrict__ y = (E *)p.y;
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const long chunk = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    const int tid = threadIdx.x, rl = tid / NNZ, j = tid - rl * NNZ;
+    const long row = chunk * RW + rl;
+    const int ncols = (int)p.ncols;
+    const bool active = rl < RW && row < p.block_rows;
+    const long q = row * NNZ + j;
+    int dj = -1;
+    E xv[BD][NC];
+    if (active) {
+        dj = p.jj[q];
+        const long d = dj < 0 ? 0 : dj;
+#pragma unroll
+        for (int e = 0; e < BD; ++e)
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const long col = c < ncols ? c : 0;
+                xv[e][c] = XROW ? x[(d + e) * p.ldx + col] : x[(d + e) + col * p.ldx];
+            }
+    }
+    E a[BLK];
+    if constexpr (DMA) {
+        // the chunk's values, lane-linear into LDS (a contiguous run of the ELL value array)
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc((void *)p.v, (short)0, (int)v_bytes, 0x00020000);
+        const unsigned base = lds_u32(sh) + (unsigned)__builtin_amdgcn_readfirstlane(tid >> 6) * 1024u;
+        const unsigned v0 = (unsigned)(chunk * NV) * 16u;
+#pragma unroll
+        for (int u = 0; u < (NV + 255) / 256; ++u) {
+            const unsigned e = (unsigned)(u * 256 + tid);
+            const unsigned off = e < (unsigned)NV ? v0 + e * 16u : 0x80000000u;
+            dma16(rs, off, __builtin_amdgcn_readfirstlane(base + (unsigned)u * 4096u));
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (active) {
+#pragma unroll
+            for (int k = 0; k < BLK; ++k) a[k] = sh[(rl * NNZ + j) * BLK + k];
+        }
+        __syncthreads(); // the buffer now holds the partial products
+    } else if (active) {
+#pragma unroll
+        for (int k = 0; k < BLK; ++k) a[k] = v[q * BLK + k];
+    }
+    E *part = sh;
+    if (active) {
+#pragma unroll
+        for (int i = 0; i < BI; ++i)
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                E acc = Ops<E>::zero();
+#pragma unroll
+                for (int e = 0; e < BD; ++e)
+                    acc = Ops<E>::fma(p.block_im_fast ? a[i + e * BI] : a[i * BD + e], xv[e][c], acc);
+                part[((rl * NNZ + j) * BI + i) * NC + c] = dj < 0 ? Ops<E>::zero() : acc;
+            }
+    }
+    __syncthreads();
+    // sums: one thread per (row, i, column)
+    for (int o = tid; o < RW * BI * ncols; o += 256) {
+        const int r2 = o / (BI * ncols), rem = o - r2 * BI * ncols, i = rem / ncols, c = rem - i * ncols;
+        const long rw = chunk * RW + r2;
+        if (rw >= p.block_rows) continue;
+        E acc = part[((r2 * NNZ) * BI + i) * NC + c];
+#pragma unroll
+        for (int jj = 1; jj < NNZ; ++jj) acc = Ops<E>::add(acc, part[((r2 * NNZ + jj) * BI + i) * NC + c]);
+        const long img = rw * BI + i;
+        E *yp = YROW ? y + img * p.ldy + c : y + img + (long)c * p.ldy;
+        const E out = Ops<E>::scale(acc, p.alpha_re, p.alpha_im);
+        *yp = p.add ? Ops<E>::add(*yp, out) : out;
+    }
+}
+
+template <typename E, int NC>
+void launch_ell9_row(const BsrArgs &a, bool yrow, bool xrow, hipStream_t s) {
+    const long blocks = (a.block_rows + 27) / 28;
+    if (blocks >= (1L << 31)) throw Error("bsr: grid too large");
+    // the LDS-DMA form for 16-byte elements whose value array has 32-bit offsets
+    const long v_bytes = a.block_rows * 81L * (long)sizeof(E);
+    const bool dma = sizeof(E) == 16 && v_bytes < (1L << 31) && g_bsr_tune.row_dma;
+    KernelTimer timer("bsr", s);
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, s, a, (unsigned)v_bytes);
+    };
+    if (dma) {
+        if (yrow && xrow) go(bsr_ell9_row_kernel<E, NC, true, true, true>);
+        else if (yrow && !xrow) go(bsr_ell9_row_kernel<E, NC, true, false, true>);
+        else if (!yrow && xrow) go(bsr_ell9_row_kernel<E, NC, false, true, true>);
+        else go(bsr_ell9_row_kernel<E, NC, false, false, true>);
+    } else {
+        if (yrow && xrow) go(bsr_ell9_row_kernel<E, NC, true, true, false>);
+        else if (yrow && !xrow) go(bsr_ell9_row_kernel<E, NC, true, false, false>);
+        else if (!yrow && xrow) go(bsr_ell9_row_kernel<E, NC, false, true, false>);
+        else go(bsr_ell9_row_kernel<E, NC, false, false, false>);
+    }
     SBX_HIP_CHECK(hipGetLastError());
 }
 
@@ -840,6 +989,13 @@ void launch_ell(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_t s) 
     // 190 -> 181-188; at n = 12 6 / 8 / 16 / 24 KB: 72 / 52 / 48 / 45 us; one or four columns
     // per thread, or the x rows of two blocks ahead: 46-82 us).  The x gathers are the bound:
     // without them the value stream and y run at 5.5 TB/s (22 us at n = 12).
+    if constexpr (BI == 3 && BD == 3) {
+        if (nnz == 9 && g_bsr_tune.variant != 1 && a.ncols <= g_bsr_tune.row_max_cols) {
+            if (a.ncols == 1) return launch_ell9_row<E, 1>(a, yrow, xrow, s);
+            if (a.ncols == 2) return launch_ell9_row<E, 2>(a, yrow, xrow, s);
+            if (a.ncols <= 4) return launch_ell9_row<E, 4>(a, yrow, xrow, s);
+        }
+    }
     if (nnz == 9 && g_bsr_tune.variant != 1) {
         const long lds = g_bsr_tune.ell9_lds > 0 ? g_bsr_tune.ell9_lds : a.ncols >= 8 ? 12288 : 24576;
         // experiments (sbx_tune_set "bsr.ell9"): workgroup size 64 / 128 / 256 threads x one or
@@ -860,7 +1016,15 @@ void launch_ell(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_t s) 
         case 13: return launch_ell9<E, BI, BD, 2, 1, 256, 0, true>(a, yrow, xrow, s, lds);
         case 14: return launch_ell9<E, BI, BD, 2, 2, 256, 0, true>(a, yrow, xrow, s, lds);
         case 15: return launch_ell9<E, BI, BD, 4, 1, 256, 0, true>(a, yrow, xrow, s, lds);
-        default: return launch_ell9<E, BI, BD, 2, 1>(a, yrow, xrow, s, lds);
+        case 16: if constexpr (sizeof(E) == 16) return launch_ell9<E, BI, BD, 2, 1, 256, 4>(a, yrow, xrow, s, lds); else break;
+        case 17: if constexpr (sizeof(E) == 16) return launch_ell9<E, BI, BD, 2, 2, 256, 4>(a, yrow, xrow, s, lds); else break;
+        case 18: if constexpr (sizeof(E) == 16) return launch_ell9<E, BI, BD, 2, 1, 256, 4, true>(a, yrow, xrow, s, lds); else break;
+        case 19: return launch_ell9<E, BI, BD, 2, 1>(a, yrow, xrow, s, lds); // round-2a default
+        default:
+            // 16-byte elements: values by LDS-DMA, a row's lanes on consecutive columns
+            // (n = 12: 42 -> 39 us, n = 24: 67 -> 61, n = 64: 182 -> 172; profiles/r02_bsr_sweep.txt)
+            if constexpr (sizeof(E) == 16) return launch_ell9<E, BI, BD, 2, 1, 256, 4, true>(a, yrow, xrow, s, lds);
+            else return launch_ell9<E, BI, BD, 2, 1>(a, yrow, xrow, s, lds);
         }
     }
     launch_ell_g<E, BI, BD, 2>(a, nnz, yrow, xrow, s, ELL_LDS_BYTES);
@@ -898,21 +1062,6 @@ static void magic(unsigned d, unsigned &m, int &s) {
     s = 0;
     while ((1ull << s) < d) ++s;
     m = (unsigned)((((1ull << 32) * ((1ull << s) - d)) / d) + 1);
-}
-
-__device__ __forceinline__ unsigned lds_u32(const void *p) {
-    return (unsigned)(size_t)(const __attribute__((address_space(3))) void *)p;
-}
-
-__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, unsigned off, unsigned dst) {
-    // inline asm: hipcc does not order its ds_reads against an LDS-DMA it cannot see; the kernel
-    // retires the DMA with an explicit vmcnt(0) before its barrier
-    asm volatile("s_mov_b32 m0, %1\n\t"
-                 "s_nop 0\n\t"
-                 "buffer_load_dwordx4 %0, %2, 0 offen lds"
-                 :
-                 : "v"(off), "s"(dst), "s"(rs)
-                 : "memory", "m0");
 }
 
 template <int ND, bool YROW, bool XROW>

@@ -229,11 +229,14 @@ struct BsrTune {
     int ell9 = 0;    ///< 9-point ELL kernel shape (workgroup size / lookahead / columns per thread), 0 = default
     long ell9_lds = 0; ///< 9-point ELL kernel: bytes of block values staged per workgroup (0 = default)
     long colsplit = 0; ///< rhs columns per launch (row-major x and y), 0 = all at once
-    int tile = 1;      ///< 9-point 3x3 operators: lattice-tiled kernel with x reuse in LDS (0 = off)
+    int tile = 0;      ///< 9-point 3x3 operators: lattice-tiled kernel with x reuse in LDS (experiment; the
+                       ///< plan is built by create_bsr only while this is on)
     long tile_min_cols = 8;  ///< ... for this many rhs columns ...
     long tile_max_cols = 16; ///< ... up to this many (measured: the chunked kernel is as fast or faster outside)
     long tile_slab = 0;      ///< ... rhs columns per workgroup (0 = default, 32)
     int tile_rows = 16;     ///< ... block rows per tile (the plan, built by create_bsr)
+    long row_max_cols = 3;  ///< 9-point 3x3 operators: one thread per nonzero block up to this many rhs columns (0 = off)
+    int row_dma = 1;        ///< ... values staged by LDS-DMA (16-byte elements)
     long long probe = 0;    ///< tools only: device buffer for per-workgroup time stamps
 };
 extern BsrTune g_bsr_tune;

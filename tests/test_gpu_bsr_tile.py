@@ -1,6 +1,7 @@
 """The lattice-tiled 9-point 3x3 BSR kernel (kernels_bsr.hip bsr_tile_kernel, plan: bsr.cpp
-build_tile_plan) against the oracle's builtin BSR loop (bsr.h:535-650) and against the chunked
-ELL kernel (sbx_tune_set("bsr.tile", 0)), on random-valued operators: lattices whose extents are
+build_tile_plan; an opt-in, sbx_tune_set("bsr.tile", 1) before create_bsr) against the oracle's builtin BSR loop (bsr.h:535-650) and against the chunked
+ELL kernels (sbx_tune_set("bsr.tile", 0): the row-chunk kernel and, up to 3 columns, the
+one-thread-per-block kernel), on random-valued operators: lattices whose extents are
 not multiples of the tile, every element type, 1..80 rhs columns (the tiled shapes and the
 fallbacks around them; the tests lift the library's 8..16 column range), alpha / beta, column-major y, blocks with column -1 (the split core /
 halo operator of tests/bsr.cpp:402-545) and a random (non-lattice) pattern whose rows exceed the
@@ -67,6 +68,7 @@ def run_case(gpu, dims, ncols, tname, kind="stencil", alpha=1.0, beta=0.0, y_lay
     full = [([0] * 6, dim)]
     tt = {np.complex128: torch.complex128, np.complex64: torch.complex64,
           np.float64: torch.float64, np.float32: torch.float32}[dt]
+    sb.tune_set("bsr.tile", 1)  # the plan is built by create_bsr while the tiled kernel is on
     op = sb.create_bsr(full, dim, full, dim, [1, 1, 1, 1, 1, 3], [1, 1, 1, 1, 1, 3], False,
                        [torch.from_numpy(ii).to(gpu)], [torch.from_numpy(jj.reshape(-1)).to(gpu)],
                        [torch.from_numpy(vals).to(gpu)])
@@ -89,7 +91,7 @@ def run_case(gpu, dims, ncols, tname, kind="stencil", alpha=1.0, beta=0.0, y_lay
             torch.cuda.synchronize()
             outs.append(ty.cpu().numpy())
     finally:
-        sb.tune_set("bsr.tile", 1)
+        sb.tune_set("bsr.tile", 0)
         sb.tune_set("bsr.tile_min_cols", 8)
         sb.tune_set("bsr.tile_max_cols", 16)
         op.destroy()

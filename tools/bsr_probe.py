@@ -52,6 +52,10 @@ def main():
         sb.tune_set("bsr.ell9", int(os.environ["ELL9"]))
     if os.environ.get("TILE"):
         sb.tune_set("bsr.tile", int(os.environ["TILE"]))
+    if os.environ.get("ROWMAX"):
+        sb.tune_set("bsr.row_max_cols", int(os.environ["ROWMAX"]))
+    if os.environ.get("ROWDMA"):
+        sb.tune_set("bsr.row_dma", int(os.environ["ROWDMA"]))
     if os.environ.get("SLAB"):
         sb.tune_set("bsr.tile_slab", int(os.environ["SLAB"]))
     if os.environ.get("TROWS"):
@@ -93,6 +97,8 @@ def main():
             by = 16.0 * (81 * V + 2 * 3 * V * ncols) + 4.0 * (9 * V + V + 1)
             print(json.dumps({"stencil": kind, "tile": os.environ.get("TILE", "default"),
                               "slab": os.environ.get("SLAB", "default"),
+                              "row_max": os.environ.get("ROWMAX", "default"),
+                              "row_dma": os.environ.get("ROWDMA", "default"),
                               "rows": os.environ.get("TROWS", "16"),
                               "n": ncols, "kernel_us": round(t * 1e6, 2),
                               "frac_hbm": round(by / t / 8e12, 4)}), flush=True)

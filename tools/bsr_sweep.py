@@ -17,7 +17,8 @@ VARIANTS = {0: "nt256 pd1 g2", 1: "nt64 pd1 g2", 2: "nt128 pd1 g2", 3: "nt64 pd2
             4: "nt128 pd2 g2", 5: "nt64 pd1 g1", 6: "nt128 pd2 g1", 7: "nt256 pd2 g2",
             8: "nt256 pd1 g2 ntY", 9: "nt256 pd1 g2 ntV", 10: "nt256 pd1 g2 ntVY",
             11: "nt256 pd2 g2 ntY", 12: "nt256 pd2 g2 ntVY",
-            13: "nt256 pd1 g2 sc", 14: "nt256 pd2 g2 sc", 15: "nt256 pd1 g4 sc"}
+            13: "nt256 pd1 g2 sc", 14: "nt256 pd2 g2 sc", 15: "nt256 pd1 g4 sc",
+            16: "nt256 pd1 g2 dma", 17: "nt256 pd2 g2 dma", 18: "nt256 pd1 g2 sc dma"}
 
 
 def main():
@@ -40,7 +41,9 @@ def main():
     op = sb.create_bsr(full, dim, full, dim, [1, 1, 1, 1, 1, 3], [1, 1, 1, 1, 1, 3], False,
                        [torch.full((V,), 9, dtype=torch.int32, device=dev)],
                        [torch.from_numpy(jj.reshape(-1)).to(dev)], [vals])
-    for ncols in (1, 12, 64):
+    sb.tune_set("bsr.tile", 0)
+    sb.tune_set("bsr.row_max_cols", 0)
+    for ncols in [int(c) for c in os.environ.get("NCOLS", "1,12,64").split(",")]:
         dimx = [1, L, L, L, L, 1, 3, ncols]
         x = torch.randn(V * 3 * ncols, dtype=torch.complex128, device=dev)
         y = torch.empty_like(x)
