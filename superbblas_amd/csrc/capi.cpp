@@ -418,6 +418,12 @@ int sbx_tune_set(const char *key, long long value) {
         else if (k == "bsr.tile_slab") g_bsr_tune.tile_slab = (long)value;
         else if (k == "bsr.row_max_cols") g_bsr_tune.row_max_cols = (long)value;
         else if (k == "bsr.row_dma") g_bsr_tune.row_dma = (int)value;
+        else if (k == "bsr.split_max_cols") g_bsr_tune.split_max_cols = (long)value;
+        else if (k == "bsr.split_cw") g_bsr_tune.split_cw = (int)value;
+        else if (k == "bsr.split_jb") g_bsr_tune.split_jb = (int)value;
+        else if (k == "bsr.split_nt") g_bsr_tune.split_nt = (int)value;
+        else if (k == "bsr.split_ilv") g_bsr_tune.split_ilv = (int)value;
+        else if (k == "bsr.ell9_ilv") g_bsr_tune.ell9_ilv = (int)value;
         else if (k == "bsr.tile_max_cols") g_bsr_tune.tile_max_cols = (long)value;
         else if (k == "bsr.tile_rows") g_bsr_tune.tile_rows = (int)value;
         else if (k == "bsr.probe") g_bsr_tune.probe = value;
@@ -446,6 +452,13 @@ int sbx_tune_get(const char *key, long long *value) {
         else if (k == "bsr.tile_slab") *value = g_bsr_tune.tile_slab;
         else if (k == "bsr.row_max_cols") *value = g_bsr_tune.row_max_cols;
         else if (k == "bsr.row_dma") *value = g_bsr_tune.row_dma;
+        else if (k == "bsr.split_max_cols") *value = g_bsr_tune.split_max_cols;
+        else if (k == "bsr.split_cw") *value = g_bsr_tune.split_cw;
+        else if (k == "bsr.split_jb") *value = g_bsr_tune.split_jb;
+        else if (k == "bsr.split_nt") *value = g_bsr_tune.split_nt;
+        else if (k == "bsr.split_ilv") *value = g_bsr_tune.split_ilv;
+        else if (k == "bsr.last_kernel") *value = g_bsr_tune.last;
+        else if (k == "bsr.ell9_ilv") *value = g_bsr_tune.ell9_ilv;
         else if (k == "bsr.tile_max_cols") *value = g_bsr_tune.tile_max_cols;
         else if (k == "bsr.tile_rows") *value = g_bsr_tune.tile_rows;
         else if (k == "bsr.probe") *value = g_bsr_tune.probe;

@@ -34,12 +34,14 @@ struct BsrArgs {
     int block_im_fast;
     const void *x;
     long ldx;
+    long x_rows; // domain rows of x
     void *y;
     long ldy;
     long ncols;
     double alpha_re, alpha_im;
     int add;
     unsigned long long *probe; // tools only (sbx_tune_set "bsr.probe"): per-workgroup time stamps
+    int ilv = 1; // bsr_ell9_kernel: an XCD's chunks visited as ilv interleaved parts
 };
 
 // tools only: 8 stamps per workgroup -- 100 MHz real time at start and end, then shader-clock
@@ -721,7 +723,10 @@ __global__ void __launch_bounds__(NT) bsr_ell9_kernel(const BsrArgs p, int rb) {
     E *__restrict__ y = (E *)p.y;
     const int nwg = gridDim.x, bid = blockIdx.x;
     const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-    const int chunk = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    // the XCD's range of chunks visited as p.ilv interleaved parts (bsr_ell9_split_kernel)
+    const int cnt = xcd < r8 ? q8 + 1 : q8, qx = bid >> 3, npart = cnt / p.ilv;
+    const int loc = (p.ilv > 1 && qx < npart * p.ilv) ? (qx % p.ilv) * npart + qx / p.ilv : qx;
+    const int chunk = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
     const unsigned long long rt0 = p.probe ? __builtin_amdgcn_s_memrealtime() : 0;
     const unsigned long long c0 = p.probe ? __builtin_amdgcn_s_memtime() : 0;
     const long row0 = (long)chunk * rb;
@@ -850,6 +855,7 @@ void launch_ell9(const BsrArgs &a, bool yrow, bool xrow, hipStream_t s, long lds
     // the DMA form fills whole workgroup-wide rows of 16-byte lanes
     const size_t lds = (NTF & 4) != 0 ? (size_t)((rb * 9L * BI * BD + NT - 1) / NT * NT) * sizeof(E)
                                       : (size_t)rb * blk_bytes;
+    g_bsr_tune.last = 3;
     KernelTimer timer("bsr", s);
     if (yrow && xrow)
         hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, true, true, NT, NTF, SC>), dim3(blocks), dim3(NT), lds, s, a, rb);
@@ -960,6 +966,7 @@ void launch_ell9_row(const BsrArgs &a, bool yrow, bool xrow, hipStream_t s) {
     // the LDS-DMA form for 16-byte elements whose value array has 32-bit offsets
     const long v_bytes = a.block_rows * 81L * (long)sizeof(E);
     const bool dma = sizeof(E) == 16 && v_bytes < (1L << 31) && g_bsr_tune.row_dma;
+    g_bsr_tune.last = 1;
     KernelTimer timer("bsr", s);
     auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, s, a, (unsigned)v_bytes);
@@ -976,6 +983,206 @@ void launch_ell9_row(const BsrArgs &a, bool yrow, bool xrow, hipStream_t s) {
         else go(bsr_ell9_row_kernel<E, NC, false, false, false>);
     }
     SBX_HIP_CHECK(hipGetLastError());
+}
+
+// Rows split over their nonzero blocks, 3x3 complex<double> blocks, 9 per row, row-major x, from
+// 4 rhs columns on: one thread per (block row, group of JB nonzero blocks, rhs lane g), the lane
+// computing columns g, g + nct, ... (CW of them; nct = ceil(ncols / CW) lanes per block group).
+//  * Every thread issues the x rows of its JB blocks at once (JB x 3 x CW independent 16-byte
+//    loads, no chain of dependent gathers), the nct lanes of a block group read whole runs of a
+//    domain row (12 columns: 192 B pieces; the row-chunk kernel's lanes read 96 B pieces, which
+//    the vector-memory pipeline serves ~1.4x slower from the Infinity Cache,
+//    tools/gather_shape.hip), through 32-bit buffer offsets (one multiply per block instead of
+//    six 64-bit address computations).
+//  * The workgroup's block values (one contiguous run) are staged by LDS-DMA and read from LDS,
+//    broadcast across the lanes of a block group.
+//  * The 9 / JB partial products of a row are summed through LDS in block order.
+__device__ __forceinline__ unsigned fdiv(unsigned n, unsigned m, int s) {
+    return (unsigned)(((unsigned long long)__umulhi(n, m) + n) >> s);
+}
+
+static void magic(unsigned d, unsigned &m, int &s) {
+    s = 0;
+    while ((1ull << s) < d) ++s;
+    m = (unsigned)((((1ull << 32) * ((1ull << s) - d)) / d) + 1);
+}
+
+struct SplitArgs {
+    int nct, tpr, rw; // lanes per block group, threads per row, rows per workgroup
+    unsigned v_bytes, x_bytes;
+    unsigned tpr_m, nct_m; // magic multipliers and shifts of tpr and nct (fdiv)
+    int tpr_s, nct_s;
+    int ilv; // an XCD's chunks visited as ilv interleaved parts (x rows reused across parts)
+};
+
+template <int CW, int JB, bool YROW>
+__global__ void __launch_bounds__(512) bsr_ell9_split_kernel(const BsrArgs p, const SplitArgs s) {
+    constexpr int NNZ = 9, NG = NNZ / JB;
+    static_assert(NNZ % JB == 0, "JB divides 9");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    double2 *vals = (double2 *)smem;
+    const int nth = blockDim.x, tid = threadIdx.x;
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    // the XCD's contiguous range of chunks, its parts interleaved: with ilv = 2 the two halves
+    // (on the 16^4 lattice: the XCD's two x slices) are visited together, so a site's +-x
+    // neighbour rows are read while the other half still holds them in this XCD's L2
+    const int cnt = xcd < r8 ? q8 + 1 : q8, q = bid >> 3, npart = cnt / s.ilv;
+    const int loc = (s.ilv > 1 && q < npart * s.ilv) ? (q % s.ilv) * npart + q / s.ilv : q;
+    const long chunk = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+    const long row0 = chunk * s.rw;
+    const int nrows = (int)min((long)s.rw, p.block_rows - row0);
+    const int nv = nrows * NNZ * 9, nvp = (s.rw * NNZ * 9 + nth - 1) / nth * nth;
+    double2 *part = vals + nvp;
+    const int rl = (int)fdiv(tid, s.tpr_m, s.tpr_s), rem = tid - rl * s.tpr;
+    const int jg = (int)fdiv(rem, s.nct_m, s.nct_s), g = rem - jg * s.nct;
+    const bool active = rl < nrows;
+    const int ncs = s.nct * CW; // padded columns of a partial-product row
+    // 1) the x rows of the thread's JB blocks
+    const __amdgpu_buffer_rsrc_t rx =
+        __builtin_amdgcn_make_buffer_rsrc((void *)p.x, (short)0, (int)s.x_bytes, 0x00020000);
+    const unsigned rowb = (unsigned)p.ldx * 16u;
+    int dj[JB];
+    double2 xv[JB][3][CW];
+#pragma unroll
+    for (int b = 0; b < JB; ++b) dj[b] = active ? p.jj[(row0 + rl) * NNZ + jg * JB + b] : -1;
+    // the lane's columns, clamped to the last one (the surplus lanes' results are not stored)
+    unsigned colb[CW];
+#pragma unroll
+    for (int k = 0; k < CW; ++k) colb[k] = (unsigned)min(g + k * s.nct, (int)p.ncols - 1) * 16u;
+#pragma unroll
+    for (int b = 0; b < JB; ++b) {
+        // skipped blocks (-1) read zero beyond the buffer range; the block's 3 domain rows by the
+        // uniform offset e * rowb
+        const unsigned vb = dj[b] < 0 ? 0x80000000u : (unsigned)dj[b] * rowb;
+#pragma unroll
+        for (int e = 0; e < 3; ++e)
+#pragma unroll
+            for (int k = 0; k < CW; ++k) {
+                const auto t = __builtin_amdgcn_raw_buffer_load_b128(rx, vb + colb[k], (unsigned)e * rowb, 0);
+                xv[b][e][k] = __builtin_bit_cast(double2, t);
+            }
+    }
+    // 2) the workgroup's block values, lane-linear into LDS
+    {
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc((void *)p.v, (short)0, (int)s.v_bytes, 0x00020000);
+        const unsigned base = lds_u32(vals) + (unsigned)__builtin_amdgcn_readfirstlane(tid >> 6) * 1024u;
+        const unsigned v0 = (unsigned)(row0 * NNZ * 9) * 16u;
+        for (int u = 0; u * nth < nv; ++u) {
+            const int e = u * nth + tid;
+            const unsigned off = e < nv ? v0 + (unsigned)e * 16u : 0x80000000u;
+            dma16(rs, off, __builtin_amdgcn_readfirstlane(base + (unsigned)(u * nth) * 16u));
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    // 3) the partial products of the thread's blocks
+    double2 acc[3][CW];
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int k = 0; k < CW; ++k) acc[c][k] = double2{0, 0};
+    if (active) {
+#pragma unroll
+        for (int b = 0; b < JB; ++b) {
+            if (dj[b] < 0) continue;
+            const double2 *vb = vals + (rl * NNZ + jg * JB + b) * 9;
+#pragma unroll
+            for (int e = 0; e < 3; ++e)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    const double2 a = p.block_im_fast ? vb[c + e * 3] : vb[c * 3 + e];
+#pragma unroll
+                    for (int k = 0; k < CW; ++k) acc[c][k] = Ops<double2>::fma(a, xv[b][e][k], acc[c][k]);
+                }
+        }
+    }
+    auto store = [&](long img, int col, double2 v) {
+        double2 *yp = YROW ? (double2 *)p.y + img * p.ldy + col : (double2 *)p.y + img + (long)col * p.ldy;
+        const double2 out = Ops<double2>::scale(v, p.alpha_re, p.alpha_im);
+        *yp = p.add ? Ops<double2>::add(*yp, out) : out;
+    };
+    if constexpr (NG == 1) {
+        if (!active) return;
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+#pragma unroll
+            for (int k = 0; k < CW; ++k) {
+                const int col = g + k * s.nct;
+                if (col < p.ncols) store((row0 + rl) * 3 + c, col, acc[c][k]);
+            }
+    } else {
+        if (active) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+#pragma unroll
+                for (int k = 0; k < CW; ++k) part[((rl * NG + jg) * 3 + c) * ncs + g + k * s.nct] = acc[c][k];
+        }
+        __syncthreads();
+        // 4) sums in block order: the lanes of block group c < 3 sum image component c
+        if (!active || jg >= 3) return;
+#pragma unroll
+        for (int k = 0; k < CW; ++k) {
+            const int col = g + k * s.nct;
+            if (col >= p.ncols) break;
+            const double2 *pp = part + ((rl * NG) * 3 + jg) * ncs + col;
+            double2 sum = pp[0];
+#pragma unroll
+            for (int q = 1; q < NG; ++q) sum = Ops<double2>::add(sum, pp[q * 3 * ncs]);
+            store((row0 + rl) * 3 + jg, col, sum);
+        }
+    }
+}
+
+/// false: not this shape (the caller falls back to the row-chunk kernel)
+template <typename E>
+bool launch_ell9_split(const BsrArgs &a, bool yrow, bool xrow, hipStream_t st) {
+    if constexpr (!std::is_same<E, double2>::value) {
+        return false;
+    } else {
+        if (!xrow || a.ncols < 1) return false;
+        const long x_bytes = a.x_rows * a.ldx * 16L;
+        const long v_bytes = a.block_rows * 81L * 16L;
+        if (v_bytes >= (1L << 31) || a.block_rows * 36L >= (1L << 31)) return false;
+        if (a.x_rows <= 0 || x_bytes >= (1L << 31)) return false;
+        // defaults from tools/bsr_split_sweep.py (16^4, profiles/r02_bsr_split_sweep.txt)
+        int cw = g_bsr_tune.split_cw;
+        if (cw <= 0) cw = a.ncols <= 4 ? 1 : 2;
+        int jb = g_bsr_tune.split_jb;
+        if (jb <= 0) jb = a.ncols <= 24 ? 3 : 9;
+        if ((cw != 1 && cw != 2 && cw != 4) || (jb != 1 && jb != 3 && jb != 9)) return false;
+        const int nct = (int)((a.ncols + cw - 1) / cw), tpr = 9 / jb * nct;
+        const int ntmax = g_bsr_tune.split_nt > 0 ? g_bsr_tune.split_nt : 256;
+        if (tpr > ntmax) return false;
+        // rows per workgroup: by the thread budget and at most 40 KB of LDS
+        const long row_lds = 81L * 16 + (jb == 9 ? 0L : (long)(9 / jb) * 3 * nct * cw * 16);
+        int rw = std::max(1, std::min<int>(ntmax / tpr, (int)(40960 / row_lds)));
+        const int nth = (rw * tpr + 63) / 64 * 64;
+        const long nvp = (rw * 81L + nth - 1) / nth * nth;
+        const long lds = (nvp + (jb == 9 ? 0L : (long)rw * (9 / jb) * 3 * nct * cw)) * 16L;
+        if (lds > 65536) return false;
+        SplitArgs sa{nct, tpr, rw, (unsigned)v_bytes, (unsigned)x_bytes, 0, 0, 0, 0,
+                     std::max(1, g_bsr_tune.split_ilv)};
+        magic((unsigned)tpr, sa.tpr_m, sa.tpr_s);
+        magic((unsigned)nct, sa.nct_m, sa.nct_s);
+        const long nchunks = (a.block_rows + rw - 1) / rw;
+        if (nchunks >= (1L << 31)) return false;
+        g_bsr_tune.last = 2;
+        KernelTimer timer("bsr", st);
+        auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(nchunks), dim3(nth), (size_t)lds, st, a, sa); };
+#define SBX_SPLIT(CW_, JB_)                                                                        \
+    if (cw == CW_ && jb == JB_) {                                                                  \
+        if (yrow) go(bsr_ell9_split_kernel<CW_, JB_, true>);                                       \
+        else go(bsr_ell9_split_kernel<CW_, JB_, false>);                                           \
+    }
+        SBX_SPLIT(1, 1) SBX_SPLIT(1, 3) SBX_SPLIT(1, 9)
+        SBX_SPLIT(2, 1) SBX_SPLIT(2, 3) SBX_SPLIT(2, 9)
+        SBX_SPLIT(4, 1) SBX_SPLIT(4, 3) SBX_SPLIT(4, 9)
+#undef SBX_SPLIT
+        SBX_HIP_CHECK(hipGetLastError());
+        return true;
+    }
 }
 
 template <typename E, int BI, int BD>
@@ -995,6 +1202,9 @@ void launch_ell(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_t s) 
             if (a.ncols == 2) return launch_ell9_row<E, 2>(a, yrow, xrow, s);
             if (a.ncols <= 4) return launch_ell9_row<E, 4>(a, yrow, xrow, s);
         }
+        if (nnz == 9 && g_bsr_tune.variant != 1 && a.ncols > g_bsr_tune.row_max_cols &&
+            a.ncols <= g_bsr_tune.split_max_cols && launch_ell9_split<E>(a, yrow, xrow, s))
+            return;
     }
     if (nnz == 9 && g_bsr_tune.variant != 1) {
         const long lds = g_bsr_tune.ell9_lds > 0 ? g_bsr_tune.ell9_lds : a.ncols >= 8 ? 12288 : 24576;
@@ -1053,16 +1263,6 @@ struct TileArgs {
     unsigned div81_m, rowlen_m, nc_m; // magic multipliers (n / d = (umulhi(n, m) + n) >> s)
     int rowlen_s, nc_s;
 };
-
-__device__ __forceinline__ unsigned fdiv(unsigned n, unsigned m, int s) {
-    return (unsigned)(((unsigned long long)__umulhi(n, m) + n) >> s);
-}
-
-static void magic(unsigned d, unsigned &m, int &s) {
-    s = 0;
-    while ((1ull << s) < d) ++s;
-    m = (unsigned)((((1ull << 32) * ((1ull << s) - d)) / d) + 1);
-}
 
 template <int ND, bool YROW, bool XROW>
 __global__ void __launch_bounds__(512) bsr_tile_kernel(const BsrArgs p, const TileArgs t) {
@@ -1209,6 +1409,7 @@ bool launch_tile(const BsrArgs &a, TileArgs t, long nchunks, long x_rows, bool y
     if ((long)lds > TILE_LDS_MAX) return false;
     t.v_bytes = (unsigned)v_bytes;
     t.x_bytes = (unsigned)x_bytes;
+    g_bsr_tune.last = 4;
     KernelTimer timer("bsr", s);
     for (long c0 = 0; c0 < a.ncols; c0 += ncs) {
         t.c0 = (int)c0;
@@ -1311,6 +1512,7 @@ void launch_gather_blocks(int t, const void *src, const int *perm, long nblocks,
 
 void launch_bsr(const BsrDesc &d, int device) {
     if (d.block_rows == 0 || d.ncols == 0) return;
+    g_bsr_tune.last = 0;
     set_device(device);
     hipStream_t s = get_stream(device);
     BsrArgs a{};
@@ -1323,6 +1525,7 @@ void launch_bsr(const BsrDesc &d, int device) {
     a.block_im_fast = d.block_im_fast ? 1 : 0;
     a.x = d.x;
     a.ldx = d.ldx;
+    a.x_rows = d.x_rows;
     a.y = d.y;
     a.ldy = d.ldy;
     a.ncols = d.ncols;
@@ -1330,6 +1533,7 @@ void launch_bsr(const BsrDesc &d, int device) {
     a.alpha_im = d.alpha.im;
     a.add = d.add ? 1 : 0;
     a.probe = (unsigned long long *)g_bsr_tune.probe;
+    a.ilv = std::max(1, g_bsr_tune.ell9_ilv);
     // column passes (experiment, sbx_tune_set "bsr.colsplit"): with row-major x and y a launch
     // over a column slice is the same product on shifted base pointers; fewer columns per pass
     // shrink the x rows that must stay in L2 between a site's neighbours

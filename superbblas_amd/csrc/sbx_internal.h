@@ -237,7 +237,17 @@ struct BsrTune {
     int tile_rows = 16;     ///< ... block rows per tile (the plan, built by create_bsr)
     long row_max_cols = 3;  ///< 9-point 3x3 operators: one thread per nonzero block up to this many rhs columns (0 = off)
     int row_dma = 1;        ///< ... values staged by LDS-DMA (16-byte elements)
+    long split_max_cols = 32; ///< 9-point 3x3 complex<double> operators, row-major x: rows split over their
+                              ///< nonzero blocks (bsr_ell9_split_kernel) from row_max_cols + 1 to this many
+                              ///< rhs columns (0 = off)
+    int split_cw = 0;  ///< ... rhs columns per thread (1, 2, 4; 0 = by the column count)
+    int split_jb = 0;  ///< ... nonzero blocks per thread (1, 3, 9; 0 = default)
+    int split_nt = 0;  ///< ... threads per workgroup to aim at (0 = 256)
+    int split_ilv = 2; ///< ... an XCD's rows visited as this many interleaved parts
+    int ell9_ilv = 2;  ///< the same for the row-chunk 9-point kernel (bsr_ell9_kernel)
     long long probe = 0;    ///< tools only: device buffer for per-workgroup time stamps
+    int last = 0; ///< read-back ("bsr.last_kernel"): the 9-point 3x3 form of the last launch -- 1 one thread
+                  ///< per block, 2 split rows, 3 row chunks, 4 lattice tiles, 0 another kernel
 };
 extern BsrTune g_bsr_tune;
 
