@@ -215,6 +215,21 @@ __global__ void __launch_bounds__(256) bsr_ell_kernel(const BsrArgs p, int nnz, 
 // global memory: lane l reads A_ij[l&15][k+(l>>4)] and x[d_j+k+(l>>4)][col0+(l&15)]
 // (contiguous along the rhs for row-major x); out-of-range rows, columns and skipped blocks
 // (-1 columns) are clamped loads replaced by zero, so the loop has no divergent branches.
+__device__ __forceinline__ unsigned lds_u32(const void *p) {
+    return (unsigned)(size_t)(const __attribute__((address_space(3))) void *)p;
+}
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, unsigned off, unsigned dst) {
+    // inline asm: hipcc does not order its ds_reads against an LDS-DMA it cannot see; the kernel
+    // retires the DMA with an explicit vmcnt(0) before its barrier
+    asm volatile("s_mov_b32 m0, %1\n\t"
+                 "s_nop 0\n\t"
+                 "buffer_load_dwordx4 %0, %2, 0 offen lds"
+                 :
+                 : "v"(off), "s"(dst), "s"(rs)
+                 : "memory", "m0");
+}
+
 template <typename R, bool CPLX> struct BsrMfmaElem;
 template <> struct BsrMfmaElem<double, true> { typedef double2 type; };
 template <> struct BsrMfmaElem<double, false> { typedef double type; };
@@ -634,6 +649,132 @@ void launch_bsr_mfma_pf(const BsrArgs &a, bool yrow, bool xrow, hipStream_t s) {
     SBX_HIP_CHECK(hipGetLastError());
 }
 
+// bsr_mfma_blk_kernel with the blocks staged by LDS-DMA (buffer_load_dwordx4 ... lds): the value
+// block A_ij and the x block of its domain rows go straight from memory into the wave's LDS slot
+// (no VGPR round trip), PD blocks ahead in a ring of PD + 1 slots; the MFMA fragments are read
+// from the slot as in the register-staged kernel.  Both blocks are contiguous runs (row-major x,
+// ldx == ncols <= 16), lane-linear in LDS.
+template <typename R, bool CPLX, int BI, int BD, bool YROW, int NNZ, int PD, bool M3>
+__global__ void __launch_bounds__(256) bsr_mfma_dma_kernel(const BsrArgs p, unsigned v_bytes, unsigned x_bytes) {
+    typedef typename BsrMfmaElem<R, CPLX>::type E;
+    typedef typename BsrMfma<R>::acc_t acc_t;
+    static_assert(BI <= 16 && BD % 4 == 0, "block shape");
+    constexpr int KS = BD / 4, ES = (int)sizeof(E);
+    constexpr int ABLK = BI * BD, XBLK = BD * 16;        // elements (x: up to 16 cols)
+    constexpr int NA = (ABLK * ES + 1023) / 1024, NX = (XBLK * ES + 1023) / 1024; // DMA instructions
+    constexpr int SLOT = (NA + NX) * 1024;               // bytes per ring slot
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    E *__restrict__ y = (E *)p.y;
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const long i = (long)blockIdx.x * 4 + w;
+    if (i >= p.block_rows) return;
+    const int nc = (int)p.ncols, xblk = BD * nc;
+    const long jb = i * NNZ;
+    int dj[NNZ];
+#pragma unroll
+    for (int k = 0; k < NNZ; ++k) dj[k] = p.jj[jb + k];
+    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void *)p.v, (short)0, (int)v_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)p.x, (short)0, (int)x_bytes, 0x00020000);
+    const unsigned slot0 = lds_u32(smem) + (unsigned)w * (unsigned)(SLOT * (PD + 1));
+    auto issue = [&](int k) {
+        const unsigned base = slot0 + (unsigned)((k % (PD + 1)) * SLOT);
+        const unsigned av = (unsigned)((jb + k) * ABLK) * ES, xv = (unsigned)((long)(dj[k] < 0 ? 0 : dj[k]) * nc) * ES;
+#pragma unroll
+        for (int q = 0; q < NA; ++q) {
+            const unsigned g = (unsigned)(lane + 64 * q) * 16u;
+            dma16(rv, g < (unsigned)(ABLK * ES) ? av + g : 0x80000000u, base + (unsigned)q * 1024u);
+        }
+#pragma unroll
+        for (int q = 0; q < NX; ++q) {
+            const unsigned g = (unsigned)(lane + 64 * q) * 16u;
+            dma16(rx, g < (unsigned)(xblk * ES) ? xv + g : 0x80000000u, base + (unsigned)(NA + q) * 1024u);
+        }
+    };
+    const int ar = lane & 15, kq = lane >> 4;
+    const bool arow_ok = ar < BI, bcol_ok = ar < nc;
+    acc_t accR = acc_t{0, 0, 0, 0}, accI = acc_t{0, 0, 0, 0}, acc3 = acc_t{0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < PD && k < NNZ; ++k) issue(k);
+#pragma unroll
+    for (int k = 0; k < NNZ; ++k) {
+        // the slot of block k + PD was last read in iteration k - 1: its reads have returned
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (k + PD < NNZ) {
+            issue(k + PD);
+            // block k landed: at most the NA + NX instructions of each later block in flight
+            if constexpr (PD == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NA + NX) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (NA + NX)) : "memory");
+        } else if (k + PD == NNZ) {
+            // no block issued this iteration: PD - 1 blocks may stay in flight
+            if constexpr (PD == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NA + NX) : "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        if (dj[k] < 0) continue;
+        const E *sa = (const E *)(smem + (slot0 - lds_u32(smem)) + (k % (PD + 1)) * SLOT);
+        const E *sx = sa + NA * 1024 / ES;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const int e = ks * 4 + kq;
+            E a = arow_ok ? (p.block_im_fast ? sa[ar + e * BI] : sa[ar * BD + e]) : E{};
+            E b = bcol_ok ? sx[e * nc + ar] : E{};
+            if constexpr (CPLX && M3) {
+                accR = BsrMfma<R>::mma(a.x, b.x, accR);
+                accI = BsrMfma<R>::mma(a.y, b.y, accI);
+                acc3 = BsrMfma<R>::mma(a.x + a.y, b.x + b.y, acc3);
+            } else if constexpr (CPLX) {
+                accR = BsrMfma<R>::mma(a.x, b.x, accR);
+                accI = BsrMfma<R>::mma(a.x, b.y, accI);
+                accR = BsrMfma<R>::mma(-a.y, b.y, accR);
+                accI = BsrMfma<R>::mma(a.y, b.x, accI);
+            } else {
+                accR = BsrMfma<R>::mma(a, b, accR);
+            }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int row = BsrMfma<R>::row(lane, q);
+        if (row >= BI || !bcol_ok) continue;
+        const long img = i * BI + row;
+        E *yp = YROW ? y + img * p.ldy + ar : y + img + ar * p.ldy;
+        E out;
+        if constexpr (CPLX && M3)
+            out = Ops<E>::scale(E{accR[q] - accI[q], acc3[q] - accR[q] - accI[q]}, p.alpha_re,
+                                p.alpha_im);
+        else if constexpr (CPLX)
+            out = Ops<E>::scale(E{accR[q], accI[q]}, p.alpha_re, p.alpha_im);
+        else
+            out = Ops<E>::scale(accR[q], p.alpha_re, p.alpha_im);
+        *yp = p.add ? Ops<E>::add(*yp, out) : out;
+    }
+}
+
+/// false: not this shape (the register-staged kernel runs)
+template <typename R, bool CPLX, int BI, int BD, int NNZ, int PD>
+bool launch_bsr_mfma_dma(const BsrArgs &a, bool yrow, hipStream_t s) {
+    typedef typename BsrMfmaElem<R, CPLX>::type E;
+    constexpr int ES = (int)sizeof(E);
+    constexpr int NA = (BI * BD * ES + 1023) / 1024, NX = (BD * 16 * ES + 1023) / 1024;
+    const long v_bytes = a.block_rows * NNZ * (long)BI * BD * ES, x_bytes = a.x_rows * a.ldx * (long)ES;
+    if (v_bytes >= (1L << 31) || a.x_rows <= 0 || x_bytes >= (1L << 31)) return false;
+    const long blocks = (a.block_rows + 3) / 4;
+    if (blocks >= (1L << 31)) return false;
+    const size_t lds = (size_t)4 * (NA + NX) * 1024 * (PD + 1);
+    KernelTimer timer("bsr", s);
+    const bool m3 = CPLX && g_gemm_tune.m3 > 0;
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), lds, s, a, (unsigned)v_bytes, (unsigned)x_bytes);
+    };
+    if (yrow && m3) go(bsr_mfma_dma_kernel<R, CPLX, BI, BD, true, NNZ, PD, true>);
+    else if (yrow) go(bsr_mfma_dma_kernel<R, CPLX, BI, BD, true, NNZ, PD, false>);
+    else if (m3) go(bsr_mfma_dma_kernel<R, CPLX, BI, BD, false, NNZ, PD, true>);
+    else go(bsr_mfma_dma_kernel<R, CPLX, BI, BD, false, NNZ, PD, false>);
+    SBX_HIP_CHECK(hipGetLastError());
+    return true;
+}
+
 template <typename R, bool CPLX, int BI, int BD, int ROWS>
 void launch_bsr_mfma(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_t s) {
     // the 9-point stencils: columns preloaded, one block ahead (16^4 complex<double> n = 12:
@@ -644,8 +785,15 @@ void launch_bsr_mfma(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_
     // through LDS (16^4 complex<double> n = 12: 372 -> 348-355 us; the chain's complex<float>
     // operator 843-922 -> 722 us; two or three blocks of lookahead: 359-377 / 739-772 us)
     if (g_bsr_tune.variant != 1 && g_bsr_tune.variant != 2 && nnz == 9 && xrow &&
-        a.ldx == a.ncols && a.ncols <= 16)
+        a.ldx == a.ncols && a.ncols <= 16) {
+        // LDS-DMA staging (tools/bsr_blk_sweep.py, profiles/r02_bsr_blk_sweep.txt): one block
+        // ahead for 8-byte reals (16^4 complex<double> n = 12: 424 -> 407 us), two for 4-byte
+        // ones (the chain's 16^3 x 64 complex<float> operator: 965 -> 794 us)
+        const int pd = g_bsr_tune.blk_dma >= 0 ? g_bsr_tune.blk_dma : sizeof(R) == 4 ? 2 : 1;
+        if (pd == 1 && launch_bsr_mfma_dma<R, CPLX, BI, BD, 9, 1>(a, yrow, s)) return;
+        if (pd == 2 && launch_bsr_mfma_dma<R, CPLX, BI, BD, 9, 2>(a, yrow, s)) return;
         return launch_bsr_mfma_blk<R, CPLX, BI, BD, 9, 1>(a, yrow, s);
+    }
     if (g_bsr_tune.variant != 1 && nnz == 9) return launch_bsr_mfma_ell<R, CPLX, BI, BD, 9, 1>(a, yrow, xrow, s);
     if (g_bsr_tune.variant != 1) return launch_bsr_mfma_pf<R, CPLX, BI, BD>(a, yrow, xrow, s);
     const long ntn = (a.ncols + 15) / 16;
@@ -686,20 +834,6 @@ void launch_ell_g(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_t s
     SBX_HIP_CHECK(hipGetLastError());
 }
 
-__device__ __forceinline__ unsigned lds_u32(const void *p) {
-    return (unsigned)(size_t)(const __attribute__((address_space(3))) void *)p;
-}
-
-__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, unsigned off, unsigned dst) {
-    // inline asm: hipcc does not order its ds_reads against an LDS-DMA it cannot see; the kernel
-    // retires the DMA with an explicit vmcnt(0) before its barrier
-    asm volatile("s_mov_b32 m0, %1\n\t"
-                 "s_nop 0\n\t"
-                 "buffer_load_dwordx4 %0, %2, 0 offen lds"
-                 :
-                 : "v"(off), "s"(dst), "s"(rs)
-                 : "memory", "m0");
-}
 
 // 9-point ELL form of bsr_ell_kernel: each thread reads its block row's 9 block columns straight
 // from global memory into registers and issues the x rows of its first PD blocks before the

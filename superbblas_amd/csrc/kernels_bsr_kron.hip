@@ -15,6 +15,7 @@
 #include "sbx_internal.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace sbx {
 namespace {
@@ -256,11 +257,144 @@ __global__ void __launch_bounds__(256) bsr_kron_generic_kernel(const KronArgs p)
     }
 }
 
+// complex<double>, 3x3 color blocks, 4x4 spin matrices, from 8 rhs columns: one wave per (block
+// row, group of 16 rhs columns), lane l = 16 b + q owning spin b of column q of the group.
+//  * color on the VALU: T_mu(i, b, q) = sum_d U_mu(i, d) x(J_mu, d, q, b) -- the row's color
+//    blocks and block columns are wave-uniform (scalar loads, SGPR operands), the x loads of a
+//    neighbour are lane-linear 16-byte pieces (1 KB per wave instruction at 16 columns);
+//  * spin on the matrix cores: acc(a, i, q) += sum_b K_mu(a, b) T_mu(i, b, q) is a 4x4x4 product
+//    per group of 4 columns, i.e. v_mfma_f64_4x4x4_4b_f64 with A = K_mu (lane 16 b + 4 g + a, the
+//    same in all 4 blocks), B = T (lane 16 b + q) and C = acc (lane 16 a + q) -- the lane maps
+//    measured by tools/mfma_small.hip -- 4 real products per complex one (the BLAS rounding);
+//  * the next neighbour's x is loaded while the current one is applied; 4 rows per workgroup,
+//    an XCD's rows visited as two interleaved halves (its ilv form of the 3x3 kernels).
+// The previous kernel (one thread per (row, column) owning all 12 outputs) ran at 256 VGPRs:
+// 2 waves per SIMD.
+template <int NNZ>
+__global__ void __launch_bounds__(256) bsr_kron_mfma_kernel(const KronArgs p, int ngroups) {
+    typedef double2 E;
+    const E *__restrict__ x = (const E *)p.x;
+    E *__restrict__ y = (E *)p.y;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // XCD-contiguous chunks of 4 block rows, the XCD's range visited as two interleaved halves
+    const long nchunk = (p.block_rows + 3) / 4;
+    const int bid = blockIdx.x, nwg = gridDim.x;
+    const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int cnt = xcd < r8 ? q8 + 1 : q8, qx = bid >> 3, npart = cnt / 2;
+    const int loc = (npart > 0 && qx < npart * 2) ? (qx % 2) * npart + qx / 2 : qx;
+    const long wgi = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+    const long task = wgi * 4 + w; // (row chunk, column group) tasks: row-major over groups
+    const long r = task / ngroups;
+    const int cg = (int)(task - r * ngroups);
+    // the color blocks of the workgroup's rows (rows of a task group are consecutive: one
+    // contiguous run) into LDS by one DMA pass, read back as broadcasts
+    __shared__ __attribute__((aligned(16))) E us[4 * NNZ * 9];
+    {
+        const long rlo = (wgi * 4) / ngroups, rhi = min((wgi * 4 + 3) / ngroups, p.block_rows - 1);
+        const int nu = (int)(rhi - rlo + 1) * NNZ * 9;
+        // (launcher: the value array is below 2 GiB)
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)p.v, (short)0, (int)(p.block_rows * NNZ * 9 * 16), 0x00020000);
+        const unsigned base = (unsigned)(size_t)(const __attribute__((address_space(3))) void *)us +
+                              (unsigned)w * 1024u;
+        for (int u = 0; u * 256 < nu; ++u) {
+            const int e = u * 256 + (int)threadIdx.x;
+            const unsigned off = e < nu ? (unsigned)(rlo * NNZ * 9 + e) * 16u : 0x80000000u;
+            asm volatile("s_mov_b32 m0, %1\n\t"
+                         "s_nop 0\n\t"
+                         "buffer_load_dwordx4 %0, %2, 0 offen lds"
+                         :
+                         : "v"(off), "s"(__builtin_amdgcn_readfirstlane(base + (unsigned)(u * 256) * 16u)),
+                           "s"(rs)
+                         : "memory", "m0");
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        (void)nchunk;
+    }
+    if (r >= p.block_rows) return;
+    const E *urow_s = us + (r - (wgi * 4) / ngroups) * NNZ * 9;
+    const int b = lane >> 4, q = lane & 15;
+    const long n = p.ncols;
+    const long col = (long)cg * 16 + q;
+    const bool ok = col < n;
+    const long colc = ok ? col : n - 1;
+    // spin matrices as the A operand: lane 16 k + 4 g + a holds K_mu(a, k)
+    const int ka = lane & 3, kk = lane >> 4;
+    const E *kron = (const E *)p.kron;
+    const int kidx = p.block_im_fast ? ka + kk * 4 : ka * 4 + kk;
+    // block columns and color blocks of the row: wave-uniform
+    const ConstPtr<int> jrow = (ConstPtr<int>)(p.jj + r * NNZ);
+    const long xsite = 3 * n * 4; // elements per domain site: (d, n, b)
+    auto load_x = [&](int J, E *xv) {
+        const E *xs = x + (long)J * xsite + colc * 4 + b;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) xv[d] = xs[d * n * 4];
+    };
+    double accR[3] = {0, 0, 0}, accI[3] = {0, 0, 0};
+    E xa[3], xb[3];
+    load_x(jrow[0], xa);
+#pragma unroll
+    for (int mu = 0; mu < NNZ; ++mu) {
+        if (mu + 1 < NNZ) load_x(jrow[mu + 1], xb);
+        const E K = kron[mu * 16 + kidx];
+        // color: T(i) = sum_d U(i, d) x(d)
+        E t[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            t[i] = Ops<E>::zero();
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                const long ui = mu * 9 + (p.block_im_fast ? i + d * 3 : i * 3 + d);
+                t[i] = Ops<E>::fma(urow_s[ui], xa[d], t[i]);
+            }
+        }
+        // spin: acc(a) += K(a, b) T(b) on the matrix cores, 4 real products per complex one
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            accR[i] = __builtin_amdgcn_mfma_f64_4x4x4f64(K.x, t[i].x, accR[i], 0, 0, 0);
+            accR[i] = __builtin_amdgcn_mfma_f64_4x4x4f64(-K.y, t[i].y, accR[i], 0, 0, 0);
+            accI[i] = __builtin_amdgcn_mfma_f64_4x4x4f64(K.x, t[i].y, accI[i], 0, 0, 0);
+            accI[i] = __builtin_amdgcn_mfma_f64_4x4x4f64(K.y, t[i].x, accI[i], 0, 0, 0);
+        }
+        if (mu + 1 < NNZ) {
+#pragma unroll
+            for (int d = 0; d < 3; ++d) xa[d] = xb[d];
+        }
+    }
+    if (!ok) return;
+    // C lane 16 a + q: spin a of column q
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        E *yp = y + ((r * 3 + i) * n + col) * 4 + b;
+        E o = Ops<E>::scale(E{accR[i], accI[i]}, p.alpha_re, p.alpha_im);
+        if (p.add) o = Ops<E>::add(o, *yp);
+        *yp = o;
+    }
+}
+
 constexpr long KRON_LDS_BYTES = 64 * 1024;
 
 template <typename E> void launch_kron_typed(const KronArgs &a, hipStream_t s) {
     KernelTimer timer("bsr", s);
     const long row_bytes = (long)a.nnz * (a.bi * a.bd * sizeof(E) + sizeof(int));
+    if constexpr (std::is_same<E, double2>::value) {
+        if (g_bsr_tune.kron_mfma && a.bi == 3 && a.bd == 3 && a.ki == 4 && a.kd == 4 && a.nnz == 9 &&
+            a.ncols >= g_bsr_tune.kron_mfma_min_cols && a.block_rows * 81L * 16 < (1L << 31)) {
+            const long ngroups = (a.ncols + 15) / 16;
+            const long tasks = a.block_rows * ngroups, blocks = (tasks + 3) / 4;
+            if (blocks < (1L << 31)) {
+                g_bsr_tune.last = 5;
+                // tools: dynamic LDS that caps the resident workgroups per CU (L2 footprint)
+                const size_t pad = (size_t)std::max(0L, g_bsr_tune.kron_lds_pad);
+                hipLaunchKernelGGL((bsr_kron_mfma_kernel<9>), dim3((unsigned)blocks), dim3(256), pad, s,
+                                   a, (int)ngroups);
+                SBX_HIP_CHECK(hipGetLastError());
+                return;
+            }
+        }
+    }
     if (a.bi == 3 && a.bd == 3 && a.ki == 4 && a.kd == 4 && a.nnz == 9 && a.ncols >= 4 &&
         row_bytes * (256 / std::min<long>(a.ncols, 256)) <= KRON_LDS_BYTES) {
         const int cpg = (int)std::min<long>(a.ncols, 256);
@@ -287,6 +421,7 @@ void launch_bsr_kron(const BsrDesc &d, int device) {
     if (d.num_nnz_per_row <= 0 || !d.kron || !d.x_row_major || !d.y_row_major)
         throw Error("kron bsr: internal error (layout or pattern)");
     set_device(device);
+    g_bsr_tune.last = 0;
     hipStream_t s = get_stream(device);
     KronArgs a{};
     a.block_rows = d.block_rows;

@@ -246,8 +246,14 @@ struct BsrTune {
     int split_ilv = 2; ///< ... an XCD's rows visited as this many interleaved parts
     int ell9_ilv = 2;  ///< the same for the row-chunk 9-point kernel (bsr_ell9_kernel)
     long long probe = 0;    ///< tools only: device buffer for per-workgroup time stamps
+    int blk_dma = -1; ///< 12x12 (block-staged) operators: blocks staged by LDS-DMA, 1 or 2 blocks ahead
+                      ///< (0 = registers, -1 = by the real type: 1 for double, 2 for float)
+    int kron_mfma = 1;          ///< Kronecker 3x3 (color) x 4x4 (spin) complex<double>: spin products on the
+                                ///< matrix cores (bsr_kron_mfma_kernel) ...
+    long kron_mfma_min_cols = 8; ///< ... from this many rhs columns
+    long kron_lds_pad = 0;       ///< tools: LDS bytes per workgroup of that kernel (caps its residency)
     int last = 0; ///< read-back ("bsr.last_kernel"): the 9-point 3x3 form of the last launch -- 1 one thread
-                  ///< per block, 2 split rows, 3 row chunks, 4 lattice tiles, 0 another kernel
+                  ///< per block, 2 split rows, 3 row chunks, 4 lattice tiles, 5 Kronecker on MFMA, 0 another kernel
 };
 extern BsrTune g_bsr_tune;
 

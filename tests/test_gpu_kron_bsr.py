@@ -164,3 +164,46 @@ def test_kron_errors(gpu):
         sb.create_kron_bsr(full, dim, full, dim, blk, blk, [1, 1, 1, 1, spin, color],
                            [1, 1, 1, 1, spin, color], False, [t(ii)], [t(jj)], [t(vals)],
                            [t(kron)])
+
+
+@pytest.mark.parametrize("ncols", [8, 12, 16, 17, 40])
+@pytest.mark.parametrize("bif,sparse", [(False, False), (True, True)])
+def test_kron_mfma_kernel(gpu, ncols, bif, sparse):
+    """complex<double> 3x3 x 4x4 from 8 rhs columns: the spin products on the matrix cores
+    (bsr_kron_mfma_kernel; 16-column groups, partial last group), complex alpha, beta, powers;
+    integer data, exact; and the same results with the kernel switched off."""
+    import torch
+    import superbblas_amd as sb
+    L, spin, color, power = 4, 4, 3, 2
+    ii, jj, vals, kron = kron_lattice(L, spin, color, sparse_kron=sparse)
+    V = L ** 4
+    n = V * color * ncols * spin
+    g = np.arange(n)
+    x = ((g % 5 - 2) + 1j * (g % 3 - 1)).astype(np.complex128)
+    y0 = ((np.arange(n * power) % 7 - 3) + 1j).astype(np.complex128)
+    alpha, beta = 1 - 1j, 2.0
+    ref = reference(L, spin, color, ncols, vals, kron, jj, x, alpha, beta, y0, power, bif)
+    dim = [L, L, L, L, spin, color]
+    full = [([0] * 6, dim)]
+    blk, kr = [1, 1, 1, 1, 1, color], [1, 1, 1, 1, spin, 1]
+    op = sb.create_kron_bsr(full, dim, full, dim, blk, blk, kr, kr, bif,
+                            [torch.from_numpy(ii).to(gpu)], [torch.from_numpy(jj).to(gpu)],
+                            [torch.from_numpy(vals).to(gpu)], [torch.from_numpy(kron).to(gpu)])
+    dimx = [1, L, L, L, L, color, ncols, spin]
+    dimy = [power] + dimx[1:]
+    outs = []
+    try:
+        for on in (1, 0):
+            sb.tune_set("bsr.kron_mfma", on)
+            ty = torch.from_numpy(y0.copy()).to(gpu)
+            sb.bsr_krylov(alpha, op, "xyztsc", "XYZTSC", [([0] * 8, dimx)], "pXYZTCnS", [0] * 8,
+                          dimx, dimx, [torch.from_numpy(x).to(gpu)], beta, [([0] * 8, dimy)],
+                          "pxyztcns", [0] * 8, dimy, dimy, "p", [ty])
+            torch.cuda.synchronize()
+            outs.append((sb.tune_get("bsr.last_kernel"), ty.cpu().numpy()))
+    finally:
+        sb.tune_set("bsr.kron_mfma", 1)
+        op.destroy()
+    assert outs[0][0] == 5 and outs[1][0] != 5
+    assert np.array_equal(outs[0][1], ref)
+    assert np.array_equal(outs[1][1], ref)

@@ -1,0 +1,74 @@
+#!/usr/bin/env python3
+"""12x12 (spin x color) 9-point BSR: the block-staged MFMA kernel with register staging
+(bsr.blk_dma 0) against LDS-DMA staging one or two blocks ahead (1 / 2); 16^4 complex<double>
+and the chain's 16^3 x 64 complex<float> operator, n = 12, x / y row major.  Outputs must be
+bit-identical (same products, same order).  One JSON line per case (not part of the product)."""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import superbblas_amd as sb  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda:0")
+    for dims, dt in (((16, 16, 16, 16), torch.complex128), ((16, 16, 16, 64), torch.complex64)):
+        V = int(np.prod(dims))
+        sites = np.array(np.unravel_index(np.arange(V), dims)).T
+        jj = np.zeros((V, 9, 6), np.int32)
+        jj[:, 0, :4] = sites
+        k = 1
+        for d in range(4):
+            for s in (-1, 1):
+                c = sites.copy()
+                c[:, d] = (c[:, d] + s) % dims[d]
+                jj[:, k, :4] = c
+                k += 1
+        dim = list(dims) + [4, 3]
+        full = [([0] * 6, dim)]
+        vals = torch.randn(V * 9 * 144, dtype=dt, device=dev)
+        op = sb.create_bsr(full, dim, full, dim, [1, 1, 1, 1, 4, 3], [1, 1, 1, 1, 4, 3], False,
+                           [torch.full((V,), 9, dtype=torch.int32, device=dev)],
+                           [torch.from_numpy(jj.reshape(-1)).to(dev)], [vals])
+        ncols = int(os.environ.get("NCOLS", "12"))
+        dimx = [1] + list(dims) + [4, 3, ncols]
+        x = torch.randn(V * 12 * ncols, dtype=dt, device=dev)
+        y = torch.empty_like(x)
+        px = [([0] * 8, dimx)]
+        es = x.element_size()
+        by = es * (9 * 144 * V + 2 * 12 * V * ncols) + 4.0 * (9 * V + V + 1)
+        ref = None
+        for mode in [int(m) for m in os.environ.get("MODES", "0,1,2").split(",")]:
+            sb.tune_set("bsr.blk_dma", mode)
+            run = lambda: sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", px, "pXYZTSCn", [0] * 8, dimx,
+                                        dimx, [x], 0.0, px, "pxyztscn", [0] * 8, dimx, dimx, "p", [y])
+            run()
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = y.clone()
+            same = bool(torch.equal(y, ref))
+            sb.timings_enable(True)
+            sb.timings_filter("bsr")
+            sb.timings_reset()
+            for _ in range(10):
+                run()
+            torch.cuda.synchronize()
+            ms, calls = sb.timings_get("bsr")
+            sb.timings_enable(False)
+            sb.timings_filter(None)
+            t = ms / calls / 1e3
+            print(json.dumps({"dims": dims, "dtype": str(dt).split(".")[-1], "n": ncols,
+                              "blk_dma": mode, "kernel_us": round(t * 1e6, 1),
+                              "GBps": round(by / t / 1e9, 1), "frac_hbm": round(by / t / 8e12, 4),
+                              "same_as_register_staged": same}), flush=True)
+        sb.tune_set("bsr.blk_dma", -1)
+        op.destroy()
+        del x, y, vals, ref
+
+
+if __name__ == "__main__":
+    main()

@@ -90,6 +90,15 @@ def main():
     dev = torch.device("cuda", 0)
     L = int(os.environ.get("L", "16"))
     only = os.environ.get("KRON_ONLY")  # e.g. "complex128:12"
+    if os.environ.get("KRON_PADS"):  # LDS padding sweep of the MFMA kernel (residency per CU)
+        for pad in [int(v) for v in os.environ["KRON_PADS"].split(",")]:
+            sb.tune_set("bsr.kron_lds_pad", pad)
+            for n in (12, 24):
+                r = run(L, n, dev)
+                r["lds_pad"] = pad
+                print(json.dumps(r), flush=True)
+        sb.tune_set("bsr.kron_lds_pad", 0)
+        return
     if only:
         dt, n = only.split(":")
         print(json.dumps(run(L, int(n), dev, getattr(torch, dt), False)), flush=True)
