@@ -81,3 +81,20 @@ def test_gemm_granule_shapes(gpu, dtype, ta, tb, m, n, k):
     # extents that are multiples of the 16-byte granule of every type: the LDS-DMA kernel path
     out, ref = _run(gpu, dtype, ta, tb, m, n, k, 3, 0.5 + 1j, -0.75)
     assert rel_err(out, ref) < TOL[dtype]
+
+
+@pytest.mark.parametrize("dtype", [np.complex128, np.float64, np.complex64, np.float32])
+@pytest.mark.parametrize("ta,tb", [("T", "N"), ("N", "N"), ("N", "T"), ("C", "N"), ("T", "C")])
+@pytest.mark.parametrize("m,n,k,batch", [(48, 48, 768, 3), (34, 46, 520, 2), (48, 40, 4096, 1)])
+@pytest.mark.parametrize("t48", [1, 2, 3, 4])
+def test_gemm_48_tiles(gpu, dtype, ta, tb, m, n, k, batch, t48):
+    """33..48 rows and columns: the 48x48 LDS-DMA tile forms (sbx_tune_set "gemm.t48"; the
+    chain's TSnsN contraction shape), with split-K over the long k"""
+    import superbblas_amd as sb
+    old = sb.tune_get("gemm.t48")
+    sb.tune_set("gemm.t48", t48)
+    try:
+        out, ref = _run(gpu, dtype, ta, tb, m, n, k, batch, 0.5 + 1j, -1.0)
+    finally:
+        sb.tune_set("gemm.t48", old)
+    assert rel_err(out, ref) < TOL[dtype]

@@ -31,12 +31,16 @@ def main():
         dim = list(dims) + [4, 3]
         full = [([0] * 6, dim)]
         vals = torch.randn(V * 9 * 144, dtype=dt, device=dev)
+        if os.environ.get("VALS") == "int":  # small integers: fewer toggling mantissa bits
+            vals = torch.randint(-2, 3, (V * 9 * 144,), device=dev).to(dt)
         op = sb.create_bsr(full, dim, full, dim, [1, 1, 1, 1, 4, 3], [1, 1, 1, 1, 4, 3], False,
                            [torch.full((V,), 9, dtype=torch.int32, device=dev)],
                            [torch.from_numpy(jj.reshape(-1)).to(dev)], [vals])
         ncols = int(os.environ.get("NCOLS", "12"))
         dimx = [1] + list(dims) + [4, 3, ncols]
         x = torch.randn(V * 12 * ncols, dtype=dt, device=dev)
+        if os.environ.get("VALS") == "int":
+            x = torch.randint(-2, 3, (V * 12 * ncols,), device=dev).to(dt)
         y = torch.empty_like(x)
         px = [([0] * 8, dimx)]
         es = x.element_size()

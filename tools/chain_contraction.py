@@ -1,0 +1,49 @@
+#!/usr/bin/env python3
+"""The configs[4] chain's contraction alone (16^3 x 64 sites, complex<float>, n = 12:
+pXYZTSCn (conj) x pXYZTsCN -> TSnsN, a batched GEMM with m = n = 48, k = 12 288, batch 64) by
+GEMM tile shape (sbx_tune_set "gemm.t48": 0 = 64x64 tiles, 1..4 = 48x48 forms); results
+compared with torch.einsum.  Not part of the product."""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import superbblas_amd as sb  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda:0")
+    Ls, Lt, s_, c_, n = 16, 64, 4, 3, 12
+    dx = [1, Ls, Ls, Ls, Lt, s_, c_, n]
+    y = torch.randn(Ls ** 3 * Lt * s_ * c_ * n, dtype=torch.complex64, device=dev)
+    dr = [Lt, s_, n, s_, n]
+    vr = torch.empty(Lt * s_ * n * s_ * n, dtype=torch.complex64, device=dev)
+    p_x, p_r = [([0] * 8, dx)], [([0] * 5, dr)]
+    yv = y.view(Ls ** 3, Lt, s_, c_, n)
+    ref = torch.einsum("XTSCn,XTsCN->TSnsN", yv.conj(), yv).reshape(-1)
+    fl = 8.0 * vr.numel() * Ls ** 3 * c_
+    for t48 in [int(v) for v in os.environ.get("T48", "0,1,2,3,4").split(",")]:
+        sb.tune_set("gemm.t48", t48)
+
+        def f():
+            sb.contraction(1.0, p_x, [0] * 8, dx, dx, "pXYZTSCn", True, [y], p_x, [0] * 8, dx, dx,
+                           "pXYZTsCN", False, [y], 0.0, p_r, [0] * 5, dr, dr, "TSnsN", [vr])
+        f()
+        torch.cuda.synchronize()
+        err = (torch.linalg.vector_norm(vr - ref) / torch.linalg.vector_norm(ref)).item()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(10):
+            f()
+        e.record()
+        torch.cuda.synchronize()
+        t = s.elapsed_time(e) / 10 / 1e3
+        print(json.dumps({"t48": t48, "ms": round(t * 1e3, 4), "TFLOPs": round(fl / t / 1e12, 2),
+                          "rel_err_vs_einsum": err}), flush=True)
+    sb.tune_set("gemm.t48", 4)
+
+
+if __name__ == "__main__":
+    main()
