@@ -268,11 +268,16 @@ def main():
     side = {}
     skip = set(x for x in args.skip.split(",") if x)
     if args.no_side:
-        skip |= {"permute", "bsr", "chain", "3m", "chain_dist", "redistribution"}
+        skip |= {"permute", "bsr", "wilson", "chain", "3m", "chain_dist", "redistribution"}
     if world == 1 and "permute" not in skip:
         side.update(permute_bench(sb, dev, 16, 64))
     if world == 1 and "bsr" not in skip:
         side.update(bsr_bench(sb, dev, 16))
+    if world == 1 and "wilson" not in skip:
+        try:
+            side.update(wilson_bench(sb, dev, 16))
+        except Exception as e:  # a side measurement never takes the bench down
+            side["wilson_error"] = str(e)[:200]
     if world == 1 and "chain" not in skip:
         try:
             side.update(chain_bench(sb, dev))
@@ -855,6 +860,96 @@ def chain_dist_bench(sb, dev, comm, world, rank, grid, barrier, Ls=16, Lt=64, nc
 
 def dist_available():
     return torch.distributed.is_available() and torch.distributed.is_initialized()
+
+
+def wilson_bench(sb, dev, L, ncols=12, reps=5):
+    """config 3's secondary shapes on the 16^4 lattice, complex<double>, n = 12: the 12x12
+    (spin 4 x color 3) block operator (bsr_mfma_dma_kernel) and the same Wilson-like operator in
+    Kronecker form (3x3 color blocks x 4x4 spin matrices, bsr_kron_mfma_kernel).  Kernel time
+    from the library's HIP-event timers; algorithmic bytes: values, x and y once, the columns."""
+    dims = [L, L, L, L]
+    V = L ** 4
+    sites = np.array(np.unravel_index(np.arange(V), dims)).T
+    jj = np.zeros((V, 9, 6), np.int32)
+    jj[:, 0, :4] = sites
+    k = 1
+    for d in range(4):
+        for sg in (-1, 1):
+            cc = sites.copy()
+            cc[:, d] = (cc[:, d] + sg) % L
+            jj[:, k, :4] = cc
+            k += 1
+    ii = torch.full((V,), 9, dtype=torch.int32, device=dev)
+    jjt = torch.from_numpy(jj.reshape(-1)).to(dev)
+    out = {}
+
+    def timed(run):
+        run()
+        torch.cuda.synchronize()
+        sb.timings_enable(True)
+        sb.timings_filter("bsr")
+        sb.timings_reset()
+        for _ in range(reps):
+            run()
+        torch.cuda.synchronize()
+        ms, calls = sb.timings_get("bsr")
+        sb.timings_enable(False)
+        sb.timings_filter(None)
+        return ms / max(calls, 1) / 1e3
+
+    # 12x12 blocks, x pXYZTSCn -> y pxyztscn
+    dim = dims + [4, 3]
+    full = [([0] * 6, dim)]
+    vals = torch.empty(V * 9 * 144, dtype=torch.complex128, device=dev)
+    fill(vals, 31)
+    op = sb.create_bsr(full, dim, full, dim, [1, 1, 1, 1, 4, 3], [1, 1, 1, 1, 4, 3], False, [ii],
+                       [jjt], [vals])
+    dimx = [1] + dims + [4, 3, ncols]
+    x = torch.empty(V * 12 * ncols, dtype=torch.complex128, device=dev)
+    fill(x, 32)
+    y = torch.empty_like(x)
+    px = [([0] * 8, dimx)]
+    t = timed(lambda: sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", px, "pXYZTSCn", [0] * 8, dimx,
+                                    dimx, [x], 0.0, px, "pxyztscn", [0] * 8, dimx, dimx, "p", [y]))
+    by = 16.0 * (9 * 144 * V + 2 * 12 * V * ncols) + 4.0 * (10 * V + 1)
+    out.update({"bsr12_n12_kernel": "bsr_mfma_dma_kernel (12x12 blocks on FP64 MFMA, blocks by "
+                                    "LDS-DMA one ahead)",
+                "bsr12_n12_kernel_ms": round(t * 1e3, 4),
+                "bsr12_n12_kernel_GBps": round(by / t / 1e9, 1),
+                "bsr12_n12_kernel_frac_hbm": round(by / t / 1e9 / PEAK_HBM_GBPS, 4),
+                "bsr12_n12_algorithmic_bytes": by})
+    op.destroy()
+    del vals
+    # Kronecker form: 3x3 color blocks, Wilson spin matrices (1 -+ gamma_mu, chiral basis)
+    i_ = 1j
+    g = [np.array([[0, 0, 0, i_], [0, 0, i_, 0], [0, -i_, 0, 0], [-i_, 0, 0, 0]]),
+         np.array([[0, 0, 0, -1], [0, 0, 1, 0], [0, 1, 0, 0], [-1, 0, 0, 0]]),
+         np.array([[0, 0, i_, 0], [0, 0, 0, -i_], [-i_, 0, 0, 0], [0, i_, 0, 0]]),
+         np.array([[0, 0, 1, 0], [0, 0, 0, 1], [1, 0, 0, 0], [0, 1, 0, 0]])]
+    ks = [np.eye(4)]
+    for gm in g:
+        ks += [np.eye(4) - gm, np.eye(4) + gm]
+    kron = torch.from_numpy(np.array(ks, np.complex128).reshape(-1)).to(dev)
+    dim = dims + [4, 3]
+    full = [([0] * 6, dim)]
+    cvals = torch.empty(V * 81, dtype=torch.complex128, device=dev)
+    fill(cvals, 33)
+    blk, kr = [1, 1, 1, 1, 1, 3], [1, 1, 1, 1, 4, 1]
+    op = sb.create_kron_bsr(full, dim, full, dim, blk, blk, kr, kr, False, [ii], [jjt], [cvals],
+                            [kron])
+    dimx = [1] + dims + [3, ncols, 4]
+    px = [([0] * 8, dimx)]
+    t = timed(lambda: sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", px, "pXYZTCnS", [0] * 8, dimx,
+                                    dimx, [x], 0.0, px, "pxyztcns", [0] * 8, dimx, dimx, "p", [y]))
+    by = 16.0 * (81 * V + 2 * 12 * V * ncols) + 4.0 * 9 * V
+    out.update({"kron_n12_kernel": "bsr_kron_mfma_kernel (color on the VALU, spin on "
+                                   "v_mfma_f64_4x4x4_4b)",
+                "kron_n12_kernel_ms": round(t * 1e3, 4),
+                "kron_n12_kernel_GBps": round(by / t / 1e9, 1),
+                "kron_n12_kernel_frac_hbm": round(by / t / 1e9 / PEAK_HBM_GBPS, 4),
+                "kron_n12_algorithmic_bytes": by})
+    op.destroy()
+    return out
 
 
 def bsr_bench(sb, dev, L, ncols_list=(1, 12, 64), reps=5):

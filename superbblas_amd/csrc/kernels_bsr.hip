@@ -673,12 +673,15 @@ __global__ void __launch_bounds__(256) bsr_mfma_dma_kernel(const BsrArgs p, unsi
     int dj[NNZ];
 #pragma unroll
     for (int k = 0; k < NNZ; ++k) dj[k] = p.jj[jb + k];
-    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void *)p.v, (short)0, (int)v_bytes, 0x00020000);
+    // the row's NNZ value blocks (one contiguous run) as the buffer: 32-bit offsets at any size
+    (void)v_bytes;
+    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)((const E *)p.v + jb * ABLK), (short)0, NNZ * ABLK * ES, 0x00020000);
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)p.x, (short)0, (int)x_bytes, 0x00020000);
     const unsigned slot0 = lds_u32(smem) + (unsigned)w * (unsigned)(SLOT * (PD + 1));
     auto issue = [&](int k) {
         const unsigned base = slot0 + (unsigned)((k % (PD + 1)) * SLOT);
-        const unsigned av = (unsigned)((jb + k) * ABLK) * ES, xv = (unsigned)((long)(dj[k] < 0 ? 0 : dj[k]) * nc) * ES;
+        const unsigned av = (unsigned)(k * ABLK * ES), xv = (unsigned)((long)(dj[k] < 0 ? 0 : dj[k]) * nc) * ES;
 #pragma unroll
         for (int q = 0; q < NA; ++q) {
             const unsigned g = (unsigned)(lane + 64 * q) * 16u;
@@ -758,7 +761,7 @@ bool launch_bsr_mfma_dma(const BsrArgs &a, bool yrow, hipStream_t s) {
     constexpr int ES = (int)sizeof(E);
     constexpr int NA = (BI * BD * ES + 1023) / 1024, NX = (BD * 16 * ES + 1023) / 1024;
     const long v_bytes = a.block_rows * NNZ * (long)BI * BD * ES, x_bytes = a.x_rows * a.ldx * (long)ES;
-    if (v_bytes >= (1L << 31) || a.x_rows <= 0 || x_bytes >= (1L << 31)) return false;
+    if (a.x_rows <= 0 || x_bytes >= (1L << 31)) return false;
     const long blocks = (a.block_rows + 3) / 4;
     if (blocks >= (1L << 31)) return false;
     const size_t lds = (size_t)4 * (NA + NX) * 1024 * (PD + 1);
@@ -786,10 +789,10 @@ void launch_bsr_mfma(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_
     // operator 843-922 -> 722 us; two or three blocks of lookahead: 359-377 / 739-772 us)
     if (g_bsr_tune.variant != 1 && g_bsr_tune.variant != 2 && nnz == 9 && xrow &&
         a.ldx == a.ncols && a.ncols <= 16) {
-        // LDS-DMA staging (tools/bsr_blk_sweep.py, profiles/r02_bsr_blk_sweep.txt): one block
-        // ahead for 8-byte reals (16^4 complex<double> n = 12: 424 -> 407 us), two for 4-byte
-        // ones (the chain's 16^3 x 64 complex<float> operator: 965 -> 794 us)
-        const int pd = g_bsr_tune.blk_dma >= 0 ? g_bsr_tune.blk_dma : sizeof(R) == 4 ? 2 : 1;
+        // LDS-DMA staging one block ahead (tools/bsr_blk_sweep.py, warm GPU, modes round-robin,
+        // profiles/r02_bsr_blk_sweep.txt): the chain's 16^3 x 64 complex<float> operator 782 ->
+        // 735 us; 16^4 complex<double> unchanged (338 / 341 us); two blocks ahead slower for both
+        const int pd = g_bsr_tune.blk_dma >= 0 ? g_bsr_tune.blk_dma : 1;
         if (pd == 1 && launch_bsr_mfma_dma<R, CPLX, BI, BD, 9, 1>(a, yrow, s)) return;
         if (pd == 2 && launch_bsr_mfma_dma<R, CPLX, BI, BD, 9, 2>(a, yrow, s)) return;
         return launch_bsr_mfma_blk<R, CPLX, BI, BD, 9, 1>(a, yrow, s);

@@ -248,7 +248,7 @@ struct BsrTune {
     int ell9_ilv = 2;  ///< the same for the row-chunk 9-point kernel (bsr_ell9_kernel)
     long long probe = 0;    ///< tools only: device buffer for per-workgroup time stamps
     int blk_dma = -1; ///< 12x12 (block-staged) operators: blocks staged by LDS-DMA, 1 or 2 blocks ahead
-                      ///< (0 = registers, -1 = by the real type: 1 for double, 2 for float)
+                      ///< (0 = registers, -1 = the library's choice: 1)
     int kron_mfma = 1;          ///< Kronecker 3x3 (color) x 4x4 (spin) complex<double>: spin products on the
                                 ///< matrix cores (bsr_kron_mfma_kernel) ...
     long kron_mfma_min_cols = 8; ///< ... from this many rhs columns
