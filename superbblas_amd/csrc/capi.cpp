@@ -423,6 +423,8 @@ int sbx_tune_set(const char *key, long long value) {
         else if (k == "bsr.split_jb") g_bsr_tune.split_jb = (int)value;
         else if (k == "bsr.split_nt") g_bsr_tune.split_nt = (int)value;
         else if (k == "bsr.split_ilv") g_bsr_tune.split_ilv = (int)value;
+        else if (k == "bsr.split_ovl") g_bsr_tune.split_ovl = (int)value;
+        else if (k == "bsr.split_rw") g_bsr_tune.split_rw = (int)value;
         else if (k == "bsr.kron_mfma") g_bsr_tune.kron_mfma = (int)value;
         else if (k == "bsr.kron_mfma_min_cols") g_bsr_tune.kron_mfma_min_cols = (long)value;
         else if (k == "bsr.kron_lds_pad") g_bsr_tune.kron_lds_pad = (long)value;
@@ -462,6 +464,8 @@ int sbx_tune_get(const char *key, long long *value) {
         else if (k == "bsr.split_jb") *value = g_bsr_tune.split_jb;
         else if (k == "bsr.split_nt") *value = g_bsr_tune.split_nt;
         else if (k == "bsr.split_ilv") *value = g_bsr_tune.split_ilv;
+        else if (k == "bsr.split_ovl") *value = g_bsr_tune.split_ovl;
+        else if (k == "bsr.split_rw") *value = g_bsr_tune.split_rw;
         else if (k == "bsr.kron_mfma") *value = g_bsr_tune.kron_mfma;
         else if (k == "bsr.kron_mfma_min_cols") *value = g_bsr_tune.kron_mfma_min_cols;
         else if (k == "bsr.blk_dma") *value = g_bsr_tune.blk_dma;

@@ -1150,6 +1150,7 @@ struct SplitArgs {
     unsigned tpr_m, nct_m; // magic multipliers and shifts of tpr and nct (fdiv)
     int tpr_s, nct_s;
     int ilv; // an XCD's chunks visited as ilv interleaved parts (x rows reused across parts)
+    int ovl; // the partial products overwrite the staged values (one more barrier, half the LDS)
 };
 
 template <int CW, int JB, bool YROW>
@@ -1170,7 +1171,7 @@ __global__ void __launch_bounds__(512) bsr_ell9_split_kernel(const BsrArgs p, co
     const long row0 = chunk * s.rw;
     const int nrows = (int)min((long)s.rw, p.block_rows - row0);
     const int nv = nrows * NNZ * 9, nvp = (s.rw * NNZ * 9 + nth - 1) / nth * nth;
-    double2 *part = vals + nvp;
+    double2 *part = s.ovl ? vals : vals + nvp;
     const int rl = (int)fdiv(tid, s.tpr_m, s.tpr_s), rem = tid - rl * s.tpr;
     const int jg = (int)fdiv(rem, s.nct_m, s.nct_s), g = rem - jg * s.nct;
     const bool active = rl < nrows;
@@ -1250,6 +1251,7 @@ __global__ void __launch_bounds__(512) bsr_ell9_split_kernel(const BsrArgs p, co
                 if (col < p.ncols) store((row0 + rl) * 3 + c, col, acc[c][k]);
             }
     } else {
+        if (s.ovl) __syncthreads(); // every thread is done reading the values
         if (active) {
 #pragma unroll
             for (int c = 0; c < 3; ++c)
@@ -1293,14 +1295,18 @@ bool launch_ell9_split(const BsrArgs &a, bool yrow, bool xrow, hipStream_t st) {
         const int ntmax = g_bsr_tune.split_nt > 0 ? g_bsr_tune.split_nt : 256;
         if (tpr > ntmax) return false;
         // rows per workgroup: by the thread budget and at most 40 KB of LDS
-        const long row_lds = 81L * 16 + (jb == 9 ? 0L : (long)(9 / jb) * 3 * nct * cw * 16);
+        const bool ovl = g_bsr_tune.split_ovl > 0;
+        const long part_row = jb == 9 ? 0L : (long)(9 / jb) * 3 * nct * cw * 16;
+        const long row_lds = ovl ? std::max(81L * 16, part_row) : 81L * 16 + part_row;
         int rw = std::max(1, std::min<int>(ntmax / tpr, (int)(40960 / row_lds)));
+        if (g_bsr_tune.split_rw > 0) rw = std::min(rw, g_bsr_tune.split_rw);
         const int nth = (rw * tpr + 63) / 64 * 64;
         const long nvp = (rw * 81L + nth - 1) / nth * nth;
-        const long lds = (nvp + (jb == 9 ? 0L : (long)rw * (9 / jb) * 3 * nct * cw)) * 16L;
+        const long npart = jb == 9 ? 0L : (long)rw * (9 / jb) * 3 * nct * cw;
+        const long lds = (ovl ? std::max(nvp, npart) : nvp + npart) * 16L;
         if (lds > 65536) return false;
         SplitArgs sa{nct, tpr, rw, (unsigned)v_bytes, (unsigned)x_bytes, 0, 0, 0, 0,
-                     std::max(1, g_bsr_tune.split_ilv)};
+                     std::max(1, g_bsr_tune.split_ilv), ovl ? 1 : 0};
         magic((unsigned)tpr, sa.tpr_m, sa.tpr_s);
         magic((unsigned)nct, sa.nct_m, sa.nct_s);
         const long nchunks = (a.block_rows + rw - 1) / rw;

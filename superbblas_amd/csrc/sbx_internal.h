@@ -245,6 +245,8 @@ struct BsrTune {
     int split_jb = 0;  ///< ... nonzero blocks per thread (1, 3, 9; 0 = default)
     int split_nt = 0;  ///< ... threads per workgroup to aim at (0 = 256)
     int split_ilv = 2; ///< ... an XCD's rows visited as this many interleaved parts
+    int split_ovl = 1; ///< ... the partial products overlay the staged values in LDS (0 = beside them)
+    int split_rw = 0;  ///< ... block rows per workgroup (0 = as many as the thread and LDS budgets allow)
     int ell9_ilv = 2;  ///< the same for the row-chunk 9-point kernel (bsr_ell9_kernel)
     long long probe = 0;    ///< tools only: device buffer for per-workgroup time stamps
     int blk_dma = -1; ///< 12x12 (block-staged) operators: blocks staged by LDS-DMA, 1 or 2 blocks ahead

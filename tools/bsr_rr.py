@@ -23,12 +23,22 @@ CONFIGS = {
     "split_cw2_jb3": {"bsr.split_cw": 2, "bsr.split_jb": 3, "bsr.split_ilv": 1},
     "split_cw2_jb3_ilv2": {"bsr.split_cw": 2, "bsr.split_jb": 3, "bsr.split_ilv": 2},
     "split_cw2_jb9_ilv2": {"bsr.split_cw": 2, "bsr.split_jb": 9, "bsr.split_ilv": 2},
+    "cw2_jb3_sep": {"bsr.split_cw": 2, "bsr.split_jb": 3, "bsr.split_ovl": 0},
+    "cw2_jb3_ovl": {"bsr.split_cw": 2, "bsr.split_jb": 3, "bsr.split_ovl": 1},
+    "cw1_jb3_ovl": {"bsr.split_cw": 1, "bsr.split_jb": 3, "bsr.split_ovl": 1},
+    "cw2_jb3_ovl_nt512": {"bsr.split_cw": 2, "bsr.split_jb": 3, "bsr.split_ovl": 1, "bsr.split_nt": 512},
+    "cw1_jb3_ovl_nt512": {"bsr.split_cw": 1, "bsr.split_jb": 3, "bsr.split_ovl": 1, "bsr.split_nt": 512},
+    "cw2_jb1_ovl": {"bsr.split_cw": 2, "bsr.split_jb": 1, "bsr.split_ovl": 1},
+    "rw10": {"bsr.split_rw": 10}, "rw11": {"bsr.split_rw": 11}, "rw12": {"bsr.split_rw": 12},
+    "rw13": {"bsr.split_rw": 13}, "rw14": {"bsr.split_rw": 14},
     "default": {},
 }
 BASE = {"bsr.split_max_cols": 1 << 20, "bsr.row_max_cols": 0, "bsr.split_cw": 0,
-        "bsr.split_jb": 0, "bsr.split_ilv": 2, "bsr.ell9_ilv": 2, "bsr.tile": 0}
+        "bsr.split_jb": 0, "bsr.split_ilv": 2, "bsr.ell9_ilv": 2, "bsr.tile": 0,
+        "bsr.split_ovl": 1, "bsr.split_nt": 0, "bsr.split_rw": 0}
 DEFAULTS = {"bsr.split_max_cols": 32, "bsr.row_max_cols": 3, "bsr.split_cw": 0,
-            "bsr.split_jb": 0, "bsr.split_ilv": 2, "bsr.ell9_ilv": 2, "bsr.tile": 0}
+            "bsr.split_jb": 0, "bsr.split_ilv": 2, "bsr.ell9_ilv": 2, "bsr.tile": 0,
+            "bsr.split_ovl": 1, "bsr.split_nt": 0, "bsr.split_rw": 0}
 
 
 def main():
