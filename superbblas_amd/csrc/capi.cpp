@@ -408,6 +408,8 @@ int sbx_tune_set(const char *key, long long value) {
         else if (k == "copy.kernel") g_copy_tune.kernel = (int)value;
         else if (k == "copy.nt") g_copy_tune.nt = (int)value;
         else if (k == "copy.max_elems") g_copy_tune.max_elems = (long)value;
+        else if (k == "copy.pair") g_copy_tune.pair = (int)value;
+        else if (k == "copy.order") g_copy_tune.order = (int)value;
         else if (k == "gemm.max_bytes") g_gemm_tune.max_bytes = (long)value;
         else if (k == "bsr.variant") g_bsr_tune.variant = (int)value;
         else if (k == "bsr.ell9") g_bsr_tune.ell9 = (int)value;
@@ -449,6 +451,9 @@ int sbx_tune_get(const char *key, long long *value) {
         else if (k == "copy.kernel") *value = g_copy_tune.kernel;
         else if (k == "copy.nt") *value = g_copy_tune.nt;
         else if (k == "copy.max_elems") *value = g_copy_tune.max_elems;
+        else if (k == "copy.pair") *value = g_copy_tune.pair;
+        else if (k == "copy.order") *value = g_copy_tune.order;
+        else if (k == "copy.last_pair") *value = g_copy_tune.last_pair;
         else if (k == "gemm.max_bytes") *value = g_gemm_tune.max_bytes;
         else if (k == "bsr.variant") *value = g_bsr_tune.variant;
         else if (k == "bsr.ell9") *value = g_bsr_tune.ell9;
@@ -674,7 +679,8 @@ int sbx_copy_req(int nd0, int nd1, const double *alpha, int t0, int t1, const in
             key.insert(key.end(), {nd0, nd1, t0, t1, ncomponents0, ncomponents1, co, copyadd,
                                    (long)a_call.is_zero(), comm ? 1L : 0L, c.device,
                                    g_copy_tune.budget, g_copy_tune.run, g_copy_tune.kernel,
-                                   g_copy_tune.nt, g_copy_tune.max_elems});
+                                   g_copy_tune.nt, g_copy_tune.max_elems, (long)g_copy_tune.pair,
+                                   (long)g_copy_tune.order});
             key_str(key, o0, nd0);
             key_str(key, o1, nd1);
             key_ints(key, p0, 2L * nd0 * ncomponents0);

@@ -23,6 +23,7 @@
 #include <cstdlib>
 #include <mutex>
 #include <numeric>
+#include <type_traits>
 #include <unordered_map>
 
 namespace sbx {
@@ -199,6 +200,7 @@ struct TiledArgs {
     FastDiv fRTU, fRTV;     // R*TU, R*TV
     uint32_t ntu, ntv;      // number of tiles along U and V
     uint32_t lr, lw;        // log2 of the lanes per tile row in the read / write phase
+    uint32_t lr2, lw2;      // ... for the paired (16-byte) forms of the phases
     int nt;                 // non-temporal stores
     int nu, nv;             // dims in the U chain (source-contiguous) / V chain (dest-contiguous)
     FastDiv usize[MAXD], vsize[MAXD];
@@ -323,7 +325,12 @@ __device__ __forceinline__ void chain_offsets4(uint32_t idx, int n, const FastDi
 // wave+4, ...; the write phase does the same over destination rows.  A lane's (u, r) split and
 // offset base are computed once, so an element costs one LDS offset read (wave-uniform), one
 // global access and one LDS access.  The u and v offset tables are filled by different waves.
-template <typename S, typename D, bool ADD, int KR>
+// VR / VW = 2 (8-byte source / destination elements): the read / write phase moves two elements per lane
+// (one 16-byte access): a tile row is then one contiguous, 16-byte aligned run of an even number
+// of elements on that side (checked by the launcher), and the lane count per access halves
+// (complex<float> transposes were bound by 8-byte lane accesses: chain redistribution 3.3 TB/s)
+template <typename D> struct alignas(16) Pair { D a, b; };
+template <typename S, typename D, bool ADD, int KR, int VR = 1, int VW = 1>
 __global__ void __launch_bounds__(256) copy_tiled3_kernel(const TiledArgs p) {
     __shared__ D tile[tile_elems<D>() + 64];
     __shared__ long su[256], du[256], sv[256], dv[256];
@@ -360,7 +367,32 @@ __global__ void __launch_bounds__(256) copy_tiled3_kernel(const TiledArgs p) {
     const uint32_t ld = p.TU * p.R + 1;
     // read phase: rows = v (nv_t of them), row width R*nu_t; 2^lr lanes per row, so a wave
     // covers 64 >> lr rows per step and a thread keeps KR rows' loads in flight
-    {
+    if constexpr (VR == 2) {
+        // pairs of a contiguous source run: element offset su[0] + pos in the row of v
+        const uint32_t wr2 = p.R * nu_t / 2, lpr = 1u << p.lr2;
+        const uint32_t step = 4u * (64u >> p.lr2);
+        const uint32_t vfirst = wave * (64u >> p.lr2) + (lane >> p.lr2);
+        for (uint32_t pp = lane & (lpr - 1); pp < wr2; pp += lpr) {
+            const uint32_t pos = 2 * pp;
+            const long base = sbase + su[0] + pos;
+            for (uint32_t vb = vfirst; vb < nv_t; vb += step * KR) {
+                Pair<S> val[KR];
+#pragma unroll
+                for (int k = 0; k < KR; ++k) {
+                    const uint32_t v = vb + step * k;
+                    val[k] = *(const Pair<S> *)(src + base + sv[v < nv_t ? v : vb]);
+                }
+#pragma unroll
+                for (int k = 0; k < KR; ++k) {
+                    const uint32_t v = vb + step * k;
+                    if (v < nv_t) {
+                        tile[v * ld + pos] = xform<D, S>(val[k].a, p.alpha);
+                        tile[v * ld + pos + 1] = xform<D, S>(val[k].b, p.alpha);
+                    }
+                }
+            }
+        }
+    } else {
         const uint32_t wr = p.R * nu_t, lpr = 1u << p.lr;
         const uint32_t step = 4u * (64u >> p.lr);
         const uint32_t vfirst = wave * (64u >> p.lr) + (lane >> p.lr);
@@ -384,6 +416,27 @@ __global__ void __launch_bounds__(256) copy_tiled3_kernel(const TiledArgs p) {
     }
     __syncthreads();
     // write phase: rows = u (nu_t of them), row width R*nv_t
+    if constexpr (VW == 2) {
+        // pairs of a contiguous destination run: element offset dv[0] + pos in the row of u
+        const uint32_t ww2 = p.R * nv_t / 2, lpr = 1u << p.lw2;
+        const uint32_t step = 4u * (64u >> p.lw2);
+        const uint32_t ufirst = wave * (64u >> p.lw2) + (lane >> p.lw2);
+        for (uint32_t pp = lane & (lpr - 1); pp < ww2; pp += lpr) {
+            const uint32_t pos = 2 * pp;
+            const uint32_t va = p.fR.div(pos), ra = pos - va * p.R;
+            const uint32_t vb = p.fR.div(pos + 1), rb = pos + 1 - vb * p.R;
+            const long base = dbase + dv[0] + pos;
+            const uint32_t la = va * ld + ra, lb = vb * ld + rb;
+            for (uint32_t u = ufirst; u < nu_t; u += step) {
+                const Pair<D> val{tile[la + u * p.R], tile[lb + u * p.R]};
+                if (p.nt)
+                    store_nt((Pair<D> *)(dst + base + du[u]), val);
+                else
+                    *(Pair<D> *)(dst + base + du[u]) = val;
+            }
+        }
+        return;
+    }
     {
         const uint32_t ww = p.R * nv_t, lpr = 1u << p.lw;
         const uint32_t step = 4u * (64u >> p.lw);
@@ -455,6 +508,7 @@ struct CopyLaunch {
     TiledArgs ta{};
     long total = 0, blocks = 0;
     int nt = 0;
+    int vr = 0, vw = 0; // tiled: the shape allows paired reads / writes (pointers checked per call)
     void (*run)(const CopyLaunch &, const void *, void *, const Alpha &, const float *,
                 const float *, hipStream_t) = nullptr;
 };
@@ -487,14 +541,42 @@ void run_launch(const CopyLaunch &l, const void *src, void *dst, const Alpha &al
     }
     case CopyLaunch::TILED1:
     case CopyLaunch::TILED3: {
+        g_copy_tune.last_pair = 0;
         TiledArgs a = l.ta;
         a.src = src;
         a.dstp = dst;
         a.alpha = alpha;
-        if (l.kind == CopyLaunch::TILED1)
+        if (l.kind == CopyLaunch::TILED1) {
             hipLaunchKernelGGL((copy_tiled_kernel<S, D, ADD>), grid, block, 0, stream, a);
-        else
+            break;
+        }
+        constexpr bool PS = sizeof(S) == 8, PD = sizeof(D) == 8 && !ADD;
+        if constexpr (PS || PD) {
+            const bool vr = PS && l.vr && ((size_t)src & 15) == 0;
+            const bool vw = PD && l.vw && ((size_t)dst & 15) == 0;
+            g_copy_tune.last_pair = (vr ? 1 : 0) | (vw ? 2 : 0);
+            if constexpr (PS && PD) {
+                if (vr && vw) {
+                    hipLaunchKernelGGL((copy_tiled3_kernel<S, D, ADD, 4, 2, 2>), grid, block, 0, stream, a);
+                    break;
+                }
+            }
+            if constexpr (PS) {
+                if (vr) {
+                    hipLaunchKernelGGL((copy_tiled3_kernel<S, D, ADD, 4, 2, 1>), grid, block, 0, stream, a);
+                    break;
+                }
+            }
+            if constexpr (PD) {
+                if (vw) {
+                    hipLaunchKernelGGL((copy_tiled3_kernel<S, D, ADD, 4, 1, 2>), grid, block, 0, stream, a);
+                    break;
+                }
+            }
             hipLaunchKernelGGL((copy_tiled3_kernel<S, D, ADD, 4>), grid, block, 0, stream, a);
+        } else {
+            hipLaunchKernelGGL((copy_tiled3_kernel<S, D, ADD, 4>), grid, block, 0, stream, a);
+        }
         break;
     }
     }
@@ -578,9 +660,35 @@ CopyLaunch prepare_pair(bool masked, Norm n, long total) {
             want *= n.size[found];
         }
     };
+    bool u_contig = false; // the U chain starts at source stride R (its items are one run)
     if (first < nd && R <= 64) {
+        const Norm n_keep = n;
+        const std::vector<bool> used_keep = used;
         build_chain(true, Vc, R);
         if (!Vc.empty()) build_chain(false, U, R);
+        u_contig = !U.empty();
+        if (!Vc.empty() && U.empty() && g_copy_tune.order >= 0 && sizeof(S) == 8 &&
+            std::is_same<S, D>::value && g_copy_tune.pair >= 0) {
+            // the destination chain took the source's contiguous dim (n <-> c <-> xyz transposes:
+            // c fastest in the source, second in the destination): with paired 8-byte accesses
+            // the source chain goes first, so both phases move whole runs (the chain
+            // redistribution tnsxyzc -> pxyztscn, complex<float>)
+            Norm n_u = n_keep;
+            std::vector<bool> used_u = used_keep;
+            std::vector<int> U2, V2;
+            std::swap(n, n_u);
+            std::swap(used, used_u);
+            build_chain(false, U2, R);
+            if (!U2.empty()) build_chain(true, V2, R);
+            if (!U2.empty() && !V2.empty()) {
+                U = U2;
+                Vc = V2;
+                u_contig = true;
+            } else {
+                std::swap(n, n_u);
+                std::swap(used, used_u);
+            }
+        }
         if (!Vc.empty() && U.empty()) {
             // the source-contiguous dims went to V: start U at the smallest remaining source
             // stride (reads of a tile then interleave across its V items, still line-complete)
@@ -645,6 +753,8 @@ CopyLaunch prepare_pair(bool masked, Norm n, long total) {
     a.nt = g_copy_tune.nt > 0 || (g_copy_tune.nt == 0 && total * (long)sizeof(D) >= (8L << 20));
     a.lr = lanes_log2(R * TU);
     a.lw = lanes_log2(R * TV);
+    a.lr2 = lanes_log2((R * TU + 1) / 2);
+    a.lw2 = lanes_log2((R * TV + 1) / 2);
     a.ntu = (uint32_t)((NU + TU - 1) / TU);
     a.ntv = (uint32_t)((NV + TV - 1) / TV);
     a.nu = (int)U.size();
@@ -670,13 +780,29 @@ CopyLaunch prepare_pair(bool masked, Norm n, long total) {
         ++nw;
     }
     a.nw = nw;
+    if (g_copy_tune.pair >= 0 && (sizeof(S) == 8 || sizeof(D) == 8)) {
+        // paired accesses: every tile row an even, 16-byte aligned run on that side (element
+        // offsets of the row starts even: the other chain's and the outer dims' strides even)
+        auto even_strides = [&](const std::vector<int> &dims, bool dst_side) {
+            for (int i : dims)
+                if (n.size[i] > 1 && ((dst_side ? n.ds[i] : n.ss[i]) & 1)) return false;
+            return true;
+        };
+        std::vector<int> W;
+        for (int i = first; i < ndd; ++i)
+            if (!used[i]) W.push_back(i);
+        const bool rows_u = (R * TU) % 2 == 0 && (R * (NU % TU)) % 2 == 0;
+        const bool rows_v = (R * TV) % 2 == 0 && (R * (NV % TV)) % 2 == 0;
+        l.vr = sizeof(S) == 8 && u_contig && rows_u && even_strides(Vc, false) && even_strides(W, false);
+        l.vw = sizeof(D) == 8 && !ADD && rows_v && even_strides(U, true) && even_strides(W, true);
+    }
     const long blocks = (long)a.ntu * a.ntv * NW;
     if (blocks >= (1L << 31)) throw Error("copy: grid too large");
     if (debug) {
         std::fprintf(stderr, "copy_tiled: dims(size/ss/ds)");
         for (int i = 0; i < ndd; ++i) std::fprintf(stderr, " %ld/%ld/%ld", n.size[i], n.ss[i], n.ds[i]);
-        std::fprintf(stderr, " | R=%ld NU=%ld NV=%ld TU=%ld TV=%ld nu=%d nv=%d nw=%d blocks=%ld\n", R,
-                     NU, NV, TU, TV, a.nu, a.nv, nw, blocks);
+        std::fprintf(stderr, " | R=%ld NU=%ld NV=%ld TU=%ld TV=%ld nu=%d nv=%d nw=%d blocks=%ld vr=%d vw=%d\n",
+                     R, NU, NV, TU, TV, a.nu, a.nv, nw, blocks, l.vr, l.vw);
     }
     l.kind = g_copy_tune.kernel == 1 ? CopyLaunch::TILED1 : CopyLaunch::TILED3;
     l.blocks = blocks;
@@ -786,7 +912,8 @@ void launch_box_copy(const BoxCopyDesc &d, int device) {
                   ((long)(d.src_mask != nullptr) << 17) | ((long)(d.dst_mask != nullptr) << 18));
     key.push_back(g_copy_tune.budget);
     key.push_back(g_copy_tune.run);
-    key.push_back(g_copy_tune.kernel + 16L * g_copy_tune.nt);
+    key.push_back(g_copy_tune.kernel + 16L * g_copy_tune.nt + 256L * g_copy_tune.pair +
+                  4096L * g_copy_tune.order);
     for (std::size_t i = 0; i < nd; ++i) {
         key.push_back(d.size[i]);
         key.push_back(d.src_stride[i]);

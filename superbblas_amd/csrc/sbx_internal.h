@@ -215,6 +215,10 @@ struct CopyTune {
     int kernel = 0;  ///< 1: the round-1 tiled kernel (element-indexed phases) instead of the row-mapped one
     int nt = 0;      ///< row-mapped kernel stores: 0 = non-temporal for large outputs, 1 = always, -1 = never
     long max_elems = 0; ///< elements per launch before a box is cut into slabs (0 = 2^31 - 1)
+    int pair = 0;  ///< tiled kernel, 8-byte elements: two elements per lane access where the runs allow (-1 = never)
+    int order = 0; ///< ... with pairs, the source chain first when the destination chain would take the
+                   ///< source's contiguous dim (-1 = always the destination chain first)
+    int last_pair = 0; ///< read-back ("copy.last_pair"): the last tiled launch's paired phases (1 reads, 2 writes)
 };
 extern CopyTune g_copy_tune;
 struct GemmTune {

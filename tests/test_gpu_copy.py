@@ -240,3 +240,46 @@ def test_copy_fast_path_replay(gpu):
                 [3, 0], dim, [t])
         torch.cuda.synchronize()
         assert np.array_equal(t.cpu().numpy().view(np.uint8), ref.view(np.uint8)), rep
+
+
+@pytest.mark.parametrize("t0,t1", [(np.complex64, np.complex64), (np.float64, np.float64),
+                                   (np.uint64, np.uint64), (np.complex64, np.complex128),
+                                   (np.complex128, np.complex64), (np.float64, np.complex64)])
+def test_paired_8byte_transposes(gpu, t0, t1):
+    """The tiled kernel's paired (16-byte) accesses for 8-byte elements: the chain's n <-> c <->
+    xyz redistribution (source chain first), its contraction-operand reorder, a whole-tensor
+    permute; even and odd rhs counts (odd rows fall back to single accesses), boxes at odd
+    origins (8-byte aligned pointers fall back), alpha and Add (paired reads only)."""
+    cases = [("tnsxyzc", "pxyztscn", lambda n: ([4, n, 4, 4, 4, 4, 3], [1, 4, 4, 4, 4, 4, 3, n])),
+             ("pXYZTSCn", "TSnpXYZC", lambda n: ([1, 4, 4, 4, 4, 4, 3, n], [4, 4, n, 1, 4, 4, 4, 3])),
+             ("xyztnsc", "tnsxyzc", lambda n: ([4, 4, 4, 4, n, 4, 3], [4, n, 4, 4, 4, 4, 3]))]
+    import superbblas_amd as sb
+    forms = set()
+    for (o0, o1, dims), n, shift, add in itertools.product(cases, (6, 5), (0, 1), (False, True)):
+        if add and np.dtype(t1).kind == "u":
+            continue
+        dim0, dim1 = dims(n)
+        size0 = list(dim0)
+        from0 = [0] * len(dim0)
+        from1 = [0] * len(dim1)
+        if shift:  # a box one short in the rhs dim, at rhs origin 1 on both sides
+            i0, i1 = o0.index("n" if "n" in o0 else "N"), o1.index("n" if "n" in o1 else "N")
+            size0[i0] -= 1
+            from0[i0] = 1
+            from1[i1] = 1
+        kind = np.dtype(t0).kind
+        v0 = index_valued(_vol(dim0), t0) if kind == "u" else int_valued(_vol(dim0), t0, 3)
+        v1 = np.arange(_vol(dim1)).astype(t1) if np.dtype(t1).kind == "u" else \
+            int_valued(_vol(dim1), t1, 4)
+        alpha = 1.0 if kind == "u" else (2.0 - 1.0j if kind == "c" else 3.0)
+        ref = v1.copy()
+        oracle_copy(alpha, o0, from0, size0, dim0, v0, o1, from1, dim1, ref, add=add)
+        out = _gpu_local_copy(gpu, alpha, o0, from0, size0, dim0, v0, o1, from1, dim1, v1.copy(),
+                              add=add)
+        forms.add(sb.tune_get("copy.last_pair"))
+        assert np.array_equal(out.view(np.uint8), ref.view(np.uint8)), (o0, o1, n, shift, add)
+    # paired reads ran for 8-byte sources, paired writes for 8-byte destinations, and the
+    # single-access fallback ran too
+    assert 0 in forms, forms
+    assert any(f & 1 for f in forms) == (np.dtype(t0).itemsize == 8), forms
+    assert any(f & 2 for f in forms) == (np.dtype(t1).itemsize == 8), forms

@@ -23,8 +23,9 @@ def vol(d):
 
 def case(name, o0, d0, o1, d1, from1, dtype, reps=10):
     dev = torch.device("cuda:0")
+    dtype, dtype_out = dtype if isinstance(dtype, tuple) else (dtype, dtype)
     a = torch.randn(vol(d0), dtype=dtype, device=dev)
-    b = torch.zeros(vol(d1), dtype=dtype, device=dev)
+    b = torch.zeros(vol(d1), dtype=dtype_out, device=dev)
     p0, p1 = [([0] * len(d0), d0)], [([0] * len(d1), d1)]
 
     def f():
@@ -40,7 +41,7 @@ def case(name, o0, d0, o1, d1, from1, dtype, reps=10):
     sb.timings_enable(False)
     t = ms / calls / 1e3
     es = torch.empty(0, dtype=dtype).element_size()
-    ok = bool(torch.equal(b.view(-1), ref_copy(a, o0, d0, o1, d1, from1).view(-1)))
+    ok = bool(torch.equal(b.view(-1), ref_copy(a.to(dtype_out), o0, d0, o1, d1, from1).view(-1)))
     print(json.dumps({"case": name, "us": round(t * 1e6, 1),
                       "GBps": round(2 * es * vol(d0) / t / 1e9, 1), "exact": ok}))
 
@@ -57,16 +58,20 @@ def ref_copy(a, o0, d0, o1, d1, from1):
 
 
 def main():
-    combos = ((0, 0, 0), (1, 0, 0), (0, -1, 0))
+    combos = ((0, 0, 0), (0, 0, -1), (0, 0, -2), (1, 0, 0), (0, -1, 0))
     if os.environ.get("COPY_QUICK"):
-        combos = combos[:2]
-    for kern, nt, _ in combos:
+        combos = combos[:3]
+    for kern, nt, pair in combos:
         sb.tune_set("copy.kernel", kern)
         sb.tune_set("copy.nt", nt)
-        print(json.dumps({"copy.kernel": kern, "copy.nt": nt}))
+        sb.tune_set("copy.pair", 0 if pair == -2 else pair)
+        sb.tune_set("copy.order", -1 if pair == -2 else 0)  # -2: pairs, destination chain first
+        print(json.dumps({"copy.kernel": kern, "copy.nt": nt, "copy.pair": pair}))
         shapes()
     sb.tune_set("copy.kernel", 0)
     sb.tune_set("copy.nt", 0)
+    sb.tune_set("copy.pair", 0)
+    sb.tune_set("copy.order", 0)
 
 
 def shapes():
@@ -79,6 +84,14 @@ def shapes():
          [1, 16, 16, 16, 64, 4, 3, 12], [0] * 8, torch.complex64)
     case("chain", "pXYZTSCn", [1, 16, 16, 16, 64, 4, 3, 12], "TSnpXYZC",
          [64, 4, 12, 1, 16, 16, 16, 3], [0] * 8, torch.complex64)
+    case("slice_cf", "xyztsc", [L, L, L, L, 4, 3], "tnsxyzc", [L, n, 4, L, L, L, 3],
+         [0, 5, 0, 0, 0, 0, 0], torch.complex64)
+    case("big_cf", "xyztnsc", [L, L, L, L, n, 4, 3], "tnsxyzc", [L, n, 4, L, L, L, 3], [0] * 7,
+         torch.complex64)
+    case("slice_cf2cd", "xyztsc", [L, L, L, L, 4, 3], "tnsxyzc", [L, n, 4, L, L, L, 3],
+         [0, 5, 0, 0, 0, 0, 0], (torch.complex64, torch.complex128))
+    case("big_f64", "xyztnsc", [L, L, L, L, n, 4, 3], "tnsxyzc", [L, n, 4, L, L, L, 3], [0] * 7,
+         torch.float64)
 
 
 if __name__ == "__main__":
