@@ -717,6 +717,9 @@ void launch_tiled_cfg(const GemmKArgs &p0, int device, hipStream_t stream, long 
     Scratch work;
     const long nwg = prepare_launch<typename Elem<R, CPLX>::type>(p, BM, BN, BKK, splits,
                                                                    target_wgs, work, device);
+    // "gemm_total": one event pair around the GEMM launch and its split-K reduce (the bench's
+    // roofline timer: two event records per GEMM instead of four)
+    KernelTimer total("gemm_total", stream);
     {
         KernelTimer timer("gemm", stream);
         hipLaunchKernelGGL((gemm_kernel<R, CPLX, AK, BK, BM, BN, BKK, WM, WN>),
@@ -740,6 +743,7 @@ void launch_dma_cfg(const GemmKArgs &p0, int device, hipStream_t stream, long sp
     if (g_gemm_tune.splits > 0) splits = g_gemm_tune.splits;
     const long nwg = prepare_launch<typename Elem<R, CPLX>::type>(p, BM, BN, BKK, splits,
                                                                    target_wgs, work, device);
+    KernelTimer total("gemm_total", stream);
     {
         KernelTimer timer("gemm", stream);
         if constexpr (ALLOW_M3) {
