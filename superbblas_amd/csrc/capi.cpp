@@ -438,6 +438,7 @@ int sbx_tune_set(const char *key, long long value) {
         else if (k == "gemm.m3") g_gemm_tune.m3 = (int)value;
         else if (k == "gemm.splits") g_gemm_tune.splits = (int)value;
         else if (k == "gemm.t48") g_gemm_tune.t48 = (int)value;
+        else if (k == "gemm.share_ab") g_gemm_tune.share_ab = (int)value;
         else throw Error("tune_set: unknown key " + k);
     });
 }
@@ -482,6 +483,7 @@ int sbx_tune_get(const char *key, long long *value) {
         else if (k == "gemm.m3") *value = g_gemm_tune.m3;
         else if (k == "gemm.splits") *value = g_gemm_tune.splits;
         else if (k == "gemm.t48") *value = g_gemm_tune.t48;
+        else if (k == "gemm.share_ab") *value = g_gemm_tune.share_ab;
         else throw Error("tune_get: unknown key " + k);
     });
 }

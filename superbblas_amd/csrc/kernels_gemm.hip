@@ -104,6 +104,10 @@ struct GemmKArgs {
     int split;
     long m_lo, n_lo, k_lo;
     long sa_m_hi, sa_k_hi, sb_k_hi, sb_n_hi, sc_m_hi, sc_n_hi;
+    // A and B are the same memory with the same M / N and K addressing (a tensor contracted with
+    // itself or its conjugate, e.g. the chain's correlator y^H y): a workgroup on a diagonal tile
+    // (m0 == n0) stages one slab image and reads both operands' fragments from it
+    int same_ab;
 };
 
 /// Offset of index i of a split group: (i / lo) * s_hi + (i % lo) * s (i < 2^31)
@@ -462,9 +466,12 @@ __global__ void __launch_bounds__(WM *WN * 64) gemm_dma_kernel(const GemmKArgs p
 
     const long nslab = (k_end - k_begin + BKK - 1) / BKK;
     const char *const base = (const char *)lds;
+    constexpr bool CAN_SHARE = AK == BK && BM == BN; // same slab image layout for A and B
+    const bool share = CAN_SHARE && p.same_ab && m0 == n0;
     if (nslab > 0) {
         da.issue(rsA, base, wave, k_begin, k_end, p.sa_k, spl, p.k_lo, p.sa_k_hi);
-        db.issue(rsB, base + BM * BKK * ES, wave, k_begin, k_end, p.sb_k, spl, p.k_lo, p.sb_k_hi);
+        if (!share)
+            db.issue(rsB, base + BM * BKK * ES, wave, k_begin, k_end, p.sb_k, spl, p.k_lo, p.sb_k_hi);
     }
     for (long s = 0; s < nslab; ++s) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // this wave's DMA of slab s landed
@@ -474,10 +481,11 @@ __global__ void __launch_bounds__(WM *WN * 64) gemm_dma_kernel(const GemmKArgs p
             const char *nb = base + (size_t)(cur ^ 1) * SLAB * ES;
             const long kn = k_begin + (s + 1) * BKK;
             da.issue(rsA, nb, wave, kn, k_end, p.sa_k, spl, p.k_lo, p.sa_k_hi);
-            db.issue(rsB, nb + BM * BKK * ES, wave, kn, k_end, p.sb_k, spl, p.k_lo, p.sb_k_hi);
+            if (!share)
+                db.issue(rsB, nb + BM * BKK * ES, wave, kn, k_end, p.sb_k, spl, p.k_lo, p.sb_k_hi);
         }
         const E *As = lds + cur * SLAB;
-        const E *Bs = As + BM * BKK;
+        const E *Bs = share ? As : As + BM * BKK;
         if constexpr (PF && CPLX && !M3) {
             E af[2][MT], bf[2][NT];
             auto frag = [&](int kk, E *a_, E *b_) {
@@ -741,6 +749,9 @@ void launch_dma_cfg(const GemmKArgs &p0, int device, hipStream_t stream, long sp
     GemmKArgs p = p0;
     Scratch work;
     if (g_gemm_tune.splits > 0) splits = g_gemm_tune.splits;
+    p.same_ab = g_gemm_tune.share_ab && p.a == p.b && p.m == p.n && p.sa_m == p.sb_n &&
+                p.sa_k == p.sb_k && p.sa_b == p.sb_b && p.m_lo == p.n_lo &&
+                p.sa_m_hi == p.sb_n_hi && p.sa_k_hi == p.sb_k_hi;
     const long nwg = prepare_launch<typename Elem<R, CPLX>::type>(p, BM, BN, BKK, splits,
                                                                    target_wgs, work, device);
     KernelTimer total("gemm_total", stream);

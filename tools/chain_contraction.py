@@ -24,8 +24,12 @@ def main():
     yv = y.view(Ls ** 3, Lt, s_, c_, n)
     ref = torch.einsum("XTSCn,XTsCN->TSnsN", yv.conj(), yv).reshape(-1)
     fl = 8.0 * vr.numel() * Ls ** 3 * c_
-    for t48 in [int(v) for v in os.environ.get("T48", "0,1,2,3,4").split(",")]:
+    combos = [(int(v), 1) for v in os.environ.get("T48", "0,1,2,3,4").split(",")]
+    if os.environ.get("SHARE"):  # one slab image for both operands (the same memory) on / off
+        combos = [(4, int(v)) for v in os.environ["SHARE"].split(",")] * 2
+    for t48, share in combos:
         sb.tune_set("gemm.t48", t48)
+        sb.tune_set("gemm.share_ab", share)
 
         def f():
             sb.contraction(1.0, p_x, [0] * 8, dx, dx, "pXYZTSCn", True, [y], p_x, [0] * 8, dx, dx,
@@ -40,9 +44,11 @@ def main():
         e.record()
         torch.cuda.synchronize()
         t = s.elapsed_time(e) / 10 / 1e3
-        print(json.dumps({"t48": t48, "ms": round(t * 1e3, 4), "TFLOPs": round(fl / t / 1e12, 2),
+        print(json.dumps({"t48": t48, "share_ab": share, "ms": round(t * 1e3, 4),
+                          "TFLOPs": round(fl / t / 1e12, 2),
                           "rel_err_vs_einsum": err}), flush=True)
     sb.tune_set("gemm.t48", 4)
+    sb.tune_set("gemm.share_ab", 1)
 
 
 if __name__ == "__main__":
