@@ -431,6 +431,7 @@ int sbx_tune_set(const char *key, long long value) {
         else if (k == "bsr.kron_mfma_min_cols") g_bsr_tune.kron_mfma_min_cols = (long)value;
         else if (k == "bsr.kron_lds_pad") g_bsr_tune.kron_lds_pad = (long)value;
         else if (k == "bsr.blk_dma") g_bsr_tune.blk_dma = (int)value;
+        else if (k == "bsr.blk_pack") g_bsr_tune.blk_pack = (int)value;
         else if (k == "bsr.ell9_ilv") g_bsr_tune.ell9_ilv = (int)value;
         else if (k == "bsr.tile_max_cols") g_bsr_tune.tile_max_cols = (long)value;
         else if (k == "bsr.tile_rows") g_bsr_tune.tile_rows = (int)value;
@@ -475,6 +476,7 @@ int sbx_tune_get(const char *key, long long *value) {
         else if (k == "bsr.kron_mfma") *value = g_bsr_tune.kron_mfma;
         else if (k == "bsr.kron_mfma_min_cols") *value = g_bsr_tune.kron_mfma_min_cols;
         else if (k == "bsr.blk_dma") *value = g_bsr_tune.blk_dma;
+        else if (k == "bsr.blk_pack") *value = g_bsr_tune.blk_pack;
         else if (k == "bsr.last_kernel") *value = g_bsr_tune.last;
         else if (k == "bsr.ell9_ilv") *value = g_bsr_tune.ell9_ilv;
         else if (k == "bsr.tile_max_cols") *value = g_bsr_tune.tile_max_cols;

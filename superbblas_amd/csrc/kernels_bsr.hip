@@ -654,7 +654,12 @@ void launch_bsr_mfma_pf(const BsrArgs &a, bool yrow, bool xrow, hipStream_t s) {
 // (no VGPR round trip), PD blocks ahead in a ring of PD + 1 slots; the MFMA fragments are read
 // from the slot as in the register-staged kernel.  Both blocks are contiguous runs (row-major x,
 // ldx == ncols <= 16), lane-linear in LDS.
-template <typename R, bool CPLX, int BI, int BD, bool YROW, int NNZ, int PD, bool M3>
+// PK > 0 (packed slots): the value block and the x block are one run of the slot (x right after
+// the values, no 1-KB rounding of each), moved by PK global_load_lds_dwordx4 instructions whose
+// lanes address either array (a buffer load takes one array per instruction) -- 2304 instead of
+// 4096 bytes per complex<float> slot at 12 rhs, 4608 instead of 6144 for complex<double>, so more
+// waves (and more bytes in flight) fit a CU's LDS
+template <typename R, bool CPLX, int BI, int BD, bool YROW, int NNZ, int PD, bool M3, int PK = 0>
 __global__ void __launch_bounds__(256) bsr_mfma_dma_kernel(const BsrArgs p, unsigned v_bytes, unsigned x_bytes) {
     typedef typename BsrMfmaElem<R, CPLX>::type E;
     typedef typename BsrMfma<R>::acc_t acc_t;
@@ -662,13 +667,15 @@ __global__ void __launch_bounds__(256) bsr_mfma_dma_kernel(const BsrArgs p, unsi
     constexpr int KS = BD / 4, ES = (int)sizeof(E);
     constexpr int ABLK = BI * BD, XBLK = BD * 16;        // elements (x: up to 16 cols)
     constexpr int NA = (ABLK * ES + 1023) / 1024, NX = (XBLK * ES + 1023) / 1024; // DMA instructions
-    constexpr int SLOT = (NA + NX) * 1024;               // bytes per ring slot
+    constexpr int NI = PK > 0 ? PK : NA + NX;            // DMA instructions per block
     extern __shared__ __attribute__((aligned(16))) char smem[];
     E *__restrict__ y = (E *)p.y;
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const long i = (long)blockIdx.x * 4 + w;
     if (i >= p.block_rows) return;
     const int nc = (int)p.ncols, xblk = BD * nc;
+    // bytes per ring slot (packed: values then x, 16-byte aligned)
+    const unsigned SLOT = PK > 0 ? (unsigned)(ABLK + xblk) * ES : (unsigned)(NA + NX) * 1024u;
     const long jb = i * NNZ;
     int dj[NNZ];
 #pragma unroll
@@ -678,19 +685,38 @@ __global__ void __launch_bounds__(256) bsr_mfma_dma_kernel(const BsrArgs p, unsi
     const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
         (void *)((const E *)p.v + jb * ABLK), (short)0, NNZ * ABLK * ES, 0x00020000);
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)p.x, (short)0, (int)x_bytes, 0x00020000);
-    const unsigned slot0 = lds_u32(smem) + (unsigned)w * (unsigned)(SLOT * (PD + 1));
+    const unsigned slot0 = lds_u32(smem) + (unsigned)w * (SLOT * (PD + 1));
     auto issue = [&](int k) {
-        const unsigned base = slot0 + (unsigned)((k % (PD + 1)) * SLOT);
-        const unsigned av = (unsigned)(k * ABLK * ES), xv = (unsigned)((long)(dj[k] < 0 ? 0 : dj[k]) * nc) * ES;
+        const unsigned base = slot0 + (unsigned)(k % (PD + 1)) * SLOT;
+        if constexpr (PK > 0) {
+            const char *vrow = (const char *)((const E *)p.v + (jb + k) * ABLK);
+            // a skipped block (column -1) reads its own values again (not used)
+            const char *xrow = dj[k] < 0 ? vrow : (const char *)((const E *)p.x + (long)dj[k] * nc);
 #pragma unroll
-        for (int q = 0; q < NA; ++q) {
-            const unsigned g = (unsigned)(lane + 64 * q) * 16u;
-            dma16(rv, g < (unsigned)(ABLK * ES) ? av + g : 0x80000000u, base + (unsigned)q * 1024u);
-        }
+            for (int q = 0; q < PK; ++q) {
+                const unsigned g = (unsigned)(lane + 64 * q) * 16u;
+                if (g < SLOT) {
+                    const char *src = g < (unsigned)(ABLK * ES) ? vrow + g : xrow + (g - ABLK * ES);
+                    asm volatile("s_mov_b32 m0, %1\n\t"
+                                 "s_nop 0\n\t"
+                                 "global_load_lds_dwordx4 %0, off"
+                                 :
+                                 : "v"(src), "s"(__builtin_amdgcn_readfirstlane(base + (unsigned)q * 1024u))
+                                 : "memory", "m0");
+                }
+            }
+        } else {
+            const unsigned av = (unsigned)(k * ABLK * ES), xv = (unsigned)((long)(dj[k] < 0 ? 0 : dj[k]) * nc) * ES;
 #pragma unroll
-        for (int q = 0; q < NX; ++q) {
-            const unsigned g = (unsigned)(lane + 64 * q) * 16u;
-            dma16(rx, g < (unsigned)(xblk * ES) ? xv + g : 0x80000000u, base + (unsigned)(NA + q) * 1024u);
+            for (int q = 0; q < NA; ++q) {
+                const unsigned g = (unsigned)(lane + 64 * q) * 16u;
+                dma16(rv, g < (unsigned)(ABLK * ES) ? av + g : 0x80000000u, base + (unsigned)q * 1024u);
+            }
+#pragma unroll
+            for (int q = 0; q < NX; ++q) {
+                const unsigned g = (unsigned)(lane + 64 * q) * 16u;
+                dma16(rx, g < (unsigned)(xblk * ES) ? xv + g : 0x80000000u, base + (unsigned)(NA + q) * 1024u);
+            }
         }
     };
     const int ar = lane & 15, kq = lane >> 4;
@@ -704,19 +730,19 @@ __global__ void __launch_bounds__(256) bsr_mfma_dma_kernel(const BsrArgs p, unsi
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (k + PD < NNZ) {
             issue(k + PD);
-            // block k landed: at most the NA + NX instructions of each later block in flight
-            if constexpr (PD == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NA + NX) : "memory");
-            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (NA + NX)) : "memory");
+            // block k landed: at most the NI instructions of each later block in flight
+            if constexpr (PD == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NI) : "memory");
         } else if (k + PD == NNZ) {
             // no block issued this iteration: PD - 1 blocks may stay in flight
             if constexpr (PD == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NA + NX) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         if (dj[k] < 0) continue;
         const E *sa = (const E *)(smem + (slot0 - lds_u32(smem)) + (k % (PD + 1)) * SLOT);
-        const E *sx = sa + NA * 1024 / ES;
+        const E *sx = sa + (PK > 0 ? ABLK : NA * 1024 / ES);
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
             const int e = ks * 4 + kq;
@@ -764,13 +790,27 @@ bool launch_bsr_mfma_dma(const BsrArgs &a, bool yrow, hipStream_t s) {
     if (a.x_rows <= 0 || x_bytes >= (1L << 31)) return false;
     const long blocks = (a.block_rows + 3) / 4;
     if (blocks >= (1L << 31)) return false;
-    const size_t lds = (size_t)4 * (NA + NX) * 1024 * (PD + 1);
-    KernelTimer timer("bsr", s);
+    // packed slots (values then x in one run): the DMA instruction count of a block
     const bool m3 = CPLX && g_gemm_tune.m3 > 0;
+    const long slot_packed = (long)(BI * BD + BD * a.ncols) * ES;
+    // default for 8-byte elements only (warm round robin, profiles/r02c_blk_pack.txt: the chain's
+    // complex<float> operator 719 -> 693 us; complex<double> 327 -> 336 us); bsr.blk_pack 2 = always
+    const bool want = g_bsr_tune.blk_pack > 1 || (g_bsr_tune.blk_pack == 1 && ES == 8);
+    const int pk = want && !m3 ? (int)((slot_packed + 1023) / 1024) : 0;
+    // (16-byte aligned pieces: the x blocks of an nc-column row and both arrays)
+    const bool packed = pk == (CPLX && ES == 16 ? 5 : 3) && a.ncols >= 1 && a.ncols <= 16 &&
+                        (BD * a.ncols * ES) % 16 == 0 && ((size_t)a.x & 15) == 0 &&
+                        ((size_t)a.v & 15) == 0;
+    const size_t lds = packed ? (size_t)4 * slot_packed * (PD + 1) : (size_t)4 * (NA + NX) * 1024 * (PD + 1);
+    KernelTimer timer("bsr", s);
     auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), lds, s, a, (unsigned)v_bytes, (unsigned)x_bytes);
     };
-    if (yrow && m3) go(bsr_mfma_dma_kernel<R, CPLX, BI, BD, true, NNZ, PD, true>);
+    if (packed && !m3) {
+        constexpr int PKN = CPLX && ES == 16 ? 5 : 3;
+        if (yrow) go(bsr_mfma_dma_kernel<R, CPLX, BI, BD, true, NNZ, PD, false, PKN>);
+        else go(bsr_mfma_dma_kernel<R, CPLX, BI, BD, false, NNZ, PD, false, PKN>);
+    } else if (yrow && m3) go(bsr_mfma_dma_kernel<R, CPLX, BI, BD, true, NNZ, PD, true>);
     else if (yrow) go(bsr_mfma_dma_kernel<R, CPLX, BI, BD, true, NNZ, PD, false>);
     else if (m3) go(bsr_mfma_dma_kernel<R, CPLX, BI, BD, false, NNZ, PD, true>);
     else go(bsr_mfma_dma_kernel<R, CPLX, BI, BD, false, NNZ, PD, false>);

@@ -256,6 +256,8 @@ struct BsrTune {
     long long probe = 0;    ///< tools only: device buffer for per-workgroup time stamps
     int blk_dma = -1; ///< 12x12 (block-staged) operators: blocks staged by LDS-DMA, 1 or 2 blocks ahead
                       ///< (0 = registers, -1 = the library's choice: 1)
+    int blk_pack = 1; ///< ... the value and x blocks packed in one run of the LDS slot: 1 = for 8-byte elements,
+                      ///< 2 = always, 0 = never (1-KB rounded each)
     int kron_mfma = 1;          ///< Kronecker 3x3 (color) x 4x4 (spin) complex<double>: spin products on the
                                 ///< matrix cores (bsr_kron_mfma_kernel) ...
     long kron_mfma_min_cols = 8; ///< ... from this many rhs columns

@@ -49,13 +49,18 @@ def main():
         es = x.element_size()
         by = es * (9 * 144 * V + 2 * 12 * V * ncols) + 4.0 * (9 * V + V + 1)
         ref = None
-        modes = [int(m) for m in os.environ.get("MODES", "0,1,2").split(",")]
+        # mode 10 + d: blocks staged d ahead with packed slots (bsr.blk_pack 1); d: 1-KB-rounded
+        modes = [int(m) for m in os.environ.get("MODES", "0,1,2,11").split(",")]
+
+        def set_mode(mode):
+            sb.tune_set("bsr.blk_dma", mode % 10)
+            sb.tune_set("bsr.blk_pack", 2 if mode >= 10 else 0)
 
         def run():
             sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", px, "pXYZTSCn", [0] * 8, dimx, dimx, [x],
                           0.0, px, "pxyztscn", [0] * 8, dimx, dimx, "p", [y])
         # clocks up first (~0.5 s of the kernel), then the modes round-robin, min and median
-        sb.tune_set("bsr.blk_dma", modes[0])
+        set_mode(modes[0])
         t0 = time.time()
         while time.time() - t0 < 0.5:
             run()
@@ -64,7 +69,7 @@ def main():
         same = {}
         for _ in range(int(os.environ.get("ROUNDS", "4"))):
             for mode in modes:
-                sb.tune_set("bsr.blk_dma", mode)
+                set_mode(mode)
                 run()
                 torch.cuda.synchronize()
                 if ref is None:
@@ -88,6 +93,7 @@ def main():
                               "GBps": round(by / t / 1e9, 1), "frac_hbm": round(by / t / 8e12, 4),
                               "same_as_first": same[mode]}), flush=True)
         sb.tune_set("bsr.blk_dma", -1)
+        sb.tune_set("bsr.blk_pack", 1)
         op.destroy()
         del x, y, vals, ref
 
