@@ -108,9 +108,13 @@ int sbx_timings_get(const char *name, double *ms, long long *calls);
 int sbx_timings_report(char *buf, int len);
 
 /* ---- tuning hook (no reference counterpart) ----
-   Override a kernel-shape choice of the library for tuning runs; value 0 restores the default.
-   Keys: "copy.budget", "copy.run", "copy.kernel", "copy.nt", "bsr.variant", "gemm.m3",
-   "gemm.splits", "copy.max_elems", "gemm.max_bytes". */
+   Override a kernel-shape choice of the library for tuning / comparison runs.  The defaults are
+   the measured winners; read a key with sbx_tune_get before changing it to
+   restore it afterwards.  Keys include "gemm.m3", "gemm.splits", "gemm.max_bytes", "gemm.t48",
+   "gemm.share_ab", "copy.kernel", "copy.nt", "copy.budget", "copy.run", "copy.max_elems",
+   "copy.pair", "copy.order", "bsr.variant", "bsr.blk_dma", "bsr.blk_pack", "bsr.split_cw",
+   "bsr.split_jb", "bsr.split_ovl", "bsr.split_ilv"; read-backs "bsr.last_kernel",
+   "copy.last_pair".  Unknown keys fail with an error. */
 int sbx_tune_set(const char *key, long long value);
 int sbx_tune_get(const char *key, long long *value);
 

@@ -824,16 +824,19 @@ void launch_tiled(const GemmKArgs &p, int device, hipStream_t stream) {
     } else {
         // small outputs (33..48 rows and columns, e.g. the chain's TSnsN contraction: m = n = 4 x
         // 12): 48x48 tiles of three 16x48 wave tiles, no MFMA rows or columns of padding (64x64
-        // tiles use 56 % of each dimension); split-K to ~2048 workgroups.  The chain's complex<float>
-        // contraction (k = 12 288, batch 64): 0.302 -> 0.197 ms (tools/chain_contraction.py,
-        // profiles/r02_chain_contraction.txt; 16x48 / 48x16 wave tiles, 16- / 32-deep slabs and
-        // 1024 / 2048 workgroups: 0.197-0.218 ms)
+        // tiles use 56 % of each dimension); split-K to ~1536 workgroups (six per CU: one round).
+        // The chain's complex<float> contraction (k = 12 288, batch 64): 0.302 -> 0.197 ms
+        // (tools/chain_contraction.py, profiles/r02_chain_contraction.txt; 16x48 / 48x16 wave
+        // tiles, 16- / 32-deep slabs and 1024 / 2048 workgroups: 0.197-0.218 ms); with one slab
+        // image for its two (identical) operands, 512 / 768 / 1024 / 1536 / 2048 / 3072 / 4096
+        // workgroups: 0.194 / 0.186 / 0.170 / 0.164 / 0.170 / 0.175 / 0.188 ms (warm,
+        // profiles/r02c_chain_splits.txt)
         const int t48 = g_gemm_tune.t48;
         if (t48 > 0 && p.m > 32 && p.m <= 48 && p.n > 32 && p.n <= 48) {
             if (t48 == 1) return launch_dma_cfg<R, CPLX, AK, BK, 48, 48, 16, 3, 1>(p, device, stream, 0, 1024);
             if (t48 == 2) return launch_dma_cfg<R, CPLX, AK, BK, 48, 48, 16, 1, 3>(p, device, stream, 0, 1024);
             if (t48 == 3) return launch_dma_cfg<R, CPLX, AK, BK, 48, 48, 32, 3, 1>(p, device, stream, 0, 1024);
-            if (t48 == 4) return launch_dma_cfg<R, CPLX, AK, BK, 48, 48, 16, 3, 1>(p, device, stream, 0, 2048);
+            if (t48 == 4) return launch_dma_cfg<R, CPLX, AK, BK, 48, 48, 16, 3, 1>(p, device, stream, 0, 1536);
         }
         // 8-byte and 4-byte elements: 32-deep slabs (fewer barriers per MFMA; measured against
         // 16 and 64 on the lattice shape: double 50.5, complex<float> 116, float 107 TFLOP/s)

@@ -27,9 +27,12 @@ def main():
     combos = [(int(v), 1) for v in os.environ.get("T48", "0,1,2,3,4").split(",")]
     if os.environ.get("SHARE"):  # one slab image for both operands (the same memory) on / off
         combos = [(4, int(v)) for v in os.environ["SHARE"].split(",")] * 2
-    for t48, share in combos:
+    splits = [int(v) for v in os.environ.get("SPLITS", "0").split(",")]  # 0: the library's choice
+    combos = [(t, sh, sp) for t, sh in combos for sp in splits]
+    for t48, share, nsplit in combos:
         sb.tune_set("gemm.t48", t48)
         sb.tune_set("gemm.share_ab", share)
+        sb.tune_set("gemm.splits", nsplit)
 
         def f():
             sb.contraction(1.0, p_x, [0] * 8, dx, dx, "pXYZTSCn", True, [y], p_x, [0] * 8, dx, dx,
@@ -44,11 +47,12 @@ def main():
         e.record()
         torch.cuda.synchronize()
         t = s.elapsed_time(e) / 10 / 1e3
-        print(json.dumps({"t48": t48, "share_ab": share, "ms": round(t * 1e3, 4),
+        print(json.dumps({"t48": t48, "share_ab": share, "splits": nsplit, "ms": round(t * 1e3, 4),
                           "TFLOPs": round(fl / t / 1e12, 2),
                           "rel_err_vs_einsum": err}), flush=True)
     sb.tune_set("gemm.t48", 4)
     sb.tune_set("gemm.share_ab", 1)
+    sb.tune_set("gemm.splits", 0)
 
 
 if __name__ == "__main__":
