@@ -430,6 +430,7 @@ int sbx_tune_set(const char *key, long long value) {
         else if (k == "bsr.kron_mfma") g_bsr_tune.kron_mfma = (int)value;
         else if (k == "bsr.kron_mfma_min_cols") g_bsr_tune.kron_mfma_min_cols = (long)value;
         else if (k == "bsr.kron_lds_pad") g_bsr_tune.kron_lds_pad = (long)value;
+        else if (k == "bsr.kron_pack") g_bsr_tune.kron_pack = (int)value;
         else if (k == "bsr.blk_dma") g_bsr_tune.blk_dma = (int)value;
         else if (k == "bsr.blk_pack") g_bsr_tune.blk_pack = (int)value;
         else if (k == "bsr.ell9_ilv") g_bsr_tune.ell9_ilv = (int)value;

@@ -374,6 +374,111 @@ __global__ void __launch_bounds__(256) bsr_kron_mfma_kernel(const KronArgs p, in
     }
 }
 
+// The same kernel for rhs counts below 16 that divide 16 W (W <= 4 waves): a wave's 16 column
+// slots are (row, column) pairs of the workgroup's RW = 16 W / n consecutive block rows, so no lane
+// idles (at n = 12 one wave per row left 4 of 16 slots empty: 25 % of the VALU and MFMA work).
+// The row's block columns and color blocks become per-lane (LDS reads of the staged color blocks,
+// block columns loaded per lane); the spin matrices stay the MFMA's A operand.
+template <int NNZ>
+__global__ void __launch_bounds__(256) bsr_kron_mfma_packed_kernel(const KronArgs p, int rw) {
+    typedef double2 E;
+    const E *__restrict__ x = (const E *)p.x;
+    E *__restrict__ y = (E *)p.y;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int bid = blockIdx.x, nwg = gridDim.x;
+    const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int cnt = xcd < r8 ? q8 + 1 : q8, qx = bid >> 3, npart = cnt / 2;
+    const int loc = (npart > 0 && qx < npart * 2) ? (qx % 2) * npart + qx / 2 : qx;
+    const long wgi = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+    const long r0 = wgi * rw;
+    const int nrows = (int)min((long)rw, p.block_rows - r0);
+    const long n = p.ncols;
+    const int b = lane >> 4, q = lane & 15;
+    const int slot = w * 16 + q, rl = slot / (int)n;
+    const long col = slot - (long)rl * n;
+    const bool live = rl < nrows;
+    const int rlc = live ? rl : nrows - 1;
+    const long r = r0 + rlc;
+    // the color blocks of the workgroup's rows (one contiguous run) into LDS by one DMA pass
+    // (dynamic LDS: rw rows of NNZ 3x3 blocks)
+    extern __shared__ __attribute__((aligned(16))) char smem_k[];
+    E *us = (E *)smem_k;
+    {
+        const int nu = nrows * NNZ * 9;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)p.v, (short)0, (int)(p.block_rows * NNZ * 9 * 16), 0x00020000);
+        const unsigned base = (unsigned)(size_t)(const __attribute__((address_space(3))) void *)smem_k +
+                              (unsigned)w * 1024u;
+        const int nth = (int)blockDim.x;
+        for (int u = 0; u * nth < nu; ++u) {
+            const int e = u * nth + (int)threadIdx.x;
+            const unsigned off = e < nu ? (unsigned)(r0 * NNZ * 9 + e) * 16u : 0x80000000u;
+            asm volatile("s_mov_b32 m0, %1\n\t"
+                         "s_nop 0\n\t"
+                         "buffer_load_dwordx4 %0, %2, 0 offen lds"
+                         :
+                         : "v"(off), "s"(__builtin_amdgcn_readfirstlane(base + (unsigned)(u * nth) * 16u)),
+                           "s"(rs)
+                         : "memory", "m0");
+        }
+    }
+    // the lane's row: block columns (per lane), then the first neighbour's x
+    int jrow[NNZ];
+#pragma unroll
+    for (int mu = 0; mu < NNZ; ++mu) jrow[mu] = p.jj[r * NNZ + mu];
+    const int ka = lane & 3, kk = lane >> 4;
+    const E *kron = (const E *)p.kron;
+    const int kidx = p.block_im_fast ? ka + kk * 4 : ka * 4 + kk;
+    const long xsite = 3 * n * 4;
+    auto load_x = [&](int J, E *xv) {
+        const E *xs = x + (long)J * xsite + col * 4 + b;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) xv[d] = xs[d * n * 4];
+    };
+    E xa[3], xb[3];
+    load_x(jrow[0], xa);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const E *urow_s = us + rlc * NNZ * 9;
+    double accR[3] = {0, 0, 0}, accI[3] = {0, 0, 0};
+#pragma unroll
+    for (int mu = 0; mu < NNZ; ++mu) {
+        if (mu + 1 < NNZ) load_x(jrow[mu + 1], xb);
+        const E K = kron[mu * 16 + kidx];
+        E t[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            t[i] = Ops<E>::zero();
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                const long ui = mu * 9 + (p.block_im_fast ? i + d * 3 : i * 3 + d);
+                t[i] = Ops<E>::fma(urow_s[ui], xa[d], t[i]);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            accR[i] = __builtin_amdgcn_mfma_f64_4x4x4f64(K.x, t[i].x, accR[i], 0, 0, 0);
+            accR[i] = __builtin_amdgcn_mfma_f64_4x4x4f64(-K.y, t[i].y, accR[i], 0, 0, 0);
+            accI[i] = __builtin_amdgcn_mfma_f64_4x4x4f64(K.x, t[i].y, accI[i], 0, 0, 0);
+            accI[i] = __builtin_amdgcn_mfma_f64_4x4x4f64(K.y, t[i].x, accI[i], 0, 0, 0);
+        }
+        if (mu + 1 < NNZ) {
+#pragma unroll
+            for (int d = 0; d < 3; ++d) xa[d] = xb[d];
+        }
+    }
+    if (!live) return;
+    // C lane 16 a + q: spin a of slot q
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        E *yp = y + ((r * 3 + i) * n + col) * 4 + b;
+        E o = Ops<E>::scale(E{accR[i], accI[i]}, p.alpha_re, p.alpha_im);
+        if (p.add) o = Ops<E>::add(o, *yp);
+        *yp = o;
+    }
+}
+
 constexpr long KRON_LDS_BYTES = 64 * 1024;
 
 template <typename E> void launch_kron_typed(const KronArgs &a, hipStream_t s) {
@@ -382,6 +487,24 @@ template <typename E> void launch_kron_typed(const KronArgs &a, hipStream_t s) {
     if constexpr (std::is_same<E, double2>::value) {
         if (g_bsr_tune.kron_mfma && a.bi == 3 && a.bd == 3 && a.ki == 4 && a.kd == 4 && a.nnz == 9 &&
             a.ncols >= g_bsr_tune.kron_mfma_min_cols && a.block_rows * 81L * 16 < (1L << 31)) {
+            // packed slots: W waves of 16 (row, column) slots hold RW = 16 W / n whole rows
+            int wpk = 0;
+            for (int wv = 4; wv >= 1 && g_bsr_tune.kron_pack; --wv)
+                if (a.ncols < 16 && (16 * wv) % a.ncols == 0 && 16 * wv / a.ncols <= 32) {
+                    wpk = wv;
+                    break;
+                }
+            if (wpk > 0) {
+                const int rw = (int)(16 * wpk / a.ncols);
+                const long blocks = (a.block_rows + rw - 1) / rw;
+                if (blocks < (1L << 31)) {
+                    g_bsr_tune.last = 6;
+                    hipLaunchKernelGGL((bsr_kron_mfma_packed_kernel<9>), dim3((unsigned)blocks),
+                                       dim3(64 * wpk), (size_t)rw * 81 * 16, s, a, rw);
+                    SBX_HIP_CHECK(hipGetLastError());
+                    return;
+                }
+            }
             const long ngroups = (a.ncols + 15) / 16;
             const long tasks = a.block_rows * ngroups, blocks = (tasks + 3) / 4;
             if (blocks < (1L << 31)) {

@@ -262,8 +262,10 @@ struct BsrTune {
                                 ///< matrix cores (bsr_kron_mfma_kernel) ...
     long kron_mfma_min_cols = 8; ///< ... from this many rhs columns
     long kron_lds_pad = 0;       ///< tools: LDS bytes per workgroup of that kernel (caps its residency)
+    int kron_pack = 1;           ///< ... below 16 rhs columns: a wave's 16 column slots span several rows (0 = off)
     int last = 0; ///< read-back ("bsr.last_kernel"): the 9-point 3x3 form of the last launch -- 1 one thread
-                  ///< per block, 2 split rows, 3 row chunks, 4 lattice tiles, 5 Kronecker on MFMA, 0 another kernel
+                  ///< per block, 2 split rows, 3 row chunks, 4 lattice tiles, 5 Kronecker on MFMA, 6 the same
+                  ///< with packed column slots, 0 another kernel
 };
 extern BsrTune g_bsr_tune;
 

@@ -170,8 +170,9 @@ def test_kron_errors(gpu):
 @pytest.mark.parametrize("bif,sparse", [(False, False), (True, True)])
 def test_kron_mfma_kernel(gpu, ncols, bif, sparse):
     """complex<double> 3x3 x 4x4 from 8 rhs columns: the spin products on the matrix cores
-    (bsr_kron_mfma_kernel; 16-column groups, partial last group), complex alpha, beta, powers;
-    integer data, exact; and the same results with the kernel switched off."""
+    (bsr_kron_mfma_kernel; 16-column groups, partial last group; bsr_kron_mfma_packed_kernel at 8
+    and 12 columns: a wave's 16 column slots over several rows), complex alpha, beta, powers;
+    integer data, exact; and the same results with either switched off."""
     import torch
     import superbblas_amd as sb
     L, spin, color, power = 4, 4, 3, 2
@@ -193,8 +194,10 @@ def test_kron_mfma_kernel(gpu, ncols, bif, sparse):
     dimy = [power] + dimx[1:]
     outs = []
     try:
-        for on in (1, 0):
+        # packed column slots (8 and 12 columns: several rows per wave), one row per wave, no MFMA
+        for on, pack in ((1, 1), (1, 0), (0, 1)):
             sb.tune_set("bsr.kron_mfma", on)
+            sb.tune_set("bsr.kron_pack", pack)
             ty = torch.from_numpy(y0.copy()).to(gpu)
             sb.bsr_krylov(alpha, op, "xyztsc", "XYZTSC", [([0] * 8, dimx)], "pXYZTCnS", [0] * 8,
                           dimx, dimx, [torch.from_numpy(x).to(gpu)], beta, [([0] * 8, dimy)],
@@ -203,7 +206,8 @@ def test_kron_mfma_kernel(gpu, ncols, bif, sparse):
             outs.append((sb.tune_get("bsr.last_kernel"), ty.cpu().numpy()))
     finally:
         sb.tune_set("bsr.kron_mfma", 1)
+        sb.tune_set("bsr.kron_pack", 1)
         op.destroy()
-    assert outs[0][0] == 5 and outs[1][0] != 5
-    assert np.array_equal(outs[0][1], ref)
-    assert np.array_equal(outs[1][1], ref)
+    assert outs[0][0] == (6 if ncols in (8, 12) else 5) and outs[1][0] == 5 and outs[2][0] not in (5, 6)
+    for form, out in outs:
+        assert np.array_equal(out, ref), form

@@ -99,6 +99,17 @@ def main():
                 print(json.dumps(r), flush=True)
         sb.tune_set("bsr.kron_lds_pad", 0)
         return
+    if os.environ.get("KRON_PACKS"):  # packed column slots of the MFMA kernel on / off, round robin
+        for n in [int(v) for v in os.environ.get("KRON_NS", "8,12").split(",")]:
+            for rnd in range(2):
+                for pk in [int(v) for v in os.environ["KRON_PACKS"].split(",")]:
+                    sb.tune_set("bsr.kron_pack", pk)
+                    r = run(L, n, dev)
+                    r.update({"kron_pack": pk, "round": rnd,
+                              "kernel_form": sb.tune_get("bsr.last_kernel")})
+                    print(json.dumps(r), flush=True)
+        sb.tune_set("bsr.kron_pack", 1)
+        return
     if only:
         dt, n = only.split(":")
         print(json.dumps(run(L, int(n), dev, getattr(torch, dt), False)), flush=True)
