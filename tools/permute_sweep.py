@@ -56,7 +56,8 @@ def main():
     print(json.dumps({"case": "torch contiguous copy x64 slices", "GBps": round(by / t / 1e9, 1),
                       "us_per_slice": round(t / n * 1e6, 2)}), flush=True)
     ref = None
-    configs = [dict(), dict(budget=1536), dict(budget=1024), dict(budget=512), dict(run=24),
+    configs = [dict(), dict(budget=1536), dict(budget=1024), dict(budget=512), dict(budget=384),
+               dict(budget=256), dict(run=24), dict(run=12, budget=384),
                dict(run=96), dict(run=96, budget=1536), dict(kernel=1), dict(nt=-1)]
     for cfg in configs:
         for k in ("budget", "run", "kernel", "nt"):
