@@ -29,6 +29,7 @@ CONFIGS = {
     "cw2_jb3_ovl_nt512": {"bsr.split_cw": 2, "bsr.split_jb": 3, "bsr.split_ovl": 1, "bsr.split_nt": 512},
     "cw1_jb3_ovl_nt512": {"bsr.split_cw": 1, "bsr.split_jb": 3, "bsr.split_ovl": 1, "bsr.split_nt": 512},
     "cw2_jb1_ovl": {"bsr.split_cw": 2, "bsr.split_jb": 1, "bsr.split_ovl": 1},
+    "ilv1": {"bsr.split_ilv": 1}, "ilv4": {"bsr.split_ilv": 4}, "ilv8": {"bsr.split_ilv": 8},
     "rw10": {"bsr.split_rw": 10}, "rw11": {"bsr.split_rw": 11}, "rw12": {"bsr.split_rw": 12},
     "rw13": {"bsr.split_rw": 13}, "rw14": {"bsr.split_rw": 14},
     "default": {},
