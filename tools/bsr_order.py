@@ -43,6 +43,22 @@ def sites_in_order(L, order):
         inner = ((nat[:, 0] % 4 * 4 + nat[:, 1] % 4) * 4 + nat[:, 2] % 4) * 4 + nat[:, 3] % 4
         key = (blk.astype(np.int64) << 40) | (tkey << 8) | inner
         return nat[np.argsort(key, kind="stable")]
+    if order.startswith("sim"):
+        # "sim16-4-4-4": each XCD's rows (one eighth, consecutive) = one region of full c0 x halves
+        # of c1, c2, c3, swept in blocks of 16 x 4 x 4 x 4 (the L2 LRU model's best order);
+        # run with the XCD interleave off (bsr.ell9_ilv / bsr.split_ilv 1)
+        import itertools
+        bs = [int(v) for v in order[3:].split("-")]
+        out = []
+        h = L // 2
+        for k in range(8):
+            hh = [(k >> 2) & 1, (k >> 1) & 1, k & 1]
+            lo, ext = [0, hh[0] * h, hh[1] * h, hh[2] * h], [L, h, h, h]
+            nb = [ext[d] // bs[d] for d in range(4)]
+            for B in itertools.product(*[range(v) for v in nb]):
+                for a in itertools.product(*[range(v) for v in bs]):
+                    out.append([lo[d] + B[d] * bs[d] + a[d] for d in range(4)])
+        return np.array(out)
     h = L // 2
     out = []
     for bx in range(2):
@@ -76,7 +92,12 @@ def main():
         op = sb.create_bsr(full, dim, full, dim, [1, 1, 1, 1, 1, 3], [1, 1, 1, 1, 1, 3], False,
                            [torch.full((V,), 9, dtype=torch.int32, device=dev)],
                            [torch.from_numpy(jj.reshape(-1)).to(dev)], [vals])
-        for ncols, split in [(1, 0), (12, 0), (64, 0)] + [(64, c) for c in (32, 16)] + [(12, 6)]:
+        ilv = 1 if order.startswith("sim") else 2
+        sb.tune_set("bsr.ell9_ilv", ilv)
+        sb.tune_set("bsr.split_ilv", ilv)
+        cases = [(12, 0), (64, 0)] if os.environ.get("ORDER_QUICK") else \
+            [(1, 0), (12, 0), (64, 0)] + [(64, c) for c in (32, 16)] + [(12, 6)]
+        for ncols, split in cases:
             sb.tune_set("bsr.colsplit", split)
             dimx = [1, L, L, L, L, 1, 3, ncols]
             x = torch.randn(V * 3 * ncols, dtype=torch.complex128, device=dev)
@@ -99,11 +120,13 @@ def main():
             sb.timings_filter(None)
             t = ms / 10 / 1e3  # one product = all its column passes
             by = 16.0 * (81 * V + 2 * 3 * V * ncols) + 4.0 * (9 * V + V + 1)
-            print(json.dumps({"order": order, "n": ncols, "colsplit": split,
+            print(json.dumps({"order": order, "ilv": ilv, "n": ncols, "colsplit": split,
                               "kernel_us": round(t * 1e6, 2),
                               "GBps": round(by / t / 1e9, 1),
                               "frac_hbm": round(by / t / 8e12, 4)}), flush=True)
         sb.tune_set("bsr.colsplit", 0)
+        sb.tune_set("bsr.ell9_ilv", 2)
+        sb.tune_set("bsr.split_ilv", 2)
         op.destroy()
 
 
