@@ -270,7 +270,7 @@ __global__ void __launch_bounds__(256) bsr_kron_generic_kernel(const KronArgs p)
 //    an XCD's rows visited as two interleaved halves (its ilv form of the 3x3 kernels).
 // The previous kernel (one thread per (row, column) owning all 12 outputs) ran at 256 VGPRs:
 // 2 waves per SIMD.
-template <int NNZ>
+template <int NNZ, bool kpf = false>
 __global__ void __launch_bounds__(256) bsr_kron_mfma_kernel(const KronArgs p, int ngroups) {
     typedef double2 E;
     const E *__restrict__ x = (const E *)p.x;
@@ -335,10 +335,20 @@ __global__ void __launch_bounds__(256) bsr_kron_mfma_kernel(const KronArgs p, in
     double accR[3] = {0, 0, 0}, accI[3] = {0, 0, 0};
     E xa[3], xb[3];
     load_x(jrow[0], xa);
+    // the spin matrix of neighbour mu + 1 is loaded with its x rows; the compiler barrier keeps
+    // the unrolled loop from hoisting all 9 spin-matrix loads to the top (36 more VGPRs: fewer
+    // waves per SIMD)
+    E Kc = kron[kidx];
 #pragma unroll
     for (int mu = 0; mu < NNZ; ++mu) {
-        if (mu + 1 < NNZ) load_x(jrow[mu + 1], xb);
-        const E K = kron[mu * 16 + kidx];
+        if constexpr (kpf) asm volatile("" ::: "memory");
+        E Kn = Kc;
+        if (mu + 1 < NNZ) {
+            load_x(jrow[mu + 1], xb);
+            if constexpr (kpf) Kn = kron[(mu + 1) * 16 + kidx];
+        }
+        const E K = kpf ? Kc : kron[mu * 16 + kidx];
+        Kc = Kn;
         // color: T(i) = sum_d U(i, d) x(d)
         E t[3];
 #pragma unroll
@@ -379,7 +389,7 @@ __global__ void __launch_bounds__(256) bsr_kron_mfma_kernel(const KronArgs p, in
 // idles (at n = 12 one wave per row left 4 of 16 slots empty: 25 % of the VALU and MFMA work).
 // The row's block columns and color blocks become per-lane (LDS reads of the staged color blocks,
 // block columns loaded per lane); the spin matrices stay the MFMA's A operand.
-template <int NNZ>
+template <int NNZ, bool kpf = false>
 __global__ void __launch_bounds__(256) bsr_kron_mfma_packed_kernel(const KronArgs p, int rw) {
     typedef double2 E;
     const E *__restrict__ x = (const E *)p.x;
@@ -442,10 +452,20 @@ __global__ void __launch_bounds__(256) bsr_kron_mfma_packed_kernel(const KronArg
     __syncthreads();
     const E *urow_s = us + rlc * NNZ * 9;
     double accR[3] = {0, 0, 0}, accI[3] = {0, 0, 0};
+    // the spin matrix of neighbour mu + 1 is loaded with its x rows; the compiler barrier keeps
+    // the unrolled loop from hoisting all 9 spin-matrix loads to the top (36 more VGPRs: fewer
+    // waves per SIMD)
+    E Kc = kron[kidx];
 #pragma unroll
     for (int mu = 0; mu < NNZ; ++mu) {
-        if (mu + 1 < NNZ) load_x(jrow[mu + 1], xb);
-        const E K = kron[mu * 16 + kidx];
+        if constexpr (kpf) asm volatile("" ::: "memory");
+        E Kn = Kc;
+        if (mu + 1 < NNZ) {
+            load_x(jrow[mu + 1], xb);
+            if constexpr (kpf) Kn = kron[(mu + 1) * 16 + kidx];
+        }
+        const E K = kpf ? Kc : kron[mu * 16 + kidx];
+        Kc = Kn;
         E t[3];
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
@@ -499,7 +519,10 @@ template <typename E> void launch_kron_typed(const KronArgs &a, hipStream_t s) {
                 const long blocks = (a.block_rows + rw - 1) / rw;
                 if (blocks < (1L << 31)) {
                     g_bsr_tune.last = 6;
-                    hipLaunchKernelGGL((bsr_kron_mfma_packed_kernel<9>), dim3((unsigned)blocks),
+                    // spin matrices one neighbour ahead: n = 8 / 12 104 / 166 -> 102 / 163 us
+                    // (the one-row-per-wave kernel: 214 -> 221 us at n = 16, so not there;
+                    // profiles/r02c_kron_kpf.txt)
+                    hipLaunchKernelGGL((bsr_kron_mfma_packed_kernel<9, true>), dim3((unsigned)blocks),
                                        dim3(64 * wpk), (size_t)rw * 81 * 16, s, a, rw);
                     SBX_HIP_CHECK(hipGetLastError());
                     return;
@@ -511,8 +534,8 @@ template <typename E> void launch_kron_typed(const KronArgs &a, hipStream_t s) {
                 g_bsr_tune.last = 5;
                 // tools: dynamic LDS that caps the resident workgroups per CU (L2 footprint)
                 const size_t pad = (size_t)std::max(0L, g_bsr_tune.kron_lds_pad);
-                hipLaunchKernelGGL((bsr_kron_mfma_kernel<9>), dim3((unsigned)blocks), dim3(256), pad, s,
-                                   a, (int)ngroups);
+                hipLaunchKernelGGL((bsr_kron_mfma_kernel<9, false>), dim3((unsigned)blocks), dim3(256), pad,
+                                   s, a, (int)ngroups);
                 SBX_HIP_CHECK(hipGetLastError());
                 return;
             }
