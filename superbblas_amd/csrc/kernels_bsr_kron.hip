@@ -289,7 +289,8 @@ __global__ void __launch_bounds__(256) bsr_kron_mfma_kernel(const KronArgs p, in
     const int cg = (int)(task - r * ngroups);
     // the color blocks of the workgroup's rows (rows of a task group are consecutive: one
     // contiguous run) into LDS by one DMA pass, read back as broadcasts
-    __shared__ __attribute__((aligned(16))) E us[4 * NNZ * 9];
+    // (rounded up to whole DMA passes of 256 lanes: the lanes past the run write zeros)
+    __shared__ __attribute__((aligned(16))) E us[(4 * NNZ * 9 + 255) / 256 * 256];
     {
         const long rlo = (wgi * 4) / ngroups, rhi = min((wgi * 4 + 3) / ngroups, p.block_rows - 1);
         const int nu = (int)(rhi - rlo + 1) * NNZ * 9;
@@ -519,11 +520,15 @@ template <typename E> void launch_kron_typed(const KronArgs &a, hipStream_t s) {
                 const long blocks = (a.block_rows + rw - 1) / rw;
                 if (blocks < (1L << 31)) {
                     g_bsr_tune.last = 6;
+                    // LDS: rw rows of 81 color values, rounded up to whole DMA passes of the
+                    // workgroup (the lanes past the run write zeros)
+                    const int nth = 64 * wpk;
+                    const size_t lds_bytes = (size_t)((rw * 81 + nth - 1) / nth * nth) * 16;
                     // spin matrices one neighbour ahead: n = 8 / 12 104 / 166 -> 102 / 163 us
                     // (the one-row-per-wave kernel: 214 -> 221 us at n = 16, so not there;
                     // profiles/r02c_kron_kpf.txt)
                     hipLaunchKernelGGL((bsr_kron_mfma_packed_kernel<9, true>), dim3((unsigned)blocks),
-                                       dim3(64 * wpk), (size_t)rw * 81 * 16, s, a, rw);
+                                       dim3(64 * wpk), lds_bytes, s, a, rw);
                     SBX_HIP_CHECK(hipGetLastError());
                     return;
                 }
