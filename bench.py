@@ -655,9 +655,14 @@ def chain_bench(sb, dev, Ls=16, Lt=64, ncols=12, reps=3):
         sb.contraction(1.0, p_x, [0] * 8, dx, dx, "pXYZTSCn", True, [y], p_x, [0] * 8, dx, dx,
                        "pXYZTsCN", False, [y], 0.0, p_r, [0] * 5, dr, dr, "TSnsN", [vr])
     stages = (stage1, stage2, stage3)
-    for f in stages:
-        f()
-    torch.cuda.synchronize()
+    # steady state first: ~0.1 s of the chain (clocks ramp over the first launches)
+    t_end = time.perf_counter() + 0.1
+    while True:
+        for f in stages:
+            f()
+        torch.cuda.synchronize()
+        if time.perf_counter() >= t_end:
+            break
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
     times = [0.0, 0.0, 0.0]
     for _ in range(reps):
