@@ -57,7 +57,27 @@ def ref_copy(a, o0, d0, o1, d1, from1):
     return out
 
 
+def sweep(spec):
+    """COPY_SWEEP="budget:run,...": tile budget / source-run target on the chain-sized cases"""
+    for item in spec.split(","):
+        budget, run = (int(v) for v in item.split(":"))
+        sb.tune_set("copy.budget", budget)
+        sb.tune_set("copy.run", run)
+        print(json.dumps({"copy.budget": budget, "copy.run": run}))
+        L, n = 16, 64
+        case("redist", "tnsxyzc", [64, 12, 4, 16, 16, 16, 3], "pxyztscn",
+             [1, 16, 16, 16, 64, 4, 3, 12], [0] * 8, torch.complex64)
+        case("chain", "pXYZTSCn", [1, 16, 16, 16, 64, 4, 3, 12], "TSnpXYZC",
+             [64, 4, 12, 1, 16, 16, 16, 3], [0] * 8, torch.complex64)
+        case("big", "xyztnsc", [L, L, L, L, n, 4, 3], "tnsxyzc", [L, n, 4, L, L, L, 3], [0] * 7,
+             torch.complex128)
+    sb.tune_set("copy.budget", 0)
+    sb.tune_set("copy.run", 0)
+
+
 def main():
+    if os.environ.get("COPY_SWEEP"):
+        return sweep(os.environ["COPY_SWEEP"])
     combos = ((0, 0, 0), (0, 0, -1), (0, 0, -2), (1, 0, 0), (0, -1, 0))
     if os.environ.get("COPY_QUICK"):
         combos = combos[:3]
