@@ -248,16 +248,16 @@ def test_copy_fast_path_replay(gpu):
 def test_paired_8byte_transposes(gpu, t0, t1):
     """The tiled kernel's paired (16-byte) accesses for 8-byte elements: the chain's n <-> c <->
     xyz redistribution (source chain first), its contraction-operand reorder, a whole-tensor
-    permute; even and odd rhs counts (odd rows fall back to single accesses), boxes at odd
-    origins (8-byte aligned pointers fall back), alpha and Add (paired reads only)."""
+    permute; even and odd rhs counts (odd tile rows are rounded to even ones), boxes at odd
+    origins (8-byte aligned pointers fall back), alpha and Add (paired reads only), and the
+    single-access form (copy.pair -1) on the same shapes."""
     cases = [("tnsxyzc", "pxyztscn", lambda n: ([4, n, 4, 4, 4, 4, 3], [1, 4, 4, 4, 4, 4, 3, n])),
              ("pXYZTSCn", "TSnpXYZC", lambda n: ([1, 4, 4, 4, 4, 4, 3, n], [4, 4, n, 1, 4, 4, 4, 3])),
              ("xyztnsc", "tnsxyzc", lambda n: ([4, 4, 4, 4, n, 4, 3], [4, n, 4, 4, 4, 4, 3]))]
     import superbblas_amd as sb
     forms = set()
-    for (o0, o1, dims), n, shift, add in itertools.product(cases, (6, 5), (0, 1), (False, True)):
-        if add and np.dtype(t1).kind == "u":
-            continue
+
+    def run(o0, o1, dims, n, shift, add):
         dim0, dim1 = dims(n)
         size0 = list(dim0)
         from0 = [0] * len(dim0)
@@ -278,6 +278,20 @@ def test_paired_8byte_transposes(gpu, t0, t1):
                               add=add)
         forms.add(sb.tune_get("copy.last_pair"))
         assert np.array_equal(out.view(np.uint8), ref.view(np.uint8)), (o0, o1, n, shift, add)
+
+    for (o0, o1, dims), n, shift, add in itertools.product(cases, (6, 5), (0, 1), (False, True)):
+        if add and np.dtype(t1).kind == "u":
+            continue
+        run(o0, o1, dims, n, shift, add)
+    # the single-access form on the same shapes (odd tile rows are rounded to even ones, so the
+    # defaults above may pair every case)
+    prev = sb.tune_get("copy.pair")
+    sb.tune_set("copy.pair", -1)
+    try:
+        for (o0, o1, dims), n in itertools.product(cases, (6, 5)):
+            run(o0, o1, dims, n, 0, False)
+    finally:
+        sb.tune_set("copy.pair", prev)
     # paired reads ran for 8-byte sources, paired writes for 8-byte destinations, and the
     # single-access fallback ran too
     assert 0 in forms, forms
