@@ -52,6 +52,57 @@ def fill(t, seed):
     t.copy_(torch.view_as_complex(r))
 
 
+_M32 = 0xffffffff
+
+
+def _mix32(x):
+    """32-bit integer finaliser (xor-shift-multiply, 'lowbias32') on int64 tensors holding values
+    < 2^32; products wrap in int64, only their low 32 bits are kept."""
+    x = x ^ (x >> 16)
+    x = (x * 0x7feb352d) & _M32
+    x = x ^ (x >> 15)
+    x = (x * 0x846ca68b) & _M32
+    return x ^ (x >> 16)
+
+
+def global_values(g, seed):
+    """val(g): a counter-based complex value in [-1, 1)^2 of the global SlowToFast index g (int64
+    tensor).  The same g gives the same value on every rank, GPU and partition."""
+    s = (seed * 0x9e3779b9) & _M32
+    h = _mix32((g & _M32) ^ _mix32(((g >> 32) + s) & _M32))
+    re = _mix32(h ^ 0x5bd1e995)
+    im = _mix32(h ^ 0x27d4eb2f)
+    sc = 2.0 / 4294967296.0
+    return torch.complex(re.double() * sc - 1, im.double() * sc - 1)
+
+
+def global_fill(t, gdim, frm, size, seed):
+    """Fill t, this rank's component `size` at `frm` (periodic) of the global tensor `gdim`
+    (SlowToFast), with val(global index): every partition of the tensor -- any number of ranks,
+    or one GPU holding it whole -- holds slices of one and the same global tensor (SURVEY §8(c)
+    5.1, distribution-invariant inputs).  Chunked over the slowest dimension."""
+    nd = len(gdim)
+    gstr = [1] * nd
+    for d in range(nd - 2, -1, -1):
+        gstr[d] = gstr[d + 1] * gdim[d + 1]
+    dev = t.device
+    off = torch.zeros(1, dtype=torch.int64, device=dev)
+    for d in range(1, nd):
+        idx = ((frm[d] + torch.arange(size[d], device=dev)) % gdim[d]) * gstr[d]
+        off = (off[:, None] + idx[None, :]).reshape(-1)
+    chunk = off.numel()
+    assert t.numel() == chunk * size[0], (t.numel(), size)
+    for i in range(size[0]):
+        g = off + ((frm[0] + i) % gdim[0]) * gstr[0]
+        t[i * chunk:(i + 1) * chunk] = global_values(g, seed).to(t.dtype)
+
+
+def rel_err(a, b):
+    """Normwise relative difference ||a - b|| / ||b|| (complex, any dtype)."""
+    a, b = a.to(torch.complex128), b.to(torch.complex128)
+    return (torch.linalg.vector_norm(a - b) / torch.linalg.vector_norm(b)).item()
+
+
 def host_cpu():
     """Host cores this process may use (its affinity mask, capped by OMP_NUM_THREADS when the box
     sets one), the machine's logical CPU count and the CPU model."""
@@ -181,6 +232,10 @@ def pmc_traffic(*kernel_substrs):
 
 # lattice grids of configs[3] (x, y, z, t split factors)
 GRIDS = {1: [1, 1, 1, 1], 2: [2, 1, 1, 1], 4: [2, 2, 1, 1], 8: [2, 2, 2, 1]}
+SEED_V0, SEED_V1 = 1, 2
+# N > 1 answers against the same global problem on one GPU (complex<double>; the chain is
+# complex<float>)
+SCALE_TOL, CHAIN_TOL = 1e-10, 1e-5
 
 
 def main():
@@ -194,6 +249,10 @@ def main():
                          "with the second operand over t only (redistributed)")
     ap.add_argument("--L", type=int, default=None)
     ap.add_argument("--n", type=int, default=64)
+    ap.add_argument("--chain-L", dest="chain_L", type=int, default=16,
+                    help="configs[4] chain: spatial extent per rank (x, y, z)")
+    ap.add_argument("--chain-T", dest="chain_T", type=int, default=64,
+                    help="configs[4] chain: time extent")
     ap.add_argument("--no-side", action="store_true", help="skip the side measurements")
     ap.add_argument("--skip", default="",
                     help="comma-separated side measurements to skip (permute, bsr, chain, 3m, "
@@ -250,8 +309,9 @@ def main():
     v0 = torch.empty(vol(p0[rank][1]), dtype=torch.complex128, device=dev)
     v1 = torch.empty(vol(p1[rank][1]), dtype=torch.complex128, device=dev)
     vr = torch.zeros(vol(gdimr) if rank == 0 else 1, dtype=torch.complex128, device=dev)
-    fill(v0, 1 + rank)
-    fill(v1, 101 + rank)
+    # slices of two global tensors (the same values at any N, and in single_gpu_time)
+    global_fill(v0, gdim0, p0[rank][0], p0[rank][1], SEED_V0)
+    global_fill(v1, gdim0, p1[rank][0], p1[rank][1], SEED_V1)
     z7, z5 = [0] * 7, [0] * 5
 
     def step():
@@ -283,9 +343,12 @@ def main():
             side.update(chain_bench(sb, dev))
         except Exception as e:  # a side measurement never takes the bench down
             side["chain_error"] = str(e)[:200]
+    # N > 1 results kept on rank 0 for the check against one GPU (scale_check_*)
+    results = {}
     if world > 1 and "chain_dist" not in skip:
         try:
-            side.update(chain_dist_bench(sb, dev, comm, world, rank, grid[:3], barrier))
+            side.update(chain_dist_bench(sb, dev, comm, world, rank, grid[:3], barrier,
+                                         Ls=args.chain_L, Lt=args.chain_T, check=not args.no_1gpu))
         except Exception as e:  # a side measurement never takes the bench down
             side["chain_dist_error"] = str(e)[:200]
     if world > 1 and config == "4a" and "redistribution" not in skip:
@@ -294,6 +357,8 @@ def main():
         try:
             side.update(redistribution_bench(sb, dev, comm, world, rank, gdim0, p0, v0, v1, pr,
                                              vr, barrier))
+            if rank == 0:
+                results["contraction_redistributed"] = vr.clone()
         except Exception as e:  # a side measurement never takes the bench down
             side["redistribution_error"] = str(e)[:200]
     flops_step = flops_of(L, n)
@@ -343,19 +408,34 @@ def main():
     algorithmic = flops_launch / kernel_s / 1e12
     achieved = algorithmic * exec_per_alg
 
-    # strong scaling: the same global problem on rank 0's GPU alone (outside the timed region)
+    # strong scaling: the same global problem on rank 0's GPU alone (outside the timed region),
+    # whose output is also the answer every N > 1 result is checked against
     scaling_fields = {}
     if world > 1 and not args.no_1gpu:
         barrier()
         if rank == 0:
+            results[config] = vr.clone()
             try:
-                t1 = single_gpu_time(sb, dev, gdim0, gdimr)
+                t1, ref = single_gpu_time(sb, dev, gdim0, gdimr)
                 scaling_fields = {"value_1gpu_same_problem": round(flops_step / t1 / 1e9, 2),
                                   "ms_per_step_1gpu": round(t1 * 1e3, 4),
                                   "strong_scaling_vs_1gpu": round(t1 / (elapsed / args.steps), 3)}
+                for name, r in results.items():
+                    scaling_fields["scale_check_rel_err_" + name] = rel_err(r, ref)
+                del ref
             except Exception as e:  # pragma: no cover
                 scaling_fields = {"single_gpu_error": str(e)[:200]}
+            results.clear()
         barrier()
+    if world > 1 and rank == 0:
+        errs = {k: v for k, v in list(scaling_fields.items()) + list(side.items())
+                if k.startswith("scale_check_rel_err")}
+        bad = [k for k, v in errs.items()
+               if not v <= (CHAIN_TOL if k.endswith("_chain") else SCALE_TOL)]
+        scaling_fields["scale_check_ok"] = bool(errs) and not bad
+        if bad:
+            print("bench: N>1 results differ from the 1-GPU answer: %s"
+                  % {k: errs[k] for k in bad}, file=sys.stderr)
 
     base = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -386,10 +466,16 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "strong" if world > 1 else "weak",
+            # the N > 1 lines strong-scale configs[3]; N = 1 is the single-GPU configs[1] point
+            # of the series (there is no scaling at N = 1)
+            "scaling": "strong",
+            "scaling_note": ("one global 32^4 problem split over the ranks" if world > 1 else
+                             "single GPU: configs[1]; the N > 1 lines are strong scaling of "
+                             "configs[3]"),
             "vs_baseline": None,
             "dtype": "complex<f64>",
-            "data": "synthetic (uniform [-1,1) complex, seeded)",
+            "data": "synthetic (complex in [-1,1)^2, a counter-based hash of each element's global "
+                    "index: identical global tensors at every N)",
             "config": {"workload": workload, "L": L, "n": n,
                        "gemm": "T,N m=n=%d k=%d batch=%d per rank" % (
                            4 * n, vol(p0[rank][1][3:]), p0[rank][1][0]),
@@ -429,12 +515,14 @@ def main():
 
 
 def single_gpu_time(sb, dev, gdim0, gdimr, reps=3):
-    """The global contraction on this GPU alone (one component per tensor): the denominator of
-    the strong-scaling figure, timed with HIP events on torch's current stream."""
+    """The global contraction on this GPU alone (one component per tensor), on the same global
+    inputs as the distributed run: the denominator of the strong-scaling figure, timed with HIP
+    events on torch's current stream.  Returns (seconds per call, its output)."""
     a = torch.empty(vol(gdim0), dtype=torch.complex128, device=dev)
     b = torch.empty_like(a)
-    fill(a, 11)
-    fill(b, 12)
+    z = [0] * len(gdim0)
+    global_fill(a, gdim0, z, gdim0, SEED_V0)
+    global_fill(b, gdim0, z, gdim0, SEED_V1)
     c = torch.empty(vol(gdimr), dtype=torch.complex128, device=dev)
     z7, z5 = [0] * 7, [0] * 5
     q0, qr = [(z7, gdim0)], [(z5, gdimr)]
@@ -451,9 +539,9 @@ def single_gpu_time(sb, dev, gdim0, gdimr, reps=3):
     e.record()
     torch.cuda.synchronize()
     t = s.elapsed_time(e) / 1e3 / reps
-    del a, b, c
+    del a, b
     torch.cuda.empty_cache()
-    return t
+    return t, c
 
 
 def redistribution_bench(sb, dev, comm, world, rank, gdim0, p0, v0, v1, pr, vr, barrier, reps=5):
@@ -716,7 +804,69 @@ def chain_bench(sb, dev, Ls=16, Lt=64, ncols=12, reps=3):
             "chain_hermitian_rel_err": herm}
 
 
-def chain_dist_bench(sb, dev, comm, world, rank, grid, barrier, Ls=16, Lt=64, ncols=12, reps=3):
+SEED_SRC, SEED_VALS = 21, 22
+
+
+def lattice_jj(sites, gdim, dfrom):
+    """Block columns of the 9-point operator (self, then -x, +x, -y, +y, -z, +z, -t, +t) of the
+    given global sites, relative to the domain's first site `dfrom` (periodic)."""
+    jj = np.zeros((len(sites), 9, 6), np.int32)
+    jj[:, 0, :4] = (sites - dfrom) % gdim
+    k = 1
+    for d in range(4):
+        for sg in (-1, 1):
+            c = sites.copy()
+            c[:, d] = (c[:, d] + sg) % gdim[d]
+            jj[:, k, :4] = (c - dfrom) % gdim
+            k += 1
+    return jj
+
+
+def chain_global(sb, dev, G, Lt, ncols):
+    """configs[4]'s chain on the WHOLE lattice G on this GPU alone, from the same global inputs
+    (SEED_SRC, SEED_VALS) as chain_dist_bench: the answer its N-rank result must equal."""
+    s_, c_ = 4, 3
+    b = s_ * c_
+    cf = torch.complex64
+    dim = G + [s_, c_]
+    dsrc = [Lt, ncols, s_, G[0], G[1], G[2], c_]
+    src = torch.empty(vol(dsrc), dtype=cf, device=dev)
+    global_fill(src, dsrc, [0] * 7, dsrc, SEED_SRC)
+    dx = [1] + G + [s_, c_, ncols]
+    x = torch.empty(vol(dx), dtype=cf, device=dev)
+    V = vol(G)
+    sites = np.array(np.unravel_index(np.arange(V), G)).T
+    jj = lattice_jj(sites, np.array(G), np.zeros(4, np.int64))
+    del sites
+    vals = torch.empty(V * 9 * b * b, dtype=cf, device=dev)
+    global_fill(vals, G + [9, b * b], [0] * 6, G + [9, b * b], SEED_VALS)
+    full = [([0] * 6, dim)]
+    blk = [1, 1, 1, 1, s_, c_]
+    op = sb.create_bsr(full, dim, full, dim, blk, blk, False,
+                       [torch.full((V,), 9, dtype=torch.int32, device=dev)],
+                       [torch.from_numpy(jj.reshape(-1)).to(dev)], [vals])
+    del jj
+    px, z8 = [([0] * 8, dx)], [0] * 8
+    sb.copy(1.0, [([0] * 7, dsrc)], "tnsxyzc", [0] * 7, dsrc, dsrc, [src], px, "pxyztscn", z8, dx,
+            [x])
+    del src
+    y = torch.empty_like(x)
+    sb.bsr_krylov(1.0, op, "XYZTSC", "xyztsc", px, "pxyztscn", z8, dx, dx, [x], 0.0, px,
+                  "pXYZTSCn", z8, dx, dx, "p", [y])
+    op.destroy()
+    del vals, x
+    dr = [Lt, s_, ncols, s_, ncols]
+    vr = torch.empty(vol(dr), dtype=cf, device=dev)
+    sb.contraction(1.0, px, z8, dx, dx, "pXYZTSCn", True, [y], px, z8, dx, dx, "pXYZTsCN", False,
+                   [y], 0.0, [([0] * 5, dr)], [0] * 5, dr, dr, "TSnsN", [vr])
+    torch.cuda.synchronize()
+    del y
+    torch.cuda.empty_cache()
+    return vr
+
+
+def chain_dist_bench(sb, dev, comm, world, rank, grid, barrier, Ls=16, Lt=64, ncols=12, reps=3,
+                     check=True):
     """configs[4] on N ranks (weak scaling, 16^3 x 64 sites per rank; N = 8: the 32^3 x 64
     lattice over a 2x2x2 grid), complex<float>: (1) redistribute the propagator from a t
     partition (source `tnsxyzc`, Lt/N t slices per rank) into the operator's xyz partition
@@ -734,8 +884,7 @@ def chain_dist_bench(sb, dev, comm, world, rank, grid, barrier, Ls=16, Lt=64, nc
     dx = [1] + G + [s_, c_, ncols]
     px = sb.basic_partitioning("pxyztscn", dx, [1] + grid + [1, 1, 1, 1], "xyz", world, 1)
     src = torch.empty(vol(psrc[rank][1]), dtype=cf, device=dev)
-    src.real.uniform_(-1, 1)
-    src.imag.uniform_(-1, 1)
+    global_fill(src, dsrc, psrc[rank][0], psrc[rank][1], SEED_SRC)
     x = torch.empty(vol(px[rank][1]), dtype=cf, device=dev)
     y = torch.empty_like(x)
     # operator: image = the rank's xyz block, domain = image + one-site halo in x, y, z
@@ -754,19 +903,11 @@ def chain_dist_bench(sb, dev, comm, world, rank, grid, barrier, Ls=16, Lt=64, nc
     V = vol(s0[:4])
     sites = np.array(np.unravel_index(np.arange(V), s0[:4])).T + np.array(f0[:4])
     gdim = np.array(G)
-    jj = np.zeros((V, 9, 6), np.int32)
-    dfrom = np.array(pd[rank][0][:4])
-    jj[:, 0, :4] = (sites - dfrom) % gdim
-    k = 1
-    for d in range(4):
-        for sg in (-1, 1):
-            c = sites.copy()
-            c[:, d] = (c[:, d] + sg) % gdim[d]
-            jj[:, k, :4] = (c - dfrom) % gdim
-            k += 1
+    jj = lattice_jj(sites, gdim, np.array(pd[rank][0][:4]))
+    # the block values of the rank's image sites: a box of the global [x, y, z, t, 9, 144] array
     vals = torch.empty(V * 9 * b * b, dtype=cf, device=dev)
-    vals.real.uniform_(-1, 1)
-    vals.imag.uniform_(-1, 1)
+    global_fill(vals, G + [9, b * b], list(f0[:4]) + [0, 0], list(s0[:4]) + [9, b * b],
+                SEED_VALS)
     blk = [1, 1, 1, 1, s_, c_]
     iiv = torch.full((V,), 9, dtype=torch.int32, device=dev)
     op = sb.create_bsr(pi, dim, pd, dim, blk, blk, False, [iiv],
@@ -861,6 +1002,15 @@ def chain_dist_bench(sb, dev, comm, world, rank, grid, barrier, Ls=16, Lt=64, nc
            "chain_dist_ms": t_all * 1e3,
            "chain_dist_bsr_unsplit_ms": t_whole * 1e3,
            "chain_dist_bsr_split_rel_diff": split_err}
+    if check:
+        # rank 0's TSnsN (after the timed repetitions: split operator, partials reduced over the
+        # ranks) against the whole chain on one GPU from the same global inputs
+        del x, y, src, vals
+        torch.cuda.empty_cache()
+        barrier()
+        if rank == 0:
+            out["scale_check_rel_err_chain"] = rel_err(vr, chain_global(sb, dev, G, Lt, ncols))
+        barrier()
     for i, name in enumerate(("redistribute", "bsr", "contraction")):
         out["chain_dist_%s_ms" % name] = times[i] * 1e3
     if world > 1 and dist_available():

@@ -690,8 +690,9 @@ __global__ void __launch_bounds__(256) bsr_mfma_dma_kernel(const BsrArgs p, unsi
         const unsigned base = slot0 + (unsigned)(k % (PD + 1)) * SLOT;
         if constexpr (PK > 0) {
             const char *vrow = (const char *)((const E *)p.v + (jb + k) * ABLK);
-            // a skipped block (column -1) reads its own values again (not used)
-            const char *xrow = dj[k] < 0 ? vrow : (const char *)((const E *)p.x + (long)dj[k] * nc);
+            // a skipped block (column -1) reads x's first block row (not used): always BD * nc
+            // valid elements, where the block's own values may end before the slot's x part
+            const char *xrow = (const char *)((const E *)p.x + (long)(dj[k] < 0 ? 0 : dj[k]) * nc);
 #pragma unroll
             for (int q = 0; q < PK; ++q) {
                 const unsigned g = (unsigned)(lane + 64 * q) * 16u;

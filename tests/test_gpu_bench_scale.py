@@ -1,0 +1,45 @@
+"""bench.py --gpus N proves its answer: every N > 1 line carries scale_check_rel_err_* fields,
+the distributed configs[3] contraction (4a), its redistributing form (4b) and the configs[4]
+chain each compared with the same global problem run on one GPU from the same global inputs.
+
+On a 1-GPU test box the two ranks share the GPU and exchange through RCCL's socket transport
+(bench.py --share-gpu rccl, one RCCL host id per rank); the library code is the xGMI path's."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("config", ["4a", "4b"])
+def test_bench_n2_scale_check(gpu, config):
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--config", config, "--L", "8", "--n", "16", "--chain-L", "4", "--chain-T", "8",
+           "--share-gpu", "rccl"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-6000:])
+    line = json.loads([s for s in r.stdout.splitlines() if s.startswith("{")][-1])
+    errs = {k: v for k, v in line.items() if k.startswith("scale_check_rel_err")}
+    want = {"scale_check_rel_err_" + config, "scale_check_rel_err_chain"}
+    if config == "4a":
+        want.add("scale_check_rel_err_contraction_redistributed")
+    assert set(errs) == want, line
+    for k, v in errs.items():
+        assert v <= (1e-5 if k.endswith("_chain") else 1e-10), (k, v)
+    assert line["scale_check_ok"] is True
+    assert line["chain_dist_bsr_split_rel_diff"] < 1e-5
