@@ -248,7 +248,8 @@ def main():
                          "the 32^4 problem over an xyz grid (the default at N > 1); 4b: the same "
                          "with the second operand over t only (redistributed)")
     ap.add_argument("--L", type=int, default=None)
-    ap.add_argument("--n", type=int, default=64)
+    # --ncols: the same (--n is ambiguous after torch.distributed.run, which reads abbreviations)
+    ap.add_argument("--n", "--ncols", dest="n", type=int, default=64)
     ap.add_argument("--chain-L", dest="chain_L", type=int, default=16,
                     help="configs[4] chain: spatial extent per rank (x, y, z)")
     ap.add_argument("--chain-T", dest="chain_T", type=int, default=64,

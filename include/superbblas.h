@@ -23,6 +23,7 @@
 
 #include "superbblas_amd/sbx.h"
 
+#include <algorithm>
 #include <array>
 #include <complex>
 #include <cstddef>
@@ -75,6 +76,105 @@ inline Context createCudaContext(int) {
 }
 
 struct BSR_handle; // opaque (sbx_bsr)
+
+/// supported_type<T>::value: whether T is an element type of the library (platform.h:686-712,
+/// 818-821)
+template <typename T> struct supported_type { static constexpr bool value = false; };
+template <> struct supported_type<int> { static constexpr bool value = true; };
+template <> struct supported_type<float> { static constexpr bool value = true; };
+template <> struct supported_type<double> { static constexpr bool value = true; };
+template <> struct supported_type<std::complex<float>> { static constexpr bool value = true; };
+template <> struct supported_type<std::complex<double>> { static constexpr bool value = true; };
+template <> struct supported_type<_Complex float> { static constexpr bool value = true; };
+template <> struct supported_type<_Complex double> { static constexpr bool value = true; };
+template <typename T> struct supported_type<const T> {
+    static constexpr bool value = supported_type<T>::value;
+};
+
+// ---- runtime features: the reference's SB_* environment flags (runtime_features.h:15-158) ----
+//
+// The library reads the same variables itself (SB_TRACK_TIME turns its kernel timers on,
+// SB_CACHEGB_GPU caps its scratch cache, SB_DEBUG adds syncs / barriers around copy and
+// contraction, SB_LOG reports failed allocations), so Python and C callers see them too.  The
+// functions returning a reference may be assigned at run time, as in the reference; a change of
+// getTrackingTime() reaches the library on the next API call.
+
+namespace sbx_detail {
+/// The integer value of an environment variable, or `def` when unset
+inline int env_int(const char *name, int def) {
+    const char *l = std::getenv(name);
+    return l ? std::atoi(l) : def;
+}
+inline double env_double(const char *name, double def) {
+    const char *l = std::getenv(name);
+    return l ? std::atof(l) : def;
+}
+} // namespace sbx_detail
+
+/// SB_LOG: 0 no log (default), >= 1 some log
+inline int getLogLevel() {
+    static const int v = std::max(0, sbx_detail::env_int("SB_LOG", 0));
+    return v;
+}
+/// SB_DEBUG: 0 no extra checks (default), >= 1 GPU sync and barriers around copy and contraction
+inline int getDebugLevel() {
+    static const int v = std::max(0, sbx_detail::env_int("SB_DEBUG", 0));
+    return v;
+}
+/// SB_TRACK_MEM: != 0 tracks memory use (reportCacheUsage / checkForMemoryLeaks always report)
+inline bool &getTrackingMemory() {
+    static bool v = sbx_detail::env_int("SB_TRACK_MEM", 0) != 0;
+    return v;
+}
+/// SB_TRACK_TIME: != 0 records the time of the library's kernels (reportTimings)
+inline bool &getTrackingTime() {
+    static bool v = sbx_detail::env_int("SB_TRACK_TIME", 0) != 0;
+    return v;
+}
+/// SB_TRACK_TIME_SYNC: accepted; timings are HIP events on the launch stream, no sync needed
+inline bool &getTrackingTimeSync() {
+    static bool v = sbx_detail::env_int("SB_TRACK_TIME_SYNC", 0) != 0;
+    return v;
+}
+/// SB_MPI_NONBLOCK (default on): exchanges are always asynchronous on the library's streams
+inline bool getUseMPINonBlock() {
+    static const bool v = sbx_detail::env_int("SB_MPI_NONBLOCK", 1) != 0;
+    return v;
+}
+/// SB_USE_ALLTOALL (default on): RCCL exchanges are grouped send/recv either way
+inline bool getUseAlltoall() {
+    static const bool v = sbx_detail::env_int("SB_USE_ALLTOALL", 1) != 0;
+    return v;
+}
+/// SB_MPI_GPU: 0 unset, 1 device buffers go straight to the transport (RCCL), -1 they are staged
+/// through host memory (the MPI_Comm overloads' transport choice)
+inline int getUseMPIGpu() {
+    static const int v =
+        std::getenv("SB_MPI_GPU") ? (sbx_detail::env_int("SB_MPI_GPU", 0) != 0 ? 1 : -1) : 0;
+    return v;
+}
+/// SB_CACHEGB_CPU: accepted (host components are mirrored through device scratch)
+inline double getMaxCacheGiBCpu() {
+    static const double v = sbx_detail::env_double("SB_CACHEGB_CPU", -1.0);
+    return v;
+}
+/// SB_CACHEGB_GPU: cap of the idle scratch cache per device in GiB (< 0: 10 % of the device)
+inline double getMaxCacheGiBGpu() {
+    static const double v = sbx_detail::env_double("SB_CACHEGB_GPU", -1.0);
+    return v;
+}
+
+namespace sbx_detail {
+/// Hand a run-time change of getTrackingTime() to the library (its timers start from the same
+/// SB_TRACK_TIME value)
+inline void sync_tracking() {
+    static bool applied = getTrackingTime();
+    if (applied != getTrackingTime()) {
+        applied = getTrackingTime();
+        (void)sbx_timings_enable(applied ? 1 : 0);
+    }
+}
+} // namespace sbx_detail
 
 /// elem<T>::type is T's element type if T is an array, otherwise T (blas.h:98-108)
 template <typename T> struct elem { using type = T; };
@@ -139,6 +239,7 @@ template <std::size_t N> inline const int *parts(const PartitionItem<N> *p) {
 
 inline void check_session(Session s) {
     if (s != 0) throw std::runtime_error("superbblas_amd: session must be 0");
+    sync_tracking(); // every entry point checks its session first
 }
 
 inline int co_of(CoorOrder co) { return co == SlowToFast ? SBX_SLOW_TO_FAST : SBX_FAST_TO_SLOW; }
@@ -346,9 +447,15 @@ template <typename OStream> void checkForMemoryLeaks(OStream &s) {
     }
 }
 
-/// Kernel timings (HIP events per kernel family); enable with sbx_timings_enable(1)
-inline void resetTimings() { sbx_detail::check(sbx_timings_reset()); }
+/// Kernel timings (HIP events per kernel family, performance.h:356-434): recorded while
+/// getTrackingTime() (SB_TRACK_TIME=1) is on; reportTimings prints nothing otherwise
+inline void resetTimings() {
+    sbx_detail::sync_tracking();
+    sbx_detail::check(sbx_timings_reset());
+}
 template <typename OStream> void reportTimings(OStream &s) {
+    sbx_detail::sync_tracking();
+    if (!getTrackingTime()) return;
     std::vector<char> buf(1 << 16);
     sbx_detail::check(sbx_timings_report(buf.data(), (int)buf.size()));
     s << "superbblas_amd kernel timings (family calls total_ms)\n" << buf.data();
@@ -962,7 +1069,9 @@ inline bool ranks_own_devices(MPI_Comm mpicomm, int device) {
 /// drives its own GPU -- the unique id is made by rank 0 and broadcast with MPI_Bcast, so device
 /// buffers travel directly (the reference's GPU-aware MPI path, dist.h:1626-1641, 1702-1773) --
 /// otherwise (ranks sharing a GPU) the host-staged transport over MPI_Alltoallv
-/// (dist.h:1426-1500).  SUPERBBLAS_AMD_MPI_TRANSPORT=host|rccl forces one.
+/// (dist.h:1426-1500).  SB_MPI_GPU (runtime_features.h:118-133) forces one: != 0 passes device
+/// buffers to the transport (RCCL), 0 stages them through host memory;
+/// SUPERBBLAS_AMD_MPI_TRANSPORT=host|rccl is an older spelling of the same choice.
 inline sbx_comm comm_of(MPI_Comm mpicomm, const Context *ctx, int ncomponents) {
     struct Entry {
         std::unique_ptr<MPI_Comm> c;
@@ -986,6 +1095,7 @@ inline sbx_comm comm_of(MPI_Comm mpicomm, const Context *ctx, int ncomponents) {
     bool rccl = ranks_own_devices(mpicomm, device); // collective: every rank decides alike
     if (force && std::string(force) == "host") rccl = false;
     if (force && std::string(force) == "rccl") rccl = true;
+    if (getUseMPIGpu() != 0) rccl = getUseMPIGpu() > 0;
     Entry e{std::unique_ptr<MPI_Comm>(new MPI_Comm(mpicomm)), nullptr};
     if (rccl) {
         unsigned char id[128] = {0};
@@ -1066,6 +1176,23 @@ void bsr_krylov(T alpha, BSR_handle *bsrh, const char *oim, const char *odm,
         sizey, dimy, okr, vy, ctx, sbx_detail::comm_of(mpicomm, ctx, ncomponents), co, request,
         session, just_local);
 }
+template <std::size_t Nd, std::size_t Ni, typename T>
+void bsr_get_preferred_layout(BSR_handle *bsrh, int ncomponents, const Context *ctx,
+                              MPI_Comm mpicomm, CoorOrder co,
+                              MatrixLayout *preferred_layout_for_x,
+                              MatrixLayout *preferred_layout_for_y) {
+    const auto c = sbx_detail::contexts(ctx, ncomponents);
+    std::vector<int> lx(ncomponents), ly(ncomponents);
+    sbx_detail::check(sbx_bsr_get_preferred_layout(
+        reinterpret_cast<sbx_bsr>(bsrh), ncomponents, c.data(),
+        sbx_detail::comm_of(mpicomm, ctx, ncomponents), sbx_detail::co_of(co), lx.data(),
+        ly.data()));
+    for (int i = 0; i < ncomponents; ++i) {
+        preferred_layout_for_x[i] = lx[i] == SBX_ROW_MAJOR ? RowMajor : ColumnMajor;
+        preferred_layout_for_y[i] = ly[i] == SBX_ROW_MAJOR ? RowMajor : ColumnMajor;
+    }
+}
+
 template <std::size_t N, typename T>
 void cholesky(const PartitionItem<N> *p, const Coor<N> &dim, int ncomponents, const char *o,
               T **v, const char *orows, const char *ocols, const Context *ctx, MPI_Comm mpicomm,

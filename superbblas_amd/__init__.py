@@ -69,9 +69,18 @@ _lib.sbx_last_error.restype = ctypes.c_char_p
 
 
 
+# errors of requests that were dropped without wait() and finished at garbage collection: raised
+# by the next call into the library (never silently lost)
+_dropped_request_errors: List[str] = []
+
+
 def _check(rc: int):
     if rc != 0:
         raise SuperbblasError(_lib.sbx_last_error().decode())
+    if _dropped_request_errors:
+        msg = _dropped_request_errors.pop(0)
+        raise SuperbblasError("a Request dropped without wait() failed when it was finished at "
+                              "garbage collection: " + msg)
 
 
 import array as _array
@@ -155,11 +164,20 @@ class Request:
             h, self._h = self._h, None
             _check(_lib.sbx_wait(h))
 
-    def __del__(self):  # a dropped request is still completed (in this process's call order)
+    def __del__(self):
+        # a dropped request is still completed, but at garbage-collection time rather than at a
+        # point every rank agrees on: warn, and hand a failure to the next library call
+        if not self._h:
+            return
+        import warnings
+        warnings.warn("superbblas_amd: a Request was dropped without wait(); finishing its "
+                      "exchange at garbage collection", ResourceWarning, stacklevel=2)
+        h, self._h = self._h, None
         try:
-            self.wait()
-        except Exception:
-            pass
+            if _lib.sbx_wait(h) != 0:
+                _dropped_request_errors.append(_lib.sbx_last_error().decode())
+        except Exception as e:  # pragma: no cover (interpreter shutdown)
+            _dropped_request_errors.append(str(e))
 
 
 def wait(request: Optional["Request"]):
@@ -321,6 +339,16 @@ def timings_report() -> str:
 def clear_caches():
     """clearCaches (alloc.h:437-443)"""
     _check(_lib.sbx_clear_caches())
+
+
+_lib.sbx_cache_usage.argtypes = [_I, _VP, _VP]
+
+
+def cache_usage(device: int = 0) -> Tuple[int, int]:
+    """(idle bytes held by the scratch cache, bytes in use) of a device (performance.h:436-495)"""
+    cached, live = ctypes.c_ulonglong(0), ctypes.c_ulonglong(0)
+    _check(_lib.sbx_cache_usage(device, ctypes.byref(cached), ctypes.byref(live)))
+    return cached.value, live.value
 
 
 # ---------------------------------------------------------------------------------------------

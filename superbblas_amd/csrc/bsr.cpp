@@ -378,6 +378,9 @@ BsrOp *make_transposed(const BsrOp &a) {
             continue;
         }
         bc.block_rows = ncb;
+        // A^H's domain rows (elements) = A's image component (the DMA / split kernels bound
+        // their x reads by it)
+        bc.x_rows = volume(a.pi[a.rank][c].size) / std::max(1L, volume(a.kroni));
         const std::vector<int> &rp = ac.h_rowptr, &jj = ac.h_jj;
         std::vector<int> cnt(ncb + 1, 0);
         for (int k = 0; k < rp.back(); ++k)

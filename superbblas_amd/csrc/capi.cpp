@@ -11,6 +11,7 @@
 
 #include <rccl/rccl.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 
@@ -441,6 +442,9 @@ int sbx_tune_set(const char *key, long long value) {
         else if (k == "gemm.splits") g_gemm_tune.splits = (int)value;
         else if (k == "gemm.t48") g_gemm_tune.t48 = (int)value;
         else if (k == "gemm.share_ab") g_gemm_tune.share_ab = (int)value;
+        else if (k == "dist.reduce") g_dist_reduce = (int)value;
+        else if (k == "dist.reduce_calls") g_dist_reduce_calls = value;
+        else if (k.compare(0, 6, "alloc.") == 0) alloc_tune(key, nullptr, &value);
         else throw Error("tune_set: unknown key " + k);
     });
 }
@@ -487,6 +491,9 @@ int sbx_tune_get(const char *key, long long *value) {
         else if (k == "gemm.splits") *value = g_gemm_tune.splits;
         else if (k == "gemm.t48") *value = g_gemm_tune.t48;
         else if (k == "gemm.share_ab") *value = g_gemm_tune.share_ab;
+        else if (k == "dist.reduce") *value = g_dist_reduce;
+        else if (k == "dist.reduce_calls") *value = g_dist_reduce_calls;
+        else if (k.compare(0, 6, "alloc.") == 0) alloc_tune(key, value, nullptr);
         else throw Error("tune_get: unknown key " + k);
     });
 }
@@ -657,6 +664,33 @@ int sbx_copy_masked(int nd0, int nd1, const double *alpha, int t0, int t1, const
                         copyadd, session, nullptr);
 }
 
+namespace {
+/// SB_DEBUG >= 1 (runtime_features.h:24-37): the GPU is synchronised and the ranks meet at a
+/// barrier before and after every copy and contraction (the reference's debug mode, dist.h:2274-2280)
+int debug_level() {
+    static const int v = [] {
+        const char *l = std::getenv("SB_DEBUG");
+        return l ? std::max(0, std::atoi(l)) : 0;
+    }();
+    return v;
+}
+struct DebugSync {
+    const Comm &c;
+    explicit DebugSync(const Comm &c_) : c(c_) { sync(); }
+    ~DebugSync() {
+        try {
+            sync();
+        } catch (...) {
+        }
+    }
+    void sync() {
+        if (debug_level() <= 0) return;
+        SBX_HIP_CHECK(hipDeviceSynchronize());
+        comm_barrier(c);
+    }
+};
+} // namespace
+
 int sbx_copy_req(int nd0, int nd1, const double *alpha, int t0, int t1, const int *p0,
                  int ncomponents0, const char *o0, const int *from0, const int *size0,
                  const int *dim0, const void *const *v0, const float *const *mask0,
@@ -671,6 +705,7 @@ int sbx_copy_req(int nd0, int nd1, const double *alpha, int t0, int t1, const in
         if (mask0 && !mask1)
             throw Error("copy: a destination mask (mask1) is required with an origin mask");
         const Comm c = get_comm(comm);
+        const DebugSync dbg(c);
         const Scalar a_call = to_scalar(alpha);
         // fast path (see above): the shape key excludes the data pointers and alpha's value
         bool fast = !mask0 && !mask1 && c.nprocs == 1 && p0 && p1 && v0 && v1 && o0 && o1 &&
@@ -844,6 +879,7 @@ int sbx_contraction(int nd0, int nd1, int ndr, int t, const double *alpha, const
         if (t != SBX_FLOAT && t != SBX_DOUBLE && t != SBX_CFLOAT && t != SBX_CDOUBLE)
             throw Error("contraction: unsupported type");
         const Comm c = get_comm(comm);
+        const DebugSync dbg(c);
         const bool rev = co == SBX_FAST_TO_SLOW;
         check_contraction_args(to_labels(o0, nd0, rev, "o0"), to_coor(size0, nd0, rev),
                                to_labels(o1, nd1, rev, "o1"), to_coor(size1, nd1, rev),

@@ -555,7 +555,8 @@ void dist_contraction(const Scalar &alpha, const DistTensor &v0, const Coor &fro
                 s0[0] = (int)(c1 - c0);
                 const int tr_in_vr = (int)vr.labels.find(lR[0]);
                 f1[tr_in_vr] = (int)normalize_coor((long)f1[tr_in_vr] + c0, vr.dim[tr_in_vr]);
-                dist_copy(Scalar{1, 0}, tr, f0, s0, vr, f1, true, comm);
+                if (!dist_reduce_collective(tr, f0, s0, vr, f1, comm))
+                    dist_copy(Scalar{1, 0}, tr, f0, s0, vr, f1, true, comm);
             }
         }
         stream_after(main_s, side_s); // join: vr complete, temporaries free in order
@@ -568,8 +569,10 @@ void dist_contraction(const Scalar &alpha, const DistTensor &v0, const Coor &fro
     // 3) local contractions into the partial outputs
     for (const LocalWork &l : lw) local_contraction(alpha, l.x, conjX, l.y, conjY, Scalar{0, 0}, l.r);
 
-    // 4) reduce the partial outputs into vr (dist.h:3183-3186)
-    dist_copy(Scalar{1, 0}, tr, tfromr, tsizer, vr, fromr, true, comm);
+    // 4) reduce the partial outputs into vr (dist.h:3183-3186): one RCCL collective where the
+    //    partitions allow, else the Add copy (point-to-point sends into the owners)
+    if (!dist_reduce_collective(tr, tfromr, tsizer, vr, fromr, comm))
+        dist_copy(Scalar{1, 0}, tr, tfromr, tsizer, vr, fromr, true, comm);
 }
 
 } // namespace sbx

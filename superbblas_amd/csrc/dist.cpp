@@ -593,6 +593,102 @@ void dist_copy(const Scalar &alpha, const DistTensor &src, const Coor &from0, co
         finish();
 }
 
+int g_dist_reduce = 1; // tune key dist.reduce: 1 collective reductions where they fit, 0 never
+std::atomic<long long> g_dist_reduce_calls{0}; // read-back dist.reduce_calls: collectives issued
+
+bool dist_reduce_collective(const DistTensor &part, const Coor &f0, const Coor &s0,
+                            const DistTensor &dst, const Coor &f1, const Comm &comm) {
+    if (!comm.nccl || comm.nprocs < 2 || g_dist_reduce <= 0) return false;
+    ncclDataType_t nt;
+    int reals = 1;
+    switch (part.dtype) {
+    case SBX_CDOUBLE: nt = ncclDouble; reals = 2; break;
+    case SBX_DOUBLE: nt = ncclDouble; break;
+    case SBX_CFLOAT: nt = ncclFloat; reals = 2; break;
+    case SBX_FLOAT: nt = ncclFloat; break;
+    default: return false;
+    }
+    if (part.dtype != dst.dtype || volume(s0) == 0 || (int)part.ranges.size() != comm.nprocs ||
+        (int)dst.ranges.size() != comm.nprocs)
+        return false;
+    const int nd = part.nd();
+    // every rank: one partial component, the same range, holding the box as one contiguous run
+    // (the box spans the component in every dimension but the slowest)
+    const Range &r0 = part.ranges[0].size() == 1 ? part.ranges[0][0] : Range{};
+    if (part.ranges[0].size() != 1) return false;
+    for (int q = 1; q < comm.nprocs; ++q)
+        if (part.ranges[q].size() != 1 || part.ranges[q][0].from != r0.from ||
+            part.ranges[q][0].size != r0.size)
+            return false;
+    Coor off(nd, 0);
+    for (int d = 0; d < nd; ++d) {
+        off[d] = normalize_coor((long)f0[d] - r0.from[d], part.dim[d]);
+        if (off[d] + s0[d] > r0.size[d]) return false;
+        if (d > 0 && (off[d] != 0 || s0[d] != r0.size[d])) return false;
+    }
+    // the destination box: owned by one rank (reduce) or whole on every rank (all-reduce)
+    Coor size1(dst.nd(), 1);
+    for (int d = 0; d < nd; ++d) {
+        const auto j = dst.labels.find(part.labels[d]);
+        if (j == std::string::npos) return false;
+        size1[j] = s0[d];
+    }
+    const Range box1{f1, size1};
+    const long vbox = volume(size1);
+    int owners = 0, root = -1, whole = 0;
+    for (int q = 0; q < comm.nprocs; ++q) {
+        long covered = 0;
+        for (const Range &r : dst.ranges[q])
+            for (const Range &x : intersection(r, box1, dst.dim)) covered += volume(x.size);
+        if (covered > 0) {
+            ++owners;
+            root = q;
+        }
+        if (covered == vbox && dst.ranges[q].size() == 1) ++whole;
+    }
+    const bool all = whole == comm.nprocs;
+    if (!(owners == 1 || all)) return false;
+    const int device = comm.device;
+    set_device(device);
+    const hipStream_t s = get_stream(device);
+    const std::size_t es = dtype_size(part.dtype);
+    const long n = volume(s0);
+    const std::vector<long> st = strides_slow_to_fast(r0.size);
+    const char *send = (const char *)part.ptr[0] + es * offset_of(off, st);
+    const bool mine = all || comm.rank == root;
+    Scratch sum(mine ? n * es : 0, device);
+    ncclComm_t nc = (ncclComm_t)comm.nccl;
+    ++g_dist_reduce_calls;
+    if (all)
+        nccl_check(ncclAllReduce(send, sum.ptr, (size_t)n * reals, nt, ncclSum, nc, s),
+                   "ncclAllReduce");
+    else
+        nccl_check(ncclReduce(send, mine ? sum.ptr : nullptr, (size_t)n * reals, nt, ncclSum, root,
+                              nc, s),
+                   "ncclReduce");
+    if (!mine) return true;
+    // Add the sum into this rank's destination components (a local copy: one process, one box)
+    DistTensor sl;
+    sl.labels = part.labels;
+    sl.dim = part.dim;
+    sl.dtype = part.dtype;
+    sl.ranges = {{Range{f0, s0}}};
+    sl.ptr = {sum.ptr};
+    sl.dev = {device};
+    DistTensor dl;
+    dl.labels = dst.labels;
+    dl.dim = dst.dim;
+    dl.dtype = dst.dtype;
+    dl.ranges = {dst.ranges[comm.rank]};
+    dl.ptr = dst.ptr;
+    dl.dev = dst.dev;
+    dl.mask = dst.mask;
+    Comm self;
+    self.device = device;
+    dist_copy(Scalar{1, 0}, sl, f0, s0, dl, f1, true, self);
+    return true;
+}
+
 void comm_barrier(const Comm &comm) {
     if (comm.nprocs <= 1) return;
     if (comm.nccl) {

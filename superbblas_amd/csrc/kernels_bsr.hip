@@ -600,6 +600,7 @@ template <typename R, bool CPLX, int BI, int BD, int NNZ, int PD>
 void launch_bsr_mfma_blk(const BsrArgs &a, bool yrow, hipStream_t s) {
     const long blocks = (a.block_rows + 3) / 4;
     if (blocks >= (1L << 31)) throw Error("bsr: grid too large");
+    g_bsr_tune.last = 9;
     KernelTimer timer("bsr", s);
     const bool m3 = CPLX && g_gemm_tune.m3 > 0;
     if (yrow && m3)
@@ -619,6 +620,7 @@ void launch_bsr_mfma_ell(const BsrArgs &a, bool yrow, bool xrow, hipStream_t s) 
     const long waves = a.block_rows * ntn;
     const long blocks = (waves + 3) / 4;
     if (blocks >= (1L << 31)) throw Error("bsr: grid too large");
+    g_bsr_tune.last = 10;
     KernelTimer timer("bsr", s);
     if (yrow && xrow)
         hipLaunchKernelGGL((bsr_mfma_ell_kernel<R, CPLX, BI, BD, true, true, NNZ, NB>), dim3(blocks), dim3(256), 0, s, a, ntn);
@@ -637,6 +639,7 @@ void launch_bsr_mfma_pf(const BsrArgs &a, bool yrow, bool xrow, hipStream_t s) {
     const long waves = a.block_rows * ntn;
     const long blocks = (waves + 3) / 4;
     if (blocks >= (1L << 31)) throw Error("bsr: grid too large");
+    g_bsr_tune.last = 11;
     KernelTimer timer("bsr", s);
     if (yrow && xrow)
         hipLaunchKernelGGL((bsr_mfma_pf_kernel<R, CPLX, BI, BD, true, true>), dim3(blocks), dim3(256), 0, s, a, ntn);
@@ -803,6 +806,13 @@ bool launch_bsr_mfma_dma(const BsrArgs &a, bool yrow, hipStream_t s) {
                         (BD * a.ncols * ES) % 16 == 0 && ((size_t)a.x & 15) == 0 &&
                         ((size_t)a.v & 15) == 0;
     const size_t lds = packed ? (size_t)4 * slot_packed * (PD + 1) : (size_t)4 * (NA + NX) * 1024 * (PD + 1);
+    // 4 waves x (PD + 1) ring slots; a packed slot's last instruction is masked to the slot
+    // (lanes past it are inactive), an unpacked slot is NA + NX whole 64-lane instructions
+    if (packed && !m3)
+        check_dma_lds("bsr_mfma_dma_kernel", lds, 4L * (PD + 1), 0, 4L * (PD + 1) * slot_packed);
+    else
+        check_dma_lds("bsr_mfma_dma_kernel", lds, 4L * (PD + 1) * (NA + NX), 64);
+    g_bsr_tune.last = packed && !m3 ? 8 : 7;
     KernelTimer timer("bsr", s);
     auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), lds, s, a, (unsigned)v_bytes, (unsigned)x_bytes);
@@ -1033,6 +1043,9 @@ void launch_ell9(const BsrArgs &a, bool yrow, bool xrow, hipStream_t s, long lds
     // the DMA form fills whole workgroup-wide rows of 16-byte lanes
     const size_t lds = (NTF & 4) != 0 ? (size_t)((rb * 9L * BI * BD + NT - 1) / NT * NT) * sizeof(E)
                                       : (size_t)rb * blk_bytes;
+    // the DMA loop: passes u < ceil(nv / NT) of NT lanes, nv <= rb * 81 (the last chunk fewer)
+    if constexpr ((NTF & 4) != 0)
+        check_dma_lds("bsr_ell9_kernel", lds, (rb * 9L * BI * BD + NT - 1) / NT, NT);
     g_bsr_tune.last = 3;
     KernelTimer timer("bsr", s);
     if (yrow && xrow)
@@ -1059,6 +1072,8 @@ __global__ void __launch_bounds__(256) bsr_ell9_row_kernel(const BsrArgs p, unsi
     constexpr int NNZ = 9, BI = 3, BD = 3, BLK = 9, RW = 28; // 28 rows x 9 blocks = 252 threads
     constexpr int NV = RW * NNZ * BLK, NP = RW * NNZ * BI * NC;
     constexpr int NS = (DMA ? (NV + 255) / 256 * 256 : 0) > NP ? (NV + 255) / 256 * 256 : NP;
+    // static LDS: every DMA pass (256 lanes, the last one partly zeros) and the partial products
+    static_assert((!DMA || NS >= (NV + 255) / 256 * 256) && NS >= NP, "LDS sizing");
     __shared__ __attribute__((aligned(16))) E sh[NS]; // values (DMA), then the partial products
     const E *__restrict__ v = (const E *)p.v;
     const E *__restrict__ x = (const E *)p.x;
@@ -1346,6 +1361,12 @@ bool launch_ell9_split(const BsrArgs &a, bool yrow, bool xrow, hipStream_t st) {
         const long npart = jb == 9 ? 0L : (long)rw * (9 / jb) * 3 * nct * cw;
         const long lds = (ovl ? std::max(nvp, npart) : nvp + npart) * 16L;
         if (lds > 65536) return false;
+        // DMA passes u < ceil(nv / nth) of nth lanes (nv <= rw * 81); the partial products
+        // overlay them (ovl) or follow them
+        check_dma_lds("bsr_ell9_split_kernel", (size_t)lds, (rw * 81L + nth - 1) / nth, nth,
+                      ovl ? 0 : npart * 16);
+        check_dma_lds("bsr_ell9_split_kernel partials", (size_t)lds, 0, 0,
+                      (ovl ? 0 : nvp * 16) + npart * 16);
         SplitArgs sa{nct, tpr, rw, (unsigned)v_bytes, (unsigned)x_bytes, 0, 0, 0, 0,
                      std::max(1, g_bsr_tune.split_ilv), ovl ? 1 : 0};
         magic((unsigned)tpr, sa.tpr_m, sa.tpr_s);

@@ -291,6 +291,8 @@ __global__ void __launch_bounds__(256) bsr_kron_mfma_kernel(const KronArgs p, in
     // contiguous run) into LDS by one DMA pass, read back as broadcasts
     // (rounded up to whole DMA passes of 256 lanes: the lanes past the run write zeros)
     __shared__ __attribute__((aligned(16))) E us[(4 * NNZ * 9 + 255) / 256 * 256];
+    // a workgroup's 4 tasks span at most 4 rows: nu <= 4 * NNZ * 9, every pass of 256 lanes fits
+    static_assert(sizeof(us) / sizeof(E) >= (4 * NNZ * 9 + 255) / 256 * 256, "LDS sizing");
     {
         const long rlo = (wgi * 4) / ngroups, rhi = min((wgi * 4 + 3) / ngroups, p.block_rows - 1);
         const int nu = (int)(rhi - rlo + 1) * NNZ * 9;
@@ -524,6 +526,8 @@ template <typename E> void launch_kron_typed(const KronArgs &a, hipStream_t s) {
                     // workgroup (the lanes past the run write zeros)
                     const int nth = 64 * wpk;
                     const size_t lds_bytes = (size_t)((rw * 81 + nth - 1) / nth * nth) * 16;
+                    // the DMA loop: passes u < ceil(nrows * 81 / nth), nrows <= rw
+                    check_dma_lds("bsr_kron_mfma_packed_kernel", lds_bytes, (rw * 81L + nth - 1) / nth, nth);
                     // spin matrices one neighbour ahead: n = 8 / 12 104 / 166 -> 102 / 163 us
                     // (the one-row-per-wave kernel: 214 -> 221 us at n = 16, so not there;
                     // profiles/r02c_kron_kpf.txt)

@@ -10,6 +10,8 @@
 // at the API boundary (the reference does the same, e.g. tensor.h:718-727, 1282-1293).
 #pragma once
 
+#include <atomic>
+
 #include "sbx_internal.h"
 
 #include <functional>
@@ -134,6 +136,19 @@ struct Local {
 
 /// Every rank of `comm` reaches this point before any leaves it (MPI_Barrier)
 void comm_barrier(const Comm &comm);
+
+/// The contraction's cross-rank sum of partial outputs as one RCCL collective (the
+/// reference Adds them with a copy, dist.h:3183-3186, 1364-1404): when every rank holds one
+/// partial component (the same range) containing the box [f0, f0 + s0) as a contiguous run, and
+/// the destination box is owned by one rank (ncclReduce to it) or whole on every rank
+/// (ncclAllReduce), RCCL sums the partials (complex as pairs of reals) into scratch and the
+/// owners Add the sum into `dst` by a local copy.  All ranks decide alike from the global
+/// partitions.  Returns false, having done nothing, when the shapes do not fit (or the tune key
+/// dist.reduce is 0): the caller then Adds through dist_copy (point-to-point sends).
+bool dist_reduce_collective(const DistTensor &part, const Coor &f0, const Coor &s0,
+                            const DistTensor &dst, const Coor &f1, const Comm &comm);
+extern int g_dist_reduce;
+extern std::atomic<long long> g_dist_reduce_calls;
 
 /// copy: dst[from1 + P(c - from0)] (=|+=) alpha * src[c] for c in [from0, from0+size0).
 /// With `deferred` and other ranks in the exchange, the call returns once the local pieces are

@@ -5,6 +5,8 @@
 // alloc.h:91-391 (cached scratch buffers) and performance.h:356-518 (timings).
 #include "sbx_internal.h"
 
+#include <atomic>
+#include <cstdio>
 #include <cstdlib>
 #include <map>
 #include <mutex>
@@ -116,18 +118,37 @@ void destroy_streams() {
 // mapped for the life of the cache: hipMallocAsync's pool was measured to hand back reused
 // memory with stale contents after many queued launches on this platform, so it is not used.
 //
+// The idle blocks of a device are capped (the reference's LRU cache bound, cache.h:237-294):
+// SB_CACHEGB_GPU GiB when set (runtime_features.h:147-158), otherwise 10 % of the device's
+// memory; past the cap the least recently freed blocks go back to the driver.
+//
+// A block is freed on the stream current at the free.  When that is not the stream it was
+// allocated on (a buffer made under a StreamOverride and released after the override ended, e.g.
+// a deferred exchange whose request is dropped without wait), the free first makes the current
+// stream wait for the allocation stream, so a reuse in the current stream's order never overlaps
+// work still queued on the other one.  Such frees are counted (tune key alloc.cross_stream_frees).
+//
 namespace {
 struct Block {
     void *p;
     std::size_t bytes;
     hipStream_t stream;
     hipEvent_t ev;
+    unsigned long long seq; // free order (LRU eviction)
+};
+struct Live {
+    std::size_t bytes;
+    hipStream_t stream; // allocation stream
 };
 struct Cache {
     std::multimap<std::size_t, Block> free_blocks;
-    std::map<void *, std::size_t> live;
+    std::map<void *, Live> live;
     std::size_t cached_bytes = 0;
+    long long max_cached = -1; // bytes; < 0: not yet decided
 };
+unsigned long long g_free_seq = 0;
+long long g_max_cached_override = -1; // tune key alloc.max_cached (bytes; < 0: the policy above)
+long long g_cross_stream_frees = 0;
 std::mutex g_cache_mutex;
 std::vector<Cache> &caches() {
     static std::vector<Cache> c;
@@ -155,6 +176,51 @@ std::size_t round_bytes(std::size_t b) {
         return r;
     }
     return (b + (2u << 20) - 1) / (2u << 20) * (2u << 20);
+}
+/// The cap of `device`'s idle blocks in bytes (callers hold g_cache_mutex)
+long long max_cached(int device) {
+    if (g_max_cached_override >= 0) return g_max_cached_override;
+    Cache &c = cache(device);
+    if (c.max_cached < 0) {
+        const char *l = std::getenv("SB_CACHEGB_GPU");
+        const double gib = l ? std::atof(l) : -1.0;
+        if (gib >= 0) {
+            c.max_cached = (long long)(gib * 1073741824.0);
+        } else {
+            std::size_t fr = 0, total = 0;
+            if (hipMemGetInfo(&fr, &total) != hipSuccess) {
+                (void)hipGetLastError();
+                total = 0;
+            }
+            c.max_cached = total > 0 ? (long long)(total / 10) : (1LL << 34);
+        }
+    }
+    return c.max_cached;
+}
+/// Return the least recently freed blocks until the idle bytes are within the cap
+void trim_to_cap(int device) {
+    Cache &c = cache(device);
+    const long long cap = max_cached(device);
+    while ((long long)c.cached_bytes > cap && !c.free_blocks.empty()) {
+        auto oldest = c.free_blocks.begin();
+        for (auto it = c.free_blocks.begin(); it != c.free_blocks.end(); ++it)
+            if (it->second.seq < oldest->second.seq) oldest = it;
+        Block b = oldest->second;
+        c.free_blocks.erase(oldest);
+        c.cached_bytes -= b.bytes;
+        if (b.ev) {
+            (void)hipEventSynchronize(b.ev);
+            (void)hipEventDestroy(b.ev);
+        }
+        device_free(b.p, device);
+    }
+}
+int log_level() {
+    static const int v = [] {
+        const char *l = std::getenv("SB_LOG");
+        return l ? std::max(0, std::atoi(l)) : 0;
+    }();
+    return v;
 }
 /// Return every cached block of `device` to the driver (callers hold g_cache_mutex)
 void release_cached(int device) {
@@ -186,7 +252,7 @@ void *scratch_alloc(std::size_t bytes, int device) {
             if (b.stream != s) SBX_HIP_CHECK(hipStreamWaitEvent(s, b.ev, 0));
             SBX_HIP_CHECK(hipEventDestroy(b.ev));
         }
-        c.live[b.p] = b.bytes;
+        c.live[b.p] = Live{b.bytes, s};
         return b.p;
     }
     void *p = nullptr;
@@ -196,9 +262,21 @@ void *scratch_alloc(std::size_t bytes, int device) {
         // out of memory: give the cached blocks back and retry once (alloc.h:104-168)
         (void)hipGetLastError();
         release_cached(device);
-        p = device_alloc(rb, device);
+        try {
+            p = device_alloc(rb, device);
+        } catch (const Error &) {
+            if (log_level() > 0) {
+                std::size_t l = 0;
+                for (auto &e : c.live) l += e.second.bytes;
+                std::fprintf(stderr,
+                             "superbblas_amd: error allocating %zu bytes on device %d; scratch in "
+                             "use %zu MiB\n",
+                             rb, device, l >> 20);
+            }
+            throw;
+        }
     }
-    c.live[p] = rb;
+    c.live[p] = Live{rb, s};
     return p;
 }
 
@@ -263,7 +341,7 @@ void cache_usage(int device, std::size_t *cached, std::size_t *live) {
     Cache &c = cache(device);
     *cached = c.cached_bytes;
     std::size_t l = 0;
-    for (auto &e : c.live) l += e.second;
+    for (auto &e : c.live) l += e.second.bytes;
     *live = l;
 }
 
@@ -275,12 +353,33 @@ void scratch_free(void *p, int device) {
     Cache &c = cache(device);
     auto it = c.live.find(p);
     if (it == c.live.end()) throw Error("scratch_free: unknown pointer");
-    Block b{p, it->second, s, nullptr};
+    Block b{p, it->second.bytes, s, nullptr, ++g_free_seq};
+    if (it->second.stream != s) {
+        // freed away from its allocation stream: the reuse order is this stream's, so it first
+        // waits for the allocation stream's queued work
+        stream_after(s, it->second.stream);
+        ++g_cross_stream_frees;
+    }
     c.live.erase(it);
     SBX_HIP_CHECK(hipEventCreateWithFlags(&b.ev, hipEventDisableTiming));
     SBX_HIP_CHECK(hipEventRecord(b.ev, s));
     c.free_blocks.emplace(b.bytes, b);
     c.cached_bytes += b.bytes;
+    trim_to_cap(device);
+}
+
+void alloc_tune(const char *key, long long *get, const long long *set) {
+    std::lock_guard<std::mutex> g(g_cache_mutex);
+    const std::string k(key);
+    if (k == "alloc.max_cached") {
+        if (set) g_max_cached_override = *set;
+        if (get) *get = g_max_cached_override >= 0 ? g_max_cached_override : max_cached(0);
+    } else if (k == "alloc.cross_stream_frees") {
+        if (set) g_cross_stream_frees = *set;
+        if (get) *get = g_cross_stream_frees;
+    } else {
+        throw Error(std::string("tune: unknown key ") + key);
+    }
 }
 
 void trim_pools() {
@@ -319,7 +418,11 @@ int pointer_device(const void *p) {
 //
 namespace {
 struct TimerState {
-    bool on = false;
+    // SB_TRACK_TIME (runtime_features.h:55-68) turns the timers on from the start
+    std::atomic<bool> on{[] {
+        const char *l = std::getenv("SB_TRACK_TIME");
+        return l && std::atoi(l) != 0;
+    }()};
     std::string only; // comma-separated kernel families to time (empty: all)
     struct Pending {
         std::string name;
@@ -353,10 +456,7 @@ void timings_enable(bool on) {
     std::lock_guard<std::mutex> g(g_timer_mutex);
     timers().on = on;
 }
-bool timings_enabled() {
-    std::lock_guard<std::mutex> g(g_timer_mutex);
-    return timers().on;
-}
+bool timings_enabled() { return timers().on; }
 void timings_reset() {
     std::lock_guard<std::mutex> g(g_timer_mutex);
     drain_timers();
@@ -383,6 +483,7 @@ void timings_filter(const char *names) {
     timers().only = names ? std::string(",") + names + "," : std::string();
 }
 KernelTimer::KernelTimer(const char *n, hipStream_t s) : name(n), stream(s) {
+    if (!timers().on) return; // the common case: no lock per launch
     {
         // the switch and the family filter are written under the lock (timings_enable/filter)
         std::lock_guard<std::mutex> g(g_timer_mutex);

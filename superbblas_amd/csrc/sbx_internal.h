@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <array>
+#include <atomic>
 #include <complex>
 #include <cstdint>
 #include <cstring>
@@ -88,6 +89,8 @@ void *device_alloc(std::size_t bytes, int device);
 void device_free(void *p, int device);
 /// Bytes held by the scratch cache of `device`: idle (cached) and in use (live)
 void cache_usage(int device, std::size_t *cached, std::size_t *live);
+/// Allocator tune keys (alloc.max_cached, alloc.cross_stream_frees): read into *get, write *set
+void alloc_tune(const char *key, long long *get, const long long *set);
 
 /// RAII scratch buffer on a device, freed in stream order
 struct Scratch {
@@ -218,7 +221,7 @@ struct CopyTune {
     int pair = 0;  ///< tiled kernel, 8-byte elements: two elements per lane access where the runs allow (-1 = never)
     int order = 0; ///< ... with pairs, the source chain first when the destination chain would take the
                    ///< source's contiguous dim (-1 = always the destination chain first)
-    int last_pair = 0; ///< read-back ("copy.last_pair"): the last tiled launch's paired phases (1 reads, 2 writes)
+    std::atomic<int> last_pair{0}; ///< read-back ("copy.last_pair"): the last tiled launch's paired phases (1 reads, 2 writes)
 };
 extern CopyTune g_copy_tune;
 struct GemmTune {
@@ -263,11 +266,26 @@ struct BsrTune {
     long kron_mfma_min_cols = 8; ///< ... from this many rhs columns
     long kron_lds_pad = 0;       ///< tools: LDS bytes per workgroup of that kernel (caps its residency)
     int kron_pack = 1;           ///< ... below 16 rhs columns: a wave's 16 column slots span several rows (0 = off)
-    int last = 0; ///< read-back ("bsr.last_kernel"): the 9-point 3x3 form of the last launch -- 1 one thread
-                  ///< per block, 2 split rows, 3 row chunks, 4 lattice tiles, 5 Kronecker on MFMA, 6 the same
-                  ///< with packed column slots, 0 another kernel
+    /// read-back ("bsr.last_kernel"; atomic: launches may come from several host threads): the form
+    /// of the last launch -- 1 one thread per block (3x3), 2 split rows (3x3), 3 row chunks (3x3),
+    /// 4 lattice tiles (3x3), 5 Kronecker on MFMA, 6 the same with packed column slots, 7 12x12 blocks
+    /// by LDS-DMA, 8 the same with packed slots, 9 12x12 blocks through registers, 10 12x12 fragment
+    /// gathers (9 blocks per row), 11 12x12 generic rows, 0 another kernel
+    std::atomic<int> last{0};
 };
 extern BsrTune g_bsr_tune;
+
+/// The LDS-DMA overrun class (39cd2bc): a DMA pass writes a whole row of 16-B lanes into LDS --
+/// lanes past the data included, they write zeros -- so a launch needs dynamic LDS for every pass
+/// it issues, not only for the data.  Each LDS-DMA launcher checks its size against the passes
+/// its kernel's loop issues (recomputed here from the loop bounds, independently of the sizing).
+inline void check_dma_lds(const char *kernel, size_t lds, long passes, long lanes_per_pass,
+                   long extra_bytes = 0) {
+    const long need = passes * lanes_per_pass * 16 + extra_bytes;
+    if ((long)lds < need)
+        throw Error(std::string("bsr: internal LDS sizing error in ") + kernel + ": " +
+                    std::to_string(lds) + " bytes for DMA passes needing " + std::to_string(need));
+}
 
 /// Fill `n` elements of type `t` with zeros
 void launch_zero(void *p, std::size_t bytes, int device);

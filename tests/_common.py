@@ -179,3 +179,25 @@ def rel_err(a, b):
     b = np.asarray(b, dtype=np.complex128).ravel()
     den = np.linalg.norm(b)
     return np.linalg.norm(a - b) / (den if den > 0 else 1.0)
+
+
+def stencil_jj(dims, kind="stencil", rng=None, cut=None):
+    """jj coordinates (x y z t s c) of a periodic 9-point stencil on `dims`, or 9 random sites;
+    `cut`: blocks whose neighbour crosses dimension 0 past that coordinate get column -1"""
+    vol = int(np.prod(dims))
+    sites = np.array(np.unravel_index(np.arange(vol), dims)).T
+    jj = np.zeros((vol, 9, 6), np.int32)
+    if kind == "random":
+        jj[:, :, :4] = sites[rng.integers(0, vol, (vol, 9))]
+        return jj
+    jj[:, 0, :4] = sites
+    k = 1
+    for d in range(4):
+        for s in (-1, 1):
+            c = sites.copy()
+            c[:, d] = (c[:, d] + s) % dims[d]
+            jj[:, k, :4] = c
+            if cut is not None and d == 0:
+                jj[(sites[:, 0] + s < 0) | (sites[:, 0] + s >= cut), k, 0] = -1
+            k += 1
+    return jj

@@ -441,6 +441,34 @@ int main() {
         CHECK(thrown, "invalid copy labels must throw");
     }
 
+    // ---- runtime features (runtime_features.h:55-68, performance.h:356-434): reportTimings
+    //      reports only while time tracking is on -- SB_TRACK_TIME=1 from the start, or
+    //      getTrackingTime() assigned at run time ----
+    {
+        const bool from_env = std::getenv("SB_TRACK_TIME") && std::atoi(std::getenv("SB_TRACK_TIME"));
+        CHECK(getTrackingTime() == from_env, "getTrackingTime follows SB_TRACK_TIME");
+        std::ostringstream before;
+        reportTimings(before);
+        // the copies above (upload / download) ran with the timers on only under SB_TRACK_TIME
+        CHECK((before.str().find("\ncopy ") != std::string::npos) == from_env,
+              "reportTimings reports the copies exactly when SB_TRACK_TIME is on");
+        getTrackingTime() = true;
+        resetTimings();
+        std::vector<Z> h(24, Z(1));
+        Z *d = upload<2>(h, Coor<2>{4, 6}, "ab");
+        (void)download<2>(d, Coor<2>{4, 6}, "ab");
+        deallocate(d, createGpuContext(0));
+        std::ostringstream after;
+        reportTimings(after);
+        CHECK(after.str().find("\ncopy ") != std::string::npos,
+              "reportTimings after getTrackingTime() = true");
+        getTrackingTime() = false;
+        std::ostringstream off;
+        reportTimings(off);
+        CHECK(off.str().empty(), "reportTimings silent with tracking off");
+        static_assert(supported_type<Z>::value && !supported_type<char>::value, "supported_type");
+    }
+
     if (failures == 0) std::printf("DROPIN OK\n");
     return failures == 0 ? 0 : 1;
 }

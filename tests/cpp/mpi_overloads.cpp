@@ -35,6 +35,8 @@ void use_mpi_overloads(MPI_Comm comm) {
     bsr_krylov<2, 2, 3, 3, Z>(Z(1), op, "ab", "AB", &px, 1, "ABn", Coor<3>{}, Coor<3>{4, 4, 2},
                               Coor<3>{4, 4, 2}, &c0, Z(0), &px, "abn", Coor<3>{}, Coor<3>{4, 4, 2},
                               Coor<3>{4, 4, 2}, 0, &v1, &gpu, comm, SlowToFast);
+    MatrixLayout lx, ly;
+    bsr_get_preferred_layout<2, 2, Z>(op, 1, &gpu, comm, SlowToFast, &lx, &ly);
     Storage_handle sto = nullptr;
     create_storage<2, Z>(d, SlowToFast, "f", "", 0, NoChecksum, comm, &sto);
     open_storage<2, Z>("f", true, comm, &sto);
@@ -52,4 +54,17 @@ void use_mpi_overloads(MPI_Comm comm) {
     read_storage_header("f", SlowToFast, vt, md, dims, comm);
     check_storage<2, Z>(sto, comm);
     close_storage<2, Z>(sto, comm);
+}
+
+// support API of the reference that needs no communicator (platform.h:818-821,
+// runtime_features.h:15-158)
+static_assert(supported_type<Z>::value && supported_type<const float>::value &&
+                  supported_type<int>::value && !supported_type<char>::value,
+              "supported_type");
+bool runtime_features() {
+    getTrackingTime() = true;
+    getTrackingMemory() = false;
+    return getLogLevel() + getDebugLevel() >= 0 && getUseMPINonBlock() && getUseAlltoall() &&
+           getUseMPIGpu() >= -1 && getMaxCacheGiBCpu() < 1e9 && getMaxCacheGiBGpu() < 1e9 &&
+           !getTrackingTimeSync();
 }

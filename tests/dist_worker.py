@@ -504,6 +504,51 @@ def case_split(sb, comm, rank, n, dev, ncols=3):
 LATTICE_GRID = {1: [1, 1, 1], 2: [2, 1, 1], 3: [3, 1, 1], 4: [2, 2, 1], 8: [2, 2, 2]}
 
 
+def case_reduce(sb, comm, rank, n, dev, transport):
+    """The contraction's partial outputs summed by one RCCL collective (ncclReduce into an owner,
+    ncclAllReduce into a replicated output) and by the point-to-point Add copy (dist.reduce 0):
+    both exact against the oracle on integer data, and the collective is what runs with RCCL."""
+    L, nn = 4, 2
+    d0 = [L, nn, 4, L, L, L * n, 3]
+    dr = [L, nn, 4, nn, 4]
+    p0 = sb.basic_partitioning("tnsxyzc", d0, [1, 1, 1, 1, 1, n, 1], "z", n, 1)
+    g0 = gen("int", vol(d0), 11, np.complex128)
+    g1 = gen("int", vol(d0), 12, np.complex128)
+    gr = gen("int", vol(dr), 13, np.complex128)
+    v0 = scatter(sb, g0, d0, p0, rank, 1, dev)
+    v1 = scatter(sb, g1, d0, p0, rank, 1, dev)
+    z7, z5 = [0] * 7, [0] * 5
+    alpha, beta = 2 - 1j, 0.5 + 1j
+    ref = gr.copy()
+    oracle_contraction(alpha, "tnsxyzc", z7, d0, d0, False, g0, "tNSxyzc", z7, d0, d0, True, g1,
+                       beta, "tNSns", z5, dr, dr, ref)
+    owner = n - 1  # not rank 0
+    outputs = {
+        "owner": [([0] * 5, dr if q == owner else [0] * 5) for q in range(n)],
+        "replicated": [([0] * 5, dr)] * n,
+    }
+    for mode in (1, 0):
+        sb.tune_set("dist.reduce", mode)
+        try:
+            for name, pr in outputs.items():
+                vr = scatter(sb, gr, dr, pr, rank, 1, dev)
+                if vr[0].numel() == 0:
+                    vr = [torch.zeros(1, dtype=torch.complex128, device=dev)]
+                sb.tune_set("dist.reduce_calls", 0)
+                sb.contraction(alpha, p0, z7, d0, d0, "tnsxyzc", False, v0, p0, z7, d0, d0,
+                               "tNSxyzc", True, v1, beta, pr, z5, dr, dr, "tNSns", vr, comm=comm)
+                torch.cuda.synchronize()
+                calls = sb.tune_get("dist.reduce_calls")
+                if transport == "rccl" and mode == 1:
+                    assert calls > 0, ("collective reduce not used", name)
+                else:
+                    assert calls == 0, ("collective reduce used", name, mode, transport)
+                if name == "replicated" or rank == owner:
+                    assert np.array_equal(vr[0].cpu().numpy(), ref), ("reduce", name, mode)
+        finally:
+            sb.tune_set("dist.reduce", 1)
+
+
 def case_golden(sb, comm, rank, n, dev):
     grid = LATTICE_GRID.get(n, [n, 1, 1])
     for case in manifest("contraction"):
@@ -525,14 +570,22 @@ def case_golden(sb, comm, rank, n, dev):
             if vr[0].numel() == 0:
                 vr = [torch.zeros(1, dtype=torch.complex128, device=dev)]
             beta = complex(*case["beta"])
-            sb.contraction(complex(*case["alpha"]), p0, case["from0"], case["size0"], d0,
-                           case["o0"], case["conj0"], v0, p1, case["from1"], case["size1"], d1,
-                           case["o1"], case["conj1"], v1, beta, pr, case["fromr"], case["sizer"],
-                           dr, case["o_r"], vr, comm=comm)
-            torch.cuda.synchronize()
-            out = gather(np.zeros_like(gr), dr, pr, 1, vr[:1] if rank == 0 else [vr[0][:0]])
-            errs = component_errors(out, output(case, np.complex128))
-            assert max(errs) < 1e-10, ("golden", case["id"], shape, errs)
+            for mode in (1, 0):  # RCCL collective reduction / point-to-point Add copy
+                sb.tune_set("dist.reduce", mode)
+                vr = scatter(sb, gr, dr, pr, rank, 1, dev)
+                if vr[0].numel() == 0:
+                    vr = [torch.zeros(1, dtype=torch.complex128, device=dev)]
+                try:
+                    sb.contraction(complex(*case["alpha"]), p0, case["from0"], case["size0"], d0,
+                                   case["o0"], case["conj0"], v0, p1, case["from1"],
+                                   case["size1"], d1, case["o1"], case["conj1"], v1, beta, pr,
+                                   case["fromr"], case["sizer"], dr, case["o_r"], vr, comm=comm)
+                finally:
+                    sb.tune_set("dist.reduce", 1)
+                torch.cuda.synchronize()
+                out = gather(np.zeros_like(gr), dr, pr, 1, vr[:1] if rank == 0 else [vr[0][:0]])
+                errs = component_errors(out, output(case, np.complex128))
+                assert max(errs) < 1e-10, ("golden", case["id"], shape, mode, errs)
 
 
 def _rand_partition(sb, rng, labels, dims, n):
@@ -638,7 +691,7 @@ def main():
         comm = sb.Comm.from_torch_distributed(dev_idx)
     else:
         comm = sb.Comm.host_staged(dev_idx)
-    cases = os.environ.get("SBX_TEST_CASES", "copy,contr,bsr,kron,dense,storage,fuzz,golden,split").split(",")
+    cases = os.environ.get("SBX_TEST_CASES", "copy,contr,bsr,kron,dense,storage,fuzz,golden,split,reduce").split(",")
     if "copy" in cases:
         case_copy(sb, comm, rank, n, dev)
     if "contr" in cases:
@@ -655,6 +708,8 @@ def main():
         case_fuzz(sb, comm, rank, n, dev)
     if "golden" in cases:
         case_golden(sb, comm, rank, n, dev)
+    if "reduce" in cases:
+        case_reduce(sb, comm, rank, n, dev, transport)
     if "split" in cases:
         case_split(sb, comm, rank, n, dev)
     dist.barrier()

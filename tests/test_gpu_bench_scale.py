@@ -29,7 +29,7 @@ def test_bench_n2_scale_check(gpu, config):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
-           "--config", config, "--L", "8", "--n", "16", "--chain-L", "4", "--chain-T", "8",
+           "--config", config, "--L", "8", "--ncols", "16", "--chain-L", "4", "--chain-T", "8",
            "--share-gpu", "rccl"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-6000:])

@@ -265,3 +265,79 @@ def test_bsr_12x12_kernel_forms(gpu, variant, ncols, dtype):
         sb.tune_set("bsr.variant", 0)
         sb.tune_set("bsr.blk_dma", -1)
     assert np.array_equal(ty.cpu().numpy(), yref)
+
+
+@pytest.mark.parametrize("dtype,ncols,form", [(np.complex64, 16, 8), (np.complex64, 13, 8),
+                                              (np.complex128, 12, 7)])
+def test_bsr_12x12_skipped_blocks_dma(gpu, dtype, ncols, form):
+    """Blocks with column -1 on the LDS-DMA 12x12 kernel (packed slots for complex<float>): a
+    skipped block's slot must not read past the caller's arrays -- with 13-16 rhs columns the x
+    part of a packed complex<float> slot is longer than a value block, and the last block of the
+    last row is skipped here -- and must contribute nothing (exact vs the oracle)."""
+    import torch
+    import superbblas_amd as sb
+    from _common import TYPE_OF
+    L, spin, color = 4, 4, 3
+    dim, ii, jj, vals, nb = lattice_operator(L, spin, color, dtype)
+    b = spin * color
+    vol = L ** 4
+    jj = jj.reshape(vol, nb, 6).copy()
+    jj[::3, 1, :] = -1           # every third row skips its -x block
+    jj[-1, nb - 1, :] = -1       # the very last block of the value array
+    jj[-2, :, :] = -1            # a row with no blocks at all
+    jj = jj.reshape(-1)
+    g = np.arange(vol * b * ncols)
+    x = ((g % 9 - 4) + 1j * (g % 5 - 2)).astype(dtype)
+    yref = np.zeros(vol * b * ncols, dtype)
+    oracle_bsr(TYPE_OF[np.dtype(dtype)], dim, 0, vol, b, b, ii, jj, vals, False, x, ncols, True,
+               yref, ncols, True, ncols, 1.0)
+    full = [([0] * 6, dim)]
+    blk = [1, 1, 1, 1, spin, color]
+    # the values exactly as long as the operator (no slack after the last block)
+    tv = torch.from_numpy(vals).to(gpu)
+    op = sb.create_bsr(full, dim, full, dim, blk, blk, False, [torch.from_numpy(ii).to(gpu)],
+                       [torch.from_numpy(jj).to(gpu)], [tv])
+    dimx = [1, L, L, L, L, spin, color, ncols]
+    ty = torch.full((vol * b * ncols,), 3.0, dtype=getattr(torch, np.dtype(dtype).name), device=gpu)
+    sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", [([0] * 8, dimx)], "pXYZTSCn", [0] * 8, dimx,
+                  dimx, [torch.from_numpy(x).to(gpu)], 0.0, [([0] * 8, dimx)], "pxyztscn",
+                  [0] * 8, dimx, dimx, "p", [ty])
+    torch.cuda.synchronize()
+    used = sb.tune_get("bsr.last_kernel")
+    op.destroy()
+    assert used == form, used
+    assert np.array_equal(ty.cpu().numpy(), yref)
+
+
+@pytest.mark.parametrize("spin,color,ncols,form", [(1, 3, 12, 2), (1, 3, 2, 1), (4, 3, 3, 7),
+                                                   (4, 3, 12, 7)])
+def test_bsr_image_side_kernel_form(gpu, spin, color, ncols, form):
+    """A^H products (x with the image labels) run the same specialised kernels as A (the
+    transposed operator carries its domain extent), exact vs the oracle's adjoint loop."""
+    import torch
+    import superbblas_amd as sb
+    from _common import oracle_bsr_adjoint
+    L = 4
+    dim, ii, jj, vals, nb = lattice_operator(L, spin, color)
+    b = spin * color
+    vol = L ** 4
+    n = vol * b * ncols
+    g = np.arange(n)
+    x = ((g % 7 - 3) + 1j * (g % 5 - 2)).astype(np.complex128)
+    yref = np.zeros(n, np.complex128)
+    oracle_bsr_adjoint(T_CDOUBLE, dim, 0, vol, b, b, ii, jj, vals, False, x, ncols, True, yref,
+                       ncols, True, vol * b, ncols, 1.0)
+    full = [([0] * 6, dim)]
+    blk = [1, 1, 1, 1, spin, color]
+    op = sb.create_bsr(full, dim, full, dim, blk, blk, False, [torch.from_numpy(ii).to(gpu)],
+                       [torch.from_numpy(jj).to(gpu)], [torch.from_numpy(vals).to(gpu)])
+    dimx = [1, L, L, L, L, spin, color, ncols]
+    ty = torch.zeros(n, dtype=torch.complex128, device=gpu)
+    sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", [([0] * 8, dimx)], "pxyztscn", [0] * 8, dimx, dimx,
+                  [torch.from_numpy(x).to(gpu)], 0.0, [([0] * 8, dimx)], "pXYZTSCn", [0] * 8,
+                  dimx, dimx, "p", [ty])
+    torch.cuda.synchronize()
+    used = sb.tune_get("bsr.last_kernel")
+    op.destroy()
+    assert used == form, used
+    assert np.array_equal(ty.cpu().numpy(), yref)

@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 from _common import T_CDOUBLE, oracle_bsr, rel_err
-from test_gpu_bsr_tile import stencil_jj
+from _common import stencil_jj
 
 pytestmark = pytest.mark.gpu
 
