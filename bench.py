@@ -113,15 +113,22 @@ def host_cpu():
     omp = os.environ.get("OMP_NUM_THREADS")
     threads = min(avail, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else avail
     model = "unknown"
+    cores = set()
     try:
         with open("/proc/cpuinfo") as f:
+            phys = core = None
             for line in f:
-                if line.startswith("model name"):
+                if line.startswith("model name") and model == "unknown":
                     model = line.split(":", 1)[1].strip()
-                    break
+                elif line.startswith("physical id"):
+                    phys = line.split(":", 1)[1].strip()
+                elif line.startswith("core id"):
+                    core = line.split(":", 1)[1].strip()
+                    cores.add((phys, core))
     except OSError:  # pragma: no cover
         pass
-    return {"threads": threads, "affinity_cpus": avail, "nproc": os.cpu_count(), "model": model}
+    return {"threads": threads, "affinity_cpus": avail, "nproc": os.cpu_count(), "model": model,
+            "physical_cores": len(cores) or None}
 
 
 REF_EXES = (("openblas", "ref_bench"), ("mkl", "ref_bench_mkl"))
@@ -167,13 +174,23 @@ def cpu_baseline():
     cpu = host_cpu()
     best, tried = best_ref(["contraction", 16, 64, 2], [cpu["threads"]], "gflops")
     if best is not None:
-        return {"value": round(best["gflops"], 2), "unit": "GFLOP/s", "cores": best["threads"],
-                "kind": "reference",
-                "sample": "superbblas::contraction tnsxyzc x tNSxyzc -> tNSns, 16^4, n=64, "
-                          "complex<double>, 2 timed reps after 1 warm-up (OpenMP over t, one "
-                          "zgemm per t; BLAS %s)" % best["blas"],
-                "blas_tried_GFLOPs": tried, "cpu_model": cpu["model"], "nproc": cpu["nproc"],
-                "affinity_cpus": cpu["affinity_cpus"]}
+        out = {"value": round(best["gflops"], 2), "unit": "GFLOP/s", "cores": best["threads"],
+               "kind": "reference",
+               "sample": "superbblas::contraction tnsxyzc x tNSxyzc -> tNSns, 16^4, n=64, "
+                         "complex<double>, 2 timed reps after 1 warm-up (OpenMP over t, one "
+                         "zgemm per t; BLAS %s)" % best["blas"],
+               "blas_tried_GFLOPs": tried, "cpu_model": cpu["model"], "nproc": cpu["nproc"],
+               "physical_cores": cpu["physical_cores"], "affinity_cpus": cpu["affinity_cpus"],
+               # the headline is the job's CPU share: the GPU box grants 16 host threads per GPU
+               # (its OMP_NUM_THREADS); the whole host is not measured, only estimated below
+               "threads_policy": "OMP_NUM_THREADS of the box (its CPU share per GPU)"}
+        one = run_ref(["contraction", 16, 64, 1], 1, best["blas"])
+        if one is not None:
+            out["value_1thread"] = round(one["gflops"], 2)
+            if cpu["physical_cores"]:
+                # an upper bound (perfect scaling over every physical core), NOT a measurement
+                out["whole_host_linear_estimate"] = round(one["gflops"] * cpu["physical_cores"], 1)
+        return out
     # restatement (oracle/oracle.c) on a small sample
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from _common import oracle_gemm, random_valued
