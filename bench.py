@@ -1208,8 +1208,7 @@ def bsr_bench(sb, dev, L, ncols_list=(1, 12, 64), reps=5):
             1: "bsr_ell9_row_kernel (one thread per nonzero block, values by LDS-DMA)",
             2: "bsr_ell9_split_kernel (a thread per block row x 3 nonzero blocks x rhs lane, "
                "partial products summed through LDS, XCD halves interleaved)",
-            3: "bsr_ell9_kernel (row chunks, values by LDS-DMA, XCD halves interleaved)",
-            4: "bsr_tile_kernel (lattice tiles)"}.get(sb.tune_get("bsr.last_kernel"), "other")
+            3: "bsr_ell9_kernel (row chunks, values by LDS-DMA, XCD halves interleaved)"}.get(sb.tune_get("bsr.last_kernel"), "other")
         out.update({p + "GFLOPs": round(flops / t / 1e9, 1), p + "GBps": round(bytes_ / t / 1e9, 1),
                     p + "ms": round(t * 1e3, 4), p + "kernel_ms": round(tk * 1e3, 4),
                     p + "kernel_GBps": round(bytes_ / tk / 1e9, 1),

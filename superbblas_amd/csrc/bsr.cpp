@@ -23,20 +23,10 @@
 
 namespace sbx {
 
-/// Lattice-tile plan of a 9-nonzero operator (see build_tile_plan); device arrays
-struct BsrTilePlan {
-    int R = 0, S = 0, nd = 0;
-    long nchunks = 0;
-    int *rows = nullptr;
-    unsigned *ent = nullptr;
-    int *staged = nullptr;
-};
-
 struct BsrComp {
     int dev = -1;
     long block_rows = 0;
     long x_rows = 0; // domain rows (elements) of the component
-    BsrTilePlan tile;
     int *ii = nullptr; // device CSR row pointers
     int *jj = nullptr; // device first domain index per nonzero block
     const void *v = nullptr;
@@ -67,140 +57,9 @@ struct BsrOp {
             if (c.ii) (void)hipFree(c.ii);
             if (c.jj) (void)hipFree(c.jj);
             if (c.owned_v) (void)hipFree(c.owned_v);
-            if (c.tile.rows) (void)hipFree(c.tile.rows);
-            if (c.tile.ent) (void)hipFree(c.tile.ent);
-            if (c.tile.staged) (void)hipFree(c.tile.staged);
         }
     }
 };
-
-namespace {
-
-/// Lattice-tile plan for the 9-nonzero-block operators (the lattice stencils).  Each x row
-/// gathered by the row-chunk kernel is read by the vector-memory pipeline once per nonzero
-/// block that uses it, and that pipeline, not HBM, bounds the chunked kernel (PMC: TA/TD 62-71 %
-/// busy at n = 12, 90 % at n = 64; the same time with all 9 blocks on the row's own site).  The
-/// plan cuts the image sites into tiles of R = 16 block rows (extent 2 in up to four site dims,
-/// the largest first) and, per tile, lists the domain rows used by two or more of its rows:
-/// those are read into LDS once and shared (a 2x2x2x2 tile of a 9-point stencil reads its own
-/// 16 sites there and 4 halo rows per site from memory: 1 + 4 instead of 9 x-row fetches per
-/// site).  Per block row: up to `nd` direct entries (domain rows read from memory), padded with
-/// j = 15, then `nnz` staged entries (slots); a row with more than `nd` direct rows moves the
-/// rest to the staged list.  Only the processing order and the summation order of each row's
-/// blocks change (direct blocks first), not the operator.
-void build_tile_plan(BsrComp &bc, const std::vector<long> &site, int nnz, int R, int nd) {
-    const int ns = (int)site.size();
-    long nrows = 1;
-    for (long v : site) nrows *= v;
-    if (nrows != bc.block_rows || (long)bc.h_jj.size() != bc.block_rows * nnz) return;
-    std::vector<long> ext(ns, 1);
-    long prod = 1;
-    while (prod < R) {
-        int best = -1;
-        for (int d = 0; d < ns; ++d)
-            if (site[d] / ext[d] >= 2 && (best < 0 || site[d] / ext[d] > site[best] / ext[best]))
-                best = d;
-        if (best < 0) break;
-        ext[best] *= 2;
-        prod *= 2;
-    }
-    std::vector<long> tg(ns), st(ns, 1);
-    long ntiles = 1;
-    for (int d = ns - 1; d >= 0; --d) {
-        tg[d] = (site[d] + ext[d] - 1) / ext[d];
-        ntiles *= tg[d];
-        if (d + 1 < ns) st[d] = st[d + 1] * site[d + 1];
-    }
-    std::vector<int> rows((std::size_t)ntiles * R, -1);
-    std::vector<long> tc(ns), lc(ns);
-    for (long t = 0; t < ntiles; ++t) {
-        long q = t;
-        for (int d = ns - 1; d >= 0; --d) {
-            tc[d] = q % tg[d];
-            q /= tg[d];
-        }
-        int k = 0;
-        for (long l = 0; l < prod; ++l) {
-            long u = l, row = 0;
-            bool in = true;
-            for (int d = ns - 1; d >= 0; --d) {
-                lc[d] = u % ext[d];
-                u /= ext[d];
-                const long c = tc[d] * ext[d] + lc[d];
-                in &= c < site[d];
-                row += c * st[d];
-            }
-            if (in) rows[(std::size_t)t * R + k++] = (int)row;
-        }
-    }
-    const int NE = nd + nnz;
-    const unsigned NONE = 15u << 28;
-    std::vector<unsigned> ent((std::size_t)ntiles * R * NE, NONE);
-    std::vector<std::vector<int>> staged(ntiles);
-    int S = 0;
-    for (long t = 0; t < ntiles; ++t) {
-        const int *rw = &rows[(std::size_t)t * R];
-        std::vector<int> cols;
-        for (int i = 0; i < R && rw[i] >= 0; ++i)
-            for (int j = 0; j < nnz; ++j) {
-                const int c = bc.h_jj[(std::size_t)rw[i] * nnz + j];
-                if (c >= 0) cols.push_back(c);
-            }
-        std::sort(cols.begin(), cols.end());
-        std::vector<int> &sl = staged[t];
-        for (std::size_t a = 0; a < cols.size();) {
-            std::size_t b = a;
-            while (b < cols.size() && cols[b] == cols[a]) ++b;
-            if (b - a >= 2) sl.push_back(cols[a]);
-            a = b;
-        }
-        auto is_staged = [&](int c) { return std::binary_search(sl.begin(), sl.end(), c); };
-        // rows with more than nd direct blocks stage the rest
-        std::vector<int> extra;
-        for (int i = 0; i < R && rw[i] >= 0; ++i) {
-            int ndir = 0;
-            for (int j = 0; j < nnz; ++j) {
-                const int c = bc.h_jj[(std::size_t)rw[i] * nnz + j];
-                if (c >= 0 && !is_staged(c) && ++ndir > nd) extra.push_back(c);
-            }
-        }
-        if (!extra.empty()) {
-            sl.insert(sl.end(), extra.begin(), extra.end());
-            std::sort(sl.begin(), sl.end());
-            sl.erase(std::unique(sl.begin(), sl.end()), sl.end());
-        }
-        S = std::max(S, (int)sl.size());
-        for (int i = 0; i < R && rw[i] >= 0; ++i) {
-            unsigned *e = &ent[((std::size_t)t * R + i) * NE];
-            int kd = 0, ks = nd;
-            for (int j = 0; j < nnz; ++j) {
-                const int c = bc.h_jj[(std::size_t)rw[i] * nnz + j];
-                if (c < 0) continue;
-                const auto it = std::lower_bound(sl.begin(), sl.end(), c);
-                if (it != sl.end() && *it == c)
-                    e[ks++] = ((unsigned)j << 28) | (unsigned)(it - sl.begin());
-                else
-                    e[kd++] = ((unsigned)j << 28) | (unsigned)c;
-            }
-        }
-    }
-    std::vector<int> st_all((std::size_t)ntiles * std::max(S, 1), -1);
-    for (long t = 0; t < ntiles; ++t)
-        std::copy(staged[t].begin(), staged[t].end(), st_all.begin() + (std::size_t)t * std::max(S, 1));
-    BsrTilePlan &p = bc.tile;
-    p.R = R;
-    p.S = std::max(S, 1);
-    p.nd = nd;
-    p.nchunks = ntiles;
-    SBX_HIP_CHECK(hipMalloc(&p.rows, sizeof(int) * rows.size()));
-    SBX_HIP_CHECK(hipMalloc(&p.ent, sizeof(unsigned) * ent.size()));
-    SBX_HIP_CHECK(hipMalloc(&p.staged, sizeof(int) * st_all.size()));
-    SBX_HIP_CHECK(hipMemcpy(p.rows, rows.data(), sizeof(int) * rows.size(), hipMemcpyHostToDevice));
-    SBX_HIP_CHECK(hipMemcpy(p.ent, ent.data(), sizeof(unsigned) * ent.size(), hipMemcpyHostToDevice));
-    SBX_HIP_CHECK(hipMemcpy(p.staged, st_all.data(), sizeof(int) * st_all.size(), hipMemcpyHostToDevice));
-}
-
-} // namespace
 
 BsrOp *bsr_create(int nd, int ni, int dtype, const std::vector<std::vector<Range>> &pi,
                   const Coor &dimi, const std::vector<std::vector<Range>> &pd, const Coor &dimd,
@@ -313,15 +172,6 @@ BsrOp *bsr_create(int nd, int ni, int dtype, const std::vector<std::vector<Range
         if (!op->is_kron) {
             bc.h_rowptr = std::move(rowptr);
             bc.h_jj = std::move(hjj);
-            // 3x3 blocks, 9 per row, domain rows < 2^28: the lattice-tile plan (image sites
-            // slow to fast)
-            if (bi == 3 && bd == 3 && bc.nnz_per_row == 9 && volume(rd.size) < (1L << 28)) {
-                std::vector<long> site;
-                for (int d = 0; d < ni; ++d)
-                    if (ri.size[d] / blocki[d] > 1) site.push_back(ri.size[d] / blocki[d]);
-                if (g_bsr_tune.tile && g_bsr_tune.tile_rows >= 2 && g_bsr_tune.tile_rows <= 128)
-                    build_tile_plan(bc, site, 9, g_bsr_tune.tile_rows, 4);
-            }
         }
         op->comps.push_back(bc);
     }
@@ -743,13 +593,6 @@ void bsr_krylov(const BsrOp &op, const Scalar &alpha, const std::string &oi,
                 d.v = bc.v;
                 d.block_im_fast = op.block_im_fast;
                 d.num_nnz_per_row = bc.nnz_per_row;
-                d.tile_R = bc.tile.R;
-                d.tile_S = bc.tile.S;
-                d.tile_nd = bc.tile.nd;
-                d.tile_chunks = bc.tile.nchunks;
-                d.tile_rows = bc.tile.rows;
-                d.tile_ent = bc.tile.ent;
-                d.tile_staged = bc.tile.staged;
                 d.x = my_x[c];
                 d.x_rows = bc.x_rows;
                 d.x_row_major = my_lx[c].row_major;

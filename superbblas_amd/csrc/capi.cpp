@@ -406,38 +406,20 @@ int sbx_tune_set(const char *key, long long value) {
         const std::string k(key);
         if (k == "copy.budget") g_copy_tune.budget = (long)value;
         else if (k == "copy.run") g_copy_tune.run = (long)value;
-        else if (k == "copy.kernel") g_copy_tune.kernel = (int)value;
         else if (k == "copy.nt") g_copy_tune.nt = (int)value;
         else if (k == "copy.max_elems") g_copy_tune.max_elems = (long)value;
         else if (k == "copy.pair") g_copy_tune.pair = (int)value;
         else if (k == "copy.order") g_copy_tune.order = (int)value;
         else if (k == "gemm.max_bytes") g_gemm_tune.max_bytes = (long)value;
         else if (k == "bsr.variant") g_bsr_tune.variant = (int)value;
-        else if (k == "bsr.ell9") g_bsr_tune.ell9 = (int)value;
-        else if (k == "bsr.ell9_lds") g_bsr_tune.ell9_lds = (long)value;
-        else if (k == "bsr.colsplit") g_bsr_tune.colsplit = (long)value;
-        else if (k == "bsr.tile") g_bsr_tune.tile = (int)value;
-        else if (k == "bsr.tile_min_cols") g_bsr_tune.tile_min_cols = (long)value;
-        else if (k == "bsr.tile_slab") g_bsr_tune.tile_slab = (long)value;
         else if (k == "bsr.row_max_cols") g_bsr_tune.row_max_cols = (long)value;
-        else if (k == "bsr.row_dma") g_bsr_tune.row_dma = (int)value;
         else if (k == "bsr.split_max_cols") g_bsr_tune.split_max_cols = (long)value;
         else if (k == "bsr.split_cw") g_bsr_tune.split_cw = (int)value;
         else if (k == "bsr.split_jb") g_bsr_tune.split_jb = (int)value;
-        else if (k == "bsr.split_nt") g_bsr_tune.split_nt = (int)value;
         else if (k == "bsr.split_ilv") g_bsr_tune.split_ilv = (int)value;
-        else if (k == "bsr.split_ovl") g_bsr_tune.split_ovl = (int)value;
-        else if (k == "bsr.split_rw") g_bsr_tune.split_rw = (int)value;
         else if (k == "bsr.kron_mfma") g_bsr_tune.kron_mfma = (int)value;
         else if (k == "bsr.kron_mfma_min_cols") g_bsr_tune.kron_mfma_min_cols = (long)value;
-        else if (k == "bsr.kron_lds_pad") g_bsr_tune.kron_lds_pad = (long)value;
         else if (k == "bsr.kron_pack") g_bsr_tune.kron_pack = (int)value;
-        else if (k == "bsr.blk_dma") g_bsr_tune.blk_dma = (int)value;
-        else if (k == "bsr.blk_pack") g_bsr_tune.blk_pack = (int)value;
-        else if (k == "bsr.ell9_ilv") g_bsr_tune.ell9_ilv = (int)value;
-        else if (k == "bsr.tile_max_cols") g_bsr_tune.tile_max_cols = (long)value;
-        else if (k == "bsr.tile_rows") g_bsr_tune.tile_rows = (int)value;
-        else if (k == "bsr.probe") g_bsr_tune.probe = value;
         else if (k == "gemm.m3") g_gemm_tune.m3 = (int)value;
         else if (k == "gemm.splits") g_gemm_tune.splits = (int)value;
         else if (k == "gemm.t48") g_gemm_tune.t48 = (int)value;
@@ -455,7 +437,6 @@ int sbx_tune_get(const char *key, long long *value) {
         const std::string k(key);
         if (k == "copy.budget") *value = g_copy_tune.budget;
         else if (k == "copy.run") *value = g_copy_tune.run;
-        else if (k == "copy.kernel") *value = g_copy_tune.kernel;
         else if (k == "copy.nt") *value = g_copy_tune.nt;
         else if (k == "copy.max_elems") *value = g_copy_tune.max_elems;
         else if (k == "copy.pair") *value = g_copy_tune.pair;
@@ -463,30 +444,14 @@ int sbx_tune_get(const char *key, long long *value) {
         else if (k == "copy.last_pair") *value = g_copy_tune.last_pair;
         else if (k == "gemm.max_bytes") *value = g_gemm_tune.max_bytes;
         else if (k == "bsr.variant") *value = g_bsr_tune.variant;
-        else if (k == "bsr.ell9") *value = g_bsr_tune.ell9;
-        else if (k == "bsr.ell9_lds") *value = g_bsr_tune.ell9_lds;
-        else if (k == "bsr.colsplit") *value = g_bsr_tune.colsplit;
-        else if (k == "bsr.tile") *value = g_bsr_tune.tile;
-        else if (k == "bsr.tile_min_cols") *value = g_bsr_tune.tile_min_cols;
-        else if (k == "bsr.tile_slab") *value = g_bsr_tune.tile_slab;
         else if (k == "bsr.row_max_cols") *value = g_bsr_tune.row_max_cols;
-        else if (k == "bsr.row_dma") *value = g_bsr_tune.row_dma;
         else if (k == "bsr.split_max_cols") *value = g_bsr_tune.split_max_cols;
         else if (k == "bsr.split_cw") *value = g_bsr_tune.split_cw;
         else if (k == "bsr.split_jb") *value = g_bsr_tune.split_jb;
-        else if (k == "bsr.split_nt") *value = g_bsr_tune.split_nt;
         else if (k == "bsr.split_ilv") *value = g_bsr_tune.split_ilv;
-        else if (k == "bsr.split_ovl") *value = g_bsr_tune.split_ovl;
-        else if (k == "bsr.split_rw") *value = g_bsr_tune.split_rw;
         else if (k == "bsr.kron_mfma") *value = g_bsr_tune.kron_mfma;
         else if (k == "bsr.kron_mfma_min_cols") *value = g_bsr_tune.kron_mfma_min_cols;
-        else if (k == "bsr.blk_dma") *value = g_bsr_tune.blk_dma;
-        else if (k == "bsr.blk_pack") *value = g_bsr_tune.blk_pack;
         else if (k == "bsr.last_kernel") *value = g_bsr_tune.last;
-        else if (k == "bsr.ell9_ilv") *value = g_bsr_tune.ell9_ilv;
-        else if (k == "bsr.tile_max_cols") *value = g_bsr_tune.tile_max_cols;
-        else if (k == "bsr.tile_rows") *value = g_bsr_tune.tile_rows;
-        else if (k == "bsr.probe") *value = g_bsr_tune.probe;
         else if (k == "gemm.m3") *value = g_gemm_tune.m3;
         else if (k == "gemm.splits") *value = g_gemm_tune.splits;
         else if (k == "gemm.t48") *value = g_gemm_tune.t48;
@@ -718,7 +683,7 @@ int sbx_copy_req(int nd0, int nd1, const double *alpha, int t0, int t1, const in
             key.reserve(32 + 6 * (nd0 + nd1) + 2 * (ncomponents0 * nd0 + ncomponents1 * nd1));
             key.insert(key.end(), {nd0, nd1, t0, t1, ncomponents0, ncomponents1, co, copyadd,
                                    (long)a_call.is_zero(), comm ? 1L : 0L, c.device,
-                                   g_copy_tune.budget, g_copy_tune.run, g_copy_tune.kernel,
+                                   g_copy_tune.budget, g_copy_tune.run,
                                    g_copy_tune.nt, g_copy_tune.max_elems, (long)g_copy_tune.pair,
                                    (long)g_copy_tune.order});
             key_str(key, o0, nd0);

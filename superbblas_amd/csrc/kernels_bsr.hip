@@ -40,16 +40,8 @@ struct BsrArgs {
     long ncols;
     double alpha_re, alpha_im;
     int add;
-    unsigned long long *probe; // tools only (sbx_tune_set "bsr.probe"): per-workgroup time stamps
     int ilv = 1; // bsr_ell9_kernel: an XCD's chunks visited as ilv interleaved parts
 };
-
-// tools only: 8 stamps per workgroup -- 100 MHz real time at start and end, then shader-clock
-// deltas of the kernel's phases
-__device__ __forceinline__ void probe_stamp(unsigned long long *probe, int slot,
-                                            unsigned long long v) {
-    if (probe && threadIdx.x == 0) probe[(long)blockIdx.x * 8 + slot] = v;
-}
 
 template <typename E, int BI_, int BD_, bool YROW, bool XROW>
 __global__ void __launch_bounds__(256) bsr_kernel(const BsrArgs p) {
@@ -206,13 +198,11 @@ __global__ void __launch_bounds__(256) bsr_ell_kernel(const BsrArgs p, int nnz, 
 }
 
 // Large blocks (12x12 spin x color, the Wilson-like operator): block-row products on the FP64
-// matrix cores.  A wave owns ROWS block rows and a tile of 16 rhs columns and computes, for each
-// of its block rows, the 16x16 tile  Y_i = sum_j A_ij X_j  with v_mfma_f64_16x16x4_f64 or
-// v_mfma_f32_16x16x4f32 (tile rows
-// >= BI are padding), K running over the BD domain rows of every nonzero block (BD/4 steps per
-// block, 4 real MFMAs per complex step).  The ROWS block rows are interleaved so their loads are
-// in flight together and their MFMA chains are independent.  Fragments come straight from
-// global memory: lane l reads A_ij[l&15][k+(l>>4)] and x[d_j+k+(l>>4)][col0+(l&15)]
+// (FP32) matrix cores.  A wave owns one block row and a tile of 16 rhs columns and computes the
+// 16x16 tile  Y_i = sum_j A_ij X_j  with v_mfma_f64_16x16x4_f64 or v_mfma_f32_16x16x4f32 (tile
+// rows >= BI are padding), K running over the BD domain rows of every nonzero block (BD/4 steps
+// per block, 4 real MFMAs per complex step).  The generic kernels read the fragments straight
+// from global memory: lane l reads A_ij[l&15][k+(l>>4)] and x[d_j+k+(l>>4)][col0+(l&15)]
 // (contiguous along the rhs for row-major x); out-of-range rows, columns and skipped blocks
 // (-1 columns) are clamped loads replaced by zero, so the loop has no divergent branches.
 __device__ __forceinline__ unsigned lds_u32(const void *p) {
@@ -251,90 +241,6 @@ template <> struct BsrMfma<float> {
     }
     static __device__ __forceinline__ int row(int lane, int q) { return 4 * (lane >> 4) + q; }
 };
-
-template <typename R, bool CPLX, int BI, int BD, int ROWS, bool YROW, bool XROW>
-__global__ void __launch_bounds__(256) bsr_mfma_kernel(const BsrArgs p, long ntiles_n) {
-    typedef typename BsrMfmaElem<R, CPLX>::type E;
-    typedef typename BsrMfma<R>::acc_t acc_t;
-    static_assert(BI <= 16 && BD % 4 == 0, "block shape");
-    const E *__restrict__ v = (const E *)p.v;
-    const E *__restrict__ x = (const E *)p.x;
-    E *__restrict__ y = (E *)p.y;
-    const int lane = threadIdx.x & 63;
-    const long wave = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const long nrow_groups = (p.block_rows + ROWS - 1) / ROWS;
-    if (wave >= nrow_groups * ntiles_n) return; // whole waves only: MFMA needs all 64 lanes
-    const long i0 = (wave / ntiles_n) * ROWS;
-    const long col0 = (wave % ntiles_n) * 16;
-    const int ar = lane & 15, kq = lane >> 4;
-    const bool arow_ok = ar < BI;
-    const int arc = arow_ok ? ar : 0;
-    const long bcol = col0 + (lane & 15);
-    const bool bcol_ok = bcol < p.ncols;
-    const long bcc = bcol_ok ? bcol : 0;
-    acc_t accR[ROWS], accI[ROWS];
-    int jb[ROWS], je[ROWS], nmax = 0;
-#pragma unroll
-    for (int r = 0; r < ROWS; ++r) {
-        accR[r] = acc_t{0, 0, 0, 0};
-        accI[r] = acc_t{0, 0, 0, 0};
-        const long i = min(i0 + r, p.block_rows - 1);
-        jb[r] = p.ii[i];
-        je[r] = i0 + r < p.block_rows ? p.ii[i + 1] : jb[r];
-        nmax = max(nmax, je[r] - jb[r]);
-    }
-    for (int t = 0; t < nmax; ++t) {
-        E af[ROWS][BD / 4], bf[ROWS][BD / 4];
-#pragma unroll
-        for (int r = 0; r < ROWS; ++r) {
-            const bool have = jb[r] + t < je[r];
-            const int j = have ? jb[r] + t : jb[r];
-            const int dj = p.jj[j];
-            const bool ok = have && dj >= 0;
-            const long d0 = dj >= 0 ? dj : 0;
-            const E *vb = v + (long)j * BI * BD;
-#pragma unroll
-            for (int ks = 0; ks < BD / 4; ++ks) {
-                const int e = ks * 4 + kq;
-                const E a = p.block_im_fast ? vb[arc + e * BI] : vb[arc * BD + e];
-                const E b = XROW ? x[(d0 + e) * p.ldx + bcc] : x[(d0 + e) + bcc * p.ldx];
-                af[r][ks] = (arow_ok && ok) ? a : E{};
-                bf[r][ks] = bcol_ok ? b : E{};
-            }
-        }
-#pragma unroll
-        for (int ks = 0; ks < BD / 4; ++ks)
-#pragma unroll
-            for (int r = 0; r < ROWS; ++r) {
-                if constexpr (CPLX) {
-                    accR[r] = BsrMfma<R>::mma(af[r][ks].x, bf[r][ks].x, accR[r]);
-                    accI[r] = BsrMfma<R>::mma(af[r][ks].x, bf[r][ks].y, accI[r]);
-                    accR[r] = BsrMfma<R>::mma(-af[r][ks].y, bf[r][ks].y, accR[r]);
-                    accI[r] = BsrMfma<R>::mma(af[r][ks].y, bf[r][ks].x, accI[r]);
-                } else {
-                    accR[r] = BsrMfma<R>::mma(af[r][ks], bf[r][ks], accR[r]);
-                }
-            }
-    }
-    // C/D map: col = lane & 15, row = BsrMfma<R>::row(lane, q)
-#pragma unroll
-    for (int r = 0; r < ROWS; ++r) {
-        if (i0 + r >= p.block_rows) break;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int row = BsrMfma<R>::row(lane, q);
-            if (row >= BI || !bcol_ok) continue;
-            const long img = (i0 + r) * BI + row;
-            E *yp = YROW ? y + img * p.ldy + bcol : y + img + bcol * p.ldy;
-            E out;
-            if constexpr (CPLX)
-                out = Ops<E>::scale(E{accR[r][q], accI[r][q]}, p.alpha_re, p.alpha_im);
-            else
-                out = Ops<E>::scale(accR[r][q], p.alpha_re, p.alpha_im);
-            *yp = p.add ? Ops<E>::add(*yp, out) : out;
-        }
-    }
-}
 
 // One block row per wave, the fragments of nonzero block t+1 loaded while block t is applied
 // (twice the bytes in flight per wave; 985 -> 880 us on the chain's complex<float> operator).
@@ -493,127 +399,6 @@ __global__ void __launch_bounds__(256) bsr_mfma_ell_kernel(const BsrArgs p, long
     }
 }
 
-// Contiguous-block form (row-major x with ldx == ncols <= 16, ELL with NNZ blocks per row): the
-// nonzero block A_ij and the x block of its domain rows are each one contiguous run of
-// BI*BD (BD*ncols) elements, so a wave fetches them with lane-linear 16-byte loads (every lane a
-// distinct 16 bytes, 1 KB per instruction) instead of 12-row fragment gathers, stages them in a
-// wave-private LDS slot and reads the MFMA fragments from there.  Block j+1 is fetched into
-// registers while block j is applied.
-template <typename R, bool CPLX, int BI, int BD, bool YROW, int NNZ, int PD, bool M3>
-__global__ void __launch_bounds__(256) bsr_mfma_blk_kernel(const BsrArgs p) {
-    typedef typename BsrMfmaElem<R, CPLX>::type E;
-    typedef typename BsrMfma<R>::acc_t acc_t;
-    static_assert(BI <= 16 && BD % 4 == 0, "block shape");
-    constexpr int KS = BD / 4;
-    constexpr int EPL = 16 / (int)sizeof(E);            // elements per 16-byte lane load
-    constexpr int ABLK = BI * BD, XBLK = BD * 16;        // staged elements (x: up to 16 cols)
-    constexpr int NA = (ABLK + 64 * EPL - 1) / (64 * EPL), NX = (XBLK + 64 * EPL - 1) / (64 * EPL);
-    typedef __attribute__((ext_vector_type(4))) unsigned u4;
-    __shared__ __attribute__((aligned(16))) E lds[4][ABLK + XBLK];
-    const E *__restrict__ v = (const E *)p.v;
-    const E *__restrict__ x = (const E *)p.x;
-    E *__restrict__ y = (E *)p.y;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const long i = (long)blockIdx.x * 4 + w;
-    if (i >= p.block_rows) return;
-    const int nc = (int)p.ncols, xblk = BD * nc;
-    const long jb = i * NNZ;
-    int dj[NNZ];
-#pragma unroll
-    for (int k = 0; k < NNZ; ++k) dj[k] = p.jj[jb + k];
-    u4 ra[PD][NA], rx[PD][NX];
-    auto fetch = [&](int k, u4 *ra_, u4 *rx_) {
-        // a skipped block (column -1: e.g. the other piece's blocks of a split core / halo
-        // operator) is not read at all
-        const bool live = dj[k] >= 0;
-        const u4 *ap = (const u4 *)(v + (jb + k) * ABLK);
-        const u4 *xp = (const u4 *)(x + (long)(live ? dj[k] : 0) * nc);
-#pragma unroll
-        for (int q = 0; q < NA; ++q) {
-            const int g = lane + 64 * q; // 16-byte granule of the block
-            ra_[q] = live && g * EPL < ABLK ? ap[g] : u4{0, 0, 0, 0};
-        }
-#pragma unroll
-        for (int q = 0; q < NX; ++q) {
-            const int g = lane + 64 * q;
-            rx_[q] = live && g * EPL < xblk ? xp[g] : u4{0, 0, 0, 0};
-        }
-    };
-    E *const sa = lds[w], *const sx = lds[w] + ABLK;
-    const int ar = lane & 15, kq = lane >> 4;
-    const bool arow_ok = ar < BI, bcol_ok = ar < nc;
-    acc_t accR = acc_t{0, 0, 0, 0}, accI = acc_t{0, 0, 0, 0}, acc3 = acc_t{0, 0, 0, 0};
-#pragma unroll
-    for (int k = 0; k < PD && k < NNZ; ++k) fetch(k, ra[k], rx[k]);
-#pragma unroll
-    for (int k = 0; k < NNZ; ++k) {
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int q = 0; q < NA; ++q)
-            if ((lane + 64 * q) * EPL < ABLK) ((u4 *)sa)[lane + 64 * q] = ra[k % PD][q];
-#pragma unroll
-        for (int q = 0; q < NX; ++q)
-            if ((lane + 64 * q) * EPL < xblk) ((u4 *)sx)[lane + 64 * q] = rx[k % PD][q];
-        __builtin_amdgcn_wave_barrier();
-        if (k + PD < NNZ) fetch(k + PD, ra[k % PD], rx[k % PD]);
-        if (dj[k] < 0) continue;
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-            const int e = ks * 4 + kq;
-            E a = arow_ok ? (p.block_im_fast ? sa[ar + e * BI] : sa[ar * BD + e]) : E{};
-            E b = bcol_ok ? sx[e * nc + ar] : E{};
-            if constexpr (CPLX && M3) {
-                // 3-multiplication form (opt-in): P1 = ar*br, P2 = ai*bi, P3 = (ar+ai)(br+bi)
-                accR = BsrMfma<R>::mma(a.x, b.x, accR);
-                accI = BsrMfma<R>::mma(a.y, b.y, accI);
-                acc3 = BsrMfma<R>::mma(a.x + a.y, b.x + b.y, acc3);
-            } else if constexpr (CPLX) {
-                // 4-multiplication form (BLAS rounding): re += ar*br - ai*bi, im += ar*bi + ai*br
-                accR = BsrMfma<R>::mma(a.x, b.x, accR);
-                accI = BsrMfma<R>::mma(a.x, b.y, accI);
-                accR = BsrMfma<R>::mma(-a.y, b.y, accR);
-                accI = BsrMfma<R>::mma(a.y, b.x, accI);
-            } else {
-                accR = BsrMfma<R>::mma(a, b, accR);
-            }
-        }
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int row = BsrMfma<R>::row(lane, q);
-        if (row >= BI || !bcol_ok) continue;
-        const long img = i * BI + row;
-        E *yp = YROW ? y + img * p.ldy + ar : y + img + ar * p.ldy;
-        E out;
-        if constexpr (CPLX && M3)
-            out = Ops<E>::scale(E{accR[q] - accI[q], acc3[q] - accR[q] - accI[q]}, p.alpha_re,
-                                p.alpha_im);
-        else if constexpr (CPLX)
-            out = Ops<E>::scale(E{accR[q], accI[q]}, p.alpha_re, p.alpha_im);
-        else
-            out = Ops<E>::scale(accR[q], p.alpha_re, p.alpha_im);
-        *yp = p.add ? Ops<E>::add(*yp, out) : out;
-    }
-}
-
-template <typename R, bool CPLX, int BI, int BD, int NNZ, int PD>
-void launch_bsr_mfma_blk(const BsrArgs &a, bool yrow, hipStream_t s) {
-    const long blocks = (a.block_rows + 3) / 4;
-    if (blocks >= (1L << 31)) throw Error("bsr: grid too large");
-    g_bsr_tune.last = 9;
-    KernelTimer timer("bsr", s);
-    const bool m3 = CPLX && g_gemm_tune.m3 > 0;
-    if (yrow && m3)
-        hipLaunchKernelGGL((bsr_mfma_blk_kernel<R, CPLX, BI, BD, true, NNZ, PD, true>), dim3(blocks), dim3(256), 0, s, a);
-    else if (yrow)
-        hipLaunchKernelGGL((bsr_mfma_blk_kernel<R, CPLX, BI, BD, true, NNZ, PD, false>), dim3(blocks), dim3(256), 0, s, a);
-    else if (m3)
-        hipLaunchKernelGGL((bsr_mfma_blk_kernel<R, CPLX, BI, BD, false, NNZ, PD, true>), dim3(blocks), dim3(256), 0, s, a);
-    else
-        hipLaunchKernelGGL((bsr_mfma_blk_kernel<R, CPLX, BI, BD, false, NNZ, PD, false>), dim3(blocks), dim3(256), 0, s, a);
-    SBX_HIP_CHECK(hipGetLastError());
-}
-
 template <typename R, bool CPLX, int BI, int BD, int NNZ, int NB>
 void launch_bsr_mfma_ell(const BsrArgs &a, bool yrow, bool xrow, hipStream_t s) {
     const long ntn = (a.ncols + 15) / 16;
@@ -652,11 +437,13 @@ void launch_bsr_mfma_pf(const BsrArgs &a, bool yrow, bool xrow, hipStream_t s) {
     SBX_HIP_CHECK(hipGetLastError());
 }
 
-// bsr_mfma_blk_kernel with the blocks staged by LDS-DMA (buffer_load_dwordx4 ... lds): the value
-// block A_ij and the x block of its domain rows go straight from memory into the wave's LDS slot
-// (no VGPR round trip), PD blocks ahead in a ring of PD + 1 slots; the MFMA fragments are read
-// from the slot as in the register-staged kernel.  Both blocks are contiguous runs (row-major x,
-// ldx == ncols <= 16), lane-linear in LDS.
+// Contiguous-block form (row-major x with ldx == ncols <= 16, ELL with NNZ blocks per row): the
+// nonzero block A_ij and the x block of its domain rows are each one contiguous run of
+// BI*BD (BD*ncols) elements, so a wave moves them by LDS-DMA (buffer_load_dwordx4 ... lds, every
+// lane a distinct 16 bytes, 1 KB per instruction, no VGPR round trip) into its LDS slot, PD
+// blocks ahead in a ring of PD + 1 slots, instead of 12-row fragment gathers, and reads the MFMA
+// fragments from the slot.  (The round-2 register-staged form measured the same on
+// complex<double> and 6 % slower on the chain's complex<float> operator, profiles/r02_bsr_blk_sweep.txt.)
 // PK > 0 (packed slots): the value block and the x block are one run of the slot (x right after
 // the values, no 1-KB rounding of each), moved by PK global_load_lds_dwordx4 instructions whose
 // lanes address either array (a buffer load takes one array per instruction) -- 2304 instead of
@@ -797,9 +584,9 @@ bool launch_bsr_mfma_dma(const BsrArgs &a, bool yrow, hipStream_t s) {
     // packed slots (values then x in one run): the DMA instruction count of a block
     const bool m3 = CPLX && g_gemm_tune.m3 > 0;
     const long slot_packed = (long)(BI * BD + BD * a.ncols) * ES;
-    // default for 8-byte elements only (warm round robin, profiles/r02c_blk_pack.txt: the chain's
-    // complex<float> operator 719 -> 693 us; complex<double> 327 -> 336 us); bsr.blk_pack 2 = always
-    const bool want = g_bsr_tune.blk_pack > 1 || (g_bsr_tune.blk_pack == 1 && ES == 8);
+    // for 8-byte elements only (warm round robin, profiles/r02c_blk_pack.txt: the chain's
+    // complex<float> operator 719 -> 693 us; complex<double> 327 -> 336 us)
+    const bool want = ES == 8;
     const int pk = want && !m3 ? (int)((slot_packed + 1023) / 1024) : 0;
     // (16-byte aligned pieces: the x blocks of an nc-column row and both arrays)
     const bool packed = pk == (CPLX && ES == 16 ? 5 : 3) && a.ncols >= 1 && a.ncols <= 16 &&
@@ -829,41 +616,20 @@ bool launch_bsr_mfma_dma(const BsrArgs &a, bool yrow, hipStream_t s) {
     return true;
 }
 
-template <typename R, bool CPLX, int BI, int BD, int ROWS>
+template <typename R, bool CPLX, int BI, int BD>
 void launch_bsr_mfma(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_t s) {
-    // the 9-point stencils: columns preloaded, one block ahead (16^4 complex<double> n = 12:
-    // 426 -> 350 us; complex<float> 16^3 x 64: 985 -> 797 us); a 3- or 9-block lookahead, the
-    // XCD-grouped row order and non-temporal value loads were all measured slower, and
-    // non-temporal stores of y no faster
-    // contiguous x blocks (row-major x, ldx == ncols <= 16): lane-linear block loads staged
-    // through LDS (16^4 complex<double> n = 12: 372 -> 348-355 us; the chain's complex<float>
-    // operator 843-922 -> 722 us; two or three blocks of lookahead: 359-377 / 739-772 us)
-    if (g_bsr_tune.variant != 1 && g_bsr_tune.variant != 2 && nnz == 9 && xrow &&
-        a.ldx == a.ncols && a.ncols <= 16) {
-        // LDS-DMA staging one block ahead (tools/bsr_blk_sweep.py, warm GPU, modes round-robin,
-        // profiles/r02_bsr_blk_sweep.txt): the chain's 16^3 x 64 complex<float> operator 782 ->
-        // 735 us; 16^4 complex<double> unchanged (338 / 341 us); two blocks ahead slower for both
-        const int pd = g_bsr_tune.blk_dma >= 0 ? g_bsr_tune.blk_dma : 1;
-        if (pd == 1 && launch_bsr_mfma_dma<R, CPLX, BI, BD, 9, 1>(a, yrow, s)) return;
-        if (pd == 2 && launch_bsr_mfma_dma<R, CPLX, BI, BD, 9, 2>(a, yrow, s)) return;
-        return launch_bsr_mfma_blk<R, CPLX, BI, BD, 9, 1>(a, yrow, s);
-    }
+    // contiguous x blocks (row-major x, ldx == ncols <= 16), 9 blocks per row: the blocks staged
+    // by LDS-DMA one ahead (16^4 complex<double> n = 12: 426 us for the round-1 fragment kernel,
+    // 348-355 us staged; the chain's complex<float> operator 985 -> 693 us with packed slots;
+    // two or three blocks of lookahead were slower, profiles/r02_bsr_blk_sweep.txt)
+    if (g_bsr_tune.variant == 0 && nnz == 9 && xrow && a.ldx == a.ncols && a.ncols <= 16 &&
+        launch_bsr_mfma_dma<R, CPLX, BI, BD, 9, 1>(a, yrow, s))
+        return;
+    // the 9-point stencils otherwise: columns preloaded, fragments one block ahead (a 3- or
+    // 9-block lookahead, the XCD-grouped row order and non-temporal value loads were all
+    // measured slower, non-temporal stores of y no faster); any other pattern: generic rows
     if (g_bsr_tune.variant != 1 && nnz == 9) return launch_bsr_mfma_ell<R, CPLX, BI, BD, 9, 1>(a, yrow, xrow, s);
-    if (g_bsr_tune.variant != 1) return launch_bsr_mfma_pf<R, CPLX, BI, BD>(a, yrow, xrow, s);
-    const long ntn = (a.ncols + 15) / 16;
-    const long waves = (a.block_rows + ROWS - 1) / ROWS * ntn;
-    const long blocks = (waves + 3) / 4;
-    if (blocks >= (1L << 31)) throw Error("bsr: grid too large");
-    KernelTimer timer("bsr", s);
-    if (yrow && xrow)
-        hipLaunchKernelGGL((bsr_mfma_kernel<R, CPLX, BI, BD, ROWS, true, true>), dim3(blocks), dim3(256), 0, s, a, ntn);
-    else if (yrow && !xrow)
-        hipLaunchKernelGGL((bsr_mfma_kernel<R, CPLX, BI, BD, ROWS, true, false>), dim3(blocks), dim3(256), 0, s, a, ntn);
-    else if (!yrow && xrow)
-        hipLaunchKernelGGL((bsr_mfma_kernel<R, CPLX, BI, BD, ROWS, false, true>), dim3(blocks), dim3(256), 0, s, a, ntn);
-    else
-        hipLaunchKernelGGL((bsr_mfma_kernel<R, CPLX, BI, BD, ROWS, false, false>), dim3(blocks), dim3(256), 0, s, a, ntn);
-    SBX_HIP_CHECK(hipGetLastError());
+    launch_bsr_mfma_pf<R, CPLX, BI, BD>(a, yrow, xrow, s);
 }
 
 template <typename E, int BI, int BD, int G>
@@ -895,13 +661,11 @@ void launch_ell_g(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_t s
 // are in flight together (bsr_ell_kernel: value stream, then the columns, then one x block at a
 // time); blocks j+PD are fetched while block j is applied.
 template <typename E, int BI, int BD, int G, int PD, bool YROW, bool XROW, int NT = 256,
-          int NTF = 0, bool SC = false>
+          bool DMAV = false, bool SC = false>
 __global__ void __launch_bounds__(NT) bsr_ell9_kernel(const BsrArgs p, int rb) {
-    // NTF (experiments): bit 0 = non-temporal value loads, bit 1 = non-temporal y stores
     // SC: a thread's G columns are g, g + ngroups, ... (the lanes of one row read consecutive
     // columns in each load) instead of g*G .. g*G + G-1
-    // NTF bit 2: the values staged by LDS-DMA (16-byte elements; launcher: 32-bit offsets)
-    constexpr bool NTV = (NTF & 1) != 0, NTY = (NTF & 2) != 0, DMAV = (NTF & 4) != 0;
+    // DMAV: the values staged by LDS-DMA (16-byte elements; launcher: 32-bit offsets)
     static_assert(!DMAV || sizeof(E) == 16, "LDS-DMA staging takes 16-byte elements");
     constexpr int NNZ = 9, BLK = BI * BD, NB = PD + 1;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -915,8 +679,6 @@ __global__ void __launch_bounds__(NT) bsr_ell9_kernel(const BsrArgs p, int rb) {
     const int cnt = xcd < r8 ? q8 + 1 : q8, qx = bid >> 3, npart = cnt / p.ilv;
     const int loc = (p.ilv > 1 && qx < npart * p.ilv) ? (qx % p.ilv) * npart + qx / p.ilv : qx;
     const int chunk = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
-    const unsigned long long rt0 = p.probe ? __builtin_amdgcn_s_memrealtime() : 0;
-    const unsigned long long c0 = p.probe ? __builtin_amdgcn_s_memtime() : 0;
     const long row0 = (long)chunk * rb;
     const int nrows = (int)min((long)rb, p.block_rows - row0);
     const long ngroups = (p.ncols + G - 1) / G;
@@ -969,21 +731,13 @@ __global__ void __launch_bounds__(NT) bsr_ell9_kernel(const BsrArgs p, int rb) {
         for (int e0 = threadIdx.x; e0 < nv; e0 += NT * 8) {
             E t[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const E *vp = v + vbase + min(e0 + NT * u, nv - 1);
-                t[u] = NTV ? load_nt(vp) : *vp;
-            }
+            for (int u = 0; u < 8; ++u) t[u] = v[vbase + min(e0 + NT * u, nv - 1)];
 #pragma unroll
             for (int u = 0; u < 8; ++u)
                 if (e0 + NT * u < nv) vals[e0 + NT * u] = t[u];
         }
     }
     __syncthreads();
-    const unsigned long long c1 = p.probe ? __builtin_amdgcn_s_memtime() : 0;
-    if (p.probe) {
-        probe_stamp(p.probe, 0, rt0);
-        probe_stamp(p.probe, 3, c1 - c0);
-    }
     if (!active) return;
     E acc[BI][G];
 #pragma unroll
@@ -1015,21 +769,12 @@ __global__ void __launch_bounds__(NT) bsr_ell9_kernel(const BsrArgs p, int rb) {
             if (col >= p.ncols) break;
             E *yp = YROW ? y + img * p.ldy + col : y + img + col * p.ldy;
             const E out = Ops<E>::scale(acc[c][k], p.alpha_re, p.alpha_im);
-            if (p.add)
-                *yp = Ops<E>::add(*yp, out);
-            else if constexpr (NTY)
-                store_nt(yp, out);
-            else
-                *yp = out;
+            *yp = p.add ? Ops<E>::add(*yp, out) : out;
         }
-    }
-    if (p.probe) {
-        probe_stamp(p.probe, 5, __builtin_amdgcn_s_memtime() - c1);
-        probe_stamp(p.probe, 1, __builtin_amdgcn_s_memrealtime());
     }
 }
 
-template <typename E, int BI, int BD, int G, int PD, int NT = 256, int NTF = 0, bool SC = false>
+template <typename E, int BI, int BD, int G, int PD, int NT = 256, bool DMAV = false, bool SC = false>
 void launch_ell9(const BsrArgs &a, bool yrow, bool xrow, hipStream_t s, long lds_bytes) {
     const long blk_bytes = 9L * BI * BD * (long)sizeof(E);
     const long ngroups = (a.ncols + G - 1) / G;
@@ -1038,28 +783,25 @@ void launch_ell9(const BsrArgs &a, bool yrow, bool xrow, hipStream_t s, long lds
     rb = (int)std::min<long>(rb, std::max(1L, NT / ngroups));
     const long blocks = (a.block_rows + rb - 1) / rb;
     if (blocks >= (1L << 31)) throw Error("bsr: grid too large");
-    if constexpr ((NTF & 4) != 0)
-        if (a.block_rows * blk_bytes >= (1L << 31)) return launch_ell9<E, BI, BD, G, PD, NT, NTF & 3, SC>(a, yrow, xrow, s, lds_bytes);
+    if constexpr (DMAV)
+        if (a.block_rows * blk_bytes >= (1L << 31)) return launch_ell9<E, BI, BD, G, PD, NT, false, SC>(a, yrow, xrow, s, lds_bytes);
     // the DMA form fills whole workgroup-wide rows of 16-byte lanes
-    const size_t lds = (NTF & 4) != 0 ? (size_t)((rb * 9L * BI * BD + NT - 1) / NT * NT) * sizeof(E)
-                                      : (size_t)rb * blk_bytes;
+    const size_t lds = DMAV ? (size_t)((rb * 9L * BI * BD + NT - 1) / NT * NT) * sizeof(E)
+                            : (size_t)rb * blk_bytes;
     // the DMA loop: passes u < ceil(nv / NT) of NT lanes, nv <= rb * 81 (the last chunk fewer)
-    if constexpr ((NTF & 4) != 0)
-        check_dma_lds("bsr_ell9_kernel", lds, (rb * 9L * BI * BD + NT - 1) / NT, NT);
+    if constexpr (DMAV) check_dma_lds("bsr_ell9_kernel", lds, (rb * 9L * BI * BD + NT - 1) / NT, NT);
     g_bsr_tune.last = 3;
     KernelTimer timer("bsr", s);
     if (yrow && xrow)
-        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, true, true, NT, NTF, SC>), dim3(blocks), dim3(NT), lds, s, a, rb);
+        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, true, true, NT, DMAV, SC>), dim3(blocks), dim3(NT), lds, s, a, rb);
     else if (yrow && !xrow)
-        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, true, false, NT, NTF, SC>), dim3(blocks), dim3(NT), lds, s, a, rb);
+        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, true, false, NT, DMAV, SC>), dim3(blocks), dim3(NT), lds, s, a, rb);
     else if (!yrow && xrow)
-        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, false, true, NT, NTF, SC>), dim3(blocks), dim3(NT), lds, s, a, rb);
+        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, false, true, NT, DMAV, SC>), dim3(blocks), dim3(NT), lds, s, a, rb);
     else
-        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, false, false, NT, NTF, SC>), dim3(blocks), dim3(NT), lds, s, a, rb);
+        hipLaunchKernelGGL((bsr_ell9_kernel<E, BI, BD, G, PD, false, false, NT, DMAV, SC>), dim3(blocks), dim3(NT), lds, s, a, rb);
     SBX_HIP_CHECK(hipGetLastError());
 }
-
-
 
 // Few rhs columns (n <= NC <= 4), 3x3 blocks, 9 per row: one thread per (block row, nonzero
 // block).  The value stream is read by 9 x more threads than in the row-chunk kernel, without
@@ -1158,7 +900,7 @@ void launch_ell9_row(const BsrArgs &a, bool yrow, bool xrow, hipStream_t s) {
     if (blocks >= (1L << 31)) throw Error("bsr: grid too large");
     // the LDS-DMA form for 16-byte elements whose value array has 32-bit offsets
     const long v_bytes = a.block_rows * 81L * (long)sizeof(E);
-    const bool dma = sizeof(E) == 16 && v_bytes < (1L << 31) && g_bsr_tune.row_dma;
+    const bool dma = sizeof(E) == 16 && v_bytes < (1L << 31);
     g_bsr_tune.last = 1;
     KernelTimer timer("bsr", s);
     auto go = [&](auto kern) {
@@ -1346,16 +1088,17 @@ bool launch_ell9_split(const BsrArgs &a, bool yrow, bool xrow, hipStream_t st) {
         if (cw <= 0) cw = a.ncols <= 4 ? 1 : 2;
         int jb = g_bsr_tune.split_jb;
         if (jb <= 0) jb = a.ncols <= 24 ? 3 : 9;
-        if ((cw != 1 && cw != 2 && cw != 4) || (jb != 1 && jb != 3 && jb != 9)) return false;
+        // the forms the defaults use (the sweep's other forms were slower everywhere)
+        if ((cw != 1 && cw != 2) || (jb != 3 && jb != 9)) return false;
         const int nct = (int)((a.ncols + cw - 1) / cw), tpr = 9 / jb * nct;
-        const int ntmax = g_bsr_tune.split_nt > 0 ? g_bsr_tune.split_nt : 256;
+        const int ntmax = 256; // 512-thread workgroups measured slower (profiles/r02c_split_ovl.txt)
         if (tpr > ntmax) return false;
-        // rows per workgroup: by the thread budget and at most 40 KB of LDS
-        const bool ovl = g_bsr_tune.split_ovl > 0;
+        // rows per workgroup: by the thread budget and at most 40 KB of LDS; the partial products
+        // overlay the staged values (one more barrier, four workgroups per CU instead of three)
+        const bool ovl = true;
         const long part_row = jb == 9 ? 0L : (long)(9 / jb) * 3 * nct * cw * 16;
-        const long row_lds = ovl ? std::max(81L * 16, part_row) : 81L * 16 + part_row;
-        int rw = std::max(1, std::min<int>(ntmax / tpr, (int)(40960 / row_lds)));
-        if (g_bsr_tune.split_rw > 0) rw = std::min(rw, g_bsr_tune.split_rw);
+        const long row_lds = std::max(81L * 16, part_row);
+        const int rw = std::max(1, std::min<int>(ntmax / tpr, (int)(40960 / row_lds)));
         const int nth = (rw * tpr + 63) / 64 * 64;
         const long nvp = (rw * 81L + nth - 1) / nth * nth;
         const long npart = jb == 9 ? 0L : (long)rw * (9 / jb) * 3 * nct * cw;
@@ -1381,9 +1124,7 @@ bool launch_ell9_split(const BsrArgs &a, bool yrow, bool xrow, hipStream_t st) {
         if (yrow) go(bsr_ell9_split_kernel<CW_, JB_, true>);                                       \
         else go(bsr_ell9_split_kernel<CW_, JB_, false>);                                           \
     }
-        SBX_SPLIT(1, 1) SBX_SPLIT(1, 3) SBX_SPLIT(1, 9)
-        SBX_SPLIT(2, 1) SBX_SPLIT(2, 3) SBX_SPLIT(2, 9)
-        SBX_SPLIT(4, 1) SBX_SPLIT(4, 3) SBX_SPLIT(4, 9)
+        SBX_SPLIT(1, 3) SBX_SPLIT(1, 9) SBX_SPLIT(2, 3) SBX_SPLIT(2, 9)
 #undef SBX_SPLIT
         SBX_HIP_CHECK(hipGetLastError());
         return true;
@@ -1412,224 +1153,15 @@ void launch_ell(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_t s) 
             return;
     }
     if (nnz == 9 && g_bsr_tune.variant != 1) {
-        const long lds = g_bsr_tune.ell9_lds > 0 ? g_bsr_tune.ell9_lds : a.ncols >= 8 ? 12288 : 24576;
-        // experiments (sbx_tune_set "bsr.ell9"): workgroup size 64 / 128 / 256 threads x one or
-        // two blocks of x lookahead, 1 or 2 rhs columns per thread
-        switch (g_bsr_tune.ell9) {
-        case 1: return launch_ell9<E, BI, BD, 2, 1, 64>(a, yrow, xrow, s, lds);
-        case 2: return launch_ell9<E, BI, BD, 2, 1, 128>(a, yrow, xrow, s, lds);
-        case 3: return launch_ell9<E, BI, BD, 2, 2, 64>(a, yrow, xrow, s, lds);
-        case 4: return launch_ell9<E, BI, BD, 2, 2, 128>(a, yrow, xrow, s, lds);
-        case 5: return launch_ell9<E, BI, BD, 1, 1, 64>(a, yrow, xrow, s, lds);
-        case 6: return launch_ell9<E, BI, BD, 1, 2, 128>(a, yrow, xrow, s, lds);
-        case 7: return launch_ell9<E, BI, BD, 2, 2, 256>(a, yrow, xrow, s, lds);
-        case 8: return launch_ell9<E, BI, BD, 2, 1, 256, 2>(a, yrow, xrow, s, lds);
-        case 9: return launch_ell9<E, BI, BD, 2, 1, 256, 1>(a, yrow, xrow, s, lds);
-        case 10: return launch_ell9<E, BI, BD, 2, 1, 256, 3>(a, yrow, xrow, s, lds);
-        case 11: return launch_ell9<E, BI, BD, 2, 2, 256, 2>(a, yrow, xrow, s, lds);
-        case 12: return launch_ell9<E, BI, BD, 2, 2, 256, 3>(a, yrow, xrow, s, lds);
-        case 13: return launch_ell9<E, BI, BD, 2, 1, 256, 0, true>(a, yrow, xrow, s, lds);
-        case 14: return launch_ell9<E, BI, BD, 2, 2, 256, 0, true>(a, yrow, xrow, s, lds);
-        case 15: return launch_ell9<E, BI, BD, 4, 1, 256, 0, true>(a, yrow, xrow, s, lds);
-        case 16: if constexpr (sizeof(E) == 16) return launch_ell9<E, BI, BD, 2, 1, 256, 4>(a, yrow, xrow, s, lds); else break;
-        case 17: if constexpr (sizeof(E) == 16) return launch_ell9<E, BI, BD, 2, 2, 256, 4>(a, yrow, xrow, s, lds); else break;
-        case 18: if constexpr (sizeof(E) == 16) return launch_ell9<E, BI, BD, 2, 1, 256, 4, true>(a, yrow, xrow, s, lds); else break;
-        case 19: return launch_ell9<E, BI, BD, 2, 1>(a, yrow, xrow, s, lds); // round-2a default
-        default:
-            // 16-byte elements: values by LDS-DMA, a row's lanes on consecutive columns
-            // (n = 12: 42 -> 39 us, n = 24: 67 -> 61, n = 64: 182 -> 172; profiles/r02_bsr_sweep.txt)
-            if constexpr (sizeof(E) == 16) return launch_ell9<E, BI, BD, 2, 1, 256, 4, true>(a, yrow, xrow, s, lds);
-            else return launch_ell9<E, BI, BD, 2, 1>(a, yrow, xrow, s, lds);
-        }
+        const long lds = a.ncols >= 8 ? 12288 : 24576;
+        // 16-byte elements: values by LDS-DMA, a row's lanes on consecutive columns (n = 12:
+        // 42 -> 39 us, n = 24: 67 -> 61, n = 64: 182 -> 172; profiles/r02_bsr_sweep.txt; 64- and
+        // 128-thread workgroups, two blocks of x lookahead, non-temporal value loads or y stores
+        // were slower)
+        if constexpr (sizeof(E) == 16) return launch_ell9<E, BI, BD, 2, 1, 256, true, true>(a, yrow, xrow, s, lds);
+        else return launch_ell9<E, BI, BD, 2, 1>(a, yrow, xrow, s, lds);
     }
     launch_ell_g<E, BI, BD, 2>(a, nnz, yrow, xrow, s, ELL_LDS_BYTES);
-}
-
-// Lattice-tiled 9-point 3x3 product, complex<double> (plan: bsr.cpp build_tile_plan).  A
-// workgroup owns one tile of R block rows and one slab of at most 32 rhs columns, one column per
-// thread:
-//   0) the tile's block-row and staged-row ids into LDS, beside the per-row entry loads;
-//   1) the gathers of each row's direct (halo) x rows into registers;
-//   2) the tile's values and its staged x rows (the domain rows two or more of its rows use)
-//      into LDS by LDS-DMA (buffer_load_dwordx4 ... lds: one 16-B element per lane, no VGPRs,
-//      all in flight at once; ids of -1 read zero through the buffer descriptor);
-//   3) the products: direct blocks from registers, staged ones from LDS.
-// Each interior x row of a tile is fetched once instead of once per block that uses it: the
-// chunked kernel (bsr_ell9_kernel) is bound by those fetches in the vector-memory pipeline and
-// by the latency of its one-block-ahead gathers (tools/bsr_timeline.py).
-struct TileArgs {
-    const int *rows;
-    const unsigned *ent;
-    const int *staged;
-    int R, S;
-    int c0, nc;          // the column slab
-    int uv, ux;          // DMA instructions per wave: values, staged x
-    unsigned v_bytes, x_bytes;
-    unsigned div81_m, rowlen_m, nc_m; // magic multipliers (n / d = (umulhi(n, m) + n) >> s)
-    int rowlen_s, nc_s;
-};
-
-template <int ND, bool YROW, bool XROW>
-__global__ void __launch_bounds__(512) bsr_tile_kernel(const BsrArgs p, const TileArgs t) {
-    typedef double2 E;
-    constexpr int NNZ = 9, BI = 3, BD = 3, BLK = 9, NE = ND + NNZ, VB = NNZ * BLK;
-    constexpr unsigned NONE = 15u, OOB = 0x80000000u;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int R = t.R, S = t.S, nc = t.nc, nt = blockDim.x, tid = threadIdx.x;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    E *vals = (E *)smem;
-    E *xs = vals + t.uv * nt;
-    int *ids = (int *)(xs + t.ux * nt);
-    const E *__restrict__ x = (const E *)p.x;
-    E *__restrict__ y = (E *)p.y;
-    // consecutive tiles on one XCD (neighbouring tiles share halo rows in its L2)
-    const int nwg = gridDim.x, bid = blockIdx.x;
-    const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-    const long chunk = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-    const unsigned long long rt0 = p.probe ? __builtin_amdgcn_s_memrealtime() : 0;
-    const unsigned long long c0 = p.probe ? __builtin_amdgcn_s_memtime() : 0;
-    const int *__restrict__ rows = t.rows + chunk * R;
-    const int *__restrict__ staged = t.staged + chunk * S;
-    const int i = tid / nc, g = tid - i * nc, col = t.c0 + g;
-    const int row = i < R ? rows[i] : -1;
-    const bool active = row >= 0;
-    // 0) the tile's block rows and staged domain rows (ids) into LDS, beside the entry loads
-    for (int q = tid; q < R + S; q += nt) ids[q] = q < R ? rows[q] : staged[q - R];
-    unsigned ent[NE];
-#pragma unroll
-    for (int q = 0; q < NE; ++q) ent[q] = active ? t.ent[(chunk * R + i) * NE + q] : NONE << 28;
-    // 1) the direct (halo) x rows into registers
-    E xg[ND][BD];
-#pragma unroll
-    for (int q = 0; q < ND; ++q) {
-        const long d = (ent[q] >> 28) != NONE ? (long)(ent[q] & 0x0fffffffu) : 0;
-#pragma unroll
-        for (int e = 0; e < BD; ++e) xg[q][e] = XROW ? x[(d + e) * p.ldx + col] : x[(d + e) + (long)col * p.ldx];
-    }
-    __syncthreads();
-    const unsigned long long c1 = p.probe ? __builtin_amdgcn_s_memtime() : 0;
-    // 2) values and staged x rows by LDS-DMA (lane-linear LDS destination)
-    const __amdgpu_buffer_rsrc_t rsv =
-        __builtin_amdgcn_make_buffer_rsrc((void *)p.v, (short)0, (int)t.v_bytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rsx =
-        __builtin_amdgcn_make_buffer_rsrc((void *)p.x, (short)0, (int)t.x_bytes, 0x00020000);
-    const unsigned vbase = lds_u32(vals) + (unsigned)wave * 1024u;
-    const int nv = R * VB;
-    for (int u = 0; u < t.uv; ++u) {
-        const unsigned e = (unsigned)(u * nt + tid), r = fdiv(e, t.div81_m, 7);
-        const int rr = (int)e < nv ? ids[r] : -1;
-        const unsigned off = rr >= 0 ? ((unsigned)rr * VB + (e - r * VB)) * 16u : OOB;
-        dma16(rsv, off, __builtin_amdgcn_readfirstlane(vbase + (unsigned)(u * nt) * 16u));
-    }
-    const unsigned xbase = lds_u32(xs) + (unsigned)wave * 1024u;
-    const int rowlen = BD * nc, nx = S * rowlen;
-    for (int u = 0; u < t.ux; ++u) {
-        const unsigned f = (unsigned)(u * nt + tid), q = fdiv(f, t.rowlen_m, t.rowlen_s);
-        const unsigned rem = f - q * (unsigned)rowlen, er = fdiv(rem, t.nc_m, t.nc_s);
-        const unsigned cl = rem - er * (unsigned)nc;
-        const int d = (int)f < nx ? ids[R + q] : -1;
-        const long el = XROW ? ((long)d + er) * p.ldx + t.c0 + cl
-                             : ((long)d + er) + (long)(t.c0 + cl) * p.ldx;
-        const unsigned off = d >= 0 ? (unsigned)(el * 16) : OOB;
-        dma16(rsx, off, __builtin_amdgcn_readfirstlane(xbase + (unsigned)(u * nt) * 16u));
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned long long c2 = p.probe ? __builtin_amdgcn_s_memtime() : 0;
-    __syncthreads();
-    const unsigned long long c3 = p.probe ? __builtin_amdgcn_s_memtime() : 0;
-    if (p.probe) {
-        probe_stamp(p.probe, 0, rt0);
-        probe_stamp(p.probe, 2, c1 - c0);
-        probe_stamp(p.probe, 3, c2 - c1);
-        probe_stamp(p.probe, 4, c3 - c2);
-    }
-    if (!active) {
-        if (p.probe) probe_stamp(p.probe, 1, __builtin_amdgcn_s_memrealtime());
-        return;
-    }
-    // 3) the products: direct blocks from registers, staged ones from LDS
-    E acc[BI];
-#pragma unroll
-    for (int c = 0; c < BI; ++c) acc[c] = Ops<E>::zero();
-    const E *vr = vals + i * VB;
-    auto apply = [&](const E *vb, const E *xv) {
-#pragma unroll
-        for (int e = 0; e < BD; ++e)
-#pragma unroll
-            for (int c = 0; c < BI; ++c) {
-                const E a = p.block_im_fast ? vb[c + e * BI] : vb[c * BD + e];
-                acc[c] = Ops<E>::fma(a, xv[e], acc[c]);
-            }
-    };
-#pragma unroll
-    for (int q = 0; q < ND; ++q) {
-        const unsigned j = ent[q] >> 28;
-        if (j == NONE) continue;
-        apply(vr + j * BLK, xg[q]);
-    }
-#pragma unroll
-    for (int q = ND; q < NE; ++q) {
-        const unsigned j = ent[q] >> 28;
-        if (j == NONE) continue;
-        const E *xr = xs + (ent[q] & 0x0fffffffu) * rowlen + g;
-        E xv[BD];
-#pragma unroll
-        for (int e = 0; e < BD; ++e) xv[e] = xr[e * nc];
-        apply(vr + j * BLK, xv);
-    }
-#pragma unroll
-    for (int c = 0; c < BI; ++c) {
-        const long img = (long)row * BI + c;
-        E *yp = YROW ? y + img * p.ldy + col : y + img + (long)col * p.ldy;
-        const E out = Ops<E>::scale(acc[c], p.alpha_re, p.alpha_im);
-        *yp = p.add ? Ops<E>::add(*yp, out) : out;
-    }
-    if (p.probe) {
-        probe_stamp(p.probe, 5, __builtin_amdgcn_s_memtime() - c3);
-        probe_stamp(p.probe, 1, __builtin_amdgcn_s_memrealtime());
-    }
-}
-
-constexpr int TILE_ND = 4;           // direct entries per row (bsr.cpp: build_tile_plan nd)
-constexpr long TILE_LDS_MAX = 65536; // two or more workgroups per CU
-constexpr int TILE_MAX_SLAB = 32;    // rhs columns per workgroup (one per thread)
-
-/// complex<double> operators with a tile plan: column slabs of at most 32 (false: not this shape)
-bool launch_tile(const BsrArgs &a, TileArgs t, long nchunks, long x_rows, bool yrow, bool xrow,
-                 hipStream_t s) {
-    if (a.ncols < g_bsr_tune.tile_min_cols || a.ncols > g_bsr_tune.tile_max_cols ||
-        nchunks >= (1L << 31))
-        return false;
-    const long v_bytes = a.block_rows * 81L * 16;
-    const long x_bytes = (xrow ? x_rows * a.ldx : a.ldx * a.ncols) * 16;
-    if (v_bytes >= (1L << 31) || x_bytes >= (1L << 31)) return false;
-    const long max_slab = g_bsr_tune.tile_slab > 0 ? g_bsr_tune.tile_slab : TILE_MAX_SLAB;
-    const long nslab = (a.ncols + max_slab - 1) / max_slab;
-    const int ncs = (int)((a.ncols + nslab - 1) / nslab);
-    const int nt = (t.R * ncs + 63) / 64 * 64;
-    if (nt > 512) return false;
-    t.uv = (t.R * 81 + nt - 1) / nt;
-    const long max_ux = ((long)t.S * 3 * ncs + nt - 1) / nt;
-    const size_t lds = (size_t)(t.uv + max_ux) * nt * 16 + 4 * (size_t)(t.R + t.S);
-    if ((long)lds > TILE_LDS_MAX) return false;
-    t.v_bytes = (unsigned)v_bytes;
-    t.x_bytes = (unsigned)x_bytes;
-    g_bsr_tune.last = 4;
-    KernelTimer timer("bsr", s);
-    for (long c0 = 0; c0 < a.ncols; c0 += ncs) {
-        t.c0 = (int)c0;
-        t.nc = (int)std::min<long>(ncs, a.ncols - c0);
-        t.ux = (t.S * 3 * t.nc + nt - 1) / nt;
-        magic((unsigned)(3 * t.nc), t.rowlen_m, t.rowlen_s);
-        magic((unsigned)t.nc, t.nc_m, t.nc_s);
-        int s81;
-        magic(81, t.div81_m, s81); // s81 == 7 (the kernel's constant)
-        auto kern = yrow ? (xrow ? bsr_tile_kernel<TILE_ND, true, true> : bsr_tile_kernel<TILE_ND, true, false>)
-                         : (xrow ? bsr_tile_kernel<TILE_ND, false, true> : bsr_tile_kernel<TILE_ND, false, false>);
-        hipLaunchKernelGGL(kern, dim3(nchunks), dim3(nt), lds, s, a, t);
-        SBX_HIP_CHECK(hipGetLastError());
-    }
-    return true;
 }
 
 template <typename E, int BI, int BD>
@@ -1661,13 +1193,13 @@ void launch_typed(const BsrArgs &a, int nnz_per_row, bool yrow, bool xrow, hipSt
         // one block row per wave: interleaving 2 or 4 rows per wave measured 6 % / 25 % slower
         // (more VGPRs, fewer waves to hide the HBM latency of the value stream)
         if constexpr (std::is_same<E, double2>::value)
-            launch_bsr_mfma<double, true, 12, 12, 1>(a, nnz_per_row, yrow, xrow, s);
+            launch_bsr_mfma<double, true, 12, 12>(a, nnz_per_row, yrow, xrow, s);
         else if constexpr (std::is_same<E, double>::value)
-            launch_bsr_mfma<double, false, 12, 12, 1>(a, nnz_per_row, yrow, xrow, s);
+            launch_bsr_mfma<double, false, 12, 12>(a, nnz_per_row, yrow, xrow, s);
         else if constexpr (std::is_same<E, float2>::value)
-            launch_bsr_mfma<float, true, 12, 12, 1>(a, nnz_per_row, yrow, xrow, s);
+            launch_bsr_mfma<float, true, 12, 12>(a, nnz_per_row, yrow, xrow, s);
         else
-            launch_bsr_mfma<float, false, 12, 12, 1>(a, nnz_per_row, yrow, xrow, s);
+            launch_bsr_mfma<float, false, 12, 12>(a, nnz_per_row, yrow, xrow, s);
     }
     else
         launch_layouts<E, 0, 0>(a, yrow, xrow, blocks, s);
@@ -1737,40 +1269,7 @@ void launch_bsr(const BsrDesc &d, int device) {
     a.alpha_re = d.alpha.re;
     a.alpha_im = d.alpha.im;
     a.add = d.add ? 1 : 0;
-    a.probe = (unsigned long long *)g_bsr_tune.probe;
-    a.ilv = std::max(1, g_bsr_tune.ell9_ilv);
-    // column passes (experiment, sbx_tune_set "bsr.colsplit"): with row-major x and y a launch
-    // over a column slice is the same product on shifted base pointers; fewer columns per pass
-    // shrink the x rows that must stay in L2 between a site's neighbours
-    const long cs = g_bsr_tune.colsplit;
-    if (cs > 0 && d.ncols > cs && d.x_row_major && d.y_row_major) {
-        const std::size_t es = dtype_size(d.t);
-        for (long c0 = 0; c0 < d.ncols; c0 += cs) {
-            BsrDesc q = d;
-            q.ncols = std::min(cs, d.ncols - c0);
-            q.x = (const char *)d.x + es * c0;
-            q.y = (char *)d.y + es * c0;
-            g_bsr_tune.colsplit = 0;
-            try {
-                launch_bsr(q, device);
-            } catch (...) {
-                g_bsr_tune.colsplit = cs;
-                throw;
-            }
-            g_bsr_tune.colsplit = cs;
-        }
-        return;
-    }
-    if (d.tile_R > 0 && g_bsr_tune.tile && g_bsr_tune.variant != 1 && d.t == SBX_CDOUBLE &&
-        d.bi == 3 && d.bd == 3 && d.num_nnz_per_row == 9) {
-        TileArgs t{};
-        t.rows = d.tile_rows;
-        t.ent = d.tile_ent;
-        t.staged = d.tile_staged;
-        t.R = d.tile_R;
-        t.S = d.tile_S;
-        if (launch_tile(a, t, d.tile_chunks, d.x_rows, d.y_row_major, d.x_row_major, s)) return;
-    }
+    a.ilv = 2; // an XCD's row chunks visited as two interleaved halves (bsr_ell9_kernel)
     switch (d.t) {
     case SBX_CDOUBLE: return launch_typed<double2>(a, d.num_nnz_per_row, d.y_row_major, d.x_row_major, s);
     case SBX_CFLOAT: return launch_typed<float2>(a, d.num_nnz_per_row, d.y_row_major, d.x_row_major, s);

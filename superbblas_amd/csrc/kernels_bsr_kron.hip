@@ -541,9 +541,7 @@ template <typename E> void launch_kron_typed(const KronArgs &a, hipStream_t s) {
             const long tasks = a.block_rows * ngroups, blocks = (tasks + 3) / 4;
             if (blocks < (1L << 31)) {
                 g_bsr_tune.last = 5;
-                // tools: dynamic LDS that caps the resident workgroups per CU (L2 footprint)
-                const size_t pad = (size_t)std::max(0L, g_bsr_tune.kron_lds_pad);
-                hipLaunchKernelGGL((bsr_kron_mfma_kernel<9, false>), dim3((unsigned)blocks), dim3(256), pad,
+                hipLaunchKernelGGL((bsr_kron_mfma_kernel<9, false>), dim3((unsigned)blocks), dim3(256), 0,
                                    s, a, (int)ngroups);
                 SBX_HIP_CHECK(hipGetLastError());
                 return;

@@ -228,80 +228,6 @@ __device__ __forceinline__ void chain_offsets(uint32_t idx, int n, const FastDiv
     }
 }
 
-// A tile = TU items of the U chain (contiguous runs in the source) x TV items of the V chain
-// (contiguous runs in the destination), each item a run of R elements contiguous on both sides.
-// Read phase: r fastest, then u, then v (coalesced source reads); write phase: r fastest, then
-// v, then u (coalesced destination writes); the tile is transposed through LDS.
-template <typename S, typename D, bool ADD>
-__global__ void __launch_bounds__(256) copy_tiled_kernel(const TiledArgs p) {
-    __shared__ D tile[tile_elems<D>() + 64];
-    __shared__ long su[256], du[256], sv[256], dv[256]; // per-item chain offsets of the tile
-
-    const S *__restrict__ src = (const S *)p.src;
-    D *__restrict__ dst = (D *)p.dstp;
-
-    // Decode the tile: blockIdx.x = (w * ntv + tv) * ntu + tu
-    uint32_t b = blockIdx.x;
-    const uint32_t tu = b % p.ntu;
-    b /= p.ntu;
-    const uint32_t tv = b % p.ntv;
-    uint32_t w = b / p.ntv;
-    long sbase = 0, dbase = 0;
-    for (int i = 0; i < p.nw; ++i) {
-        const uint32_t q = p.wsize[i].div(w);
-        const uint32_t c = w - q * p.wsize[i].d;
-        w = q;
-        sbase += (long)c * p.wsst[i];
-        dbase += (long)c * p.wdst[i];
-    }
-    const uint32_t u0 = tu * p.TU, v0 = tv * p.TV;
-    const uint32_t nu_t = min(p.TU, p.NU - u0), nv_t = min(p.TV, p.NV - v0);
-    for (uint32_t u = threadIdx.x; u < nu_t; u += 256)
-        chain_offsets(u0 + u, p.nu, p.usize, p.usst, p.udst, su[u], du[u]);
-    for (uint32_t v = threadIdx.x; v < nv_t; v += 256)
-        chain_offsets(v0 + v, p.nv, p.vsize, p.vsst, p.vdst, sv[v], dv[v]);
-    __syncthreads();
-
-    const uint32_t ld = p.TU * p.R + 1; // padded LDS row (one row per v)
-    constexpr int EPT = 4;              // elements per thread in flight
-    const uint32_t nread = p.R * p.TU * nv_t;
-    for (uint32_t e0 = threadIdx.x; e0 < nread; e0 += 256 * EPT) {
-        D val[EPT];
-        uint32_t li[EPT];
-#pragma unroll
-        for (int q = 0; q < EPT; ++q) {
-            const uint32_t e = e0 + 256 * q;
-            const uint32_t vv = p.fRTU.div(e);
-            const uint32_t rem = e - vv * (p.R * p.TU);
-            const uint32_t u = p.fR.div(rem);
-            const uint32_t r = rem - u * p.R;
-            const bool ok = e < nread && u < nu_t;
-            li[q] = ok ? vv * ld + u * p.R + r : 0xffffffffu;
-            // clamped (always valid) address: the loads of the EPT elements are all issued
-            // before the first use instead of one branch + wait per element
-            const uint32_t uc = ok ? u : 0, vc = ok ? vv : 0, rc = ok ? r : 0;
-            val[q] = xform<D, S>(src[sbase + su[uc] + sv[vc] + rc], p.alpha);
-        }
-#pragma unroll
-        for (int q = 0; q < EPT; ++q)
-            if (li[q] != 0xffffffffu) tile[li[q]] = val[q];
-    }
-    __syncthreads();
-    const uint32_t nwrite = p.R * p.TV * nu_t;
-    for (uint32_t e0 = threadIdx.x; e0 < nwrite; e0 += 256 * EPT) {
-#pragma unroll
-        for (int q = 0; q < EPT; ++q) {
-            const uint32_t e = e0 + 256 * q;
-            const uint32_t u = p.fRTV.div(e);
-            const uint32_t rem = e - u * (p.R * p.TV);
-            const uint32_t vv = p.fR.div(rem);
-            const uint32_t r = rem - vv * p.R;
-            if (e < nwrite && vv < nv_t)
-                put<ADD, D>(dst + dbase + du[u] + dv[vv] + r,
-                            tile[vv * ld + u * p.R + r]);
-        }
-    }
-}
 
 /// Offsets of item `idx` of a chain of dims (fastest first), unrolled for short chains
 __device__ __forceinline__ void chain_offsets4(uint32_t idx, int n, const FastDiv *size,
@@ -503,7 +429,7 @@ Norm normalize(const BoxCopyDesc &d) {
 /// (the launch cache below keys it on the box shape, element types and tuning switches; the
 /// reference caches its permutation index vectors the same way, tensor.h:919-961)
 struct CopyLaunch {
-    enum Kind { MASKED, CONTIG, DIRECT, TILED1, TILED3 } kind = DIRECT;
+    enum Kind { MASKED, CONTIG, DIRECT, TILED3 } kind = DIRECT;
     DirectArgs da{};
     TiledArgs ta{};
     long total = 0, blocks = 0;
@@ -539,17 +465,12 @@ void run_launch(const CopyLaunch &l, const void *src, void *dst, const Alpha &al
         hipLaunchKernelGGL((copy_direct_kernel<S, D, ADD>), grid, block, 0, stream, a);
         break;
     }
-    case CopyLaunch::TILED1:
     case CopyLaunch::TILED3: {
         g_copy_tune.last_pair = 0;
         TiledArgs a = l.ta;
         a.src = src;
         a.dstp = dst;
         a.alpha = alpha;
-        if (l.kind == CopyLaunch::TILED1) {
-            hipLaunchKernelGGL((copy_tiled_kernel<S, D, ADD>), grid, block, 0, stream, a);
-            break;
-        }
         constexpr bool PS = sizeof(S) == 8, PD = sizeof(D) == 8 && !ADD;
         if constexpr (PS || PD) {
             const bool vr = PS && l.vr && ((size_t)src & 15) == 0;
@@ -810,7 +731,7 @@ CopyLaunch prepare_pair(bool masked, Norm n, long total) {
         std::fprintf(stderr, " | R=%ld NU=%ld NV=%ld TU=%ld TV=%ld nu=%d nv=%d nw=%d blocks=%ld vr=%d vw=%d\n",
                      R, NU, NV, TU, TV, a.nu, a.nv, nw, blocks, l.vr, l.vw);
     }
-    l.kind = g_copy_tune.kernel == 1 ? CopyLaunch::TILED1 : CopyLaunch::TILED3;
+    l.kind = CopyLaunch::TILED3;
     l.blocks = blocks;
     return l;
 }
@@ -918,7 +839,7 @@ void launch_box_copy(const BoxCopyDesc &d, int device) {
                   ((long)(d.src_mask != nullptr) << 17) | ((long)(d.dst_mask != nullptr) << 18));
     key.push_back(g_copy_tune.budget);
     key.push_back(g_copy_tune.run);
-    key.push_back(g_copy_tune.kernel + 16L * g_copy_tune.nt + 256L * g_copy_tune.pair +
+    key.push_back(16L * g_copy_tune.nt + 256L * g_copy_tune.pair +
                   4096L * g_copy_tune.order);
     for (std::size_t i = 0; i < nd; ++i) {
         key.push_back(d.size[i]);

@@ -215,7 +215,6 @@ void clear_copy_plan_cache();
 struct CopyTune {
     long budget = 0; ///< elements per LDS tile
     long run = 0;    ///< target elements of a tile row's contiguous source run
-    int kernel = 0;  ///< 1: the round-1 tiled kernel (element-indexed phases) instead of the row-mapped one
     int nt = 0;      ///< row-mapped kernel stores: 0 = non-temporal for large outputs, 1 = always, -1 = never
     long max_elems = 0; ///< elements per launch before a box is cut into slabs (0 = 2^31 - 1)
     int pair = 0;  ///< tiled kernel, 8-byte elements: two elements per lane access where the runs allow (-1 = never)
@@ -234,43 +233,24 @@ struct GemmTune {
 };
 extern GemmTune g_gemm_tune;
 struct BsrTune {
-    int variant = 0; ///< BSR kernels: 0 = the library's choice, 1 = the round-1 kernels, 2 = no 12x12 block-staged kernel
-    int ell9 = 0;    ///< 9-point ELL kernel shape (workgroup size / lookahead / columns per thread), 0 = default
-    long ell9_lds = 0; ///< 9-point ELL kernel: bytes of block values staged per workgroup (0 = default)
-    long colsplit = 0; ///< rhs columns per launch (row-major x and y), 0 = all at once
-    int tile = 0;      ///< 9-point 3x3 operators: lattice-tiled kernel with x reuse in LDS (experiment; the
-                       ///< plan is built by create_bsr only while this is on)
-    long tile_min_cols = 8;  ///< ... for this many rhs columns ...
-    long tile_max_cols = 16; ///< ... up to this many (measured: the chunked kernel is as fast or faster outside)
-    long tile_slab = 0;      ///< ... rhs columns per workgroup (0 = default, 32)
-    int tile_rows = 16;     ///< ... block rows per tile (the plan, built by create_bsr)
+    int variant = 0; ///< BSR kernels: 0 = the library's choice, 1 = the generic kernels only (no 9-point
+                     ///< or block-staged specialisation), 2 = no 12x12 block-staged kernel
     long row_max_cols = 3;  ///< 9-point 3x3 operators: one thread per nonzero block up to this many rhs columns (0 = off)
-    int row_dma = 1;        ///< ... values staged by LDS-DMA (16-byte elements)
     long split_max_cols = 32; ///< 9-point 3x3 complex<double> operators, row-major x: rows split over their
                               ///< nonzero blocks (bsr_ell9_split_kernel) from row_max_cols + 1 to this many
                               ///< rhs columns (0 = off)
-    int split_cw = 0;  ///< ... rhs columns per thread (1, 2, 4; 0 = by the column count)
-    int split_jb = 0;  ///< ... nonzero blocks per thread (1, 3, 9; 0 = default)
-    int split_nt = 0;  ///< ... threads per workgroup to aim at (0 = 256)
+    int split_cw = 0;  ///< ... rhs columns per thread (1 or 2; 0 = by the column count)
+    int split_jb = 0;  ///< ... nonzero blocks per thread (3 or 9; 0 = by the column count)
     int split_ilv = 2; ///< ... an XCD's rows visited as this many interleaved parts
-    int split_ovl = 1; ///< ... the partial products overlay the staged values in LDS (0 = beside them)
-    int split_rw = 0;  ///< ... block rows per workgroup (0 = as many as the thread and LDS budgets allow)
-    int ell9_ilv = 2;  ///< the same for the row-chunk 9-point kernel (bsr_ell9_kernel)
-    long long probe = 0;    ///< tools only: device buffer for per-workgroup time stamps
-    int blk_dma = -1; ///< 12x12 (block-staged) operators: blocks staged by LDS-DMA, 1 or 2 blocks ahead
-                      ///< (0 = registers, -1 = the library's choice: 1)
-    int blk_pack = 1; ///< ... the value and x blocks packed in one run of the LDS slot: 1 = for 8-byte elements,
-                      ///< 2 = always, 0 = never (1-KB rounded each)
     int kron_mfma = 1;          ///< Kronecker 3x3 (color) x 4x4 (spin) complex<double>: spin products on the
                                 ///< matrix cores (bsr_kron_mfma_kernel) ...
     long kron_mfma_min_cols = 8; ///< ... from this many rhs columns
-    long kron_lds_pad = 0;       ///< tools: LDS bytes per workgroup of that kernel (caps its residency)
     int kron_pack = 1;           ///< ... below 16 rhs columns: a wave's 16 column slots span several rows (0 = off)
     /// read-back ("bsr.last_kernel"; atomic: launches may come from several host threads): the form
     /// of the last launch -- 1 one thread per block (3x3), 2 split rows (3x3), 3 row chunks (3x3),
-    /// 4 lattice tiles (3x3), 5 Kronecker on MFMA, 6 the same with packed column slots, 7 12x12 blocks
-    /// by LDS-DMA, 8 the same with packed slots, 9 12x12 blocks through registers, 10 12x12 fragment
-    /// gathers (9 blocks per row), 11 12x12 generic rows, 0 another kernel
+    /// 5 Kronecker on MFMA, 6 the same with packed column slots, 7 12x12 blocks by LDS-DMA, 8 the
+    /// same with packed slots, 10 12x12 fragment gathers (9 blocks per row), 11 12x12 generic rows,
+    /// 0 another kernel
     std::atomic<int> last{0};
 };
 extern BsrTune g_bsr_tune;
@@ -315,16 +295,6 @@ struct BsrDesc {
     // (block row, bi, ncols, ki), both row major; jj holds the domain site of each nonzero
     int ki = 1, kd = 1;
     const void *kron = nullptr; ///< num_nnz_per_row matrices of ki x kd
-    // lattice-tile plan of a 9-nonzero 3x3 operator (bsr.cpp build_tile_plan), or tile_R = 0:
-    // chunks of tile_R block rows (tile_rows, -1 = padding), per row tile_nd direct entries then
-    // num_nnz_per_row staged entries ((j << 28) | index, j = 15: none; index = domain block row
-    // for direct entries, slot in the chunk's staged list for staged ones), and per chunk tile_S
-    // staged domain block rows (-1 = padding), read into LDS once and shared by the chunk's rows
-    int tile_R = 0, tile_S = 0, tile_nd = 0;
-    long tile_chunks = 0;
-    const int *tile_rows = nullptr;
-    const unsigned *tile_ent = nullptr;
-    const int *tile_staged = nullptr;
 };
 void launch_bsr(const BsrDesc &d, int device);
 void launch_bsr_kron(const BsrDesc &d, int device);

@@ -77,7 +77,7 @@ def test_bsr_lattice(gpu, spin, color, ncols, y_layout):
 @pytest.mark.parametrize("variant", [0, 1])
 def test_bsr_ragged_rows(gpu, spin, color, ncols, variant):
     """Rows with 0..9 nonzero blocks (a CSR operator, not ELL): the general-row kernels (12x12:
-    the one-block-ahead MFMA kernel, variant 0, and the round-1 kernel, variant 1), exact."""
+    the one-block-ahead MFMA kernel, variant 0, and the generic-row kernels, variant 1), exact."""
     import torch
     import superbblas_amd as sb
     L = 4
@@ -95,9 +95,6 @@ def test_bsr_ragged_rows(gpu, spin, color, ncols, variant):
     oracle_bsr(T_CDOUBLE, dim, 0, vol, b, b, ii2, jj2, vals2, False, x, ncols, True, yref, ncols,
                True, ncols, 1.0)
     full = [([0] * 6, dim)]
-    if isinstance(variant, str):  # the block-staged kernel's LDS-DMA ring (1 / 2 ahead) or registers
-        sb.tune_set("bsr.blk_dma", {"dma1": 1, "dma2": 2, "reg": 0}[variant])
-        variant = 0
     sb.tune_set("bsr.variant", variant)
     try:
         op = sb.create_bsr(full, dim, full, dim, [1, 1, 1, 1, spin, color],
@@ -112,7 +109,6 @@ def test_bsr_ragged_rows(gpu, spin, color, ncols, variant):
         op.destroy()
     finally:
         sb.tune_set("bsr.variant", 0)
-        sb.tune_set("bsr.blk_dma", -1)
     assert np.array_equal(ty.cpu().numpy(), yref)
 
 
@@ -225,14 +221,14 @@ def test_bsr_image_side(gpu, spin, color, ncols, beta, power):
     assert np.array_equal(ty.cpu().numpy(), yref)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, "dma1", "dma2", "reg"])
+@pytest.mark.parametrize("variant", [0, 1, 2])
 @pytest.mark.parametrize("ncols,dtype", [(3, np.complex128), (16, np.complex64), (20, np.complex128),
                                          (5, np.float64), (12, np.complex64), (12, np.float32)])
 def test_bsr_12x12_kernel_forms(gpu, variant, ncols, dtype):
     """The 12x12 (spin x color) 9-point operator through every kernel form: the block-staged
-    MFMA kernel (variant 0, row-major x with ncols <= 16; its blocks staged by LDS-DMA one or two
-    blocks ahead, dma1 / dma2, or through registers, reg), the column-preloading MFMA kernel
-    (variant 2, and variant 0 beyond 16 columns) and the round-1 kernel (variant 1); exact."""
+    MFMA kernel (variant 0, row-major x with ncols <= 16; blocks staged by LDS-DMA one ahead,
+    packed slots for 8-byte elements), the column-preloading MFMA kernel (variant 2, and variant
+    0 beyond 16 columns) and the generic-row MFMA kernel (variant 1); exact."""
     import torch
     import superbblas_amd as sb
     from _common import TYPE_OF
@@ -247,9 +243,6 @@ def test_bsr_12x12_kernel_forms(gpu, variant, ncols, dtype):
                yref, ncols, True, ncols, 1.0)
     full = [([0] * 6, dim)]
     blk = [1, 1, 1, 1, spin, color]
-    if isinstance(variant, str):  # the block-staged kernel's LDS-DMA ring (1 / 2 ahead) or registers
-        sb.tune_set("bsr.blk_dma", {"dma1": 1, "dma2": 2, "reg": 0}[variant])
-        variant = 0
     sb.tune_set("bsr.variant", variant)
     try:
         op = sb.create_bsr(full, dim, full, dim, blk, blk, False, [torch.from_numpy(ii).to(gpu)],
@@ -263,7 +256,6 @@ def test_bsr_12x12_kernel_forms(gpu, variant, ncols, dtype):
         op.destroy()
     finally:
         sb.tune_set("bsr.variant", 0)
-        sb.tune_set("bsr.blk_dma", -1)
     assert np.array_equal(ty.cpu().numpy(), yref)
 
 

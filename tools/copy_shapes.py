@@ -78,17 +78,15 @@ def sweep(spec):
 def main():
     if os.environ.get("COPY_SWEEP"):
         return sweep(os.environ["COPY_SWEEP"])
-    combos = ((0, 0, 0), (0, 0, -1), (0, 0, -2), (1, 0, 0), (0, -1, 0))
+    combos = ((0, 0, 0), (0, 0, -1), (0, 0, -2), (0, -1, 0))
     if os.environ.get("COPY_QUICK"):
         combos = combos[:3]
     for kern, nt, pair in combos:
-        sb.tune_set("copy.kernel", kern)
         sb.tune_set("copy.nt", nt)
         sb.tune_set("copy.pair", 0 if pair == -2 else pair)
         sb.tune_set("copy.order", -1 if pair == -2 else 0)  # -2: pairs, destination chain first
-        print(json.dumps({"copy.kernel": kern, "copy.nt": nt, "copy.pair": pair}))
+        print(json.dumps({"copy.nt": nt, "copy.pair": pair}))
         shapes()
-    sb.tune_set("copy.kernel", 0)
     sb.tune_set("copy.nt", 0)
     sb.tune_set("copy.pair", 0)
     sb.tune_set("copy.order", 0)

@@ -90,15 +90,6 @@ def main():
     dev = torch.device("cuda", 0)
     L = int(os.environ.get("L", "16"))
     only = os.environ.get("KRON_ONLY")  # e.g. "complex128:12"
-    if os.environ.get("KRON_PADS"):  # LDS padding sweep of the MFMA kernel (residency per CU)
-        for pad in [int(v) for v in os.environ["KRON_PADS"].split(",")]:
-            sb.tune_set("bsr.kron_lds_pad", pad)
-            for n in (12, 24):
-                r = run(L, n, dev)
-                r["lds_pad"] = pad
-                print(json.dumps(r), flush=True)
-        sb.tune_set("bsr.kron_lds_pad", 0)
-        return
     if os.environ.get("KRON_PACKS"):  # packed column slots of the MFMA kernel on / off, round robin
         for n in [int(v) for v in os.environ.get("KRON_NS", "8,12").split(",")]:
             for rnd in range(2):

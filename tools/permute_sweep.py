@@ -58,9 +58,9 @@ def main():
     ref = None
     configs = [dict(), dict(budget=1536), dict(budget=1024), dict(budget=512), dict(budget=384),
                dict(budget=256), dict(run=24), dict(run=12, budget=384),
-               dict(run=96), dict(run=96, budget=1536), dict(kernel=1), dict(nt=-1)]
+               dict(run=96), dict(run=96, budget=1536), dict(nt=-1)]
     for cfg in configs:
-        for k in ("budget", "run", "kernel", "nt"):
+        for k in ("budget", "run", "nt"):
             sb.tune_set("copy." + k, cfg.get(k, 0))
         b.zero_()
 
