@@ -297,3 +297,4 @@ def test_paired_8byte_transposes(gpu, t0, t1):
     assert 0 in forms, forms
     assert any(f & 1 for f in forms) == (np.dtype(t0).itemsize == 8), forms
     assert any(f & 2 for f in forms) == (np.dtype(t1).itemsize == 8), forms
+
