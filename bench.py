@@ -1143,10 +1143,8 @@ def wilson_bench(sb, dev, L, ncols=12, reps=5):
     return out
 
 
-def bsr_bench(sb, dev, L, ncols_list=(1, 12, 64), reps=5):
-    """config 3: 16^4 periodic 9-point stencil, 3x3 blocks, complex<double>, n = 1 / 12 / 64 rhs.
-    Kernel time from the library's HIP-event timers on the launch stream; algorithmic bytes
-    16 (81 V + 2 3 V n) + 4 (9 V + V + 1) per application (DESIGN.md 5.3)."""
+def bsr_operator(sb, dev, L):
+    """config 3's operator: 16^4 periodic 9-point stencil, 3x3 blocks, complex<double>."""
     dim = [L, L, L, L, 1, 3]
     V = L ** 4
     sites = np.array(np.unravel_index(np.arange(V), (L, L, L, L))).T
@@ -1163,20 +1161,35 @@ def bsr_bench(sb, dev, L, ncols_list=(1, 12, 64), reps=5):
     vals = torch.empty(V * 9 * 9, dtype=torch.complex128, device=dev)
     fill(vals, 9)
     full = [([0] * 6, dim)]
-    op = sb.create_bsr(full, dim, full, dim, [1, 1, 1, 1, 1, 3], [1, 1, 1, 1, 1, 3], False,
-                       [torch.from_numpy(ii).to(dev)], [torch.from_numpy(jj.reshape(-1)).to(dev)],
-                       [vals])
+    return sb.create_bsr(full, dim, full, dim, [1, 1, 1, 1, 1, 3], [1, 1, 1, 1, 1, 3], False,
+                         [torch.from_numpy(ii).to(dev)],
+                         [torch.from_numpy(jj.reshape(-1)).to(dev)], [vals])
+
+
+def bsr_setup(sb, dev, L, ncols, op=None):
+    """(op, x, y, run) for one config-3 product y = A x with ncols rhs (run() launches it)."""
+    op = op or bsr_operator(sb, dev, L)
+    dimx = [1, L, L, L, L, 1, 3, ncols]
+    x = torch.empty(vol(dimx), dtype=torch.complex128, device=dev)
+    fill(x, 10)
+    y = torch.empty_like(x)
+    px = [([0] * 8, dimx)]
+
+    def run():
+        sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", px, "pXYZTSCn", [0] * 8, dimx, dimx, [x],
+                      0.0, px, "pxyztscn", [0] * 8, dimx, dimx, "p", [y])
+    return op, x, y, run
+
+
+def bsr_bench(sb, dev, L, ncols_list=(1, 12, 64), reps=5):
+    """config 3: 16^4 periodic 9-point stencil, 3x3 blocks, complex<double>, n = 1 / 12 / 64 rhs.
+    Kernel time from the library's HIP-event timers on the launch stream; algorithmic bytes
+    16 (81 V + 2 3 V n) + 4 (9 V + V + 1) per application (DESIGN.md 5.3)."""
+    V = L ** 4
+    op = bsr_operator(sb, dev, L)
     out = {}
     for ncols in ncols_list:
-        dimx = [1, L, L, L, L, 1, 3, ncols]
-        x = torch.empty(vol(dimx), dtype=torch.complex128, device=dev)
-        fill(x, 10)
-        y = torch.empty_like(x)
-        px = [([0] * 8, dimx)]
-
-        def run():
-            sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", px, "pXYZTSCn", [0] * 8, dimx, dimx, [x],
-                          0.0, px, "pxyztscn", [0] * 8, dimx, dimx, "p", [y])
+        _, x, y, run = bsr_setup(sb, dev, L, ncols, op)
         # first launch loads the code object; then ~0.1 s of the kernel to steady clocks
         t_end = time.perf_counter() + 0.1
         while True:
