@@ -462,6 +462,11 @@ def main():
             side.update(cpu_side_baselines())
 
     traffic, traffic_src = pmc_traffic("dma_kernel<", "128, 128, 16, 4, 4")
+    if world > 1:
+        # the committed PMC pass is of the single-GPU configs[1] GEMM; a rank's configs[3] GEMM
+        # has another shape (k, batch), so its traffic is not known from it
+        traffic, traffic_src = None, ("no PMC pass of the per-rank configs[3] GEMM shape (%s)"
+                                      % traffic_src)
     if rank == 0:
         if config == "1":
             workload = ("configs[1]: 16^4 lattice spin x color contraction tnsxyzc x tNSxyzc -> "
@@ -506,6 +511,9 @@ def main():
                          "traffic_source": traffic_src,
                          "algorithmic_bytes": 16.0 * (vol(p0[rank][1]) + vol(p1[rank][1]) +
                                                       vol(gdimr)),
+                         "per": ("one GEMM launch of rank 0 (achieved, traffic and "
+                                 "algorithmic_bytes are per rank)" if world > 1 else
+                                 "one GEMM launch"),
                          "kernel": "gemm_dma_kernel<complex<double>, 128x128x%d, %d waves> (FP64 "
                                    "MFMA 16x16x4, complex %s) + split-K reduce, %d launches, %.4f "
                                    "ms avg (HIP events on its launch stream)" % (
