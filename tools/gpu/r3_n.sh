@@ -1,0 +1,5 @@
+# round 3 (session 2): freshly rebuilt tree -- smoke, the whole -m gpu suite, the default bench line
+cd /root/repo && export TMPDIR=/tmp && mkdir -p gpurun_out/r3_n && O=gpurun_out/r3_n &&
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 &&
+timeout -k 10 1100 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 &&
+timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err
