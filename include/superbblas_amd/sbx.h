@@ -110,11 +110,13 @@ int sbx_timings_report(char *buf, int len);
 /* ---- tuning hook (no reference counterpart) ----
    Override a kernel-shape choice of the library for tuning / comparison runs.  The defaults are
    the measured winners; read a key with sbx_tune_get before changing it to
-   restore it afterwards.  Keys include "gemm.m3", "gemm.splits", "gemm.max_bytes", "gemm.t48",
-   "gemm.share_ab", "copy.kernel", "copy.nt", "copy.budget", "copy.run", "copy.max_elems",
-   "copy.pair", "copy.order", "bsr.variant", "bsr.blk_dma", "bsr.blk_pack", "bsr.split_cw",
-   "bsr.split_jb", "bsr.split_ovl", "bsr.split_ilv"; read-backs "bsr.last_kernel",
-   "copy.last_pair".  Unknown keys fail with an error. */
+   restore it afterwards.  Keys: "gemm.m3", "gemm.splits", "gemm.max_bytes", "gemm.t48",
+   "gemm.share_ab", "copy.nt", "copy.budget", "copy.run", "copy.max_elems", "copy.pair",
+   "copy.order", "copy.trans", "bsr.variant", "bsr.row_max_cols", "bsr.split_max_cols",
+   "bsr.split_cw", "bsr.split_jb", "bsr.split_ilv", "bsr.kron_mfma", "bsr.kron_mfma_min_cols",
+   "bsr.kron_pack", "dist.reduce", "alloc.max_cached"; read-backs "bsr.last_kernel",
+   "copy.last_pair", "dist.reduce_calls", "alloc.cross_stream_frees".  Unknown keys fail with an
+   error. */
 int sbx_tune_set(const char *key, long long value);
 int sbx_tune_get(const char *key, long long *value);
 

@@ -410,6 +410,7 @@ int sbx_tune_set(const char *key, long long value) {
         else if (k == "copy.max_elems") g_copy_tune.max_elems = (long)value;
         else if (k == "copy.pair") g_copy_tune.pair = (int)value;
         else if (k == "copy.order") g_copy_tune.order = (int)value;
+        else if (k == "copy.trans") g_copy_tune.trans = (int)value;
         else if (k == "gemm.max_bytes") g_gemm_tune.max_bytes = (long)value;
         else if (k == "bsr.variant") g_bsr_tune.variant = (int)value;
         else if (k == "bsr.row_max_cols") g_bsr_tune.row_max_cols = (long)value;
@@ -428,6 +429,11 @@ int sbx_tune_set(const char *key, long long value) {
         else if (k == "dist.reduce_calls") g_dist_reduce_calls = value;
         else if (k.compare(0, 6, "alloc.") == 0) alloc_tune(key, nullptr, &value);
         else throw Error("tune_set: unknown key " + k);
+        if (k.compare(0, 5, "copy.") == 0) {
+            // recorded launch tapes replay the kernel form chosen when they were recorded
+            std::lock_guard<std::mutex> g(g_tape_mutex);
+            tapes().clear();
+        }
     });
 }
 
@@ -441,6 +447,7 @@ int sbx_tune_get(const char *key, long long *value) {
         else if (k == "copy.max_elems") *value = g_copy_tune.max_elems;
         else if (k == "copy.pair") *value = g_copy_tune.pair;
         else if (k == "copy.order") *value = g_copy_tune.order;
+        else if (k == "copy.trans") *value = g_copy_tune.trans;
         else if (k == "copy.last_pair") *value = g_copy_tune.last_pair;
         else if (k == "gemm.max_bytes") *value = g_gemm_tune.max_bytes;
         else if (k == "bsr.variant") *value = g_bsr_tune.variant;

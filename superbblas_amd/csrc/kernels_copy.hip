@@ -383,6 +383,131 @@ __global__ void __launch_bounds__(256) copy_tiled3_kernel(const TiledArgs p) {
     }
 }
 
+// Site-block transpose (round 3): the copies whose source is one contiguous run over
+// [R, the U chain, a dimension V1] and whose destination is contiguous over [R, V1] -- a transpose
+// of V1 against the U chain in items of R elements, e.g. the config-2p permute xyztsc -> slice n
+// of tnsxyzc (R = c, U = (s, t), V1 = xyz).  A workgroup takes QT items of V1 with ALL of U: its
+// source is one contiguous run of QT*NU*R elements, loaded coalesced with every load of a thread
+// in flight at once, transposed through LDS (one element of padding per V1 item) and written as
+// NU runs of QT*R destination elements.  Against the general tile kernel (a tile row spans only
+// part of U, offset tables per element, rows walked in several dependent rounds) the config-2p
+// slice loop goes 5.2 -> 3.5 us per slice (tools/permute_micro.hip).
+constexpr int TRANS_EMAX = 1536; // elements per tile
+constexpr int TRANS_KMAX = TRANS_EMAX / 256;
+struct TransArgs {
+    uint32_t R, NU, QT, NV1;  // run, U chain items, V1 items per tile, V1 extent
+    uint32_t ntv;             // tiles along V1
+    FastDiv fNUR, fQTR, fR;   // NU*R, QT*R, R
+    // thread strides of the two phases, as whole steps: 256 = qi*NU*R + ri (loads), 256 =
+    // qo*QT*R + ro and ro = qr*R + rr (stores)
+    uint32_t qi, ri, qo, ro, qr, rr;
+    long ssv, dsv;            // V1 strides (source NU*R, destination R)
+    int nu;                   // U chain dims (source order, fastest first)
+    FastDiv usize[MAXD];
+    long udst[MAXD];
+    int nw;                   // outer dims
+    FastDiv wsize[MAXD];
+    long wsst[MAXD], wdst[MAXD];
+    int nt;                   // non-temporal stores
+    const void *src;
+    void *dstp;
+    Alpha alpha;
+};
+
+// A1: alpha == 1 (plain data movement, no scaling code); FULL (uniform per workgroup): the tile
+// fills every thread's KMAX elements on both phases (no per-element guards)
+template <typename S, typename D, bool ADD, bool A1, bool FULL>
+__device__ __forceinline__ void trans_body(const TransArgs &p, D *tile, const long *du, const S *s0,
+                                           D *d0, uint32_t qt, uint32_t E) {
+    const uint32_t t = threadIdx.x, NUR = p.NU * p.R, LD = NUR + 1;
+    S r[TRANS_KMAX];
+#pragma unroll
+    for (int k = 0; k < TRANS_KMAX; ++k)
+        if (FULL || t + 256 * k < E) r[k] = s0[t + 256 * k];
+    // element j of the run sits at (item, e) = divmod(j, NU*R), stepped incrementally
+    uint32_t item = p.fNUR.div(t), e = t - item * NUR;
+#pragma unroll
+    for (int k = 0; k < TRANS_KMAX; ++k) {
+        if (FULL || t + 256 * k < E)
+            tile[item * LD + e] = A1 ? conv<D, S>(r[k]) : xform<D, S>(r[k], p.alpha);
+        item += p.qi;
+        e += p.ri;
+        if (e >= NUR) {
+            e -= NUR;
+            ++item;
+        }
+    }
+    __syncthreads();
+    // the destination: for each U item a run of QT*R elements (items v0.. of V1, R each); thread
+    // t writes (u, item, c) of positions t, t + 256, ... of the U-major order
+    const uint32_t QTR = p.QT * p.R;
+    uint32_t u = p.fQTR.div(t), x = t - u * QTR;
+    uint32_t it = p.fR.div(x), c = x - it * p.R;
+#pragma unroll
+    for (int k = 0; k < TRANS_KMAX; ++k) {
+        if (FULL || (u < p.NU && it < qt)) {
+            const D val = tile[it * LD + u * p.R + c];
+            D *q = d0 + du[u] + (long)it * p.dsv + c;
+            if (!ADD && p.nt)
+                store_nt(q, val);
+            else
+                put<ADD, D>(q, val);
+        }
+        u += p.qo;
+        it += p.qr;
+        c += p.rr;
+        if (c >= p.R) {
+            c -= p.R;
+            ++it;
+        }
+        if (it >= p.QT) {
+            it -= p.QT;
+            ++u;
+        }
+    }
+}
+
+template <typename S, typename D, bool ADD, bool A1>
+__global__ void __launch_bounds__(256) copy_trans_kernel(const TransArgs p) {
+    __shared__ D tile[TRANS_EMAX + 256];
+    __shared__ long du[256];
+    uint32_t b = blockIdx.x;
+    const uint32_t tv = b % p.ntv;
+    uint32_t w = b / p.ntv;
+    long sbase = 0, dbase = 0;
+#pragma unroll
+    for (int i = 0; i < MAXD; ++i) {
+        if (i >= p.nw) break;
+        const uint32_t q = p.wsize[i].div(w);
+        const uint32_t c = w - q * p.wsize[i].d;
+        w = q;
+        sbase += (long)c * p.wsst[i];
+        dbase += (long)c * p.wdst[i];
+    }
+    const uint32_t t = threadIdx.x, v0 = tv * p.QT;
+    const uint32_t qt = min(p.QT, p.NV1 - v0), E = qt * p.NU * p.R;
+    if (t < p.NU) {
+        // destination offset of U item t (the U chain's dims, fastest first)
+        uint32_t idx = t;
+        long o = 0;
+#pragma unroll
+        for (int i = 0; i < MAXD; ++i) {
+            if (i >= p.nu) break;
+            const uint32_t q = p.usize[i].div(idx);
+            o += (long)(idx - q * p.usize[i].d) * p.udst[i];
+            idx = q;
+        }
+        du[t] = o;
+    }
+    // the tile's source: one contiguous run of E elements
+    const S *s0 = (const S *)p.src + sbase + (long)v0 * p.ssv;
+    D *d0 = (D *)p.dstp + dbase + (long)v0 * p.dsv;
+    if (E == 256 * TRANS_KMAX && p.NU * p.QT * p.R == 256 * TRANS_KMAX)
+        trans_body<S, D, ADD, A1, true>(p, tile, du, s0, d0, qt, E);
+    else
+        trans_body<S, D, ADD, A1, false>(p, tile, du, s0, d0, qt, E);
+}
+
 template <typename T> struct DT;
 template <> struct DT<float> { static constexpr int v = SBX_FLOAT; };
 template <> struct DT<double> { static constexpr int v = SBX_DOUBLE; };
@@ -429,9 +554,10 @@ Norm normalize(const BoxCopyDesc &d) {
 /// (the launch cache below keys it on the box shape, element types and tuning switches; the
 /// reference caches its permutation index vectors the same way, tensor.h:919-961)
 struct CopyLaunch {
-    enum Kind { MASKED, CONTIG, DIRECT, TILED3 } kind = DIRECT;
+    enum Kind { MASKED, CONTIG, DIRECT, TILED3, TRANS } kind = DIRECT;
     DirectArgs da{};
     TiledArgs ta{};
+    TransArgs tr{};
     long total = 0, blocks = 0;
     int nt = 0;
     int vr = 0, vw = 0; // tiled: the shape allows paired reads / writes (pointers checked per call)
@@ -463,6 +589,18 @@ void run_launch(const CopyLaunch &l, const void *src, void *dst, const Alpha &al
         a.dstp = dst;
         a.alpha = alpha;
         hipLaunchKernelGGL((copy_direct_kernel<S, D, ADD>), grid, block, 0, stream, a);
+        break;
+    }
+    case CopyLaunch::TRANS: {
+        g_copy_tune.last_pair = 4;
+        TransArgs a = l.tr;
+        a.src = src;
+        a.dstp = dst;
+        a.alpha = alpha;
+        if (alpha.one == 1)
+            hipLaunchKernelGGL((copy_trans_kernel<S, D, ADD, true>), grid, block, 0, stream, a);
+        else
+            hipLaunchKernelGGL((copy_trans_kernel<S, D, ADD, false>), grid, block, 0, stream, a);
         break;
     }
     case CopyLaunch::TILED3: {
@@ -504,6 +642,81 @@ void run_launch(const CopyLaunch &l, const void *src, void *dst, const Alpha &al
     SBX_HIP_CHECK(hipGetLastError());
 }
 
+/// The site-block transpose (copy_trans_kernel) when the normalised box has the shape it takes:
+/// a dim V1 of destination stride R whose source stride is R * NU, NU the product of a chain of
+/// dims whose source strides run R, R*u0, ... up to it (the U chain; at most 256 items and at
+/// least two V1 items per tile)
+template <typename D>
+bool prepare_trans(CopyLaunch &l, const Norm &n, int first, long R, long total) {
+    const int nd = (int)n.size.size();
+    int v1 = -1;
+    for (int i = first; i < nd; ++i)
+        if (n.ds[i] == R && n.size[i] > 1) v1 = i;
+    if (v1 < 0 || n.ss[v1] % R) return false;
+    const long NU = n.ss[v1] / R;
+    if (NU < 2 || NU > 256 || NU * R * 2 > TRANS_EMAX) return false;
+    std::vector<bool> used(nd, false);
+    for (int i = 0; i < first; ++i) used[i] = true;
+    used[v1] = true;
+    std::vector<int> U;
+    long want = R;
+    while (want < n.ss[v1]) {
+        int f = -1;
+        for (int i = first; i < nd; ++i)
+            if (!used[i] && n.ss[i] == want) f = i;
+        if (f < 0) return false;
+        U.push_back(f);
+        used[f] = true;
+        want *= n.size[f];
+    }
+    if (want != n.ss[v1] || (int)U.size() > MAXD) return false;
+    TransArgs &a = l.tr;
+    const long QT = std::min(n.size[v1], (long)TRANS_EMAX / (NU * R));
+    a.R = (uint32_t)R;
+    a.NU = (uint32_t)NU;
+    a.QT = (uint32_t)QT;
+    a.NV1 = (uint32_t)n.size[v1];
+    a.ntv = (uint32_t)((n.size[v1] + QT - 1) / QT);
+    a.fNUR = FastDiv((uint32_t)(NU * R));
+    a.fQTR = FastDiv((uint32_t)(QT * R));
+    a.fR = FastDiv((uint32_t)R);
+    a.qi = (uint32_t)(256 / (NU * R));
+    a.ri = (uint32_t)(256 % (NU * R));
+    a.qo = (uint32_t)(256 / (QT * R));
+    a.ro = (uint32_t)(256 % (QT * R));
+    a.qr = a.ro / (uint32_t)R;
+    a.rr = a.ro % (uint32_t)R;
+    a.ssv = n.ss[v1];
+    a.dsv = n.ds[v1];
+    a.nu = (int)U.size();
+    for (std::size_t k = 0; k < U.size(); ++k) {
+        a.usize[k] = FastDiv((uint32_t)n.size[U[k]]);
+        a.udst[k] = n.ds[U[k]];
+    }
+    long NW = 1;
+    int nw = 0;
+    for (int i = first; i < nd; ++i) {
+        if (used[i]) continue;
+        if (nw == MAXD) return false;
+        a.wsize[nw] = FastDiv((uint32_t)n.size[i]);
+        a.wsst[nw] = n.ss[i];
+        a.wdst[nw] = n.ds[i];
+        NW *= n.size[i];
+        ++nw;
+    }
+    a.nw = nw;
+    a.nt = g_copy_tune.nt > 0 || (g_copy_tune.nt == 0 && total * (long)sizeof(D) >= (8L << 20));
+    const long blocks = (long)a.ntv * NW;
+    if (blocks >= (1L << 31)) return false;
+    l.kind = CopyLaunch::TRANS;
+    l.blocks = blocks;
+    static const bool debug = getenv("SBX_COPY_DEBUG") != nullptr;
+    if (debug)
+        std::fprintf(stderr, "copy_trans: R=%ld NU=%ld V1=%ld QT=%ld nu=%d nw=%d blocks=%ld\n", R, NU,
+                     n.size[v1], QT, a.nu, nw, blocks);
+    return true;
+}
+
 template <typename S, typename D, bool ADD>
 CopyLaunch prepare_pair(bool masked, Norm n, long total) {
     CopyLaunch l;
@@ -542,6 +755,7 @@ CopyLaunch prepare_pair(bool masked, Norm n, long total) {
         R = n.size[0];
         first = 1;
     }
+    if (g_copy_tune.trans >= 0 && sizeof(S) == 16 && prepare_trans<D>(l, n, first, R, total)) return l;
     // V chain: dims contiguous in the destination from stride R (destination order);
     // U chain: dims contiguous in the source from stride R, not in V.  Both are capped so that a
     // tile holds a few hundred items on each side.
@@ -840,7 +1054,7 @@ void launch_box_copy(const BoxCopyDesc &d, int device) {
     key.push_back(g_copy_tune.budget);
     key.push_back(g_copy_tune.run);
     key.push_back(16L * g_copy_tune.nt + 256L * g_copy_tune.pair +
-                  4096L * g_copy_tune.order);
+                  4096L * g_copy_tune.order + 65536L * g_copy_tune.trans);
     for (std::size_t i = 0; i < nd; ++i) {
         key.push_back(d.size[i]);
         key.push_back(d.src_stride[i]);

@@ -1,0 +1,111 @@
+"""The site-block transpose copy kernel (copy_trans_kernel): the boxes whose source is contiguous
+over [R, a U chain, V1] and whose destination is contiguous over [R, V1] -- bit-exact against the
+oracle, with partial tiles, outer dims, alpha, Add and conversions, and identical to the general
+tile kernel (sbx_tune_set("copy.trans", -1))."""
+import numpy as np
+import pytest
+
+from _common import index_valued, int_valued, oracle_copy
+
+pytestmark = pytest.mark.gpu
+
+
+def _vol(d):
+    n = 1
+    for x in d:
+        n *= x
+    return n
+
+
+def _copy(gpu, alpha, o0, from0, size0, dim0, v0, o1, from1, dim1, v1, add=False):
+    import torch
+    import superbblas_amd as sb
+    t0 = torch.from_numpy(v0).to(gpu)
+    t1 = torch.from_numpy(v1).to(gpu)
+    sb.copy(alpha, [([0] * len(o0), list(dim0))], o0, from0, size0, dim0, [t0],
+            [([0] * len(o1), list(dim1))], o1, from1, dim1, [t1],
+            copyadd=sb.Add if add else sb.Copy)
+    torch.cuda.synchronize()
+    return t1.cpu().numpy(), sb.tune_get("copy.last_pair")
+
+
+def test_trans_lattice_slices(gpu):
+    """configs[1]'s permute shape (xyztsc -> slice n of tnsxyzc) at 8^4: the transpose kernel
+    runs (read-back 4) and every slice is bit-exact."""
+    L, n = 8, 5
+    dim0 = [L, L, L, L, 4, 3]
+    dim1 = [L, n, 4, L, L, L, 3]
+    v0 = index_valued(_vol(dim0), np.complex128)
+    ref = np.zeros(_vol(dim1), np.complex128)
+    out = ref.copy()
+    for k in range(n):
+        oracle_copy(1.0, "xyztsc", [0] * 6, dim0, dim0, v0, "tnsxyzc", [0, k, 0, 0, 0, 0, 0],
+                    dim1, ref)
+        out, kind = _copy(gpu, 1.0, "xyztsc", [0] * 6, dim0, dim0, v0, "tnsxyzc",
+                          [0, k, 0, 0, 0, 0, 0], dim1, out)
+        assert kind == 4
+    assert np.array_equal(out.view(np.uint8), ref.view(np.uint8))
+
+
+# source wvabc (c fastest): R = c, U = (b, a), V1 = v; destinations that keep c then v fastest
+SHAPES = [
+    ("wvabc", [3, 37, 4, 5, 3], "awbvc"),   # 25 + 12 items of v per tile (a partial tile)
+    ("wvabc", [2, 64, 4, 16, 3], "bawvc"),  # U = 64 items (192 elements per v item), QT = 8
+    ("vabc", [100, 2, 3, 1], "bavc"),       # R = 1 after dropping c
+    ("wvab", [5, 300, 2, 3], "wbav"),       # no run (R = 1), U = (b, a)
+    ("wvabc", [2, 9, 16, 16, 2], "awbvc"),  # U = 256 items
+]
+
+
+@pytest.mark.parametrize("o0,dim0,o1", SHAPES)
+def test_trans_shapes_bitexact(gpu, o0, dim0, o1):
+    import superbblas_amd as sb
+    dim1 = [dim0[o0.index(c)] for c in o1]
+    v0 = index_valued(_vol(dim0), np.complex128)
+    v1 = int_valued(_vol(dim1), np.complex128, 3)
+    ref = v1.copy()
+    oracle_copy(1.0, o0, [0] * len(o0), dim0, dim0, v0, o1, [0] * len(o1), dim1, ref)
+    out, kind = _copy(gpu, 1.0, o0, [0] * len(o0), dim0, dim0, v0, o1, [0] * len(o1), dim1,
+                      v1.copy())
+    assert np.array_equal(out.view(np.uint8), ref.view(np.uint8))
+    # the general tile kernel gives the same bytes
+    sb.tune_set("copy.trans", -1)
+    try:
+        out2, kind2 = _copy(gpu, 1.0, o0, [0] * len(o0), dim0, dim0, v0, o1, [0] * len(o1),
+                            dim1, v1.copy())
+    finally:
+        sb.tune_set("copy.trans", 0)
+    assert kind2 != 4
+    assert np.array_equal(out2.view(np.uint8), ref.view(np.uint8))
+    if dim0[-1] > 1 or o0 == "wvab":
+        assert kind == 4, (o0, o1)
+
+
+@pytest.mark.parametrize("add", [False, True])
+@pytest.mark.parametrize("t1", [np.complex128, np.complex64])
+def test_trans_alpha_add_conversion(gpu, add, t1):
+    o0, dim0, o1 = "wvabc", [3, 37, 4, 5, 3], "awbvc"
+    dim1 = [dim0[o0.index(c)] for c in o1]
+    v0 = int_valued(_vol(dim0), np.complex128, 1)
+    v1 = int_valued(_vol(dim1), t1, 2)
+    ref = v1.copy()
+    alpha = 2.0 - 1.0j
+    oracle_copy(alpha, o0, [0] * 5, dim0, dim0, v0, o1, [0] * 5, dim1, ref, add=add)
+    out, kind = _copy(gpu, alpha, o0, [0] * 5, dim0, dim0, v0, o1, [0] * 5, dim1, v1.copy(),
+                      add=add)
+    assert kind == 4
+    assert np.array_equal(out.view(np.uint8), ref.view(np.uint8))
+
+
+def test_trans_subbox_falls_back(gpu):
+    """A sub-box whose source is not one run over [R, U, V1] takes the general kernel."""
+    o0, dim0, o1 = "wvabc", [3, 37, 4, 5, 3], "awbvc"
+    dim1 = [dim0[o0.index(c)] for c in o1]
+    from0, size0 = [0, 2, 0, 1, 0], [3, 30, 4, 4, 3]
+    v0 = index_valued(_vol(dim0), np.complex128)
+    v1 = np.zeros(_vol(dim1), np.complex128)
+    ref = v1.copy()
+    oracle_copy(1.0, o0, from0, size0, dim0, v0, o1, [0] * 5, dim1, ref)
+    out, kind = _copy(gpu, 1.0, o0, from0, size0, dim0, v0, o1, [0] * 5, dim1, v1.copy())
+    assert kind != 4
+    assert np.array_equal(out.view(np.uint8), ref.view(np.uint8))

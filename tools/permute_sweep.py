@@ -64,7 +64,7 @@ def main():
     configs = [dict(), dict(budget=1536), dict(budget=512), dict(nt=-1)]
     if os.environ.get("PERMUTE_CONFIGS"):
         configs = json.loads(os.environ["PERMUTE_CONFIGS"])
-    defaults = {"budget": 0, "run": 0, "nt": 0}
+    defaults = {"budget": 0, "run": 0, "nt": 0, "trans": 0}
     for cfg in configs:
         for k, v in defaults.items():
             sb.tune_set("copy." + k, cfg.get(k, v))
