@@ -401,6 +401,8 @@ struct TransArgs {
     // thread strides of the two phases, as whole steps: 256 = qi*NU*R + ri (loads), 256 =
     // qo*QT*R + ro and ro = qr*R + rr (stores)
     uint32_t qi, ri, qo, ro, qr, rr;
+    uint32_t qi2, ri2, qo2, ro2, qr2, rr2; // the same for 512 (paired phases)
+    int pr, pw;                            // the planner allows paired reads / writes
     long ssv, dsv;            // V1 strides (source NU*R, destination R)
     int nu;                   // U chain dims (source order, fastest first)
     FastDiv usize[MAXD];
@@ -415,59 +417,99 @@ struct TransArgs {
 };
 
 // A1: alpha == 1 (plain data movement, no scaling code); FULL (uniform per workgroup): the tile
-// fills every thread's KMAX elements on both phases (no per-element guards)
-template <typename S, typename D, bool ADD, bool A1, bool FULL>
+// fills every thread's KMAX elements on both phases (no per-element guards); PR / PW (8-byte
+// elements): the loads / stores move two consecutive elements per lane (one 16-byte access; the
+// planner checks that the runs are even and their starts even, the launch that the pointers are
+// 16-byte aligned)
+template <typename S, typename D, bool ADD, bool A1, bool FULL, bool PR, bool PW>
 __device__ __forceinline__ void trans_body(const TransArgs &p, D *tile, const long *du, const S *s0,
                                            D *d0, uint32_t qt, uint32_t E) {
     const uint32_t t = threadIdx.x, NUR = p.NU * p.R, LD = NUR + 1;
-    S r[TRANS_KMAX];
+    constexpr int KR = PR ? TRANS_KMAX / 2 : TRANS_KMAX;
+    constexpr uint32_t ER = PR ? 2 : 1; // elements per lane access
+    S r[KR][ER];
 #pragma unroll
-    for (int k = 0; k < TRANS_KMAX; ++k)
-        if (FULL || t + 256 * k < E) r[k] = s0[t + 256 * k];
+    for (int k = 0; k < KR; ++k) {
+        const uint32_t j = ER * (t + 256 * k);
+        if (FULL || j < E) {
+            if constexpr (PR) {
+                const Pair<S> v = *(const Pair<S> *)(s0 + j);
+                r[k][0] = v.a;
+                r[k][ER - 1] = v.b;
+            } else {
+                r[k][0] = s0[j];
+            }
+        }
+    }
     // element j of the run sits at (item, e) = divmod(j, NU*R), stepped incrementally
-    uint32_t item = p.fNUR.div(t), e = t - item * NUR;
+    uint32_t item = p.fNUR.div(ER * t), e = ER * t - item * NUR;
 #pragma unroll
-    for (int k = 0; k < TRANS_KMAX; ++k) {
-        if (FULL || t + 256 * k < E)
-            tile[item * LD + e] = A1 ? conv<D, S>(r[k]) : xform<D, S>(r[k], p.alpha);
-        item += p.qi;
-        e += p.ri;
+    for (int k = 0; k < KR; ++k) {
+        if (FULL || ER * (t + 256 * k) < E) {
+#pragma unroll
+            for (uint32_t h = 0; h < ER; ++h) {
+                // the pair's second element: e + 1 < NU*R (NU*R even, e even)
+                tile[item * LD + e + h] = A1 ? conv<D, S>(r[k][h]) : xform<D, S>(r[k][h], p.alpha);
+            }
+        }
+        item += PR ? p.qi2 : p.qi;
+        e += PR ? p.ri2 : p.ri;
         if (e >= NUR) {
             e -= NUR;
             ++item;
         }
     }
     __syncthreads();
-    // the destination: for each U item a run of QT*R elements (items v0.. of V1, R each); thread
-    // t writes (u, item, c) of positions t, t + 256, ... of the U-major order
+    // the destination: for each U item a run of QT*R elements (items v0.. of V1, R each) at
+    // d0 + du[u] + x (V1's destination stride is R); thread t writes positions EW*t, EW*(t + 256),
+    // ... of the U-major order
+    constexpr int KW = PW ? TRANS_KMAX / 2 : TRANS_KMAX;
+    constexpr uint32_t EW = PW ? 2 : 1;
     const uint32_t QTR = p.QT * p.R;
-    uint32_t u = p.fQTR.div(t), x = t - u * QTR;
+    uint32_t u = p.fQTR.div(EW * t), x = EW * t - u * QTR;
     uint32_t it = p.fR.div(x), c = x - it * p.R;
 #pragma unroll
-    for (int k = 0; k < TRANS_KMAX; ++k) {
+    for (int k = 0; k < KW; ++k) {
         if (FULL || (u < p.NU && it < qt)) {
-            const D val = tile[it * LD + u * p.R + c];
-            D *q = d0 + du[u] + (long)it * p.dsv + c;
-            if (!ADD && p.nt)
-                store_nt(q, val);
-            else
-                put<ADD, D>(q, val);
+            D *q = d0 + du[u] + x;
+            const D v0 = tile[it * LD + u * p.R + c];
+            if constexpr (PW) {
+                // the pair's second element: position x + 1 of the same U item (QT*R even)
+                const uint32_t it1 = c + 1 == p.R ? it + 1 : it, c1 = c + 1 == p.R ? 0 : c + 1;
+                if (FULL || it1 < qt) {
+                    const Pair<D> v{v0, tile[it1 * LD + u * p.R + c1]};
+                    if (p.nt)
+                        store_nt((Pair<D> *)q, v);
+                    else
+                        *(Pair<D> *)q = v;
+                } else if (p.nt) {
+                    store_nt(q, v0);
+                } else {
+                    *q = v0;
+                }
+            } else if (!ADD && p.nt) {
+                store_nt(q, v0);
+            } else {
+                put<ADD, D>(q, v0);
+            }
         }
-        u += p.qo;
-        it += p.qr;
-        c += p.rr;
+        u += PW ? p.qo2 : p.qo;
+        x += PW ? p.ro2 : p.ro;
+        it += PW ? p.qr2 : p.qr;
+        c += PW ? p.rr2 : p.rr;
         if (c >= p.R) {
             c -= p.R;
             ++it;
         }
-        if (it >= p.QT) {
+        if (x >= QTR) {
+            x -= QTR;
             it -= p.QT;
             ++u;
         }
     }
 }
 
-template <typename S, typename D, bool ADD, bool A1>
+template <typename S, typename D, bool ADD, bool A1, bool PR, bool PW>
 __global__ void __launch_bounds__(256) copy_trans_kernel(const TransArgs p) {
     __shared__ D tile[TRANS_EMAX + 256];
     __shared__ long du[256];
@@ -503,9 +545,9 @@ __global__ void __launch_bounds__(256) copy_trans_kernel(const TransArgs p) {
     const S *s0 = (const S *)p.src + sbase + (long)v0 * p.ssv;
     D *d0 = (D *)p.dstp + dbase + (long)v0 * p.dsv;
     if (E == 256 * TRANS_KMAX && p.NU * p.QT * p.R == 256 * TRANS_KMAX)
-        trans_body<S, D, ADD, A1, true>(p, tile, du, s0, d0, qt, E);
+        trans_body<S, D, ADD, A1, true, PR, PW>(p, tile, du, s0, d0, qt, E);
     else
-        trans_body<S, D, ADD, A1, false>(p, tile, du, s0, d0, qt, E);
+        trans_body<S, D, ADD, A1, false, PR, PW>(p, tile, du, s0, d0, qt, E);
 }
 
 template <typename T> struct DT;
@@ -592,15 +634,43 @@ void run_launch(const CopyLaunch &l, const void *src, void *dst, const Alpha &al
         break;
     }
     case CopyLaunch::TRANS: {
-        g_copy_tune.last_pair = 4;
         TransArgs a = l.tr;
         a.src = src;
         a.dstp = dst;
         a.alpha = alpha;
-        if (alpha.one == 1)
-            hipLaunchKernelGGL((copy_trans_kernel<S, D, ADD, true>), grid, block, 0, stream, a);
-        else
-            hipLaunchKernelGGL((copy_trans_kernel<S, D, ADD, false>), grid, block, 0, stream, a);
+        const bool pr = a.pr && ((size_t)src & 15) == 0, pw = a.pw && ((size_t)dst & 15) == 0;
+        g_copy_tune.last_pair = 4 | (pr ? 1 : 0) | (pw ? 2 : 0);
+        auto go = [&](auto a1, auto pr_, auto pw_) {
+            hipLaunchKernelGGL((copy_trans_kernel<S, D, ADD, decltype(a1)::value, decltype(pr_)::value,
+                                                  decltype(pw_)::value>),
+                               grid, block, 0, stream, a);
+        };
+        using T_ = std::true_type;
+        using F_ = std::false_type;
+        constexpr bool CR = sizeof(S) == 8, CW = sizeof(D) == 8 && !ADD;
+        if (alpha.one == 1) {
+            if constexpr (CR && CW) {
+                if (pr && pw) { go(T_{}, T_{}, T_{}); break; }
+            }
+            if constexpr (CR) {
+                if (pr) { go(T_{}, T_{}, F_{}); break; }
+            }
+            if constexpr (CW) {
+                if (pw) { go(T_{}, F_{}, T_{}); break; }
+            }
+            go(T_{}, F_{}, F_{});
+        } else {
+            if constexpr (CR && CW) {
+                if (pr && pw) { go(F_{}, T_{}, T_{}); break; }
+            }
+            if constexpr (CR) {
+                if (pr) { go(F_{}, T_{}, F_{}); break; }
+            }
+            if constexpr (CW) {
+                if (pw) { go(F_{}, F_{}, T_{}); break; }
+            }
+            go(F_{}, F_{}, F_{});
+        }
         break;
     }
     case CopyLaunch::TILED3: {
@@ -646,7 +716,7 @@ void run_launch(const CopyLaunch &l, const void *src, void *dst, const Alpha &al
 /// a dim V1 of destination stride R whose source stride is R * NU, NU the product of a chain of
 /// dims whose source strides run R, R*u0, ... up to it (the U chain; at most 256 items and at
 /// least two V1 items per tile)
-template <typename D>
+template <typename S, typename D, bool ADD>
 bool prepare_trans(CopyLaunch &l, const Norm &n, int first, long R, long total) {
     const int nd = (int)n.size.size();
     int v1 = -1;
@@ -686,6 +756,12 @@ bool prepare_trans(CopyLaunch &l, const Norm &n, int first, long R, long total) 
     a.ro = (uint32_t)(256 % (QT * R));
     a.qr = a.ro / (uint32_t)R;
     a.rr = a.ro % (uint32_t)R;
+    a.qi2 = (uint32_t)(512 / (NU * R));
+    a.ri2 = (uint32_t)(512 % (NU * R));
+    a.qo2 = (uint32_t)(512 / (QT * R));
+    a.ro2 = (uint32_t)(512 % (QT * R));
+    a.qr2 = a.ro2 / (uint32_t)R;
+    a.rr2 = a.ro2 % (uint32_t)R;
     a.ssv = n.ss[v1];
     a.dsv = n.ds[v1];
     a.nu = (int)U.size();
@@ -706,6 +782,16 @@ bool prepare_trans(CopyLaunch &l, const Norm &n, int first, long R, long total) 
     }
     a.nw = nw;
     a.nt = g_copy_tune.nt > 0 || (g_copy_tune.nt == 0 && total * (long)sizeof(D) >= (8L << 20));
+    // paired 16-byte accesses for 8-byte elements: even runs with even starts on that side
+    bool ws_even = true, wd_even = true, ud_even = true;
+    for (int i = 0; i < nw; ++i) {
+        ws_even = ws_even && a.wsst[i] % 2 == 0;
+        wd_even = wd_even && a.wdst[i] % 2 == 0;
+    }
+    for (int k = 0; k < a.nu; ++k) ud_even = ud_even && a.udst[k] % 2 == 0;
+    // (a 16-byte destination element: single reads measured faster, cf2cd 4.83 -> 5.01 TB/s)
+    a.pr = sizeof(S) == 8 && sizeof(D) == 8 && g_copy_tune.pair >= 0 && (NU * R) % 2 == 0 && ws_even;
+    a.pw = sizeof(D) == 8 && !ADD && g_copy_tune.pair >= 0 && (QT * R) % 2 == 0 && ud_even && wd_even;
     const long blocks = (long)a.ntv * NW;
     if (blocks >= (1L << 31)) return false;
     l.kind = CopyLaunch::TRANS;
@@ -755,7 +841,7 @@ CopyLaunch prepare_pair(bool masked, Norm n, long total) {
         R = n.size[0];
         first = 1;
     }
-    if (g_copy_tune.trans >= 0 && sizeof(S) == 16 && prepare_trans<D>(l, n, first, R, total)) return l;
+    if (g_copy_tune.trans >= 0 && prepare_trans<S, D, ADD>(l, n, first, R, total)) return l;
     // V chain: dims contiguous in the destination from stride R (destination order);
     // U chain: dims contiguous in the source from stride R, not in V.  Both are capped so that a
     // tile holds a few hundred items on each side.

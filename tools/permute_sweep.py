@@ -83,9 +83,22 @@ def main():
                 sb.copy(1.0, p0, "xyztsc", [0] * 6, d0, d0, [af], p1, "tnsxyzc",
                         [0, k, 0, 0, 0, 0, 0], d1, [b])
         t2 = graph_time(run_f)
+        torch.cuda.synchronize()
+        ok_f = bool(torch.equal(b, ref.to(torch.complex64).to(torch.complex128)))
+        bf = torch.zeros(vol(d1), dtype=torch.complex64, device=dev)
+
+        def run_ff():
+            for k in range(n):
+                sb.copy(1.0, p0, "xyztsc", [0] * 6, d0, d0, [af], p1, "tnsxyzc",
+                        [0, k, 0, 0, 0, 0, 0], d1, [bf])
+        t3 = graph_time(run_ff)
+        torch.cuda.synchronize()
+        ok_ff = bool(torch.equal(bf, ref.to(torch.complex64)))
         print(json.dumps({"case": cfg, "GBps": round(by / t / 1e9, 1),
                           "us_per_slice": round(t / n * 1e6, 2), "exact": ok,
-                          "cf2cd_GBps": round(24.0 * vol(d1) / t2 / 1e9, 1)}), flush=True)
+                          "cf2cd_GBps": round(24.0 * vol(d1) / t2 / 1e9, 1), "cf2cd_exact": ok_f,
+                          "cf2cf_GBps": round(16.0 * vol(d1) / t3 / 1e9, 1), "cf2cf_exact": ok_ff}),
+              flush=True)
 
 
     for k, v in defaults.items():
