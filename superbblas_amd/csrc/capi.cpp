@@ -411,6 +411,7 @@ int sbx_tune_set(const char *key, long long value) {
         else if (k == "copy.pair") g_copy_tune.pair = (int)value;
         else if (k == "copy.order") g_copy_tune.order = (int)value;
         else if (k == "copy.trans") g_copy_tune.trans = (int)value;
+        else if (k == "copy.btrans") g_copy_tune.btrans = (int)value;
         else if (k == "gemm.max_bytes") g_gemm_tune.max_bytes = (long)value;
         else if (k == "bsr.variant") g_bsr_tune.variant = (int)value;
         else if (k == "bsr.row_max_cols") g_bsr_tune.row_max_cols = (long)value;
@@ -448,6 +449,7 @@ int sbx_tune_get(const char *key, long long *value) {
         else if (k == "copy.pair") *value = g_copy_tune.pair;
         else if (k == "copy.order") *value = g_copy_tune.order;
         else if (k == "copy.trans") *value = g_copy_tune.trans;
+        else if (k == "copy.btrans") *value = g_copy_tune.btrans;
         else if (k == "copy.last_pair") *value = g_copy_tune.last_pair;
         else if (k == "gemm.max_bytes") *value = g_gemm_tune.max_bytes;
         else if (k == "bsr.variant") *value = g_bsr_tune.variant;

@@ -550,6 +550,176 @@ __global__ void __launch_bounds__(256) copy_trans_kernel(const TransArgs p) {
         trans_body<S, D, ADD, A1, false, PR, PW>(p, tile, du, s0, d0, qt, E);
 }
 
+// Block transpose (round 3): a tile of QT items of a dimension V1 with all NU items of a set U
+// of dims, U = SI + SO = DI + DO where SI (DI) are the dims contiguous in the source (destination)
+// from the run R: the source holds runs of R*|SI| elements (longer when V1 follows SI), the
+// destination runs of R*|DI| elements (longer when V1 follows DI).  Loads walk the source order
+// (run, V1, SO), stores the destination order (run, V1, DO); the LDS tile is [V1 item][U item in
+// source order][R] and a table maps a destination-order U item to it.  Covers the three-way
+// transposes the site-block kernel does not (the chain's tnsxyzc -> pxyztscn: V1 = xyz, SI = c,
+// DI = (n, c, s)).  Every index is stepped incrementally (mixed-radix digits, 256 per step).
+struct BtransArgs {
+    uint32_t R, NU, QT, NV1, ntv;
+    uint32_t RS, NSO, RD, NDI, NDO; // source run R*|SI|, SO items; destination run R*|DI|, DI / DO items
+    long ssv, dsv;                  // V1 strides
+    uint32_t la, lv, lo;            // 256 in the load radix (RS, QT, NSO)
+    uint32_t sr, sd, sv, so;        // 256 in the store radix (R, NDI, QT, NDO)
+    int nso, ndo, nud;
+    FastDiv sosize[MAXD], dosize[MAXD], udsize[MAXD];
+    long sost[MAXD], dost[MAXD];
+    uint32_t ucmul[MAXD];           // U dims in destination order (DI then DO): canonical multipliers
+    int nw;
+    FastDiv wsize[MAXD];
+    long wsst[MAXD], wdst[MAXD];
+    int nt;
+    const void *src;
+    void *dstp;
+    Alpha alpha;
+};
+
+template <typename S, typename D, bool ADD, bool A1>
+__global__ void __launch_bounds__(256) copy_btrans_kernel(const BtransArgs p) {
+    __shared__ D tile[TRANS_EMAX + 256];
+    __shared__ long so_off[256], do_off[256];
+    __shared__ uint16_t ucan[256];
+    uint32_t b = blockIdx.x;
+    const uint32_t tv = b % p.ntv;
+    uint32_t w = b / p.ntv;
+    long sbase = 0, dbase = 0;
+#pragma unroll
+    for (int i = 0; i < MAXD; ++i) {
+        if (i >= p.nw) break;
+        const uint32_t q = p.wsize[i].div(w);
+        const uint32_t c = w - q * p.wsize[i].d;
+        w = q;
+        sbase += (long)c * p.wsst[i];
+        dbase += (long)c * p.wdst[i];
+    }
+    const uint32_t t = threadIdx.x, v0 = tv * p.QT;
+    const uint32_t qt = min(p.QT, p.NV1 - v0);
+    if (t < p.NSO) {
+        uint32_t idx = t;
+        long o = 0;
+#pragma unroll
+        for (int i = 0; i < MAXD; ++i) {
+            if (i >= p.nso) break;
+            const uint32_t q = p.sosize[i].div(idx);
+            o += (long)(idx - q * p.sosize[i].d) * p.sost[i];
+            idx = q;
+        }
+        so_off[t] = o;
+    }
+    if (t < p.NDO) {
+        uint32_t idx = t;
+        long o = 0;
+#pragma unroll
+        for (int i = 0; i < MAXD; ++i) {
+            if (i >= p.ndo) break;
+            const uint32_t q = p.dosize[i].div(idx);
+            o += (long)(idx - q * p.dosize[i].d) * p.dost[i];
+            idx = q;
+        }
+        do_off[t] = o;
+    }
+    if (t < p.NU) {
+        uint32_t idx = t, uc = 0;
+#pragma unroll
+        for (int i = 0; i < MAXD; ++i) {
+            if (i >= p.nud) break;
+            const uint32_t q = p.udsize[i].div(idx);
+            uc += (idx - q * p.udsize[i].d) * p.ucmul[i];
+            idx = q;
+        }
+        ucan[t] = (uint16_t)uc;
+    }
+    __syncthreads();
+    const S *s0 = (const S *)p.src + sbase + (long)v0 * p.ssv;
+    D *d0 = (D *)p.dstp + dbase + (long)v0 * p.dsv;
+    const uint32_t LD = p.NU * p.R + 1, E = p.RS * p.QT * p.NSO;
+    // loads in the source order (a in the run, v, so); every load of a thread in flight at once
+    S r[TRANS_KMAX];
+    {
+        uint32_t a = t, v = 0, o = 0;
+        // t < 256: its digits (a, v, o) by two divisions, then the step carries
+        v = p.RS > t ? 0 : t / p.RS;
+        a = t - v * p.RS;
+        o = v / p.QT;
+        v -= o * p.QT;
+        const uint32_t a0 = a, v0_ = v, o0 = o;
+#pragma unroll
+        for (int k = 0; k < TRANS_KMAX; ++k) {
+            if (t + 256 * k < E && v < qt) r[k] = s0[a + (long)v * p.ssv + so_off[o < p.NSO ? o : 0]];
+            a += p.la;
+            v += p.lv;
+            o += p.lo;
+            if (a >= p.RS) {
+                a -= p.RS;
+                ++v;
+            }
+            if (v >= p.QT) {
+                v -= p.QT;
+                ++o;
+            }
+        }
+        a = a0;
+        v = v0_;
+        o = o0;
+#pragma unroll
+        for (int k = 0; k < TRANS_KMAX; ++k) {
+            if (t + 256 * k < E && v < qt)
+                tile[v * LD + o * p.RS + a] = A1 ? conv<D, S>(r[k]) : xform<D, S>(r[k], p.alpha);
+            a += p.la;
+            v += p.lv;
+            o += p.lo;
+            if (a >= p.RS) {
+                a -= p.RS;
+                ++v;
+            }
+            if (v >= p.QT) {
+                v -= p.QT;
+                ++o;
+            }
+        }
+    }
+    __syncthreads();
+    // stores in the destination order (c in R, di, v, do)
+    {
+        uint32_t x = t / p.R, c = t - x * p.R;
+        uint32_t v = x / p.NDI, di = x - v * p.NDI;
+        uint32_t o = v / p.QT;
+        v -= o * p.QT;
+        const uint32_t ES = p.RD * p.QT * p.NDO;
+#pragma unroll
+        for (int k = 0; k < TRANS_KMAX; ++k) {
+            if (t + 256 * k < ES && v < qt) {
+                const uint32_t uc = ucan[o * p.NDI + di];
+                const D val = tile[v * LD + uc * p.R + c];
+                D *q = d0 + (di * p.R + c) + (long)v * p.dsv + do_off[o];
+                if (!ADD && p.nt)
+                    store_nt(q, val);
+                else
+                    put<ADD, D>(q, val);
+            }
+            c += p.sr;
+            di += p.sd;
+            v += p.sv;
+            o += p.so;
+            if (c >= p.R) {
+                c -= p.R;
+                ++di;
+            }
+            if (di >= p.NDI) {
+                di -= p.NDI;
+                ++v;
+            }
+            if (v >= p.QT) {
+                v -= p.QT;
+                ++o;
+            }
+        }
+    }
+}
+
 template <typename T> struct DT;
 template <> struct DT<float> { static constexpr int v = SBX_FLOAT; };
 template <> struct DT<double> { static constexpr int v = SBX_DOUBLE; };
@@ -596,10 +766,11 @@ Norm normalize(const BoxCopyDesc &d) {
 /// (the launch cache below keys it on the box shape, element types and tuning switches; the
 /// reference caches its permutation index vectors the same way, tensor.h:919-961)
 struct CopyLaunch {
-    enum Kind { MASKED, CONTIG, DIRECT, TILED3, TRANS } kind = DIRECT;
+    enum Kind { MASKED, CONTIG, DIRECT, TILED3, TRANS, BTRANS } kind = DIRECT;
     DirectArgs da{};
     TiledArgs ta{};
     TransArgs tr{};
+    BtransArgs bt{};
     long total = 0, blocks = 0;
     int nt = 0;
     int vr = 0, vw = 0; // tiled: the shape allows paired reads / writes (pointers checked per call)
@@ -673,6 +844,18 @@ void run_launch(const CopyLaunch &l, const void *src, void *dst, const Alpha &al
         }
         break;
     }
+    case CopyLaunch::BTRANS: {
+        g_copy_tune.last_pair = 8;
+        BtransArgs a = l.bt;
+        a.src = src;
+        a.dstp = dst;
+        a.alpha = alpha;
+        if (alpha.one == 1)
+            hipLaunchKernelGGL((copy_btrans_kernel<S, D, ADD, true>), grid, block, 0, stream, a);
+        else
+            hipLaunchKernelGGL((copy_btrans_kernel<S, D, ADD, false>), grid, block, 0, stream, a);
+        break;
+    }
     case CopyLaunch::TILED3: {
         g_copy_tune.last_pair = 0;
         TiledArgs a = l.ta;
@@ -716,6 +899,7 @@ void run_launch(const CopyLaunch &l, const void *src, void *dst, const Alpha &al
 /// a dim V1 of destination stride R whose source stride is R * NU, NU the product of a chain of
 /// dims whose source strides run R, R*u0, ... up to it (the U chain; at most 256 items and at
 /// least two V1 items per tile)
+constexpr long BTRANS_MIN_RUN = 128; // bytes: the shortest run either transpose kernel takes
 template <typename S, typename D, bool ADD>
 bool prepare_trans(CopyLaunch &l, const Norm &n, int first, long R, long total) {
     const int nd = (int)n.size.size();
@@ -742,6 +926,9 @@ bool prepare_trans(CopyLaunch &l, const Norm &n, int first, long R, long total) 
     if (want != n.ss[v1] || (int)U.size() > MAXD) return false;
     TransArgs &a = l.tr;
     const long QT = std::min(n.size[v1], (long)TRANS_EMAX / (NU * R));
+    // destination runs of QT*R elements: at least BTRANS_MIN_RUN bytes (a 3-item V1 against a
+    // 12-item U measured 10x slower than the tile kernel)
+    if (QT * R * (long)sizeof(D) < BTRANS_MIN_RUN) return false;
     a.R = (uint32_t)R;
     a.NU = (uint32_t)NU;
     a.QT = (uint32_t)QT;
@@ -803,6 +990,172 @@ bool prepare_trans(CopyLaunch &l, const Norm &n, int first, long R, long total) 
     return true;
 }
 
+/// The block transpose (copy_btrans_kernel): over every choice of V1, U = the source chain SI
+/// and the destination chain DI from the run R (at most 256 items, the source and destination
+/// runs as long as possible); taken when both runs reach `BTRANS_MIN_RUN` bytes
+template <typename S, typename D, bool ADD>
+bool prepare_btrans(CopyLaunch &l, const Norm &n, int first, long R, long total) {
+    const int nd = (int)n.size.size();
+    struct Plan {
+        int v1 = -1;
+        std::vector<int> si, di;
+        long score = 0;
+    } best;
+    const long cap = std::min(256L, (long)TRANS_EMAX / (2 * R));
+    for (int v1 = first; v1 < nd; ++v1) {
+        if (n.size[v1] < 2) continue;
+        auto chain = [&](bool dst_side) {
+            std::vector<int> c;
+            std::vector<bool> used(nd, false);
+            used[v1] = true;
+            long want = R, prod = 1;
+            while (true) {
+                int f = -1;
+                for (int i = first; i < nd; ++i)
+                    if (!used[i] && (dst_side ? n.ds[i] : n.ss[i]) == want && n.size[i] > 1) f = i;
+                if (f < 0 || prod * n.size[f] > cap) break;
+                c.push_back(f);
+                used[f] = true;
+                prod *= n.size[f];
+                want *= n.size[f];
+            }
+            return c;
+        };
+        std::vector<int> si = chain(false), di = chain(true);
+        auto nu_of = [&]() {
+            std::vector<bool> in(nd, false);
+            long nu = 1;
+            for (int i : si) in[i] = true;
+            for (int i : di) in[i] = true;
+            for (int i = 0; i < nd; ++i)
+                if (in[i]) nu *= n.size[i];
+            return nu;
+        };
+        // too many U items: drop the outermost dim of the longer chain (it becomes an outer dim)
+        while (nu_of() > cap && !(si.empty() && di.empty())) {
+            long ps = 1, pd = 1;
+            for (int i : si) ps *= n.size[i];
+            for (int i : di) pd *= n.size[i];
+            if (ps >= pd) si.pop_back();
+            else di.pop_back();
+        }
+        const long NU = nu_of();
+        if (NU < 2 || NU > cap) continue;
+        long rs = R, rd = R;
+        for (int i : si) rs *= n.size[i];
+        for (int i : di) rd *= n.size[i];
+        const long QT = std::min(n.size[v1], std::min(256L, (long)TRANS_EMAX / (NU * R)));
+        const long srun = n.ss[v1] == rs ? rs * QT : rs, drun = n.ds[v1] == rd ? rd * QT : rd;
+        const long score = std::min(srun * (long)sizeof(S), drun * (long)sizeof(D));
+        if (score > best.score) {
+            best.v1 = v1;
+            best.si = si;
+            best.di = di;
+            best.score = score;
+        }
+    }
+    if (best.v1 < 0 || best.score < BTRANS_MIN_RUN) return false;
+    const int v1 = best.v1;
+    std::vector<bool> inU(nd, false), inSI(nd, false), inDI(nd, false);
+    for (int i : best.si) inU[i] = inSI[i] = true;
+    for (int i : best.di) inU[i] = inDI[i] = true;
+    // SO / DO: the rest of U, by source / destination stride
+    std::vector<int> so, dO;
+    for (int i = first; i < nd; ++i) {
+        if (inU[i] && !inSI[i]) so.push_back(i);
+        if (inU[i] && !inDI[i]) dO.push_back(i);
+    }
+    std::sort(so.begin(), so.end(), [&](int a, int b) { return n.ss[a] < n.ss[b]; });
+    std::sort(dO.begin(), dO.end(), [&](int a, int b) { return n.ds[a] < n.ds[b]; });
+    if ((int)so.size() > MAXD || (int)dO.size() > MAXD || (int)(best.di.size() + dO.size()) > MAXD)
+        return false;
+    BtransArgs &a = l.bt;
+    long NU = 1, NSI = 1, NSO = 1, NDI = 1, NDO = 1;
+    for (int i = 0; i < nd; ++i)
+        if (inU[i]) NU *= n.size[i];
+    for (int i : best.si) NSI *= n.size[i];
+    for (int i : so) NSO *= n.size[i];
+    for (int i : best.di) NDI *= n.size[i];
+    for (int i : dO) NDO *= n.size[i];
+    const long QT = std::min(n.size[v1], std::min(256L, (long)TRANS_EMAX / (NU * R)));
+    a.R = (uint32_t)R;
+    a.NU = (uint32_t)NU;
+    a.QT = (uint32_t)QT;
+    a.NV1 = (uint32_t)n.size[v1];
+    a.ntv = (uint32_t)((n.size[v1] + QT - 1) / QT);
+    a.RS = (uint32_t)(R * NSI);
+    a.NSO = (uint32_t)NSO;
+    a.RD = (uint32_t)(R * NDI);
+    a.NDI = (uint32_t)NDI;
+    a.NDO = (uint32_t)NDO;
+    a.ssv = n.ss[v1];
+    a.dsv = n.ds[v1];
+    {
+        const long q1 = 256 / (R * NSI);
+        a.la = (uint32_t)(256 % (R * NSI));
+        a.lv = (uint32_t)(q1 % QT);
+        a.lo = (uint32_t)(q1 / QT);
+        const long p1 = 256 / R, p2 = p1 / NDI;
+        a.sr = (uint32_t)(256 % R);
+        a.sd = (uint32_t)(p1 % NDI);
+        a.sv = (uint32_t)(p2 % QT);
+        a.so = (uint32_t)(p2 / QT);
+    }
+    a.nso = (int)so.size();
+    for (std::size_t k = 0; k < so.size(); ++k) {
+        a.sosize[k] = FastDiv((uint32_t)n.size[so[k]]);
+        a.sost[k] = n.ss[so[k]];
+    }
+    a.ndo = (int)dO.size();
+    for (std::size_t k = 0; k < dO.size(); ++k) {
+        a.dosize[k] = FastDiv((uint32_t)n.size[dO[k]]);
+        a.dost[k] = n.ds[dO[k]];
+    }
+    // canonical U index = SI digits (fastest first) then SO digits; its multiplier per dim
+    std::vector<long> cmul(nd, 0);
+    {
+        long m = 1;
+        for (int i : best.si) {
+            cmul[i] = m;
+            m *= n.size[i];
+        }
+        for (int i : so) {
+            cmul[i] = m;
+            m *= n.size[i];
+        }
+    }
+    std::vector<int> ud = best.di;
+    ud.insert(ud.end(), dO.begin(), dO.end());
+    a.nud = (int)ud.size();
+    for (std::size_t k = 0; k < ud.size(); ++k) {
+        a.udsize[k] = FastDiv((uint32_t)n.size[ud[k]]);
+        a.ucmul[k] = (uint32_t)cmul[ud[k]];
+    }
+    long NW = 1;
+    int nw = 0;
+    for (int i = first; i < nd; ++i) {
+        if (inU[i] || i == v1) continue;
+        if (nw == MAXD) return false;
+        a.wsize[nw] = FastDiv((uint32_t)n.size[i]);
+        a.wsst[nw] = n.ss[i];
+        a.wdst[nw] = n.ds[i];
+        NW *= n.size[i];
+        ++nw;
+    }
+    a.nw = nw;
+    a.nt = g_copy_tune.nt > 0 || (g_copy_tune.nt == 0 && total * (long)sizeof(D) >= (8L << 20));
+    const long blocks = (long)a.ntv * NW;
+    if (blocks >= (1L << 31)) return false;
+    l.kind = CopyLaunch::BTRANS;
+    l.blocks = blocks;
+    static const bool debug = getenv("SBX_COPY_DEBUG") != nullptr;
+    if (debug)
+        std::fprintf(stderr, "copy_btrans: R=%ld NU=%ld (SI %ld SO %ld DI %ld DO %ld) V1=%ld QT=%ld nw=%d "
+                     "blocks=%ld runs %ld B\n", R, NU, NSI, NSO, NDI, NDO, n.size[v1], QT, nw, blocks,
+                     best.score);
+    return true;
+}
+
 template <typename S, typename D, bool ADD>
 CopyLaunch prepare_pair(bool masked, Norm n, long total) {
     CopyLaunch l;
@@ -842,6 +1195,7 @@ CopyLaunch prepare_pair(bool masked, Norm n, long total) {
         first = 1;
     }
     if (g_copy_tune.trans >= 0 && prepare_trans<S, D, ADD>(l, n, first, R, total)) return l;
+    if (g_copy_tune.btrans >= 0 && prepare_btrans<S, D, ADD>(l, n, first, R, total)) return l;
     // V chain: dims contiguous in the destination from stride R (destination order);
     // U chain: dims contiguous in the source from stride R, not in V.  Both are capped so that a
     // tile holds a few hundred items on each side.
@@ -1140,7 +1494,8 @@ void launch_box_copy(const BoxCopyDesc &d, int device) {
     key.push_back(g_copy_tune.budget);
     key.push_back(g_copy_tune.run);
     key.push_back(16L * g_copy_tune.nt + 256L * g_copy_tune.pair +
-                  4096L * g_copy_tune.order + 65536L * g_copy_tune.trans);
+                  4096L * g_copy_tune.order + 65536L * g_copy_tune.trans +
+                  1048576L * g_copy_tune.btrans);
     for (std::size_t i = 0; i < nd; ++i) {
         key.push_back(d.size[i]);
         key.push_back(d.src_stride[i]);

@@ -220,9 +220,11 @@ struct CopyTune {
     int pair = 0;  ///< tiled kernel, 8-byte elements: two elements per lane access where the runs allow (-1 = never)
     int order = 0; ///< ... with pairs, the source chain first when the destination chain would take the
                    ///< source's contiguous dim (-1 = always the destination chain first)
-    int trans = 0; ///< 16-byte source elements: the site-block transpose kernel for the boxes it takes (-1 = never)
+    int trans = 0; ///< the site-block transpose kernel for the boxes it takes (-1 = never)
+    int btrans = 0; ///< the block transpose kernel for the boxes it takes (-1 = never)
     std::atomic<int> last_pair{0}; ///< read-back ("copy.last_pair"): the last tiled launch's paired phases (1 reads,
-                                   ///< 2 writes), 4 = the site-block transpose kernel
+                                   ///< 2 writes), 4 = the site-block transpose kernel (| 1, 2 for
+                                   ///< its paired phases), 8 = the block transpose kernel
 };
 extern CopyTune g_copy_tune;
 struct GemmTune {

@@ -279,19 +279,32 @@ def test_paired_8byte_transposes(gpu, t0, t1):
         forms.add(sb.tune_get("copy.last_pair"))
         assert np.array_equal(out.view(np.uint8), ref.view(np.uint8)), (o0, o1, n, shift, add)
 
+    # the library's defaults (the transpose kernels take most of these shapes): bit-exact
     for (o0, o1, dims), n, shift, add in itertools.product(cases, (6, 5), (0, 1), (False, True)):
         if add and np.dtype(t1).kind == "u":
             continue
         run(o0, o1, dims, n, shift, add)
-    # the single-access form on the same shapes (odd tile rows are rounded to even ones, so the
-    # defaults above may pair every case)
-    prev = sb.tune_get("copy.pair")
-    sb.tune_set("copy.pair", -1)
+    # the tile kernel itself (transpose kernels off): paired and single-access forms
+    forms.clear()
+    sb.tune_set("copy.trans", -1)
+    sb.tune_set("copy.btrans", -1)
     try:
-        for (o0, o1, dims), n in itertools.product(cases, (6, 5)):
-            run(o0, o1, dims, n, 0, False)
+        for (o0, o1, dims), n, shift, add in itertools.product(cases, (6, 5), (0, 1), (False, True)):
+            if add and np.dtype(t1).kind == "u":
+                continue
+            run(o0, o1, dims, n, shift, add)
+        # the single-access form on the same shapes (odd tile rows are rounded to even ones, so
+        # the defaults above may pair every case)
+        prev = sb.tune_get("copy.pair")
+        sb.tune_set("copy.pair", -1)
+        try:
+            for (o0, o1, dims), n in itertools.product(cases, (6, 5)):
+                run(o0, o1, dims, n, 0, False)
+        finally:
+            sb.tune_set("copy.pair", prev)
     finally:
-        sb.tune_set("copy.pair", prev)
+        sb.tune_set("copy.trans", 0)
+        sb.tune_set("copy.btrans", 0)
     # paired reads ran for 8-byte sources, paired writes for 8-byte destinations, and the
     # single-access fallback ran too
     assert 0 in forms, forms

@@ -78,7 +78,7 @@ def test_trans_shapes_bitexact(gpu, o0, dim0, o1):
     assert not kind2 & 4
     assert np.array_equal(out2.view(np.uint8), ref.view(np.uint8))
     if dim0[-1] > 1 or o0 == "wvab":
-        assert kind & 4, (o0, o1)
+        assert kind & 12, (o0, o1)  # a transpose kernel (U = 256 items: the block transpose)
 
 
 @pytest.mark.parametrize("add", [False, True])
@@ -129,7 +129,8 @@ def test_trans_types_and_pairs(gpu, t0, t1, o0, dim0, o1):
     ref = v1.copy()
     oracle_copy(1.0, o0, [0] * len(o0), dim0, dim0, v0, o1, [0] * len(o1), dim1, ref)
     out, kind = _copy(gpu, 1.0, o0, [0] * len(o0), dim0, dim0, v0, o1, [0] * len(o1), dim1, v1)
-    assert kind & 4
+    if np.dtype(t1).itemsize >= 8:  # (4-byte destinations: runs of 24 elements are too short)
+        assert kind & 4
     assert np.array_equal(out.view(np.uint8), ref.view(np.uint8))
     if np.dtype(t0).itemsize == 8 and np.dtype(t1).itemsize == 8 and dim0[-1] % 2 == 0:
         assert kind & 3 == 3  # even runs of 8-byte elements: paired reads and writes

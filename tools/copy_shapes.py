@@ -42,8 +42,10 @@ def case(name, o0, d0, o1, d1, from1, dtype, reps=10):
     t = ms / calls / 1e3
     es = torch.empty(0, dtype=dtype).element_size()
     ok = bool(torch.equal(b.view(-1), ref_copy(a.to(dtype_out), o0, d0, o1, d1, from1).view(-1)))
+    eo = torch.empty(0, dtype=dtype_out).element_size()
     print(json.dumps({"case": name, "us": round(t * 1e6, 1),
-                      "GBps": round(2 * es * vol(d0) / t / 1e9, 1), "exact": ok}))
+                      "GBps": round((es + eo) * vol(d0) / t / 1e9, 1), "exact": ok,
+                      "kind": sb.tune_get("copy.last_pair")}))
 
 
 def ref_copy(a, o0, d0, o1, d1, from1):
@@ -75,9 +77,22 @@ def sweep(spec):
     sb.tune_set("copy.run", 0)
 
 
+def kinds():
+    """COPY_KINDS=1: the transpose kernels on / off on every case (copy.trans, copy.btrans)"""
+    for trans, btrans in ((0, 0), (0, -1), (-1, -1)):
+        sb.tune_set("copy.trans", trans)
+        sb.tune_set("copy.btrans", btrans)
+        print(json.dumps({"copy.trans": trans, "copy.btrans": btrans}))
+        shapes()
+    sb.tune_set("copy.trans", 0)
+    sb.tune_set("copy.btrans", 0)
+
+
 def main():
     if os.environ.get("COPY_SWEEP"):
         return sweep(os.environ["COPY_SWEEP"])
+    if os.environ.get("COPY_KINDS"):
+        return kinds()
     combos = ((0, 0, 0), (0, 0, -1), (0, 0, -2), (0, -1, 0))
     if os.environ.get("COPY_QUICK"):
         combos = combos[:3]
