@@ -994,34 +994,58 @@ bool prepare_trans(CopyLaunch &l, const Norm &n, int first, long R, long total) 
 /// and the destination chain DI from the run R (at most 256 items, the source and destination
 /// runs as long as possible); taken when both runs reach `BTRANS_MIN_RUN` bytes
 template <typename S, typename D, bool ADD>
-bool prepare_btrans(CopyLaunch &l, const Norm &n, int first, long R, long total) {
-    const int nd = (int)n.size.size();
+bool prepare_btrans(CopyLaunch &l, const Norm &n0, int first, long R, long total) {
     struct Plan {
+        Norm n;
         int v1 = -1;
         std::vector<int> si, di;
         long score = 0;
     } best;
-    const long cap = std::min(256L, (long)TRANS_EMAX / (2 * R));
-    for (int v1 = first; v1 < nd; ++v1) {
-        if (n.size[v1] < 2) continue;
-        auto chain = [&](bool dst_side) {
-            std::vector<int> c;
-            std::vector<bool> used(nd, false);
-            used[v1] = true;
+    const long cap0 = std::min(256L, (long)TRANS_EMAX / (2 * R));
+    const int nd0 = (int)n0.size.size();
+    // chain caps: whole dims first, then (16-byte elements) inner factors of a dim (split) so
+    // that a tile holds more V1 items -- longer runs on V1's side (the whole-tensor complex<double>
+    // permute 335 -> 310 us); for smaller elements the split plans measured slower than the tile
+    // kernel's paired accesses (profiles/r03_copy_btrans.txt)
+    const long cap_min = sizeof(D) >= 16 ? 8 : cap0;
+    for (long cap = cap0; cap >= cap_min; cap /= 2)
+    for (int v1 = first; v1 < nd0; ++v1) {
+        if (n0.size[v1] < 2) continue;
+        Norm n = n0;
+        auto chain = [&](bool dst_side, std::vector<int> &c, std::vector<bool> &used) {
             long want = R, prod = 1;
-            while (true) {
+            while ((int)n.size.size() <= MAXD) {
                 int f = -1;
-                for (int i = first; i < nd; ++i)
+                for (int i = first; i < (int)n.size.size(); ++i)
                     if (!used[i] && (dst_side ? n.ds[i] : n.ss[i]) == want && n.size[i] > 1) f = i;
-                if (f < 0 || prod * n.size[f] > cap) break;
+                if (f < 0) break;
+                if (prod * n.size[f] > cap) {
+                    if (sizeof(D) < 16) break; // (no split plans for smaller elements, above)
+                    long d = 1; // the largest inner factor that fits
+                    for (long q = 2; q <= cap / prod; ++q)
+                        if (n.size[f] % q == 0) d = q;
+                    if (d < 2) break;
+                    n.size.push_back(n.size[f] / d);
+                    n.ss.push_back(n.ss[f] * d);
+                    n.ds.push_back(n.ds[f] * d);
+                    n.size[f] = d;
+                    used.push_back(false);
+                }
                 c.push_back(f);
                 used[f] = true;
                 prod *= n.size[f];
                 want *= n.size[f];
+                if (prod >= cap) break;
             }
-            return c;
         };
-        std::vector<int> si = chain(false), di = chain(true);
+        std::vector<int> si, di;
+        std::vector<bool> us(n.size.size(), false), ud(n.size.size(), false);
+        us[v1] = ud[v1] = true;
+        chain(false, si, us);
+        ud.resize(n.size.size(), false);
+        chain(true, di, ud);
+        const int nd = (int)n.size.size();
+        if (nd > MAXD) continue;
         auto nu_of = [&]() {
             std::vector<bool> in(nd, false);
             long nu = 1;
@@ -1032,7 +1056,7 @@ bool prepare_btrans(CopyLaunch &l, const Norm &n, int first, long R, long total)
             return nu;
         };
         // too many U items: drop the outermost dim of the longer chain (it becomes an outer dim)
-        while (nu_of() > cap && !(si.empty() && di.empty())) {
+        while (nu_of() > cap0 && !(si.empty() && di.empty())) {
             long ps = 1, pd = 1;
             for (int i : si) ps *= n.size[i];
             for (int i : di) pd *= n.size[i];
@@ -1040,7 +1064,7 @@ bool prepare_btrans(CopyLaunch &l, const Norm &n, int first, long R, long total)
             else di.pop_back();
         }
         const long NU = nu_of();
-        if (NU < 2 || NU > cap) continue;
+        if (NU < 2 || NU > cap0) continue;
         long rs = R, rd = R;
         for (int i : si) rs *= n.size[i];
         for (int i : di) rd *= n.size[i];
@@ -1048,6 +1072,7 @@ bool prepare_btrans(CopyLaunch &l, const Norm &n, int first, long R, long total)
         const long srun = n.ss[v1] == rs ? rs * QT : rs, drun = n.ds[v1] == rd ? rd * QT : rd;
         const long score = std::min(srun * (long)sizeof(S), drun * (long)sizeof(D));
         if (score > best.score) {
+            best.n = n;
             best.v1 = v1;
             best.si = si;
             best.di = di;
@@ -1055,6 +1080,8 @@ bool prepare_btrans(CopyLaunch &l, const Norm &n, int first, long R, long total)
         }
     }
     if (best.v1 < 0 || best.score < BTRANS_MIN_RUN) return false;
+    const Norm &n = best.n;
+    const int nd = (int)n.size.size();
     const int v1 = best.v1;
     std::vector<bool> inU(nd, false), inSI(nd, false), inDI(nd, false);
     for (int i : best.si) inU[i] = inSI[i] = true;
