@@ -112,7 +112,7 @@ int sbx_timings_report(char *buf, int len);
    the measured winners; read a key with sbx_tune_get before changing it to
    restore it afterwards.  Keys: "gemm.m3", "gemm.splits", "gemm.max_bytes", "gemm.t48",
    "gemm.share_ab", "copy.nt", "copy.budget", "copy.run", "copy.max_elems", "copy.pair",
-   "copy.order", "copy.trans", "bsr.variant", "bsr.row_max_cols", "bsr.split_max_cols",
+   "copy.order", "copy.trans", "copy.btrans", "bsr.variant", "bsr.row_max_cols", "bsr.split_max_cols",
    "bsr.split_cw", "bsr.split_jb", "bsr.split_ilv", "bsr.kron_mfma", "bsr.kron_mfma_min_cols",
    "bsr.kron_pack", "dist.reduce", "alloc.max_cached"; read-backs "bsr.last_kernel",
    "copy.last_pair", "dist.reduce_calls", "alloc.cross_stream_frees".  Unknown keys fail with an
