@@ -564,6 +564,8 @@ struct BtransArgs {
     long ssv, dsv;                  // V1 strides
     uint32_t la, lv, lo;            // 256 in the load radix (RS, QT, NSO)
     uint32_t sr, sd, sv, so;        // 256 in the store radix (R, NDI, QT, NDO)
+    uint32_t sr2, sd2, sv2, so2;    // 512 in the store radix (paired stores)
+    int pw;                         // the planner allows paired stores (8-byte elements)
     int nso, ndo, nud;
     FastDiv sosize[MAXD], dosize[MAXD], udsize[MAXD];
     long sost[MAXD], dost[MAXD];
@@ -577,7 +579,7 @@ struct BtransArgs {
     Alpha alpha;
 };
 
-template <typename S, typename D, bool ADD, bool A1>
+template <typename S, typename D, bool ADD, bool A1, bool PW>
 __global__ void __launch_bounds__(256) copy_btrans_kernel(const BtransArgs p) {
     __shared__ D tile[TRANS_EMAX + 256];
     __shared__ long so_off[256], do_off[256];
@@ -682,6 +684,50 @@ __global__ void __launch_bounds__(256) copy_btrans_kernel(const BtransArgs p) {
         }
     }
     __syncthreads();
+    // PW (8-byte elements, even destination runs, 16-byte aligned): two consecutive positions per
+    // lane, one 16-byte store (the second element is in the same run: runs and starts are even)
+    if constexpr (PW) {
+        const uint32_t t2 = 2 * t;
+        uint32_t x = t2 / p.R, c = t2 - x * p.R;
+        uint32_t v = x / p.NDI, di = x - v * p.NDI;
+        uint32_t o = v / p.QT;
+        v -= o * p.QT;
+        const uint32_t ES = p.RD * p.QT * p.NDO;
+#pragma unroll
+        for (int k = 0; k < TRANS_KMAX / 2; ++k) {
+            if (t2 + 512 * k < ES && v < qt) {
+                uint32_t c1 = c + 1, di1 = di;
+                if (c1 == p.R) {
+                    c1 = 0;
+                    ++di1;
+                }
+                const Pair<D> val{tile[v * LD + ucan[o * p.NDI + di] * p.R + c],
+                                  tile[v * LD + ucan[o * p.NDI + di1] * p.R + c1]};
+                Pair<D> *q = (Pair<D> *)(d0 + (di * p.R + c) + (long)v * p.dsv + do_off[o]);
+                if (p.nt)
+                    store_nt(q, val);
+                else
+                    *q = val;
+            }
+            c += p.sr2;
+            di += p.sd2;
+            v += p.sv2;
+            o += p.so2;
+            if (c >= p.R) {
+                c -= p.R;
+                ++di;
+            }
+            if (di >= p.NDI) {
+                di -= p.NDI;
+                ++v;
+            }
+            if (v >= p.QT) {
+                v -= p.QT;
+                ++o;
+            }
+        }
+        return;
+    }
     // stores in the destination order (c in R, di, v, do)
     {
         uint32_t x = t / p.R, c = t - x * p.R;
@@ -845,15 +891,30 @@ void run_launch(const CopyLaunch &l, const void *src, void *dst, const Alpha &al
         break;
     }
     case CopyLaunch::BTRANS: {
-        g_copy_tune.last_pair = 8;
         BtransArgs a = l.bt;
         a.src = src;
         a.dstp = dst;
         a.alpha = alpha;
-        if (alpha.one == 1)
-            hipLaunchKernelGGL((copy_btrans_kernel<S, D, ADD, true>), grid, block, 0, stream, a);
-        else
-            hipLaunchKernelGGL((copy_btrans_kernel<S, D, ADD, false>), grid, block, 0, stream, a);
+        constexpr bool CW = sizeof(D) == 8 && !ADD;
+        const bool pw = CW && a.pw && ((size_t)dst & 15) == 0;
+        g_copy_tune.last_pair = 8 | (pw ? 2 : 0);
+        if (alpha.one == 1) {
+            if constexpr (CW) {
+                if (pw) {
+                    hipLaunchKernelGGL((copy_btrans_kernel<S, D, ADD, true, CW>), grid, block, 0, stream, a);
+                    break;
+                }
+            }
+            hipLaunchKernelGGL((copy_btrans_kernel<S, D, ADD, true, false>), grid, block, 0, stream, a);
+        } else {
+            if constexpr (CW) {
+                if (pw) {
+                    hipLaunchKernelGGL((copy_btrans_kernel<S, D, ADD, false, CW>), grid, block, 0, stream, a);
+                    break;
+                }
+            }
+            hipLaunchKernelGGL((copy_btrans_kernel<S, D, ADD, false, false>), grid, block, 0, stream, a);
+        }
         break;
     }
     case CopyLaunch::TILED3: {
@@ -1127,6 +1188,11 @@ bool prepare_btrans(CopyLaunch &l, const Norm &n0, int first, long R, long total
         a.sd = (uint32_t)(p1 % NDI);
         a.sv = (uint32_t)(p2 % QT);
         a.so = (uint32_t)(p2 / QT);
+        const long e1 = 512 / R, e2 = e1 / NDI;
+        a.sr2 = (uint32_t)(512 % R);
+        a.sd2 = (uint32_t)(e1 % NDI);
+        a.sv2 = (uint32_t)(e2 % QT);
+        a.so2 = (uint32_t)(e2 / QT);
     }
     a.nso = (int)so.size();
     for (std::size_t k = 0; k < so.size(); ++k) {
@@ -1171,6 +1237,14 @@ bool prepare_btrans(CopyLaunch &l, const Norm &n0, int first, long R, long total
     }
     a.nw = nw;
     a.nt = g_copy_tune.nt > 0 || (g_copy_tune.nt == 0 && total * (long)sizeof(D) >= (8L << 20));
+    // paired stores: even destination runs whose starts are even (V1, DO and outer strides)
+    bool d_even = a.RD % 2 == 0 && a.dsv % 2 == 0;
+    for (int k = 0; k < a.ndo; ++k) d_even = d_even && a.dost[k] % 2 == 0;
+    for (int k = 0; k < nw; ++k) d_even = d_even && a.wdst[k] % 2 == 0;
+    a.pw = sizeof(D) == 8 && !ADD && g_copy_tune.pair >= 0 && d_even;
+    // 8-byte destinations without paired stores: the tile kernel's paired accesses measured
+    // faster (the chain's operand reorder pXYZTSCn -> TSnpXYZC, odd runs: 121 vs 116 us)
+    if (sizeof(D) == 8 && !a.pw && g_copy_tune.pair >= 0 && g_copy_tune.btrans == 0) return false;
     const long blocks = (long)a.ntv * NW;
     if (blocks >= (1L << 31)) return false;
     l.kind = CopyLaunch::BTRANS;

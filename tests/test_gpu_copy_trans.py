@@ -153,3 +153,38 @@ def test_trans_misaligned_pointers(gpu):
     torch.cuda.synchronize()
     assert sb.tune_get("copy.last_pair") == 4
     assert np.array_equal(d_buf[1:].cpu().numpy().view(np.uint8), ref.view(np.uint8))
+
+
+@pytest.mark.parametrize("t0,t1", [(np.complex64, np.complex64), (np.complex128, np.complex128),
+                                   (np.complex64, np.complex128), (np.float64, np.float64)])
+@pytest.mark.parametrize("n", [12, 5])
+@pytest.mark.parametrize("add", [False, True])
+def test_btrans_chain_redistribution(gpu, t0, t1, n, add):
+    """The block transpose (read-back 8; | 2 for paired stores) on the chain's three-way
+    redistribution tnsxyzc -> pxyztscn (n <-> c <-> xyz) at a reduced lattice, with an odd rhs
+    count, Add and conversions; identical to the tile kernel (copy.btrans -1)."""
+    import superbblas_amd as sb
+    L, T = 8, 6
+    o0, dim0 = "tnsxyzc", [T, n, 4, L, L, L, 3]
+    o1, dim1 = "pxyztscn", [1, L, L, L, T, 4, 3, n]
+    v0 = int_valued(_vol(dim0), t0, 1)
+    v1 = int_valued(_vol(dim1), t1, 2)
+    ref = v1.copy()
+    oracle_copy(1.0, o0, [0] * 7, dim0, dim0, v0, o1, [0] * 8, dim1, ref, add=add)
+    out, kind = _copy(gpu, 1.0, o0, [0] * 7, dim0, dim0, v0, o1, [0] * 8, dim1, v1.copy(), add=add)
+    assert np.array_equal(out.view(np.uint8), ref.view(np.uint8))
+    if np.dtype(t1).itemsize == 8:
+        # 8-byte destinations take the block transpose only with paired stores (no Add)
+        assert bool(kind & 8) == (not add), kind
+        if not add:
+            assert kind & 2, kind
+    else:
+        assert kind & 8, kind
+    sb.tune_set("copy.btrans", -1)
+    try:
+        out2, kind2 = _copy(gpu, 1.0, o0, [0] * 7, dim0, dim0, v0, o1, [0] * 8, dim1, v1.copy(),
+                            add=add)
+    finally:
+        sb.tune_set("copy.btrans", 0)
+    assert not kind2 & 8
+    assert np.array_equal(out2.view(np.uint8), ref.view(np.uint8))
