@@ -394,6 +394,8 @@ __global__ void __launch_bounds__(256) copy_tiled3_kernel(const TiledArgs p) {
 // slice loop goes 5.2 -> 3.5 us per slice (tools/permute_micro.hip).
 constexpr int TRANS_EMAX = 1536; // elements per tile
 constexpr int TRANS_KMAX = TRANS_EMAX / 256;
+/// block transpose tile (elements): 24 KB of 16-byte elements, 3072 smaller ones (12 per thread)
+template <typename D> constexpr int btrans_emax() { return sizeof(D) >= 16 ? 1536 : 3072; }
 struct TransArgs {
     uint32_t R, NU, QT, NV1;  // run, U chain items, V1 items per tile, V1 extent
     uint32_t ntv;             // tiles along V1
@@ -581,7 +583,8 @@ struct BtransArgs {
 
 template <typename S, typename D, bool ADD, bool A1, bool PW>
 __global__ void __launch_bounds__(256) copy_btrans_kernel(const BtransArgs p) {
-    __shared__ D tile[TRANS_EMAX + 256];
+    constexpr int BE = btrans_emax<D>(), BK = BE / 256;
+    __shared__ D tile[BE + 256];
     __shared__ long so_off[256], do_off[256];
     __shared__ uint16_t ucan[256];
     uint32_t b = blockIdx.x;
@@ -639,7 +642,7 @@ __global__ void __launch_bounds__(256) copy_btrans_kernel(const BtransArgs p) {
     D *d0 = (D *)p.dstp + dbase + (long)v0 * p.dsv;
     const uint32_t LD = p.NU * p.R + 1, E = p.RS * p.QT * p.NSO;
     // loads in the source order (a in the run, v, so); every load of a thread in flight at once
-    S r[TRANS_KMAX];
+    S r[BK];
     {
         uint32_t a = t, v = 0, o = 0;
         // t < 256: its digits (a, v, o) by two divisions, then the step carries
@@ -649,7 +652,7 @@ __global__ void __launch_bounds__(256) copy_btrans_kernel(const BtransArgs p) {
         v -= o * p.QT;
         const uint32_t a0 = a, v0_ = v, o0 = o;
 #pragma unroll
-        for (int k = 0; k < TRANS_KMAX; ++k) {
+        for (int k = 0; k < BK; ++k) {
             if (t + 256 * k < E && v < qt) r[k] = s0[a + (long)v * p.ssv + so_off[o < p.NSO ? o : 0]];
             a += p.la;
             v += p.lv;
@@ -667,7 +670,7 @@ __global__ void __launch_bounds__(256) copy_btrans_kernel(const BtransArgs p) {
         v = v0_;
         o = o0;
 #pragma unroll
-        for (int k = 0; k < TRANS_KMAX; ++k) {
+        for (int k = 0; k < BK; ++k) {
             if (t + 256 * k < E && v < qt)
                 tile[v * LD + o * p.RS + a] = A1 ? conv<D, S>(r[k]) : xform<D, S>(r[k], p.alpha);
             a += p.la;
@@ -694,7 +697,7 @@ __global__ void __launch_bounds__(256) copy_btrans_kernel(const BtransArgs p) {
         v -= o * p.QT;
         const uint32_t ES = p.RD * p.QT * p.NDO;
 #pragma unroll
-        for (int k = 0; k < TRANS_KMAX / 2; ++k) {
+        for (int k = 0; k < BK / 2; ++k) {
             if (t2 + 512 * k < ES && v < qt) {
                 uint32_t c1 = c + 1, di1 = di;
                 if (c1 == p.R) {
@@ -736,7 +739,7 @@ __global__ void __launch_bounds__(256) copy_btrans_kernel(const BtransArgs p) {
         v -= o * p.QT;
         const uint32_t ES = p.RD * p.QT * p.NDO;
 #pragma unroll
-        for (int k = 0; k < TRANS_KMAX; ++k) {
+        for (int k = 0; k < BK; ++k) {
             if (t + 256 * k < ES && v < qt) {
                 const uint32_t uc = ucan[o * p.NDI + di];
                 const D val = tile[v * LD + uc * p.R + c];
@@ -1062,7 +1065,20 @@ bool prepare_btrans(CopyLaunch &l, const Norm &n0, int first, long R, long total
         std::vector<int> si, di;
         long score = 0;
     } best;
-    const long cap0 = std::min(256L, (long)TRANS_EMAX / (2 * R));
+    constexpr long EMAX = btrans_emax<D>();
+    const long cap0 = std::min(256L, EMAX / (2 * R));
+    // V1 items per tile: as many as fit, rounded so that runs continuing over V1 (source first)
+    // are whole 128-B lines (the chain redistribution's 240-B source runs read 1.47x their bytes)
+    auto qt_of = [&](long nv1, long NU, long rs, long ssv, long rd, long dsv) {
+        long QT = std::min(nv1, std::min(256L, EMAX / (NU * R)));
+        auto round_to = [&](long run_bytes) {
+            const long qa = 128 / std::gcd(run_bytes, 128L);
+            if (QT >= qa && QT < nv1) QT = QT / qa * qa;
+        };
+        if (ssv == rs) round_to(rs * (long)sizeof(S));
+        else if (dsv == rd) round_to(rd * (long)sizeof(D));
+        return QT;
+    };
     const int nd0 = (int)n0.size.size();
     // chain caps: whole dims first, then (16-byte elements) inner factors of a dim (split) so
     // that a tile holds more V1 items -- longer runs on V1's side (the whole-tensor complex<double>
@@ -1129,7 +1145,7 @@ bool prepare_btrans(CopyLaunch &l, const Norm &n0, int first, long R, long total
         long rs = R, rd = R;
         for (int i : si) rs *= n.size[i];
         for (int i : di) rd *= n.size[i];
-        const long QT = std::min(n.size[v1], std::min(256L, (long)TRANS_EMAX / (NU * R)));
+        const long QT = qt_of(n.size[v1], NU, rs, n.ss[v1], rd, n.ds[v1]);
         const long srun = n.ss[v1] == rs ? rs * QT : rs, drun = n.ds[v1] == rd ? rd * QT : rd;
         const long score = std::min(srun * (long)sizeof(S), drun * (long)sizeof(D));
         if (score > best.score) {
@@ -1165,7 +1181,7 @@ bool prepare_btrans(CopyLaunch &l, const Norm &n0, int first, long R, long total
     for (int i : so) NSO *= n.size[i];
     for (int i : best.di) NDI *= n.size[i];
     for (int i : dO) NDO *= n.size[i];
-    const long QT = std::min(n.size[v1], std::min(256L, (long)TRANS_EMAX / (NU * R)));
+    const long QT = qt_of(n.size[v1], NU, R * NSI, n.ss[v1], R * NDI, n.ds[v1]);
     a.R = (uint32_t)R;
     a.NU = (uint32_t)NU;
     a.QT = (uint32_t)QT;
