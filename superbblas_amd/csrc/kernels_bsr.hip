@@ -1152,7 +1152,8 @@ void launch_ell(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_t s) 
             a.ncols <= g_bsr_tune.split_max_cols && launch_ell9_split<E>(a, yrow, xrow, s))
             return;
     }
-    if (nnz == 9 && g_bsr_tune.variant != 1) {
+    // (the row-chunk kernel takes at most 2 x 256 rhs columns per workgroup row)
+    if (nnz == 9 && g_bsr_tune.variant != 1 && a.ncols <= 512) {
         const long lds = a.ncols >= 8 ? 12288 : 24576;
         // 16-byte elements: values by LDS-DMA, a row's lanes on consecutive columns (n = 12:
         // 42 -> 39 us, n = 24: 67 -> 61, n = 64: 182 -> 172; profiles/r02_bsr_sweep.txt; 64- and

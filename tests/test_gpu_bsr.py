@@ -40,9 +40,10 @@ def lattice_operator(L, spin, color, dtype=np.complex128):
     return dim, ii, jj, vals.astype(dtype), nb
 
 
-@pytest.mark.parametrize("spin,color,ncols", [(1, 3, 1), (1, 3, 5), (4, 3, 2)])
+@pytest.mark.parametrize("spin,color,ncols", [(1, 3, 1), (1, 3, 5), (4, 3, 2), (1, 3, 600)])
 @pytest.mark.parametrize("y_layout", ["row", "col"])
 def test_bsr_lattice(gpu, spin, color, ncols, y_layout):
+    """(600 rhs columns: past the row-chunk kernel's 512, the generic ELL kernel)"""
     import torch
     import superbblas_amd as sb
     L = 4
