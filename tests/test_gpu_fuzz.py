@@ -226,3 +226,61 @@ def test_fuzz_oversize_paths(gpu, seed):
     finally:
         sb.tune_set("copy.max_elems", 0)
         sb.tune_set("gemm.max_bytes", 0)
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_fuzz_bsr_wide(gpu, seed):
+    """bsr_krylov across rhs column counts 1-1100 (log-uniform) and every element type, so each
+    kernel form's column limits are crossed (the 3x3 row / split / row-chunk kernels, the 12x12
+    MFMA kernels, the generic ELL and CSR kernels); 9-point or ragged stencils, integer-valued
+    data, exact against the oracle's builtin loop."""
+    import torch
+    import superbblas_amd as sb
+    from _common import NP, T_CDOUBLE, T_CFLOAT, T_DOUBLE, T_FLOAT, oracle_bsr
+    rng = np.random.default_rng(7000 + seed)
+    t = [T_CDOUBLE, T_CFLOAT, T_DOUBLE, T_FLOAT][seed % 4]
+    dt = NP[t]
+    L = [int(rng.integers(1, 4)) for _ in range(4)]
+    spin, color = [(1, 3), (4, 3), (1, 1), (2, 3)][int(rng.integers(0, 4))]
+    b = spin * color
+    V = _vol(L)
+    dim = L + [spin, color]
+    sites = np.array(np.unravel_index(np.arange(V), L)).T
+    dirs = [(None, 0)] + [(d, s) for d in range(4) for s in (-1, 1)]
+    ragged = rng.random() < 0.25
+    jj, ii = [], []
+    for st in sites:
+        k = int(rng.integers(0, 10)) if ragged else 9
+        for d, sg in dirs[:k]:
+            c = st.copy()
+            if d is not None:
+                c[d] = (c[d] + sg) % L[d]
+            jj.append(list(c) + [0, 0])
+        ii.append(k)
+    ii = np.array(ii, np.int32)
+    jj = np.array(jj, np.int32).reshape(-1, 6) if jj else np.zeros((0, 6), np.int32)
+    nnz = int(ii.sum())
+    vals = int_valued(nnz * b * b, dt, seed)
+    ncols = int(np.exp(rng.uniform(0, np.log(1100))))
+    x = int_valued(V * b * ncols, dt, seed + 1)
+    xrow, yrow = bool(rng.random() < 0.75), bool(rng.random() < 0.75)
+    ref = np.zeros(V * b * ncols, dt)
+    oracle_bsr(t, dim, 0, V, b, b, ii, jj.ravel(), vals, False, x, ncols if xrow else V * b, xrow,
+               ref, ncols if yrow else V * b, yrow, ncols, 1.0)
+    full = [([0] * 6, dim)]
+    blk = [1, 1, 1, 1, spin, color]
+    op = sb.create_bsr(full, dim, full, dim, blk, blk, False, [torch.from_numpy(ii).to(gpu)],
+                       [torch.from_numpy(jj.ravel().copy()).to(gpu)],
+                       [torch.from_numpy(vals).to(gpu)])
+    ox = "pXYZTSCn" if xrow else "pnXYZTSC"
+    dx = [1] + L + [spin, color, ncols] if xrow else [1, ncols] + L + [spin, color]
+    oy = "pxyztscn" if yrow else "pnxyztsc"
+    dy = [1] + L + [spin, color, ncols] if yrow else [1, ncols] + L + [spin, color]
+    ty = torch.zeros(V * b * ncols, dtype=torch.from_numpy(ref[:1]).dtype, device=gpu)
+    sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", [([0] * 8, dx)], ox, [0] * 8, dx, dx,
+                  [torch.from_numpy(x).to(gpu)], 0.0, [([0] * 8, dy)], oy, [0] * 8, dy, dy, "p",
+                  [ty])
+    torch.cuda.synchronize()
+    op.destroy()
+    assert np.array_equal(ty.cpu().numpy(), ref), (t, L, spin, color, ragged, ncols, xrow, yrow,
+                                                   sb.tune_get("bsr.last_kernel"))
