@@ -832,6 +832,7 @@ void run_launch(const CopyLaunch &l, const void *src, void *dst, const Alpha &al
                 const float *smask, const float *dmask, hipStream_t stream) {
     KernelTimer timer("copy", stream);
     const dim3 grid((unsigned)l.blocks), block(256);
+    g_copy_tune.last_pair = 0;
     switch (l.kind) {
     case CopyLaunch::MASKED: {
         DirectArgs a = l.da;
@@ -989,7 +990,9 @@ bool prepare_trans(CopyLaunch &l, const Norm &n, int first, long R, long total) 
     }
     if (want != n.ss[v1] || (int)U.size() > MAXD) return false;
     TransArgs &a = l.tr;
-    const long QT = std::min(n.size[v1], (long)TRANS_EMAX / (NU * R));
+    // (at most 256 items: the tile's padding, one element per item, must fit its 256 spare slots)
+    const long QT = std::min({n.size[v1], 256L, (long)TRANS_EMAX / (NU * R)});
+    if (QT * (NU * R + 1) > TRANS_EMAX + 256) throw Error("copy: internal transpose tile sizing error");
     // destination runs of QT*R elements: at least BTRANS_MIN_RUN bytes (a 3-item V1 against a
     // 12-item U measured 10x slower than the tile kernel)
     if (QT * R * (long)sizeof(D) < BTRANS_MIN_RUN) return false;
@@ -1182,6 +1185,7 @@ bool prepare_btrans(CopyLaunch &l, const Norm &n0, int first, long R, long total
     for (int i : best.di) NDI *= n.size[i];
     for (int i : dO) NDO *= n.size[i];
     const long QT = qt_of(n.size[v1], NU, R * NSI, n.ss[v1], R * NDI, n.ds[v1]);
+    if (QT > 256 || QT * (NU * R + 1) > EMAX + 256) throw Error("copy: internal block transpose tile sizing error");
     a.R = (uint32_t)R;
     a.NU = (uint32_t)NU;
     a.QT = (uint32_t)QT;

@@ -222,9 +222,10 @@ struct CopyTune {
                    ///< source's contiguous dim (-1 = always the destination chain first)
     int trans = 0; ///< the site-block transpose kernel for the boxes it takes (-1 = never)
     int btrans = 0; ///< the block transpose kernel for the boxes it takes (-1 = never)
-    std::atomic<int> last_pair{0}; ///< read-back ("copy.last_pair"): the last tiled launch's paired phases (1 reads,
-                                   ///< 2 writes), 4 = the site-block transpose kernel (| 1, 2 for
-                                   ///< its paired phases), 8 = the block transpose kernel
+    std::atomic<int> last_pair{0}; ///< read-back ("copy.last_pair"): the last box-copy launch -- the tile
+                                   ///< kernel's paired phases (1 reads, 2 writes), 4 = the site-block
+                                   ///< transpose kernel (| 1, 2 for its paired phases), 8 = the block
+                                   ///< transpose kernel (| 2), 0 any other kernel
 };
 extern CopyTune g_copy_tune;
 struct GemmTune {

@@ -188,3 +188,19 @@ def test_btrans_chain_redistribution(gpu, t0, t1, n, add):
         sb.tune_set("copy.btrans", 0)
     assert not kind2 & 8
     assert np.array_equal(out2.view(np.uint8), ref.view(np.uint8))
+
+
+@pytest.mark.parametrize("t", [np.float32, np.complex64, np.complex128])
+@pytest.mark.parametrize("add", [False, True])
+def test_trans_many_items_small_chain(gpu, t, add):
+    """A short U chain (NU * R = 4) against a long V1 (1584 items): the tile takes at most 256 V1
+    items, so its one element of padding per item stays inside the tile (found by the copy fuzz:
+    384-item tiles wrote past it into the destination-offset table)."""
+    o0, dim0, o1 = "bad", [48, 33, 4], "dba"
+    dim1 = [dim0[o0.index(c)] for c in o1]
+    v0 = index_valued(_vol(dim0), t) if np.dtype(t).kind == "c" else np.arange(_vol(dim0)).astype(t)
+    v1 = int_valued(_vol(dim1), t, 3)
+    ref = v1.copy()
+    oracle_copy(1.0, o0, [0] * 3, dim0, dim0, v0, o1, [0] * 3, dim1, ref, add=add)
+    out, kind = _copy(gpu, 1.0, o0, [0] * 3, dim0, dim0, v0, o1, [0] * 3, dim1, v1.copy(), add=add)
+    assert np.array_equal(out.view(np.uint8), ref.view(np.uint8))

@@ -284,3 +284,60 @@ def test_fuzz_bsr_wide(gpu, seed):
     op.destroy()
     assert np.array_equal(ty.cpu().numpy(), ref), (t, L, spin, color, ragged, ncols, xrow, yrow,
                                                    sb.tune_get("bsr.last_kernel"))
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_fuzz_copy_transpose(gpu, seed):
+    """Larger permutations (3-6 labels, extents up to 48, up to ~1M elements, mostly whole boxes)
+    so the transpose kernels' planners take part (site-block transpose, block transpose, the tile
+    kernel and their paired 8-byte forms); every type pair, Copy / Add, alpha; bit-exact against
+    the oracle, and identical with both transpose kernels switched off."""
+    import torch
+    import superbblas_amd as sb
+    rng = np.random.default_rng(6000 + seed)
+    nd = int(rng.integers(3, 7))
+    labels = "".join(rng.permutation(list(_LETTERS))[:nd])
+    while True:
+        ext = {c: int(rng.choice([1, 2, 3, 4, 5, 8, 12, 16, 24, 33, 48])) for c in labels}
+        if 2000 <= _vol(ext.values()) <= 1 << 20:
+            break
+    o0 = labels
+    o1 = "".join(rng.permutation(list(labels)))
+    d0 = [ext[c] for c in o0]
+    d1 = [ext[c] for c in o1]
+    if rng.random() < 0.8:
+        f0, s0 = [0] * nd, list(d0)
+    else:
+        f0, s0 = _box(rng, d0)
+    f1 = [0] * nd if rng.random() < 0.8 else [int(rng.integers(0, d)) for d in d1]
+    t0, t1 = [(np.complex128, np.complex128), (np.complex64, np.complex64),
+              (np.complex64, np.complex128), (np.complex128, np.complex64),
+              (np.float64, np.float64), (np.float32, np.float32), (np.float64, np.complex128),
+              (np.int32, np.int32)][seed % 8]
+    add = bool(rng.random() < 0.3) and np.dtype(t1).kind != "i"
+    alpha = 1.0 if np.dtype(t0).kind == "i" else [1.0, 1.0, -0.5][int(rng.integers(0, 3))]
+    v0 = int_valued(_vol(d0), t0, seed) if np.dtype(t0).kind != "i" else \
+        np.arange(_vol(d0), dtype=t0)
+    v1 = int_valued(_vol(d1), t1, seed + 1) if np.dtype(t1).kind != "i" else \
+        -np.arange(_vol(d1), dtype=t1)
+    ref = v1.copy()
+    oracle_copy(alpha, o0, f0, s0, d0, v0, o1, f1, d1, ref, add=add)
+    outs, kinds = [], []
+    for off in (0, -1):
+        sb.tune_set("copy.trans", off)
+        sb.tune_set("copy.btrans", off)
+        try:
+            t_in = torch.from_numpy(v0).to(gpu)
+            t_out = torch.from_numpy(v1.copy()).to(gpu)
+            sb.copy(alpha, [([0] * nd, d0)], o0, f0, s0, d0, [t_in], [([0] * nd, d1)], o1, f1, d1,
+                    [t_out], copyadd=sb.Add if add else sb.Copy)
+            torch.cuda.synchronize()
+            kinds.append(sb.tune_get("copy.last_pair"))
+        finally:
+            sb.tune_set("copy.trans", 0)
+            sb.tune_set("copy.btrans", 0)
+        outs.append(t_out.cpu().numpy())
+    case = (o0, o1, d0, f0, s0, f1, t0, t1, add, alpha, kinds)
+    assert np.array_equal(outs[0].view(np.uint8), ref.view(np.uint8)), case
+    assert np.array_equal(outs[1].view(np.uint8), ref.view(np.uint8)), case
+    assert not kinds[1] & 12, case
