@@ -341,3 +341,53 @@ def test_fuzz_copy_transpose(gpu, seed):
     assert np.array_equal(outs[0].view(np.uint8), ref.view(np.uint8)), case
     assert np.array_equal(outs[1].view(np.uint8), ref.view(np.uint8)), case
     assert not kinds[1] & 12, case
+
+
+@pytest.mark.parametrize("seed", range(96))
+def test_fuzz_contraction_large(gpu, seed):
+    """Contractions large enough for the matrix-core GEMM forms (LDS-DMA tiles, 48x48 tiles,
+    split-K, the shared-operand image, stride forms): T / A / B / C groups of 0-2 labels with
+    extents up to 96 and operands up to ~1M elements, whole boxes, random label orders,
+    conjugation, alpha / beta, every type; against the oracle within the type's bar."""
+    import torch
+    import superbblas_amd as sb
+    rng = np.random.default_rng(8000 + seed)
+    dtype, tol = [(np.complex128, 1e-10), (np.complex64, 2e-5), (np.float64, 1e-12),
+                  (np.float32, 2e-5)][seed % 4]
+    while True:
+        counts = [int(rng.integers(0, 3)) for _ in range(4)]
+        counts[1] = max(counts[1], 1)
+        if counts[2] + counts[3] == 0:
+            counts[2] = 1
+        letters = list(rng.permutation(list(_LETTERS)))
+        T = "".join(letters[:counts[0]])
+        A = "".join(letters[counts[0]:sum(counts[:2])])
+        B = "".join(letters[sum(counts[:2]):sum(counts[:3])])
+        C = "".join(letters[sum(counts[:3]):sum(counts)])
+        ext = {c: int(rng.choice([1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64, 96])) for c in
+               T + A + B + C}
+        vt, va, vb, vc = (_vol([ext[c] for c in g]) for g in (T, A, B, C))
+        if max(vt * va * vb, vt * va * vc, vt * vb * vc) <= 1 << 20 and vt * va * vb * vc <= 4 << 20 \
+                and vt * va * vb * vc >= 1 << 14:
+            break
+    o0 = "".join(rng.permutation(list(T + A + B)))
+    o1 = "".join(rng.permutation(list(T + A + C)))
+    o_r = "".join(rng.permutation(list(T + B + C)))
+    d0, d1, dr = ([ext[c] for c in o] for o in (o0, o1, o_r))
+    conj0, conj1 = bool(rng.integers(0, 2)), bool(rng.integers(0, 2))
+    cplx = np.dtype(dtype).kind == "c"
+    alpha = complex(rng.uniform(-2, 2), rng.uniform(-2, 2)) if cplx else float(rng.uniform(-2, 2))
+    beta = [0.0, 1.0, 0.5][int(rng.integers(0, 3))]
+    v0 = random_valued(_vol(d0), dtype, 3 * seed + 1)
+    v1 = random_valued(_vol(d1), dtype, 3 * seed + 2)
+    vr = random_valued(_vol(dr), dtype, 3 * seed + 3)
+    ref = vr.copy()
+    z = lambda d: [0] * len(d)  # noqa: E731
+    oracle_contraction(alpha, o0, z(d0), d0, d0, conj0, v0, o1, z(d1), d1, d1, conj1, v1, beta,
+                       o_r, z(dr), dr, dr, ref)
+    t0, t1, tr = (torch.from_numpy(v.copy()).to(gpu) for v in (v0, v1, vr))
+    sb.contraction(alpha, [(z(d0), d0)], z(d0), d0, d0, o0, conj0, [t0], [(z(d1), d1)], z(d1), d1,
+                   d1, o1, conj1, [t1], beta, [(z(dr), dr)], z(dr), dr, dr, o_r, [tr])
+    torch.cuda.synchronize()
+    err = rel_err(tr.cpu().numpy(), ref)
+    assert err < tol, (o0, o1, o_r, d0, d1, dr, conj0, conj1, alpha, beta, err)
