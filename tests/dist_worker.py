@@ -600,15 +600,24 @@ def _nonempty(ts, dev):
     return [t if t.numel() else torch.zeros(1, dtype=t.dtype, device=dev) for t in ts]
 
 
-def case_fuzz(sb, comm, rank, n, dev, ncases=12):
+def case_fuzz(sb, comm, rank, n, dev, ncases=12, big=False):
+    """big: extents to 16 (operands to ~64K elements), so the pieces exchanged take the
+    transpose / tile kernels and the contractions the matrix-core GEMM forms"""
     letters = "abcdefgh"
+
+    def extent(rng):
+        return int(rng.choice([1, 2, 3, 4, 6, 8, 12, 16])) if big else int(rng.integers(1, 6))
+
     for seed in range(ncases):
-        rng = np.random.default_rng(777 + seed)
+        rng = np.random.default_rng((4242 if big else 777) + seed)
         # copy
         nd = int(rng.integers(1, 6))
         o0 = "".join(rng.permutation(list(letters))[:nd])
         o1 = "".join(rng.permutation(list(o0)))
-        ext = {c: int(rng.integers(1, 6)) for c in o0}
+        while True:
+            ext = {c: extent(rng) for c in o0}
+            if vol(ext.values()) <= 1 << 16:
+                break
         d0, d1 = [ext[c] for c in o0], [ext[c] for c in o1]
         f0 = [int(rng.integers(0, d)) for d in d0]
         s0 = [int(rng.integers(1, d + 1)) for d in d0]
@@ -635,10 +644,15 @@ def case_fuzz(sb, comm, rank, n, dev, ncases=12):
             cnt[2] = 1  # every tensor has a label (a partition needs a dimension)
         if cnt[0] + cnt[1] + cnt[3] == 0:
             cnt[3] = 1
+        if cnt[0] + cnt[2] + cnt[3] == 0:
+            cnt[2] = 1
         ls = list(rng.permutation(list(letters)))
         T, A = "".join(ls[:cnt[0]]), "".join(ls[cnt[0]:sum(cnt[:2])])
         B, C = "".join(ls[sum(cnt[:2]):sum(cnt[:3])]), "".join(ls[sum(cnt[:3]):sum(cnt)])
-        ext = {c: int(rng.integers(1, 5)) for c in T + A + B + C}
+        while True:
+            ext = {c: (extent(rng) if big else int(rng.integers(1, 5))) for c in T + A + B + C}
+            if max(vol([ext[c] for c in g]) for g in (T + A + B, T + A + C, T + B + C)) <= 1 << 16:
+                break
         o0 = "".join(rng.permutation(list(T + A + B)))
         o1 = "".join(rng.permutation(list(T + A + C)))
         o_r = "".join(rng.permutation(list(T + B + C)))
@@ -691,7 +705,7 @@ def main():
         comm = sb.Comm.from_torch_distributed(dev_idx)
     else:
         comm = sb.Comm.host_staged(dev_idx)
-    cases = os.environ.get("SBX_TEST_CASES", "copy,contr,bsr,kron,dense,storage,fuzz,golden,split,reduce").split(",")
+    cases = os.environ.get("SBX_TEST_CASES", "copy,contr,bsr,kron,dense,storage,fuzz,fuzzl,golden,split,reduce").split(",")
     if "copy" in cases:
         case_copy(sb, comm, rank, n, dev)
     if "contr" in cases:
@@ -706,6 +720,8 @@ def main():
         case_storage(sb, comm, rank, n, dev)
     if "fuzz" in cases:
         case_fuzz(sb, comm, rank, n, dev)
+    if "fuzzl" in cases:
+        case_fuzz(sb, comm, rank, n, dev, ncases=16, big=True)
     if "golden" in cases:
         case_golden(sb, comm, rank, n, dev)
     if "reduce" in cases:
