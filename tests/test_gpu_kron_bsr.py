@@ -211,3 +211,48 @@ def test_kron_mfma_kernel(gpu, ncols, bif, sparse):
     assert outs[0][0] == (6 if ncols in (8, 12) else 5) and outs[1][0] == 5 and outs[2][0] not in (5, 6)
     for form, out in outs:
         assert np.array_equal(out, ref), form
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_kron_fuzz(gpu, seed):
+    """Random Kronecker operators: lattice 1-4, spin 1 / 2 / 4, color 1-3, rhs columns 1-300
+    (log-uniform), every type, either block order, sparse or dense spin matrices; so every Kron
+    kernel form (MFMA, packed MFMA, LDS, generic) meets ragged column counts.  Exact."""
+    import torch
+    import superbblas_amd as sb
+    rng = np.random.default_rng(3100 + seed)
+    dtype = [np.complex128, np.complex64, np.float64, np.float32][seed % 4]
+    cplx = np.dtype(dtype).kind == "c"
+    L = int(rng.integers(1, 5))
+    spin = int(rng.choice([1, 2, 4]))
+    color = int(rng.choice([1, 2, 3, 3]))
+    if seed % 3 == 0:
+        spin, color = 4, 3  # the specialised kernels
+    ncols = int(np.exp(rng.uniform(0, np.log(300))))
+    bif = bool(rng.integers(0, 2))
+    ii, jj, vals, kron = kron_lattice(L, spin, color, sparse_kron=bool(rng.integers(0, 2)))
+    if not cplx:
+        vals, kron = vals.real.copy(), kron.real.copy()
+    V = L ** 4
+    g = np.arange(V * color * ncols * spin)
+    x = ((g % 7 - 3) + (1j * (g % 5 - 2) if cplx else 0)).astype(np.complex128)
+    ref = reference(L, spin, color, ncols, vals.astype(np.complex128),
+                    kron.astype(np.complex128), jj, x, 1.0, 0.0, np.zeros_like(x), 1, bif=bif)
+    dim = [L, L, L, L, spin, color]
+    full = [([0] * 6, dim)]
+    blk, kr = [1, 1, 1, 1, 1, color], [1, 1, 1, 1, spin, 1]
+    op = sb.create_kron_bsr(full, dim, full, dim, blk, blk, kr, kr, bif,
+                            [torch.from_numpy(ii).to(gpu)], [torch.from_numpy(jj).to(gpu)],
+                            [torch.from_numpy(vals.astype(dtype)).to(gpu)],
+                            [torch.from_numpy(kron.astype(dtype)).to(gpu)])
+    dimx = [1, L, L, L, L, color, ncols, spin]
+    tx = torch.from_numpy((x if cplx else x.real).astype(dtype)).to(gpu)
+    ty = torch.zeros(V * color * ncols * spin, dtype=tx.dtype, device=gpu)
+    sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", [([0] * 8, dimx)], "pXYZTCnS", [0] * 8, dimx,
+                  dimx, [tx], 0.0, [([0] * 8, dimx)], "pxyztcns", [0] * 8, dimx, dimx, "p", [ty])
+    torch.cuda.synchronize()
+    kind = sb.tune_get("bsr.last_kernel")
+    op.destroy()
+    out = ty.cpu().numpy().astype(np.complex128)
+    assert np.array_equal(out, ref if cplx else ref.real.astype(np.complex128)), \
+        (dtype, L, spin, color, ncols, bif, kind)
