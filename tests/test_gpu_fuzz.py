@@ -391,3 +391,61 @@ def test_fuzz_contraction_large(gpu, seed):
     torch.cuda.synchronize()
     err = rel_err(tr.cpu().numpy(), ref)
     assert err < tol, (o0, o1, o_r, d0, d1, dr, conj0, conj1, alpha, beta, err)
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_fuzz_bsr_image_side(gpu, seed):
+    """y = alpha A^H x + beta y (x with the image labels; the conjugate-transposed operator built on
+    first use) across lattice shapes, block shapes, ragged stencils, block order, 1-600 rhs columns
+    and every type; integer-valued data, exact against the oracle's adjoint loop."""
+    import torch
+    import superbblas_amd as sb
+    from _common import NP, T_CDOUBLE, T_CFLOAT, T_DOUBLE, T_FLOAT, oracle_bsr_adjoint
+    rng = np.random.default_rng(7500 + seed)
+    t = [T_CDOUBLE, T_CFLOAT, T_DOUBLE, T_FLOAT][seed % 4]
+    dt = NP[t]
+    L = [int(rng.integers(1, 4)) for _ in range(4)]
+    spin, color = [(1, 3), (4, 3), (1, 1), (2, 3)][int(rng.integers(0, 4))]
+    b = spin * color
+    V = _vol(L)
+    dim = L + [spin, color]
+    sites = np.array(np.unravel_index(np.arange(V), L)).T
+    dirs = [(None, 0)] + [(d, s) for d in range(4) for s in (-1, 1)]
+    ragged = rng.random() < 0.3
+    jj, ii = [], []
+    for st in sites:
+        k = int(rng.integers(0, 10)) if ragged else 9
+        for d, sg in dirs[:k]:
+            c = st.copy()
+            if d is not None:
+                c[d] = (c[d] + sg) % L[d]
+            jj.append(list(c) + [0, 0])
+        ii.append(k)
+    ii = np.array(ii, np.int32)
+    jj = np.array(jj, np.int32).reshape(-1, 6) if jj else np.zeros((0, 6), np.int32)
+    nnz = int(ii.sum())
+    bif = bool(rng.integers(0, 2))
+    vals = int_valued(nnz * b * b, dt, seed)
+    ncols = int(np.exp(rng.uniform(0, np.log(600))))
+    n = V * b * ncols
+    x = int_valued(n, dt, seed + 1)
+    y0 = int_valued(n, dt, seed + 2)
+    beta = [0.0, 1.0][int(rng.integers(0, 2))]
+    ax = np.zeros(n, dt)
+    oracle_bsr_adjoint(t, dim, 0, V, b, b, ii, jj.ravel(), vals, bif, x, ncols, True, ax, ncols,
+                       True, V * b, ncols, 1.0)
+    ref = ax + beta * y0
+    full = [([0] * 6, dim)]
+    blk = [1, 1, 1, 1, spin, color]
+    op = sb.create_bsr(full, dim, full, dim, blk, blk, bif, [torch.from_numpy(ii).to(gpu)],
+                       [torch.from_numpy(jj.ravel().copy()).to(gpu)],
+                       [torch.from_numpy(vals).to(gpu)])
+    dx = [1] + L + [spin, color, ncols]
+    tx = torch.from_numpy(x).to(gpu)
+    ty = torch.from_numpy(y0.copy()).to(gpu)
+    sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", [([0] * 8, dx)], "pxyztscn", [0] * 8, dx, dx, [tx],
+                  beta, [([0] * 8, dx)], "pXYZTSCn", [0] * 8, dx, dx, None, [ty])
+    torch.cuda.synchronize()
+    op.destroy()
+    assert np.array_equal(ty.cpu().numpy(), ref.astype(dt)), (t, L, spin, color, ragged, bif,
+                                                            ncols, beta)
