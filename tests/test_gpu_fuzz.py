@@ -449,3 +449,65 @@ def test_fuzz_bsr_image_side(gpu, seed):
     op.destroy()
     assert np.array_equal(ty.cpu().numpy(), ref.astype(dt)), (t, L, spin, color, ragged, bif,
                                                             ncols, beta)
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_fuzz_copy_masked(gpu, seed):
+    """Masked copies (sbx_copy_masked; the reference's masked local_copy, tensor.h:1019-1027):
+    one logical mask over the labels, given to both sides in each side's layout and split with
+    each side's components, random permutations, sub-boxes from the origin, Copy / Add, types;
+    bit-exact against the oracle's masked copy."""
+    import torch
+    import superbblas_amd as sb
+    from _common import oracle_copy as oc
+    rng = np.random.default_rng(5600 + seed)
+    nd = int(rng.integers(1, 6))
+    labels = "".join(rng.permutation(list(_LETTERS))[:nd])
+    while True:
+        ext = {c: int(rng.choice([1, 2, 3, 5, 8, 12, 17, 32])) for c in labels}
+        if _vol(ext.values()) <= 1 << 18:
+            break
+    o0 = labels
+    o1 = "".join(rng.permutation(list(labels)))
+    d0 = [ext[c] for c in o0]
+    d1 = [ext[c] for c in o1]
+    s0 = [int(rng.integers(1, d + 1)) if rng.random() < 0.4 else d for d in d0]
+    t0, t1 = [(np.complex128, np.complex128), (np.complex64, np.complex128), (np.float64, np.float64),
+              (np.float32, np.complex64)][seed % 4]
+    add = bool(rng.integers(0, 2))
+    v0 = int_valued(_vol(d0), t0, seed)
+    v1 = int_valued(_vol(d1), t1, seed + 1)
+    # the logical mask: a function of the label coordinates, laid out for each side
+    salt = {c: int(rng.integers(1, 7)) for c in labels}
+    grid0 = np.indices(d0).reshape(nd, -1)
+    m0 = (sum(salt[c] * grid0[i] for i, c in enumerate(o0)) % 3 != 0).astype(np.float32)
+    grid1 = np.indices(d1).reshape(nd, -1)
+    m1 = (sum(salt[c] * grid1[j] for j, c in enumerate(o1)) % 3 != 0).astype(np.float32)
+    ref = v1.copy()
+    oc(1.0, o0, [0] * nd, s0, d0, v0, o1, [0] * nd, d1, ref, add=add, mask0=m0, mask1=m1)
+
+    def pieces(v, labels_, dims, p):
+        full = v.reshape(dims)
+        out = []
+        for frm, size in p:
+            sl = tuple(slice(f, f + s) for f, s in zip(frm, size))
+            out.append(torch.from_numpy(np.ascontiguousarray(full[sl]).ravel()).to(gpu))
+        return out
+
+    def part(labels_, dims):
+        cand = [i for i, d in enumerate(dims) if d >= 2]
+        if not cand or rng.random() < 0.5:
+            return [([0] * len(dims), list(dims))]
+        i = int(rng.choice(cand))
+        procs = [1] * len(dims)
+        procs[i] = 2
+        return sb.basic_partitioning(labels_, dims, procs, labels_[i], 2, 1)
+
+    p0, p1 = part(o0, d0), part(o1, d1)
+    c0, c1 = pieces(v0, o0, d0, p0), pieces(v1, o1, d1, p1)
+    k0, k1 = pieces(m0, o0, d0, p0), pieces(m1, o1, d1, p1)
+    sb.copy(1.0, p0, o0, [0] * nd, s0, d0, c0, p1, o1, [0] * nd, d1, c1,
+            copyadd=sb.Add if add else sb.Copy, mask0=k0, mask1=k1)
+    torch.cuda.synchronize()
+    out = _gather(p1, c1, d1, t1)
+    assert np.array_equal(out.view(np.uint8), ref.view(np.uint8)), (o0, o1, d0, s0, t0, t1, add)
