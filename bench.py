@@ -255,6 +255,33 @@ SEED_V0, SEED_V1 = 1, 2
 SCALE_TOL, CHAIN_TOL = 1e-10, 1e-5
 
 
+_T_START = time.perf_counter()
+
+
+def progress(msg):
+    """A progress line on stderr (ranks > 1: every rank), so long multi-rank runs show where
+    they are"""
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1 or os.environ.get("SBX_BENCH_PROGRESS"):
+        print("bench[rank %s +%.1fs]: %s" % (os.environ.get("RANK", "0"),
+                                             time.perf_counter() - _T_START, msg),
+              file=sys.stderr, flush=True)
+
+
+def launch_ranks(n, argv):
+    """Run this script on n ranks under torch.distributed.run (one process per GPU, rendezvous on
+    127.0.0.1) as a child process; rank 0 prints the JSON line to the inherited stdout.  Returns
+    the launcher's exit code."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
+           str(n), "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__)] + list(argv)
+    sys.stdout.flush()
+    return subprocess.run(cmd).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -284,6 +311,21 @@ def main():
                          "with one host id per rank (socket transport) -- not a bench")
     args = ap.parse_args()
 
+    # --gpus N is the number of ranks: without a launcher, start one (a child process, before
+    # anything touches the GPU; never exec) and relay its exit code; under a launcher, its world
+    # size must be N (the reference's `mpirun -np N` convention, tests/Makefile:77-84)
+    env_world = os.environ.get("WORLD_SIZE")
+    if args.gpus not in GRIDS:
+        print("bench: --gpus %d: the lattice grids are for 1, 2, 4 or 8 GPUs (%s)"
+              % (args.gpus, GRIDS), file=sys.stderr)
+        sys.exit(2)
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if env_world is not None and int(env_world) != args.gpus:
+        print("bench: the launcher started WORLD_SIZE=%s ranks but --gpus %d was asked"
+              % (env_world, args.gpus), file=sys.stderr)
+        sys.exit(2)
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -307,6 +349,15 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=dev)
             comm = sb.Comm.from_torch_distributed(local_rank)
+
+    progress("communicator ready")
+    transport = {"kind": "none", "count": 1}
+    if comm is not None:
+        kind, count, urank = comm.transport()
+        transport = {"kind": kind, "count": count}
+        if count != world or urank != rank:
+            raise SystemExit("bench: the communicator sees %d ranks (this one %d) but the launcher "
+                             "started %d (this one %d)" % (count, urank, world, rank))
 
     config = args.config or ("1" if world == 1 else "4a")
     if config == "1" and world > 1:
@@ -364,6 +415,7 @@ def main():
     # N > 1 results kept on rank 0 for the check against one GPU (scale_check_*)
     results = {}
     if world > 1 and "chain_dist" not in skip:
+        progress("chain_dist")
         try:
             side.update(chain_dist_bench(sb, dev, comm, world, rank, grid[:3], barrier,
                                          Ls=args.chain_L, Lt=args.chain_T, check=not args.no_1gpu))
@@ -372,6 +424,7 @@ def main():
     if world > 1 and config == "4a" and "redistribution" not in skip:
         # configs[3] "4b" beside the 4a headline: v1 over t only, (a) its all-to-all
         # redistribution alone, (b) the contraction that pipelines it behind the GEMMs
+        progress("redistribution")
         try:
             side.update(redistribution_bench(sb, dev, comm, world, rank, gdim0, p0, v0, v1, pr,
                                              vr, barrier))
@@ -385,6 +438,7 @@ def main():
         # comparison point (not the headline: only a normwise error bound), and ~20 ms of MFMA
         # load right before the timed region
         side.update(form3m_bench(sb, step, flops_step))
+    progress("warm-up")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -396,6 +450,7 @@ def main():
     sb.timings_enable(True)
     sb.timings_filter("gemm_total")
     sb.timings_reset()
+    progress("timed steps")
     t0 = time.perf_counter()
     for i in range(args.steps):
         step()
@@ -433,6 +488,7 @@ def main():
         barrier()
         if rank == 0:
             results[config] = vr.clone()
+            progress("same problem on one GPU")
             try:
                 t1, ref = single_gpu_time(sb, dev, gdim0, gdimr)
                 scaling_fields = {"value_1gpu_same_problem": round(flops_step / t1 / 1e9, 2),
@@ -485,6 +541,9 @@ def main():
             "value": round(value, 2),
             "unit": "GFLOP/s",
             "n_gpus": world,
+            # what the exchanges actually ran on: RCCL's own rank count (ncclCommCount)
+            "world_size_seen_by_rccl": transport["count"] if transport["kind"] == "rccl" else None,
+            "comm_transport": transport["kind"],
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
@@ -936,6 +995,7 @@ def chain_dist_bench(sb, dev, comm, world, rank, grid, barrier, Ls=16, Lt=64, nc
                 SEED_VALS)
     blk = [1, 1, 1, 1, s_, c_]
     iiv = torch.full((V,), 9, dtype=torch.int32, device=dev)
+    progress("chain_dist: create_bsr")
     op = sb.create_bsr(pi, dim, pd, dim, blk, blk, False, [iiv],
                        [torch.from_numpy(jj.reshape(-1)).to(dev)], [vals], comm=comm)
     # the same operator split as the reference's create_lattice_split (tests/bsr.cpp:402-545):
@@ -989,11 +1049,15 @@ def chain_dist_bench(sb, dev, comm, world, rank, grid, barrier, Ls=16, Lt=64, nc
         sb.contraction(1.0, px, z8, dx, dx, "pXYZTSCn", True, [y], px, z8, dx, dx, "pXYZTsCN",
                        False, [y], 0.0, pr, z5, dr, dr, "TSnsN", [vr], comm=comm)
     # the split application must equal the whole operator's
+    progress("chain_dist: redistribute")
     stage1()
+    progress("chain_dist: bsr (whole)")
     stage2_whole()
     y_whole = y.clone()
+    progress("chain_dist: bsr (split)")
     stage2()
     torch.cuda.synchronize()
+    progress("chain_dist: timed")
     split_err = (torch.linalg.vector_norm(y - y_whole) / torch.linalg.vector_norm(y_whole)).item()
     del y_whole
     t_whole = 0.0
@@ -1034,6 +1098,7 @@ def chain_dist_bench(sb, dev, comm, world, rank, grid, barrier, Ls=16, Lt=64, nc
         del x, y, src, vals
         torch.cuda.empty_cache()
         barrier()
+        progress("chain_dist: whole chain on one GPU")
         if rank == 0:
             out["scale_check_rel_err_chain"] = rel_err(vr, chain_global(sb, dev, G, Lt, ncols))
         barrier()

@@ -114,7 +114,8 @@ int sbx_timings_report(char *buf, int len);
    "gemm.share_ab", "copy.nt", "copy.budget", "copy.run", "copy.max_elems", "copy.pair",
    "copy.order", "copy.trans", "copy.btrans", "bsr.variant", "bsr.row_max_cols", "bsr.split_max_cols",
    "bsr.split_cw", "bsr.split_jb", "bsr.split_ilv", "bsr.kron_mfma", "bsr.kron_mfma_min_cols",
-   "bsr.kron_pack", "dist.reduce", "alloc.max_cached"; read-backs "bsr.last_kernel",
+   "bsr.kron_pack", "dist.reduce", "alloc.max_cached", "debug.level" (overrides SB_DEBUG),
+   "debug.corrupt_copy" (tests of the SB_DEBUG checks: drop that local piece of every copy); read-backs "bsr.last_kernel",
    "copy.last_pair", "dist.reduce_calls", "alloc.cross_stream_frees".  Unknown keys fail with an
    error. */
 int sbx_tune_set(const char *key, long long value);
@@ -140,6 +141,9 @@ typedef int (*sbx_alltoallv_fn)(const void *sendbuf, const unsigned long long *s
 int sbx_comm_create_host(int nprocs, int rank, int device, sbx_alltoallv_fn fn, void *user,
                          sbx_comm *comm);
 int sbx_comm_rank(sbx_comm comm, int *rank, int *nprocs);
+/* What carries the exchanges: kind 0 = none (one rank), 1 = RCCL (count / user_rank from
+   ncclCommCount / ncclCommUserRank, i.e. what RCCL itself sees), 2 = host-staged callback */
+int sbx_comm_transport(sbx_comm comm, int *kind, int *count, int *user_rank);
 int sbx_comm_destroy(sbx_comm comm);
 
 /* ---- partitioning helpers (dist.h:3318-3509, 3744-3825) ---- */

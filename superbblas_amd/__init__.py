@@ -69,18 +69,32 @@ _lib.sbx_last_error.restype = ctypes.c_char_p
 
 
 
-# errors of requests that were dropped without wait() and finished at garbage collection: raised
-# by the next call into the library (never silently lost)
+# errors of requests that were dropped without wait() and finished at garbage collection: they
+# are never silently lost -- a warning at once, then raised by the next Request.wait() or by
+# check_dropped() (never by an unrelated call that succeeded)
+import threading as _threading
+
+_dropped_lock = _threading.Lock()
 _dropped_request_errors: List[str] = []
 
 
 def _check(rc: int):
     if rc != 0:
         raise SuperbblasError(_lib.sbx_last_error().decode())
-    if _dropped_request_errors:
-        msg = _dropped_request_errors.pop(0)
+
+
+def _raise_dropped():
+    with _dropped_lock:
+        msg = _dropped_request_errors.pop(0) if _dropped_request_errors else None
+    if msg is not None:
         raise SuperbblasError("a Request dropped without wait() failed when it was finished at "
                               "garbage collection: " + msg)
+
+
+def check_dropped():
+    """Raise the failure of a Request that was dropped without wait() and failed when garbage
+    collection finished it (oldest first); no-op when there is none."""
+    _raise_dropped()
 
 
 import array as _array
@@ -163,6 +177,7 @@ class Request:
         if self._h:
             h, self._h = self._h, None
             _check(_lib.sbx_wait(h))
+        _raise_dropped()
 
     def __del__(self):
         # a dropped request is still completed, but at garbage-collection time rather than at a
@@ -174,10 +189,14 @@ class Request:
                       "exchange at garbage collection", ResourceWarning, stacklevel=2)
         h, self._h = self._h, None
         try:
-            if _lib.sbx_wait(h) != 0:
-                _dropped_request_errors.append(_lib.sbx_last_error().decode())
+            msg = _lib.sbx_last_error().decode() if _lib.sbx_wait(h) != 0 else None
         except Exception as e:  # pragma: no cover (interpreter shutdown)
-            _dropped_request_errors.append(str(e))
+            msg = str(e)
+        if msg is not None:
+            warnings.warn("superbblas_amd: the dropped Request failed: " + msg, RuntimeWarning,
+                          stacklevel=2)
+            with _dropped_lock:
+                _dropped_request_errors.append(msg)
 
 
 def wait(request: Optional["Request"]):
@@ -434,6 +453,14 @@ class Comm:
     def handle(self):
         return self._h
 
+    def transport(self):
+        """(kind, count, user_rank): kind "none" (one rank), "rccl" (count and user_rank as RCCL
+        itself reports them: ncclCommCount / ncclCommUserRank) or "host" (host-staged)."""
+        k, c, r = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _check(_lib.sbx_comm_transport(self._h, ctypes.byref(k), ctypes.byref(c),
+                                       ctypes.byref(r)))
+        return ({0: "none", 1: "rccl", 2: "host"}[k.value], c.value, r.value)
+
     def close(self):
         if self._h:
             _check(_lib.sbx_comm_destroy(self._h))
@@ -659,6 +686,14 @@ class BSR:
     @property
     def handle(self):
         return self._h
+
+    def transport(self):
+        """(kind, count, user_rank): kind "none" (one rank), "rccl" (count and user_rank as RCCL
+        itself reports them: ncclCommCount / ncclCommUserRank) or "host" (host-staged)."""
+        k, c, r = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _check(_lib.sbx_comm_transport(self._h, ctypes.byref(k), ctypes.byref(c),
+                                       ctypes.byref(r)))
+        return ({0: "none", 1: "rccl", 2: "host"}[k.value], c.value, r.value)
 
     def destroy(self):
         if self._h:

@@ -325,6 +325,22 @@ void bsr_krylov(const BsrOp &op, const Scalar &alpha, const std::string &oi,
     // just_local (bsr.h:2020-2075, 2188): only this rank's part of the product, no exchange --
     // the other ranks' components are ignored and every copy stays on this process
     const bool local_only = just_local && comm_in.nprocs > 1;
+    if (debug_level() > 0 && comm_in.nprocs > 1 && !local_only) { // check_consistency (bsr.h:2123)
+        Hasher h;
+        h.add(std::string("bsr_krylov"));
+        h.add(alpha);
+        h.add(beta);
+        h.add(oi);
+        h.add(od);
+        h.add(x_in);
+        h.add(fromx);
+        h.add(sizex);
+        h.add(y_in);
+        h.add(fromy);
+        h.add(sizey);
+        h.add((long)okr);
+        check_consistency(h, "bsr_krylov", comm_in);
+    }
     Comm comm = comm_in;
     DistTensor x = x_in, y = y_in;
     const int base = local_only ? op.rank : 0; // op.pi / op.pd index of rank 0 of `comm`

@@ -427,6 +427,8 @@ int sbx_tune_set(const char *key, long long value) {
         else if (k == "gemm.t48") g_gemm_tune.t48 = (int)value;
         else if (k == "gemm.share_ab") g_gemm_tune.share_ab = (int)value;
         else if (k == "dist.reduce") g_dist_reduce = (int)value;
+        else if (k == "debug.level") g_debug_level = (int)value;
+        else if (k == "debug.corrupt_copy") g_debug_corrupt = (int)value;
         else if (k == "dist.reduce_calls") g_dist_reduce_calls = value;
         else if (k.compare(0, 6, "alloc.") == 0) alloc_tune(key, nullptr, &value);
         else throw Error("tune_set: unknown key " + k);
@@ -466,6 +468,8 @@ int sbx_tune_get(const char *key, long long *value) {
         else if (k == "gemm.t48") *value = g_gemm_tune.t48;
         else if (k == "gemm.share_ab") *value = g_gemm_tune.share_ab;
         else if (k == "dist.reduce") *value = g_dist_reduce;
+        else if (k == "debug.level") *value = g_debug_level;
+        else if (k == "debug.corrupt_copy") *value = g_debug_corrupt;
         else if (k == "dist.reduce_calls") *value = g_dist_reduce_calls;
         else if (k.compare(0, 6, "alloc.") == 0) alloc_tune(key, value, nullptr);
         else throw Error("tune_get: unknown key " + k);
@@ -558,6 +562,24 @@ int sbx_comm_rank(sbx_comm comm, int *rank, int *nprocs) {
     });
 }
 
+int sbx_comm_transport(sbx_comm comm, int *kind, int *count, int *user_rank) {
+    return guard([&] {
+        const Comm c = get_comm(comm);
+        int k = 0, n = c.nprocs, r = c.rank;
+        if (c.nccl) {
+            k = 1;
+            ncclResult_t e = ncclCommCount((ncclComm_t)c.nccl, &n);
+            if (e == ncclSuccess) e = ncclCommUserRank((ncclComm_t)c.nccl, &r);
+            if (e != ncclSuccess) throw Error(std::string("RCCL: ") + ncclGetErrorString(e));
+        } else if (c.host_fn) {
+            k = 2;
+        }
+        if (kind) *kind = k;
+        if (count) *count = n;
+        if (user_rank) *user_rank = r;
+    });
+}
+
 int sbx_comm_destroy(sbx_comm comm) {
     return guard([&] {
         if (!comm) return;
@@ -640,14 +662,8 @@ int sbx_copy_masked(int nd0, int nd1, const double *alpha, int t0, int t1, const
 
 namespace {
 /// SB_DEBUG >= 1 (runtime_features.h:24-37): the GPU is synchronised and the ranks meet at a
-/// barrier before and after every copy and contraction (the reference's debug mode, dist.h:2274-2280)
-int debug_level() {
-    static const int v = [] {
-        const char *l = std::getenv("SB_DEBUG");
-        return l ? std::max(0, std::atoi(l)) : 0;
-    }();
-    return v;
-}
+/// barrier before and after every copy and contraction (the reference's debug mode, dist.h:2274-2280);
+/// debug_level() is in debug.cpp (the tune key debug.level overrides SB_DEBUG)
 struct DebugSync {
     const Comm &c;
     explicit DebugSync(const Comm &c_) : c(c_) { sync(); }
@@ -682,7 +698,9 @@ int sbx_copy_req(int nd0, int nd1, const double *alpha, int t0, int t1, const in
         const DebugSync dbg(c);
         const Scalar a_call = to_scalar(alpha);
         // fast path (see above): the shape key excludes the data pointers and alpha's value
-        bool fast = !mask0 && !mask1 && c.nprocs == 1 && p0 && p1 && v0 && v1 && o0 && o1 &&
+        // (SB_DEBUG >= 2 checks every copy through dist_copy: no replay)
+        bool fast = !mask0 && !mask1 && c.nprocs == 1 && debug_level() < 2 && p0 && p1 && v0 &&
+                    v1 && o0 && o1 &&
                     ncomponents0 >= 1 && ncomponents1 >= 1 && ctx0 && ctx1 &&
                     (int)std::strlen(o0) == nd0 && (int)std::strlen(o1) == nd1;
         for (int i = 0; fast && i < ncomponents0; ++i) fast = ctx0[i].plat == SBX_GPU;

@@ -267,6 +267,16 @@ void dist_contraction(const Scalar &alpha, const DistTensor &v0, const Coor &fro
     check_contraction_args(v0.labels, size0, v1.labels, size1, vr.labels, sizer, v0.dtype,
                            v1.dtype, vr.dtype);
     if (v0.dtype != v1.dtype || v0.dtype != vr.dtype) throw Error("contraction: mixed types");
+    if (debug_level() > 0 && comm.nprocs > 1) { // check_consistency (dist.h:3105-3119)
+        Hasher h;
+        h.add(std::string("contraction"));
+        h.add(alpha);
+        h.add(beta);
+        for (const DistTensor *t : {&v0, &v1, &vr}) h.add(*t);
+        for (const Coor *c : {&from0, &size0, &from1, &size1, &fromr, &sizer}) h.add(*c);
+        h.add((long)conj0 * 2 + (long)conj1);
+        check_consistency(h, "contraction", comm);
+    }
 
     const int dtype = v0.dtype;
     const std::size_t es = dtype_size(dtype);

@@ -402,6 +402,19 @@ void dist_copy(const Scalar &alpha, const DistTensor &src, const Coor &from0, co
             throw Error("Invalid copy operation");
         }
     }
+    if (debug_level() > 0 && comm.nprocs > 1) {
+        Hasher h;
+        h.add(std::string("copy"));
+        h.add(alpha);
+        h.add(src);
+        h.add(from0);
+        h.add(size0);
+        h.add(dst);
+        h.add(from1);
+        h.add((long)add);
+        check_consistency(h, "copy", comm);
+    }
+    copy_mock_test(src, from0, size0, dst, from1, add, comm);
     if (volume(size0) == 0) return;
 
     const std::vector<CompRef> sc = flatten_components(src), dc = flatten_components(dst);
@@ -453,9 +466,12 @@ void dist_copy(const Scalar &alpha, const DistTensor &src, const Coor &from0, co
     if (!add && !plan->full) zero_region();
 
     // Local pieces
+    int local_no = 0;
+    const int corrupt = g_debug_corrupt.load(std::memory_order_relaxed);
     for (const Piece &p : pieces) {
         const CompRef &ca = sc[p.a], &cb = dc[p.b];
         if (ca.rank != comm.rank || cb.rank != comm.rank) continue;
+        if (++local_no == corrupt) continue; // a deliberately wrong plan (debug.corrupt_copy)
         const Range &ra = src.ranges[ca.rank][ca.idx];
         const Range &rb = dst.ranges[cb.rank][cb.idx];
         const int da = src.dev[ca.idx], db = dst.dev[cb.idx];
@@ -686,6 +702,35 @@ bool dist_reduce_collective(const DistTensor &part, const Coor &f0, const Coor &
     Comm self;
     self.device = device;
     dist_copy(Scalar{1, 0}, sl, f0, s0, dl, f1, true, self);
+    return true;
+}
+
+bool comm_all_equal(const Comm &comm, unsigned long long v) {
+    if (comm.nprocs <= 1) return true;
+    if (comm.nccl) {
+        // one all-reduce (max) of (v, ~v): every rank learns max(v) and ~min(v)
+        set_device(comm.device);
+        hipStream_t s = get_stream(comm.device);
+        unsigned long long h[2] = {v, ~v};
+        Scratch buf(sizeof(h), comm.device);
+        SBX_HIP_CHECK(hipMemcpyAsync(buf.ptr, h, sizeof(h), hipMemcpyHostToDevice, s));
+        nccl_check(ncclAllReduce(buf.ptr, buf.ptr, 2, ncclUint64, ncclMax, (ncclComm_t)comm.nccl, s),
+                   "ncclAllReduce");
+        SBX_HIP_CHECK(hipMemcpyAsync(h, buf.ptr, sizeof(h), hipMemcpyDeviceToHost, s));
+        SBX_HIP_CHECK(hipStreamSynchronize(s));
+        return h[0] == ~h[1];
+    }
+    if (!comm.host_fn) throw Error("the communicator has no transport");
+    // every rank sends its value to every other rank through the caller's all-to-all
+    std::vector<unsigned long long> sn(comm.nprocs, sizeof(v)), sd(comm.nprocs, 0),
+        rn(comm.nprocs, sizeof(v)), rd(comm.nprocs), all(comm.nprocs, v);
+    sn[comm.rank] = rn[comm.rank] = 0;
+    for (int q = 0; q < comm.nprocs; ++q) rd[q] = q * sizeof(v);
+    const int rc = comm.host_fn(&v, sn.data(), sd.data(), all.data(), rn.data(), rd.data(),
+                                comm.host_user);
+    if (rc != 0) throw Error("the host all-to-all callback failed (" + std::to_string(rc) + ")");
+    for (unsigned long long x : all)
+        if (x != v) return false;
     return true;
 }
 

@@ -1092,7 +1092,10 @@ bool prepare_btrans(CopyLaunch &l, const Norm &n0, int first, long R, long total
     for (int v1 = first; v1 < nd0; ++v1) {
         if (n0.size[v1] < 2) continue;
         Norm n = n0;
-        auto chain = [&](bool dst_side, std::vector<int> &c, std::vector<bool> &used) {
+        // `other`: the chain built before this one; a dim of it may be split here only when it is
+        // that chain's last dim (splitting an inner one would break its run of strides)
+        auto chain = [&](bool dst_side, std::vector<int> &c, std::vector<bool> &used,
+                         const std::vector<int> *other) {
             long want = R, prod = 1;
             while ((int)n.size.size() <= MAXD) {
                 int f = -1;
@@ -1101,6 +1104,9 @@ bool prepare_btrans(CopyLaunch &l, const Norm &n0, int first, long R, long total
                 if (f < 0) break;
                 if (prod * n.size[f] > cap) {
                     if (sizeof(D) < 16) break; // (no split plans for smaller elements, above)
+                    if (other && std::find(other->begin(), other->end(), f) != other->end() &&
+                        other->back() != f)
+                        break;
                     long d = 1; // the largest inner factor that fits
                     for (long q = 2; q <= cap / prod; ++q)
                         if (n.size[f] % q == 0) d = q;
@@ -1121,11 +1127,22 @@ bool prepare_btrans(CopyLaunch &l, const Norm &n0, int first, long R, long total
         std::vector<int> si, di;
         std::vector<bool> us(n.size.size(), false), ud(n.size.size(), false);
         us[v1] = ud[v1] = true;
-        chain(false, si, us);
+        chain(false, si, us, nullptr);
         ud.resize(n.size.size(), false);
-        chain(true, di, ud);
+        chain(true, di, ud, &si);
         const int nd = (int)n.size.size();
         if (nd > MAXD) continue;
+        // both chains must still be runs: strides R, R*s0, R*s0*s1, ... on their side (a split
+        // made by the later chain changes the sizes the earlier one was built from)
+        auto is_run = [&](const std::vector<int> &c, const std::vector<long> &st) {
+            long want = R;
+            for (int i : c) {
+                if (st[i] != want) return false;
+                want *= n.size[i];
+            }
+            return true;
+        };
+        if (!is_run(si, n.ss) || !is_run(di, n.ds)) continue;
         auto nu_of = [&]() {
             std::vector<bool> in(nd, false);
             long nu = 1;

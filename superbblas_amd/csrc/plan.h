@@ -136,6 +136,37 @@ struct Local {
 
 /// Every rank of `comm` reaches this point before any leaves it (MPI_Barrier)
 void comm_barrier(const Comm &comm);
+/// Whether every rank passed the same `v` (the answer is the same on every rank)
+bool comm_all_equal(const Comm &comm, unsigned long long v);
+
+//
+// SB_DEBUG self-checks (debug.cpp; runtime_features.h:24-37)
+//
+/// SB_DEBUG (read once; the tune key debug.level overrides it)
+int debug_level();
+extern std::atomic<int> g_debug_level;
+/// tune key debug.corrupt_copy (tests of the checks only): > 0 drops that local piece (1-based) of
+/// every distributed copy, a deliberately wrong plan
+extern std::atomic<int> g_debug_corrupt;
+/// Hash of call arguments (check_consistency's Hash, dist.h:513-606)
+struct Hasher {
+    unsigned long long h = 1469598103934665603ull;
+    void add_bytes(const void *p, std::size_t n);
+    void add(long v) { add_bytes(&v, sizeof(v)); }
+    void add(const Coor &c);
+    void add(const std::string &s);
+    void add(const Scalar &s);
+    void add(const struct DistTensor &t);
+};
+/// SB_DEBUG >= 1, several ranks: throws on EVERY rank unless every rank hashed the same
+/// arguments (check_consistency, dist.h:702-736, which compares with rank 0's hash only and so
+/// lets the agreeing ranks run on into an exchange the others never join)
+void check_consistency(const Hasher &h, const char *what, const Comm &comm);
+/// SB_DEBUG >= 2: run the copy on index-valued size_t mock tensors (same partitions, masks,
+/// devices, communicator) and check every destination element exactly (ns_copy_test,
+/// dist.h:1919-2116); throws "test_copy_check does not pass!" on a mismatch
+void copy_mock_test(const struct DistTensor &src, const Coor &from0, const Coor &size0,
+                    const struct DistTensor &dst, const Coor &from1, bool add, const Comm &comm);
 
 /// The contraction's cross-rank sum of partial outputs as one RCCL collective (the
 /// reference Adds them with a copy, dist.h:3183-3186, 1364-1404): when every rank holds one

@@ -588,6 +588,35 @@ def case_golden(sb, comm, rank, n, dev):
                 assert max(errs) < 1e-10, ("golden", case["id"], shape, mode, errs)
 
 
+def case_debug(sb, comm, rank, n, dev):
+    """SB_DEBUG (tune key debug.level): at 2 the distributed copies run the mock-index check
+    (dist.h:1919-2116) on every rank; at 1 a rank called with different arguments makes EVERY
+    rank fail (check_consistency, dist.h:702-736) instead of leaving the others in an exchange"""
+    old = sb.tune_get("debug.level")
+    try:
+        sb.tune_set("debug.level", 2)
+        case_copy(sb, comm, rank, n, dev)
+        case_fuzz(sb, comm, rank, n, dev, ncases=4)
+        sb.tune_set("debug.level", 1)
+        dim0, dim1 = [4, 4, 2, 6], [6, 2, 4, 4]
+        p0 = sb.basic_partitioning("xyzt", dim0, [1, 1, 1, n], "t", n, 1)
+        p1 = sb.basic_partitioning("tzyx", dim1, [1, 1, 1, n], "x", n, 1)
+        v0 = scatter(sb, gen("index", vol(dim0), 1, np.complex128), dim0, p0, rank, 1, dev)
+        v1 = scatter(sb, gen("int", vol(dim1), 2, np.complex128), dim1, p1, rank, 1, dev)
+        try:
+            sb.copy(2.0 if rank == n - 1 else 1.0, p0, "xyzt", [0] * 4, dim0, dim0, v0, p1,
+                    "tzyx", [0] * 4, dim1, v1, comm=comm)
+        except sb.SuperbblasError as e:
+            assert "check_consistency failed" in str(e), e
+        else:
+            raise AssertionError("check_consistency missed different arguments on rank %d" % rank)
+        # the same call with equal arguments still works afterwards
+        sb.copy(1.0, p0, "xyzt", [0] * 4, dim0, dim0, v0, p1, "tzyx", [0] * 4, dim1, v1, comm=comm)
+        torch.cuda.synchronize()
+    finally:
+        sb.tune_set("debug.level", old)
+
+
 def _rand_partition(sb, rng, labels, dims, n):
     i = int(rng.integers(0, len(dims)))
     procs = [1] * len(dims)
@@ -705,7 +734,7 @@ def main():
         comm = sb.Comm.from_torch_distributed(dev_idx)
     else:
         comm = sb.Comm.host_staged(dev_idx)
-    cases = os.environ.get("SBX_TEST_CASES", "copy,contr,bsr,kron,dense,storage,fuzz,fuzzl,golden,split,reduce").split(",")
+    cases = os.environ.get("SBX_TEST_CASES", "copy,contr,bsr,kron,dense,storage,fuzz,fuzzl,golden,split,reduce,debug").split(",")
     if "copy" in cases:
         case_copy(sb, comm, rank, n, dev)
     if "contr" in cases:
@@ -728,6 +757,8 @@ def main():
         case_reduce(sb, comm, rank, n, dev, transport)
     if "split" in cases:
         case_split(sb, comm, rank, n, dev)
+    if "debug" in cases:
+        case_debug(sb, comm, rank, n, dev)
     dist.barrier()
     comm.close()
     dist.destroy_process_group()

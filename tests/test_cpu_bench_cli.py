@@ -35,3 +35,34 @@ def test_global_fill_partition_invariant():
     assert not torch.equal(other, full)
     assert full.real.abs().max() <= 1 and full.imag.abs().max() <= 1
     assert abs(full.real.mean().item()) < 0.1 and full.real.std().item() > 0.5
+
+
+def test_bench_gpus_must_match_launcher():
+    """Under a launcher, --gpus must equal its WORLD_SIZE (a silent N = 1 line otherwise);
+    unsupported N fail before any rank starts.  No GPU is touched on these paths."""
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr, r.stderr
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "--gpus 3" in r.stderr, r.stderr
+
+
+def test_bench_launch_command():
+    """Without a launcher, --gpus N > 1 starts torch.distributed.run with N ranks as a child
+    process on 127.0.0.1, passing the same arguments through."""
+    import unittest.mock as um
+    sys.path.insert(0, ROOT)
+    import bench
+    with um.patch.object(bench.subprocess, "run") as run:
+        run.return_value.returncode = 7
+        rc = bench.launch_ranks(8, ["--gpus", "8", "--steps", "3"])
+    assert rc == 7
+    cmd = run.call_args[0][0]
+    assert cmd[1:4] == ["-m", "torch.distributed.run", "--nnodes=1"]
+    assert cmd[cmd.index("--nproc-per-node") + 1] == "8"
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-4:] == ["--gpus", "8", "--steps", "3"]
+    assert cmd[-5].endswith("bench.py")

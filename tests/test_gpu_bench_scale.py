@@ -43,3 +43,45 @@ def test_bench_n2_scale_check(gpu, config):
         assert v <= (1e-5 if k.endswith("_chain") else 1e-10), (k, v)
     assert line["scale_check_ok"] is True
     assert line["chain_dist_bsr_split_rel_diff"] < 1e-5
+
+
+def _bench_no_launcher(n, extra, timeout=420):
+    """bench.py --gpus n run WITHOUT a launcher: it must start the n ranks itself"""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "2"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--share-gpu",
+           "rccl"] + extra
+    # the ranks' progress lines (stderr) go to a file under gpurun_out/ when it exists, so a long
+    # multi-rank run keeps showing signs of life
+    outdir = os.path.join(ROOT, "gpurun_out")
+    os.makedirs(outdir, exist_ok=True)
+    log = os.path.join(outdir, "bench_n%d.log" % n)
+    with open(log, "w") as f:
+        r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=f, text=True,
+                           timeout=timeout)
+    with open(log) as f:
+        err = f.read()
+    assert r.returncode == 0, (r.stdout[-3000:], err[-6000:])
+    lines = [s for s in r.stdout.splitlines() if s.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_bench_gpus_n_launches_ranks(gpu, n):
+    """`bench.py --gpus N` with no launcher runs N ranks (configs[3]'s grids 2x1x1x1, 2x2x1x1,
+    2x2x2x1 at a reduced lattice), RCCL reports N ranks, and the 4a, 4b-redistributed and chain
+    answers match the same global problem on one GPU"""
+    line = _bench_no_launcher(n, ["--steps", "2", "--warmup", "1", "--L", "8", "--ncols", "8",
+                                  "--chain-L", "4", "--chain-T", "8"])
+    assert line["n_gpus"] == n
+    assert line["world_size_seen_by_rccl"] == n and line["comm_transport"] == "rccl"
+    assert line["config"]["parallelism"] == "xyzt grid " + {2: "2x1x1x1", 4: "2x2x1x1",
+                                                           8: "2x2x2x1"}[n]
+    errs = {k: v for k, v in line.items() if k.startswith("scale_check_rel_err")}
+    assert set(errs) == {"scale_check_rel_err_4a", "scale_check_rel_err_contraction_redistributed",
+                         "scale_check_rel_err_chain"}, line
+    for k, v in errs.items():
+        assert v <= (1e-5 if k.endswith("_chain") else 1e-10), (k, v)
+    assert line["scale_check_ok"] is True

@@ -204,3 +204,29 @@ def test_trans_many_items_small_chain(gpu, t, add):
     oracle_copy(1.0, o0, [0] * 3, dim0, dim0, v0, o1, [0] * 3, dim1, ref, add=add)
     out, kind = _copy(gpu, 1.0, o0, [0] * 3, dim0, dim0, v0, o1, [0] * 3, dim1, v1.copy(), add=add)
     assert np.array_equal(out.view(np.uint8), ref.view(np.uint8))
+
+
+@pytest.mark.parametrize("o0,dim0,o1", [("vpba", [64, 2, 32, 8], "vabp"),
+                                        ("vpba", [16, 2, 32, 8], "vabp"),
+                                        ("wvpba", [3, 16, 4, 16, 8], "wvabp")])
+def test_btrans_split_keeps_source_run(gpu, o0, dim0, o1):
+    """the destination chain of the block transpose split a dimension the
+    source chain had already taken in the middle of its run (complex<double>, source a,b,p,v
+    fastest first, destination p,b,a,v), so the kernel read the source run as contiguous across
+    a broken stride.  Bit-exact against the oracle and the tile kernel (copy.btrans -1)."""
+    import superbblas_amd as sb
+    dim1 = [dim0[o0.index(c)] for c in o1]
+    v0 = index_valued(_vol(dim0), np.complex128)
+    v1 = int_valued(_vol(dim1), np.complex128, 3)
+    ref = v1.copy()
+    oracle_copy(1.0, o0, [0] * len(o0), dim0, dim0, v0, o1, [0] * len(o1), dim1, ref)
+    out, kind = _copy(gpu, 1.0, o0, [0] * len(o0), dim0, dim0, v0, o1, [0] * len(o1), dim1,
+                      v1.copy())
+    assert np.array_equal(out.view(np.uint8), ref.view(np.uint8)), kind
+    sb.tune_set("copy.btrans", -1)
+    try:
+        out2, _ = _copy(gpu, 1.0, o0, [0] * len(o0), dim0, dim0, v0, o1, [0] * len(o1), dim1,
+                        v1.copy())
+    finally:
+        sb.tune_set("copy.btrans", 0)
+    assert np.array_equal(out2.view(np.uint8), ref.view(np.uint8))

@@ -58,3 +58,12 @@ def test_dist_host_staged_grid4(gpu):
 def test_dist_rccl(gpu, nprocs):
     import torch
     _run(nprocs, "rccl", shared=torch.cuda.device_count() < nprocs)
+
+
+@pytest.mark.parametrize("nprocs", [4, 8])
+def test_dist_rccl_golden_grid(gpu, nprocs):
+    """configs[3]'s lattice grids at N = 4 (2x2x1) and N = 8 (2x2x2): the reference's golden
+    random-valued contractions with v0 / v1 on the xyz grid (4a) or v1 over t (4b, redistributed)
+    over RCCL, both reductions (collective / point-to-point), within 1e-10 per component"""
+    import torch
+    _run(nprocs, "rccl", cases="golden", shared=torch.cuda.device_count() < nprocs)
