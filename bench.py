@@ -753,19 +753,81 @@ def permute_bench(sb, dev, L, n, reps=3):
     except Exception:  # pragma: no cover
         t2 = timed(run_f)
     res["permute_cf2cd_GBps"] = round(24.0 * vol(d1) / t2 / 1e9, 1)
+
+    def graph_time(fn):
+        try:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                fn()
+            return timed(g.replay)
+        except Exception:  # pragma: no cover
+            return timed(fn)
+    # the reference's own element type (tests/dist.cpp:200, Scalar = complex<float>) and its
+    # "overhead" figure: the permute loop against the same bytes copied contiguously into the 64
+    # slices (its "dummy copying", dist.cpp:205-235)
+    bf = torch.empty(vol(d1), dtype=torch.complex64, device=dev)
+
+    def run_ff():
+        for k in range(n):
+            sb.copy(1.0, p0, "xyztsc", [0] * 6, d0, d0, [af], p1, "tnsxyzc", [0, k, 0, 0, 0, 0, 0],
+                    d1, [bf])
+    nel0 = vol(d0)
+
+    def memcpy_f():
+        for k in range(n):
+            bf[k * nel0:(k + 1) * nel0].copy_(af)
+
+    def memcpy_d():
+        for k in range(n):
+            b[k * nel0:(k + 1) * nel0].copy_(a)
+    t3 = graph_time(run_ff)
+    tmf, tmd = graph_time(memcpy_f), graph_time(memcpy_d)
+    res.update({"permute_cf2cf_GBps": round(16.0 * vol(d1) / t3 / 1e9, 1),
+                "permute_cf2cf_ms": round(t3 * 1e3, 3),
+                "memcpy_slices_cf_GBps": round(16.0 * vol(d1) / tmf / 1e9, 1),
+                "permute_cf2cf_overhead_vs_memcpy": round(t3 / tmf, 3),
+                "memcpy_slices_cd_GBps": round(32.0 * vol(d1) / tmd / 1e9, 1),
+                "permute_overhead_vs_memcpy": round(t / tmd, 3)})
+    del bf
+    # what the slice loop's bytes are: the 12.6 / 25.2 MB source is re-read by all 64 slices and
+    # stays in the Infinity Cache (256 MB), so half of the algorithmic bytes never reach HBM; the
+    # HBM figures are the write stream of the loop and the whole-tensor permute below
+    res["permute_frac_note"] = ("permute_frac_hbm counts 32 B per element (read + write) against "
+                                "8 TB/s, but the 25 MB source is re-read from the Infinity Cache "
+                                "by every slice; HBM: permute_write_stream_frac_hbm and "
+                                "permute_whole_frac_hbm")
+    res["permute_write_stream_frac_hbm"] = round(16.0 * vol(d1) / t / 1e9 / PEAK_HBM_GBPS, 4)
+    # the whole-tensor permute xyztnsc -> tnsxyzc (1.61 GB, every byte to and from HBM)
+    dw = [L, L, L, L, n, 4, 3]
+    w = torch.empty(vol(dw), dtype=torch.complex128, device=dev)
+    w.view(torch.float64).zero_()
+
+    def run_w():
+        sb.copy(1.0, [([0] * 7, dw)], "xyztnsc", [0] * 7, dw, dw, [w], p1, "tnsxyzc", [0] * 7, d1,
+                [b])
+    tw = timed(run_w)
+    del w
+    res.update({"permute_whole_GBps": round(32.0 * vol(d1) / tw / 1e9, 1),
+                "permute_whole_frac_hbm": round(32.0 * vol(d1) / tw / 1e9 / PEAK_HBM_GBPS, 4),
+                "permute_whole_ms": round(tw * 1e3, 3)})
     # the same 64-slice loop called eagerly from C++ through the C ABI (tests/dist.cpp's loop;
-    # no Python between calls): the host cost per sbx_copy with the plan / launch caches warm
+    # no Python between calls): the host cost per sbx_copy with the plan / launch caches warm,
+    # and the reference's overhead-vs-memcpy ratio of that loop, for both element types
     exe = os.path.join(ROOT, "tools", "capi_overhead")
     if os.path.exists(exe):
-        try:
-            r = subprocess.run([exe, "permute", str(L), str(n), "5"], timeout=120,
-                               capture_output=True, text=True, check=True).stdout
-            r = json.loads(r.strip().splitlines()[-1])
-            res["permute_eager_cpp_GBps"] = r["GBps"]
-            res["permute_eager_cpp_frac_hbm"] = round(r["GBps"] / PEAK_HBM_GBPS, 4)
-            res["capi_host_us_per_copy"] = r["host_us_per_copy"]
-        except Exception as e:  # pragma: no cover
-            res["permute_eager_cpp_error"] = str(e)[:200]
+        for ty in ("cd", "cf"):
+            try:
+                r = subprocess.run([exe, "permute", str(L), str(n), "5", ty], timeout=120,
+                                   capture_output=True, text=True, check=True).stdout
+                r = json.loads(r.strip().splitlines()[-1])
+                key = "permute_eager_cpp" if ty == "cd" else "permute_cf2cf_eager_cpp"
+                res[key + "_GBps"] = r["GBps"]
+                res[key + "_overhead_vs_memcpy"] = r["overhead_vs_memcpy"]
+                if ty == "cd":
+                    res["permute_eager_cpp_frac_hbm"] = round(r["GBps"] / PEAK_HBM_GBPS, 4)
+                    res["capi_host_us_per_copy"] = r["host_us_per_copy"]
+            except Exception as e:  # pragma: no cover
+                res["permute_eager_cpp_error"] = str(e)[:200]
     return res
 
 

@@ -699,7 +699,8 @@ int sbx_copy_req(int nd0, int nd1, const double *alpha, int t0, int t1, const in
         const Scalar a_call = to_scalar(alpha);
         // fast path (see above): the shape key excludes the data pointers and alpha's value
         // (SB_DEBUG >= 2 checks every copy through dist_copy: no replay)
-        bool fast = !mask0 && !mask1 && c.nprocs == 1 && debug_level() < 2 && p0 && p1 && v0 &&
+        bool fast = !mask0 && !mask1 && c.nprocs == 1 && debug_level() < 2 &&
+                    g_debug_corrupt.load() == 0 && p0 && p1 && v0 &&
                     v1 && o0 && o1 &&
                     ncomponents0 >= 1 && ncomponents1 >= 1 && ctx0 && ctx1 &&
                     (int)std::strlen(o0) == nd0 && (int)std::strlen(o1) == nd1;

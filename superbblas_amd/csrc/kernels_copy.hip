@@ -1070,6 +1070,9 @@ bool prepare_btrans(CopyLaunch &l, const Norm &n0, int first, long R, long total
     } best;
     constexpr long EMAX = btrans_emax<D>();
     const long cap0 = std::min(256L, EMAX / (2 * R));
+    // (runs too long for two items per tile: nothing to transpose here -- and cap0 = 0 would never
+    // end the halving loop below, which hung the chain's halo copies with 4.6K-element runs)
+    if (cap0 < 2) return false;
     // V1 items per tile: as many as fit, rounded so that runs continuing over V1 (source first)
     // are whole 128-B lines (the chain redistribution's 240-B source runs read 1.47x their bytes)
     auto qt_of = [&](long nv1, long NU, long rs, long ssv, long rd, long dsv) {
@@ -1087,7 +1090,7 @@ bool prepare_btrans(CopyLaunch &l, const Norm &n0, int first, long R, long total
     // that a tile holds more V1 items -- longer runs on V1's side (the whole-tensor complex<double>
     // permute 335 -> 310 us); for smaller elements the split plans measured slower than the tile
     // kernel's paired accesses (profiles/r03_copy_btrans.txt)
-    const long cap_min = sizeof(D) >= 16 ? 8 : cap0;
+    const long cap_min = std::max(2L, sizeof(D) >= 16 ? 8L : cap0);
     for (long cap = cap0; cap >= cap_min; cap /= 2)
     for (int v1 = first; v1 < nd0; ++v1) {
         if (n0.size[v1] < 2) continue;

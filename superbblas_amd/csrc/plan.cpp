@@ -205,6 +205,11 @@ std::vector<Range> basic_partitioning(const char *order, const Coor &dim, const 
         for (std::size_t i = 0; i < Nd; ++i) perm[i] = (int)i;
     }
 
+    // (the reference constructs this error without throwing it, dist.h:3400-3402, and then writes
+    // past the end of its result; here it is thrown)
+    if (nprocs >= 0 && vol_procs > nprocs)
+        throw Error("The total number of processes from `procs` is greater than `nprocs`");
+    if (ncomponents < 1) throw Error("basic_partitioning: invalid `ncomponents`");
     std::vector<Range> fs((std::size_t)(nprocs < 0 ? vol_procs : nprocs) * ncomponents,
                           Range{Coor(Nd, 0), Coor(Nd, 0)});
     Coor procs_perm(Nd);

@@ -90,3 +90,15 @@ def test_fast_to_slow_plan_matches_slow_to_fast():
         b = sb.copy_plan(rev(p0), "tzyx", [3, 0, 2, 1], [5, 2, 4, 3], dim0[::-1], 1, rev(p1),
                          "xyzt", [3, 1, 0, 2], dim1[::-1], 1, 2, rank, co=sb.FastToSlow)
         assert a == b
+
+
+def test_basic_partitioning_more_procs_than_nprocs():
+    """procs covering more processes than nprocs: the reference builds this error without
+    throwing it and then writes past its result (dist.h:3400-3402); here it is raised"""
+    import pytest
+    import superbblas_amd as sb
+    with pytest.raises(sb.SuperbblasError, match="greater than `nprocs`"):
+        sb.basic_partitioning("tnsxyzc", [8, 12, 4, 8, 8, 4, 3], [4, 1, 1, 1, 1, 1, 1], "t", 1, 4)
+    # components of one process: procs is the process grid, components split inside
+    p = sb.basic_partitioning("xyzt", [8, 8, 4, 8], [1, 1, 1, 1], "xyz", 1, 4)
+    assert len(p) == 4 and sum(a * b * c * d for _, (a, b, c, d) in p) == 8 * 8 * 4 * 8

@@ -230,3 +230,17 @@ def test_btrans_split_keeps_source_run(gpu, o0, dim0, o1):
     finally:
         sb.tune_set("copy.btrans", 0)
     assert np.array_equal(out2.view(np.uint8), ref.view(np.uint8))
+
+
+@pytest.mark.parametrize("t", [np.complex64, np.float64, np.complex128])
+def test_long_runs_strided_box(gpu, t):
+    """Runs longer than half a block-transpose tile with one strided outer dim (the chain's halo
+    copies: 4608-element runs into a domain with a halo): the block-transpose planner's halving
+    loop never ended when no two items fit a tile (cap 0) -- a host hang.  Bit-exact."""
+    o, d0, d1 = "ab", [4, 2000], [5, 2001]
+    v0 = index_valued(_vol(d0), t) if np.dtype(t).kind == "c" else np.arange(_vol(d0)).astype(t)
+    v1 = int_valued(_vol(d1), t, 3)
+    ref = v1.copy()
+    oracle_copy(1.0, o, [0, 0], d0, d0, v0, o, [1, 1], d1, ref)
+    out, _ = _copy(gpu, 1.0, o, [0, 0], d0, d0, v0, o, [1, 1], d1, v1.copy())
+    assert np.array_equal(out.view(np.uint8), ref.view(np.uint8))
