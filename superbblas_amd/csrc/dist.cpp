@@ -537,14 +537,28 @@ void dist_copy(const Scalar &alpha, const DistTensor &src, const Coor &from0, co
         for (const Piece &p : pieces) {
             const CompRef &ca = sc[p.a], &cb = dc[p.b];
             if (ca.rank != comm.rank || cb.rank == comm.rank) continue;
-            if (src.dev[ca.idx] != device)
-                throw Error("copy: with a communicator every component must be on the "
-                            "communicator's device");
+            const int da = src.dev[ca.idx];
+            char *slot = (char *)sbuf->ptr + cur[cb.rank];
+            const std::size_t bytes = volume(p.size) * es;
+            cur[cb.rank] += bytes;
+            if (da == device) {
+                local_piece_copy(Scalar{1, 0}, src.dtype, src.ptr[ca.idx],
+                                 src.ranges[ca.rank][ca.idx].size, p.src_from, src.dtype, slot,
+                                 p.size, Coor(src.nd(), 0), p.size, id, false, device);
+                continue;
+            }
+            // a component on another GPU of this rank (several components per rank, the
+            // reference's --components, dist.h:205-241): packed on its own device, then peer-
+            // copied (xGMI) into the communicator device's send buffer
+            if (CopyTape *t = current_copy_tape()) t->valid = false;
+            Scratch tmp(bytes, da);
             local_piece_copy(Scalar{1, 0}, src.dtype, src.ptr[ca.idx],
-                             src.ranges[ca.rank][ca.idx].size, p.src_from, src.dtype,
-                             (char *)sbuf->ptr + cur[cb.rank], p.size, Coor(src.nd(), 0), p.size,
-                             id, false, device);
-            cur[cb.rank] += volume(p.size) * es;
+                             src.ranges[ca.rank][ca.idx].size, p.src_from, src.dtype, tmp.ptr,
+                             p.size, Coor(src.nd(), 0), p.size, id, false, da);
+            stream_wait(da, device);
+            set_device(device);
+            SBX_HIP_CHECK(hipMemcpyPeerAsync(slot, device, tmp.ptr, da, bytes, get_stream(device)));
+            stream_wait(device, da); // tmp is reused on `da` only after the peer copy
         }
         if (comm.nccl) {
             // RCCL: grouped point-to-point send/recv straight from/to device memory (xGMI)
@@ -593,14 +607,28 @@ void dist_copy(const Scalar &alpha, const DistTensor &src, const Coor &from0, co
         for (const Piece &p : plan_ref->pieces) {
             const CompRef &ca = sc2[p.a], &cb = dc2[p.b];
             if (cb.rank != comm.rank || ca.rank == comm.rank) continue;
-            if (dst_c.dev[cb.idx] != device)
-                throw Error("copy: with a communicator every component must be on the "
-                            "communicator's device");
-            local_piece_copy(alpha, src_c.dtype, (char *)rbuf->ptr + cur[ca.rank], p.size,
-                             Coor(src_c.nd(), 0), dst_c.dtype, dst_c.ptr[cb.idx],
-                             dst_c.ranges[cb.rank][cb.idx].size, p.dst_from, p.size, perm_s2d,
-                             add, device, nullptr, dst_c.mask_of(cb.idx));
-            cur[ca.rank] += volume(p.size) * es;
+            const int db = dst_c.dev[cb.idx];
+            const char *slot = (const char *)rbuf->ptr + cur[ca.rank];
+            const std::size_t bytes = volume(p.size) * es;
+            cur[ca.rank] += bytes;
+            if (db == device) {
+                local_piece_copy(alpha, src_c.dtype, slot, p.size, Coor(src_c.nd(), 0),
+                                 dst_c.dtype, dst_c.ptr[cb.idx], dst_c.ranges[cb.rank][cb.idx].size,
+                                 p.dst_from, p.size, perm_s2d, add, device, nullptr,
+                                 dst_c.mask_of(cb.idx));
+                continue;
+            }
+            // a destination component on another GPU of this rank: peer copy of the received
+            // piece to that device, unpacked there
+            Scratch tmp(bytes, db);
+            stream_wait(device, db);
+            set_device(db);
+            SBX_HIP_CHECK(hipMemcpyPeerAsync(tmp.ptr, db, slot, device, bytes, get_stream(db)));
+            local_piece_copy(alpha, src_c.dtype, tmp.ptr, p.size, Coor(src_c.nd(), 0), dst_c.dtype,
+                             dst_c.ptr[cb.idx], dst_c.ranges[cb.rank][cb.idx].size, p.dst_from,
+                             p.size, perm_s2d, add, db, nullptr, dst_c.mask_of(cb.idx));
+            stream_wait(db, device); // the receive buffer outlives the peer copy
+            set_device(device);
         }
     };
     if (deferred)

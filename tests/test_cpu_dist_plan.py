@@ -83,6 +83,21 @@ def _cases(nprocs):
     q1 = sb.basic_partitioning("cqab", [6, 2, 5, 4], [1, 1, 2 * nprocs, 1], "a", 2 * nprocs, 1)
     cases.append((q0, "abcd", [1, 0, 2, 1], [4, 4, 5, 1], [5, 4, 6, 3], 2, q1, "cqab",
                   [3, 1, 2, 0], [6, 2, 5, 4], 2, sb.Copy))
+    # several components per rank (the reference's --components=2, each on its own GPU): a
+    # field split over nprocs x 2 components into a domain partition with a one-site halo in x
+    # and y (the BSR halo exchange of the chain), and back with Add (the image-side sum)
+    dim = [8, 6, 2, 3]
+    pf = sb.basic_partitioning("xyzt", dim, [nprocs, 1, 1, 1], "xy", nprocs, 2)
+    ph = []
+    for f, sz in pf:
+        f, sz = list(f), list(sz)
+        for d in range(2):
+            if 0 < sz[d] and sz[d] + 2 <= dim[d]:
+                sz[d] += 2
+                f[d] = (f[d] - 1) % dim[d]
+        ph.append((f, sz))
+    cases.append((pf, "xyzt", [0] * 4, dim, dim, 2, ph, "xyzt", [0] * 4, dim, 2, sb.Copy))
+    cases.append((ph, "xyzt", [0] * 4, dim, dim, 2, pf, "xyzt", [0] * 4, dim, 2, sb.Add))
     return cases
 
 
