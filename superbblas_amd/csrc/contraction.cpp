@@ -275,6 +275,9 @@ void dist_contraction(const Scalar &alpha, const DistTensor &v0, const Coor &fro
         for (const DistTensor *t : {&v0, &v1, &vr}) h.add(*t);
         for (const Coor *c : {&from0, &size0, &from1, &size1, &fromr, &sizer}) h.add(*c);
         h.add((long)conj0 * 2 + (long)conj1);
+        // the tune key dist.reduce picks collective or point-to-point reductions and must be the
+        // same on every rank: a mismatch is caught here
+        h.add((long)g_dist_reduce);
         check_consistency(h, "contraction", comm);
     }
 

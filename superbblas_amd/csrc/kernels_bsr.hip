@@ -595,8 +595,17 @@ bool launch_bsr_mfma_dma(const BsrArgs &a, bool yrow, hipStream_t s) {
     const size_t lds = packed ? (size_t)4 * slot_packed * (PD + 1) : (size_t)4 * (NA + NX) * 1024 * (PD + 1);
     // 4 waves x (PD + 1) ring slots; a packed slot's last instruction is masked to the slot
     // (lanes past it are inactive), an unpacked slot is NA + NX whole 64-lane instructions
-    if (packed && !m3)
-        check_dma_lds("bsr_mfma_dma_kernel", lds, 4L * (PD + 1), 0, 4L * (PD + 1) * slot_packed);
+    if (packed && !m3) {
+        // the kernel's issue loop: PKN instructions per slot, lane l of instruction q writes the
+        // 16 bytes at q * 1024 + 16 l of the slot when that offset is below the slot size; so a
+        // slot's DMA writes min(PKN * 1024, slot rounded up to 16 bytes) bytes and must cover the
+        // slot's data, and the ring of 4 waves x (PD + 1) slots, slot_packed bytes apart, must fit
+        constexpr long PKN = CPLX && ES == 16 ? 5 : 3;
+        const long written = std::min(PKN * 1024, (slot_packed + 15) / 16 * 16);
+        if (PKN * 1024 < slot_packed || written > slot_packed)
+            throw Error("bsr: internal packed-slot sizing error in bsr_mfma_dma_kernel");
+        check_dma_lds("bsr_mfma_dma_kernel", lds, 0, 0, 4L * (PD + 1) * written);
+    }
     else
         check_dma_lds("bsr_mfma_dma_kernel", lds, 4L * (PD + 1) * (NA + NX), 64);
     g_bsr_tune.last = packed && !m3 ? 8 : 7;

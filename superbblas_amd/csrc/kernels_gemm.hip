@@ -333,8 +333,12 @@ template <bool XK, int R, int BKK, int NTH, int ES>
 struct DmaOperand {
     static constexpr int EPG = 16 / ES;          // elements per 16-B granule
     static constexpr int GR = BKK / EPG;         // granules per K-major row
-    static constexpr int NI = R * BKK / EPG / NTH; // DMA lanes per thread per slab
-    static_assert(NI * NTH * EPG == R * BKK && GR >= 1 && GR <= 16, "tile/threads mismatch");
+    static constexpr int GTOT = R * BKK / EPG;   // granules per slab image
+    static constexpr int NI = (GTOT + NTH - 1) / NTH; // DMA lanes per thread per slab
+    // a partial last pass is skipped by whole waves (a DMA instruction writes 64 lanes of LDS,
+    // out-of-range lanes included): the image must be a whole number of wave passes
+    static_assert(GTOT * EPG == R * BKK && GTOT % 64 == 0 && GR >= 1 && (!XK || GR <= 16),
+                  "tile/threads mismatch");
     unsigned roff[NI]; // byte offset of this lane's granule at k0 = 0
     int kl[NI];        // first k of the granule within the slab
     bool rok[NI];
@@ -369,6 +373,7 @@ struct DmaOperand {
                                           long s_k_hi = 0) const {
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
+            if (GTOT % NTH && i * NTH + wave * 64 >= GTOT) break; // (wave-uniform)
             const bool ok = rok[i] && (k0 + kl[i] < k_end);
             const unsigned kpart = split ? (unsigned)(split_off(k0 + kl[i], k_lo, s_k, s_k_hi) * ES)
                                          : (unsigned)(k0 * s_k * ES);
@@ -397,20 +402,31 @@ struct DmaOperand {
 // PF: the 4-multiplication path reads the fragments of k-step kk+4 from LDS before issuing the
 // MFMAs of k-step kk (a register double buffer), so a wave's LDS latency hides behind its own
 // MFMAs, not only behind the other wave of its SIMD
+// KG > 1: the workgroup's waves form KG groups of WM x WN; group g takes the k-steps g, g + KG,
+// ... of every slab (an intra-workgroup split-K: a 48x48 output in 4 waves of the whole tile, so
+// every SIMD of a CU gets the same share and each wave issues 36 MFMAs per 6 fragment reads); the
+// groups' partial tiles are summed through LDS in group order at the end (deterministic)
+// SH: every tile of the launch is a diagonal tile of a tensor contracted with itself (same_ab,
+// one tile row and column): the slab image holds A only, so the double buffer takes half the LDS
+// and twice the workgroups fit a CU
 template <typename R, bool CPLX, bool AK, bool BK, int BM, int BN, int BKK, int WM, int WN,
-          bool M3 = false, bool PF = false>
-__global__ void __launch_bounds__(WM *WN * 64) gemm_dma_kernel(const GemmKArgs p) {
+          bool M3 = false, bool PF = false, int KG = 1, bool SH = false>
+__global__ void __launch_bounds__(WM *WN *KG * 64) gemm_dma_kernel(const GemmKArgs p) {
     typedef typename Elem<R, CPLX>::type E;
     typedef typename Mfma<R>::acc_t acc_t;
     constexpr int ES = (int)sizeof(E);
-    constexpr int NTH = WM * WN * 64;
+    constexpr int NTH = WM * WN * KG * 64;
+    static_assert(KG == 1 || (!M3 && !PF && BKK % (4 * KG) == 0), "k-groups: 4M form only");
     constexpr int WTM = BM / WM, WTN = BN / WN;
     constexpr int MT = WTM / 16, NT = WTN / 16;
-    constexpr int SLAB = (BM + BN) * BKK; // elements per slab (A then B)
+    constexpr int SLAB = (BM + (SH ? 0 : BN)) * BKK; // elements per slab (A then B)
+    static_assert(!SH || (AK == BK && BM == BN), "shared image: A and B laid out alike");
     static_assert(MT * 16 == WTM && NT * 16 == WTN, "bad wave tile");
     typedef DmaOperand<AK, BM, BKK, NTH, ES> OpA;
     typedef DmaOperand<BK, BN, BKK, NTH, ES> OpB;
-    __shared__ __attribute__((aligned(16))) E lds[2 * SLAB]; // the only LDS object
+    // the double buffer, also the k-groups' reduction area at the end
+    constexpr int LDS_E = KG > 1 && BM * BN > 2 * SLAB ? BM * BN : 2 * SLAB;
+    __shared__ __attribute__((aligned(16))) E lds[LDS_E]; // the only LDS object
 
     const int nwg = gridDim.x, bid = blockIdx.x;
     const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
@@ -445,7 +461,8 @@ __global__ void __launch_bounds__(WM *WN * 64) gemm_dma_kernel(const GemmKArgs p
     da.init(tid, m0, p.m, p.sa_m, p.sa_k, spl, p.m_lo, p.sa_m_hi);
     db.init(tid, n0, p.n, p.sb_n, p.sb_k, spl, p.n_lo, p.sb_n_hi);
 
-    const int wm = wave / WN, wn = wave % WN;
+    const int kg = KG > 1 ? wave / (WM * WN) : 0, w2 = KG > 1 ? wave % (WM * WN) : wave;
+    const int wm = w2 / WN, wn = w2 % WN;
     const int frow = wm * WTM + (lane & 15), fcol = wn * WTN + (lane & 15), kq = lane >> 4;
     // conjugation: the imaginary parts' sign bit flipped with an integer xor (no FP64 multiply)
     typedef typename std::conditional<sizeof(R) == 8, unsigned long long, unsigned>::type U;
@@ -467,7 +484,7 @@ __global__ void __launch_bounds__(WM *WN * 64) gemm_dma_kernel(const GemmKArgs p
     const long nslab = (k_end - k_begin + BKK - 1) / BKK;
     const char *const base = (const char *)lds;
     constexpr bool CAN_SHARE = AK == BK && BM == BN; // same slab image layout for A and B
-    const bool share = CAN_SHARE && p.same_ab && m0 == n0;
+    const bool share = SH || (CAN_SHARE && p.same_ab && m0 == n0);
     if (nslab > 0) {
         da.issue(rsA, base, wave, k_begin, k_end, p.sa_k, spl, p.k_lo, p.sa_k_hi);
         if (!share)
@@ -522,7 +539,7 @@ __global__ void __launch_bounds__(WM *WN * 64) gemm_dma_kernel(const GemmKArgs p
             continue;
         }
 #pragma unroll
-        for (int kk = 0; kk < BKK; kk += 4) {
+        for (int kk = 4 * kg; kk < BKK; kk += 4 * KG) {
             E af[MT], bf[NT];
 #pragma unroll
             for (int i = 0; i < MT; ++i) af[i] = As[OpA::slot(frow + 16 * i, kk + kq)];
@@ -577,6 +594,47 @@ __global__ void __launch_bounds__(WM *WN * 64) gemm_dma_kernel(const GemmKArgs p
         }
     }
 
+    if constexpr (KG > 1) {
+        // sum the k-groups' partial tiles into group 0, one group at a time through the (now
+        // free) slab buffers, in group order
+        static_assert(BM * BN <= LDS_E, "k-group reduction: LDS too small");
+        E *red = lds;
+#pragma unroll
+        for (int g = 1; g < KG; ++g) {
+            __syncthreads(); // every wave is done with the slab buffers / the previous round
+            if (kg == g) {
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+#pragma unroll
+                    for (int j = 0; j < NT; ++j)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            E v;
+                            if constexpr (CPLX) v = E{accR[i][j][r], accI[i][j][r]};
+                            else v = accR[i][j][r];
+                            red[(((w2 * MT + i) * NT + j) * 4 + r) * 64 + lane] = v;
+                        }
+            }
+            __syncthreads();
+            if (kg == 0) {
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+#pragma unroll
+                    for (int j = 0; j < NT; ++j)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const E v = red[(((w2 * MT + i) * NT + j) * 4 + r) * 64 + lane];
+                            if constexpr (CPLX) {
+                                accR[i][j][r] += v.x;
+                                accI[i][j][r] += v.y;
+                            } else {
+                                accR[i][j][r] += v;
+                            }
+                        }
+            }
+        }
+        if (kg != 0) return;
+    }
     if (p.probe && bid == 0 && tid == 0) {
         const unsigned long long clk1 = __builtin_amdgcn_s_memtime();
         const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
@@ -611,6 +669,215 @@ __global__ void __launch_bounds__(WM *WN * 64) gemm_dma_kernel(const GemmKArgs p
                         *w = vr;
                 }
             }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Wave-private slabs, for a tensor contracted with itself with one output tile per batch entry
+// (same_ab, m = n <= BM: the chain's y^H y correlator, TSnsN with m = n = 48).  Every wave of the
+// workgroup owns the whole BM x BM tile over its own contiguous part of the workgroup's k-chunk
+// and stages that part by LDS-DMA into a RING-deep slab ring of its own (A only: B's fragments are
+// read from the same image), so the main loop has no barrier at all -- a wave waits only on its
+// own DMA (vmcnt) and its own LDS reads.  Round-4 measurement: a workgroup-wide slab with a
+// barrier per slab kept the MFMA pipe 67 % busy (every workgroup of a CU reaching its barrier and
+// DMA wait in lockstep).  The waves' partial tiles are summed through LDS in wave order at the end
+// (deterministic), then written like the other kernels (split-K partial or C).
+// ---------------------------------------------------------------------------------------------
+// FUSE: the split-K partials are summed by the last workgroup of each batch entry to finish
+// (an agent-scope counter per entry, zeroed before the launch): it adds the partials of all
+// splits in split order -- the same order and arithmetic as splitk_reduce_kernel, so the result
+// does not depend on which workgroup finishes last -- and writes C; no second kernel
+template <typename R, bool CPLX, bool AK, int BM, int BKK, int KG, int RING, bool FUSE = false>
+__global__ void __launch_bounds__(KG * 64) gemm_wave_kernel(const GemmKArgs p, unsigned *counters) {
+    typedef typename Elem<R, CPLX>::type E;
+    typedef typename Mfma<R>::acc_t acc_t;
+    constexpr int ES = (int)sizeof(E);
+    constexpr int MT = BM / 16;
+    static_assert(MT * 16 == BM && RING >= 2 && BKK % 4 == 0, "wave kernel shape");
+    typedef DmaOperand<AK, BM, BKK, 64, ES> Op;
+    constexpr int SLAB = BM * BKK;
+    constexpr int NI = Op::NI; // DMA instructions per slab
+    static_assert(NI * (RING - 1) <= 60, "vmcnt range");
+    constexpr int LDS_E = KG * RING * SLAB > BM * BM ? KG * RING * SLAB : BM * BM;
+    __shared__ __attribute__((aligned(16))) E lds[LDS_E];
+
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
+    const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+    const int split = wg % p.splits;
+    const long bb = wg / p.splits;
+    const long k_begin = (long)split * p.kchunk;
+    const long k_end = min(p.k, k_begin + p.kchunk);
+    const E *A = (const E *)p.a + bb * p.sa_b;
+    const __amdgpu_buffer_rsrc_t rsA =
+        __builtin_amdgcn_make_buffer_rsrc((void *)A, (short)0, (int)p.a_bytes, 0x00020000);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool spl = p.split != 0;
+    Op da;
+    da.init(lane, 0, p.m, p.sa_m, p.sa_k, spl, p.m_lo, p.sa_m_hi);
+    // this wave's slabs [s0, s1) of the workgroup's chunk
+    const long nsl = (k_end - k_begin + BKK - 1) / BKK;
+    const long per = (nsl + KG - 1) / KG;
+    const long s0 = min(nsl, (long)wave * per), s1 = min(nsl, s0 + per);
+    const char *const mine = (const char *)lds + (size_t)wave * RING * SLAB * ES;
+    auto issue = [&](long sl) {
+        da.issue(rsA, mine + (size_t)((sl - s0) % RING) * SLAB * ES, 0, k_begin + sl * BKK, k_end,
+                 p.sa_k, spl, p.k_lo, p.sa_k_hi);
+    };
+    typedef typename std::conditional<sizeof(R) == 8, unsigned long long, unsigned>::type U;
+    const U sign = (U)1 << (sizeof(R) * 8 - 1);
+    const U ma = p.conja ? sign : 0, mb = p.conjb ? sign : 0;
+    auto flip = [](R v, U m) { return __builtin_bit_cast(R, __builtin_bit_cast(U, v) ^ m); };
+    acc_t accR[MT][MT], accI[MT][MT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < MT; ++j) {
+            accR[i][j] = acc_t{0, 0, 0, 0};
+            accI[i][j] = acc_t{0, 0, 0, 0};
+        }
+    const int frow = lane & 15, kq = lane >> 4;
+#pragma unroll
+    for (int r = 0; r < RING - 1; ++r)
+        if (s0 + r < s1) issue(s0 + r);
+    for (long sl = s0; sl < s1; ++sl) {
+        const long sn = sl + RING - 1;
+        if (sn < s1) {
+            // the slot of slab sn was last read for slab sl - 1: those LDS reads have returned
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            issue(sn);
+        }
+        // slab sl landed: the DMA of the slabs issued after it may stay in flight
+        const long after = min((long)(RING - 1), s1 - 1 - sl);
+        if constexpr (RING >= 3) {
+            if (after >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NI) : "memory");
+            else if (after == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+            if (after >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        const E *As = (const E *)(mine + (size_t)((sl - s0) % RING) * SLAB * ES);
+#pragma unroll
+        for (int kk = 0; kk < BKK; kk += 4) {
+            E af[MT], bf[MT];
+#pragma unroll
+            for (int i = 0; i < MT; ++i) af[i] = As[Op::slot(frow + 16 * i, kk + kq)];
+#pragma unroll
+            for (int j = 0; j < MT; ++j) bf[j] = af[j]; // the same image: B's fragment = A's
+            if constexpr (CPLX) {
+#pragma unroll
+                for (int i = 0; i < MT; ++i) af[i].y = flip(af[i].y, ma);
+#pragma unroll
+                for (int j = 0; j < MT; ++j) bf[j].y = flip(bf[j].y, mb);
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+#pragma unroll
+                    for (int j = 0; j < MT; ++j) {
+                        accR[i][j] = Mfma<R>::mma(af[i].x, bf[j].x, accR[i][j]);
+                        accI[i][j] = Mfma<R>::mma(af[i].x, bf[j].y, accI[i][j]);
+                    }
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+#pragma unroll
+                    for (int j = 0; j < MT; ++j) {
+                        accR[i][j] = Mfma<R>::mma(-af[i].y, bf[j].y, accR[i][j]);
+                        accI[i][j] = Mfma<R>::mma(af[i].y, bf[j].x, accI[i][j]);
+                    }
+            } else {
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+#pragma unroll
+                    for (int j = 0; j < MT; ++j) accR[i][j] = Mfma<R>::mma(af[i], bf[j], accR[i][j]);
+            }
+        }
+    }
+    // the waves' partial tiles summed into wave 0, one wave at a time, in wave order
+    E *red = lds;
+#pragma unroll
+    for (int g = 1; g < KG; ++g) {
+        __syncthreads();
+        if (wave == g) {
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int j = 0; j < MT; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        E v;
+                        if constexpr (CPLX) v = E{accR[i][j][r], accI[i][j][r]};
+                        else v = accR[i][j][r];
+                        red[((i * MT + j) * 4 + r) * 64 + lane] = v;
+                    }
+        }
+        __syncthreads();
+        if (wave == 0) {
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int j = 0; j < MT; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const E v = red[((i * MT + j) * 4 + r) * 64 + lane];
+                        if constexpr (CPLX) {
+                            accR[i][j][r] += v.x;
+                            accI[i][j][r] += v.y;
+                        } else {
+                            accR[i][j][r] += v;
+                        }
+                    }
+        }
+    }
+    if (wave != 0) return;
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < MT; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const long gi = 16 * i + Mfma<R>::row(lane, r);
+                const long gj = 16 * j + frow;
+                if (gi >= p.m || gj >= p.n) continue;
+                const R vr = accR[i][j][r];
+                const R vi = CPLX ? accI[i][j][r] : R(0);
+                if (p.splits == 1) {
+                    R *cptr = (R *)((E *)p.c + bb * p.sc_b + c_off(p, gi, gj));
+                    epilogue_store<R>(cptr, vr, vi, p, CPLX);
+                } else {
+                    E *w = (E *)p.work + (((long)split * p.batch + bb) * p.n + gj) * p.m + gi;
+                    if constexpr (CPLX)
+                        *w = E{vr, vi};
+                    else
+                        *w = vr;
+                }
+            }
+    if constexpr (FUSE) {
+        if (p.splits == 1) return;
+        // publish this split's partial, count it; the last split of the entry sums them all
+        __threadfence();
+        unsigned old = 0;
+        if (lane == 0) old = atomicAdd(counters + bb, 1u);
+        old = __shfl(old, 0);
+        if (old != (unsigned)p.splits - 1) return;
+        __threadfence();
+        const long mn = p.m * p.n;
+        for (long e = lane; e < mn; e += 64) {
+            const long gi = e % p.m, gj = e / p.m;
+            const E *w = (const E *)p.work + (long)bb * mn + e;
+            R sr = 0, si = 0;
+            for (int sp = 0; sp < p.splits; ++sp) {
+                const E v = w[(long)sp * p.batch * mn];
+                if constexpr (CPLX) {
+                    sr += v.x;
+                    si += v.y;
+                } else {
+                    sr += v;
+                }
+            }
+            R *cptr = (R *)((E *)p.c + bb * p.sc_b + c_off(p, gi, gj));
+            epilogue_store<R>(cptr, sr, si, p, CPLX);
+        }
+    }
 }
 
 // C = alpha * sum_s W[s] + beta * C, summed in split order (deterministic)
@@ -739,7 +1006,7 @@ void launch_tiled_cfg(const GemmKArgs &p0, int device, hipStream_t stream, long 
 
 /// Launch one tile configuration of the LDS-DMA kernel
 template <typename R, bool CPLX, bool AK, bool BK, int BM, int BN, int BKK, int WM, int WN,
-          bool ALLOW_M3 = true, bool PF = false>
+          bool ALLOW_M3 = true, bool PF = false, int KG = 1, bool SH = false>
 void launch_dma_cfg(const GemmKArgs &p0, int device, hipStream_t stream, long splits = 0,
                     long target_wgs = 1024) {
     // complex: the 4-multiplication form unless the 3-multiplication form is asked for (config
@@ -754,6 +1021,8 @@ void launch_dma_cfg(const GemmKArgs &p0, int device, hipStream_t stream, long sp
                 p.sa_m_hi == p.sb_n_hi && p.sa_k_hi == p.sb_k_hi;
     const long nwg = prepare_launch<typename Elem<R, CPLX>::type>(p, BM, BN, BKK, splits,
                                                                    target_wgs, work, device);
+    if (SH && !(p.same_ab && p.tm == 1 && p.tn == 1))
+        throw Error("gemm: internal error, shared slab image for a launch with off-diagonal tiles");
     KernelTimer total("gemm_total", stream);
     {
         KernelTimer timer("gemm", stream);
@@ -765,11 +1034,37 @@ void launch_dma_cfg(const GemmKArgs &p0, int device, hipStream_t stream, long sp
                 hipLaunchKernelGGL((gemm_dma_kernel<R, CPLX, AK, BK, BM, BN, BKK, WM, WN>),
                                    dim3((unsigned)nwg), dim3(WM * WN * 64), 0, stream, p);
         } else
-            hipLaunchKernelGGL((gemm_dma_kernel<R, CPLX, AK, BK, BM, BN, BKK, WM, WN, false, PF>),
-                               dim3((unsigned)nwg), dim3(WM * WN * 64), 0, stream, p);
+            hipLaunchKernelGGL((gemm_dma_kernel<R, CPLX, AK, BK, BM, BN, BKK, WM, WN, false, PF, KG, SH>),
+                               dim3((unsigned)nwg), dim3(WM * WN * KG * 64), 0, stream, p);
         SBX_HIP_CHECK(hipGetLastError());
     }
     launch_reduce<R, CPLX>(p, stream);
+}
+
+/// Launch the wave-private-slab kernel (tensor contracted with itself, one tile per batch entry)
+template <typename R, bool CPLX, bool AK, int BM, int BKK, int KG, int RING, bool FUSE = false>
+void launch_wave_cfg(const GemmKArgs &p0, int device, hipStream_t stream, long target_wgs) {
+    GemmKArgs p = p0;
+    Scratch work;
+    long splits = g_gemm_tune.splits > 0 ? g_gemm_tune.splits : 0;
+    const long nwg = prepare_launch<typename Elem<R, CPLX>::type>(p, BM, BM, BKK * KG, splits,
+                                                                   target_wgs, work, device);
+    if (p.tm != 1 || p.tn != 1 || p.m != p.n)
+        throw Error("gemm: internal error, wave kernel for a launch with several tiles");
+    Scratch counters;
+    if (FUSE && p.splits > 1) {
+        counters = Scratch(sizeof(unsigned) * p.batch, device);
+        SBX_HIP_CHECK(hipMemsetAsync(counters.ptr, 0, sizeof(unsigned) * p.batch, stream));
+    }
+    KernelTimer total("gemm_total", stream);
+    {
+        KernelTimer timer("gemm", stream);
+        hipLaunchKernelGGL((gemm_wave_kernel<R, CPLX, AK, BM, BKK, KG, RING, FUSE>),
+                           dim3((unsigned)nwg), dim3(KG * 64), 0, stream, p,
+                           (unsigned *)counters.ptr);
+        SBX_HIP_CHECK(hipGetLastError());
+    }
+    if (!FUSE) launch_reduce<R, CPLX>(p, stream);
 }
 
 /// The LDS-DMA kernel reads whole 16-B granules: every granule must lie inside the operand
@@ -833,10 +1128,24 @@ void launch_tiled(const GemmKArgs &p, int device, hipStream_t stream) {
         // profiles/r02c_chain_splits.txt)
         const int t48 = g_gemm_tune.t48;
         if (t48 > 0 && p.m > 32 && p.m <= 48 && p.n > 32 && p.n <= 48) {
+            // (round-2 forms, kept for comparison runs)
             if (t48 == 1) return launch_dma_cfg<R, CPLX, AK, BK, 48, 48, 16, 3, 1>(p, device, stream, 0, 1024);
             if (t48 == 2) return launch_dma_cfg<R, CPLX, AK, BK, 48, 48, 16, 1, 3>(p, device, stream, 0, 1024);
             if (t48 == 3) return launch_dma_cfg<R, CPLX, AK, BK, 48, 48, 32, 3, 1>(p, device, stream, 0, 1024);
             if (t48 == 4) return launch_dma_cfg<R, CPLX, AK, BK, 48, 48, 16, 3, 1>(p, device, stream, 0, 1536);
+            // a tensor contracted with itself, one tile per batch entry (the chain's y^H y):
+            // wave-private slab rings, A-only images (tools/chain_contraction.py, round 4: 0.167 ->
+            // 0.142-0.146 ms warm against the t48 = 4 form, profiles/r04_chain_gemm.txt)
+            const bool sh = g_gemm_tune.share_ab && p.a == p.b && p.m == p.n && p.sa_m == p.sb_n &&
+                            p.sa_k == p.sb_k && p.sa_b == p.sb_b && p.m_lo == p.n_lo &&
+                            p.sa_m_hi == p.sb_n_hi && p.sa_k_hi == p.sb_k_hi;
+            if constexpr (!AK && !BK && sizeof(E) >= 8) {
+                if (sh && t48 == 14) return launch_wave_cfg<R, CPLX, AK, 48, 16, 4, 2>(p, device, stream, 768);
+                if (sh && t48 != 6) return launch_wave_cfg<R, CPLX, AK, 48, 8, 4, 2>(p, device, stream, 1024);
+            }
+            // otherwise four k-groups of whole 48x48 tiles per workgroup (one wave per SIMD each),
+            // 32-deep workgroup slabs: 0.167 -> 0.147-0.150 ms on the same shape unshared
+            return launch_dma_cfg<R, CPLX, AK, BK, 48, 48, 32, 1, 1, false, false, 4>(p, device, stream, 0, 768);
         }
         // 8-byte and 4-byte elements: 32-deep slabs (fewer barriers per MFMA; measured against
         // 16 and 64 on the lattice shape: double 50.5, complex<float> 116, float 107 TFLOP/s)

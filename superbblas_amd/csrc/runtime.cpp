@@ -188,7 +188,13 @@ long long max_cached(int device) {
             c.max_cached = (long long)(gib * 1073741824.0);
         } else {
             std::size_t fr = 0, total = 0;
-            if (hipMemGetInfo(&fr, &total) != hipSuccess) {
+            // (hipMemGetInfo reports the current device: make it `device`, then restore)
+            int prev = -1;
+            (void)hipGetDevice(&prev);
+            if (prev != device) (void)hipSetDevice(device);
+            const hipError_t e = hipMemGetInfo(&fr, &total);
+            if (prev != device && prev >= 0) (void)hipSetDevice(prev);
+            if (e != hipSuccess) {
                 (void)hipGetLastError();
                 total = 0;
             }
@@ -197,19 +203,28 @@ long long max_cached(int device) {
     }
     return c.max_cached;
 }
-/// Return the least recently freed blocks until the idle bytes are within the cap
-void trim_to_cap(int device) {
+/// Take the least recently freed blocks out of the cache until the idle bytes are within the cap
+/// (callers hold g_cache_mutex); the caller returns them to the driver with release_blocks after
+/// dropping the lock, so a small cap does not serialise every thread behind a host sync
+std::vector<Block> take_over_cap(int device) {
+    std::vector<Block> out;
     Cache &c = cache(device);
     const long long cap = max_cached(device);
     while ((long long)c.cached_bytes > cap && !c.free_blocks.empty()) {
         auto oldest = c.free_blocks.begin();
         for (auto it = c.free_blocks.begin(); it != c.free_blocks.end(); ++it)
             if (it->second.seq < oldest->second.seq) oldest = it;
-        Block b = oldest->second;
+        out.push_back(oldest->second);
+        c.cached_bytes -= oldest->second.bytes;
         c.free_blocks.erase(oldest);
-        c.cached_bytes -= b.bytes;
+    }
+    return out;
+}
+/// Return blocks taken out of the cache to the driver (without g_cache_mutex held)
+void release_blocks(const std::vector<Block> &blocks, int device) {
+    for (const Block &b : blocks) {
         if (b.ev) {
-            (void)hipEventSynchronize(b.ev);
+            (void)hipEventSynchronize(b.ev); // its last use is done
             (void)hipEventDestroy(b.ev);
         }
         device_free(b.p, device);
@@ -349,6 +364,8 @@ void scratch_free(void *p, int device) {
     if (!p) return;
     set_device(device);
     const hipStream_t s = get_stream(device);
+    std::vector<Block> evict;
+    {
     std::lock_guard<std::mutex> g(g_cache_mutex);
     Cache &c = cache(device);
     auto it = c.live.find(p);
@@ -365,7 +382,9 @@ void scratch_free(void *p, int device) {
     SBX_HIP_CHECK(hipEventRecord(b.ev, s));
     c.free_blocks.emplace(b.bytes, b);
     c.cached_bytes += b.bytes;
-    trim_to_cap(device);
+    evict = take_over_cap(device);
+    }
+    release_blocks(evict, device);
 }
 
 void alloc_tune(const char *key, long long *get, const long long *set) {

@@ -233,7 +233,10 @@ struct GemmTune {
                ///< 3-multiplication (Gauss) form, else the 4-multiplication form (the default: BLAS rounding)
     int splits = 0; ///< LDS-DMA kernel split-K factor (0 = the library's choice)
     long max_bytes = 0; ///< operand bytes per batch entry before a GEMM is cut (0 = 2^31 - 1)
-    int t48 = 4; ///< 4- and 8-byte elements, 33..48 rows and columns: 48x48 tiles (0 = off; 1..4 shapes)
+    int t48 = 5; ///< 4- and 8-byte elements, 33..48 rows and columns: 48x48 tiles (0 = off; 1..4 the
+                 ///< round-2 forms; 6 k-group workgroups; 14 wave rings of 16-deep slabs; any other
+                 ///< value the library's choice: wave rings of 8-deep slabs for a tensor
+                 ///< contracted with itself, else k-group workgroups)
     int share_ab = 1; ///< LDS-DMA kernel: one slab image for A and B when they are the same memory (0 = off)
 };
 extern GemmTune g_gemm_tune;

@@ -86,10 +86,11 @@ def test_gemm_granule_shapes(gpu, dtype, ta, tb, m, n, k):
 @pytest.mark.parametrize("dtype", [np.complex128, np.float64, np.complex64, np.float32])
 @pytest.mark.parametrize("ta,tb", [("T", "N"), ("N", "N"), ("N", "T"), ("C", "N"), ("T", "C")])
 @pytest.mark.parametrize("m,n,k,batch", [(48, 48, 768, 3), (34, 46, 520, 2), (48, 40, 4096, 1)])
-@pytest.mark.parametrize("t48", [1, 2, 3, 4])
+@pytest.mark.parametrize("t48", [1, 2, 3, 4, 5, 6])
 def test_gemm_48_tiles(gpu, dtype, ta, tb, m, n, k, batch, t48):
     """33..48 rows and columns: the 48x48 LDS-DMA tile forms (sbx_tune_set "gemm.t48"; the
-    chain's TSnsN contraction shape), with split-K over the long k"""
+    chain's TSnsN contraction shape), with split-K over the long k; 5 = the library's choice, 6
+    = four k-groups of the whole tile per workgroup"""
     import superbblas_amd as sb
     old = sb.tune_get("gemm.t48")
     sb.tune_set("gemm.t48", t48)
@@ -125,3 +126,39 @@ def test_gemm_same_operand(gpu, dtype, m, k):
                 k * m, 0.0, ref, m, m * m, batch)
     assert np.array_equal(outs[0], outs[1])
     assert rel_err(outs[0], ref) < TOL[dtype]
+
+
+@pytest.mark.parametrize("dtype", [np.complex128, np.complex64, np.float64])
+@pytest.mark.parametrize("m,k,batch", [(48, 3072, 3), (40, 1000, 2), (48, 96, 5), (36, 24, 1)])
+@pytest.mark.parametrize("tb", ["T", "C"])
+@pytest.mark.parametrize("t48", [5, 14])
+def test_gemm_same_operand_mmajor(gpu, dtype, m, k, batch, tb, t48):
+    """A op(A) with one M-major buffer as both operands and one output tile per batch entry (the
+    chain's y^H y shape): the wave-private slab-ring kernel (A-only slab images, no barrier in the
+    main loop; partial k ranges summed through LDS), against the oracle and the unshared form
+    (within rounding: the k order of the two forms differs), with ragged k and m < 48"""
+    import torch
+    import superbblas_amd as sb
+    if tb == "C" and np.dtype(dtype).kind != "c":
+        tb = "T"
+    a = random_valued(k * m * batch, dtype, 7)
+    ta = torch.from_numpy(a).to(gpu)
+    outs = []
+    old = sb.tune_get("gemm.t48")
+    sb.tune_set("gemm.t48", t48)
+    try:
+        for share in (1, 0):
+            sb.tune_set("gemm.share_ab", share)
+            c = torch.zeros(m * m * batch, dtype=ta.dtype, device=gpu)
+            sb.xgemm_batch_strided("N", tb, m, m, k, 0.5 - 0.5j if np.dtype(dtype).kind == "c"
+                                   else 0.5, ta, m, k * m, ta, m, k * m, 0.0, c, m, m * m, batch)
+            torch.cuda.synchronize()
+            outs.append(c.cpu().numpy())
+    finally:
+        sb.tune_set("gemm.share_ab", 1)
+        sb.tune_set("gemm.t48", old)
+    ref = np.zeros(m * m * batch, dtype)
+    oracle_gemm("N", tb, m, m, k, 0.5 - 0.5j if np.dtype(dtype).kind == "c" else 0.5, a, m, k * m,
+                a, m, k * m, 0.0, ref, m, m * m, batch)
+    assert rel_err(outs[0], ref) < TOL[dtype]
+    assert rel_err(outs[1], ref) < TOL[dtype]
