@@ -12,8 +12,8 @@ reuse distance changes.  Not part of the product.
 
 Printed per case and rhs count: kernel time (library timers, median of 3 rounds of 20
 launches), the stencil's algorithmic bytes / time as a fraction of 8 TB/s, and the bytes the
-case must move beyond L2 at the least (values + y + indices + x once).  With PMC=1 nothing else
-runs (for rocprofv3 --pmc passes)."""
+case must move beyond L2 at the least (values + y + indices + x once).  BLK=12 / DT=cf: the
+12x12-block (spin 4 x color 3) operator, complex<float>."""
 import json
 import os
 import statistics
@@ -54,19 +54,25 @@ def main():
     V = L ** 4
     kinds = os.environ.get("KINDS", "stencil,local,self,one").split(",")
     ncols_list = [int(v) for v in os.environ.get("NCOLS", "12,64").split(",")]
-    dim = [L, L, L, L, 1, 3]
+    # BLK=12: spin 4 x color 3 blocks (config 3's secondary shape / the chain's operator);
+    # DT=cf: complex<float>
+    spin = 4 if os.environ.get("BLK", "3") == "12" else 1
+    dt = torch.complex64 if os.environ.get("DT", "cd") == "cf" else torch.complex128
+    es = 8 if dt == torch.complex64 else 16
+    b = 3 * spin
+    dim = [L, L, L, L, spin, 3]
     full = [([0] * 6, dim)]
-    blk = [1, 1, 1, 1, 1, 3]
+    blk = [1, 1, 1, 1, spin, 3]
     for kind in kinds:
         jj, nnz = columns(kind, L)
-        vals = torch.randn(V * nnz * 9, dtype=torch.complex128, device=dev)
+        vals = torch.randn(V * nnz * b * b, dtype=dt, device=dev)
         op = sb.create_bsr(full, dim, full, dim, blk, blk, False,
                            [torch.full((V,), nnz, dtype=torch.int32, device=dev)],
                            [torch.from_numpy(jj.reshape(-1)).to(dev)], [vals])
         for n in ncols_list:
-            dx = [1, L, L, L, L, 1, 3, n]
+            dx = [1, L, L, L, L, spin, 3, n]
             px = [([0] * 8, dx)]
-            x = torch.randn(V * 3 * n, dtype=torch.complex128, device=dev)
+            x = torch.randn(V * b * n, dtype=dt, device=dev)
             y = torch.empty_like(x)
 
             def f():
@@ -86,9 +92,10 @@ def main():
                 sb.timings_enable(False)
                 ts.append(ms / calls / 1e3)
             t = statistics.median(ts)
-            algo = 16.0 * (81 * V + 2 * 3 * V * n) + 4.0 * (9 * V + V + 1)  # the stencil's bytes
-            floor = 16.0 * (nnz * 9 * V + 2 * 3 * V * n) + 4.0 * (nnz * V + V + 1)
-            print(json.dumps({"kind": kind, "ncols": n, "us": round(t * 1e6, 1),
+            algo = es * (9 * b * b * V + 2 * b * V * n) + 4.0 * (9 * V + V + 1)  # the stencil's
+            floor = es * (nnz * b * b * V + 2 * b * V * n) + 4.0 * (nnz * V + V + 1)
+            print(json.dumps({"blk": b, "dtype": str(dt), "kind": kind, "ncols": n,
+                              "us": round(t * 1e6, 1),
                               "kernel": sb.tune_get("bsr.last_kernel"),
                               "stencil_bytes_frac_hbm": round(algo / t / 8e12, 4),
                               "min_bytes_MB": round(floor / 1e6, 1),
