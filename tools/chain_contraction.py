@@ -17,8 +17,10 @@ import superbblas_amd as sb  # noqa: E402
 def main():
     dev = torch.device("cuda:0")
     Ls, Lt, s_, c_, n = 16, 64, 4, 3, 12
-    dx = [1, Ls, Ls, Ls, Lt, s_, c_, n]
-    y = torch.randn(Ls ** 3 * Lt * s_ * c_ * n, dtype=torch.complex64, device=dev)
+    Lz = int(os.environ.get("LZ", Ls))  # (LZ: a shorter z extent, i.e. a shorter k, for the
+    dx = [1, Ls, Ls, Lz, Lt, s_, c_, n]  # fixed-cost / per-k split of the launch time)
+    V3 = Ls * Ls * Lz
+    y = torch.randn(V3 * Lt * s_ * c_ * n, dtype=torch.complex64, device=dev)
     # DATA=zero / int: operands that switch fewer MFMA bits (a power / clock diagnostic)
     data = os.environ.get("DATA", "rand")
     if data == "zero":
@@ -29,9 +31,9 @@ def main():
     dr = [Lt, s_, n, s_, n]
     vr = torch.empty(Lt * s_ * n * s_ * n, dtype=torch.complex64, device=dev)
     p_x, p_r = [([0] * 8, dx)], [([0] * 5, dr)]
-    yv = y.view(Ls ** 3, Lt, s_, c_, n)
+    yv = y.view(V3, Lt, s_, c_, n)
     ref = torch.einsum("XTSCn,XTsCN->TSnsN", yv.conj(), yv).reshape(-1)
-    fl = 8.0 * vr.numel() * Ls ** 3 * c_
+    fl = 8.0 * vr.numel() * V3 * c_
     combos = [(int(v), 1) for v in os.environ.get("T48", "0,1,2,3,4").split(",")]
     if os.environ.get("SHARE"):  # one slab image for both operands (the same memory) on / off
         combos = [(4, int(v)) for v in os.environ["SHARE"].split(",")] * 2
@@ -55,7 +57,7 @@ def main():
         e.record()
         torch.cuda.synchronize()
         t = s.elapsed_time(e) / 10 / 1e3
-        print(json.dumps({"data": data, "t48": t48, "share_ab": share, "splits": nsplit, "ms": round(t * 1e3, 4),
+        print(json.dumps({"k": V3 * c_, "data": data, "t48": t48, "share_ab": share, "splits": nsplit, "ms": round(t * 1e3, 4),
                           "TFLOPs": round(fl / t / 1e12, 2),
                           "rel_err_vs_einsum": err}), flush=True)
     sb.tune_set("gemm.t48", 5)
