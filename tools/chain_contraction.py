@@ -47,7 +47,8 @@ def main():
         def f():
             sb.contraction(1.0, p_x, [0] * 8, dx, dx, "pXYZTSCn", True, [y], p_x, [0] * 8, dx, dx,
                            "pXYZTsCN", False, [y], 0.0, p_r, [0] * 5, dr, dr, "TSnsN", [vr])
-        f()
+        for _ in range(int(os.environ.get("WARM", "1"))):  # (WARM: clocks up before timing)
+            f()
         torch.cuda.synchronize()
         err = (torch.linalg.vector_norm(vr - ref) / max(torch.linalg.vector_norm(ref), 1e-30)).item()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
