@@ -54,7 +54,7 @@ def test_dist_host_staged_grid4(gpu):
     _run(4, "host", cases="golden")
 
 
-@pytest.mark.parametrize("nprocs", [2, 3])
+@pytest.mark.parametrize("nprocs", [2, 3, 4])
 def test_dist_rccl(gpu, nprocs):
     import torch
     _run(nprocs, "rccl", shared=torch.cuda.device_count() < nprocs)
