@@ -697,7 +697,9 @@ __global__ void __launch_bounds__(KG * 64) gemm_wave_kernel(const GemmKArgs p, u
     constexpr int SLAB = BM * BKK;
     constexpr int NI = Op::NI; // DMA instructions per slab
     static_assert(NI * (RING - 1) <= 60, "vmcnt range");
-    constexpr int LDS_E = KG * RING * SLAB > BM * BM ? KG * RING * SLAB : BM * BM;
+    // the rings; at the end, the KG / 2 partial tiles of the first round of the tree sum
+    constexpr int RED_E = (KG / 2 > 1 ? KG / 2 : 1) * BM * BM;
+    constexpr int LDS_E = KG * RING * SLAB > RED_E ? KG * RING * SLAB : RED_E;
     __shared__ __attribute__((aligned(16))) E lds[LDS_E];
 
     const int nwg = gridDim.x, bid = blockIdx.x;
@@ -792,12 +794,13 @@ __global__ void __launch_bounds__(KG * 64) gemm_wave_kernel(const GemmKArgs p, u
             }
         }
     }
-    // the waves' partial tiles summed into wave 0, one wave at a time, in wave order
-    E *red = lds;
+    // the waves' partial tiles summed into wave 0 by a fixed binary tree (wave w + step into wave
+    // w at each level), so the order, and the result, do not depend on timing
 #pragma unroll
-    for (int g = 1; g < KG; ++g) {
+    for (int step = 1; step < KG; step *= 2) {
         __syncthreads();
-        if (wave == g) {
+        E *red = lds + (size_t)(wave / (2 * step)) * BM * BM;
+        if (wave % (2 * step) == step) {
 #pragma unroll
             for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -811,7 +814,7 @@ __global__ void __launch_bounds__(KG * 64) gemm_wave_kernel(const GemmKArgs p, u
                     }
         }
         __syncthreads();
-        if (wave == 0) {
+        if (wave % (2 * step) == 0) {
 #pragma unroll
             for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -1141,6 +1144,10 @@ void launch_tiled(const GemmKArgs &p, int device, hipStream_t stream) {
                             p.sa_m_hi == p.sb_n_hi && p.sa_k_hi == p.sb_k_hi;
             if constexpr (!AK && !BK && sizeof(E) >= 8) {
                 if (sh && t48 == 14) return launch_wave_cfg<R, CPLX, AK, 48, 16, 4, 2>(p, device, stream, 768);
+                // more waves per workgroup, fewer split-K partials to write and sum
+                if (sh && t48 == 15) return launch_wave_cfg<R, CPLX, AK, 48, 8, 8, 2>(p, device, stream, 512);
+                if (sh && t48 == 16) return launch_wave_cfg<R, CPLX, AK, 48, 8, 16, 2>(p, device, stream, 256);
+                if (sh && t48 == 17) return launch_wave_cfg<R, CPLX, AK, 48, 16, 8, 2>(p, device, stream, 512);
                 if (sh && t48 != 6) return launch_wave_cfg<R, CPLX, AK, 48, 8, 4, 2>(p, device, stream, 1024);
             }
             // otherwise four k-groups of whole 48x48 tiles per workgroup (one wave per SIMD each),
