@@ -120,6 +120,13 @@ int sbx_timings_report(char *buf, int len);
    "copy.last_pair", "dist.reduce_calls", "alloc.cross_stream_frees".  Unknown keys fail with an
    error. */
 int sbx_tune_set(const char *key, long long value);
+/* The box-copy kernel the library's planner picks for an N-d box copy (sizes and element strides
+   of both sides, element types, Copy/Add, masked): *kind 0 masked, 1 contiguous, 2 direct
+   gather, 3 LDS tile, 4 site-block transpose, 5 block transpose, -1 empty box; *blocks its grid.
+   Host only (no GPU work): lets the planner be tested on machines without a GPU. */
+int sbx_copy_kernel_plan(int nd, const long long *size, const long long *src_stride,
+                         const long long *dst_stride, int t0, int t1, int add, int masked,
+                         int *kind, long long *blocks);
 int sbx_tune_get(const char *key, long long *value);
 
 /* ---- communicator (replaces MPI; dist.h:1426-1773 send_receive) ---- */

@@ -562,6 +562,30 @@ int sbx_comm_rank(sbx_comm comm, int *rank, int *nprocs) {
     });
 }
 
+int sbx_copy_kernel_plan(int nd, const long long *size, const long long *src_stride,
+                         const long long *dst_stride, int t0, int t1, int add, int masked,
+                         int *kind, long long *blocks) {
+    return guard([&] {
+        check_copy_types(t0, t1);
+        BoxCopyDesc d{};
+        d.src_t = t0;
+        d.dst_t = t1;
+        d.add = add != 0;
+        static const float mask_token = 1;
+        if (masked) d.src_mask = d.dst_mask = &mask_token; // (only the presence matters here)
+        for (int i = 0; i < nd; ++i) {
+            if (size[i] < 0 || src_stride[i] < 0 || dst_stride[i] < 0)
+                throw Error("copy_kernel_plan: negative size or stride");
+            d.size.push_back((long)size[i]);
+            d.src_stride.push_back((long)src_stride[i]);
+            d.dst_stride.push_back((long)dst_stride[i]);
+        }
+        long b = 0;
+        *kind = copy_kernel_plan(d, &b);
+        if (blocks) *blocks = b;
+    });
+}
+
 int sbx_comm_transport(sbx_comm comm, int *kind, int *count, int *user_rank) {
     return guard([&] {
         const Comm c = get_comm(comm);

@@ -1669,6 +1669,15 @@ void launch_box_copy(const BoxCopyDesc &d, int device) {
     l.run(l, d.src, d.dst, alpha, d.src_mask, d.dst_mask, s);
 }
 
+int copy_kernel_plan(const BoxCopyDesc &d, long *blocks) {
+    long total = 1;
+    for (long x : d.size) total *= x;
+    if (total == 0) return -1;
+    const CopyLaunch l = prepare_launch(d, total);
+    if (blocks) *blocks = l.blocks;
+    return (int)l.kind;
+}
+
 void launch_zero(void *p, std::size_t bytes, int device) {
     if (bytes == 0) return;
     set_device(device);

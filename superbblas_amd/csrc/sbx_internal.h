@@ -183,6 +183,10 @@ struct BoxCopyDesc {
 void launch_box_copy(const BoxCopyDesc &d, int device);
 /// Drop the prepared box-copy launches (clearCaches)
 void clear_copy_launch_cache();
+/// The box-copy kernel the planner picks for a box (no GPU work; tests of the host planner):
+/// 0 masked, 1 contiguous, 2 direct gather, 3 LDS tile, 4 site-block transpose, 5 block
+/// transpose (-1: empty box); *blocks = its grid size
+int copy_kernel_plan(const BoxCopyDesc &d, long *blocks);
 
 /// Launch tape of one copy() call: the box-copy launches it issued, so that a later call of the
 /// same shape on other pointers replays them without planning (the C ABI's copy fast path;
