@@ -84,9 +84,9 @@ def test_lattice_permutations_every_kernel():
 
 @pytest.mark.timeout(120)
 def test_random_layouts_fuzz():
-    """Random boxes (1-6 dims, sizes 1-69 and powers of two, with degenerate ones, packed or padded layouts in
-    random dimension orders, every type pair and Copy/Add): the planner returns a kernel and a
-    positive grid for each, within the test's time limit."""
+    """Random boxes (1-6 dims, sizes 1-69 and powers of two, degenerate ones included, packed or
+    padded layouts in random dimension orders, every type pair and Copy/Add): the planner
+    returns a kernel and a positive grid for each, within the test's time limit."""
     rng = np.random.default_rng(20261017)
     counts = {}
     for it in range(20000):
