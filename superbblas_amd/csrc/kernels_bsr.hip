@@ -41,6 +41,7 @@ struct BsrArgs {
     double alpha_re, alpha_im;
     int add;
     int ilv = 1; // bsr_ell9_kernel: an XCD's chunks visited as ilv interleaved parts
+    int nt = 0;  // the value stream's LDS-DMA loads non-temporal: g_bsr_tune.nt's kernel bits
 };
 
 template <typename E, int BI_, int BD_, bool YROW, bool XROW>
@@ -209,15 +210,24 @@ __device__ __forceinline__ unsigned lds_u32(const void *p) {
     return (unsigned)(size_t)(const __attribute__((address_space(3))) void *)p;
 }
 
-__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, unsigned off, unsigned dst) {
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, unsigned off, unsigned dst, int nt = 0) {
     // inline asm: hipcc does not order its ds_reads against an LDS-DMA it cannot see; the kernel
-    // retires the DMA with an explicit vmcnt(0) before its barrier
-    asm volatile("s_mov_b32 m0, %1\n\t"
-                 "s_nop 0\n\t"
-                 "buffer_load_dwordx4 %0, %2, 0 offen lds"
-                 :
-                 : "v"(off), "s"(dst), "s"(rs)
-                 : "memory", "m0");
+    // retires the DMA with an explicit vmcnt(0) before its barrier.  nt (a uniform kernel
+    // argument, so a scalar branch): the streaming policy for data read once (the values)
+    if (nt)
+        asm volatile("s_mov_b32 m0, %1\n\t"
+                     "s_nop 0\n\t"
+                     "buffer_load_dwordx4 %0, %2, 0 offen nt lds"
+                     :
+                     : "v"(off), "s"(dst), "s"(rs)
+                     : "memory", "m0");
+    else
+        asm volatile("s_mov_b32 m0, %1\n\t"
+                     "s_nop 0\n\t"
+                     "buffer_load_dwordx4 %0, %2, 0 offen lds"
+                     :
+                     : "v"(off), "s"(dst), "s"(rs)
+                     : "memory", "m0");
 }
 
 template <typename R, bool CPLX> struct BsrMfmaElem;
@@ -488,12 +498,21 @@ __global__ void __launch_bounds__(256) bsr_mfma_dma_kernel(const BsrArgs p, unsi
                 const unsigned g = (unsigned)(lane + 64 * q) * 16u;
                 if (g < SLOT) {
                     const char *src = g < (unsigned)(ABLK * ES) ? vrow + g : xrow + (g - ABLK * ES);
-                    asm volatile("s_mov_b32 m0, %1\n\t"
-                                 "s_nop 0\n\t"
-                                 "global_load_lds_dwordx4 %0, off"
-                                 :
-                                 : "v"(src), "s"(__builtin_amdgcn_readfirstlane(base + (unsigned)q * 1024u))
-                                 : "memory", "m0");
+                    // nt on the instructions that carry values only (x rows are reused)
+                    if ((p.nt & 1) && (q + 1) * 1024 <= ABLK * ES)
+                        asm volatile("s_mov_b32 m0, %1\n\t"
+                                     "s_nop 0\n\t"
+                                     "global_load_lds_dwordx4 %0, off nt"
+                                     :
+                                     : "v"(src), "s"(__builtin_amdgcn_readfirstlane(base + (unsigned)q * 1024u))
+                                     : "memory", "m0");
+                    else
+                        asm volatile("s_mov_b32 m0, %1\n\t"
+                                     "s_nop 0\n\t"
+                                     "global_load_lds_dwordx4 %0, off"
+                                     :
+                                     : "v"(src), "s"(__builtin_amdgcn_readfirstlane(base + (unsigned)q * 1024u))
+                                     : "memory", "m0");
                 }
             }
         } else {
@@ -501,7 +520,7 @@ __global__ void __launch_bounds__(256) bsr_mfma_dma_kernel(const BsrArgs p, unsi
 #pragma unroll
             for (int q = 0; q < NA; ++q) {
                 const unsigned g = (unsigned)(lane + 64 * q) * 16u;
-                dma16(rv, g < (unsigned)(ABLK * ES) ? av + g : 0x80000000u, base + (unsigned)q * 1024u);
+                dma16(rv, g < (unsigned)(ABLK * ES) ? av + g : 0x80000000u, base + (unsigned)q * 1024u, p.nt & 1);
             }
 #pragma unroll
             for (int q = 0; q < NX; ++q) {
@@ -733,7 +752,7 @@ __global__ void __launch_bounds__(NT) bsr_ell9_kernel(const BsrArgs p, int rb) {
         for (int u = 0; u * NT < nv; ++u) {
             const int e = u * NT + (int)threadIdx.x;
             const unsigned off = e < nv ? (unsigned)((vbase + e) * 16) : 0x80000000u;
-            dma16(rs, off, __builtin_amdgcn_readfirstlane(base + (unsigned)(u * NT) * 16u));
+            dma16(rs, off, __builtin_amdgcn_readfirstlane(base + (unsigned)(u * NT) * 16u), p.nt & 2);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
@@ -861,7 +880,7 @@ __global__ void __launch_bounds__(256) bsr_ell9_row_kernel(const BsrArgs p, unsi
         for (int u = 0; u < (NV + 255) / 256; ++u) {
             const unsigned e = (unsigned)(u * 256 + tid);
             const unsigned off = e < (unsigned)NV ? v0 + e * 16u : 0x80000000u;
-            dma16(rs, off, __builtin_amdgcn_readfirstlane(base + (unsigned)u * 4096u));
+            dma16(rs, off, __builtin_amdgcn_readfirstlane(base + (unsigned)u * 4096u), p.nt & 8);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -1017,7 +1036,7 @@ __global__ void __launch_bounds__(512) bsr_ell9_split_kernel(const BsrArgs p, co
         for (int u = 0; u * nth < nv; ++u) {
             const int e = u * nth + tid;
             const unsigned off = e < nv ? v0 + (unsigned)e * 16u : 0x80000000u;
-            dma16(rs, off, __builtin_amdgcn_readfirstlane(base + (unsigned)(u * nth) * 16u));
+            dma16(rs, off, __builtin_amdgcn_readfirstlane(base + (unsigned)(u * nth) * 16u), p.nt & 4);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -1280,6 +1299,7 @@ void launch_bsr(const BsrDesc &d, int device) {
     a.alpha_im = d.alpha.im;
     a.add = d.add ? 1 : 0;
     a.ilv = 2; // an XCD's row chunks visited as two interleaved halves (bsr_ell9_kernel)
+    a.nt = g_bsr_tune.nt;
     switch (d.t) {
     case SBX_CDOUBLE: return launch_typed<double2>(a, d.num_nnz_per_row, d.y_row_major, d.x_row_major, s);
     case SBX_CFLOAT: return launch_typed<float2>(a, d.num_nnz_per_row, d.y_row_major, d.x_row_major, s);

@@ -258,6 +258,9 @@ struct BsrTune {
                                 ///< matrix cores (bsr_kron_mfma_kernel) ...
     long kron_mfma_min_cols = 8; ///< ... from this many rhs columns
     int kron_pack = 1;           ///< ... below 16 rhs columns: a wave's 16 column slots span several rows (0 = off)
+    int nt = 0; ///< the value stream's LDS-DMA loads with the non-temporal (streaming) policy, per
+                ///< kernel: 1 12x12 blocks by LDS-DMA, 2 3x3 row chunks, 4 3x3 split rows, 8 3x3 one
+                ///< thread per block
     /// read-back ("bsr.last_kernel"; atomic: launches may come from several host threads): the form
     /// of the last launch -- 1 one thread per block (3x3), 2 split rows (3x3), 3 row chunks (3x3),
     /// 5 Kronecker on MFMA, 6 the same with packed column slots, 7 12x12 blocks by LDS-DMA, 8 the
