@@ -1143,12 +1143,15 @@ void launch_tiled(const GemmKArgs &p, int device, hipStream_t stream) {
                             p.sa_k == p.sb_k && p.sa_b == p.sb_b && p.m_lo == p.n_lo &&
                             p.sa_m_hi == p.sb_n_hi && p.sa_k_hi == p.sb_k_hi;
             if constexpr (!AK && !BK && sizeof(E) >= 8) {
+                // (comparison forms: 13 four waves per workgroup, 1024 workgroups; 14 the same with
+                // 16-deep slabs; 16 sixteen waves, 256 workgroups)
+                if (sh && t48 == 13) return launch_wave_cfg<R, CPLX, AK, 48, 8, 4, 2>(p, device, stream, 1024);
                 if (sh && t48 == 14) return launch_wave_cfg<R, CPLX, AK, 48, 16, 4, 2>(p, device, stream, 768);
-                // more waves per workgroup, fewer split-K partials to write and sum
-                if (sh && t48 == 15) return launch_wave_cfg<R, CPLX, AK, 48, 8, 8, 2>(p, device, stream, 512);
                 if (sh && t48 == 16) return launch_wave_cfg<R, CPLX, AK, 48, 8, 16, 2>(p, device, stream, 256);
-                if (sh && t48 == 17) return launch_wave_cfg<R, CPLX, AK, 48, 16, 8, 2>(p, device, stream, 512);
-                if (sh && t48 != 6) return launch_wave_cfg<R, CPLX, AK, 48, 8, 4, 2>(p, device, stream, 1024);
+                // eight waves per workgroup, 512 workgroups: half the split-K partials of the
+                // four-wave form to write and sum (their per-wave tiles summed through LDS first):
+                // 0.138-0.139 -> 0.136-0.137 ms warm, interleaved (profiles/r04_chain_gemm.txt)
+                if (sh && t48 != 6) return launch_wave_cfg<R, CPLX, AK, 48, 8, 8, 2>(p, device, stream, 512);
             }
             // otherwise four k-groups of whole 48x48 tiles per workgroup (one wave per SIMD each),
             // 32-deep workgroup slabs: 0.167 -> 0.147-0.150 ms on the same shape unshared

@@ -238,9 +238,10 @@ struct GemmTune {
     int splits = 0; ///< LDS-DMA kernel split-K factor (0 = the library's choice)
     long max_bytes = 0; ///< operand bytes per batch entry before a GEMM is cut (0 = 2^31 - 1)
     int t48 = 5; ///< 4- and 8-byte elements, 33..48 rows and columns: 48x48 tiles (0 = off; 1..4 the
-                 ///< round-2 forms; 6 k-group workgroups; 14 wave rings of 16-deep slabs; any other
-                 ///< value the library's choice: wave rings of 8-deep slabs for a tensor
-                 ///< contracted with itself, else k-group workgroups)
+                 ///< round-2 forms; 6 k-group workgroups; 13 / 14 / 16 wave rings of 4 waves
+                 ///< 8-deep, 4 waves 16-deep, 16 waves 8-deep; any other value the library's
+                 ///< choice: wave rings of 8 waves, 8-deep slabs, for a tensor contracted with
+                 ///< itself, else k-group workgroups)
     int share_ab = 1; ///< LDS-DMA kernel: one slab image for A and B when they are the same memory (0 = off)
 };
 extern GemmTune g_gemm_tune;
@@ -258,9 +259,11 @@ struct BsrTune {
                                 ///< matrix cores (bsr_kron_mfma_kernel) ...
     long kron_mfma_min_cols = 8; ///< ... from this many rhs columns
     int kron_pack = 1;           ///< ... below 16 rhs columns: a wave's 16 column slots span several rows (0 = off)
-    int nt = 0; ///< the value stream's LDS-DMA loads with the non-temporal (streaming) policy, per
+    int nt = 11; ///< the value stream's LDS-DMA loads with the non-temporal (streaming) policy, per
                 ///< kernel: 1 12x12 blocks by LDS-DMA, 2 3x3 row chunks, 4 3x3 split rows, 8 3x3 one
-                ///< thread per block
+                ///< thread per block.  Default 1 | 2 | 8 (tools/bsr_bound.py NTS, warm, interleaved:
+                ///< 12x12 complex<double> 340 -> 328 us, complex<float> 179 -> 168 us, 3x3 n = 64
+                ///< 161 -> 158 us, n = 1 19.0 -> 18.2 us; the split-row kernel 34.4 -> 42.5 us: off)
     /// read-back ("bsr.last_kernel"; atomic: launches may come from several host threads): the form
     /// of the last launch -- 1 one thread per block (3x3), 2 split rows (3x3), 3 row chunks (3x3),
     /// 5 Kronecker on MFMA, 6 the same with packed column slots, 7 12x12 blocks by LDS-DMA, 8 the

@@ -131,7 +131,7 @@ def test_gemm_same_operand(gpu, dtype, m, k):
 @pytest.mark.parametrize("dtype", [np.complex128, np.complex64, np.float64])
 @pytest.mark.parametrize("m,k,batch", [(48, 3072, 3), (40, 1000, 2), (48, 96, 5), (36, 24, 1)])
 @pytest.mark.parametrize("tb", ["T", "C"])
-@pytest.mark.parametrize("t48", [5, 14])
+@pytest.mark.parametrize("t48", [5, 13, 14, 16])
 def test_gemm_same_operand_mmajor(gpu, dtype, m, k, batch, tb, t48):
     """A op(A) with one M-major buffer as both operands and one output tile per batch entry (the
     chain's y^H y shape): the wave-private slab-ring kernel (A-only slab images, no barrier in the

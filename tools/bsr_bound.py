@@ -55,7 +55,7 @@ def main():
     V = L ** 4
     kinds = os.environ.get("KINDS", "stencil,local,self,one").split(",")
     ncols_list = [int(v) for v in os.environ.get("NCOLS", "12,64").split(",")]
-    nts = [int(v) for v in os.environ.get("NTS", "0").split(",")]
+    nts = [int(v) for v in os.environ.get("NTS", str(sb.tune_get("bsr.nt"))).split(",")]
     # BLK=12: spin 4 x color 3 blocks (config 3's secondary shape / the chain's operator);
     # DT=cf: complex<float>
     spin = 4 if os.environ.get("BLK", "3") == "12" else 1

@@ -2,7 +2,8 @@
 """The configs[4] chain's contraction alone (16^3 x 64 sites, complex<float>, n = 12:
 pXYZTSCn (conj) x pXYZTsCN -> TSnsN, a batched GEMM with m = n = 48, k = 12 288, batch 64) by
 GEMM tile shape (sbx_tune_set "gemm.t48": 0 = 64x64 tiles, 1..4 = the round-2 48x48 forms, 5 =
-the library's choice, 6 = k-group workgroups, 14 = wave rings of 16-deep slabs); results
+the library's choice, 6 = k-group workgroups, 13 / 14 / 16 = wave rings of 4 waves 8-deep, 4 waves
+16-deep, 16 waves 8-deep; the default is 8 waves 8-deep); results
 compared with torch.einsum.  Not part of the product."""
 import json
 import os
