@@ -392,8 +392,16 @@ __global__ void __launch_bounds__(256) bsr_kron_mfma_kernel(const KronArgs p, in
 // idles (at n = 12 one wave per row left 4 of 16 slots empty: 25 % of the VALU and MFMA work).
 // The row's block columns and color blocks become per-lane (LDS reads of the staged color blocks,
 // block columns loaded per lane); the spin matrices stay the MFMA's A operand.
-template <int NNZ, bool kpf = false>
-__global__ void __launch_bounds__(256) bsr_kron_mfma_packed_kernel(const KronArgs p, int rw) {
+// XL: the neighbours' x pieces staged by LDS-DMA instead of VGPR loads.  The MFMA's B operand
+// wants lane 16 b + q = spin b of slot q, but spin is the fastest index of x in memory, so a
+// 16-lane quarter of such a load touches 16 pieces 64 B apart (8 cache lines; 32 TA/TCP accesses
+// per 1-KB instruction against 8 for a linear one, and TA/TD busy 85-92 %).  The DMA instead
+// moves each slot's 4 spins as one 64-B piece (lane l: slot l / 4), writes them lane-linear into
+// the wave's ring (one neighbour ahead, 3 KB per neighbour), and the B lanes read them back with
+// the spins rotated by the slot's quarter (position 4 q + (b + q / 4) mod 4), which puts a read
+// quarter's 16 lanes on 16 different bank groups.
+template <int NNZ, bool kpf = false, bool XL = false>
+__global__ void __launch_bounds__(256) bsr_kron_mfma_packed_kernel(const KronArgs p, int rw, int xring) {
     typedef double2 E;
     const E *__restrict__ x = (const E *)p.x;
     E *__restrict__ y = (E *)p.y;
@@ -450,7 +458,38 @@ __global__ void __launch_bounds__(256) bsr_kron_mfma_packed_kernel(const KronArg
         for (int d = 0; d < 3; ++d) xv[d] = xs[d * n * 4];
     };
     E xa[3], xb[3];
-    load_x(jrow[0], xa);
+    // XL: the DMA lane's piece (slot lane / 4, spin rotated back) and its slot's block columns
+    int jd[XL ? NNZ : 1];
+    unsigned xoff_d = 0, xring_w = 0;
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, 0x7fffffff, 0x00020000);
+    if constexpr (XL) {
+        const int qd = lane >> 2, bd = ((lane & 3) - (qd >> 2)) & 3;
+        const int sd = w * 16 + qd, rld = sd / (int)n;
+        const long cold = sd - (long)rld * n;
+        const long rd = r0 + (rld < nrows ? rld : nrows - 1);
+#pragma unroll
+        for (int mu = 0; mu < NNZ; ++mu) jd[mu] = p.jj[rd * NNZ + mu];
+        xoff_d = (unsigned)(cold * 4 + bd) * 16u;
+        xring_w = (unsigned)xring + (unsigned)w * 6144u;
+    }
+    const unsigned lds0 = (unsigned)(size_t)(const __attribute__((address_space(3))) void *)smem_k;
+    auto issue_x = [&](int mu) {
+        const unsigned base = lds0 + xring_w + (unsigned)(mu & 1) * 3072u;
+        const unsigned o = (unsigned)((long)jd[mu] * xsite) * 16u + xoff_d;
+#pragma unroll
+        for (int d = 0; d < 3; ++d)
+            asm volatile("s_mov_b32 m0, %1\n\t"
+                         "s_nop 0\n\t"
+                         "buffer_load_dwordx4 %0, %2, 0 offen lds"
+                         :
+                         : "v"(o + (unsigned)(d * n * 4) * 16u),
+                           "s"(__builtin_amdgcn_readfirstlane(base + (unsigned)d * 1024u)), "s"(rx)
+                         : "memory", "m0");
+    };
+    // the B lane's position in a ring slot
+    const int xpos = 4 * q + ((b + (q >> 2)) & 3);
+    if constexpr (XL) issue_x(0);
+    else load_x(jrow[0], xa);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const E *urow_s = us + rlc * NNZ * 9;
@@ -463,7 +502,22 @@ __global__ void __launch_bounds__(256) bsr_kron_mfma_packed_kernel(const KronArg
     for (int mu = 0; mu < NNZ; ++mu) {
         if constexpr (kpf) asm volatile("" ::: "memory");
         E Kn = Kc;
-        if (mu + 1 < NNZ) {
+        if constexpr (XL) {
+            // the ring slot of neighbour mu + 1 was read in iteration mu - 1: those reads are done
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (mu + 1 < NNZ) {
+                issue_x(mu + 1);
+                if constexpr (kpf) Kn = kron[(mu + 1) * 16 + kidx];
+                // neighbour mu landed: at most its successor's 3 DMAs and spin load in flight
+                if constexpr (kpf) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            const E *xs = (const E *)(smem_k + xring_w + (mu & 1) * 3072);
+#pragma unroll
+            for (int d = 0; d < 3; ++d) xa[d] = xs[d * 64 + xpos];
+        } else if (mu + 1 < NNZ) {
             load_x(jrow[mu + 1], xb);
             if constexpr (kpf) Kn = kron[(mu + 1) * 16 + kidx];
         }
@@ -486,7 +540,7 @@ __global__ void __launch_bounds__(256) bsr_kron_mfma_packed_kernel(const KronArg
             accI[i] = __builtin_amdgcn_mfma_f64_4x4x4f64(K.x, t[i].y, accI[i], 0, 0, 0);
             accI[i] = __builtin_amdgcn_mfma_f64_4x4x4f64(K.y, t[i].x, accI[i], 0, 0, 0);
         }
-        if (mu + 1 < NNZ) {
+        if (!XL && mu + 1 < NNZ) {
 #pragma unroll
             for (int d = 0; d < 3; ++d) xa[d] = xb[d];
         }
@@ -525,14 +579,23 @@ template <typename E> void launch_kron_typed(const KronArgs &a, hipStream_t s) {
                     // LDS: rw rows of 81 color values, rounded up to whole DMA passes of the
                     // workgroup (the lanes past the run write zeros)
                     const int nth = 64 * wpk;
-                    const size_t lds_bytes = (size_t)((rw * 81 + nth - 1) / nth * nth) * 16;
+                    const size_t lds_cb = (size_t)((rw * 81 + nth - 1) / nth * nth) * 16;
                     // the DMA loop: passes u < ceil(nrows * 81 / nth), nrows <= rw
-                    check_dma_lds("bsr_kron_mfma_packed_kernel", lds_bytes, (rw * 81L + nth - 1) / nth, nth);
+                    check_dma_lds("bsr_kron_mfma_packed_kernel", lds_cb, (rw * 81L + nth - 1) / nth, nth);
+                    // x by LDS-DMA: a ring of 2 x 3 KB per wave after the color blocks (lds_cb is
+                    // a multiple of 16); 32-bit buffer offsets
+                    const bool xl = g_bsr_tune.kron_xlds && a.block_rows * 12L * a.ncols * 16 < (1L << 31);
+                    const size_t lds_bytes = lds_cb + (xl ? (size_t)wpk * 6144 : 0);
+                    if (xl) check_dma_lds("bsr_kron_mfma_packed_kernel x ring", lds_bytes, 0, 0, (long)lds_cb + wpk * 6144L);
                     // spin matrices one neighbour ahead: n = 8 / 12 104 / 166 -> 102 / 163 us
                     // (the one-row-per-wave kernel: 214 -> 221 us at n = 16, so not there;
                     // profiles/r02c_kron_kpf.txt)
-                    hipLaunchKernelGGL((bsr_kron_mfma_packed_kernel<9, true>), dim3((unsigned)blocks),
-                                       dim3(64 * wpk), lds_bytes, s, a, rw);
+                    if (xl)
+                        hipLaunchKernelGGL((bsr_kron_mfma_packed_kernel<9, true, true>), dim3((unsigned)blocks),
+                                           dim3(64 * wpk), lds_bytes, s, a, rw, (int)lds_cb);
+                    else
+                        hipLaunchKernelGGL((bsr_kron_mfma_packed_kernel<9, true>), dim3((unsigned)blocks),
+                                           dim3(64 * wpk), lds_bytes, s, a, rw, (int)lds_cb);
                     SBX_HIP_CHECK(hipGetLastError());
                     return;
                 }

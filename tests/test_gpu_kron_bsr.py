@@ -166,16 +166,17 @@ def test_kron_errors(gpu):
                            [t(kron)])
 
 
-@pytest.mark.parametrize("ncols", [8, 12, 16, 17, 40])
+@pytest.mark.parametrize("ncols,L", [(8, 4), (12, 4), (12, 3), (16, 4), (17, 4), (40, 4)])
 @pytest.mark.parametrize("bif,sparse", [(False, False), (True, True)])
-def test_kron_mfma_kernel(gpu, ncols, bif, sparse):
+def test_kron_mfma_kernel(gpu, ncols, L, bif, sparse):
     """complex<double> 3x3 x 4x4 from 8 rhs columns: the spin products on the matrix cores
     (bsr_kron_mfma_kernel; 16-column groups, partial last group; bsr_kron_mfma_packed_kernel at 8
-    and 12 columns: a wave's 16 column slots over several rows), complex alpha, beta, powers;
-    integer data, exact; and the same results with either switched off."""
+    and 12 columns: a wave's 16 column slots over several rows, x staged by LDS-DMA or loaded
+    per lane; 3^4 sites: a last workgroup with fewer rows than its slots), complex alpha, beta,
+    powers; integer data, exact; and the same results with each form switched off."""
     import torch
     import superbblas_amd as sb
-    L, spin, color, power = 4, 4, 3, 2
+    spin, color, power = 4, 3, 2
     ii, jj, vals, kron = kron_lattice(L, spin, color, sparse_kron=sparse)
     V = L ** 4
     n = V * color * ncols * spin
@@ -195,9 +196,10 @@ def test_kron_mfma_kernel(gpu, ncols, bif, sparse):
     outs = []
     try:
         # packed column slots (8 and 12 columns: several rows per wave), one row per wave, no MFMA
-        for on, pack in ((1, 1), (1, 0), (0, 1)):
+        for on, pack, xl in ((1, 1, 1), (1, 1, 0), (1, 0, 1), (0, 1, 1)):
             sb.tune_set("bsr.kron_mfma", on)
             sb.tune_set("bsr.kron_pack", pack)
+            sb.tune_set("bsr.kron_xlds", xl)
             ty = torch.from_numpy(y0.copy()).to(gpu)
             sb.bsr_krylov(alpha, op, "xyztsc", "XYZTSC", [([0] * 8, dimx)], "pXYZTCnS", [0] * 8,
                           dimx, dimx, [torch.from_numpy(x).to(gpu)], beta, [([0] * 8, dimy)],
@@ -207,8 +209,10 @@ def test_kron_mfma_kernel(gpu, ncols, bif, sparse):
     finally:
         sb.tune_set("bsr.kron_mfma", 1)
         sb.tune_set("bsr.kron_pack", 1)
+        sb.tune_set("bsr.kron_xlds", 1)
         op.destroy()
-    assert outs[0][0] == (6 if ncols in (8, 12) else 5) and outs[1][0] == 5 and outs[2][0] not in (5, 6)
+    packed = 6 if ncols in (8, 12) else 5
+    assert [o[0] for o in outs[:3]] == [packed, packed, 5] and outs[3][0] not in (5, 6)
     for form, out in outs:
         assert np.array_equal(out, ref), form
 

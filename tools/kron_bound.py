@@ -2,8 +2,9 @@
 """Bound model of the Kronecker BSR kernel (bench `kron_n12`: 16^4, 3x3 color blocks x 4x4 spin
 matrices, complex<double>): the same kernel and launch on operators that differ only in where
 the nine block columns of a row point (tools/bsr_bound.py's kinds: stencil, local, self, one),
-so the value, y and gather streams stay fixed while the x reuse distance changes.  Not part of
-the product."""
+so the value, y and gather streams stay fixed while the x reuse distance changes.  XLS=1,0: the
+bsr.kron_xlds settings to compare (x staged by LDS-DMA or loaded per lane).  Not part of the
+product."""
 import json
 import os
 import statistics
@@ -35,6 +36,7 @@ def main():
     V = L ** 4
     kinds = os.environ.get("KINDS", "stencil,local,self,one").split(",")
     ncols_list = [int(v) for v in os.environ.get("NCOLS", "12").split(",")]
+    xls = [int(v) for v in os.environ.get("XLS", str(sb.tune_get("bsr.kron_xlds"))).split(",")]
     dims = [L, L, L, L]
     dim = dims + [4, 3]
     full = [([0] * 6, dim)]
@@ -47,7 +49,8 @@ def main():
         op = sb.create_kron_bsr(full, dim, full, dim, blk, blk, kr, kr, False,
                                 [torch.full((V,), nnz, dtype=torch.int32, device=dev)],
                                 [torch.from_numpy(jj.reshape(-1)).to(dev)], [cvals], [kron])
-        for n in ncols_list:
+        for n, xl in [(n, xl) for n in ncols_list for xl in xls]:
+            sb.tune_set("bsr.kron_xlds", xl)
             dimx = [1] + dims + [3, n, 4]
             px = [([0] * 8, dimx)]
             x = torch.randn(V * 12 * n, dtype=torch.complex128, device=dev)
@@ -72,7 +75,7 @@ def main():
             t = statistics.median(ts)
             algo = 16.0 * (81 * V + 2 * 12 * V * n) + 4.0 * 9 * V  # the stencil's
             floor = 16.0 * (nnz * 9 * V + 2 * 12 * V * n) + 4.0 * nnz * V
-            print(json.dumps({"kind": kind, "ncols": n, "us": round(t * 1e6, 1),
+            print(json.dumps({"kind": kind, "ncols": n, "xlds": xl, "us": round(t * 1e6, 1),
                               "kernel": sb.tune_get("bsr.last_kernel"),
                               "stencil_bytes_frac_hbm": round(algo / t / 8e12, 4),
                               "min_bytes_MB": round(floor / 1e6, 1),
@@ -80,6 +83,7 @@ def main():
             del x, y
         op.destroy()
         del cvals
+    sb.tune_set("bsr.kron_xlds", xls[0])
 
 
 if __name__ == "__main__":
