@@ -270,7 +270,8 @@ __global__ void __launch_bounds__(256) bsr_kron_generic_kernel(const KronArgs p)
 //    an XCD's rows visited as two interleaved halves (its ilv form of the 3x3 kernels).
 // The previous kernel (one thread per (row, column) owning all 12 outputs) ran at 256 VGPRs:
 // 2 waves per SIMD.
-template <int NNZ, bool kpf = false>
+// XL: x staged by LDS-DMA in whole 64-B spin pieces (see bsr_kron_mfma_packed_kernel)
+template <int NNZ, bool kpf = false, bool XL = false>
 __global__ void __launch_bounds__(256) bsr_kron_mfma_kernel(const KronArgs p, int ngroups) {
     typedef double2 E;
     const E *__restrict__ x = (const E *)p.x;
@@ -337,7 +338,30 @@ __global__ void __launch_bounds__(256) bsr_kron_mfma_kernel(const KronArgs p, in
     };
     double accR[3] = {0, 0, 0}, accI[3] = {0, 0, 0};
     E xa[3], xb[3];
-    load_x(jrow[0], xa);
+    // XL: a ring of 2 neighbours x 3 KB per wave; the DMA lane's piece: column lane / 4 of the
+    // group, its spins rotated by the column's quarter
+    __shared__ __attribute__((aligned(16))) E xr[XL ? 4 * 2 * 3 * 64 : 1];
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, 0x7fffffff, 0x00020000);
+    const int qd = lane >> 2, bd = ((lane & 3) - (qd >> 2)) & 3;
+    const long cold = min((long)cg * 16 + qd, n - 1);
+    const unsigned xoff_d = (unsigned)(cold * 4 + bd) * 16u;
+    const unsigned ring = (unsigned)(size_t)(const __attribute__((address_space(3))) void *)xr + (unsigned)w * 6144u;
+    auto issue_x = [&](int mu) {
+        const unsigned base = ring + (unsigned)(mu & 1) * 3072u;
+        const unsigned o = (unsigned)((long)jrow[mu] * xsite) * 16u + xoff_d;
+#pragma unroll
+        for (int d = 0; d < 3; ++d)
+            asm volatile("s_mov_b32 m0, %1\n\t"
+                         "s_nop 0\n\t"
+                         "buffer_load_dwordx4 %0, %2, 0 offen lds"
+                         :
+                         : "v"(o + (unsigned)(d * n * 4) * 16u),
+                           "s"(__builtin_amdgcn_readfirstlane(base + (unsigned)d * 1024u)), "s"(rx)
+                         : "memory", "m0");
+    };
+    const int xpos = 4 * q + ((b + (q >> 2)) & 3);
+    if constexpr (XL) issue_x(0);
+    else load_x(jrow[0], xa);
     // the spin matrix of neighbour mu + 1 is loaded with its x rows; the compiler barrier keeps
     // the unrolled loop from hoisting all 9 spin-matrix loads to the top (36 more VGPRs: fewer
     // waves per SIMD)
@@ -346,7 +370,22 @@ __global__ void __launch_bounds__(256) bsr_kron_mfma_kernel(const KronArgs p, in
     for (int mu = 0; mu < NNZ; ++mu) {
         if constexpr (kpf) asm volatile("" ::: "memory");
         E Kn = Kc;
-        if (mu + 1 < NNZ) {
+        if constexpr (XL) {
+            // the ring slot of neighbour mu + 1 was read in iteration mu - 1: those reads are done
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (mu + 1 < NNZ) {
+                issue_x(mu + 1);
+                if constexpr (kpf) Kn = kron[(mu + 1) * 16 + kidx];
+                // neighbour mu landed: at most its successor's DMAs (and spin load) in flight
+                if constexpr (kpf) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            const E *xs = xr + w * 384 + (mu & 1) * 192;
+#pragma unroll
+            for (int d = 0; d < 3; ++d) xa[d] = xs[d * 64 + xpos];
+        } else if (mu + 1 < NNZ) {
             load_x(jrow[mu + 1], xb);
             if constexpr (kpf) Kn = kron[(mu + 1) * 16 + kidx];
         }
@@ -371,7 +410,7 @@ __global__ void __launch_bounds__(256) bsr_kron_mfma_kernel(const KronArgs p, in
             accI[i] = __builtin_amdgcn_mfma_f64_4x4x4f64(K.x, t[i].y, accI[i], 0, 0, 0);
             accI[i] = __builtin_amdgcn_mfma_f64_4x4x4f64(K.y, t[i].x, accI[i], 0, 0, 0);
         }
-        if (mu + 1 < NNZ) {
+        if (!XL && mu + 1 < NNZ) {
 #pragma unroll
             for (int d = 0; d < 3; ++d) xa[d] = xb[d];
         }
@@ -604,8 +643,13 @@ template <typename E> void launch_kron_typed(const KronArgs &a, hipStream_t s) {
             const long tasks = a.block_rows * ngroups, blocks = (tasks + 3) / 4;
             if (blocks < (1L << 31)) {
                 g_bsr_tune.last = 5;
-                hipLaunchKernelGGL((bsr_kron_mfma_kernel<9, false>), dim3((unsigned)blocks), dim3(256), 0,
-                                   s, a, (int)ngroups);
+                // x by LDS-DMA (32-bit buffer offsets)
+                if (g_bsr_tune.kron_xlds && a.block_rows * 12L * a.ncols * 16 < (1L << 31))
+                    hipLaunchKernelGGL((bsr_kron_mfma_kernel<9, false, true>), dim3((unsigned)blocks), dim3(256),
+                                       0, s, a, (int)ngroups);
+                else
+                    hipLaunchKernelGGL((bsr_kron_mfma_kernel<9, false>), dim3((unsigned)blocks), dim3(256), 0,
+                                       s, a, (int)ngroups);
                 SBX_HIP_CHECK(hipGetLastError());
                 return;
             }
