@@ -33,6 +33,7 @@ struct KronArgs {
     long ncols;
     double alpha_re, alpha_im;
     int add;
+    int ylds; ///< the XL kernels: y written through the wave's LDS ring in whole 64-B spin pieces
 };
 
 template <typename E, int BI, int BD, int KI, int KD>
@@ -415,6 +416,27 @@ __global__ void __launch_bounds__(256) bsr_kron_mfma_kernel(const KronArgs p, in
             for (int d = 0; d < 3; ++d) xa[d] = xb[d];
         }
     }
+    if constexpr (XL) {
+        if (p.ylds) {
+            // C lane 16 a + q -> ring position 4 q + (a + q / 4) mod 4; lane l stores column l / 4
+            E *ys = xr + w * 384;
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+                ys[i * 64 + xpos] = Ops<E>::scale(E{accR[i], accI[i]}, p.alpha_re, p.alpha_im);
+            asm volatile("" ::: "memory");
+            const long cs = (long)cg * 16 + qd;
+            if (cs >= n) return;
+            const int ad = bd;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                E *yp = y + ((r * 3 + i) * n + cs) * 4 + ad;
+                E o = ys[i * 64 + lane];
+                if (p.add) o = Ops<E>::add(o, *yp);
+                *yp = o;
+            }
+            return;
+        }
+    }
     if (!ok) return;
     // C lane 16 a + q: spin a of column q
 #pragma unroll
@@ -584,6 +606,29 @@ __global__ void __launch_bounds__(256) bsr_kron_mfma_packed_kernel(const KronArg
             for (int d = 0; d < 3; ++d) xa[d] = xb[d];
         }
     }
+    if constexpr (XL) {
+        if (p.ylds) {
+            // C lane 16 a + q -> ring position 4 q + (a + q / 4) mod 4 (the B read's map); then
+            // lane l stores the piece of slot l / 4: each slot's 4 spins one 64-B run
+            E *ys = (E *)(smem_k + xring_w);
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+                ys[i * 64 + xpos] = Ops<E>::scale(E{accR[i], accI[i]}, p.alpha_re, p.alpha_im);
+            asm volatile("" ::: "memory");
+            const int qd = lane >> 2, ad = ((lane & 3) - (qd >> 2)) & 3;
+            const int sd = w * 16 + qd, rld = sd / (int)n;
+            if (rld >= nrows) return;
+            const long cold = sd - (long)rld * n;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                E *yp = y + (((r0 + rld) * 3 + i) * n + cold) * 4 + ad;
+                E o = ys[i * 64 + lane];
+                if (p.add) o = Ops<E>::add(o, *yp);
+                *yp = o;
+            }
+            return;
+        }
+    }
     if (!live) return;
     // C lane 16 a + q: spin a of slot q
 #pragma unroll
@@ -700,6 +745,7 @@ void launch_bsr_kron(const BsrDesc &d, int device) {
     a.alpha_re = d.alpha.re;
     a.alpha_im = d.alpha.im;
     a.add = d.add ? 1 : 0;
+    a.ylds = g_bsr_tune.kron_xlds >= 2 ? 1 : 0;
     switch (d.t) {
     case SBX_CDOUBLE: return launch_kron_typed<double2>(a, s);
     case SBX_CFLOAT: return launch_kron_typed<float2>(a, s);

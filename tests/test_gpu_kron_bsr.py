@@ -172,7 +172,8 @@ def test_kron_mfma_kernel(gpu, ncols, L, bif, sparse):
     """complex<double> 3x3 x 4x4 from 8 rhs columns: the spin products on the matrix cores
     (bsr_kron_mfma_kernel; 16-column groups, partial last group; bsr_kron_mfma_packed_kernel at 8
     and 12 columns: a wave's 16 column slots over several rows, x staged by LDS-DMA or loaded
-    per lane; 3^4 sites: a last workgroup with fewer rows than its slots), complex alpha, beta,
+    per lane, y written per lane or through the same ring; 3^4 sites: a last workgroup with
+    fewer rows than its slots), complex alpha, beta,
     powers; integer data, exact; and the same results with each form switched off."""
     import torch
     import superbblas_amd as sb
@@ -196,7 +197,7 @@ def test_kron_mfma_kernel(gpu, ncols, L, bif, sparse):
     outs = []
     try:
         # packed column slots (8 and 12 columns: several rows per wave), one row per wave, no MFMA
-        for on, pack, xl in ((1, 1, 1), (1, 1, 0), (1, 0, 1), (0, 1, 1)):
+        for on, pack, xl in ((1, 1, 1), (1, 1, 2), (1, 1, 0), (1, 0, 2), (1, 0, 0), (0, 1, 1)):
             sb.tune_set("bsr.kron_mfma", on)
             sb.tune_set("bsr.kron_pack", pack)
             sb.tune_set("bsr.kron_xlds", xl)
@@ -212,7 +213,7 @@ def test_kron_mfma_kernel(gpu, ncols, L, bif, sparse):
         sb.tune_set("bsr.kron_xlds", 1)
         op.destroy()
     packed = 6 if ncols in (8, 12) else 5
-    assert [o[0] for o in outs[:3]] == [packed, packed, 5] and outs[3][0] not in (5, 6)
+    assert [o[0] for o in outs[:5]] == [packed] * 3 + [5, 5] and outs[5][0] not in (5, 6)
     for form, out in outs:
         assert np.array_equal(out, ref), form
 

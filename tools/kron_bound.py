@@ -2,8 +2,8 @@
 """Bound model of the Kronecker BSR kernel (bench `kron_n12`: 16^4, 3x3 color blocks x 4x4 spin
 matrices, complex<double>): the same kernel and launch on operators that differ only in where
 the nine block columns of a row point (tools/bsr_bound.py's kinds: stencil, local, self, one),
-so the value, y and gather streams stay fixed while the x reuse distance changes.  XLS=1,0: the
-bsr.kron_xlds settings to compare (x staged by LDS-DMA or loaded per lane).  Not part of the
+so the value, y and gather streams stay fixed while the x reuse distance changes.  XLS=2,1,0: the
+bsr.kron_xlds settings to compare (x staged by LDS-DMA, y too, or both per lane).  Not part of the
 product."""
 import json
 import os
