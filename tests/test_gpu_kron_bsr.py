@@ -195,6 +195,7 @@ def test_kron_mfma_kernel(gpu, ncols, L, bif, sparse):
     dimx = [1, L, L, L, L, color, ncols, spin]
     dimy = [power] + dimx[1:]
     outs = []
+    old_xl = sb.tune_get("bsr.kron_xlds")
     try:
         # packed column slots (8 and 12 columns: several rows per wave), one row per wave, no MFMA
         for on, pack, xl in ((1, 1, 1), (1, 1, 2), (1, 1, 0), (1, 0, 2), (1, 0, 0), (0, 1, 1)):
@@ -210,7 +211,7 @@ def test_kron_mfma_kernel(gpu, ncols, L, bif, sparse):
     finally:
         sb.tune_set("bsr.kron_mfma", 1)
         sb.tune_set("bsr.kron_pack", 1)
-        sb.tune_set("bsr.kron_xlds", 1)
+        sb.tune_set("bsr.kron_xlds", old_xl)
         op.destroy()
     packed = 6 if ncols in (8, 12) else 5
     assert [o[0] for o in outs[:5]] == [packed] * 3 + [5, 5] and outs[5][0] not in (5, 6)
