@@ -423,6 +423,7 @@ int sbx_tune_set(const char *key, long long value) {
         else if (k == "bsr.kron_mfma_min_cols") g_bsr_tune.kron_mfma_min_cols = (long)value;
         else if (k == "bsr.kron_pack") g_bsr_tune.kron_pack = (int)value;
         else if (k == "bsr.kron_xlds") g_bsr_tune.kron_xlds = (int)value;
+        else if (k == "bsr.kron_ylds") g_bsr_tune.kron_ylds = (int)value;
         else if (k == "bsr.nt") g_bsr_tune.nt = (int)value;
         else if (k == "gemm.m3") g_gemm_tune.m3 = (int)value;
         else if (k == "gemm.splits") g_gemm_tune.splits = (int)value;
@@ -466,6 +467,7 @@ int sbx_tune_get(const char *key, long long *value) {
         else if (k == "bsr.kron_mfma_min_cols") *value = g_bsr_tune.kron_mfma_min_cols;
         else if (k == "bsr.kron_pack") *value = g_bsr_tune.kron_pack;
         else if (k == "bsr.kron_xlds") *value = g_bsr_tune.kron_xlds;
+        else if (k == "bsr.kron_ylds") *value = g_bsr_tune.kron_ylds;
         else if (k == "bsr.nt") *value = g_bsr_tune.nt;
         else if (k == "bsr.last_kernel") *value = g_bsr_tune.last;
         else if (k == "gemm.m3") *value = g_gemm_tune.m3;

@@ -98,6 +98,23 @@ __global__ void __launch_bounds__(256) bsr_kron_kernel(const KronArgs p) {
     }
 }
 
+/// s_waitcnt vmcnt(n) for an n the unrolled caller knows at compile time (folds to one wait)
+__device__ __forceinline__ void wait_vmcnt(int n) {
+    switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    }
+}
+
 /// Wave-uniform element load through the constant address space (scalar loads into SGPRs)
 template <typename R> using ConstPtr = const __attribute__((address_space(4))) R *;
 template <typename E> struct Uniform {
@@ -271,8 +288,9 @@ __global__ void __launch_bounds__(256) bsr_kron_generic_kernel(const KronArgs p)
 //    an XCD's rows visited as two interleaved halves (its ilv form of the 3x3 kernels).
 // The previous kernel (one thread per (row, column) owning all 12 outputs) ran at 256 VGPRs:
 // 2 waves per SIMD.
-// XL: x staged by LDS-DMA in whole 64-B spin pieces (see bsr_kron_mfma_packed_kernel)
-template <int NNZ, bool kpf = false, bool XL = false>
+// XL > 0: x staged by LDS-DMA in whole 64-B spin pieces, XL neighbours ahead (see
+// bsr_kron_mfma_packed_kernel)
+template <int NNZ, bool kpf = false, int XL = 0>
 __global__ void __launch_bounds__(256) bsr_kron_mfma_kernel(const KronArgs p, int ngroups) {
     typedef double2 E;
     const E *__restrict__ x = (const E *)p.x;
@@ -295,6 +313,11 @@ __global__ void __launch_bounds__(256) bsr_kron_mfma_kernel(const KronArgs p, in
     __shared__ __attribute__((aligned(16))) E us[(4 * NNZ * 9 + 255) / 256 * 256];
     // a workgroup's 4 tasks span at most 4 rows: nu <= 4 * NNZ * 9, every pass of 256 lanes fits
     static_assert(sizeof(us) / sizeof(E) >= (4 * NNZ * 9 + 255) / 256 * 256, "LDS sizing");
+    // XL: the spin matrices in LDS -- no vector-memory load in the main loop, where the
+    // compiler's own vmcnt waits (blind to the DMAs) would drain the x ring
+    __shared__ __attribute__((aligned(16))) E ks[XL ? NNZ * 16 : 1];
+    if constexpr (XL > 0)
+        for (int e = (int)threadIdx.x; e < NNZ * 16; e += 256) ks[e] = ((const E *)p.kron)[e];
     {
         const long rlo = (wgi * 4) / ngroups, rhi = min((wgi * 4 + 3) / ngroups, p.block_rows - 1);
         const int nu = (int)(rhi - rlo + 1) * NNZ * 9;
@@ -339,16 +362,17 @@ __global__ void __launch_bounds__(256) bsr_kron_mfma_kernel(const KronArgs p, in
     };
     double accR[3] = {0, 0, 0}, accI[3] = {0, 0, 0};
     E xa[3], xb[3];
-    // XL: a ring of 2 neighbours x 3 KB per wave; the DMA lane's piece: column lane / 4 of the
-    // group, its spins rotated by the column's quarter
-    __shared__ __attribute__((aligned(16))) E xr[XL ? 4 * 2 * 3 * 64 : 1];
+    // XL: a ring of XL + 1 neighbours x 3 KB per wave; the DMA lane's piece: column lane / 4 of
+    // the group, its spins rotated as xpos below
+    constexpr int NS = XL + 1;
+    __shared__ __attribute__((aligned(16))) E xr[XL ? 4 * NS * 3 * 64 : 1];
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, 0x7fffffff, 0x00020000);
-    const int qd = lane >> 2, bd = ((lane & 3) - (qd >> 2)) & 3;
+    const int qd = lane >> 2, bd = ((lane & 3) - (qd >> 1) - (qd >> 3)) & 3;
     const long cold = min((long)cg * 16 + qd, n - 1);
     const unsigned xoff_d = (unsigned)(cold * 4 + bd) * 16u;
-    const unsigned ring = (unsigned)(size_t)(const __attribute__((address_space(3))) void *)xr + (unsigned)w * 6144u;
+    const unsigned ring = (unsigned)(size_t)(const __attribute__((address_space(3))) void *)xr + (unsigned)w * (NS * 3072u);
     auto issue_x = [&](int mu) {
-        const unsigned base = ring + (unsigned)(mu & 1) * 3072u;
+        const unsigned base = ring + (unsigned)(mu % NS) * 3072u;
         const unsigned o = (unsigned)((long)jrow[mu] * xsite) * 16u + xoff_d;
 #pragma unroll
         for (int d = 0; d < 3; ++d)
@@ -360,37 +384,35 @@ __global__ void __launch_bounds__(256) bsr_kron_mfma_kernel(const KronArgs p, in
                            "s"(__builtin_amdgcn_readfirstlane(base + (unsigned)d * 1024u)), "s"(rx)
                          : "memory", "m0");
     };
-    const int xpos = 4 * q + ((b + (q >> 2)) & 3);
-    if constexpr (XL) issue_x(0);
-    else load_x(jrow[0], xa);
+    const int xpos = 4 * q + ((b + (q >> 1) + (q >> 3)) & 3);
+    if constexpr (XL > 0) {
+#pragma unroll
+        for (int mu = 0; mu < XL && mu < NNZ; ++mu) issue_x(mu);
+    } else {
+        load_x(jrow[0], xa);
+    }
     // the spin matrix of neighbour mu + 1 is loaded with its x rows; the compiler barrier keeps
     // the unrolled loop from hoisting all 9 spin-matrix loads to the top (36 more VGPRs: fewer
     // waves per SIMD)
-    E Kc = kron[kidx];
+    E Kc = XL > 0 ? E{} : kron[kidx];
 #pragma unroll
     for (int mu = 0; mu < NNZ; ++mu) {
         if constexpr (kpf) asm volatile("" ::: "memory");
         E Kn = Kc;
-        if constexpr (XL) {
-            // the ring slot of neighbour mu + 1 was read in iteration mu - 1: those reads are done
+        if constexpr (XL > 0) {
+            // the ring slot of neighbour mu + XL was read in iteration mu - 1: those reads are done
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if (mu + 1 < NNZ) {
-                issue_x(mu + 1);
-                if constexpr (kpf) Kn = kron[(mu + 1) * 16 + kidx];
-                // neighbour mu landed: at most its successor's DMAs (and spin load) in flight
-                if constexpr (kpf) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-                else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-            } else {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            const E *xs = xr + w * 384 + (mu & 1) * 192;
+            if (mu + XL < NNZ) issue_x(mu + XL);
+            // neighbour mu landed: its successors' DMAs (and the next spin load) may stay in flight
+            wait_vmcnt(3 * (NNZ - 1 - mu < XL ? NNZ - 1 - mu : XL));
+            const E *xs = xr + w * (NS * 192) + (mu % NS) * 192;
 #pragma unroll
             for (int d = 0; d < 3; ++d) xa[d] = xs[d * 64 + xpos];
         } else if (mu + 1 < NNZ) {
             load_x(jrow[mu + 1], xb);
             if constexpr (kpf) Kn = kron[(mu + 1) * 16 + kidx];
         }
-        const E K = kpf ? Kc : kron[mu * 16 + kidx];
+        const E K = XL > 0 ? ks[mu * 16 + kidx] : kpf ? Kc : kron[mu * 16 + kidx];
         Kc = Kn;
         // color: T(i) = sum_d U(i, d) x(d)
         E t[3];
@@ -411,15 +433,15 @@ __global__ void __launch_bounds__(256) bsr_kron_mfma_kernel(const KronArgs p, in
             accI[i] = __builtin_amdgcn_mfma_f64_4x4x4f64(K.x, t[i].y, accI[i], 0, 0, 0);
             accI[i] = __builtin_amdgcn_mfma_f64_4x4x4f64(K.y, t[i].x, accI[i], 0, 0, 0);
         }
-        if (!XL && mu + 1 < NNZ) {
+        if (XL == 0 && mu + 1 < NNZ) {
 #pragma unroll
             for (int d = 0; d < 3; ++d) xa[d] = xb[d];
         }
     }
-    if constexpr (XL) {
+    if constexpr (XL > 0) {
         if (p.ylds) {
-            // C lane 16 a + q -> ring position 4 q + (a + q / 4) mod 4; lane l stores column l / 4
-            E *ys = xr + w * 384;
+            // C lane 16 a + q -> ring position xpos (a in place of b); lane l stores column l / 4
+            E *ys = xr + w * (NS * 192);
 #pragma unroll
             for (int i = 0; i < 3; ++i)
                 ys[i * 64 + xpos] = Ops<E>::scale(E{accR[i], accI[i]}, p.alpha_re, p.alpha_im);
@@ -458,11 +480,12 @@ __global__ void __launch_bounds__(256) bsr_kron_mfma_kernel(const KronArgs p, in
 // 16-lane quarter of such a load touches 16 pieces 64 B apart (8 cache lines; 32 TA/TCP accesses
 // per 1-KB instruction against 8 for a linear one, and TA/TD busy 85-92 %).  The DMA instead
 // moves each slot's 4 spins as one 64-B piece (lane l: slot l / 4), writes them lane-linear into
-// the wave's ring (one neighbour ahead, 3 KB per neighbour), and the B lanes read them back with
-// the spins rotated by the slot's quarter (position 4 q + (b + q / 4) mod 4), which puts a read
-// quarter's 16 lanes on 16 different bank groups.
-template <int NNZ, bool kpf = false, bool XL = false>
+// the wave's ring (XL neighbours ahead, 3 KB per neighbour: deeper prefetch costs LDS, not
+// VGPRs), and the B lanes read them back with the spins rotated (position 4 q + (b + q / 2 +
+// q / 8) mod 4: the 16-B granules of any 8 or 16 lanes reading together fall on distinct banks).
+template <int NNZ, bool kpf = false, int XL = 0>
 __global__ void __launch_bounds__(256) bsr_kron_mfma_packed_kernel(const KronArgs p, int rw, int xring) {
+    constexpr int NS = XL + 1;
     typedef double2 E;
     const E *__restrict__ x = (const E *)p.x;
     E *__restrict__ y = (E *)p.y;
@@ -520,22 +543,32 @@ __global__ void __launch_bounds__(256) bsr_kron_mfma_packed_kernel(const KronArg
     };
     E xa[3], xb[3];
     // XL: the DMA lane's piece (slot lane / 4, spin rotated back) and its slot's block columns
-    int jd[XL ? NNZ : 1];
+    int jd[XL > 0 ? NNZ : 1];
     unsigned xoff_d = 0, xring_w = 0;
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void *)x, (short)0, 0x7fffffff, 0x00020000);
-    if constexpr (XL) {
-        const int qd = lane >> 2, bd = ((lane & 3) - (qd >> 2)) & 3;
+    if constexpr (XL > 0) {
+        const int qd = lane >> 2, bd = ((lane & 3) - (qd >> 1) - (qd >> 3)) & 3;
         const int sd = w * 16 + qd, rld = sd / (int)n;
         const long cold = sd - (long)rld * n;
         const long rd = r0 + (rld < nrows ? rld : nrows - 1);
 #pragma unroll
         for (int mu = 0; mu < NNZ; ++mu) jd[mu] = p.jj[rd * NNZ + mu];
         xoff_d = (unsigned)(cold * 4 + bd) * 16u;
-        xring_w = (unsigned)xring + (unsigned)w * 6144u;
+        xring_w = (unsigned)xring + (unsigned)w * (NS * 3072u);
     }
     const unsigned lds0 = (unsigned)(size_t)(const __attribute__((address_space(3))) void *)smem_k;
+    // XL: the spin matrices in LDS after the rings -- no vector-memory load in the main loop,
+    // where the compiler's own vmcnt waits (blind to the DMAs) would drain the x ring
+    E *ks = (E *)(smem_k + xring + (int)(blockDim.x >> 6) * NS * 3072);
+    if constexpr (XL > 0) {
+        for (int e = (int)threadIdx.x; e < NNZ * 16; e += (int)blockDim.x) ks[e] = kron[e];
+        // the DMA lanes' block columns: consumed here, so that no load of them is pending
+        // (and waited for by the compiler) inside the loop
+#pragma unroll
+        for (int mu = 0; mu < NNZ; ++mu) asm volatile("" : "+v"(jd[mu]));
+    }
     auto issue_x = [&](int mu) {
-        const unsigned base = lds0 + xring_w + (unsigned)(mu & 1) * 3072u;
+        const unsigned base = lds0 + xring_w + (unsigned)(mu % NS) * 3072u;
         const unsigned o = (unsigned)((long)jd[mu] * xsite) * 16u + xoff_d;
 #pragma unroll
         for (int d = 0; d < 3; ++d)
@@ -548,9 +581,13 @@ __global__ void __launch_bounds__(256) bsr_kron_mfma_packed_kernel(const KronArg
                          : "memory", "m0");
     };
     // the B lane's position in a ring slot
-    const int xpos = 4 * q + ((b + (q >> 2)) & 3);
-    if constexpr (XL) issue_x(0);
-    else load_x(jrow[0], xa);
+    const int xpos = 4 * q + ((b + (q >> 1) + (q >> 3)) & 3);
+    if constexpr (XL > 0) {
+#pragma unroll
+        for (int mu = 0; mu < XL && mu < NNZ; ++mu) issue_x(mu);
+    } else {
+        load_x(jrow[0], xa);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const E *urow_s = us + rlc * NNZ * 9;
@@ -558,31 +595,25 @@ __global__ void __launch_bounds__(256) bsr_kron_mfma_packed_kernel(const KronArg
     // the spin matrix of neighbour mu + 1 is loaded with its x rows; the compiler barrier keeps
     // the unrolled loop from hoisting all 9 spin-matrix loads to the top (36 more VGPRs: fewer
     // waves per SIMD)
-    E Kc = kron[kidx];
+    E Kc = XL > 0 ? E{} : kron[kidx];
 #pragma unroll
     for (int mu = 0; mu < NNZ; ++mu) {
         if constexpr (kpf) asm volatile("" ::: "memory");
         E Kn = Kc;
-        if constexpr (XL) {
-            // the ring slot of neighbour mu + 1 was read in iteration mu - 1: those reads are done
+        if constexpr (XL > 0) {
+            // the ring slot of neighbour mu + XL was read in iteration mu - 1: those reads are done
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if (mu + 1 < NNZ) {
-                issue_x(mu + 1);
-                if constexpr (kpf) Kn = kron[(mu + 1) * 16 + kidx];
-                // neighbour mu landed: at most its successor's 3 DMAs and spin load in flight
-                if constexpr (kpf) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-                else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-            } else {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            const E *xs = (const E *)(smem_k + xring_w + (mu & 1) * 3072);
+            if (mu + XL < NNZ) issue_x(mu + XL);
+            // neighbour mu landed: its successors' DMAs (and the next spin load) may stay in flight
+            wait_vmcnt(3 * (NNZ - 1 - mu < XL ? NNZ - 1 - mu : XL));
+            const E *xs = (const E *)(smem_k + xring_w + (mu % NS) * 3072);
 #pragma unroll
             for (int d = 0; d < 3; ++d) xa[d] = xs[d * 64 + xpos];
         } else if (mu + 1 < NNZ) {
             load_x(jrow[mu + 1], xb);
             if constexpr (kpf) Kn = kron[(mu + 1) * 16 + kidx];
         }
-        const E K = kpf ? Kc : kron[mu * 16 + kidx];
+        const E K = XL > 0 ? ks[mu * 16 + kidx] : kpf ? Kc : kron[mu * 16 + kidx];
         Kc = Kn;
         E t[3];
 #pragma unroll
@@ -601,21 +632,21 @@ __global__ void __launch_bounds__(256) bsr_kron_mfma_packed_kernel(const KronArg
             accI[i] = __builtin_amdgcn_mfma_f64_4x4x4f64(K.x, t[i].y, accI[i], 0, 0, 0);
             accI[i] = __builtin_amdgcn_mfma_f64_4x4x4f64(K.y, t[i].x, accI[i], 0, 0, 0);
         }
-        if (!XL && mu + 1 < NNZ) {
+        if (XL == 0 && mu + 1 < NNZ) {
 #pragma unroll
             for (int d = 0; d < 3; ++d) xa[d] = xb[d];
         }
     }
-    if constexpr (XL) {
+    if constexpr (XL > 0) {
         if (p.ylds) {
-            // C lane 16 a + q -> ring position 4 q + (a + q / 4) mod 4 (the B read's map); then
+            // C lane 16 a + q -> ring position xpos (the B read's map, a in place of b); then
             // lane l stores the piece of slot l / 4: each slot's 4 spins one 64-B run
             E *ys = (E *)(smem_k + xring_w);
 #pragma unroll
             for (int i = 0; i < 3; ++i)
                 ys[i * 64 + xpos] = Ops<E>::scale(E{accR[i], accI[i]}, p.alpha_re, p.alpha_im);
             asm volatile("" ::: "memory");
-            const int qd = lane >> 2, ad = ((lane & 3) - (qd >> 2)) & 3;
+            const int qd = lane >> 2, ad = ((lane & 3) - (qd >> 1) - (qd >> 3)) & 3;
             const int sd = w * 16 + qd, rld = sd / (int)n;
             if (rld >= nrows) return;
             const long cold = sd - (long)rld * n;
@@ -668,15 +699,20 @@ template <typename E> void launch_kron_typed(const KronArgs &a, hipStream_t s) {
                     check_dma_lds("bsr_kron_mfma_packed_kernel", lds_cb, (rw * 81L + nth - 1) / nth, nth);
                     // x by LDS-DMA: a ring of 2 x 3 KB per wave after the color blocks (lds_cb is
                     // a multiple of 16); 32-bit buffer offsets
-                    const bool xl = g_bsr_tune.kron_xlds && a.block_rows * 12L * a.ncols * 16 < (1L << 31);
-                    const size_t lds_bytes = lds_cb + (xl ? (size_t)wpk * 6144 : 0);
-                    if (xl) check_dma_lds("bsr_kron_mfma_packed_kernel x ring", lds_bytes, 0, 0, (long)lds_cb + wpk * 6144L);
+                    const int xl = a.block_rows * 12L * a.ncols * 16 < (1L << 31)
+                                       ? std::max(0, std::min(3, g_bsr_tune.kron_xlds)) : 0;
+                    // (+ the 9 spin matrices)
+                    const size_t lds_bytes = lds_cb + (xl > 0 ? (size_t)wpk * (xl + 1) * 3072 + 9 * 16 * 16 : 0);
+                    if (xl) check_dma_lds("bsr_kron_mfma_packed_kernel x ring", lds_bytes, 0, 0, (long)lds_cb + wpk * (xl + 1) * 3072L + 9 * 16 * 16);
                     // spin matrices one neighbour ahead: n = 8 / 12 104 / 166 -> 102 / 163 us
                     // (the one-row-per-wave kernel: 214 -> 221 us at n = 16, so not there;
                     // profiles/r02c_kron_kpf.txt)
-                    if (xl)
-                        hipLaunchKernelGGL((bsr_kron_mfma_packed_kernel<9, true, true>), dim3((unsigned)blocks),
-                                           dim3(64 * wpk), lds_bytes, s, a, rw, (int)lds_cb);
+                    auto go = [&](auto kern) {
+                        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(64 * wpk), lds_bytes, s, a, rw, (int)lds_cb);
+                    };
+                    if (xl == 1) go(bsr_kron_mfma_packed_kernel<9, true, 1>);
+                    else if (xl == 2) go(bsr_kron_mfma_packed_kernel<9, true, 2>);
+                    else if (xl == 3) go(bsr_kron_mfma_packed_kernel<9, true, 3>);
                     else
                         hipLaunchKernelGGL((bsr_kron_mfma_packed_kernel<9, true>), dim3((unsigned)blocks),
                                            dim3(64 * wpk), lds_bytes, s, a, rw, (int)lds_cb);
@@ -689,9 +725,14 @@ template <typename E> void launch_kron_typed(const KronArgs &a, hipStream_t s) {
             if (blocks < (1L << 31)) {
                 g_bsr_tune.last = 5;
                 // x by LDS-DMA (32-bit buffer offsets)
-                if (g_bsr_tune.kron_xlds && a.block_rows * 12L * a.ncols * 16 < (1L << 31))
-                    hipLaunchKernelGGL((bsr_kron_mfma_kernel<9, false, true>), dim3((unsigned)blocks), dim3(256),
-                                       0, s, a, (int)ngroups);
+                const int xl = a.block_rows * 12L * a.ncols * 16 < (1L << 31)
+                                   ? std::max(0, std::min(3, g_bsr_tune.kron_xlds)) : 0;
+                auto go = [&](auto kern) {
+                    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, s, a, (int)ngroups);
+                };
+                if (xl == 1) go(bsr_kron_mfma_kernel<9, false, 1>);
+                else if (xl == 2) go(bsr_kron_mfma_kernel<9, false, 2>);
+                else if (xl == 3) go(bsr_kron_mfma_kernel<9, false, 3>);
                 else
                     hipLaunchKernelGGL((bsr_kron_mfma_kernel<9, false>), dim3((unsigned)blocks), dim3(256), 0,
                                        s, a, (int)ngroups);
@@ -745,7 +786,7 @@ void launch_bsr_kron(const BsrDesc &d, int device) {
     a.alpha_re = d.alpha.re;
     a.alpha_im = d.alpha.im;
     a.add = d.add ? 1 : 0;
-    a.ylds = g_bsr_tune.kron_xlds >= 2 ? 1 : 0;
+    a.ylds = g_bsr_tune.kron_ylds ? 1 : 0;
     switch (d.t) {
     case SBX_CDOUBLE: return launch_kron_typed<double2>(a, s);
     case SBX_CFLOAT: return launch_kron_typed<float2>(a, s);
