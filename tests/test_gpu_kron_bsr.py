@@ -171,8 +171,8 @@ def test_kron_errors(gpu):
 def test_kron_mfma_kernel(gpu, ncols, L, bif, sparse):
     """complex<double> 3x3 x 4x4 from 8 rhs columns: the spin products on the matrix cores
     (bsr_kron_mfma_kernel; 16-column groups, partial last group; bsr_kron_mfma_packed_kernel at 8
-    and 12 columns: a wave's 16 column slots over several rows, x staged by LDS-DMA or loaded
-    per lane, y written per lane or through the same ring; 3^4 sites: a last workgroup with
+    and 12 columns: a wave's 16 column slots over several rows; x staged by LDS-DMA 1-3
+    neighbours ahead or loaded per lane, y written per lane or through the same ring; 3^4 sites: a last workgroup with
     fewer rows than its slots), complex alpha, beta,
     powers; integer data, exact; and the same results with each form switched off."""
     import torch
@@ -195,13 +195,16 @@ def test_kron_mfma_kernel(gpu, ncols, L, bif, sparse):
     dimx = [1, L, L, L, L, color, ncols, spin]
     dimy = [power] + dimx[1:]
     outs = []
-    old_xl = sb.tune_get("bsr.kron_xlds")
+    old_xl, old_yl = sb.tune_get("bsr.kron_xlds"), sb.tune_get("bsr.kron_ylds")
     try:
         # packed column slots (8 and 12 columns: several rows per wave), one row per wave, no MFMA
-        for on, pack, xl in ((1, 1, 1), (1, 1, 2), (1, 1, 0), (1, 0, 2), (1, 0, 0), (0, 1, 1)):
+        # (MFMA kernels, packed slots, x staging depth, y staged)
+        for on, pack, xl, yl in ((1, 1, 1, 0), (1, 1, 2, 1), (1, 1, 3, 0), (1, 1, 0, 0),
+                                 (1, 0, 2, 1), (1, 0, 3, 0), (1, 0, 0, 0), (0, 1, 1, 1)):
             sb.tune_set("bsr.kron_mfma", on)
             sb.tune_set("bsr.kron_pack", pack)
             sb.tune_set("bsr.kron_xlds", xl)
+            sb.tune_set("bsr.kron_ylds", yl)
             ty = torch.from_numpy(y0.copy()).to(gpu)
             sb.bsr_krylov(alpha, op, "xyztsc", "XYZTSC", [([0] * 8, dimx)], "pXYZTCnS", [0] * 8,
                           dimx, dimx, [torch.from_numpy(x).to(gpu)], beta, [([0] * 8, dimy)],
@@ -212,9 +215,10 @@ def test_kron_mfma_kernel(gpu, ncols, L, bif, sparse):
         sb.tune_set("bsr.kron_mfma", 1)
         sb.tune_set("bsr.kron_pack", 1)
         sb.tune_set("bsr.kron_xlds", old_xl)
+        sb.tune_set("bsr.kron_ylds", old_yl)
         op.destroy()
     packed = 6 if ncols in (8, 12) else 5
-    assert [o[0] for o in outs[:5]] == [packed] * 3 + [5, 5] and outs[5][0] not in (5, 6)
+    assert [o[0] for o in outs[:7]] == [packed] * 4 + [5] * 3 and outs[7][0] not in (5, 6)
     for form, out in outs:
         assert np.array_equal(out, ref), form
 

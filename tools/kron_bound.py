@@ -2,8 +2,9 @@
 """Bound model of the Kronecker BSR kernel (bench `kron_n12`: 16^4, 3x3 color blocks x 4x4 spin
 matrices, complex<double>): the same kernel and launch on operators that differ only in where
 the nine block columns of a row point (tools/bsr_bound.py's kinds: stencil, local, self, one),
-so the value, y and gather streams stay fixed while the x reuse distance changes.  XLS=2,1,0: the
-bsr.kron_xlds settings to compare (x staged by LDS-DMA, y too, or both per lane).  Not part of the
+so the value, y and gather streams stay fixed while the x reuse distance changes.  XLS=3,2,1,0: the
+bsr.kron_xlds settings to compare (x staged by LDS-DMA that many neighbours ahead, or per lane);
+YL=1: y through the same ring (bsr.kron_ylds).  Not part of the
 product."""
 import json
 import os
@@ -37,6 +38,7 @@ def main():
     kinds = os.environ.get("KINDS", "stencil,local,self,one").split(",")
     ncols_list = [int(v) for v in os.environ.get("NCOLS", "12").split(",")]
     xls = [int(v) for v in os.environ.get("XLS", str(sb.tune_get("bsr.kron_xlds"))).split(",")]
+    sb.tune_set("bsr.kron_ylds", int(os.environ.get("YL", sb.tune_get("bsr.kron_ylds"))))
     dims = [L, L, L, L]
     dim = dims + [4, 3]
     full = [([0] * 6, dim)]
