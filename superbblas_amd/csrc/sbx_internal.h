@@ -259,7 +259,7 @@ struct BsrTune {
                                 ///< matrix cores (bsr_kron_mfma_kernel) ...
     long kron_mfma_min_cols = 8; ///< ... from this many rhs columns
     int kron_pack = 1;           ///< ... below 16 rhs columns: a wave's 16 column slots span several rows (0 = off)
-    int kron_xlds = 0;           ///< ... x staged by LDS-DMA, a column's 4 spins as one 64-B piece, this many
+    int kron_xlds = 1;           ///< ... x staged by LDS-DMA, a column's 4 spins as one 64-B piece, this many
                                  ///< neighbours ahead (0 = off: per-lane loads one ahead; 1..3)
     int kron_ylds = 0;           ///< ... with x staged: y written through the same ring in whole pieces
     int nt = 11; ///< the value stream's LDS-DMA loads with the non-temporal (streaming) policy, per
