@@ -210,6 +210,26 @@ __device__ __forceinline__ unsigned lds_u32(const void *p) {
     return (unsigned)(size_t)(const __attribute__((address_space(3))) void *)p;
 }
 
+/// s_waitcnt vmcnt(n) for an n the unrolled caller knows at compile time (folds to one wait)
+__device__ __forceinline__ void wait_vmcnt_n(int n) {
+    switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+    case 18: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+}
+
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, unsigned off, unsigned dst, int nt = 0) {
     // inline asm: hipcc does not order its ds_reads against an LDS-DMA it cannot see; the kernel
     // retires the DMA with an explicit vmcnt(0) before its barrier.  nt (a uniform kernel
@@ -538,18 +558,9 @@ __global__ void __launch_bounds__(256) bsr_mfma_dma_kernel(const BsrArgs p, unsi
     for (int k = 0; k < NNZ; ++k) {
         // the slot of block k + PD was last read in iteration k - 1: its reads have returned
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (k + PD < NNZ) {
-            issue(k + PD);
-            // block k landed: at most the NI instructions of each later block in flight
-            if constexpr (PD == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
-            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NI) : "memory");
-        } else if (k + PD == NNZ) {
-            // no block issued this iteration: PD - 1 blocks may stay in flight
-            if constexpr (PD == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
+        if (k + PD < NNZ) issue(k + PD);
+        // block k landed: the NI instructions of each later block issued so far may stay in flight
+        wait_vmcnt_n(NI * (NNZ - 1 - k < PD ? NNZ - 1 - k : PD));
         if (dj[k] < 0) continue;
         const E *sa = (const E *)(smem + (slot0 - lds_u32(smem)) + (k % (PD + 1)) * SLOT);
         const E *sx = sa + (PK > 0 ? ABLK : NA * 1024 / ES);
@@ -651,7 +662,9 @@ void launch_bsr_mfma(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_
     // 348-355 us staged; the chain's complex<float> operator 985 -> 693 us with packed slots;
     // two or three blocks of lookahead were slower, profiles/r02_bsr_blk_sweep.txt)
     if (g_bsr_tune.variant == 0 && nnz == 9 && xrow && a.ldx == a.ncols && a.ncols <= 16 &&
-        launch_bsr_mfma_dma<R, CPLX, BI, BD, 9, 1>(a, yrow, s))
+        (g_bsr_tune.blk_pd == 2   ? launch_bsr_mfma_dma<R, CPLX, BI, BD, 9, 2>(a, yrow, s)
+         : g_bsr_tune.blk_pd == 3 ? launch_bsr_mfma_dma<R, CPLX, BI, BD, 9, 3>(a, yrow, s)
+                                  : launch_bsr_mfma_dma<R, CPLX, BI, BD, 9, 1>(a, yrow, s)))
         return;
     // the 9-point stencils otherwise: columns preloaded, fragments one block ahead (a 3- or
     // 9-block lookahead, the XCD-grouped row order and non-temporal value loads were all

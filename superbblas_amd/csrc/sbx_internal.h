@@ -262,6 +262,7 @@ struct BsrTune {
     int kron_xlds = 1;           ///< ... x staged by LDS-DMA, a column's 4 spins as one 64-B piece, this many
                                  ///< neighbours ahead (0 = off: per-lane loads one ahead; 1..3)
     int kron_ylds = 0;           ///< ... with x staged: y written through the same ring in whole pieces
+    int blk_pd = 1; ///< 12x12 blocks by LDS-DMA: blocks in flight ahead of the one in use (1..3)
     int nt = 11; ///< the value stream's LDS-DMA loads with the non-temporal (streaming) policy, per
                 ///< kernel: 1 12x12 blocks by LDS-DMA, 2 3x3 row chunks, 4 3x3 split rows, 8 3x3 one
                 ///< thread per block.  Default 1 | 2 | 8 (tools/bsr_bound.py NTS, warm, interleaved:

@@ -222,14 +222,14 @@ def test_bsr_image_side(gpu, spin, color, ncols, beta, power):
     assert np.array_equal(ty.cpu().numpy(), yref)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant,pd", [(0, 1), (0, 2), (0, 3), (1, 1), (2, 1)])
 @pytest.mark.parametrize("ncols,dtype", [(3, np.complex128), (16, np.complex64), (20, np.complex128),
                                          (5, np.float64), (12, np.complex64), (12, np.float32)])
-def test_bsr_12x12_kernel_forms(gpu, variant, ncols, dtype):
+def test_bsr_12x12_kernel_forms(gpu, variant, pd, ncols, dtype):
     """The 12x12 (spin x color) 9-point operator through every kernel form: the block-staged
-    MFMA kernel (variant 0, row-major x with ncols <= 16; blocks staged by LDS-DMA one ahead,
-    packed slots for 8-byte elements), the column-preloading MFMA kernel (variant 2, and variant
-    0 beyond 16 columns) and the generic-row MFMA kernel (variant 1); exact."""
+    MFMA kernel (variant 0, row-major x with ncols <= 16; blocks staged by LDS-DMA 1-3 ahead,
+    `bsr.blk_pd`, packed slots for 8-byte elements), the column-preloading MFMA kernel (variant
+    2, and variant 0 beyond 16 columns) and the generic-row MFMA kernel (variant 1); exact."""
     import torch
     import superbblas_amd as sb
     from _common import TYPE_OF
@@ -245,6 +245,8 @@ def test_bsr_12x12_kernel_forms(gpu, variant, ncols, dtype):
     full = [([0] * 6, dim)]
     blk = [1, 1, 1, 1, spin, color]
     sb.tune_set("bsr.variant", variant)
+    old_pd = sb.tune_get("bsr.blk_pd")
+    sb.tune_set("bsr.blk_pd", pd)
     try:
         op = sb.create_bsr(full, dim, full, dim, blk, blk, False, [torch.from_numpy(ii).to(gpu)],
                            [torch.from_numpy(jj).to(gpu)], [torch.from_numpy(vals).to(gpu)])
@@ -257,12 +259,14 @@ def test_bsr_12x12_kernel_forms(gpu, variant, ncols, dtype):
         op.destroy()
     finally:
         sb.tune_set("bsr.variant", 0)
+        sb.tune_set("bsr.blk_pd", old_pd)
     assert np.array_equal(ty.cpu().numpy(), yref)
 
 
+@pytest.mark.parametrize("pd", [1, 3])
 @pytest.mark.parametrize("dtype,ncols,form", [(np.complex64, 16, 8), (np.complex64, 13, 8),
                                               (np.complex128, 12, 7)])
-def test_bsr_12x12_skipped_blocks_dma(gpu, dtype, ncols, form):
+def test_bsr_12x12_skipped_blocks_dma(gpu, dtype, ncols, form, pd):
     """Blocks with column -1 on the LDS-DMA 12x12 kernel (packed slots for complex<float>): a
     skipped block's slot must not read past the caller's arrays -- with 13-16 rhs columns the x
     part of a packed complex<float> slot is longer than a value block, and the last block of the
@@ -292,10 +296,15 @@ def test_bsr_12x12_skipped_blocks_dma(gpu, dtype, ncols, form):
                        [torch.from_numpy(jj).to(gpu)], [tv])
     dimx = [1, L, L, L, L, spin, color, ncols]
     ty = torch.full((vol * b * ncols,), 3.0, dtype=getattr(torch, np.dtype(dtype).name), device=gpu)
-    sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", [([0] * 8, dimx)], "pXYZTSCn", [0] * 8, dimx,
-                  dimx, [torch.from_numpy(x).to(gpu)], 0.0, [([0] * 8, dimx)], "pxyztscn",
-                  [0] * 8, dimx, dimx, "p", [ty])
-    torch.cuda.synchronize()
+    old_pd = sb.tune_get("bsr.blk_pd")
+    sb.tune_set("bsr.blk_pd", pd)
+    try:
+        sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", [([0] * 8, dimx)], "pXYZTSCn", [0] * 8, dimx,
+                      dimx, [torch.from_numpy(x).to(gpu)], 0.0, [([0] * 8, dimx)], "pxyztscn",
+                      [0] * 8, dimx, dimx, "p", [ty])
+        torch.cuda.synchronize()
+    finally:
+        sb.tune_set("bsr.blk_pd", old_pd)
     used = sb.tune_get("bsr.last_kernel")
     op.destroy()
     assert used == form, used

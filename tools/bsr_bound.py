@@ -14,7 +14,8 @@ Printed per case and rhs count: kernel time (library timers, median of 3 rounds 
 launches), the stencil's algorithmic bytes / time as a fraction of 8 TB/s, and the bytes the
 case must move beyond L2 at the least (values + y + indices + x once).  BLK=12 / DT=cf: the
 12x12-block (spin 4 x color 3) operator, complex<float>.  NTS=0,1,...: the bsr.nt settings to
-compare (the value stream's non-temporal load policy, per kernel bit)."""
+compare (the value stream's non-temporal load policy, per kernel bit); PDS=1,2,3: the 12x12
+kernel's block lookahead (bsr.blk_pd)."""
 import json
 import os
 import statistics
@@ -56,6 +57,7 @@ def main():
     kinds = os.environ.get("KINDS", "stencil,local,self,one").split(",")
     ncols_list = [int(v) for v in os.environ.get("NCOLS", "12,64").split(",")]
     nts = [int(v) for v in os.environ.get("NTS", str(sb.tune_get("bsr.nt"))).split(",")]
+    pds = [int(v) for v in os.environ.get("PDS", str(sb.tune_get("bsr.blk_pd"))).split(",")]
     # BLK=12: spin 4 x color 3 blocks (config 3's secondary shape / the chain's operator);
     # DT=cf: complex<float>
     spin = 4 if os.environ.get("BLK", "3") == "12" else 1
@@ -71,8 +73,9 @@ def main():
         op = sb.create_bsr(full, dim, full, dim, blk, blk, False,
                            [torch.full((V,), nnz, dtype=torch.int32, device=dev)],
                            [torch.from_numpy(jj.reshape(-1)).to(dev)], [vals])
-        for n, nt in [(n, nt) for n in ncols_list for nt in nts]:
+        for n, nt, pd in [(n, nt, pd) for n in ncols_list for nt in nts for pd in pds]:
             sb.tune_set("bsr.nt", nt)
+            sb.tune_set("bsr.blk_pd", pd)
             dx = [1, L, L, L, L, spin, 3, n]
             px = [([0] * 8, dx)]
             x = torch.randn(V * b * n, dtype=dt, device=dev)
@@ -97,7 +100,7 @@ def main():
             t = statistics.median(ts)
             algo = es * (9 * b * b * V + 2 * b * V * n) + 4.0 * (9 * V + V + 1)  # the stencil's
             floor = es * (nnz * b * b * V + 2 * b * V * n) + 4.0 * (nnz * V + V + 1)
-            print(json.dumps({"blk": b, "dtype": str(dt), "kind": kind, "ncols": n, "nt": nt,
+            print(json.dumps({"blk": b, "dtype": str(dt), "kind": kind, "ncols": n, "nt": nt, "blk_pd": pd,
                               "us": round(t * 1e6, 1),
                               "kernel": sb.tune_get("bsr.last_kernel"),
                               "stencil_bytes_frac_hbm": round(algo / t / 8e12, 4),
