@@ -114,7 +114,7 @@ int sbx_timings_report(char *buf, int len);
    "gemm.share_ab", "copy.nt", "copy.budget", "copy.run", "copy.max_elems", "copy.pair",
    "copy.order", "copy.trans", "copy.btrans", "bsr.variant", "bsr.row_max_cols", "bsr.split_max_cols",
    "bsr.split_cw", "bsr.split_jb", "bsr.split_ilv", "bsr.kron_mfma", "bsr.kron_mfma_min_cols",
-   "bsr.kron_pack", "bsr.kron_xlds", "bsr.kron_ylds", "bsr.nt", "bsr.blk_pd", "dist.reduce" (must be set alike on every rank: the ranks' reductions must
+   "bsr.kron_pack", "bsr.kron_xlds", "bsr.kron_ylds", "bsr.nt", "bsr.blk_pd", "dense.wave", "dist.reduce" (must be set alike on every rank: the ranks' reductions must
    match; SB_DEBUG >= 1 checks it), "alloc.max_cached", "debug.level" (overrides SB_DEBUG),
    "debug.corrupt_copy" (tests of the SB_DEBUG checks: drop that local piece of every copy); read-backs "bsr.last_kernel",
    "copy.last_pair", "dist.reduce_calls", "alloc.cross_stream_frees".  Unknown keys fail with an

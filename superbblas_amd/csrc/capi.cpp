@@ -425,6 +425,7 @@ int sbx_tune_set(const char *key, long long value) {
         else if (k == "bsr.kron_xlds") g_bsr_tune.kron_xlds = (int)value;
         else if (k == "bsr.kron_ylds") g_bsr_tune.kron_ylds = (int)value;
         else if (k == "bsr.nt") g_bsr_tune.nt = (int)value;
+        else if (k == "dense.wave") g_dense_wave = (int)value;
         else if (k == "bsr.blk_pd") g_bsr_tune.blk_pd = (int)value;
         else if (k == "gemm.m3") g_gemm_tune.m3 = (int)value;
         else if (k == "gemm.splits") g_gemm_tune.splits = (int)value;
@@ -470,6 +471,7 @@ int sbx_tune_get(const char *key, long long *value) {
         else if (k == "bsr.kron_xlds") *value = g_bsr_tune.kron_xlds;
         else if (k == "bsr.kron_ylds") *value = g_bsr_tune.kron_ylds;
         else if (k == "bsr.nt") *value = g_bsr_tune.nt;
+        else if (k == "dense.wave") *value = g_dense_wave;
         else if (k == "bsr.blk_pd") *value = g_bsr_tune.blk_pd;
         else if (k == "bsr.last_kernel") *value = g_bsr_tune.last;
         else if (k == "gemm.m3") *value = g_gemm_tune.m3;

@@ -17,6 +17,7 @@
 #include <algorithm>
 
 namespace sbx {
+int g_dense_wave = 1;
 namespace {
 
 constexpr int DTH = 256;
@@ -252,9 +253,197 @@ __global__ void __launch_bounds__(DTH) trsm_kernel(const E *a, long n, E *x, lon
     }
 }
 
+// Small matrices (n <= WNM: the 12x12 spin-color blocks of a lattice, 3x3 color blocks): one
+// wave per matrix, four per workgroup, no barrier.  Lane c < n holds column c in registers; a
+// step's pivot, multipliers and row are broadcast across the wave (the source lane is uniform),
+// so the factorisation is wave-synchronous.  The arithmetic is the block kernels' operation for
+// operation (same pivots, same multiply / subtract order), so results agree with them bit for bit
+// up to the compiler's contraction choices.  The solve keeps one right-hand side per lane, the
+// factors in the wave's LDS slice (broadcast reads).
+constexpr int WNMAX = 16;
+
+template <typename E> __device__ __forceinline__ E wshfl(E v, int l);
+template <> __device__ __forceinline__ double wshfl<double>(double v, int l) { return __shfl(v, l); }
+template <> __device__ __forceinline__ float wshfl<float>(float v, int l) { return __shfl(v, l); }
+template <> __device__ __forceinline__ double2 wshfl<double2>(double2 v, int l) {
+    return double2{__shfl(v.x, l), __shfl(v.y, l)};
+}
+template <> __device__ __forceinline__ float2 wshfl<float2>(float2 v, int l) {
+    return float2{__shfl(v.x, l), __shfl(v.y, l)};
+}
+
+template <typename E, int WNM>
+__global__ void __launch_bounds__(256) potrf_wave_kernel(E *a, int n, long k, int *info) {
+    typedef DOps<E> O;
+    const int lane = threadIdx.x & 63;
+    const long mi = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (mi >= k) return;
+    E *g = a + mi * n * n;
+    const int c = lane < n ? lane : 0;
+    E v[WNM];
+#pragma unroll
+    for (int r = 0; r < WNM; ++r) v[r] = r < n ? g[r + (long)c * n] : O::real(0);
+    int bad = 0;
+#pragma unroll
+    for (int j = 0; j < WNM; ++j) {
+        if (j >= n) break;
+        double d = wshfl<double>(O::re(v[j]), j);
+        if (!(d > 0)) {
+            bad = j + 1;
+            break;
+        }
+        d = sqrt(d);
+        if (lane == j) v[j] = O::real(d);
+        if (lane > j) v[j] = O::divr(v[j], d);
+        // row j of U: element r from lane r
+        E rowj[WNM];
+#pragma unroll
+        for (int r = j + 1; r < WNM; ++r) rowj[r] = wshfl<E>(v[j], r);
+#pragma unroll
+        for (int r = j + 1; r < WNM; ++r)
+            if (r <= lane && lane < n) v[r] = O::sub(v[r], O::mul(O::conj(rowj[r]), v[j]));
+    }
+    if (lane < n)
+#pragma unroll
+        for (int r = 0; r < WNM; ++r)
+            if (r < n) g[r + (long)c * n] = v[r];
+    if (lane == 0) info[mi] = bad;
+}
+
+template <typename E, int WNM>
+__global__ void __launch_bounds__(256) gesv_wave_kernel(E *a, int n, long k, E *b, long m, int identity,
+                                                        double alpha_re, double alpha_im,
+                                                        int *info) {
+    typedef DOps<E> O;
+    __shared__ E lu_s[4][WNM * WNM];
+    __shared__ int piv_s[4][WNM];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const long mi = (long)blockIdx.x * 4 + w;
+    if (mi >= k) return;
+    E *g = a + mi * n * n;
+    const int c = lane < n ? lane : 0;
+    E v[WNM];
+#pragma unroll
+    for (int r = 0; r < WNM; ++r) v[r] = r < n ? g[r + (long)c * n] : O::real(0);
+    int bad = 0;
+#pragma unroll
+    for (int j = 0; j < WNM; ++j) {
+        if (j >= n) break;
+        // pivot: the largest |re| + |im| in column j at or below the diagonal, first on ties
+        double bv = -1;
+        int bi = j;
+#pragma unroll
+        for (int r = j; r < WNM; ++r)
+            if (r < n) {
+                const double t = O::abs1(v[r]);
+                if (t > bv) {
+                    bv = t;
+                    bi = r;
+                }
+            }
+        const int p = __shfl(bi, j);
+        const double pv = __shfl(bv, j);
+        if (lane == 0) piv_s[w][j] = p;
+        if (!(pv > 0)) {
+            bad = j + 1;
+            break;
+        }
+        if (p != j) {
+            E vp = v[j];
+#pragma unroll
+            for (int r = j + 1; r < WNM; ++r)
+                if (r == p) vp = v[r];
+#pragma unroll
+            for (int r = j + 1; r < WNM; ++r)
+                if (r == p) v[r] = v[j];
+            v[j] = vp;
+        }
+        const E d = wshfl<E>(v[j], j);
+        if (lane == j)
+#pragma unroll
+            for (int r = j + 1; r < WNM; ++r)
+                if (r < n) v[r] = O::div(v[r], d);
+#pragma unroll
+        for (int r = j + 1; r < WNM; ++r) {
+            if (r >= n) break;
+            const E l = wshfl<E>(v[r], j);
+            if (lane > j && lane < n) v[r] = O::sub(v[r], O::mul(l, v[j]));
+        }
+    }
+    if (lane < n)
+#pragma unroll
+        for (int r = 0; r < WNM; ++r)
+            if (r < n) {
+                g[r + (long)c * n] = v[r];
+                lu_s[w][r + c * n] = v[r];
+            }
+    if (!bad && b) {
+        // (the wave's LDS writes above are ordered before its reads below)
+        const E *M = lu_s[w];
+        E *B = b + mi * n * m;
+        for (long col = lane; col < m; col += 64) {
+            E *xg = B + col * n;
+            E x[WNM];
+#pragma unroll
+            for (int r = 0; r < WNM; ++r)
+                x[r] = r < n ? (identity ? (r == col ? O::one() : O::real(0)) : xg[r]) : O::real(0);
+#pragma unroll
+            for (int j = 0; j < WNM; ++j) {
+                if (j >= n) break;
+                const int p = piv_s[w][j];
+                if (p != j) {
+                    E xp = x[j];
+#pragma unroll
+                    for (int r = j + 1; r < WNM; ++r)
+                        if (r == p) xp = x[r];
+#pragma unroll
+                    for (int r = j + 1; r < WNM; ++r)
+                        if (r == p) x[r] = x[j];
+                    x[j] = xp;
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < WNM; ++r) {
+                if (r >= n) break;
+                E t = x[r];
+#pragma unroll
+                for (int q = 0; q < r; ++q) t = O::sub(t, O::mul(M[r + q * n], x[q]));
+                x[r] = t;
+            }
+#pragma unroll
+            for (int r = WNM - 1; r >= 0; --r) {
+                if (r >= n) continue;
+                E t = x[r];
+#pragma unroll
+                for (int q = r + 1; q < WNM; ++q)
+                    if (q < n) t = O::sub(t, O::mul(M[r + q * n], x[q]));
+                x[r] = O::div(t, M[r + r * n]);
+            }
+            if (alpha_re != 1 || alpha_im != 0)
+#pragma unroll
+                for (int r = 0; r < WNM; ++r) x[r] = scale_by<E>(x[r], alpha_re, alpha_im);
+#pragma unroll
+            for (int r = 0; r < WNM; ++r)
+                if (r < n) xg[r] = x[r];
+        }
+    }
+    if (lane == 0) info[mi] = bad;
+}
+
 template <typename E> bool fits_lds(long n) { return n * n * (long)sizeof(E) <= DENSE_LDS_BYTES; }
 
 template <typename E> void potrf_typed(void *a, long n, long k, int *info, hipStream_t s) {
+    if (n <= WNMAX && g_dense_wave) {
+        auto go = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3((unsigned)((k + 3) / 4)), dim3(256), 0, s, (E *)a, (int)n, k, info);
+        };
+        if (n <= 4) go(potrf_wave_kernel<E, 4>);
+        else if (n <= 8) go(potrf_wave_kernel<E, 8>);
+        else if (n <= 12) go(potrf_wave_kernel<E, 12>);
+        else go(potrf_wave_kernel<E, 16>);
+        SBX_HIP_CHECK(hipGetLastError());
+        return;
+    }
     const bool lds = fits_lds<E>(n);
     hipLaunchKernelGGL(potrf_kernel<E>, dim3((unsigned)k), dim3(DTH),
                        lds ? (size_t)(n * n * sizeof(E)) : 0, s, (E *)a, n, lds ? 1 : 0, info);
@@ -263,6 +452,18 @@ template <typename E> void potrf_typed(void *a, long n, long k, int *info, hipSt
 template <typename E>
 void gesv_typed(void *a, long n, long k, void *b, long m, bool identity, const Scalar &alpha,
                 int *ipiv, int *info, hipStream_t s) {
+    if (n <= WNMAX && g_dense_wave) {
+        auto go = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3((unsigned)((k + 3) / 4)), dim3(256), 0, s, (E *)a, (int)n, k,
+                               (E *)b, m, identity ? 1 : 0, alpha.re, alpha.im, info);
+        };
+        if (n <= 4) go(gesv_wave_kernel<E, 4>);
+        else if (n <= 8) go(gesv_wave_kernel<E, 8>);
+        else if (n <= 12) go(gesv_wave_kernel<E, 12>);
+        else go(gesv_wave_kernel<E, 16>);
+        SBX_HIP_CHECK(hipGetLastError());
+        return;
+    }
     const bool lds = fits_lds<E>(n);
     hipLaunchKernelGGL(gesv_kernel<E>, dim3((unsigned)k), dim3(DTH),
                        lds ? (size_t)(n * n * sizeof(E)) : 0, s, (E *)a, n, (E *)b, m,

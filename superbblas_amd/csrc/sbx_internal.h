@@ -276,6 +276,9 @@ struct BsrTune {
     std::atomic<int> last{0};
 };
 extern BsrTune g_bsr_tune;
+/// dense solvers: matrices up to 16 x 16 one wave each, four per workgroup (0 = the
+/// workgroup-per-matrix kernels for every size)
+extern int g_dense_wave;
 
 /// The LDS-DMA overrun class (39cd2bc): a DMA pass writes a whole row of 16-B lanes into LDS --
 /// lanes past the data included, they write zeros -- so a launch needs dynamic LDS for every pass

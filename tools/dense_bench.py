@@ -4,7 +4,8 @@ matrix per lattice site (16^4 sites, 12x12 spin-color blocks, complex<double>: t
 inverse) and the chain's 2-point matrices (64 time slices of 48x48, complex<float>).  Per case:
 library time of the whole call (copy into the working layout, the kernel, copy back) and of the
 kernel alone (library timers, median of 3 rounds of 10 calls), and the kernel's bytes (the
-matrices in and out once) / time.  CASES=site12,t48; Not part of the product."""
+matrices in and out once) / time.  CASES=site12,t48; WAVE=1,0: the dense.wave settings (a wave
+per matrix up to 16 x 16, or a workgroup per matrix).  Not part of the product."""
 import json
 import os
 import statistics
@@ -53,7 +54,9 @@ def main():
         dim = [nb, n, n]
         full = [([0, 0, 0], dim)]
         a0 = hpd(nb, n, dt, dev)
-        for op in ("cholesky", "inversion"):
+        for op, wv in [(op, wv) for op in ("cholesky", "inversion")
+                       for wv in [int(x) for x in os.environ.get("WAVE", "1,0").split(",")]]:
+            sb.tune_set("dense.wave", wv)
             v = a0.clone().reshape(-1)
 
             def f():
@@ -61,7 +64,7 @@ def main():
                 getattr(sb, op)(full, dim, "tij", [v], "i", "j")
             wall, kern = timed(f)
             by = 2.0 * nb * n * n * es
-            print(json.dumps({"case": name, "op": op, "matrices": nb, "n": n, "dtype": str(dt),
+            print(json.dumps({"case": name, "op": op, "wave": wv, "matrices": nb, "n": n, "dtype": str(dt),
                               "call_us": round(wall * 1e6, 1), "kernel_us": round(kern * 1e6, 1),
                               "kernel_GBps": round(by / kern / 1e9, 1)}), flush=True)
 
