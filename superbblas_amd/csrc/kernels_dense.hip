@@ -272,6 +272,24 @@ template <> __device__ __forceinline__ float2 wshfl<float2>(float2 v, int l) {
     return float2{__shfl(v.x, l), __shfl(v.y, l)};
 }
 
+/// A column of up to N elements in registers; complex elements as separate real and imaginary
+/// arrays (arrays of the vector types are not promoted to registers: they went to scratch)
+template <typename E, int N> struct Col {
+    E v[N];
+    __device__ __forceinline__ E get(int r) const { return v[r]; }
+    __device__ __forceinline__ void set(int r, E e) { v[r] = e; }
+};
+template <typename E, typename R, int N> struct CCol {
+    R re[N], im[N];
+    __device__ __forceinline__ E get(int r) const { return E{re[r], im[r]}; }
+    __device__ __forceinline__ void set(int r, E e) {
+        re[r] = e.x;
+        im[r] = e.y;
+    }
+};
+template <int N> struct Col<double2, N> : CCol<double2, double, N> {};
+template <int N> struct Col<float2, N> : CCol<float2, float, N> {};
+
 template <typename E, int WNM>
 __global__ void __launch_bounds__(256) potrf_wave_kernel(E *a, int n, long k, int *info) {
     typedef DOps<E> O;
@@ -280,33 +298,35 @@ __global__ void __launch_bounds__(256) potrf_wave_kernel(E *a, int n, long k, in
     if (mi >= k) return;
     E *g = a + mi * n * n;
     const int c = lane < n ? lane : 0;
-    E v[WNM];
+    Col<E, WNM> v;
 #pragma unroll
-    for (int r = 0; r < WNM; ++r) v[r] = r < n ? g[r + (long)c * n] : O::real(0);
+    for (int r = 0; r < WNM; ++r) v.set(r, r < n ? g[r + (long)c * n] : O::real(0));
     int bad = 0;
+    // (no early exits: constant trip counts, so the loops unroll fully and the columns stay in
+    // registers; with breaks the 12- and 16-row complex forms went to scratch)
 #pragma unroll
     for (int j = 0; j < WNM; ++j) {
-        if (j >= n) break;
-        double d = wshfl<double>(O::re(v[j]), j);
+        if (j >= n || bad) continue;
+        double d = wshfl<double>(O::re(v.get(j)), j);
         if (!(d > 0)) {
             bad = j + 1;
-            break;
+            continue;
         }
         d = sqrt(d);
-        if (lane == j) v[j] = O::real(d);
-        if (lane > j) v[j] = O::divr(v[j], d);
+        if (lane == j) v.set(j, O::real(d));
+        if (lane > j) v.set(j, O::divr(v.get(j), d));
+        const E vj = v.get(j);
         // row j of U: element r from lane r
-        E rowj[WNM];
 #pragma unroll
-        for (int r = j + 1; r < WNM; ++r) rowj[r] = wshfl<E>(v[j], r);
-#pragma unroll
-        for (int r = j + 1; r < WNM; ++r)
-            if (r <= lane && lane < n) v[r] = O::sub(v[r], O::mul(O::conj(rowj[r]), v[j]));
+        for (int r = j + 1; r < WNM; ++r) {
+            const E rj = wshfl<E>(vj, r);
+            if (r <= lane && lane < n) v.set(r, O::sub(v.get(r), O::mul(O::conj(rj), vj)));
+        }
     }
     if (lane < n)
 #pragma unroll
         for (int r = 0; r < WNM; ++r)
-            if (r < n) g[r + (long)c * n] = v[r];
+            if (r < n) g[r + (long)c * n] = v.get(r);
     if (lane == 0) info[mi] = bad;
 }
 
@@ -322,20 +342,20 @@ __global__ void __launch_bounds__(256) gesv_wave_kernel(E *a, int n, long k, E *
     if (mi >= k) return;
     E *g = a + mi * n * n;
     const int c = lane < n ? lane : 0;
-    E v[WNM];
+    Col<E, WNM> v;
 #pragma unroll
-    for (int r = 0; r < WNM; ++r) v[r] = r < n ? g[r + (long)c * n] : O::real(0);
+    for (int r = 0; r < WNM; ++r) v.set(r, r < n ? g[r + (long)c * n] : O::real(0));
     int bad = 0;
 #pragma unroll
     for (int j = 0; j < WNM; ++j) {
-        if (j >= n) break;
+        if (j >= n || bad) continue;
         // pivot: the largest |re| + |im| in column j at or below the diagonal, first on ties
         double bv = -1;
         int bi = j;
 #pragma unroll
         for (int r = j; r < WNM; ++r)
             if (r < n) {
-                const double t = O::abs1(v[r]);
+                const double t = O::abs1(v.get(r));
                 if (t > bv) {
                     bv = t;
                     bi = r;
@@ -346,36 +366,37 @@ __global__ void __launch_bounds__(256) gesv_wave_kernel(E *a, int n, long k, E *
         if (lane == 0) piv_s[w][j] = p;
         if (!(pv > 0)) {
             bad = j + 1;
-            break;
+            continue;
         }
         if (p != j) {
-            E vp = v[j];
+            E vp = v.get(j);
 #pragma unroll
             for (int r = j + 1; r < WNM; ++r)
-                if (r == p) vp = v[r];
+                if (r == p) vp = v.get(r);
 #pragma unroll
             for (int r = j + 1; r < WNM; ++r)
-                if (r == p) v[r] = v[j];
-            v[j] = vp;
+                if (r == p) v.set(r, v.get(j));
+            v.set(j, vp);
         }
-        const E d = wshfl<E>(v[j], j);
+        const E d = wshfl<E>(v.get(j), j);
         if (lane == j)
 #pragma unroll
             for (int r = j + 1; r < WNM; ++r)
-                if (r < n) v[r] = O::div(v[r], d);
+                if (r < n) v.set(r, O::div(v.get(r), d));
+        const E vj = v.get(j);
 #pragma unroll
         for (int r = j + 1; r < WNM; ++r) {
-            if (r >= n) break;
-            const E l = wshfl<E>(v[r], j);
-            if (lane > j && lane < n) v[r] = O::sub(v[r], O::mul(l, v[j]));
+            if (r >= n) continue;
+            const E l = wshfl<E>(v.get(r), j);
+            if (lane > j && lane < n) v.set(r, O::sub(v.get(r), O::mul(l, vj)));
         }
     }
     if (lane < n)
 #pragma unroll
         for (int r = 0; r < WNM; ++r)
             if (r < n) {
-                g[r + (long)c * n] = v[r];
-                lu_s[w][r + c * n] = v[r];
+                g[r + (long)c * n] = v.get(r);
+                lu_s[w][r + c * n] = v.get(r);
             }
     if (!bad && b) {
         // (the wave's LDS writes above are ordered before its reads below)
@@ -383,48 +404,48 @@ __global__ void __launch_bounds__(256) gesv_wave_kernel(E *a, int n, long k, E *
         E *B = b + mi * n * m;
         for (long col = lane; col < m; col += 64) {
             E *xg = B + col * n;
-            E x[WNM];
+            Col<E, WNM> x;
 #pragma unroll
             for (int r = 0; r < WNM; ++r)
-                x[r] = r < n ? (identity ? (r == col ? O::one() : O::real(0)) : xg[r]) : O::real(0);
+                x.set(r, r < n ? (identity ? (r == col ? O::one() : O::real(0)) : xg[r]) : O::real(0));
 #pragma unroll
             for (int j = 0; j < WNM; ++j) {
-                if (j >= n) break;
+                if (j >= n) continue;
                 const int p = piv_s[w][j];
                 if (p != j) {
-                    E xp = x[j];
+                    E xp = x.get(j);
 #pragma unroll
                     for (int r = j + 1; r < WNM; ++r)
-                        if (r == p) xp = x[r];
+                        if (r == p) xp = x.get(r);
 #pragma unroll
                     for (int r = j + 1; r < WNM; ++r)
-                        if (r == p) x[r] = x[j];
-                    x[j] = xp;
+                        if (r == p) x.set(r, x.get(j));
+                    x.set(j, xp);
                 }
             }
 #pragma unroll
             for (int r = 0; r < WNM; ++r) {
-                if (r >= n) break;
-                E t = x[r];
+                if (r >= n) continue;
+                E t = x.get(r);
 #pragma unroll
-                for (int q = 0; q < r; ++q) t = O::sub(t, O::mul(M[r + q * n], x[q]));
-                x[r] = t;
+                for (int q = 0; q < r; ++q) t = O::sub(t, O::mul(M[r + q * n], x.get(q)));
+                x.set(r, t);
             }
 #pragma unroll
             for (int r = WNM - 1; r >= 0; --r) {
                 if (r >= n) continue;
-                E t = x[r];
+                E t = x.get(r);
 #pragma unroll
                 for (int q = r + 1; q < WNM; ++q)
-                    if (q < n) t = O::sub(t, O::mul(M[r + q * n], x[q]));
-                x[r] = O::div(t, M[r + r * n]);
+                    if (q < n) t = O::sub(t, O::mul(M[r + q * n], x.get(q)));
+                x.set(r, O::div(t, M[r + r * n]));
             }
             if (alpha_re != 1 || alpha_im != 0)
 #pragma unroll
-                for (int r = 0; r < WNM; ++r) x[r] = scale_by<E>(x[r], alpha_re, alpha_im);
+                for (int r = 0; r < WNM; ++r) x.set(r, scale_by<E>(x.get(r), alpha_re, alpha_im));
 #pragma unroll
             for (int r = 0; r < WNM; ++r)
-                if (r < n) xg[r] = x[r];
+                if (r < n) xg[r] = x.get(r);
         }
     }
     if (lane == 0) info[mi] = bad;

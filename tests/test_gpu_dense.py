@@ -74,14 +74,28 @@ def test_golden_dense_solve(gpu, case):
 
 
 @pytest.mark.parametrize("dtype", [np.complex128, np.float64, np.complex64, np.float32])
-@pytest.mark.parametrize("n", [5, 100])
-def test_dense_types_sizes(gpu, dtype, n):
-    """n = 100 exceeds the LDS staging (global-memory path for complex<double> / double)."""
+@pytest.mark.parametrize("n,wave", [(5, 1), (5, 0), (12, 1), (12, 0), (16, 1), (3, 1), (100, 1)])
+def test_dense_types_sizes(gpu, dtype, n, wave):
+    """Up to 16 x 16 a wave per matrix (dense.wave 1; 0: the workgroup-per-matrix kernels);
+    n = 100 exceeds the LDS staging (global-memory path for complex<double> / double)."""
     import torch
     import superbblas_amd as sb
     from _common import oracle_getrf, oracle_getrs, oracle_potrf
     from _dense import dense_input
-    nt = 3
+    old = sb.tune_get("dense.wave")
+    sb.tune_set("dense.wave", wave)
+    try:
+        _types_sizes(gpu, dtype, n)
+    finally:
+        sb.tune_set("dense.wave", old)
+
+
+def _types_sizes(gpu, dtype, n):
+    import torch
+    import superbblas_amd as sb
+    from _common import oracle_getrf, oracle_getrs, oracle_potrf
+    from _dense import dense_input
+    nt = 6
     full = [([0, 0, 0], [nt, n, n])]
     dim = [nt, n, n]
     # Cholesky of an HPD matrix (tij: the column index fastest in memory)
