@@ -253,9 +253,9 @@ __global__ void __launch_bounds__(DTH) trsm_kernel(const E *a, long n, E *x, lon
     }
 }
 
-// Small matrices (n <= WNM: the 12x12 spin-color blocks of a lattice, 3x3 color blocks): one
-// wave per matrix, four per workgroup, no barrier.  Lane c < n holds column c in registers; a
-// step's pivot, multipliers and row are broadcast across the wave (the source lane is uniform),
+// Small matrices (n <= 16: the 12x12 spin-color blocks of a lattice, 3x3 color blocks): 64 / n
+// matrices per wave, four waves per workgroup, no barrier.  A lane holds one column of one
+// matrix in registers; a step's pivot, multipliers and row are shuffled from the matrix's lanes,
 // so the factorisation is wave-synchronous.  The arithmetic is the block kernels' operation for
 // operation (same pivots, same multiply / subtract order), so results agree with them bit for bit
 // up to the compiler's contraction choices.  The solve keeps one right-hand side per lane, the
@@ -290,44 +290,45 @@ template <typename E, typename R, int N> struct CCol {
 template <int N> struct Col<double2, N> : CCol<double2, double, N> {};
 template <int N> struct Col<float2, N> : CCol<float2, float, N> {};
 
+// A wave holds G = 64 / n matrices: lane l = n s + c is column c of slot s (lanes past G n
+// idle); slots past the batch hold the identity and write nothing.
 template <typename E, int WNM>
 __global__ void __launch_bounds__(256) potrf_wave_kernel(E *a, int n, long k, int *info) {
     typedef DOps<E> O;
-    const int lane = threadIdx.x & 63;
-    const long mi = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (mi >= k) return;
-    E *g = a + mi * n * n;
-    const int c = lane < n ? lane : 0;
+    const int lane = threadIdx.x & 63, G = 64 / n;
+    const int s = lane / n, c = lane - s * n, s0 = s * n;
+    const long mi = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * G + s;
+    const bool valid = s < G && mi < k;
+    E *g = a + (valid ? mi : 0) * n * n;
     Col<E, WNM> v;
 #pragma unroll
-    for (int r = 0; r < WNM; ++r) v.set(r, r < n ? g[r + (long)c * n] : O::real(0));
+    for (int r = 0; r < WNM; ++r)
+        v.set(r, r < n ? (valid ? g[r + (long)c * n] : (r == c ? O::one() : O::real(0))) : O::real(0));
     int bad = 0;
     // (no early exits: constant trip counts, so the loops unroll fully and the columns stay in
     // registers; with breaks the 12- and 16-row complex forms went to scratch)
 #pragma unroll
     for (int j = 0; j < WNM; ++j) {
-        if (j >= n || bad) continue;
-        double d = wshfl<double>(O::re(v.get(j)), j);
-        if (!(d > 0)) {
-            bad = j + 1;
-            continue;
-        }
-        d = sqrt(d);
-        if (lane == j) v.set(j, O::real(d));
-        if (lane > j) v.set(j, O::divr(v.get(j), d));
+        if (j >= n) continue;
+        double d = wshfl<double>(O::re(v.get(j)), s0 + j);
+        const bool ok = !bad && d > 0;
+        if (!bad && !(d > 0)) bad = j + 1;
+        d = sqrt(ok ? d : 1.0);
+        if (ok && c == j) v.set(j, O::real(d));
+        if (ok && c > j) v.set(j, O::divr(v.get(j), d));
         const E vj = v.get(j);
-        // row j of U: element r from lane r
+        // row j of U: element r from the slot's lane r
 #pragma unroll
         for (int r = j + 1; r < WNM; ++r) {
-            const E rj = wshfl<E>(vj, r);
-            if (r <= lane && lane < n) v.set(r, O::sub(v.get(r), O::mul(O::conj(rj), vj)));
+            const E rj = wshfl<E>(vj, s0 + r);
+            if (ok && r <= c && r < n) v.set(r, O::sub(v.get(r), O::mul(O::conj(rj), vj)));
         }
     }
-    if (lane < n)
+    if (valid)
 #pragma unroll
         for (int r = 0; r < WNM; ++r)
             if (r < n) g[r + (long)c * n] = v.get(r);
-    if (lane == 0) info[mi] = bad;
+    if (valid && c == 0) info[mi] = bad;
 }
 
 template <typename E, int WNM>
@@ -335,20 +336,21 @@ __global__ void __launch_bounds__(256) gesv_wave_kernel(E *a, int n, long k, E *
                                                         double alpha_re, double alpha_im,
                                                         int *info) {
     typedef DOps<E> O;
-    __shared__ E lu_s[4][WNM * WNM];
-    __shared__ int piv_s[4][WNM];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const long mi = (long)blockIdx.x * 4 + w;
-    if (mi >= k) return;
-    E *g = a + mi * n * n;
-    const int c = lane < n ? lane : 0;
+    __shared__ E lu_s[4][64 * WNM];
+    __shared__ int piv_s[4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, G = 64 / n;
+    const int s = lane / n, c = lane - s * n, s0 = s * n;
+    const long mi = ((long)blockIdx.x * 4 + w) * G + s;
+    const bool valid = s < G && mi < k;
+    E *g = a + (valid ? mi : 0) * n * n;
     Col<E, WNM> v;
 #pragma unroll
-    for (int r = 0; r < WNM; ++r) v.set(r, r < n ? g[r + (long)c * n] : O::real(0));
+    for (int r = 0; r < WNM; ++r)
+        v.set(r, r < n ? (valid ? g[r + (long)c * n] : (r == c ? O::one() : O::real(0))) : O::real(0));
     int bad = 0;
 #pragma unroll
     for (int j = 0; j < WNM; ++j) {
-        if (j >= n || bad) continue;
+        if (j >= n) continue;
         // pivot: the largest |re| + |im| in column j at or below the diagonal, first on ties
         double bv = -1;
         int bi = j;
@@ -361,14 +363,12 @@ __global__ void __launch_bounds__(256) gesv_wave_kernel(E *a, int n, long k, E *
                     bi = r;
                 }
             }
-        const int p = __shfl(bi, j);
-        const double pv = __shfl(bv, j);
-        if (lane == 0) piv_s[w][j] = p;
-        if (!(pv > 0)) {
-            bad = j + 1;
-            continue;
-        }
-        if (p != j) {
+        const int p = __shfl(bi, s0 + j);
+        const double pv = __shfl(bv, s0 + j);
+        if (!bad && c == 0 && s < G) piv_s[w][s0 + j] = p;
+        const bool ok = !bad && pv > 0;
+        if (!bad && !(pv > 0)) bad = j + 1;
+        if (ok && p != j) {
             E vp = v.get(j);
 #pragma unroll
             for (int r = j + 1; r < WNM; ++r)
@@ -378,8 +378,8 @@ __global__ void __launch_bounds__(256) gesv_wave_kernel(E *a, int n, long k, E *
                 if (r == p) v.set(r, v.get(j));
             v.set(j, vp);
         }
-        const E d = wshfl<E>(v.get(j), j);
-        if (lane == j)
+        const E d = wshfl<E>(v.get(j), s0 + j);
+        if (ok && c == j)
 #pragma unroll
             for (int r = j + 1; r < WNM; ++r)
                 if (r < n) v.set(r, O::div(v.get(r), d));
@@ -387,22 +387,23 @@ __global__ void __launch_bounds__(256) gesv_wave_kernel(E *a, int n, long k, E *
 #pragma unroll
         for (int r = j + 1; r < WNM; ++r) {
             if (r >= n) continue;
-            const E l = wshfl<E>(v.get(r), j);
-            if (lane > j && lane < n) v.set(r, O::sub(v.get(r), O::mul(l, vj)));
+            const E l = wshfl<E>(v.get(r), s0 + j);
+            if (ok && c > j) v.set(r, O::sub(v.get(r), O::mul(l, vj)));
         }
     }
-    if (lane < n)
+    if (s < G)
 #pragma unroll
         for (int r = 0; r < WNM; ++r)
             if (r < n) {
-                g[r + (long)c * n] = v.get(r);
-                lu_s[w][r + c * n] = v.get(r);
+                if (valid) g[r + (long)c * n] = v.get(r);
+                lu_s[w][s0 * n + r + c * n] = v.get(r);
             }
-    if (!bad && b) {
+    if (valid && !bad && b) {
         // (the wave's LDS writes above are ordered before its reads below)
-        const E *M = lu_s[w];
+        const E *M = lu_s[w] + s0 * n;
+        const int *piv = piv_s[w] + s0;
         E *B = b + mi * n * m;
-        for (long col = lane; col < m; col += 64) {
+        for (long col = c; col < m; col += n) {
             E *xg = B + col * n;
             Col<E, WNM> x;
 #pragma unroll
@@ -411,7 +412,7 @@ __global__ void __launch_bounds__(256) gesv_wave_kernel(E *a, int n, long k, E *
 #pragma unroll
             for (int j = 0; j < WNM; ++j) {
                 if (j >= n) continue;
-                const int p = piv_s[w][j];
+                const int p = piv[j];
                 if (p != j) {
                     E xp = x.get(j);
 #pragma unroll
@@ -448,7 +449,7 @@ __global__ void __launch_bounds__(256) gesv_wave_kernel(E *a, int n, long k, E *
                 if (r < n) xg[r] = x.get(r);
         }
     }
-    if (lane == 0) info[mi] = bad;
+    if (valid && c == 0) info[mi] = bad;
 }
 
 template <typename E> bool fits_lds(long n) { return n * n * (long)sizeof(E) <= DENSE_LDS_BYTES; }
@@ -456,7 +457,8 @@ template <typename E> bool fits_lds(long n) { return n * n * (long)sizeof(E) <= 
 template <typename E> void potrf_typed(void *a, long n, long k, int *info, hipStream_t s) {
     if (n <= WNMAX && g_dense_wave) {
         auto go = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3((unsigned)((k + 3) / 4)), dim3(256), 0, s, (E *)a, (int)n, k, info);
+            const long per = 4 * (64 / n);
+            hipLaunchKernelGGL(kern, dim3((unsigned)((k + per - 1) / per)), dim3(256), 0, s, (E *)a, (int)n, k, info);
         };
         if (n <= 4) go(potrf_wave_kernel<E, 4>);
         else if (n <= 8) go(potrf_wave_kernel<E, 8>);
@@ -475,7 +477,8 @@ void gesv_typed(void *a, long n, long k, void *b, long m, bool identity, const S
                 int *ipiv, int *info, hipStream_t s) {
     if (n <= WNMAX && g_dense_wave) {
         auto go = [&](auto kern) {
-            hipLaunchKernelGGL(kern, dim3((unsigned)((k + 3) / 4)), dim3(256), 0, s, (E *)a, (int)n, k,
+            const long per = 4 * (64 / n);
+            hipLaunchKernelGGL(kern, dim3((unsigned)((k + per - 1) / per)), dim3(256), 0, s, (E *)a, (int)n, k,
                                (E *)b, m, identity ? 1 : 0, alpha.re, alpha.im, info);
         };
         if (n <= 4) go(gesv_wave_kernel<E, 4>);
