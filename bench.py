@@ -397,7 +397,7 @@ def main():
     side = {}
     skip = set(x for x in args.skip.split(",") if x)
     if args.no_side:
-        skip |= {"permute", "bsr", "wilson", "chain", "3m", "chain_dist", "redistribution"}
+        skip |= {"permute", "bsr", "wilson", "chain", "3m", "chain_dist", "redistribution", "dense"}
     if world == 1 and "permute" not in skip:
         side.update(permute_bench(sb, dev, 16, 64))
     if world == 1 and "bsr" not in skip:
@@ -407,6 +407,11 @@ def main():
             side.update(wilson_bench(sb, dev, 16))
         except Exception as e:  # a side measurement never takes the bench down
             side["wilson_error"] = str(e)[:200]
+    if world == 1 and "dense" not in skip:
+        try:
+            side.update(dense_bench(sb, dev))
+        except Exception as e:  # a side measurement never takes the bench down
+            side["dense_error"] = str(e)[:200]
     if world == 1 and "chain" not in skip:
         try:
             side.update(chain_bench(sb, dev))
@@ -1181,6 +1186,49 @@ def chain_dist_bench(sb, dev, comm, world, rank, grid, barrier, Ls=16, Lt=64, nc
 
 def dist_available():
     return torch.distributed.is_available() and torch.distributed.is_initialized()
+
+
+def dense_bench(sb, dev, L=16, n=12, reps=5):
+    """The dense batched solvers on one 12x12 complex<double> matrix per site of
+    the 16^4 lattice (tools/dense_bench.py): inversion and Cholesky, kernel time from the
+    library's timers and the whole call (layout copies included); bytes = the matrices in and
+    out once."""
+    nb = L ** 4
+    dim = [nb, n, n]
+    full = [([0, 0, 0], dim)]
+    g = torch.Generator(device=dev).manual_seed(7)
+    a = torch.randn(nb, n, n, dtype=torch.complex128, device=dev, generator=g)
+    a0 = (a @ a.conj().transpose(1, 2) + n * torch.eye(n, dtype=torch.complex128, device=dev)).reshape(-1)
+    del a
+    v = torch.empty_like(a0)
+    out = {}
+    for op in ("inversion", "cholesky"):
+        def f():
+            v.copy_(a0)
+            getattr(sb, op)(full, dim, "tij", [v], "i", "j")
+        for _ in range(3):
+            f()
+        torch.cuda.synchronize()
+        sb.timings_enable(True)
+        sb.timings_filter("dense")
+        sb.timings_reset()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            f()
+        torch.cuda.synchronize()
+        call = (time.perf_counter() - t0) / reps
+        ms, calls = sb.timings_get("dense")
+        sb.timings_enable(False)
+        sb.timings_filter(None)
+        kern = ms / max(calls, 1) / 1e3
+        by = 2.0 * nb * n * n * 16
+        out.update({"dense_%s_12x12_kernel_us" % op: round(kern * 1e6, 1),
+                    "dense_%s_12x12_kernel_GBps" % op: round(by / kern / 1e9, 1),
+                    "dense_%s_12x12_call_us" % op: round(call * 1e6, 1)})
+    if sb.tune_get("dense.wave"):
+        out["dense_kernel"] = "potrf_wave_kernel / gesv_wave_kernel (64 / n matrices per wave)"
+    out["dense_workload"] = "16^4 matrices of 12x12 complex<double> (one per site), tij, rows i"
+    return out
 
 
 def wilson_bench(sb, dev, L, ncols=12, reps=5):
