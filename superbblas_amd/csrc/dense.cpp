@@ -25,12 +25,13 @@ struct Work {
     DistTensor t;
     std::vector<Scratch> bufs;
     long n = 0;
+    bool rm = false; // matrices row-major (batch, rows, columns): the caller's own order
     std::string ot; // batch labels (in the tensor's order)
 };
 
 /// Working copy of a tensor of square matrices (prepare_for_cholesky, dense.h:507-560)
 Work prepare(const DistTensor &v, const std::string &orows, const std::string &ocols,
-             const Comm &comm, bool copy_in, const char *what) {
+             const Comm &comm, bool copy_in, const char *what, bool allow_rm = false) {
     for (char c : orows) {
         if (has(ocols, c)) throw Error("Invalid `orows' and `ocols': they share labels");
         if (!has(v.labels, c)) throw Error("Invalid `orows': invalid labels");
@@ -40,13 +41,16 @@ Work prepare(const DistTensor &v, const std::string &orows, const std::string &o
     Work w;
     for (char c : v.labels)
         if (!has(orows, c) && !has(ocols, c)) w.ot += c;
-    const std::string ow = w.ot + ocols + orows;
     long n = 1, m = 1;
     for (char c : orows) n *= v.dim[v.labels.find(c)];
     for (char c : ocols) m *= v.dim[v.labels.find(c)];
     // (the reference builds this error without throwing it, dense.h:543; a non-square shape is
     // rejected here)
     if (n != m) throw Error(std::string(what) + ": the matrices to factorize should be square");
+    // a caller whose matrices are already whole and row-major (batch, rows, columns) keeps its
+    // order: the working copies are then plain copies instead of transposes (small-matrix kernels)
+    w.rm = allow_rm && v.labels == w.ot + orows + ocols && dense_wave_rows(n);
+    const std::string ow = w.rm ? w.ot + orows + ocols : w.ot + ocols + orows;
     w.n = n;
     w.t.labels = ow;
     w.t.dtype = v.dtype;
@@ -97,17 +101,17 @@ void check_dims(const DistTensor &a, const DistTensor &b) {
 
 void dense_cholesky(const DistTensor &v, const std::string &orows, const std::string &ocols,
                     const Comm &comm) {
-    Work w = prepare(v, orows, ocols, comm, true, "cholesky");
+    Work w = prepare(v, orows, ocols, comm, true, "cholesky", true);
     for (std::size_t c = 0; c < w.t.ptr.size(); ++c) {
         const long k = w.n ? volume(w.t.ranges[comm.rank][c].size) / (w.n * w.n) : 0;
-        check_info(launch_potrf(v.dtype, w.t.ptr[c], w.n, k, w.t.dev[c]));
+        check_info(launch_potrf(v.dtype, w.t.ptr[c], w.n, k, w.t.dev[c], w.rm));
     }
     dist_copy(Scalar{1, 0}, w.t, Coor(w.t.nd(), 0), w.t.dim, v, Coor(v.nd(), 0), false, comm);
 }
 
 void dense_inversion(const DistTensor &v, const std::string &orows, const std::string &ocols,
                      const Comm &comm) {
-    Work w = prepare(v, orows, ocols, comm, true, "inversion");
+    Work w = prepare(v, orows, ocols, comm, true, "inversion", true);
     std::vector<Scratch> inv;
     DistTensor wi = w.t;
     for (std::size_t c = 0; c < w.t.ptr.size(); ++c) {
@@ -115,7 +119,7 @@ void dense_inversion(const DistTensor &v, const std::string &orows, const std::s
         inv.emplace_back(w.bufs[c].bytes, w.t.dev[c]);
         wi.ptr[c] = inv.back().ptr;
         check_info(launch_gesv(v.dtype, w.t.ptr[c], w.n, k, wi.ptr[c], w.n, true, Scalar{1, 0},
-                               w.t.dev[c]));
+                               w.t.dev[c], w.rm));
     }
     dist_copy(Scalar{1, 0}, wi, Coor(wi.nd(), 0), wi.dim, v, Coor(v.nd(), 0), false, comm);
 }

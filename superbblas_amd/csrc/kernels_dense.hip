@@ -293,7 +293,7 @@ template <int N> struct Col<float2, N> : CCol<float2, float, N> {};
 // A wave holds G = 64 / n matrices: lane l = n s + c is column c of slot s (lanes past G n
 // idle); slots past the batch hold the identity and write nothing.
 template <typename E, int WNM>
-__global__ void __launch_bounds__(256) potrf_wave_kernel(E *a, int n, long k, int *info) {
+__global__ void __launch_bounds__(256) potrf_wave_kernel(E *a, int n, long k, int *info, int rm) {
     typedef DOps<E> O;
     const int lane = threadIdx.x & 63, G = 64 / n;
     const int s = lane / n, c = lane - s * n, s0 = s * n;
@@ -303,7 +303,8 @@ __global__ void __launch_bounds__(256) potrf_wave_kernel(E *a, int n, long k, in
     Col<E, WNM> v;
 #pragma unroll
     for (int r = 0; r < WNM; ++r)
-        v.set(r, r < n ? (valid ? g[r + (long)c * n] : (r == c ? O::one() : O::real(0))) : O::real(0));
+        v.set(r, r < n ? (valid ? g[rm ? c + (long)r * n : r + (long)c * n] : (r == c ? O::one() : O::real(0)))
+                       : O::real(0));
     int bad = 0;
     // (no early exits: constant trip counts, so the loops unroll fully and the columns stay in
     // registers; with breaks the 12- and 16-row complex forms went to scratch)
@@ -327,14 +328,14 @@ __global__ void __launch_bounds__(256) potrf_wave_kernel(E *a, int n, long k, in
     if (valid)
 #pragma unroll
         for (int r = 0; r < WNM; ++r)
-            if (r < n) g[r + (long)c * n] = v.get(r);
+            if (r < n) g[rm ? c + (long)r * n : r + (long)c * n] = v.get(r);
     if (valid && c == 0) info[mi] = bad;
 }
 
 template <typename E, int WNM>
 __global__ void __launch_bounds__(256) gesv_wave_kernel(E *a, int n, long k, E *b, long m, int identity,
                                                         double alpha_re, double alpha_im,
-                                                        int *info) {
+                                                        int *info, int rm) {
     typedef DOps<E> O;
     __shared__ E lu_s[4][64 * WNM];
     __shared__ int piv_s[4][64];
@@ -346,7 +347,8 @@ __global__ void __launch_bounds__(256) gesv_wave_kernel(E *a, int n, long k, E *
     Col<E, WNM> v;
 #pragma unroll
     for (int r = 0; r < WNM; ++r)
-        v.set(r, r < n ? (valid ? g[r + (long)c * n] : (r == c ? O::one() : O::real(0))) : O::real(0));
+        v.set(r, r < n ? (valid ? g[rm ? c + (long)r * n : r + (long)c * n] : (r == c ? O::one() : O::real(0)))
+                       : O::real(0));
     int bad = 0;
 #pragma unroll
     for (int j = 0; j < WNM; ++j) {
@@ -395,7 +397,7 @@ __global__ void __launch_bounds__(256) gesv_wave_kernel(E *a, int n, long k, E *
 #pragma unroll
         for (int r = 0; r < WNM; ++r)
             if (r < n) {
-                if (valid) g[r + (long)c * n] = v.get(r);
+                if (valid) g[rm ? c + (long)r * n : r + (long)c * n] = v.get(r);
                 lu_s[w][s0 * n + r + c * n] = v.get(r);
             }
     if (valid && !bad && b) {
@@ -404,11 +406,13 @@ __global__ void __launch_bounds__(256) gesv_wave_kernel(E *a, int n, long k, E *
         const int *piv = piv_s[w] + s0;
         E *B = b + mi * n * m;
         for (long col = c; col < m; col += n) {
-            E *xg = B + col * n;
+            // column col of the n x m right-hand side: column-major, or row-major (rm)
+            E *xg = rm ? B + col : B + col * n;
+            const long xs = rm ? m : 1;
             Col<E, WNM> x;
 #pragma unroll
             for (int r = 0; r < WNM; ++r)
-                x.set(r, r < n ? (identity ? (r == col ? O::one() : O::real(0)) : xg[r]) : O::real(0));
+                x.set(r, r < n ? (identity ? (r == col ? O::one() : O::real(0)) : xg[r * xs]) : O::real(0));
 #pragma unroll
             for (int j = 0; j < WNM; ++j) {
                 if (j >= n) continue;
@@ -446,7 +450,7 @@ __global__ void __launch_bounds__(256) gesv_wave_kernel(E *a, int n, long k, E *
                 for (int r = 0; r < WNM; ++r) x.set(r, scale_by<E>(x.get(r), alpha_re, alpha_im));
 #pragma unroll
             for (int r = 0; r < WNM; ++r)
-                if (r < n) xg[r] = x.get(r);
+                if (r < n) xg[r * xs] = x.get(r);
         }
     }
     if (valid && c == 0) info[mi] = bad;
@@ -454,11 +458,12 @@ __global__ void __launch_bounds__(256) gesv_wave_kernel(E *a, int n, long k, E *
 
 template <typename E> bool fits_lds(long n) { return n * n * (long)sizeof(E) <= DENSE_LDS_BYTES; }
 
-template <typename E> void potrf_typed(void *a, long n, long k, int *info, hipStream_t s) {
+template <typename E> void potrf_typed(void *a, long n, long k, int *info, bool rm, hipStream_t s) {
     if (n <= WNMAX && g_dense_wave) {
         auto go = [&](auto kern) {
             const long per = 4 * (64 / n);
-            hipLaunchKernelGGL(kern, dim3((unsigned)((k + per - 1) / per)), dim3(256), 0, s, (E *)a, (int)n, k, info);
+            hipLaunchKernelGGL(kern, dim3((unsigned)((k + per - 1) / per)), dim3(256), 0, s, (E *)a, (int)n, k, info,
+                               rm ? 1 : 0);
         };
         if (n <= 4) go(potrf_wave_kernel<E, 4>);
         else if (n <= 8) go(potrf_wave_kernel<E, 8>);
@@ -467,6 +472,7 @@ template <typename E> void potrf_typed(void *a, long n, long k, int *info, hipSt
         SBX_HIP_CHECK(hipGetLastError());
         return;
     }
+    if (rm) throw Error("dense: internal error (row-major matrices need the wave kernels)");
     const bool lds = fits_lds<E>(n);
     hipLaunchKernelGGL(potrf_kernel<E>, dim3((unsigned)k), dim3(DTH),
                        lds ? (size_t)(n * n * sizeof(E)) : 0, s, (E *)a, n, lds ? 1 : 0, info);
@@ -474,12 +480,12 @@ template <typename E> void potrf_typed(void *a, long n, long k, int *info, hipSt
 }
 template <typename E>
 void gesv_typed(void *a, long n, long k, void *b, long m, bool identity, const Scalar &alpha,
-                int *ipiv, int *info, hipStream_t s) {
+                int *ipiv, int *info, bool rm, hipStream_t s) {
     if (n <= WNMAX && g_dense_wave) {
         auto go = [&](auto kern) {
             const long per = 4 * (64 / n);
             hipLaunchKernelGGL(kern, dim3((unsigned)((k + per - 1) / per)), dim3(256), 0, s, (E *)a, (int)n, k,
-                               (E *)b, m, identity ? 1 : 0, alpha.re, alpha.im, info);
+                               (E *)b, m, identity ? 1 : 0, alpha.re, alpha.im, info, rm ? 1 : 0);
         };
         if (n <= 4) go(gesv_wave_kernel<E, 4>);
         else if (n <= 8) go(gesv_wave_kernel<E, 8>);
@@ -488,6 +494,7 @@ void gesv_typed(void *a, long n, long k, void *b, long m, bool identity, const S
         SBX_HIP_CHECK(hipGetLastError());
         return;
     }
+    if (rm) throw Error("dense: internal error (row-major matrices need the wave kernels)");
     const bool lds = fits_lds<E>(n);
     hipLaunchKernelGGL(gesv_kernel<E>, dim3((unsigned)k), dim3(DTH),
                        lds ? (size_t)(n * n * sizeof(E)) : 0, s, (E *)a, n, (E *)b, m,
@@ -527,7 +534,9 @@ template <typename F> void dispatch(int t, F &&f) {
 
 } // namespace
 
-int launch_potrf(int t, void *a, long n, long k, int device) {
+bool dense_wave_rows(long n) { return n <= WNMAX && g_dense_wave; }
+
+int launch_potrf(int t, void *a, long n, long k, int device, bool rm) {
     if (n == 0 || k == 0) return 0;
     if (k >= (1L << 31)) throw Error("dense: too many matrices");
     set_device(device);
@@ -535,13 +544,13 @@ int launch_potrf(int t, void *a, long n, long k, int device) {
     Scratch info(sizeof(int) * k, device);
     {
         KernelTimer timer("dense", s);
-        dispatch(t, [&](auto z) { potrf_typed<decltype(z)>(a, n, k, (int *)info.ptr, s); });
+        dispatch(t, [&](auto z) { potrf_typed<decltype(z)>(a, n, k, (int *)info.ptr, rm, s); });
     }
     return first_info((const int *)info.ptr, k, s);
 }
 
 int launch_gesv(int t, void *a, long n, long k, void *b, long m, bool identity,
-                const Scalar &alpha, int device) {
+                const Scalar &alpha, int device, bool rm) {
     if (n == 0 || k == 0) return 0;
     if (k >= (1L << 31)) throw Error("dense: too many matrices");
     set_device(device);
@@ -551,7 +560,7 @@ int launch_gesv(int t, void *a, long n, long k, void *b, long m, bool identity,
         KernelTimer timer("dense", s);
         dispatch(t, [&](auto z) {
             gesv_typed<decltype(z)>(a, n, k, b, m, identity, alpha, (int *)ipiv.ptr,
-                                    (int *)info.ptr, s);
+                                    (int *)info.ptr, rm, s);
         });
     }
     return first_info((const int *)info.ptr, k, s);

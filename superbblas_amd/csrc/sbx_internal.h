@@ -323,12 +323,14 @@ struct BsrDesc {
 };
 void launch_bsr(const BsrDesc &d, int device);
 void launch_bsr_kron(const BsrDesc &d, int device);
-/// Dense batched solvers on k column-major n x n matrices (kernels_dense.hip); the int results
-/// are the first nonzero LAPACK info of the batch (0: success)
-int launch_potrf(int t, void *a, long n, long k, int device);
+/// Dense batched solvers on k column-major n x n matrices (kernels_dense.hip; rm: row-major
+/// matrices and right-hand sides, possible when dense_wave_rows(n)); the int results are the
+/// first nonzero LAPACK info of the batch (0: success)
+bool dense_wave_rows(long n);
+int launch_potrf(int t, void *a, long n, long k, int device, bool rm = false);
 /// LU + solve: B (n x m per matrix) <- alpha A^-1 B (identity: B starts as I); A gets the LU
 int launch_gesv(int t, void *a, long n, long k, void *b, long m, bool identity,
-                const Scalar &alpha, int device);
+                const Scalar &alpha, int device, bool rm = false);
 /// left: X (n x m) <- alpha U^-1 X;  right: X (m x n) <- alpha X U^-1  (U upper, non-unit)
 void launch_trsm(int t, const void *a, long n, long k, void *x, long m, bool left,
                  const Scalar &alpha, int device);
