@@ -26,6 +26,7 @@ struct Work {
     std::vector<Scratch> bufs;
     long n = 0;
     bool rm = false; // matrices row-major (batch, rows, columns): the caller's own order
+    bool inplace = false; // the working tensor IS the caller's (same order, whole matrices)
     std::string ot; // batch labels (in the tensor's order)
 };
 
@@ -69,6 +70,22 @@ Work prepare(const DistTensor &v, const std::string &orows, const std::string &o
                 }
             w.t.ranges[r].push_back(o);
         }
+    // the caller's order kept and every component already holding whole matrices: work on the
+    // caller's memory (no copies; every rank decides alike from the global ranges)
+    if (w.rm && v.mask.empty()) {
+        bool same = true;
+        for (std::size_t r = 0; r < v.ranges.size() && same; ++r)
+            for (std::size_t c = 0; c < v.ranges[r].size() && same; ++c) {
+                const Range &q = v.ranges[r][c], &o = w.t.ranges[r][c];
+                if (volume(q.size) > 0 && (q.from != o.from || q.size != o.size)) same = false;
+            }
+        if (same) {
+            w.inplace = true;
+            w.t.ptr = v.ptr;
+            w.t.dev = v.dev;
+            return w;
+        }
+    }
     const std::size_t es = dtype_size(v.dtype);
     for (std::size_t c = 0; c < w.t.ranges[comm.rank].size(); ++c) {
         w.bufs.emplace_back(volume(w.t.ranges[comm.rank][c].size) * es, v.dev[c]);
@@ -106,7 +123,8 @@ void dense_cholesky(const DistTensor &v, const std::string &orows, const std::st
         const long k = w.n ? volume(w.t.ranges[comm.rank][c].size) / (w.n * w.n) : 0;
         check_info(launch_potrf(v.dtype, w.t.ptr[c], w.n, k, w.t.dev[c], w.rm));
     }
-    dist_copy(Scalar{1, 0}, w.t, Coor(w.t.nd(), 0), w.t.dim, v, Coor(v.nd(), 0), false, comm);
+    if (!w.inplace)
+        dist_copy(Scalar{1, 0}, w.t, Coor(w.t.nd(), 0), w.t.dim, v, Coor(v.nd(), 0), false, comm);
 }
 
 void dense_inversion(const DistTensor &v, const std::string &orows, const std::string &ocols,
@@ -114,6 +132,21 @@ void dense_inversion(const DistTensor &v, const std::string &orows, const std::s
     Work w = prepare(v, orows, ocols, comm, true, "inversion", true);
     std::vector<Scratch> inv;
     DistTensor wi = w.t;
+    if (w.inplace) {
+        // the factors go to a copy; the inverse straight into the caller's tensor
+        DistTensor lu = w.t;
+        for (std::size_t c = 0; c < w.t.ptr.size(); ++c) {
+            inv.emplace_back(volume(w.t.ranges[comm.rank][c].size) * dtype_size(v.dtype), w.t.dev[c]);
+            lu.ptr[c] = inv.back().ptr;
+        }
+        dist_copy(Scalar{1, 0}, v, Coor(v.nd(), 0), v.dim, lu, Coor(lu.nd(), 0), false, comm);
+        for (std::size_t c = 0; c < w.t.ptr.size(); ++c) {
+            const long k = w.n ? volume(w.t.ranges[comm.rank][c].size) / (w.n * w.n) : 0;
+            check_info(launch_gesv(v.dtype, lu.ptr[c], w.n, k, v.ptr[c], w.n, true, Scalar{1, 0},
+                                   w.t.dev[c], w.rm));
+        }
+        return;
+    }
     for (std::size_t c = 0; c < w.t.ptr.size(); ++c) {
         const long k = w.n ? volume(w.t.ranges[comm.rank][c].size) / (w.n * w.n) : 0;
         inv.emplace_back(w.bufs[c].bytes, w.t.dev[c]);
