@@ -67,6 +67,26 @@ def main():
             print(json.dumps({"case": name, "op": op, "wave": wv, "matrices": nb, "n": n, "dtype": str(dt),
                               "call_us": round(wall * 1e6, 1), "kernel_us": round(kern * 1e6, 1),
                               "kernel_GBps": round(by / kern / 1e9, 1)}), flush=True)
+        # solves with the factor / the matrix: x with C's column labels, 12 right-hand sides
+        nr = 12
+        u = a0.clone().reshape(-1)
+        sb.cholesky(full, dim, "tij", [u], "i", "j")
+        dimx = [nb, n, nr]
+        px = [([0, 0, 0], dimx)]
+        x = torch.randn(nb * n * nr, dtype=dt, device=dev)
+        y = torch.empty_like(x)
+        for op, mat in (("trsm", u), ("gesm", a0.reshape(-1))):
+            wv = sb.tune_get("dense.wave")
+
+            def f():
+                getattr(sb, op)(1.0, full, dim, "tij", [mat], "i", "j", px, dimx, "tjr", [x], px,
+                                dimx, "tir", [y])
+            wall, kern = timed(f)
+            by = 16.0 * nb * n * n * es / 16 + 2.0 * nb * n * nr * es
+            print(json.dumps({"case": name, "op": op, "wave": wv, "matrices": nb, "n": n, "rhs": nr,
+                              "dtype": str(dt), "call_us": round(wall * 1e6, 1),
+                              "kernel_us": round(kern * 1e6, 1),
+                              "kernel_GBps": round(by / kern / 1e9, 1)}), flush=True)
 
 
 if __name__ == "__main__":
