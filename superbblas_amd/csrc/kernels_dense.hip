@@ -456,6 +456,52 @@ __global__ void __launch_bounds__(256) gesv_wave_kernel(E *a, int n, long k, E *
     if (valid && c == 0) info[mi] = bad;
 }
 
+// Triangular solves with small factors (n <= 16): a lane per right-hand side (left: a column of
+// X; right: a row), 64 / m matrices per wave when m <= 64, the factor's elements read by every
+// lane of its matrix (one address per matrix: broadcast loads); the block kernel's operation
+// order.
+template <typename E, int WNM>
+__global__ void __launch_bounds__(256) trsm_wave_kernel(const E *a, int n, long k, E *x, long m, int left,
+                                                        double alpha_re, double alpha_im) {
+    typedef DOps<E> O;
+    const int lane = threadIdx.x & 63;
+    const int per = m <= 64 ? (int)(64 / m) : 1;
+    const int s = m <= 64 ? lane / (int)m : 0;
+    const long mi = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * per + s;
+    if (s >= per || mi >= k) return;
+    const E *U = a + mi * n * n;
+    E *X = x + mi * n * m;
+    for (long t = m <= 64 ? lane - (long)s * m : lane; t < m; t += (m <= 64 ? m : 64)) {
+        Col<E, WNM> v;
+        const long base = left ? t * n : t, st = left ? 1 : m;
+#pragma unroll
+        for (int r = 0; r < WNM; ++r) v.set(r, r < n ? X[base + r * st] : O::real(0));
+        if (left) {
+#pragma unroll
+            for (int r = WNM - 1; r >= 0; --r) {
+                if (r >= n) continue;
+                E w = scale_by<E>(v.get(r), alpha_re, alpha_im);
+#pragma unroll
+                for (int q = r + 1; q < WNM; ++q)
+                    if (q < n) w = O::sub(w, O::mul(U[r + q * n], v.get(q)));
+                v.set(r, O::div(w, U[r + r * n]));
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < WNM; ++c) {
+                if (c >= n) continue;
+                E w = scale_by<E>(v.get(c), alpha_re, alpha_im);
+#pragma unroll
+                for (int q = 0; q < c; ++q) w = O::sub(w, O::mul(v.get(q), U[q + c * n]));
+                v.set(c, O::div(w, U[c + c * n]));
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < WNM; ++r)
+            if (r < n) X[base + r * st] = v.get(r);
+    }
+}
+
 template <typename E> bool fits_lds(long n) { return n * n * (long)sizeof(E) <= DENSE_LDS_BYTES; }
 
 template <typename E> void potrf_typed(void *a, long n, long k, int *info, bool rm, hipStream_t s) {
@@ -504,6 +550,19 @@ void gesv_typed(void *a, long n, long k, void *b, long m, bool identity, const S
 template <typename E>
 void trsm_typed(const void *a, long n, long k, void *x, long m, bool left, const Scalar &alpha,
                 hipStream_t s) {
+    if (n <= WNMAX && g_dense_wave) {
+        const long per = 4 * (m <= 64 ? 64 / m : 1);
+        auto go = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3((unsigned)((k + per - 1) / per)), dim3(256), 0, s, (const E *)a, (int)n,
+                               k, (E *)x, m, left ? 1 : 0, alpha.re, alpha.im);
+        };
+        if (n <= 4) go(trsm_wave_kernel<E, 4>);
+        else if (n <= 8) go(trsm_wave_kernel<E, 8>);
+        else if (n <= 12) go(trsm_wave_kernel<E, 12>);
+        else go(trsm_wave_kernel<E, 16>);
+        SBX_HIP_CHECK(hipGetLastError());
+        return;
+    }
     const bool lds = fits_lds<E>(n);
     hipLaunchKernelGGL(trsm_kernel<E>, dim3((unsigned)k), dim3(DTH),
                        lds ? (size_t)(n * n * sizeof(E)) : 0, s, (const E *)a, n, (E *)x, m,

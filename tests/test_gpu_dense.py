@@ -51,7 +51,21 @@ def test_golden_dense_inplace(gpu, case):
 
 @pytest.mark.parametrize("case", manifest("trsm") + manifest("gesm"),
                          ids=lambda c: "%s%d" % (c["kind"], c["id"]))
-def test_golden_dense_solve(gpu, case):
+@pytest.mark.parametrize("wave", [1, 0])
+def test_golden_dense_solve(gpu, case, wave):
+    """The reference's trsm / gesm outputs, with the small-matrix wave kernels (dense.wave 1)
+    and with the workgroup-per-matrix kernels (0)."""
+    import torch
+    import superbblas_amd as sb
+    old = sb.tune_get("dense.wave")
+    sb.tune_set("dense.wave", wave)
+    try:
+        _golden_solve(gpu, case)
+    finally:
+        sb.tune_set("dense.wave", old)
+
+
+def _golden_solve(gpu, case):
     import torch
     import superbblas_amd as sb
     from _dense import dense_input, from_matrices
