@@ -550,7 +550,7 @@ void gesv_typed(void *a, long n, long k, void *b, long m, bool identity, const S
 template <typename E>
 void trsm_typed(const void *a, long n, long k, void *x, long m, bool left, const Scalar &alpha,
                 hipStream_t s) {
-    if (n <= WNMAX && g_dense_wave) {
+    if (n <= WNMAX && g_dense_wave >= 2) {
         const long per = 4 * (m <= 64 ? 64 / m : 1);
         auto go = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3((unsigned)((k + per - 1) / per)), dim3(256), 0, s, (const E *)a, (int)n,

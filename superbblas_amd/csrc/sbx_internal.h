@@ -276,8 +276,8 @@ struct BsrTune {
     std::atomic<int> last{0};
 };
 extern BsrTune g_bsr_tune;
-/// dense solvers: matrices up to 16 x 16 one wave each, four per workgroup (0 = the
-/// workgroup-per-matrix kernels for every size)
+/// dense solvers: matrices up to 16 x 16 packed 64 / n per wave -- 1: Cholesky and LU
+/// (inversion, gesm), 2: the triangular solves too; 0 = the workgroup-per-matrix kernels
 extern int g_dense_wave;
 
 /// The LDS-DMA overrun class (39cd2bc): a DMA pass writes a whole row of 16-B lanes into LDS --

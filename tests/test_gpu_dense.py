@@ -51,10 +51,10 @@ def test_golden_dense_inplace(gpu, case):
 
 @pytest.mark.parametrize("case", manifest("trsm") + manifest("gesm"),
                          ids=lambda c: "%s%d" % (c["kind"], c["id"]))
-@pytest.mark.parametrize("wave", [1, 0])
+@pytest.mark.parametrize("wave", [2, 1, 0])
 def test_golden_dense_solve(gpu, case, wave):
-    """The reference's trsm / gesm outputs, with the small-matrix wave kernels (dense.wave 1)
-    and with the workgroup-per-matrix kernels (0)."""
+    """The reference's trsm / gesm outputs, with the small-matrix wave kernels (dense.wave 2:
+    the triangular solves too, 1: the LU) and with the workgroup-per-matrix kernels (0)."""
     import torch
     import superbblas_amd as sb
     old = sb.tune_get("dense.wave")
