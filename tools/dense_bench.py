@@ -75,8 +75,9 @@ def main():
         px = [([0, 0, 0], dimx)]
         x = torch.randn(nb * n * nr, dtype=dt, device=dev)
         y = torch.empty_like(x)
-        for op, mat in (("trsm", u), ("gesm", a0.reshape(-1))):
-            wv = sb.tune_get("dense.wave")
+        for op, mat, wv in [(op, mat, wv) for op, mat in (("trsm", u), ("gesm", a0.reshape(-1)))
+                            for wv in [int(x) for x in os.environ.get("WAVE", "1,0").split(",")]]:
+            sb.tune_set("dense.wave", wv)
 
             def f():
                 getattr(sb, op)(1.0, full, dim, "tij", [mat], "i", "j", px, dimx, "tjr", [x], px,
