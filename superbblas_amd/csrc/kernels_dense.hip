@@ -17,7 +17,7 @@
 #include <algorithm>
 
 namespace sbx {
-int g_dense_wave = 2;
+int g_dense_wave = 1;
 namespace {
 
 constexpr int DTH = 256;

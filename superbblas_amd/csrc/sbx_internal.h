@@ -277,7 +277,8 @@ struct BsrTune {
 };
 extern BsrTune g_bsr_tune;
 /// dense solvers: matrices up to 16 x 16 packed 64 / n per wave -- 1: Cholesky and LU
-/// (inversion, gesm), 2: the triangular solves too; 0 = the workgroup-per-matrix kernels
+/// (inversion, gesm; the default), 2: the triangular solves too; 0 = the workgroup-per-matrix
+/// kernels
 extern int g_dense_wave;
 
 /// The LDS-DMA overrun class (39cd2bc): a DMA pass writes a whole row of 16-B lanes into LDS --
