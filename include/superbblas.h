@@ -25,16 +25,33 @@
 
 #include <algorithm>
 #include <array>
+#include <cmath>
 #include <complex>
 #include <cstddef>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <functional>
+#include <iostream>
+#include <limits>
+#include <map>
 #include <memory>
 #include <ostream>
+#include <sstream>
 #include <stdexcept>
 #include <string>
+#include <tuple>
 #include <type_traits>
-#include <cstdlib>
 #include <vector>
+
+// The library always drives AMD GPUs (HIP): callers' GPU sections compile in, as with a reference
+// build configured for HIP (superbblas_flags.h)
+#ifndef SUPERBBLAS_USE_HIP
+#    define SUPERBBLAS_USE_HIP
+#endif
+#ifndef SUPERBBLAS_USE_GPU
+#    define SUPERBBLAS_USE_GPU
+#endif
 
 #ifdef SUPERBBLAS_USE_MPI
 #    include <map>
@@ -61,11 +78,19 @@ enum platform { CPU, CUDA, HIP };
 constexpr int CPU_DEVICE_ID = -1;
 const platform GPU = HIP;
 
+namespace detail {
+struct Cpu;
+struct Hip;
+} // namespace detail
+
 class Context {
 public:
     enum platform plat;
     int device;
     Context(enum platform plat, int device) : plat(plat), device(device) {}
+    /// The low-level contexts of the superbblas::detail surface (platform.h:765-773)
+    detail::Cpu toCpu(Session session) const;
+    detail::Hip toGpu(Session session) const;
 };
 
 inline Context createCpuContext() { return Context{CPU, CPU_DEVICE_ID}; }
@@ -1301,5 +1326,7 @@ template <std::size_t Nd1, typename Q> void close_storage(Storage_handle stoh, M
 #endif // SUPERBBLAS_USE_MPI
 
 } // namespace superbblas
+
+#include "superbblas_amd/detail.h"
 
 #endif // SUPERBBLAS_AMD_SUPERBBLAS_H

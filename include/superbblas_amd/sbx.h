@@ -363,6 +363,34 @@ int sbx_xgemm_batch_strided(int t, char transa, char transb, int m, int n, int k
                             const void *b, int ldb, long long strideb, const double *beta,
                             void *c, int ldc, long long stridec, int batch, int device);
 
+/* xgemm_batch_strided on a context (blas.h:662-810 GPU, blas_cpu_tmpl.hpp:376-478 CPU): a CPU
+   context means host pointers, mirrored through device scratch for the product (complete on
+   return); a GPU context is sbx_xgemm_batch_strided on its device */
+int sbx_xgemm_batch_strided_ctx(int t, char transa, char transb, int m, int n, int k,
+                                const double *alpha, const void *a, int lda, long long stridea,
+                                const void *b, int ldb, long long strideb, const double *beta,
+                                void *c, int ldc, long long stridec, int batch, sbx_context ctx);
+
+/* ---- low-level memory of the superbblas::detail surface (include/superbblas_amd/detail.h) ----
+   A CPU context means host memory (pageable or pinned).  Host destinations are complete on
+   return; device work is enqueued on the library stream of the device. */
+/* copy_n(v, xpu0, n, w, xpu1) (blas.h:170-231): bytes from src to dst (H2H, H2D, D2H, D2D, peer) */
+int sbx_memcpy(void *dst, sbx_context dst_ctx, const void *src, sbx_context src_ctx,
+               unsigned long long bytes);
+/* zero_n (blas.h:436-490) */
+int sbx_memset_zero(void *ptr, sbx_context ctx, unsigned long long bytes);
+/* copy_n / copy_n_blocking with index vectors (copy_n.h:584-1050):
+     w[(iw ? iw[d] : d*blocking) + r] (= | +=) alpha * v[(iv ? iv[d] : d*blocking) + r]
+   for d < n, r < blocking, with the element conversion tv -> tw of copy(); index vectors (int)
+   and data may live on the host or on one device each side */
+int sbx_copy_n_blocking(const double *alpha, int tv, const void *v, sbx_context vctx,
+                        long long blocking, const int *iv, sbx_context ivctx, long long n, int tw,
+                        void *w, sbx_context wctx, const int *iw, sbx_context iwctx, int copyadd);
+/* intersection(from0, size0, from1, size1, dim) of two periodic ranges (dist.h:461-486): up to
+   maxout pieces of 2*nd ints {from, size}, first dimension fastest; *nout is the count */
+int sbx_intersection(int nd, const int *from0, const int *size0, const int *from1,
+                     const int *size1, const int *dim, int maxout, int *out, int *nout);
+
 /* local_copy on one device (tensor.h:1055-1129): single component copy with labels */
 int sbx_local_copy(int nd0, int nd1, const double *alpha, int t0, int t1, const char *o0,
                    const int *from0, const int *size0, const int *dim0, const void *v0,

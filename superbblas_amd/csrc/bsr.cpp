@@ -33,7 +33,9 @@ struct BsrComp {
     const void *kron = nullptr; // Kronecker matrices (user memory, device)
     int nnz_per_row = -1;
     std::vector<int> h_rowptr, h_jj; // host copies of the pattern (for the transposed operator)
-    void *owned_v = nullptr;         // values owned by the operator (transposed operator)
+    void *owned_v = nullptr;         // values owned by the operator (transposed operator, or
+                                     // the device copy of a host component's values)
+    void *owned_kron = nullptr;      // device copy of a host component's Kronecker matrices
 };
 
 struct BsrOp {
@@ -57,6 +59,7 @@ struct BsrOp {
             if (c.ii) (void)hipFree(c.ii);
             if (c.jj) (void)hipFree(c.jj);
             if (c.owned_v) (void)hipFree(c.owned_v);
+            if (c.owned_kron) (void)hipFree(c.owned_kron);
         }
     }
 };
@@ -99,7 +102,11 @@ BsrOp *bsr_create(int nd, int ni, int dtype, const std::vector<std::vector<Range
     for (int c = 0; c < ncomp; ++c) {
         BsrComp bc;
         bc.dev = devs[c];
-        if (bc.dev < 0) throw Error("create_bsr: only GPU contexts are supported");
+        // a host (CPU-context) component: its pattern is read from the host and its values are
+        // copied to the device the host tensors of bsr_krylov are mirrored to (the values are a
+        // snapshot taken here, where the reference keeps reading the caller's host array)
+        const bool host = bc.dev < 0;
+        if (host) bc.dev = comm.device >= 0 ? comm.device : 0;
         const Range &ri = pi[comm.rank][c], &rd = pd[comm.rank][c];
         const long nii = bi > 0 ? volume(ri.size) / (bi * ki) : 0;
         bc.block_rows = nii;
@@ -114,7 +121,10 @@ BsrOp *bsr_create(int nd, int ni, int dtype, const std::vector<std::vector<Range
         // ii: number of nonzero blocks per block row (host or device memory)
         std::vector<int> hii(nii);
         set_device(bc.dev);
-        SBX_HIP_CHECK(hipMemcpy(hii.data(), ii[c], sizeof(int) * nii, hipMemcpyDefault));
+        if (host)
+            std::memcpy(hii.data(), ii[c], sizeof(int) * nii);
+        else
+            SBX_HIP_CHECK(hipMemcpy(hii.data(), ii[c], sizeof(int) * nii, hipMemcpyDefault));
         std::vector<int> rowptr(nii + 1, 0);
         bool same = true;
         for (long i = 0; i < nii; ++i) {
@@ -124,9 +134,27 @@ BsrOp *bsr_create(int nd, int ni, int dtype, const std::vector<std::vector<Range
         const long nnz = rowptr[nii];
         bc.nnz_per_row = same ? hii[0] : -1;
         std::vector<int> hjj_coor((std::size_t)nnz * nd);
-        if (nnz > 0)
+        if (nnz > 0 && host)
+            std::memcpy(hjj_coor.data(), jj[c], sizeof(int) * nnz * nd);
+        else if (nnz > 0)
             SBX_HIP_CHECK(hipMemcpy(hjj_coor.data(), jj[c], sizeof(int) * nnz * nd,
                                     hipMemcpyDefault));
+        if (host) {
+            const std::size_t es = dtype_size(dtype);
+            const std::size_t vbytes = es * (std::size_t)nnz * bi * bd;
+            SBX_HIP_CHECK(hipMalloc(&bc.owned_v, std::max<std::size_t>(vbytes, 1)));
+            if (vbytes) SBX_HIP_CHECK(hipMemcpy(bc.owned_v, v[c], vbytes, hipMemcpyHostToDevice));
+            bc.v = bc.owned_v;
+            if (op->is_kron) {
+                const std::size_t kbytes =
+                    es * (std::size_t)(same ? hii[0] : 0) * ki * volume(op->krond);
+                SBX_HIP_CHECK(hipMalloc(&bc.owned_kron, std::max<std::size_t>(kbytes, 1)));
+                if (kbytes)
+                    SBX_HIP_CHECK(hipMemcpy(bc.owned_kron, (*kronv)[c], kbytes,
+                                            hipMemcpyHostToDevice));
+                bc.kron = bc.owned_kron;
+            }
+        }
         // linear domain index of each block (get_bsr_indices, bsr.h:1451-1459): periodic
         // coordinates over the component's domain dims; for Kronecker operators the index of
         // the domain site, over the dims that are neither blocked nor Kronecker-blocked

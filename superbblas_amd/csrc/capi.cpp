@@ -945,8 +945,7 @@ int create_bsr_any(int nd, int ni, int t, const int *pim, const int *dimi, const
             vjj.push_back(jj[i]);
             vv.push_back(v[i]);
             if (kronv) vk.push_back(kronv[i]);
-            if (ctx[i].plat != SBX_GPU) throw Error("create_bsr: only GPU contexts are supported");
-            devs.push_back(ctx[i].device);
+            devs.push_back(ctx[i].plat == SBX_GPU ? ctx[i].device : -1); // -1: host component
         }
         const Coor ki = kronv ? to_coor(kronim, ni, rev) : Coor(), kd = kronv ? to_coor(krondm, nd, rev) : Coor();
         std::unique_ptr<sbx_bsr_s> h(new sbx_bsr_s());
@@ -1171,6 +1170,204 @@ int sbx_xgemm_batch_strided(int t, char transa, char transb, int m, int n, int k
         d.alpha = to_scalar(alpha);
         d.beta = to_scalar(beta);
         launch_gemm(d, device);
+    });
+}
+
+//
+// Low-level memory entry points of the superbblas::detail surface (include/superbblas_amd/
+// detail.h): the reference's copy_n / zero_n / copy_n_blocking / xgemm_batch_strided on a
+// context (blas.h:170-231, 436-490, 662-810; copy_n.h:584-1050).  Host operands are mirrored
+// through device scratch like the host components of the distributed calls: every flop and
+// every element conversion runs on the GPU; host destinations are complete on return.
+//
+
+namespace {
+
+bool on_host(const sbx_context &c) { return c.plat != SBX_GPU; }
+
+/// The one device an entry point runs on: the device of its GPU operands (all must agree), or
+/// device 0 when every operand is host memory
+int single_device(std::initializer_list<sbx_context> ctxs, const char *what) {
+    int dev = -1;
+    for (const auto &c : ctxs) {
+        if (on_host(c)) continue;
+        if (c.device < 0) throw Error(std::string(what) + ": invalid device");
+        if (dev >= 0 && dev != c.device)
+            throw Error(std::string(what) + ": operands on different devices are not supported");
+        dev = c.device;
+    }
+    return dev < 0 ? 0 : dev;
+}
+
+/// Largest index of an index vector (read from the host or the device)
+long index_max(const int *idx, const sbx_context &c, long n) {
+    std::vector<int> h;
+    const int *p = idx;
+    if (!on_host(c)) {
+        h.resize(n);
+        set_device(c.device);
+        SBX_HIP_CHECK(hipStreamSynchronize(get_stream(c.device)));
+        SBX_HIP_CHECK(hipMemcpy(h.data(), idx, sizeof(int) * n, hipMemcpyDeviceToHost));
+        p = h.data();
+    }
+    long m = -1;
+    for (long i = 0; i < n; ++i) {
+        if (p[i] < 0) throw Error("copy_n: negative index");
+        m = std::max(m, (long)p[i]);
+    }
+    return m;
+}
+
+/// Host memory mirrored into device scratch for the length of one call
+const void *upload(std::vector<Scratch> &bufs, const void *host, std::size_t bytes, int device) {
+    bufs.emplace_back(bytes, device);
+    if (bytes > 0)
+        SBX_HIP_CHECK(hipMemcpyAsync(bufs.back().ptr, host, bytes, hipMemcpyHostToDevice,
+                                     get_stream(device)));
+    return bufs.back().ptr;
+}
+
+/// Elements spanned by a column-major strided batch of rows x cols matrices
+long gemm_span(long rows, long cols, long ld, long stride, long batch) {
+    if (rows <= 0 || cols <= 0 || batch <= 0) return 0;
+    return (batch - 1) * stride + (cols - 1) * ld + rows;
+}
+
+} // namespace
+
+int sbx_memcpy(void *dst, sbx_context dctx, const void *src, sbx_context sctx,
+               unsigned long long bytes) {
+    return guard([&] {
+        if (bytes == 0 || dst == src) return;
+        if (!dst || !src) throw Error("copy_n: null pointer");
+        if (on_host(dctx) && on_host(sctx)) {
+            std::memcpy(dst, src, bytes);
+        } else if (on_host(sctx)) {
+            set_device(dctx.device);
+            hipStream_t s = get_stream(dctx.device);
+            SBX_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+            SBX_HIP_CHECK(hipStreamSynchronize(s)); // the host source may change on return
+        } else if (on_host(dctx)) {
+            set_device(sctx.device);
+            hipStream_t s = get_stream(sctx.device);
+            SBX_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
+            SBX_HIP_CHECK(hipStreamSynchronize(s));
+        } else if (sctx.device == dctx.device) {
+            set_device(sctx.device);
+            SBX_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice,
+                                         get_stream(sctx.device)));
+        } else {
+            // peer copy on the source's stream; the destination's stream then waits for it
+            // (the reference's causalConnectTo, blas.h:218-228)
+            set_device(dctx.device);
+            stream_after(get_stream(sctx.device), get_stream(dctx.device));
+            set_device(sctx.device);
+            SBX_HIP_CHECK(hipMemcpyPeerAsync(dst, dctx.device, src, sctx.device, bytes,
+                                             get_stream(sctx.device)));
+            stream_after(get_stream(dctx.device), get_stream(sctx.device));
+        }
+    });
+}
+
+int sbx_memset_zero(void *ptr, sbx_context ctx, unsigned long long bytes) {
+    return guard([&] {
+        if (bytes == 0) return;
+        if (!ptr) throw Error("zero_n: null pointer");
+        if (on_host(ctx))
+            std::memset(ptr, 0, bytes);
+        else
+            launch_zero(ptr, bytes, ctx.device);
+    });
+}
+
+int sbx_copy_n_blocking(const double *alpha, int tv, const void *v, sbx_context vctx,
+                        long long blocking, const int *iv, sbx_context ivctx, long long n, int tw,
+                        void *w, sbx_context wctx, const int *iw, sbx_context iwctx,
+                        int copyadd) {
+    return guard([&] {
+        if (n < 0 || blocking < 0) throw Error("copy_n: negative size");
+        if (n == 0 || blocking == 0) return;
+        check_copy_types(tv, tw);
+        if (!v || !w) throw Error("copy_n: null pointer");
+        const int dev = single_device({vctx, wctx, iv ? ivctx : vctx, iw ? iwctx : wctx},
+                                      "copy_n");
+        set_device(dev);
+        hipStream_t s = get_stream(dev);
+        std::vector<Scratch> bufs;
+        const std::size_t esv = dtype_size(tv), esw = dtype_size(tw);
+        const long extv = iv ? index_max(iv, ivctx, n) + blocking : n * blocking;
+        const long extw = iw ? index_max(iw, iwctx, n) + blocking : n * blocking;
+        if (extv > 0x7fffffffL || extw > 0x7fffffffL)
+            throw Error("copy_n: index vectors address at most 2^31 elements");
+        IndexCopyDesc d;
+        d.src_t = tv;
+        d.dst_t = tw;
+        d.n = n;
+        d.blocking = blocking;
+        d.alpha = to_scalar(alpha);
+        d.add = copyadd == SBX_ADD;
+        d.src_idx = iv && on_host(ivctx)
+                        ? (const int *)upload(bufs, iv, sizeof(int) * n, dev) : iv;
+        d.dst_idx = iw && on_host(iwctx)
+                        ? (const int *)upload(bufs, iw, sizeof(int) * n, dev) : iw;
+        d.src = on_host(vctx) ? upload(bufs, v, esv * extv, dev) : v;
+        // a host destination is mirrored whole (its untouched elements come back unchanged)
+        d.dst = on_host(wctx) ? const_cast<void *>(upload(bufs, w, esw * extw, dev)) : w;
+        launch_index_copy(d, dev);
+        if (on_host(wctx))
+            SBX_HIP_CHECK(hipMemcpyAsync(w, d.dst, esw * extw, hipMemcpyDeviceToHost, s));
+        if (!bufs.empty()) SBX_HIP_CHECK(hipStreamSynchronize(s));
+    });
+}
+
+int sbx_intersection(int nd, const int *from0, const int *size0, const int *from1,
+                     const int *size1, const int *dim, int maxout, int *out, int *nout) {
+    return guard([&] {
+        const Range a{to_coor(from0, nd, false), to_coor(size0, nd, false)};
+        const Range b{to_coor(from1, nd, false), to_coor(size1, nd, false)};
+        const std::vector<Range> r = intersection(a, b, to_coor(dim, nd, false));
+        *nout = (int)r.size();
+        if ((int)r.size() > maxout) throw Error("intersection: output too small");
+        for (std::size_t i = 0; i < r.size(); ++i)
+            for (int j = 0; j < nd; ++j) {
+                out[i * 2 * nd + j] = r[i].from[j];
+                out[i * 2 * nd + nd + j] = r[i].size[j];
+            }
+    });
+}
+
+int sbx_xgemm_batch_strided_ctx(int t, char transa, char transb, int m, int n, int k,
+                                const double *alpha, const void *a, int lda, long long stridea,
+                                const void *b, int ldb, long long strideb, const double *beta,
+                                void *c, int ldc, long long stridec, int batch, sbx_context ctx) {
+    if (!on_host(ctx))
+        return sbx_xgemm_batch_strided(t, transa, transb, m, n, k, alpha, a, lda, stridea, b, ldb,
+                                       strideb, beta, c, ldc, stridec, batch, ctx.device);
+    std::vector<Scratch> bufs;
+    const void *da = nullptr, *db = nullptr;
+    void *dc = nullptr;
+    long span_c = 0;
+    const int dev = 0;
+    const int rc = guard([&] {
+        const std::size_t es = dtype_size(t);
+        const bool na = transa == 'n' || transa == 'N', nb = transb == 'n' || transb == 'N';
+        const long span_a = gemm_span(na ? m : k, na ? k : m, lda, stridea, batch);
+        const long span_b = gemm_span(nb ? k : n, nb ? n : k, ldb, strideb, batch);
+        span_c = gemm_span(m, n, ldc, stridec, batch);
+        set_device(dev);
+        da = upload(bufs, a, es * span_a, dev);
+        db = upload(bufs, b, es * span_b, dev);
+        dc = const_cast<void *>(upload(bufs, c, es * span_c, dev));
+    });
+    if (rc != SBX_OK) return rc;
+    const int rg = sbx_xgemm_batch_strided(t, transa, transb, m, n, k, alpha, da, lda, stridea, db,
+                                           ldb, strideb, beta, dc, ldc, stridec, batch, dev);
+    if (rg != SBX_OK) return rg;
+    return guard([&] {
+        hipStream_t s = get_stream(dev);
+        if (span_c > 0)
+            SBX_HIP_CHECK(hipMemcpyAsync(c, dc, dtype_size(t) * span_c, hipMemcpyDeviceToHost, s));
+        SBX_HIP_CHECK(hipStreamSynchronize(s));
     });
 }
 

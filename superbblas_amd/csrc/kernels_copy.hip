@@ -1684,4 +1684,71 @@ void launch_zero(void *p, std::size_t bytes, int device) {
     SBX_HIP_CHECK(hipMemsetAsync(p, 0, bytes, get_stream(device)));
 }
 
+//
+// Index-vector gather / scatter of `blocking`-element runs: the reference's low-level
+// copy_n / copy_n_blocking with explicit index vectors (copy_n.h:584-740, 898-1050), which the
+// library's own copy() never materialises but which callers of superbblas::detail use directly.
+// One lane per element of the n * blocking runs; a run's lanes are consecutive, so the accesses
+// of a wave are coalesced whenever blocking >= 16 and contiguous for null index vectors.
+//
+namespace {
+template <typename S, typename D, bool ADD>
+__global__ void __launch_bounds__(256)
+    copy_index_kernel(const S *__restrict__ src, const int *__restrict__ sidx, D *dst,
+                      const int *__restrict__ didx, long n, long blocking, Alpha alpha) {
+    const long total = n * blocking;
+    for (long e = blockIdx.x * 256L + threadIdx.x; e < total; e += (long)gridDim.x * 256L) {
+        const long d = e / blocking, r = e - d * blocking;
+        const long so = (sidx ? (long)sidx[d] : d * blocking) + r;
+        const long wo = (didx ? (long)didx[d] : d * blocking) + r;
+        put<ADD, D>(dst + wo, xform<D, S>(src[so], alpha));
+    }
+}
+
+template <typename S, typename D>
+void index_copy_typed(const IndexCopyDesc &c, const Alpha &a, hipStream_t s) {
+    const long total = c.n * c.blocking;
+    const long blocks = std::max(1L, std::min((total + 255) / 256, 256L * 64));
+    if (c.add)
+        copy_index_kernel<S, D, true><<<blocks, 256, 0, s>>>((const S *)c.src, c.src_idx,
+                                                             (D *)c.dst, c.dst_idx, c.n,
+                                                             c.blocking, a);
+    else
+        copy_index_kernel<S, D, false><<<blocks, 256, 0, s>>>((const S *)c.src, c.src_idx,
+                                                              (D *)c.dst, c.dst_idx, c.n,
+                                                              c.blocking, a);
+    SBX_HIP_CHECK(hipGetLastError());
+}
+} // namespace
+
+void launch_index_copy(const IndexCopyDesc &c, int device) {
+    if (c.n <= 0 || c.blocking <= 0) return;
+    set_device(device);
+    hipStream_t s = get_stream(device);
+    KernelTimer timer("copy", s);
+    const Alpha a{c.alpha.re, c.alpha.im, c.alpha.is_one() ? 1 : c.alpha.is_zero() ? 2 : 0};
+    const int st = c.src_t, dt = c.dst_t;
+    if (st == dt) {
+        switch (st) {
+        case SBX_FLOAT: return index_copy_typed<float, float>(c, a, s);
+        case SBX_DOUBLE: return index_copy_typed<double, double>(c, a, s);
+        case SBX_CFLOAT: return index_copy_typed<float2, float2>(c, a, s);
+        case SBX_CDOUBLE: return index_copy_typed<double2, double2>(c, a, s);
+        case SBX_INT: return index_copy_typed<int, int>(c, a, s);
+        case SBX_SIZE_T: return index_copy_typed<unsigned long, unsigned long>(c, a, s);
+        }
+    }
+    if (st == SBX_FLOAT && dt == SBX_DOUBLE) return index_copy_typed<float, double>(c, a, s);
+    if (st == SBX_DOUBLE && dt == SBX_FLOAT) return index_copy_typed<double, float>(c, a, s);
+    if (st == SBX_CFLOAT && dt == SBX_CDOUBLE) return index_copy_typed<float2, double2>(c, a, s);
+    if (st == SBX_CDOUBLE && dt == SBX_CFLOAT) return index_copy_typed<double2, float2>(c, a, s);
+    if (st == SBX_FLOAT && dt == SBX_CFLOAT) return index_copy_typed<float, float2>(c, a, s);
+    if (st == SBX_FLOAT && dt == SBX_CDOUBLE) return index_copy_typed<float, double2>(c, a, s);
+    if (st == SBX_DOUBLE && dt == SBX_CFLOAT) return index_copy_typed<double, float2>(c, a, s);
+    if (st == SBX_DOUBLE && dt == SBX_CDOUBLE) return index_copy_typed<double, double2>(c, a, s);
+    if (st == SBX_INT && dt == SBX_SIZE_T) return index_copy_typed<int, unsigned long>(c, a, s);
+    if (st == SBX_SIZE_T && dt == SBX_INT) return index_copy_typed<unsigned long, int>(c, a, s);
+    throw Error("copy_n: unsupported type conversion");
+}
+
 } // namespace sbx

@@ -296,6 +296,20 @@ inline void check_dma_lds(const char *kernel, size_t lds, long passes, long lane
 /// Fill `n` elements of type `t` with zeros
 void launch_zero(void *p, std::size_t bytes, int device);
 
+/// Gather / scatter of runs through index vectors (reference copy_n_blocking, copy_n.h:584-1050):
+///   dst[(dst_idx ? dst_idx[d] : d*blocking) + r] (=|+=) alpha * src[(src_idx ? src_idx[d] :
+///   d*blocking) + r],  d < n, r < blocking; all pointers on `device`
+struct IndexCopyDesc {
+    int src_t, dst_t;
+    const void *src;
+    void *dst;
+    const int *src_idx = nullptr, *dst_idx = nullptr;
+    long n = 0, blocking = 1;
+    Scalar alpha;
+    bool add = false;
+};
+void launch_index_copy(const IndexCopyDesc &d, int device);
+
 /// BSR SpMM on one component (reference bsr.h:535-650 builtin loop, bsr.h:855-928 GPU):
 ///   y[row-block i] = alpha * sum_{j in row i} V_j * x[jj_j],  for every rhs column
 struct BsrDesc {
