@@ -305,10 +305,13 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--no-1gpu", action="store_true",
                     help="N > 1: skip the same global problem on rank 0's GPU alone")
-    ap.add_argument("--share-gpu", choices=["host", "rccl"], nargs="?", const="host", default=None,
+    ap.add_argument("--share-gpu", choices=["host", "rccl", "nccl"], nargs="?", const="host",
+                    default=None,
                     help="rehearsal of the N>1 path on a box with fewer GPUs than ranks: ranks "
                          "share GPUs; 'host': host-staged exchanges over gloo, 'rccl': RCCL "
-                         "with one host id per rank (socket transport) -- not a bench")
+                         "with one host id per rank (socket transport) under a gloo process "
+                         "group, 'nccl': the same RCCL transport under the real start-up "
+                         "(init_process_group('nccl', device_id=...)) -- not a bench")
     args = ap.parse_args()
 
     # --gpus N is the number of ranks: without a launcher, start one (a child process, before
@@ -329,7 +332,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.share_gpu == "rccl":
+    if args.share_gpu in ("rccl", "nccl"):
         os.environ["NCCL_HOSTID"] = "sbx-bench-rank-%d" % rank
         os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
         os.environ.setdefault("NCCL_IB_DISABLE", "1")
@@ -342,11 +345,11 @@ def main():
     comm = None
     if world > 1:
         import torch.distributed as dist
-        if args.share_gpu:
+        if args.share_gpu in ("host", "rccl"):
             dist.init_process_group("gloo")
             comm = (sb.Comm.host_staged(local_rank) if args.share_gpu == "host"
                     else sb.Comm.from_torch_distributed(local_rank))
-        else:
+        else:  # the real start-up (also --share-gpu nccl)
             dist.init_process_group("nccl", device_id=dev)
             comm = sb.Comm.from_torch_distributed(local_rank)
 
@@ -465,7 +468,7 @@ def main():
     elapsed = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64,
-                         device="cpu" if args.share_gpu else dev)
+                         device="cpu" if args.share_gpu in ("host", "rccl") else dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     gemm_ms, gemm_calls = sb.timings_get("gemm_total")
@@ -539,7 +542,7 @@ def main():
                         % (config, L, n, grid[0], grid[1], grid[2], grid[3],
                            "the same" if config == "4a" else "split over t (redistributed to "
                            "v0's partition by an all-to-all)",
-                           "RCCL" if not args.share_gpu or args.share_gpu == "rccl" else
+                           "RCCL" if args.share_gpu != "host" else
                            "host staging"))
         line = {
             "metric": "lattice contraction GFLOP/s + permute GB/s, 16^4 spin×color, 1/2/4/8 GPUs",

@@ -115,8 +115,8 @@ int sbx_timings_report(char *buf, int len);
    "copy.order", "copy.trans", "copy.btrans", "bsr.variant", "bsr.row_max_cols", "bsr.split_max_cols",
    "bsr.split_cw", "bsr.split_jb", "bsr.split_ilv", "bsr.kron_mfma", "bsr.kron_mfma_min_cols",
    "bsr.kron_pack", "bsr.kron_xlds", "bsr.kron_ylds", "bsr.nt", "bsr.blk_pd", "dense.wave", "dist.reduce" (must be set alike on every rank: the ranks' reductions must
-   match; SB_DEBUG >= 1 checks it), "alloc.max_cached", "debug.level" (overrides SB_DEBUG),
-   "debug.corrupt_copy" (tests of the SB_DEBUG checks: drop that local piece of every copy); read-backs "bsr.last_kernel",
+   match; SB_DEBUG >= 1 checks it), "dist.force_peer" (1: the several-GPUs-per-rank path -- pack, hipMemcpyPeerAsync, unpack -- for every piece between components of a rank even on one device), "alloc.max_cached", "debug.level" (overrides SB_DEBUG),
+   "debug.corrupt_copy" (tests of the SB_DEBUG checks: drop that local piece of every copy); read-backs "bsr.last_kernel", "dist.peer_copies",
    "copy.last_pair", "dist.reduce_calls", "alloc.cross_stream_frees".  Unknown keys fail with an
    error. */
 int sbx_tune_set(const char *key, long long value);

@@ -163,6 +163,7 @@ _lib.sbx_copy_masked.argtypes = [_I, _I, _VP, _I, _I, _VP, _I, ctypes.c_char_p, 
                                  _VP, _I, _I, _I]
 _lib.sbx_copy_req.argtypes = _lib.sbx_copy_masked.argtypes + [_VP]
 _lib.sbx_wait.argtypes = [_VP]
+_lib.sbx_comm_transport.argtypes = [_VP, _VP, _VP, _VP]
 
 
 class Request:
@@ -686,14 +687,6 @@ class BSR:
     @property
     def handle(self):
         return self._h
-
-    def transport(self):
-        """(kind, count, user_rank): kind "none" (one rank), "rccl" (count and user_rank as RCCL
-        itself reports them: ncclCommCount / ncclCommUserRank) or "host" (host-staged)."""
-        k, c, r = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-        _check(_lib.sbx_comm_transport(self._h, ctypes.byref(k), ctypes.byref(c),
-                                       ctypes.byref(r)))
-        return ({0: "none", 1: "rccl", 2: "host"}[k.value], c.value, r.value)
 
     def destroy(self):
         if self._h:

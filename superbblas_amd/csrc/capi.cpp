@@ -435,6 +435,8 @@ int sbx_tune_set(const char *key, long long value) {
         else if (k == "debug.level") g_debug_level = (int)value;
         else if (k == "debug.corrupt_copy") g_debug_corrupt = (int)value;
         else if (k == "dist.reduce_calls") g_dist_reduce_calls = value;
+        else if (k == "dist.force_peer") g_dist_force_peer = (int)value;
+        else if (k == "dist.peer_copies") g_dist_peer_copies = value;
         else if (k.compare(0, 6, "alloc.") == 0) alloc_tune(key, nullptr, &value);
         else throw Error("tune_set: unknown key " + k);
         if (k.compare(0, 5, "copy.") == 0) {
@@ -482,6 +484,8 @@ int sbx_tune_get(const char *key, long long *value) {
         else if (k == "debug.level") *value = g_debug_level;
         else if (k == "debug.corrupt_copy") *value = g_debug_corrupt;
         else if (k == "dist.reduce_calls") *value = g_dist_reduce_calls;
+        else if (k == "dist.force_peer") *value = g_dist_force_peer;
+        else if (k == "dist.peer_copies") *value = g_dist_peer_copies;
         else if (k.compare(0, 6, "alloc.") == 0) alloc_tune(key, value, nullptr);
         else throw Error("tune_get: unknown key " + k);
     });

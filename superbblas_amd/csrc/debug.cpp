@@ -153,7 +153,10 @@ void copy_mock_test(const DistTensor &src, const Coor &from0, const Coor &size0,
     for (int k = 0; k < nd0; ++k)
         if (perm1[k] >= 0) size1[perm1[k]] = size0[k];
     const std::vector<long> st0 = strides_slow_to_fast(src.dim);
-    for (std::size_t i = 0; i < d.ptr.size(); ++i) {
+    // the first mismatch of this rank; every rank learns whether any rank failed before throwing
+    // (a rank throwing alone would leave the others in the real copy's exchange)
+    std::string fail;
+    for (std::size_t i = 0; i < d.ptr.size() && fail.empty(); ++i) {
         const Range &rb = dst.ranges[comm.rank][i];
         const long n = volume(rb.size);
         if (n == 0) continue;
@@ -190,7 +193,8 @@ void copy_mock_test(const DistTensor &src, const Coor &from0, const Coor &size0,
                    << comm.rank << ", destination component " << i << ", coordinate (";
                 for (int j = 0; j < nd1; ++j) os << (j ? "," : "") << c1[j];
                 os << ") of '" << dst.labels << "' holds " << got[e] << ", expected " << want << ")";
-                throw Error(os.str());
+                fail = os.str();
+                break;
             }
             for (int j = nd1 - 1; j >= 0; --j) {
                 if (++lc[j] < rb.size[j]) break;
@@ -198,6 +202,11 @@ void copy_mock_test(const DistTensor &src, const Coor &from0, const Coor &size0,
             }
         }
     }
+    const bool ok = fail.empty();
+    if (!comm_all_equal(comm, ok ? 1ull : 0ull) && ok)
+        throw Error("test_copy_check does not pass! (SB_DEBUG mock-index copy check failed on "
+                    "another rank)");
+    if (!ok) throw Error(fail);
 }
 
 } // namespace sbx

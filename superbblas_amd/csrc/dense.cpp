@@ -99,6 +99,24 @@ Work prepare(const DistTensor &v, const std::string &orows, const std::string &o
     return w;
 }
 
+/// SB_DEBUG >= 1, several ranks: the ranks were called alike (check_consistency, dist.h:702-736).
+/// The tune key dense.wave is part of the hash: it decides whether a rank works in place (no
+/// dist_copy at all) or through working copies, so ranks set differently would run different
+/// collective sequences -- it must be the same on every rank.
+void check_dense_call(const char *what, const std::vector<const DistTensor *> &ts,
+                      const std::string &orows, const std::string &ocols, const Scalar &alpha,
+                      const Comm &comm) {
+    if (debug_level() <= 0 || comm.nprocs <= 1) return;
+    Hasher h;
+    h.add(std::string(what));
+    for (const DistTensor *t : ts) h.add(*t);
+    h.add(orows);
+    h.add(ocols);
+    h.add(alpha);
+    h.add((long)g_dense_wave);
+    check_consistency(h, what, comm);
+}
+
 void check_info(int info) {
     if (info < 0)
         throw Error("Error in a lapack routine: wrong argument at position " + std::to_string(-info));
@@ -116,8 +134,13 @@ void check_dims(const DistTensor &a, const DistTensor &b) {
 
 } // namespace
 
+/// Note: when the caller's matrices are already whole and row-major per component and small
+/// (dense.wave), the factorization runs in place: a matrix that is not Hermitian positive definite
+/// then leaves the caller's tensor partly factorized when the error is thrown (the reference
+/// factorizes a copy and leaves its input untouched on failure, dense.h:600-650).
 void dense_cholesky(const DistTensor &v, const std::string &orows, const std::string &ocols,
                     const Comm &comm) {
+    check_dense_call("cholesky", {&v}, orows, ocols, Scalar{1, 0}, comm);
     Work w = prepare(v, orows, ocols, comm, true, "cholesky", true);
     for (std::size_t c = 0; c < w.t.ptr.size(); ++c) {
         const long k = w.n ? volume(w.t.ranges[comm.rank][c].size) / (w.n * w.n) : 0;
@@ -129,6 +152,7 @@ void dense_cholesky(const DistTensor &v, const std::string &orows, const std::st
 
 void dense_inversion(const DistTensor &v, const std::string &orows, const std::string &ocols,
                      const Comm &comm) {
+    check_dense_call("inversion", {&v}, orows, ocols, Scalar{1, 0}, comm);
     Work w = prepare(v, orows, ocols, comm, true, "inversion", true);
     std::vector<Scratch> inv;
     DistTensor wi = w.t;
@@ -162,6 +186,7 @@ void dense_solve(bool gesm, const Scalar &alpha, const DistTensor &c, const std:
                  const std::string &ocols, const DistTensor &x, const DistTensor &y,
                  const Comm &comm) {
     const char *what = gesm ? "gesm" : "trsm";
+    check_dense_call(what, {&c, &x, &y}, orows, ocols, alpha, comm);
     check_dims(c, x);
     check_dims(c, y);
     check_dims(x, y);

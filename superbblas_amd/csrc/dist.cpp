@@ -205,7 +205,7 @@ void local_piece_copy(const Scalar &alpha, int src_t, const void *src, const Coo
 
 /// Cross-device stream ordering: make `to` wait for the work enqueued so far on `from`
 void stream_wait(int from, int to) {
-    if (from == to) return;
+    if (from == to && !g_dist_force_peer) return; // (forced peer path: the events run too)
     hipEvent_t ev;
     set_device(from);
     SBX_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
@@ -475,7 +475,7 @@ void dist_copy(const Scalar &alpha, const DistTensor &src, const Coor &from0, co
         const Range &ra = src.ranges[ca.rank][ca.idx];
         const Range &rb = dst.ranges[cb.rank][cb.idx];
         const int da = src.dev[ca.idx], db = dst.dev[cb.idx];
-        if (da == db) {
+        if (da == db && !g_dist_force_peer) {
             local_piece_copy(alpha, src.dtype, src.ptr[ca.idx], ra.size, p.src_from, dst.dtype,
                              dst.ptr[cb.idx], rb.size, p.dst_from, p.size, perm_s2d, add, db,
                              src.mask_of(ca.idx), dst.mask_of(cb.idx));
@@ -493,6 +493,7 @@ void dist_copy(const Scalar &alpha, const DistTensor &src, const Coor &from0, co
             stream_wait(da, db);
             set_device(db);
             SBX_HIP_CHECK(hipMemcpyPeerAsync(dbuf.ptr, db, sbuf.ptr, da, bytes, get_stream(db)));
+            ++g_dist_peer_copies;
             local_piece_copy(alpha, src.dtype, dbuf.ptr, p.size, Coor(src.nd(), 0), dst.dtype,
                              dst.ptr[cb.idx], rb.size, p.dst_from, p.size, perm_s2d, add, db,
                              nullptr, dst.mask_of(cb.idx));
@@ -541,7 +542,7 @@ void dist_copy(const Scalar &alpha, const DistTensor &src, const Coor &from0, co
             char *slot = (char *)sbuf->ptr + cur[cb.rank];
             const std::size_t bytes = volume(p.size) * es;
             cur[cb.rank] += bytes;
-            if (da == device) {
+            if (da == device && !g_dist_force_peer) {
                 local_piece_copy(Scalar{1, 0}, src.dtype, src.ptr[ca.idx],
                                  src.ranges[ca.rank][ca.idx].size, p.src_from, src.dtype, slot,
                                  p.size, Coor(src.nd(), 0), p.size, id, false, device);
@@ -558,6 +559,7 @@ void dist_copy(const Scalar &alpha, const DistTensor &src, const Coor &from0, co
             stream_wait(da, device);
             set_device(device);
             SBX_HIP_CHECK(hipMemcpyPeerAsync(slot, device, tmp.ptr, da, bytes, get_stream(device)));
+            ++g_dist_peer_copies;
             stream_wait(device, da); // tmp is reused on `da` only after the peer copy
         }
         if (comm.nccl) {
@@ -611,7 +613,7 @@ void dist_copy(const Scalar &alpha, const DistTensor &src, const Coor &from0, co
             const char *slot = (const char *)rbuf->ptr + cur[ca.rank];
             const std::size_t bytes = volume(p.size) * es;
             cur[ca.rank] += bytes;
-            if (db == device) {
+            if (db == device && !g_dist_force_peer) {
                 local_piece_copy(alpha, src_c.dtype, slot, p.size, Coor(src_c.nd(), 0),
                                  dst_c.dtype, dst_c.ptr[cb.idx], dst_c.ranges[cb.rank][cb.idx].size,
                                  p.dst_from, p.size, perm_s2d, add, device, nullptr,
@@ -624,6 +626,7 @@ void dist_copy(const Scalar &alpha, const DistTensor &src, const Coor &from0, co
             stream_wait(device, db);
             set_device(db);
             SBX_HIP_CHECK(hipMemcpyPeerAsync(tmp.ptr, db, slot, device, bytes, get_stream(db)));
+            ++g_dist_peer_copies;
             local_piece_copy(alpha, src_c.dtype, tmp.ptr, p.size, Coor(src_c.nd(), 0), dst_c.dtype,
                              dst_c.ptr[cb.idx], dst_c.ranges[cb.rank][cb.idx].size, p.dst_from,
                              p.size, perm_s2d, add, db, nullptr, dst_c.mask_of(cb.idx));
@@ -637,6 +640,8 @@ void dist_copy(const Scalar &alpha, const DistTensor &src, const Coor &from0, co
         finish();
 }
 
+int g_dist_force_peer = 0;
+std::atomic<long long> g_dist_peer_copies{0};
 int g_dist_reduce = 1; // tune key dist.reduce: 1 collective reductions where they fit, 0 never
 std::atomic<long long> g_dist_reduce_calls{0}; // read-back dist.reduce_calls: collectives issued
 

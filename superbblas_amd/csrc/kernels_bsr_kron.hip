@@ -34,6 +34,7 @@ struct KronArgs {
     double alpha_re, alpha_im;
     int add;
     int ylds; ///< the XL kernels: y written through the wave's LDS ring in whole 64-B spin pieces
+    long x_rows; ///< domain rows of x (sites * bd): the extent x's LDS-DMA buffer offsets address
 };
 
 template <typename E, int BI, int BD, int KI, int KD>
@@ -699,7 +700,7 @@ template <typename E> void launch_kron_typed(const KronArgs &a, hipStream_t s) {
                     check_dma_lds("bsr_kron_mfma_packed_kernel", lds_cb, (rw * 81L + nth - 1) / nth, nth);
                     // x by LDS-DMA: a ring of 2 x 3 KB per wave after the color blocks (lds_cb is
                     // a multiple of 16); 32-bit buffer offsets
-                    const int xl = a.block_rows * 12L * a.ncols * 16 < (1L << 31)
+                    const int xl = std::max(a.block_rows * 12L, a.x_rows * 4L) * a.ncols * 16 < (1L << 31)
                                        ? std::max(0, std::min(3, g_bsr_tune.kron_xlds)) : 0;
                     // (+ the 9 spin matrices)
                     const size_t lds_bytes = lds_cb + (xl > 0 ? (size_t)wpk * (xl + 1) * 3072 + 9 * 16 * 16 : 0);
@@ -725,7 +726,7 @@ template <typename E> void launch_kron_typed(const KronArgs &a, hipStream_t s) {
             if (blocks < (1L << 31)) {
                 g_bsr_tune.last = 5;
                 // x by LDS-DMA (32-bit buffer offsets)
-                const int xl = a.block_rows * 12L * a.ncols * 16 < (1L << 31)
+                const int xl = std::max(a.block_rows * 12L, a.x_rows * 4L) * a.ncols * 16 < (1L << 31)
                                    ? std::max(0, std::min(3, g_bsr_tune.kron_xlds)) : 0;
                 auto go = [&](auto kern) {
                     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, s, a, (int)ngroups);
@@ -787,6 +788,9 @@ void launch_bsr_kron(const BsrDesc &d, int device) {
     a.alpha_im = d.alpha.im;
     a.add = d.add ? 1 : 0;
     a.ylds = g_bsr_tune.kron_ylds ? 1 : 0;
+    // domain sites can exceed block_rows (halo sites): the x staging's 32-bit buffer offsets are
+    // bounded by x's extent, not y's
+    a.x_rows = d.x_rows > 0 ? d.x_rows : d.block_rows * d.bd;
     switch (d.t) {
     case SBX_CDOUBLE: return launch_kron_typed<double2>(a, s);
     case SBX_CFLOAT: return launch_kron_typed<float2>(a, s);

@@ -180,6 +180,13 @@ bool dist_reduce_collective(const DistTensor &part, const Coor &f0, const Coor &
                             const DistTensor &dst, const Coor &f1, const Comm &comm);
 extern int g_dist_reduce;
 extern std::atomic<long long> g_dist_reduce_calls;
+/// tune key dist.force_peer: 1 takes the several-GPUs-per-rank path (pack on the origin device,
+/// hipMemcpyPeerAsync, unpack on the destination device) for every piece between two components
+/// of a rank and for every component away from the communicator's device, even when the devices
+/// are the same one -- so that path runs on a 1-GPU box; read-back dist.peer_copies counts the
+/// peer copies issued
+extern int g_dist_force_peer;
+extern std::atomic<long long> g_dist_peer_copies;
 
 /// copy: dst[from1 + P(c - from0)] (=|+=) alpha * src[c] for c in [from0, from0+size0).
 /// With `deferred` and other ranks in the exchange, the call returns once the local pieces are

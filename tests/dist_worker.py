@@ -24,6 +24,11 @@ Cases (all multi-rank: the exchange, pack/unpack kernels and reductions run for 
   split  -- the reference's split operator: a halo piece applied with a deferred request (its
             exchange in flight) and a core piece with just_local, then wait; a deferred copy
             [tests/bsr.cpp:402-545, 779-818; bsr.h:2199-2257, 2352-2359; dist.h:54-61]
+  peer   -- two components per rank (the reference's --components=2, tests/contract.cpp:452-461)
+            through the several-GPUs-per-rank path (pack on the origin device, hipMemcpyPeerAsync,
+            unpack on the destination device; dist.h:205-241) forced on the one device of a test
+            box by the tune key dist.force_peer: copies between t- and x-split tensors and the
+            golden contractions, bit-exact / within 1e-10
   fuzz   -- seeded random copies (permutation, wrapping box, Copy/Add, type pairs) and
             contractions (label groups, orders, boxes, conj, alpha/beta) between random
             distributions over the ranks (some ranks may own nothing)
@@ -613,8 +618,74 @@ def case_debug(sb, comm, rank, n, dev):
         # the same call with equal arguments still works afterwards
         sb.copy(1.0, p0, "xyzt", [0] * 4, dim0, dim0, v0, p1, "tzyx", [0] * 4, dim1, v1, comm=comm)
         torch.cuda.synchronize()
+        # at 2 a wrong plan on ONE rank (debug.corrupt_copy drops its first local piece) makes
+        # EVERY rank fail the mock-index check, so no rank is left waiting in the real copy's
+        # exchange; the library is usable afterwards
+        sb.tune_set("debug.level", 2)
+        if rank == 0:
+            sb.tune_set("debug.corrupt_copy", 1)
+        try:
+            sb.copy(1.0, p0, "xyzt", [0] * 4, dim0, dim0, v0, p1, "tzyx", [0] * 4, dim1, v1,
+                    comm=comm)
+        except sb.SuperbblasError as e:
+            assert "test_copy_check does not pass" in str(e), e
+        else:
+            raise AssertionError("the mock-index check let a corrupt copy through on rank %d" % rank)
+        finally:
+            sb.tune_set("debug.corrupt_copy", 0)
+        sb.copy(1.0, p0, "xyzt", [0] * 4, dim0, dim0, v0, p1, "tzyx", [0] * 4, dim1, v1, comm=comm)
+        torch.cuda.synchronize()
     finally:
         sb.tune_set("debug.level", old)
+
+
+def case_peer(sb, comm, rank, n, dev):
+    nc = 2
+    sb.tune_set("dist.force_peer", 1)
+    sb.tune_set("dist.peer_copies", 0)
+    try:
+        dim0, dim1 = [4, 4, 2, 6], [6, 2, 4, 4]
+        p0 = sb.basic_partitioning("xyzt", dim0, [1, 1, 1, n], "t", n, nc)
+        p1 = sb.basic_partitioning("tzyx", dim1, [1, 1, 1, n], "x", n, nc)
+        g0 = gen("index", vol(dim0), 1, np.complex128)
+        for add in (False, True):
+            g1 = gen("int", vol(dim1), 2, np.complex128)
+            v0 = _nonempty(scatter(sb, g0, dim0, p0, rank, nc, dev), dev)
+            v1 = _nonempty(scatter(sb, g1, dim1, p1, rank, nc, dev), dev)
+            sb.copy(2.0 if add else 1.0, p0, "xyzt", [1, 2, 0, 3], [3, 4, 2, 5], dim0, v0, p1,
+                    "tzyx", [2, 0, 1, 3], dim1, v1, copyadd=sb.Add if add else sb.Copy, comm=comm)
+            torch.cuda.synchronize()
+            out = gather(np.zeros_like(g1), dim1, p1, nc,
+                         [v1[i][:vol(p1[rank * nc + i][1])] for i in range(nc)])
+            ref = g1.copy()
+            oracle_copy(2.0 if add else 1.0, "xyzt", [1, 2, 0, 3], [3, 4, 2, 5], dim0, g0, "tzyx",
+                        [2, 0, 1, 3], dim1, ref, add=add)
+            assert np.array_equal(out.view(np.uint8), ref.view(np.uint8)), ("peer copy", add)
+        grid = LATTICE_GRID.get(n, [n, 1, 1])
+        for case in manifest("contraction"):
+            if (case.get("gen", "int") == "int" or case["o0"] != "tnsxyzc" or len(case["p0"]) != 1
+                    or case["t"] != "cdouble"):
+                continue
+            g0, g1, gr = contraction_inputs(case)
+            d0, d1, dr = case["dim0"], case["dim1"], case["dimr"]
+            p0 = sb.basic_partitioning("tnsxyzc", d0, [1, 1, 1] + grid + [1], "xyz", n, nc)
+            p1 = sb.basic_partitioning(case["o1"], d1, [n, 1, 1, 1, 1, 1, 1], "t", n, nc)
+            pr = [([0] * len(dr), dr)] + [([0] * len(dr), [0] * len(dr))] * (n * nc - 1)
+            v0 = _nonempty(scatter(sb, g0, d0, p0, rank, nc, dev), dev)
+            v1 = _nonempty(scatter(sb, g1, d1, p1, rank, nc, dev), dev)
+            vr = _nonempty(scatter(sb, gr, dr, pr, rank, nc, dev), dev)
+            sb.contraction(complex(*case["alpha"]), p0, case["from0"], case["size0"], d0,
+                           case["o0"], case["conj0"], v0, p1, case["from1"], case["size1"], d1,
+                           case["o1"], case["conj1"], v1, complex(*case["beta"]), pr,
+                           case["fromr"], case["sizer"], dr, case["o_r"], vr, comm=comm)
+            torch.cuda.synchronize()
+            out = gather(np.zeros_like(gr), dr, pr, nc,
+                         [vr[i][:vol(pr[rank * nc + i][1])] for i in range(nc)])
+            errs = component_errors(out, output(case, np.complex128))
+            assert max(errs) < 1e-10, ("peer golden", case["id"], errs)
+        assert sb.tune_get("dist.peer_copies") > 0, "the peer path did not run"
+    finally:
+        sb.tune_set("dist.force_peer", 0)
 
 
 def _rand_partition(sb, rng, labels, dims, n):
@@ -723,12 +794,17 @@ def main():
         os.environ["NCCL_HOSTID"] = "sbx-test-rank-%s" % os.environ.get("RANK", "0")
         os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
         os.environ.setdefault("NCCL_IB_DISABLE", "1")
-    dist.init_process_group("gloo")
-    rank, n = dist.get_rank(), dist.get_world_size()
     ndev = torch.cuda.device_count()
     dev_idx = int(os.environ.get("LOCAL_RANK", "0")) % ndev
     torch.cuda.set_device(dev_idx)
     dev = torch.device("cuda", dev_idx)
+    if os.environ.get("SBX_TEST_PG") == "nccl":
+        # the process group of bench.py's real N > 1 start-up: torch's own RCCL communicator,
+        # created eagerly on this rank's device, beside the library's (Comm.from_torch_distributed)
+        dist.init_process_group("nccl", device_id=dev)
+    else:
+        dist.init_process_group("gloo")
+    rank, n = dist.get_rank(), dist.get_world_size()
     import superbblas_amd as sb
     if transport == "rccl":
         comm = sb.Comm.from_torch_distributed(dev_idx)
@@ -759,6 +835,8 @@ def main():
         case_split(sb, comm, rank, n, dev)
     if "debug" in cases:
         case_debug(sb, comm, rank, n, dev)
+    if "peer" in cases:
+        case_peer(sb, comm, rank, n, dev)
     dist.barrier()
     comm.close()
     dist.destroy_process_group()

@@ -45,13 +45,13 @@ def test_bench_n2_scale_check(gpu, config):
     assert line["chain_dist_bsr_split_rel_diff"] < 1e-5
 
 
-def _bench_no_launcher(n, extra, timeout=420):
+def _bench_no_launcher(n, extra, timeout=420, share="rccl"):
     """bench.py --gpus n run WITHOUT a launcher: it must start the n ranks itself"""
     env = {k: v for k, v in os.environ.items()
            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
     env["OMP_NUM_THREADS"] = "2"
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--share-gpu",
-           "rccl"] + extra
+           share] + extra
     # the ranks' progress lines (stderr) go to a file under gpurun_out/ when it exists, so a long
     # multi-rank run keeps showing signs of life
     outdir = os.path.join(ROOT, "gpurun_out")
@@ -85,3 +85,16 @@ def test_bench_gpus_n_launches_ranks(gpu, n):
     for k, v in errs.items():
         assert v <= (1e-5 if k.endswith("_chain") else 1e-10), (k, v)
     assert line["scale_check_ok"] is True
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_bench_real_startup_nccl_pg(gpu, n):
+    """the start-up of the driver's multi-GPU run itself: init_process_group("nccl",
+    device_id=dev) plus the library's own RCCL communicator (two per process); only RCCL's
+    host ids differ (--share-gpu nccl), so the ranks can share the test box's GPU"""
+    line = _bench_no_launcher(n, ["--steps", "2", "--warmup", "1", "--L", "8", "--ncols", "8",
+                                  "--chain-L", "4", "--chain-T", "8"], share="nccl")
+    assert line["n_gpus"] == n
+    assert line["world_size_seen_by_rccl"] == n and line["comm_transport"] == "rccl"
+    errs = {k: v for k, v in line.items() if k.startswith("scale_check_rel_err")}
+    assert len(errs) == 3 and line["scale_check_ok"] is True, line

@@ -25,8 +25,10 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run(nprocs, transport, cases=None, shared=False):
+def _run(nprocs, transport, cases=None, shared=False, pg=None):
     env = dict(os.environ, SBX_TEST_TRANSPORT=transport, OMP_NUM_THREADS="2")
+    if pg:
+        env["SBX_TEST_PG"] = pg
     if cases:
         env["SBX_TEST_CASES"] = cases
     if shared:
@@ -67,3 +69,18 @@ def test_dist_rccl_golden_grid(gpu, nprocs):
     over RCCL, both reductions (collective / point-to-point), within 1e-10 per component"""
     import torch
     _run(nprocs, "rccl", cases="golden", shared=torch.cuda.device_count() < nprocs)
+
+
+def test_dist_peer_host_staged(gpu):
+    """two components per rank through the several-GPUs-per-rank path (dist.force_peer)"""
+    _run(2, "host", cases="peer")
+
+
+@pytest.mark.parametrize("nprocs", [2, 4])
+def test_dist_rccl_nccl_pg_peer(gpu, nprocs):
+    """bench.py's real N > 1 start-up -- init_process_group("nccl", device_id=...) and a second
+    RCCL communicator for the library (Comm.from_torch_distributed) -- with the golden
+    contractions, the reductions, and two components per rank through the peer path"""
+    import torch
+    _run(nprocs, "rccl", cases="golden,reduce,peer", shared=torch.cuda.device_count() < nprocs,
+         pg="nccl")
