@@ -1193,7 +1193,7 @@ def dist_available():
 
 def dense_bench(sb, dev, L=16, n=12, reps=5):
     """The dense batched solvers on one 12x12 complex<double> matrix per site of
-    the 16^4 lattice (tools/dense_bench.py): inversion and Cholesky, kernel time from the
+    the 16^4 lattice (tools/studies/dense_bench.py): inversion and Cholesky, kernel time from the
     library's timers and the whole call (layout copies included); bytes = the matrices in and
     out once."""
     nb = L ** 4

@@ -111,7 +111,7 @@ int sbx_timings_report(char *buf, int len);
    Override a kernel-shape choice of the library for tuning / comparison runs.  The defaults are
    the measured winners; read a key with sbx_tune_get before changing it to
    restore it afterwards.  Keys: "gemm.m3", "gemm.splits", "gemm.max_bytes", "gemm.t48",
-   "gemm.share_ab", "copy.nt", "copy.budget", "copy.run", "copy.max_elems", "copy.pair",
+   "gemm.share_ab", "gemm.loaders", "gemm.dma_spread", "gemm.skinny", "copy.nt", "copy.budget", "copy.run", "copy.max_elems", "copy.pair",
    "copy.order", "copy.trans", "copy.btrans", "bsr.variant", "bsr.row_max_cols", "bsr.split_max_cols",
    "bsr.split_cw", "bsr.split_jb", "bsr.split_ilv", "bsr.kron_mfma", "bsr.kron_mfma_min_cols",
    "bsr.kron_pack", "bsr.kron_xlds", "bsr.kron_ylds", "bsr.nt", "bsr.blk_pd", "dense.wave", "dist.reduce" (must be set alike on every rank: the ranks' reductions must

@@ -413,6 +413,9 @@ int sbx_tune_set(const char *key, long long value) {
         else if (k == "copy.trans") g_copy_tune.trans = (int)value;
         else if (k == "copy.btrans") g_copy_tune.btrans = (int)value;
         else if (k == "gemm.max_bytes") g_gemm_tune.max_bytes = (long)value;
+        else if (k == "gemm.loaders") g_gemm_tune.loaders = (int)value;
+        else if (k == "gemm.dma_spread") g_gemm_tune.dma_spread = (int)value;
+        else if (k == "gemm.skinny") g_gemm_tune.skinny = (int)value;
         else if (k == "bsr.variant") g_bsr_tune.variant = (int)value;
         else if (k == "bsr.row_max_cols") g_bsr_tune.row_max_cols = (long)value;
         else if (k == "bsr.split_max_cols") g_bsr_tune.split_max_cols = (long)value;
@@ -461,6 +464,9 @@ int sbx_tune_get(const char *key, long long *value) {
         else if (k == "copy.btrans") *value = g_copy_tune.btrans;
         else if (k == "copy.last_pair") *value = g_copy_tune.last_pair;
         else if (k == "gemm.max_bytes") *value = g_gemm_tune.max_bytes;
+        else if (k == "gemm.loaders") *value = g_gemm_tune.loaders;
+        else if (k == "gemm.dma_spread") *value = g_gemm_tune.dma_spread;
+        else if (k == "gemm.skinny") *value = g_gemm_tune.skinny;
         else if (k == "bsr.variant") *value = g_bsr_tune.variant;
         else if (k == "bsr.row_max_cols") *value = g_bsr_tune.row_max_cols;
         else if (k == "bsr.split_max_cols") *value = g_bsr_tune.split_max_cols;

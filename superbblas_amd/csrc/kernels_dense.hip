@@ -17,7 +17,10 @@
 #include <algorithm>
 
 namespace sbx {
-int g_dense_wave = 1;
+// 2: the small-matrix wave kernels for the factorizations and the triangular solves (round 5:
+// 12 rhs per site trsm 467 -> 266 us; the multi-rank dense cases run with every setting,
+// tests/dist_worker.py case_dense)
+int g_dense_wave = 2;
 namespace {
 
 constexpr int DTH = 256;

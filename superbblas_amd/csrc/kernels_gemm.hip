@@ -97,6 +97,8 @@ struct GemmKArgs {
     long kchunk;
     void *work;
     unsigned long long *probe; // tools only: workgroup 0 stores s_memtime / s_memrealtime at its start and end
+    int probe_all;             // tools only: every workgroup stores s_memrealtime at its start, at the end of
+                               // its main loop and at its end in probe[2 + 3 * blockIdx.x ...]
     int tm, tn;
     unsigned a_bytes, b_bytes; // extent of one batch entry of A / B (buffer descriptor range)
     // split label groups: index i of M (N, K) is (i / m_lo, i % m_lo) with strides (sa_m_hi,
@@ -308,6 +310,13 @@ __global__ void __launch_bounds__(WM *WN * 64) gemm_kernel(const GemmKArgs p) {
                         *w = vr;
                 }
             }
+    if (p.probe && p.probe_all) {
+        __syncthreads();
+        if (tid == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            p.probe[4 + 3 * bid] = __builtin_amdgcn_s_memrealtime();
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -396,6 +405,53 @@ struct DmaOperand {
     }
 };
 
+// Loader-wave DMA of a K-major operand whose rows are one run (no split groups): the first LWT
+// threads of the workgroup (LW = LWT / 64 "loader" waves) issue the whole slab image while the
+// other waves only read fragments and issue MFMAs.  Lane slot = tid + LWT * i (i < NI), so a
+// lane's granule column and swizzle are the same for every i and its state is three registers
+// (the per-lane arrays of DmaOperand would cost 6 NI of them).  The image is DmaOperand<true>'s.
+template <int R, int BKK, int LWT, int ES> struct DmaRowsK {
+    static constexpr int EPG = 16 / ES, GR = BKK / EPG, GTOT = R * BKK / EPG, NI = GTOT / LWT;
+    static constexpr int RSTEP = LWT / GR; // rows between a lane's consecutive granules
+    static_assert(GTOT % LWT == 0 && LWT % GR == 0 && GR <= 16 && (RSTEP / (16 / GR)) % GR == 0,
+                  "loader lane map");
+    unsigned off0, step;
+    int k, rleft;
+    __device__ __forceinline__ void init(int tid, long r0, long nrows, long s_r, long s_k) {
+        const int r = tid / GR;
+        k = ((tid % GR) ^ ((r / (16 / GR)) & (GR - 1))) * EPG;
+        rleft = (int)min(nrows - r0 - r, (long)0x7fffffff);
+        off0 = (unsigned)(((r0 + r) * s_r + (long)k * s_k) * ES); // (used only while in range)
+        step = (unsigned)((long)RSTEP * s_r * ES);
+    }
+    // issue granules i in [ib, ie) of slab [k0, k0+BKK) into the image at `lds_base`
+    __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, const char *lds_base,
+                                          int wave, long k0, long k_end, long s_k, int ib,
+                                          int ie) const {
+        const unsigned kpart = (unsigned)(k0 * s_k * ES);
+        const bool kok = k0 + k < k_end;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            if (i < ib || i >= ie) continue;
+            const bool ok = kok && RSTEP * i < rleft;
+            const unsigned off = ok ? off0 + (unsigned)i * step + kpart : 0x80000000u;
+            const unsigned dst = lds_addr(lds_base) + (unsigned)(i * LWT + wave * 64) * 16;
+            asm volatile("s_mov_b32 m0, %1\n\t"
+                         "s_nop 0\n\t"
+                         "buffer_load_dwordx4 %0, %2, 0 offen lds"
+                         :
+                         : "v"(off), "s"(dst), "s"(rs)
+                         : "memory", "m0");
+        }
+    }
+};
+
+struct NoLoader { // (LW == 0: every wave issues its share through DmaOperand)
+    static constexpr int NI = 0;
+    __device__ void init(int, long, long, long, long) {}
+    __device__ void issue(__amdgpu_buffer_rsrc_t, const char *, int, long, long, long, int, int) const {}
+};
+
 // M3: complex products in the 3-multiplication (Gauss) form, P1 = ar*br, P2 = ai*bi,
 // P3 = (ar+ai)*(br+bi), re = P1 - P2, im = P3 - P1 - P2: 3 real MFMAs per complex k-step instead
 // of 4 (a third accumulator per tile; the operand sums are one VALU add per fragment element)
@@ -409,8 +465,10 @@ struct DmaOperand {
 // SH: every tile of the launch is a diagonal tile of a tensor contracted with itself (same_ab,
 // one tile row and column): the slab image holds A only, so the double buffer takes half the LDS
 // and twice the workgroups fit a CU
+// LW > 0: only waves 0..LW-1 issue the slab DMA (K-major operands without split groups), each
+// spreading its share over the first SP k-steps of the slab; the other waves issue no DMA
 template <typename R, bool CPLX, bool AK, bool BK, int BM, int BN, int BKK, int WM, int WN,
-          bool M3 = false, bool PF = false, int KG = 1, bool SH = false>
+          bool M3 = false, bool PF = false, int KG = 1, bool SH = false, int LW = 0, int SP = 1>
 __global__ void __launch_bounds__(WM *WN *KG * 64) gemm_dma_kernel(const GemmKArgs p) {
     typedef typename Elem<R, CPLX>::type E;
     typedef typename Mfma<R>::acc_t acc_t;
@@ -424,6 +482,10 @@ __global__ void __launch_bounds__(WM *WN *KG * 64) gemm_dma_kernel(const GemmKAr
     static_assert(MT * 16 == WTM && NT * 16 == WTN, "bad wave tile");
     typedef DmaOperand<AK, BM, BKK, NTH, ES> OpA;
     typedef DmaOperand<BK, BN, BKK, NTH, ES> OpB;
+    static_assert(LW == 0 || (AK && BK && !SH && KG == 1 && !PF), "loader waves: K-major operands");
+    typedef typename std::conditional<(LW > 0), DmaRowsK<BM, BKK, LW * 64, ES>, NoLoader>::type LdA;
+    typedef typename std::conditional<(LW > 0), DmaRowsK<BN, BKK, LW * 64, ES>, NoLoader>::type LdB;
+    static_assert(LW == 0 || BKK / 4 >= SP, "loader spread: SP k-steps per slab at most");
     // the double buffer, also the k-groups' reduction area at the end
     constexpr int LDS_E = KG > 1 && BM * BN > 2 * SLAB ? BM * BN : 2 * SLAB;
     __shared__ __attribute__((aligned(16))) E lds[LDS_E]; // the only LDS object
@@ -451,15 +513,23 @@ __global__ void __launch_bounds__(WM *WN *KG * 64) gemm_dma_kernel(const GemmKAr
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     unsigned long long clk0 = 0, rt0 = 0;
-    if (p.probe && bid == 0) {
+    if (p.probe && (bid == 0 || p.probe_all)) {
         clk0 = __builtin_amdgcn_s_memtime();
         rt0 = __builtin_amdgcn_s_memrealtime();
     }
     OpA da;
     OpB db;
+    LdA la;
+    LdB lb;
     const bool spl = p.split != 0;
-    da.init(tid, m0, p.m, p.sa_m, p.sa_k, spl, p.m_lo, p.sa_m_hi);
-    db.init(tid, n0, p.n, p.sb_n, p.sb_k, spl, p.n_lo, p.sb_n_hi);
+    if constexpr (LW == 0) {
+        da.init(tid, m0, p.m, p.sa_m, p.sa_k, spl, p.m_lo, p.sa_m_hi);
+        db.init(tid, n0, p.n, p.sb_n, p.sb_k, spl, p.n_lo, p.sb_n_hi);
+    } else {
+        la.init(tid, m0, p.m, p.sa_m, p.sa_k);
+        lb.init(tid, n0, p.n, p.sb_n, p.sb_k);
+    }
+    const bool loader = LW > 0 && wave < LW;
 
     const int kg = KG > 1 ? wave / (WM * WN) : 0, w2 = KG > 1 ? wave % (WM * WN) : wave;
     const int wm = w2 / WN, wn = w2 % WN;
@@ -486,21 +556,39 @@ __global__ void __launch_bounds__(WM *WN *KG * 64) gemm_dma_kernel(const GemmKAr
     constexpr bool CAN_SHARE = AK == BK && BM == BN; // same slab image layout for A and B
     const bool share = SH || (CAN_SHARE && p.same_ab && m0 == n0);
     if (nslab > 0) {
-        da.issue(rsA, base, wave, k_begin, k_end, p.sa_k, spl, p.k_lo, p.sa_k_hi);
-        if (!share)
-            db.issue(rsB, base + BM * BKK * ES, wave, k_begin, k_end, p.sb_k, spl, p.k_lo, p.sb_k_hi);
+        if constexpr (LW == 0) {
+            da.issue(rsA, base, wave, k_begin, k_end, p.sa_k, spl, p.k_lo, p.sa_k_hi);
+            if (!share)
+                db.issue(rsB, base + BM * BKK * ES, wave, k_begin, k_end, p.sb_k, spl, p.k_lo, p.sb_k_hi);
+        } else if (loader) {
+            la.issue(rsA, base, wave, k_begin, k_end, p.sa_k, 0, LdA::NI);
+            if (!share) lb.issue(rsB, base + BM * BKK * ES, wave, k_begin, k_end, p.sb_k, 0, LdB::NI);
+        }
     }
     for (long s = 0; s < nslab; ++s) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // this wave's DMA of slab s landed
         __syncthreads(); // ... and every wave's; the other buffer is free again
         const int cur = (int)(s & 1);
-        if (s + 1 < nslab) {
-            const char *nb = base + (size_t)(cur ^ 1) * SLAB * ES;
-            const long kn = k_begin + (s + 1) * BKK;
+        const char *nb = base + (size_t)(cur ^ 1) * SLAB * ES;
+        const long kn = k_begin + (s + 1) * BKK;
+        if (LW == 0 && s + 1 < nslab) {
             da.issue(rsA, nb, wave, kn, k_end, p.sa_k, spl, p.k_lo, p.sa_k_hi);
             if (!share)
                 db.issue(rsB, nb + BM * BKK * ES, wave, kn, k_end, p.sb_k, spl, p.k_lo, p.sb_k_hi);
         }
+        // loader waves: the pieces of k-step q of SP (the next slab's DMA spread over this one's
+        // first SP k-steps)
+        auto load_part = [&](int q) {
+            if constexpr (LW > 0) {
+                if (loader && s + 1 < nslab && q < SP) {
+                    la.issue(rsA, nb, wave, kn, k_end, p.sa_k, q * LdA::NI / SP,
+                             (q + 1) * LdA::NI / SP);
+                    if (!share)
+                        lb.issue(rsB, nb + BM * BKK * ES, wave, kn, k_end, p.sb_k,
+                                 q * LdB::NI / SP, (q + 1) * LdB::NI / SP);
+                }
+            }
+        };
         const E *As = lds + cur * SLAB;
         const E *Bs = share ? As : As + BM * BKK;
         if constexpr (PF && CPLX && !M3) {
@@ -540,6 +628,7 @@ __global__ void __launch_bounds__(WM *WN *KG * 64) gemm_dma_kernel(const GemmKAr
         }
 #pragma unroll
         for (int kk = 4 * kg; kk < BKK; kk += 4 * KG) {
+            load_part(kk / 4);
             E af[MT], bf[NT];
 #pragma unroll
             for (int i = 0; i < MT; ++i) af[i] = As[OpA::slot(frow + 16 * i, kk + kq)];
@@ -640,6 +729,10 @@ __global__ void __launch_bounds__(WM *WN *KG * 64) gemm_dma_kernel(const GemmKAr
         const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
         p.probe[0] = clk1 - clk0; // shader clock cycles
         p.probe[1] = rt1 - rt0;   // 100 MHz reference ticks
+    }
+    if (p.probe && p.probe_all && tid == 0) {
+        p.probe[2 + 3 * bid] = rt0;
+        p.probe[3 + 3 * bid] = __builtin_amdgcn_s_memrealtime();
     }
     const int ccol = lane & 15;
 #pragma unroll
@@ -883,6 +976,121 @@ __global__ void __launch_bounds__(KG * 64) gemm_wave_kernel(const GemmKArgs p, u
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Skinny products: an output dimension of a few rows gets no 16x16 MFMA padding (the
+// reference's dot / gemv shortcuts for m = 1 / n = 1, blas.h:686-800; the inner-product and
+// update shapes its tests/dist.cpp:160-195 times).
+//  * gemm_dot_kernel, m, n <= 4 (inner products, long k): one workgroup per (batch entry,
+//    k-chunk); lanes stride over k keeping all m x n sums in registers, which are reduced across
+//    the wave (xor shuffles) and the workgroup (LDS) in a fixed order; split-K partials are summed
+//    by splitk_reduce_kernel in split order -- deterministic.
+//  * gemm_rows_kernel, n <= 16 (updates and matrix-vector products, long m): one lane per (row,
+//    batch entry) keeps its row's n outputs; the lanes of a wave read 64 consecutive rows of A.
+//    m <= 16 with a long n runs as the transposed problem (C^T = op(B)^T op(A)^T).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ double2 madd(double2 c, double2 a, double2 b) {
+    return double2{c.x + a.x * b.x - a.y * b.y, c.y + a.x * b.y + a.y * b.x};
+}
+__device__ __forceinline__ float2 madd(float2 c, float2 a, float2 b) {
+    return float2{c.x + a.x * b.x - a.y * b.y, c.y + a.x * b.y + a.y * b.x};
+}
+__device__ __forceinline__ double madd(double c, double a, double b) { return c + a * b; }
+__device__ __forceinline__ float madd(float c, float a, float b) { return c + a * b; }
+template <typename E> __device__ __forceinline__ E xor_sum(E v, int m) {
+    if constexpr (std::is_same<E, double2>::value || std::is_same<E, float2>::value)
+        return E{v.x + __shfl_xor(v.x, m), v.y + __shfl_xor(v.y, m)};
+    else
+        return v + __shfl_xor(v, m);
+}
+template <typename R, bool CPLX> __device__ __forceinline__ void store_out(const GemmKArgs &p, long bb, long gi, long gj, typename Elem<R, CPLX>::type v) {
+    if constexpr (CPLX)
+        epilogue_store<R>((R *)((typename Elem<R, CPLX>::type *)p.c + bb * p.sc_b + gi * p.sc_m + gj * p.sc_n), v.x, v.y, p, true);
+    else
+        epilogue_store<R>((R *)p.c + bb * p.sc_b + gi * p.sc_m + gj * p.sc_n, v, R(0), p, false);
+}
+
+template <typename R, bool CPLX, int MM, int NN>
+__global__ void __launch_bounds__(256) gemm_dot_kernel(const GemmKArgs p) {
+    typedef typename Elem<R, CPLX>::type E;
+    const int split = (int)(blockIdx.x % (unsigned)p.splits);
+    const long bb = blockIdx.x / (unsigned)p.splits;
+    const long k0 = (long)split * p.kchunk, k1 = min(p.k, k0 + p.kchunk);
+    const E *A = (const E *)p.a + bb * p.sa_b, *B = (const E *)p.b + bb * p.sb_b;
+    const int m = (int)p.m, n = (int)p.n;
+    E acc[MM][NN];
+#pragma unroll
+    for (int i = 0; i < MM; ++i)
+#pragma unroll
+        for (int j = 0; j < NN; ++j) acc[i][j] = zero_elem<E>();
+    for (long k = k0 + threadIdx.x; k < k1; k += 256) {
+        E a[MM], b[NN];
+#pragma unroll
+        for (int i = 0; i < MM; ++i)
+            a[i] = i < m ? conj_if(A[i * p.sa_m + k * p.sa_k], p.conja) : zero_elem<E>();
+#pragma unroll
+        for (int j = 0; j < NN; ++j)
+            b[j] = j < n ? conj_if(B[k * p.sb_k + j * p.sb_n], p.conjb) : zero_elem<E>();
+#pragma unroll
+        for (int i = 0; i < MM; ++i)
+#pragma unroll
+            for (int j = 0; j < NN; ++j) acc[i][j] = madd(acc[i][j], a[i], b[j]);
+    }
+    __shared__ E red[4][MM * NN];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < MM; ++i)
+#pragma unroll
+        for (int j = 0; j < NN; ++j) {
+            E v = acc[i][j];
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) v = xor_sum(v, o);
+            if (lane == 0) red[wave][i * NN + j] = v;
+        }
+    __syncthreads();
+    const int t = threadIdx.x;
+    if (t < m * n) {
+        const int i = t % m, j = t / m;
+        E v = red[0][i * NN + j];
+#pragma unroll
+        for (int w = 1; w < 4; ++w) {
+            if constexpr (CPLX) {
+                v.x += red[w][i * NN + j].x;
+                v.y += red[w][i * NN + j].y;
+            } else {
+                v += red[w][i * NN + j];
+            }
+        }
+        if (p.splits == 1)
+            store_out<R, CPLX>(p, bb, i, j, v);
+        else
+            ((E *)p.work)[(((long)split * p.batch + bb) * p.n + j) * p.m + i] = v;
+    }
+}
+
+template <typename R, bool CPLX, int NN>
+__global__ void __launch_bounds__(256) gemm_rows_kernel(const GemmKArgs p) {
+    typedef typename Elem<R, CPLX>::type E;
+    const long total = p.m * p.batch;
+    const int n = (int)p.n;
+    for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256L) {
+        const long i = idx % p.m, bb = idx / p.m;
+        const E *A = (const E *)p.a + bb * p.sa_b + i * p.sa_m;
+        const E *B = (const E *)p.b + bb * p.sb_b;
+        E acc[NN];
+#pragma unroll
+        for (int j = 0; j < NN; ++j) acc[j] = zero_elem<E>();
+        for (long k = 0; k < p.k; ++k) {
+            const E a = conj_if(A[k * p.sa_k], p.conja);
+#pragma unroll
+            for (int j = 0; j < NN; ++j)
+                if (j < n) acc[j] = madd(acc[j], a, conj_if(B[k * p.sb_k + j * p.sb_n], p.conjb));
+        }
+#pragma unroll
+        for (int j = 0; j < NN; ++j)
+            if (j < n) store_out<R, CPLX>(p, bb, i, j, acc[j]);
+    }
+}
+
 // C = alpha * sum_s W[s] + beta * C, summed in split order (deterministic)
 template <typename R, bool CPLX>
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(const GemmKArgs p) {
@@ -1009,7 +1217,7 @@ void launch_tiled_cfg(const GemmKArgs &p0, int device, hipStream_t stream, long 
 
 /// Launch one tile configuration of the LDS-DMA kernel
 template <typename R, bool CPLX, bool AK, bool BK, int BM, int BN, int BKK, int WM, int WN,
-          bool ALLOW_M3 = true, bool PF = false, int KG = 1, bool SH = false>
+          bool ALLOW_M3 = true, bool PF = false, int KG = 1, bool SH = false, int LW = 0, int SP = 1>
 void launch_dma_cfg(const GemmKArgs &p0, int device, hipStream_t stream, long splits = 0,
                     long target_wgs = 1024) {
     // complex: the 4-multiplication form unless the 3-multiplication form is asked for (config
@@ -1037,7 +1245,7 @@ void launch_dma_cfg(const GemmKArgs &p0, int device, hipStream_t stream, long sp
                 hipLaunchKernelGGL((gemm_dma_kernel<R, CPLX, AK, BK, BM, BN, BKK, WM, WN>),
                                    dim3((unsigned)nwg), dim3(WM * WN * 64), 0, stream, p);
         } else
-            hipLaunchKernelGGL((gemm_dma_kernel<R, CPLX, AK, BK, BM, BN, BKK, WM, WN, false, PF, KG, SH>),
+            hipLaunchKernelGGL((gemm_dma_kernel<R, CPLX, AK, BK, BM, BN, BKK, WM, WN, false, PF, KG, SH, LW, SP>),
                                dim3((unsigned)nwg), dim3(WM * WN * KG * 64), 0, stream, p);
         SBX_HIP_CHECK(hipGetLastError());
     }
@@ -1114,7 +1322,23 @@ void launch_tiled(const GemmKArgs &p, int device, hipStream_t stream) {
         if (p.m >= 128 && p.n >= 128) {
             if (m3)
                 launch_dma_cfg<R, CPLX, AK, BK, 128, 128, 8, 4, 2>(p, device, stream, 0, 256);
-            else
+            else if constexpr (AK && BK) {
+                // loader waves (gemm.loaders / gemm.dma_spread, K-major operands without split
+                // groups): only waves 0..LW-1 issue the slab DMA
+                const int lw = p.split ? 0 : g_gemm_tune.loaders, sp = g_gemm_tune.dma_spread;
+                if (lw == 4 && sp == 4)
+                    launch_dma_cfg<R, CPLX, AK, BK, 128, 128, 16, 4, 4, false, false, 1, false, 4, 4>(p, device, stream, 0, 256);
+                else if (lw == 4)
+                    launch_dma_cfg<R, CPLX, AK, BK, 128, 128, 16, 4, 4, false, false, 1, false, 4, 1>(p, device, stream, 0, 256);
+                else if (lw == 8 && sp == 4)
+                    launch_dma_cfg<R, CPLX, AK, BK, 128, 128, 16, 4, 4, false, false, 1, false, 8, 4>(p, device, stream, 0, 256);
+                else if (lw == 8)
+                    launch_dma_cfg<R, CPLX, AK, BK, 128, 128, 16, 4, 4, false, false, 1, false, 8, 1>(p, device, stream, 0, 256);
+                else if (lw == 16 && sp == 4)
+                    launch_dma_cfg<R, CPLX, AK, BK, 128, 128, 16, 4, 4, false, false, 1, false, 16, 4>(p, device, stream, 0, 256);
+                else
+                    launch_dma_cfg<R, CPLX, AK, BK, 128, 128, 16, 4, 4, false>(p, device, stream, 0, 256);
+            } else
                 launch_dma_cfg<R, CPLX, AK, BK, 128, 128, 16, 4, 4, false>(p, device, stream, 0, 256);
         } else {
             launch_dma_cfg<R, CPLX, AK, BK, 64, 64, 8, 2, 2>(p, device, stream, 0, 1024);
@@ -1166,7 +1390,73 @@ void launch_tiled(const GemmKArgs &p, int device, hipStream_t stream) {
     }
 }
 
+/// The skinny forms (gemm_dot_kernel / gemm_rows_kernel) when an output dimension is tiny;
+/// false when the shape is for the MFMA kernels
+template <typename R, bool CPLX> bool launch_skinny(const GemmKArgs &p0, int device, hipStream_t s) {
+    if (!g_gemm_tune.skinny || p0.split) return false;
+    typedef typename Elem<R, CPLX>::type E;
+    GemmKArgs p = p0;
+    if (p.m <= 4 && p.n <= 4) {
+        // split-K to ~256 workgroups, chunks of >= 1024 k
+        long splits = std::max(1L, std::min((256 + p.batch - 1) / p.batch, (p.k + 1023) / 1024));
+        p.kchunk = (p.k + splits - 1) / splits;
+        splits = std::max(1L, (p.k + p.kchunk - 1) / p.kchunk);
+        p.splits = (int)splits;
+        Scratch work;
+        if (splits > 1) {
+            work = Scratch(sizeof(E) * splits * p.batch * p.m * p.n, device);
+            p.work = work.ptr;
+        }
+        const long nwg = p.batch * splits;
+        if (nwg > 0x7fffffffL) return false;
+        KernelTimer total("gemm_total", s);
+        {
+            KernelTimer timer("gemm", s);
+            const long mx = std::max(p.m, p.n);
+            if (mx == 1)
+                hipLaunchKernelGGL((gemm_dot_kernel<R, CPLX, 1, 1>), dim3((unsigned)nwg), dim3(256), 0, s, p);
+            else if (mx == 2)
+                hipLaunchKernelGGL((gemm_dot_kernel<R, CPLX, 2, 2>), dim3((unsigned)nwg), dim3(256), 0, s, p);
+            else
+                hipLaunchKernelGGL((gemm_dot_kernel<R, CPLX, 4, 4>), dim3((unsigned)nwg), dim3(256), 0, s, p);
+            SBX_HIP_CHECK(hipGetLastError());
+        }
+        launch_reduce<R, CPLX>(p, s);
+        return true;
+    }
+    // one long output dimension, the other <= 16, and a short k (updates) or a vector
+    const bool rows = p.n <= 16 && p.m >= 2 * p.n && (p.k <= 64 || p.n == 1);
+    const bool cols = p.m <= 16 && p.n >= 2 * p.m && (p.k <= 64 || p.m == 1);
+    if (!rows && !cols) return false;
+    if (!rows) { // C^T = op(B)^T op(A)^T: the long dimension becomes the rows
+        std::swap(p.m, p.n);
+        std::swap(p.a, p.b);
+        std::swap(p.sa_m, p.sb_n);
+        std::swap(p.sa_k, p.sb_k);
+        std::swap(p.sa_b, p.sb_b);
+        std::swap(p.conja, p.conjb);
+        std::swap(p.sc_m, p.sc_n);
+    }
+    const long total = p.m * p.batch;
+    const long blocks = std::max(1L, std::min((total + 255) / 256, 65536L));
+    KernelTimer total_t("gemm_total", s);
+    KernelTimer timer("gemm", s);
+    if (p.n == 1)
+        hipLaunchKernelGGL((gemm_rows_kernel<R, CPLX, 1>), dim3((unsigned)blocks), dim3(256), 0, s, p);
+    else if (p.n <= 2)
+        hipLaunchKernelGGL((gemm_rows_kernel<R, CPLX, 2>), dim3((unsigned)blocks), dim3(256), 0, s, p);
+    else if (p.n <= 4)
+        hipLaunchKernelGGL((gemm_rows_kernel<R, CPLX, 4>), dim3((unsigned)blocks), dim3(256), 0, s, p);
+    else if (p.n <= 8)
+        hipLaunchKernelGGL((gemm_rows_kernel<R, CPLX, 8>), dim3((unsigned)blocks), dim3(256), 0, s, p);
+    else
+        hipLaunchKernelGGL((gemm_rows_kernel<R, CPLX, 16>), dim3((unsigned)blocks), dim3(256), 0, s, p);
+    SBX_HIP_CHECK(hipGetLastError());
+    return true;
+}
+
 template <typename R, bool CPLX> void launch_typed(const GemmKArgs &p, int device, hipStream_t s) {
+    if (launch_skinny<R, CPLX>(p, device, s)) return;
     // Pick the stage-load thread map from the unit stride of each operand
     const bool ak = (p.sa_k == 1) || (p.sa_m != 1 && std::labs(p.sa_k) <= std::labs(p.sa_m));
     const bool bk = (p.sb_k == 1) || (p.sb_n != 1 && std::labs(p.sb_k) <= std::labs(p.sb_n));

@@ -243,6 +243,11 @@ struct GemmTune {
                  ///< choice: wave rings of 8 waves, 8-deep slabs, for a tensor contracted with
                  ///< itself, else k-group workgroups)
     int share_ab = 1; ///< LDS-DMA kernel: one slab image for A and B when they are the same memory (0 = off)
+    int loaders = 0; ///< complex<double> 128x128 LDS-DMA kernel, K-major operands: only this many waves
+                     ///< (4, 8, 16) issue the slab DMA (0 = every wave its share)
+    int dma_spread = 1; ///< ... the loader waves spread their DMA over this many k-steps (1 or 4)
+    int skinny = 1; ///< outputs with a dimension of <= 4 (and <= 16 with a short k): the dot / rows
+                    ///< kernels instead of MFMA tiles (0 = off)
 };
 extern GemmTune g_gemm_tune;
 struct BsrTune {
@@ -277,7 +282,7 @@ struct BsrTune {
 };
 extern BsrTune g_bsr_tune;
 /// dense solvers: matrices up to 16 x 16 packed 64 / n per wave -- 1: Cholesky and LU
-/// (inversion, gesm; the default), 2: the triangular solves too; 0 = the workgroup-per-matrix
+/// (inversion, gesm), 2: the triangular solves too (the default); 0 = the workgroup-per-matrix
 /// kernels
 extern int g_dense_wave;
 

@@ -321,8 +321,20 @@ def case_kron(sb, comm, rank, n, dev, ncols=2, power=2):
 
 
 def case_dense(sb, comm, rank, n, dev):
-    """cholesky / gesm with the matrices split over ranks along a row label (the working copy
-    gathers whole matrices: a redistribution), and the batch label split too."""
+    """cholesky / gesm / trsm with the matrices split over ranks along a row label (the working
+    copy gathers whole matrices: a redistribution), and the batch label split too; with every
+    dense.wave setting (2: the wave kernels for the triangular solves too, the default; 1: for
+    the factorizations only; 0: the workgroup-per-matrix kernels), set alike on every rank"""
+    old = sb.tune_get("dense.wave")
+    try:
+        for wave in (2, 1, 0):
+            sb.tune_set("dense.wave", wave)
+            _case_dense(sb, comm, rank, n, dev)
+    finally:
+        sb.tune_set("dense.wave", old)
+
+
+def _case_dense(sb, comm, rank, n, dev):
     from _common import oracle_getrf, oracle_getrs, oracle_potrf
     from _dense import dense_input, from_matrices, to_matrices, to_panel, from_panel
     nt, ni = 4, 6
@@ -364,6 +376,18 @@ def case_dense(sb, comm, rank, n, dev):
     oracle_getrs(w, ni, nt, piv, 4, xm)
     ref = 2.0 * from_panel(xm.reshape(nt, 4, ni), "tin", dimx, "n", "i")
     assert np.allclose(out, ref, rtol=0, atol=1e-12 * np.abs(ref).max()), "dense gesm"
+    # trsm: an upper triangular C (its strict lower part is garbage the solve must not read)
+    # split over t, x over t, y over its rows
+    ct = dense_input("tri", nt, ni, np.complex128)
+    vc = scatter(sb, from_matrices(ct, "tij", dim, "i", "j"), dim, pc, rank, 1, dev)
+    vy = scatter(sb, np.zeros_like(gx), dimx, py, rank, 1, dev)
+    sb.trsm(0.5 - 1j, pc, dim, "tij", vc, "i", "j", px, dimxp, "ntj", vx, py, dimx, "tin", vy,
+            comm=comm)
+    torch.cuda.synchronize()
+    out = gather(np.zeros_like(gx), dimx, py, 1, vy)
+    xs = gx.reshape(dimx)
+    ref = np.stack([(0.5 - 1j) * np.linalg.solve(np.triu(ct[t]), xs[t]) for t in range(nt)]).ravel()
+    assert np.allclose(out, ref, rtol=0, atol=1e-12 * np.abs(ref).max()), "dense trsm"
 
 
 def case_storage(sb, comm, rank, n, dev):

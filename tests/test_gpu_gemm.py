@@ -34,8 +34,7 @@ def _run(gpu, dtype, ta, tb, m, n, k, batch, alpha, beta, pad=0):
 
 
 @pytest.mark.parametrize("dtype", [np.complex128, np.float64, np.complex64, np.float32])
-@pytest.mark.parametrize("ta,tb", [("N", "N"), ("T", "N"), ("N", "T"), ("T", "T"), ("C", "N"),
-                                   ("C", "T"), ("N", "C")])
+@pytest.mark.parametrize("ta,tb", [(x, y) for x in "NTC" for y in "NTC"])
 def test_gemm_small(gpu, dtype, ta, tb):
     out, ref = _run(gpu, dtype, ta, tb, 37, 21, 45, 3, 1.5 - 0.5j, 0.25 + 1j, pad=3)
     assert rel_err(out, ref) < TOL[dtype]
@@ -162,3 +161,27 @@ def test_gemm_same_operand_mmajor(gpu, dtype, m, k, batch, tb, t48):
                 a, m, k * m, 0.0, ref, m, m * m, batch)
     assert rel_err(outs[0], ref) < TOL[dtype]
     assert rel_err(outs[1], ref) < TOL[dtype]
+
+
+# the skinny forms (blas.h:686-800's dot / gemv shortcuts; tests/dist.cpp:160-195's inner-product
+# m = n <= 12, k = 6144 and update m = 6144, n = k <= 12 shapes): gemm_dot_kernel for m, n <= 4,
+# gemm_rows_kernel for one dimension <= 16 (and a short k, or a vector), the transposed problem
+# for a short m; the same shapes through the MFMA tiles (gemm.skinny 0) agree with the oracle too
+SKINNY = [(1, 1, 6144, 8), (2, 2, 6144, 8), (3, 4, 6000, 2), (4, 1, 100, 5), (1, 3, 7, 3),
+          (6144, 1, 1, 8), (6144, 3, 3, 2), (1000, 12, 12, 2), (999, 16, 5, 1), (1, 700, 9, 2),
+          (12, 500, 12, 2), (777, 1, 300, 2), (1, 500, 301, 1)]
+
+
+@pytest.mark.parametrize("dtype", [np.complex128, np.float64, np.complex64, np.float32])
+@pytest.mark.parametrize("ta,tb", [("N", "N"), ("T", "N"), ("C", "T"), ("N", "C"), ("T", "C")])
+@pytest.mark.parametrize("m,n,k,batch", SKINNY)
+@pytest.mark.parametrize("skinny", [1, 0])
+def test_gemm_skinny(gpu, dtype, ta, tb, m, n, k, batch, skinny):
+    import superbblas_amd as sb
+    old = sb.tune_get("gemm.skinny")
+    sb.tune_set("gemm.skinny", skinny)
+    try:
+        out, ref = _run(gpu, dtype, ta, tb, m, n, k, batch, 0.5 + 0.25j, -1.0 + 0.5j, pad=1)
+    finally:
+        sb.tune_set("gemm.skinny", old)
+    assert rel_err(out, ref) < TOL[dtype]
