@@ -243,8 +243,9 @@ struct GemmTune {
                  ///< choice: wave rings of 8 waves, 8-deep slabs, for a tensor contracted with
                  ///< itself, else k-group workgroups)
     int share_ab = 1; ///< LDS-DMA kernel: one slab image for A and B when they are the same memory (0 = off)
-    int loaders = 0; ///< complex<double> 128x128 LDS-DMA kernel, K-major operands: only this many waves
-                     ///< (4, 8, 16) issue the slab DMA (0 = every wave its share)
+    int loaders = 8; ///< complex<double> 128x128 LDS-DMA kernel, K-major operands: only this many waves
+                     ///< (4, 8, 16) issue the slab DMA (0 = every wave its share); config 2: 1.491 ->
+                     ///< 1.475 ms at 4 or 8 (tools/studies/gemm_loaders.py, profiles/r05_gemm_loaders.txt)
     int dma_spread = 1; ///< ... the loader waves spread their DMA over this many k-steps (1 or 4)
     int skinny = 1; ///< outputs with a dimension of <= 4 (and <= 16 with a short k): the dot / rows
                     ///< kernels instead of MFMA tiles (0 = off)
