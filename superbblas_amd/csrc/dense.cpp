@@ -156,6 +156,18 @@ void dense_inversion(const DistTensor &v, const std::string &orows, const std::s
     Work w = prepare(v, orows, ocols, comm, true, "inversion", true);
     std::vector<Scratch> inv;
     DistTensor wi = w.t;
+    if (dense_wave_rows(w.n)) {
+        // the small-matrix wave kernels read a matrix whole before writing its inverse: inverted in
+        // place, no copy of the factors (a failed matrix is left as it was)
+        for (std::size_t c = 0; c < w.t.ptr.size(); ++c) {
+            const long k = w.n ? volume(w.t.ranges[comm.rank][c].size) / (w.n * w.n) : 0;
+            check_info(launch_gesv(v.dtype, w.t.ptr[c], w.n, k, w.t.ptr[c], w.n, true, Scalar{1, 0},
+                                   w.t.dev[c], w.rm, false));
+        }
+        if (!w.inplace)
+            dist_copy(Scalar{1, 0}, w.t, Coor(w.t.nd(), 0), w.t.dim, v, Coor(v.nd(), 0), false, comm);
+        return;
+    }
     if (w.inplace) {
         // the factors go to a copy; the inverse straight into the caller's tensor
         DistTensor lu = w.t;

@@ -35,6 +35,7 @@ template <> struct DOps<double> {
     static __device__ __forceinline__ double sub(double a, double b) { return a - b; }
     static __device__ __forceinline__ double div(double a, double b) { return a / b; }
     static __device__ __forceinline__ double divr(double a, double b) { return a / b; }
+    static __device__ __forceinline__ double inv(double b) { return 1.0 / b; }
     static __device__ __forceinline__ double real(double r) { return r; }
     static __device__ __forceinline__ double one() { return 1; }
 };
@@ -46,6 +47,7 @@ template <> struct DOps<float> {
     static __device__ __forceinline__ float sub(float a, float b) { return a - b; }
     static __device__ __forceinline__ float div(float a, float b) { return a / b; }
     static __device__ __forceinline__ float divr(float a, double b) { return a / (float)b; }
+    static __device__ __forceinline__ float inv(float b) { return 1.f / b; }
     static __device__ __forceinline__ float real(double r) { return (float)r; }
     static __device__ __forceinline__ float one() { return 1; }
 };
@@ -65,6 +67,15 @@ template <typename E, typename R> struct CplxOps {
         }
         const R r = b.x / b.y, d = b.y + b.x * r;
         return E{(a.x * r + a.y) / d, (a.y * r - a.x) / d};
+    }
+    /// 1 / b by Smith's algorithm: two real divisions, then a product per use instead of a
+    /// complex division per element (LAPACK's getf2 scales the column by the reciprocal pivot)
+    /// (branch-free: lanes of different matrices take either form without diverging)
+    static __device__ __forceinline__ E inv(E b) {
+        const bool xf = fabs((double)b.y) <= fabs((double)b.x);
+        const R u = xf ? b.x : b.y, w = xf ? b.y : b.x;
+        const R r = w / u, q = (R)1 / (u + w * r);
+        return xf ? E{q, -r * q} : E{r * q, -q};
     }
     static __device__ __forceinline__ E divr(E a, double b) { return E{(R)(a.x / b), (R)(a.y / b)}; }
     static __device__ __forceinline__ E real(double r) { return E{(R)r, 0}; }
@@ -338,9 +349,10 @@ __global__ void __launch_bounds__(256) potrf_wave_kernel(E *a, int n, long k, in
 template <typename E, int WNM>
 __global__ void __launch_bounds__(256) gesv_wave_kernel(E *a, int n, long k, E *b, long m, int identity,
                                                         double alpha_re, double alpha_im,
-                                                        int *info, int rm) {
+                                                        int *info, int rm, int keep_lu) {
     typedef DOps<E> O;
     __shared__ E lu_s[4][64 * WNM];
+    __shared__ E dinv_s[4][64];
     __shared__ int piv_s[4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, G = 64 / n;
     const int s = lane / n, c = lane - s * n, s0 = s * n;
@@ -383,11 +395,13 @@ __global__ void __launch_bounds__(256) gesv_wave_kernel(E *a, int n, long k, E *
                 if (r == p) v.set(r, v.get(j));
             v.set(j, vp);
         }
-        const E d = wshfl<E>(v.get(j), s0 + j);
+        // the multipliers: the column times the reciprocal pivot (kept for the solve's U^-1)
+        const E dinv = O::inv(wshfl<E>(v.get(j), s0 + j));
+        if (c == j && s < G) dinv_s[w][s0 + j] = dinv;
         if (ok && c == j)
 #pragma unroll
             for (int r = j + 1; r < WNM; ++r)
-                if (r < n) v.set(r, O::div(v.get(r), d));
+                if (r < n) v.set(r, O::mul(v.get(r), dinv));
         const E vj = v.get(j);
 #pragma unroll
         for (int r = j + 1; r < WNM; ++r) {
@@ -400,12 +414,13 @@ __global__ void __launch_bounds__(256) gesv_wave_kernel(E *a, int n, long k, E *
 #pragma unroll
         for (int r = 0; r < WNM; ++r)
             if (r < n) {
-                if (valid) g[rm ? c + (long)r * n : r + (long)c * n] = v.get(r);
+                if (valid && keep_lu) g[rm ? c + (long)r * n : r + (long)c * n] = v.get(r);
                 lu_s[w][s0 * n + r + c * n] = v.get(r);
             }
     if (valid && !bad && b) {
         // (the wave's LDS writes above are ordered before its reads below)
         const E *M = lu_s[w] + s0 * n;
+        const E *Dinv = dinv_s[w] + s0;
         const int *piv = piv_s[w] + s0;
         E *B = b + mi * n * m;
         for (long col = c; col < m; col += n) {
@@ -446,7 +461,7 @@ __global__ void __launch_bounds__(256) gesv_wave_kernel(E *a, int n, long k, E *
 #pragma unroll
                 for (int q = r + 1; q < WNM; ++q)
                     if (q < n) t = O::sub(t, O::mul(M[r + q * n], x.get(q)));
-                x.set(r, O::div(t, M[r + r * n]));
+                x.set(r, O::mul(t, Dinv[r]));
             }
             if (alpha_re != 1 || alpha_im != 0)
 #pragma unroll
@@ -457,6 +472,106 @@ __global__ void __launch_bounds__(256) gesv_wave_kernel(E *a, int n, long k, E *
         }
     }
     if (valid && c == 0) info[mi] = bad;
+}
+
+/// lane L's value of each 16-lane row (DPP row_newbcast: a VALU move, no LDS)
+template <int L> __device__ __forceinline__ int rbc_i(int v) {
+    return __builtin_amdgcn_mov_dpp(v, 0x150 + L, 0xf, 0xf, true);
+}
+template <int L> __device__ __forceinline__ float rbc(float v) {
+    return __builtin_bit_cast(float, rbc_i<L>(__builtin_bit_cast(int, v)));
+}
+template <int L> __device__ __forceinline__ double rbc(double v) {
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = rbc_i<L>((int)b), hi = rbc_i<L>((int)(b >> 32));
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+template <int L> __device__ __forceinline__ double2 rbc(double2 v) { return double2{rbc<L>(v.x), rbc<L>(v.y)}; }
+template <int L> __device__ __forceinline__ float2 rbc(float2 v) { return float2{rbc<L>(v.x), rbc<L>(v.y)}; }
+
+// In-place inversion of small matrices (n <= 16, B = A^-1, B may be A): Gauss-Jordan with
+// LAPACK's partial pivoting (largest |re| + |im| at or below the diagonal, first on ties; rows
+// swapped), one 16-lane row of the wave per matrix, lane c holding column c in registers.  A
+// step's pivot column reaches the other lanes by DPP row broadcasts (no LDS, no barrier); the
+// pivot column is replaced by the inverse's column as it is eliminated, and the row swaps are
+// undone on the columns at the end (one shuffle per element).  getrf + getri in one pass over
+// registers: n^3 complex multiply-adds per matrix, the matrix read and written once.
+template <typename E, int WNM, int J>
+__device__ __forceinline__ void gj_step(Col<E, WNM> &v, int n, int c, int &bad, int (&pj)[WNM]) {
+    typedef DOps<E> O;
+    if constexpr (J < WNM) {
+        if (J < n) {
+            double bv = -1;
+            int bi = J;
+#pragma unroll
+            for (int r = J; r < WNM; ++r)
+                if (r < n) {
+                    const double t = O::abs1(v.get(r));
+                    if (t > bv) {
+                        bv = t;
+                        bi = r;
+                    }
+                }
+            const int p = rbc_i<J>(bi);
+            const double pv = rbc<J>(bv);
+            const bool ok = !bad && pv > 0;
+            if (!bad && !(pv > 0)) bad = J + 1;
+            pj[J] = ok ? p : J;
+            if (ok && p != J) {
+                E vp = v.get(J);
+#pragma unroll
+                for (int r = J + 1; r < WNM; ++r)
+                    if (r == p) vp = v.get(r);
+#pragma unroll
+                for (int r = J + 1; r < WNM; ++r)
+                    if (r == p) v.set(r, v.get(J));
+                v.set(J, vp);
+            }
+            const E dinv = O::inv(rbc<J>(v.get(J)));
+            // the pivot row scaled; the pivot column (lane J) as the identity's column.  (A
+            // singular matrix -- !ok -- goes on with infinities: its lanes are its own and its
+            // result is not written.)
+            const E aj = O::mul(c == J ? O::one() : v.get(J), dinv);
+#pragma unroll
+            for (int r = 0; r < WNM; ++r) {
+                if (r >= n || r == J) continue;
+                const E mr = rbc<J>(v.get(r));
+                v.set(r, O::sub(c == J ? O::real(0) : v.get(r), O::mul(mr, aj)));
+            }
+            v.set(J, aj);
+        }
+        gj_step<E, WNM, J + 1>(v, n, c, bad, pj);
+    }
+}
+
+template <typename E, int WNM>
+__global__ void __launch_bounds__(256) inv_wave_kernel(const E *a, int n, long k, E *b, int *info, int rm) {
+    typedef DOps<E> O;
+    const int lane = threadIdx.x & 63, s = lane >> 4, c = lane & 15;
+    const long mi = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * 4 + s;
+    const bool live = mi < k, valid = live && c < n;
+    const E *g = a + (live ? mi : 0) * n * n;
+    // lanes past n and matrices past the batch: identity columns (well-defined pivots)
+    Col<E, WNM> v;
+#pragma unroll
+    for (int r = 0; r < WNM; ++r)
+        v.set(r, (r < n && valid) ? g[rm ? c + (long)r * n : r + (long)c * n] : (r == c ? O::one() : O::real(0)));
+    int bad = 0, pj[WNM];
+    gj_step<E, WNM, 0>(v, n, c, bad, pj);
+    // undo the row swaps on the columns (last swap first): column c of A^-1 is column src
+    int src = c;
+#pragma unroll
+    for (int l = 0; l < WNM; ++l)
+        if (l < n) src = src == l ? pj[l] : (src == pj[l] ? l : src);
+    const int from = (lane & 48) + src;
+    E *o = b + (live ? mi : 0) * n * n;
+#pragma unroll
+    for (int r = 0; r < WNM; ++r) {
+        if (r >= n) continue;
+        const E e = wshfl<E>(v.get(r), from);
+        if (valid && !bad) o[rm ? c + (long)r * n : r + (long)c * n] = e;
+    }
+    if (live && c == 0) info[mi] = bad;
 }
 
 // Triangular solves with small factors (n <= 16): a lane per right-hand side (left: a column of
@@ -474,6 +589,12 @@ __global__ void __launch_bounds__(256) trsm_wave_kernel(const E *a, int n, long 
     if (s >= per || mi >= k) return;
     const E *U = a + mi * n * n;
     E *X = x + mi * n * m;
+    // the reciprocals of U's diagonal: when the matrix has at least n lanes, lane q of the matrix
+    // computes 1 / U(q, q) and the others read it (one reciprocal per lane instead of n divisions)
+    const int mp = m <= 64 ? (int)m : 64, base = m <= 64 ? s * (int)m : 0, tl = lane - base;
+    const bool shared = mp >= n;
+    const E rinv = O::inv(U[(tl < n ? tl : 0) * (n + 1)]);
+    auto dinv = [&](int r) { return shared ? wshfl<E>(rinv, base + r) : O::inv(U[r + r * n]); };
     for (long t = m <= 64 ? lane - (long)s * m : lane; t < m; t += (m <= 64 ? m : 64)) {
         Col<E, WNM> v;
         const long base = left ? t * n : t, st = left ? 1 : m;
@@ -487,7 +608,7 @@ __global__ void __launch_bounds__(256) trsm_wave_kernel(const E *a, int n, long 
 #pragma unroll
                 for (int q = r + 1; q < WNM; ++q)
                     if (q < n) w = O::sub(w, O::mul(U[r + q * n], v.get(q)));
-                v.set(r, O::div(w, U[r + r * n]));
+                v.set(r, O::mul(w, dinv(r)));
             }
         } else {
 #pragma unroll
@@ -496,7 +617,7 @@ __global__ void __launch_bounds__(256) trsm_wave_kernel(const E *a, int n, long 
                 E w = scale_by<E>(v.get(c), alpha_re, alpha_im);
 #pragma unroll
                 for (int q = 0; q < c; ++q) w = O::sub(w, O::mul(v.get(q), U[q + c * n]));
-                v.set(c, O::div(w, U[c + c * n]));
+                v.set(c, O::mul(w, dinv(c)));
             }
         }
 #pragma unroll
@@ -529,12 +650,26 @@ template <typename E> void potrf_typed(void *a, long n, long k, int *info, bool 
 }
 template <typename E>
 void gesv_typed(void *a, long n, long k, void *b, long m, bool identity, const Scalar &alpha,
-                int *ipiv, int *info, bool rm, hipStream_t s) {
+                int *ipiv, int *info, bool rm, bool keep_lu, hipStream_t s) {
+    if (n <= WNMAX && g_dense_wave && identity && !keep_lu && alpha.re == 1 && alpha.im == 0) {
+        // the inverse only (the factors not kept): Gauss-Jordan, a 16-lane row per matrix
+        auto go = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3((unsigned)((k + 15) / 16)), dim3(256), 0, s, (const E *)a, (int)n, k,
+                               (E *)b, info, rm ? 1 : 0);
+        };
+        if (n <= 4) go(inv_wave_kernel<E, 4>);
+        else if (n <= 8) go(inv_wave_kernel<E, 8>);
+        else if (n <= 12) go(inv_wave_kernel<E, 12>);
+        else go(inv_wave_kernel<E, 16>);
+        SBX_HIP_CHECK(hipGetLastError());
+        return;
+    }
     if (n <= WNMAX && g_dense_wave) {
         auto go = [&](auto kern) {
             const long per = 4 * (64 / n);
             hipLaunchKernelGGL(kern, dim3((unsigned)((k + per - 1) / per)), dim3(256), 0, s, (E *)a, (int)n, k,
-                               (E *)b, m, identity ? 1 : 0, alpha.re, alpha.im, info, rm ? 1 : 0);
+                               (E *)b, m, identity ? 1 : 0, alpha.re, alpha.im, info, rm ? 1 : 0,
+                               keep_lu ? 1 : 0);
         };
         if (n <= 4) go(gesv_wave_kernel<E, 4>);
         else if (n <= 8) go(gesv_wave_kernel<E, 8>);
@@ -544,6 +679,7 @@ void gesv_typed(void *a, long n, long k, void *b, long m, bool identity, const S
         return;
     }
     if (rm) throw Error("dense: internal error (row-major matrices need the wave kernels)");
+    if (!keep_lu || a == b) throw Error("dense: internal error (in-place inversion needs the wave kernels)");
     const bool lds = fits_lds<E>(n);
     hipLaunchKernelGGL(gesv_kernel<E>, dim3((unsigned)k), dim3(DTH),
                        lds ? (size_t)(n * n * sizeof(E)) : 0, s, (E *)a, n, (E *)b, m,
@@ -612,7 +748,7 @@ int launch_potrf(int t, void *a, long n, long k, int device, bool rm) {
 }
 
 int launch_gesv(int t, void *a, long n, long k, void *b, long m, bool identity,
-                const Scalar &alpha, int device, bool rm) {
+                const Scalar &alpha, int device, bool rm, bool keep_lu) {
     if (n == 0 || k == 0) return 0;
     if (k >= (1L << 31)) throw Error("dense: too many matrices");
     set_device(device);
@@ -622,7 +758,7 @@ int launch_gesv(int t, void *a, long n, long k, void *b, long m, bool identity,
         KernelTimer timer("dense", s);
         dispatch(t, [&](auto z) {
             gesv_typed<decltype(z)>(a, n, k, b, m, identity, alpha, (int *)ipiv.ptr,
-                                    (int *)info.ptr, rm, s);
+                                    (int *)info.ptr, rm, keep_lu, s);
         });
     }
     return first_info((const int *)info.ptr, k, s);

@@ -350,8 +350,10 @@ void launch_bsr_kron(const BsrDesc &d, int device);
 bool dense_wave_rows(long n);
 int launch_potrf(int t, void *a, long n, long k, int device, bool rm = false);
 /// LU + solve: B (n x m per matrix) <- alpha A^-1 B (identity: B starts as I); A gets the LU
+/// (keep_lu = false: A is left as it was -- the wave kernels only, where B may be A itself: the
+/// in-place inversion)
 int launch_gesv(int t, void *a, long n, long k, void *b, long m, bool identity,
-                const Scalar &alpha, int device, bool rm = false);
+                const Scalar &alpha, int device, bool rm = false, bool keep_lu = true);
 /// left: X (n x m) <- alpha U^-1 X;  right: X (m x n) <- alpha X U^-1  (U upper, non-unit)
 void launch_trsm(int t, const void *a, long n, long k, void *x, long m, bool left,
                  const Scalar &alpha, int device);

@@ -12,7 +12,8 @@ reuse distance changes.  Not part of the product.
 
 Printed per case and rhs count: kernel time (library timers, median of 3 rounds of 20
 launches), the stencil's algorithmic bytes / time as a fraction of 8 TB/s, and the bytes the
-case must move beyond L2 at the least (values + y + indices + x once).  BLK=12 / DT=cf: the
+case must move beyond L2 at the least (values + y + indices + x once).  DIMS=16,16,16,64: the lattice (default L^4, L=16).  VARIANTS / REGS: bsr.variant /
+bsr.reg values to compare.  BLK=12 / DT=cf: the
 12x12-block (spin 4 x color 3) operator, complex<float>.  NTS=0,1,...: the bsr.nt settings to
 compare (the value stream's non-temporal load policy, per kernel bit); PDS=1,2,3: the 12x12
 kernel's block lookahead (bsr.blk_pd)."""
@@ -29,8 +30,8 @@ import superbblas_amd as sb  # noqa: E402
 
 
 def columns(kind, L):
-    V = L ** 4
-    sites = np.array(np.unravel_index(np.arange(V), (L,) * 4)).T
+    V = int(np.prod(L))
+    sites = np.array(np.unravel_index(np.arange(V), tuple(L))).T
     if kind == "one":
         jj = np.zeros((V, 1, 6), np.int32)
         jj[:, 0, :4] = sites
@@ -42,9 +43,9 @@ def columns(kind, L):
         for s in (-1, 1):
             c = sites.copy()
             if kind == "stencil":
-                c[:, d] = (c[:, d] + s) % L
+                c[:, d] = (c[:, d] + s) % L[d]
             elif kind == "local":
-                c[:, 3] = (c[:, 3] + s * (d + 1)) % L  # t +- 1..4: rows +- 1..4
+                c[:, 3] = (c[:, 3] + s * (d + 1)) % L[3]  # t +- 1..4: rows +- 1..4
             jj[:, k, :4] = c
             k += 1
     return jj, 9
@@ -52,19 +53,21 @@ def columns(kind, L):
 
 def main():
     dev = torch.device("cuda:0")
-    L = int(os.environ.get("L", "16"))
-    V = L ** 4
+    L = [int(v) for v in os.environ.get("DIMS", ",".join([os.environ.get("L", "16")] * 4)).split(",")]
+    V = int(np.prod(L))
     kinds = os.environ.get("KINDS", "stencil,local,self,one").split(",")
     ncols_list = [int(v) for v in os.environ.get("NCOLS", "12,64").split(",")]
     nts = [int(v) for v in os.environ.get("NTS", str(sb.tune_get("bsr.nt"))).split(",")]
     pds = [int(v) for v in os.environ.get("PDS", str(sb.tune_get("bsr.blk_pd"))).split(",")]
+    variants = [int(v) for v in os.environ.get("VARIANTS", str(sb.tune_get("bsr.variant"))).split(",")]
+    regs = [int(v) for v in os.environ.get("REGS", "-1").split(",")]
     # BLK=12: spin 4 x color 3 blocks (config 3's secondary shape / the chain's operator);
     # DT=cf: complex<float>
     spin = 4 if os.environ.get("BLK", "3") == "12" else 1
     dt = torch.complex64 if os.environ.get("DT", "cd") == "cf" else torch.complex128
     es = 8 if dt == torch.complex64 else 16
     b = 3 * spin
-    dim = [L, L, L, L, spin, 3]
+    dim = L + [spin, 3]
     full = [([0] * 6, dim)]
     blk = [1, 1, 1, 1, spin, 3]
     for kind in kinds:
@@ -73,10 +76,14 @@ def main():
         op = sb.create_bsr(full, dim, full, dim, blk, blk, False,
                            [torch.full((V,), nnz, dtype=torch.int32, device=dev)],
                            [torch.from_numpy(jj.reshape(-1)).to(dev)], [vals])
-        for n, nt, pd in [(n, nt, pd) for n in ncols_list for nt in nts for pd in pds]:
+        for n, nt, pd, var, reg in [(n, nt, pd, var, reg) for n in ncols_list for nt in nts
+                                    for pd in pds for var in variants for reg in regs]:
+            sb.tune_set("bsr.variant", var)
+            if reg >= 0:  # bsr.reg: the round-5 register-staged experiment (removed again)
+                sb.tune_set("bsr.reg", reg)
             sb.tune_set("bsr.nt", nt)
             sb.tune_set("bsr.blk_pd", pd)
-            dx = [1, L, L, L, L, spin, 3, n]
+            dx = [1] + L + [spin, 3, n]
             px = [([0] * 8, dx)]
             x = torch.randn(V * b * n, dtype=dt, device=dev)
             y = torch.empty_like(x)
@@ -100,7 +107,7 @@ def main():
             t = statistics.median(ts)
             algo = es * (9 * b * b * V + 2 * b * V * n) + 4.0 * (9 * V + V + 1)  # the stencil's
             floor = es * (nnz * b * b * V + 2 * b * V * n) + 4.0 * (nnz * V + V + 1)
-            print(json.dumps({"blk": b, "dtype": str(dt), "kind": kind, "ncols": n, "nt": nt, "blk_pd": pd,
+            print(json.dumps({"blk": b, "dtype": str(dt), "kind": kind, "ncols": n, "nt": nt, "blk_pd": pd, "variant": var, "reg": reg,
                               "us": round(t * 1e6, 1),
                               "kernel": sb.tune_get("bsr.last_kernel"),
                               "stencil_bytes_frac_hbm": round(algo / t / 8e12, 4),
