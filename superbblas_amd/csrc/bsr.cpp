@@ -33,6 +33,13 @@ struct BsrComp {
     const void *kron = nullptr; // Kronecker matrices (user memory, device)
     int nnz_per_row = -1;
     std::vector<int> h_rowptr, h_jj; // host copies of the pattern (for the transposed operator)
+    // site tiles of the 3x3 9-point kernel (bsr_ell9_tile_kernel): one device buffer holding
+    // rows [chunks][16], distinct block columns [chunks][umax], slots [chunks][16][9]
+    void *tile_buf = nullptr;
+    const int *tile_rows = nullptr, *tile_uniq = nullptr;
+    const unsigned char *tile_loc = nullptr;
+    int tile_umax = 0;
+    long tile_chunks = 0;
     void *owned_v = nullptr;         // values owned by the operator (transposed operator, or
                                      // the device copy of a host component's values)
     void *owned_kron = nullptr;      // device copy of a host component's Kronecker matrices
@@ -60,9 +67,95 @@ struct BsrOp {
             if (c.jj) (void)hipFree(c.jj);
             if (c.owned_v) (void)hipFree(c.owned_v);
             if (c.owned_kron) (void)hipFree(c.owned_kron);
+            if (c.tile_buf) (void)hipFree(c.tile_buf);
         }
     }
 };
+
+namespace {
+
+/// The site-tile schedule of a 3x3-block operator with 9 nonzero blocks per row (the 9-point
+/// stencils): the block rows are the component's image sites (SlowToFast over the image dims
+/// without the block dims), grouped into tiles of up to 16 sites -- 2 along each of the fastest
+/// dims, 2x2x2x2 on a 4-d lattice -- visited with the fastest tile coordinate fastest; per tile
+/// its rows, its distinct block columns and the slot of each nonzero block among them.  Any
+/// pattern is valid (a tile whose columns are scattered only stages more rows); no schedule when
+/// a tile has more than 116 distinct columns (the kernel's LDS budget).
+void build_tile_schedule(BsrComp &bc, const Coor &isize, const Coor &blocki) {
+    constexpr int TT = 16, NNZ = 9, UMAX_LIMIT = 116;
+    std::vector<long> dims;
+    for (std::size_t d = 0; d < isize.size(); ++d) {
+        const long r = blocki[d] > 0 ? isize[d] / blocki[d] : 1;
+        if (r > 1) dims.push_back(r);
+    }
+    long vol = 1;
+    for (long r : dims) vol *= r;
+    if (vol != bc.block_rows || bc.h_jj.size() != (std::size_t)bc.block_rows * NNZ) return;
+    const int nd = (int)dims.size();
+    std::vector<long> tsz(nd, 1), ntile(nd, 1), rstride(nd, 1);
+    long prod = 1;
+    for (int pass = 0; pass < 4 && prod < TT; ++pass)
+        for (int d = nd - 1; d >= 0 && prod < TT; --d)
+            if (tsz[d] * 2 <= dims[d]) tsz[d] *= 2, prod *= 2;
+    long nchunks = 1;
+    for (int d = nd - 1; d >= 0; --d) {
+        ntile[d] = (dims[d] + tsz[d] - 1) / tsz[d];
+        nchunks *= ntile[d];
+        if (d + 1 < nd) rstride[d] = rstride[d + 1] * dims[d + 1];
+    }
+    std::vector<int> rows((std::size_t)nchunks * TT, -1);
+    std::vector<std::vector<int>> uniq(nchunks);
+    std::vector<unsigned char> loc((std::size_t)nchunks * TT * NNZ, 255);
+    int umax = 0;
+    std::vector<long> tc(nd), lc(nd);
+    for (long ch = 0; ch < nchunks; ++ch) {
+        long rem = ch;
+        for (int d = nd - 1; d >= 0; --d) tc[d] = rem % ntile[d], rem /= ntile[d];
+        int nr = 0;
+        for (long e = 0; e < prod; ++e) {
+            long r2 = e, row = 0;
+            bool in = true;
+            for (int d = nd - 1; d >= 0; --d) {
+                lc[d] = r2 % tsz[d], r2 /= tsz[d];
+                const long cc = tc[d] * tsz[d] + lc[d];
+                in &= cc < dims[d];
+                row += cc * rstride[d];
+            }
+            if (in) rows[ch * TT + nr++] = (int)row;
+        }
+        std::vector<int> &u = uniq[ch];
+        for (int q = 0; q < nr; ++q) {
+            const long row = rows[ch * TT + q];
+            for (int k = 0; k < NNZ; ++k) {
+                const int j = bc.h_jj[row * NNZ + k];
+                if (j < 0) continue;
+                int at = (int)(std::find(u.begin(), u.end(), j) - u.begin());
+                if (at == (int)u.size()) u.push_back(j);
+                if (at >= UMAX_LIMIT) return;
+                loc[(ch * TT + q) * NNZ + k] = (unsigned char)at;
+            }
+        }
+        umax = std::max(umax, (int)u.size());
+    }
+    if (umax == 0) return;
+    std::vector<int> flat((std::size_t)nchunks * umax, -1);
+    for (long ch = 0; ch < nchunks; ++ch)
+        std::copy(uniq[ch].begin(), uniq[ch].end(), flat.begin() + ch * umax);
+    const std::size_t b_rows = rows.size() * sizeof(int), b_uniq = flat.size() * sizeof(int);
+    const std::size_t total = b_rows + b_uniq + loc.size();
+    SBX_HIP_CHECK(hipMalloc(&bc.tile_buf, total));
+    char *b = (char *)bc.tile_buf;
+    SBX_HIP_CHECK(hipMemcpy(b, rows.data(), b_rows, hipMemcpyHostToDevice));
+    SBX_HIP_CHECK(hipMemcpy(b + b_rows, flat.data(), b_uniq, hipMemcpyHostToDevice));
+    SBX_HIP_CHECK(hipMemcpy(b + b_rows + b_uniq, loc.data(), loc.size(), hipMemcpyHostToDevice));
+    bc.tile_rows = (const int *)b;
+    bc.tile_uniq = (const int *)(b + b_rows);
+    bc.tile_loc = (const unsigned char *)(b + b_rows + b_uniq);
+    bc.tile_umax = umax;
+    bc.tile_chunks = nchunks;
+}
+
+} // namespace
 
 BsrOp *bsr_create(int nd, int ni, int dtype, const std::vector<std::vector<Range>> &pi,
                   const Coor &dimi, const std::vector<std::vector<Range>> &pd, const Coor &dimd,
@@ -200,6 +293,8 @@ BsrOp *bsr_create(int nd, int ni, int dtype, const std::vector<std::vector<Range
         if (!op->is_kron) {
             bc.h_rowptr = std::move(rowptr);
             bc.h_jj = std::move(hjj);
+            if (bi == 3 && bd == 3 && bc.nnz_per_row == 9 && dtype == SBX_CDOUBLE)
+                build_tile_schedule(bc, ri.size, blocki);
         }
         op->comps.push_back(bc);
     }
@@ -647,6 +742,11 @@ void bsr_krylov(const BsrOp &op, const Scalar &alpha, const std::string &oi,
                 d.ncols = volC;
                 d.alpha = pw == 0 ? alpha : Scalar{1, 0};
                 d.add = plans[comm.rank][c].ydirect ? !beta.is_zero() : false;
+                d.tile_rows = bc.tile_rows;
+                d.tile_uniq = bc.tile_uniq;
+                d.tile_loc = bc.tile_loc;
+                d.tile_umax = bc.tile_umax;
+                d.tile_chunks = bc.tile_chunks;
                 if (op.is_kron) {
                     d.ki = (int)volume(op.kroni);
                     d.kd = (int)volume(op.krond);

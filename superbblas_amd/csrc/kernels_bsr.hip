@@ -42,6 +42,11 @@ struct BsrArgs {
     int add;
     int ilv = 1; // bsr_ell9_kernel: an XCD's chunks visited as ilv interleaved parts
     int nt = 0;  // the value stream's LDS-DMA loads non-temporal: g_bsr_tune.nt's kernel bits
+    // site tiles (bsr_ell9_tile_kernel; t_rows == nullptr: none)
+    const int *t_rows = nullptr, *t_uniq = nullptr;
+    const unsigned char *t_loc = nullptr;
+    int t_umax = 0;
+    long t_chunks = 0;
 };
 
 template <typename E, int BI_, int BD_, bool YROW, bool XROW>
@@ -815,6 +820,148 @@ __global__ void __launch_bounds__(NT) bsr_ell9_kernel(const BsrArgs p, int rb) {
     }
 }
 
+// Site tiles with their halo in LDS (3x3 complex<double> blocks, 9 per row, many rhs columns;
+// row-major x and y).  The rows are grouped into tiles of up to TT lattice sites (the host's
+// schedule, bsr.cpp: 2x2x2x2 on a 4-d lattice) and a tile's distinct x rows -- its own sites and
+// their halo, UMAX at most -- are staged once per slice of NS rhs columns into LDS by LDS-DMA
+// (each x row 3 colours x NS columns, 128-byte runs), so the nine neighbours of every row are
+// read from LDS instead of nine gathers through the vector-memory path (5 staged rows per site
+// instead of 9 fetched ones on the 9-point stencil).  The tile's values (TT x 9 blocks) are
+// staged once and reused by every slice.  Thread (site s, colour i, column e) of 16 x 3 x 8.
+constexpr int TILE_T = 16;
+
+struct TileArgs {
+    const int *rows;          // [chunk][TILE_T] block rows of the tile (-1: none)
+    const int *uniq;          // [chunk][umax] first domain row of each distinct block column (-1: none)
+    const unsigned char *loc; // [chunk][TILE_T][9] slot of each nonzero block in uniq (255: skip)
+    int umax;
+};
+
+__device__ __forceinline__ void dma16_lane(const void *src, unsigned m0, bool nt) {
+    if (nt)
+        asm volatile("s_mov_b32 m0, %1\n\t"
+                     "s_nop 0\n\t"
+                     "global_load_lds_dwordx4 %0, off nt"
+                     :
+                     : "v"(src), "s"(m0)
+                     : "memory", "m0");
+    else
+        asm volatile("s_mov_b32 m0, %1\n\t"
+                     "s_nop 0\n\t"
+                     "global_load_lds_dwordx4 %0, off"
+                     :
+                     : "v"(src), "s"(m0)
+                     : "memory", "m0");
+}
+
+// Thread (site s, colour i, rhs column e) of 16 x 3 x 8.  A slice's y stores are issued after
+// the next slice's DMA, so the wait for that DMA (vmcnt(1)) leaves them in flight.
+template <bool BIMF>
+__global__ void __launch_bounds__(TILE_T * 3 * 8) bsr_ell9_tile_kernel(const BsrArgs p, const TileArgs t, int nchunks) {
+    typedef double2 E;
+    constexpr int NS = 8, NNZ = 9, VP = TILE_T * NNZ * 9, NT = TILE_T * 3 * NS; // value pieces (16 B)
+    constexpr int MAXP = 8; // x DMA passes: umax * 3 * NS <= MAXP * NT (launcher: umax <= 128)
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    E *vals = (E *)smem;
+    E *xs = vals + VP;
+    const int tid = threadIdx.x, w = tid >> 6;
+    // XCD-contiguous ranges of tiles: neighbouring tiles share halo rows in that XCD's L2
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int chunk = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    if (chunk >= nchunks) return;
+    const int umax = t.umax, XP = umax * 3 * NS; // x pieces of a slice
+    const int *rows = t.rows + (long)chunk * TILE_T;
+    const int *uq = t.uniq + (long)chunk * umax;
+    const unsigned char *lc = t.loc + (long)chunk * TILE_T * NNZ;
+    const unsigned vbase = lds_u32(vals), xbase = lds_u32(xs);
+    // the values of the tile's rows (read once: nt)
+    const E *v = (const E *)p.v;
+    for (int u = 0; u * NT < VP; ++u) {
+        const int L = u * NT + tid;
+        if (L < VP) {
+            const int s = L / 81, r = rows[s];
+            dma16_lane(v + (long)(r < 0 ? 0 : r) * 81 + (L - s * 81),
+                       __builtin_amdgcn_readfirstlane(vbase + (unsigned)(u * NT + w * 64) * 16u), (p.nt & 2) != 0);
+        }
+    }
+    // this lane's x pieces (pass u: distinct row pu, colour pd, column pe), the same every slice
+    // (element offsets into x: 32 bits, the launcher checks x's size)
+    unsigned src[MAXP];
+    const E *x = (const E *)p.x;
+#pragma unroll
+    for (int u = 0; u < MAXP; ++u) {
+        const int L = u * NT + tid;
+        const int pu = L / (3 * NS), rem = L - pu * 3 * NS, pd = rem / NS, pe = rem - pd * NS;
+        const int d = (L < XP) ? uq[L < XP ? pu : 0] : -1; // (the index clamped: no load past the list)
+        src[u] = (unsigned)(((long)(d < 0 ? 0 : d) + pd) * p.ldx + pe);
+    }
+    auto stage = [&](int q) {
+#pragma unroll
+        for (int u = 0; u < MAXP; ++u) {
+            const int L = u * NT + tid;
+            if (u * NT < XP && L < XP)
+                dma16_lane(x + src[u] + q * NS, __builtin_amdgcn_readfirstlane(xbase + (unsigned)(u * NT + w * 64) * 16u), false);
+        }
+    };
+    // this thread's output and its nine slots
+    const int e = tid % NS, i = (tid / NS) % 3, s = tid / (3 * NS);
+    const int row = rows[s];
+    const bool wave_stores = __ballot(row >= 0) != 0;
+    int slot[NNZ];
+#pragma unroll
+    for (int k = 0; k < NNZ; ++k) slot[k] = lc[s * NNZ + k];
+    const E *vr = vals + s * NNZ * 9;
+    E *y = (E *)p.y;
+    const int nslices = (int)(p.ncols / NS);
+    stage(0);
+    for (int q = 0; q < nslices; ++q) {
+        // slice q landed (only the previous slice's y store, issued after it, may be pending; a
+        // wave whose rows are all padding stores nothing: it waits for everything)
+        if (q == 0 || !wave_stores) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+        __syncthreads();
+        E acc = Ops<E>::zero();
+#pragma unroll
+        for (int k = 0; k < NNZ; ++k) {
+            if (slot[k] == 255) continue;
+            const E *xr = xs + slot[k] * 3 * NS + e;
+            const E *vb = vr + k * 9;
+#pragma unroll
+            for (int d = 0; d < 3; ++d) acc = Ops<E>::fma(BIMF ? vb[i + d * 3] : vb[i * 3 + d], xr[d * NS], acc);
+        }
+        __syncthreads(); // every read of the buffer is done
+        if (q + 1 < nslices) stage(q + 1);
+        if (row >= 0) {
+            E *yp = y + ((long)row * 3 + i) * p.ldy + q * NS + e;
+            const E out = Ops<E>::scale(acc, p.alpha_re, p.alpha_im);
+            *yp = p.add ? Ops<E>::add(*yp, out) : out;
+        }
+    }
+}
+
+/// false: no tile schedule, not this shape, or bsr.tile off
+bool launch_ell9_tile(const BsrArgs &a, const TileArgs &t, long nchunks, bool yrow, bool xrow, hipStream_t s) {
+    constexpr int NS = 8;
+    if (!t.rows || !yrow || !xrow || g_bsr_tune.tile != 1 || a.ncols % NS != 0 || t.umax < 1 ||
+        t.umax > 128 || nchunks >= (1L << 31) || a.ldx < a.ncols || a.ldy < a.ncols ||
+        a.x_rows <= 0 || a.x_rows * a.ldx >= (1L << 32))
+        return false;
+    const long vp = TILE_T * 9L * 9, xp = t.umax * 3L * NS;
+    const size_t lds = (size_t)(vp + xp) * 16;
+    // the DMA passes write lanes L < vp (values) and L < xp (x) only
+    check_dma_lds("bsr_ell9_tile_kernel", lds, 1, vp + xp);
+    g_bsr_tune.last = 4;
+    KernelTimer timer("bsr", s);
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3((unsigned)nchunks), dim3(TILE_T * 3 * NS), lds, s, a, t, (int)nchunks);
+    };
+    if (a.block_im_fast) go(bsr_ell9_tile_kernel<true>);
+    else go(bsr_ell9_tile_kernel<false>);
+    SBX_HIP_CHECK(hipGetLastError());
+    return true;
+}
+
 template <typename E, int BI, int BD, int G, int PD, int NT = 256, bool DMAV = false, bool SC = false>
 void launch_ell9(const BsrArgs &a, bool yrow, bool xrow, hipStream_t s, long lds_bytes) {
     const long blk_bytes = 9L * BI * BD * (long)sizeof(E);
@@ -1193,6 +1340,11 @@ void launch_ell(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_t s) 
             a.ncols <= g_bsr_tune.split_max_cols && launch_ell9_split<E>(a, yrow, xrow, s))
             return;
     }
+    if constexpr (std::is_same<E, double2>::value && BI == 3 && BD == 3) {
+        if (nnz == 9 && g_bsr_tune.variant != 1 && g_bsr_tune.tile && a.ncols >= g_bsr_tune.tile_min_cols &&
+            launch_ell9_tile(a, TileArgs{a.t_rows, a.t_uniq, a.t_loc, a.t_umax}, a.t_chunks, yrow, xrow, s))
+            return;
+    }
     // (the row-chunk kernel takes at most 2 x 256 rhs columns per workgroup row)
     if (nnz == 9 && g_bsr_tune.variant != 1 && a.ncols <= 512) {
         const long lds = a.ncols >= 8 ? 12288 : 24576;
@@ -1313,6 +1465,11 @@ void launch_bsr(const BsrDesc &d, int device) {
     a.add = d.add ? 1 : 0;
     a.ilv = 2; // an XCD's row chunks visited as two interleaved halves (bsr_ell9_kernel)
     a.nt = g_bsr_tune.nt;
+    a.t_rows = d.tile_rows;
+    a.t_uniq = d.tile_uniq;
+    a.t_loc = d.tile_loc;
+    a.t_umax = d.tile_umax;
+    a.t_chunks = d.tile_chunks;
     switch (d.t) {
     case SBX_CDOUBLE: return launch_typed<double2>(a, d.num_nnz_per_row, d.y_row_major, d.x_row_major, s);
     case SBX_CFLOAT: return launch_typed<float2>(a, d.num_nnz_per_row, d.y_row_major, d.x_row_major, s);

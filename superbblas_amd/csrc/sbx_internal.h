@@ -269,6 +269,10 @@ struct BsrTune {
                                  ///< neighbours ahead (0 = off: per-lane loads one ahead; 1..3)
     int kron_ylds = 0;           ///< ... with x staged: y written through the same ring in whole pieces
     int blk_pd = 1; ///< 12x12 blocks by LDS-DMA: blocks in flight ahead of the one in use (1..3)
+    int tile = 0;   ///< 9-point 3x3 complex<double> operators, row-major x and y: site tiles with
+                    ///< their halo staged in LDS (bsr_ell9_tile_kernel) ... (opt-in: 16^4 n = 64
+                    ///< 180 vs 169 us for the row-chunk kernel)
+    long tile_min_cols = 33; ///< ... from this many rhs columns (a multiple of 8)
     int nt = 11; ///< the value stream's LDS-DMA loads with the non-temporal (streaming) policy, per
                 ///< kernel: 1 12x12 blocks by LDS-DMA, 2 3x3 row chunks, 4 3x3 split rows, 8 3x3 one
                 ///< thread per block.  Default 1 | 2 | 8 (tools/bsr_bound.py NTS, warm, interleaved:
@@ -276,6 +280,7 @@ struct BsrTune {
                 ///< 161 -> 158 us, n = 1 19.0 -> 18.2 us; the split-row kernel 34.4 -> 42.5 us: off)
     /// read-back ("bsr.last_kernel"; atomic: launches may come from several host threads): the form
     /// of the last launch -- 1 one thread per block (3x3), 2 split rows (3x3), 3 row chunks (3x3),
+    /// 4 site tiles (3x3),
     /// 5 Kronecker on MFMA, 6 the same with packed column slots, 7 12x12 blocks by LDS-DMA, 8 the
     /// same with packed slots, 10 12x12 fragment gathers (9 blocks per row), 11 12x12 generic rows,
     /// 0 another kernel
@@ -341,6 +346,11 @@ struct BsrDesc {
     // (block row, bi, ncols, ki), both row major; jj holds the domain site of each nonzero
     int ki = 1, kd = 1;
     const void *kron = nullptr; ///< num_nnz_per_row matrices of ki x kd
+    // site tiles of 3x3 9-point operators (bsr.cpp build_tile_schedule; tile_rows == nullptr: none)
+    const int *tile_rows = nullptr, *tile_uniq = nullptr;
+    const unsigned char *tile_loc = nullptr;
+    int tile_umax = 0;
+    long tile_chunks = 0;
 };
 void launch_bsr(const BsrDesc &d, int device);
 void launch_bsr_kron(const BsrDesc &d, int device);

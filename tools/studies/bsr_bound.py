@@ -12,8 +12,8 @@ reuse distance changes.  Not part of the product.
 
 Printed per case and rhs count: kernel time (library timers, median of 3 rounds of 20
 launches), the stencil's algorithmic bytes / time as a fraction of 8 TB/s, and the bytes the
-case must move beyond L2 at the least (values + y + indices + x once).  DIMS=16,16,16,64: the lattice (default L^4, L=16).  VARIANTS / REGS: bsr.variant /
-bsr.reg values to compare.  BLK=12 / DT=cf: the
+case must move beyond L2 at the least (values + y + indices + x once).  DIMS=16,16,16,64: the lattice (default L^4, L=16).  VARIANTS / REGS / TILES: bsr.variant /
+bsr.reg / bsr.tile values to compare.  BLK=12 / DT=cf: the
 12x12-block (spin 4 x color 3) operator, complex<float>.  NTS=0,1,...: the bsr.nt settings to
 compare (the value stream's non-temporal load policy, per kernel bit); PDS=1,2,3: the 12x12
 kernel's block lookahead (bsr.blk_pd)."""
@@ -61,6 +61,7 @@ def main():
     pds = [int(v) for v in os.environ.get("PDS", str(sb.tune_get("bsr.blk_pd"))).split(",")]
     variants = [int(v) for v in os.environ.get("VARIANTS", str(sb.tune_get("bsr.variant"))).split(",")]
     regs = [int(v) for v in os.environ.get("REGS", "-1").split(",")]
+    tiles = [int(v) for v in os.environ.get("TILES", str(sb.tune_get("bsr.tile"))).split(",")]
     # BLK=12: spin 4 x color 3 blocks (config 3's secondary shape / the chain's operator);
     # DT=cf: complex<float>
     spin = 4 if os.environ.get("BLK", "3") == "12" else 1
@@ -76,8 +77,10 @@ def main():
         op = sb.create_bsr(full, dim, full, dim, blk, blk, False,
                            [torch.full((V,), nnz, dtype=torch.int32, device=dev)],
                            [torch.from_numpy(jj.reshape(-1)).to(dev)], [vals])
-        for n, nt, pd, var, reg in [(n, nt, pd, var, reg) for n in ncols_list for nt in nts
-                                    for pd in pds for var in variants for reg in regs]:
+        for n, nt, pd, var, reg, tile in [(n, nt, pd, var, reg, tile) for n in ncols_list for nt in nts
+                                          for pd in pds for var in variants for reg in regs
+                                          for tile in tiles]:
+            sb.tune_set("bsr.tile", tile)
             sb.tune_set("bsr.variant", var)
             if reg >= 0:  # bsr.reg: the round-5 register-staged experiment (removed again)
                 sb.tune_set("bsr.reg", reg)
@@ -107,7 +110,7 @@ def main():
             t = statistics.median(ts)
             algo = es * (9 * b * b * V + 2 * b * V * n) + 4.0 * (9 * V + V + 1)  # the stencil's
             floor = es * (nnz * b * b * V + 2 * b * V * n) + 4.0 * (nnz * V + V + 1)
-            print(json.dumps({"blk": b, "dtype": str(dt), "kind": kind, "ncols": n, "nt": nt, "blk_pd": pd, "variant": var, "reg": reg,
+            print(json.dumps({"blk": b, "dtype": str(dt), "kind": kind, "ncols": n, "nt": nt, "blk_pd": pd, "variant": var, "reg": reg, "tile": tile,
                               "us": round(t * 1e6, 1),
                               "kernel": sb.tune_get("bsr.last_kernel"),
                               "stencil_bytes_frac_hbm": round(algo / t / 8e12, 4),
