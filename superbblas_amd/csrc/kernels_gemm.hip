@@ -25,6 +25,8 @@
 #include "sbx_internal.h"
 
 #include <algorithm>
+#include <map>
+#include <mutex>
 #include <cstdint>
 #include <type_traits>
 
@@ -924,45 +926,79 @@ __global__ void __launch_bounds__(KG * 64) gemm_wave_kernel(const GemmKArgs p, u
                     }
         }
     }
-    if (wave != 0) return;
+    const bool fuse = FUSE && p.splits > 1;
+    if (wave != 0 && !fuse) return;
+    if (wave == 0) {
 #pragma unroll
-    for (int i = 0; i < MT; ++i)
+        for (int i = 0; i < MT; ++i)
 #pragma unroll
-        for (int j = 0; j < MT; ++j)
+            for (int j = 0; j < MT; ++j)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const long gi = 16 * i + Mfma<R>::row(lane, r);
-                const long gj = 16 * j + frow;
-                if (gi >= p.m || gj >= p.n) continue;
-                const R vr = accR[i][j][r];
-                const R vi = CPLX ? accI[i][j][r] : R(0);
-                if (p.splits == 1) {
-                    R *cptr = (R *)((E *)p.c + bb * p.sc_b + c_off(p, gi, gj));
-                    epilogue_store<R>(cptr, vr, vi, p, CPLX);
-                } else {
-                    E *w = (E *)p.work + (((long)split * p.batch + bb) * p.n + gj) * p.m + gi;
-                    if constexpr (CPLX)
-                        *w = E{vr, vi};
-                    else
-                        *w = vr;
+                for (int r = 0; r < 4; ++r) {
+                    const long gi = 16 * i + Mfma<R>::row(lane, r);
+                    const long gj = 16 * j + frow;
+                    if (gi >= p.m || gj >= p.n) continue;
+                    const R vr = accR[i][j][r];
+                    const R vi = CPLX ? accI[i][j][r] : R(0);
+                    if (p.splits == 1) {
+                        R *cptr = (R *)((E *)p.c + bb * p.sc_b + c_off(p, gi, gj));
+                        epilogue_store<R>(cptr, vr, vi, p, CPLX);
+                    } else {
+                        E *w = (E *)p.work + (((long)split * p.batch + bb) * p.n + gj) * p.m + gi;
+                        E v;
+                        if constexpr (CPLX) v = E{vr, vi};
+                        else v = vr;
+                        if constexpr (FUSE) {
+                            // write-through (sc1) stores: the partial reaches memory without a
+                            // release fence (no L2 write-back)
+                            if constexpr (sizeof(E) == 8)
+                                __hip_atomic_store((unsigned long long *)w, __builtin_bit_cast(unsigned long long, v),
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            else if constexpr (sizeof(E) == 4)
+                                __hip_atomic_store((unsigned *)w, __builtin_bit_cast(unsigned, v),
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            else {
+                                const R re = vr, im = vi;
+                                __hip_atomic_store((unsigned long long *)w, __builtin_bit_cast(unsigned long long, re),
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                __hip_atomic_store((unsigned long long *)w + 1, __builtin_bit_cast(unsigned long long, im),
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            }
+                        } else {
+                            *w = v;
+                        }
+                    }
+                }
+    }
+    if constexpr (FUSE) {
+        if (!fuse) return;
+        // the partial published (wave 0's stores drained, then one agent-scope add on the batch
+        // entry's counter); the workgroup whose add comes last sums the entry's partials of all
+        // splits in split order -- the arithmetic of splitk_reduce_kernel, so the result does not
+        // depend on which workgroup finishes last -- writes C and resets the counter for the next
+        // launch on this stream
+        __shared__ int last_s;
+        if (wave == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) {
+                const unsigned old = __hip_atomic_fetch_add(counters + bb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                last_s = old == (unsigned)p.splits - 1;
+                if (old == (unsigned)p.splits - 1) {
+                    // one agent-scope acquire (this CU's L1 dropped) before the workgroup's loads
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 }
             }
-    if constexpr (FUSE) {
-        if (p.splits == 1) return;
-        // publish this split's partial, count it; the last split of the entry sums them all
-        __threadfence();
-        unsigned old = 0;
-        if (lane == 0) old = atomicAdd(counters + bb, 1u);
-        old = __shfl(old, 0);
-        if (old != (unsigned)p.splits - 1) return;
-        __threadfence();
-        const long mn = p.m * p.n;
-        for (long e = lane; e < mn; e += 64) {
+        }
+        __syncthreads();
+        if (!last_s) return;
+        const long mn = p.m * p.n, sstride = p.batch * mn;
+        const E *wb = (const E *)p.work + bb * mn;
+        for (long e = tid; e < mn; e += KG * 64) {
             const long gi = e % p.m, gj = e / p.m;
-            const E *w = (const E *)p.work + (long)bb * mn + e;
             R sr = 0, si = 0;
             for (int sp = 0; sp < p.splits; ++sp) {
-                const E v = w[(long)sp * p.batch * mn];
+                const E v = wb[(long)sp * sstride + e];
                 if constexpr (CPLX) {
                     sr += v.x;
                     si += v.y;
@@ -973,6 +1009,7 @@ __global__ void __launch_bounds__(KG * 64) gemm_wave_kernel(const GemmKArgs p, u
             R *cptr = (R *)((E *)p.c + bb * p.sc_b + c_off(p, gi, gj));
             epilogue_store<R>(cptr, sr, si, p, CPLX);
         }
+        if (tid == 0) __hip_atomic_store(counters + bb, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -1252,6 +1289,31 @@ void launch_dma_cfg(const GemmKArgs &p0, int device, hipStream_t stream, long sp
     launch_reduce<R, CPLX>(p, stream);
 }
 
+/// The fused split-K sums' per-batch-entry counters of a stream: zero when allocated and left zero
+/// by every launch (the last workgroup of an entry resets its counter), so no memset per call;
+/// one array per stream, so launches on different streams never share a counter
+unsigned *splitk_counters(hipStream_t stream, long n, int device) {
+    static std::mutex mu;
+    static std::map<hipStream_t, std::pair<unsigned *, long>> arrays;
+    std::lock_guard<std::mutex> lock(mu);
+    auto &a = arrays[stream];
+    if (a.second < n) {
+        // (a smaller array of this stream: its launches have completed in stream order before
+        // the new one is used; the old one is released after the stream drains)
+        if (a.first) {
+            SBX_HIP_CHECK(hipStreamSynchronize(stream));
+            SBX_HIP_CHECK(hipFree(a.first));
+        }
+        const long cap = std::max(n, 1024L);
+        void *ptr = nullptr;
+        SBX_HIP_CHECK(hipMalloc(&ptr, sizeof(unsigned) * cap));
+        SBX_HIP_CHECK(hipMemset(ptr, 0, sizeof(unsigned) * cap));
+        a = {(unsigned *)ptr, cap};
+    }
+    (void)device;
+    return a.first;
+}
+
 /// Launch the wave-private-slab kernel (tensor contracted with itself, one tile per batch entry)
 template <typename R, bool CPLX, bool AK, int BM, int BKK, int KG, int RING, bool FUSE = false>
 void launch_wave_cfg(const GemmKArgs &p0, int device, hipStream_t stream, long target_wgs) {
@@ -1262,17 +1324,12 @@ void launch_wave_cfg(const GemmKArgs &p0, int device, hipStream_t stream, long t
                                                                    target_wgs, work, device);
     if (p.tm != 1 || p.tn != 1 || p.m != p.n)
         throw Error("gemm: internal error, wave kernel for a launch with several tiles");
-    Scratch counters;
-    if (FUSE && p.splits > 1) {
-        counters = Scratch(sizeof(unsigned) * p.batch, device);
-        SBX_HIP_CHECK(hipMemsetAsync(counters.ptr, 0, sizeof(unsigned) * p.batch, stream));
-    }
+    unsigned *counters = FUSE && p.splits > 1 ? splitk_counters(stream, p.batch, device) : nullptr;
     KernelTimer total("gemm_total", stream);
     {
         KernelTimer timer("gemm", stream);
         hipLaunchKernelGGL((gemm_wave_kernel<R, CPLX, AK, BM, BKK, KG, RING, FUSE>),
-                           dim3((unsigned)nwg), dim3(KG * 64), 0, stream, p,
-                           (unsigned *)counters.ptr);
+                           dim3((unsigned)nwg), dim3(KG * 64), 0, stream, p, counters);
         SBX_HIP_CHECK(hipGetLastError());
     }
     if (!FUSE) launch_reduce<R, CPLX>(p, stream);
@@ -1372,6 +1429,9 @@ void launch_tiled(const GemmKArgs &p, int device, hipStream_t stream) {
                 if (sh && t48 == 13) return launch_wave_cfg<R, CPLX, AK, 48, 8, 4, 2>(p, device, stream, 1024);
                 if (sh && t48 == 14) return launch_wave_cfg<R, CPLX, AK, 48, 16, 4, 2>(p, device, stream, 768);
                 if (sh && t48 == 16) return launch_wave_cfg<R, CPLX, AK, 48, 8, 16, 2>(p, device, stream, 256);
+                // 17: the default form with the split-K sum fused (write-through partials, the
+                // last workgroup of a batch entry sums them)
+                if (sh && t48 == 17) return launch_wave_cfg<R, CPLX, AK, 48, 8, 8, 2, true>(p, device, stream, 512);
                 // eight waves per workgroup, 512 workgroups: half the split-K partials of the
                 // four-wave form to write and sum (their per-wave tiles summed through LDS first):
                 // 0.138-0.139 -> 0.136-0.137 ms warm, interleaved (profiles/r04_chain_gemm.txt)

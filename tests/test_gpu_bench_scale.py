@@ -98,3 +98,19 @@ def test_bench_real_startup_nccl_pg(gpu, n):
     assert line["world_size_seen_by_rccl"] == n and line["comm_transport"] == "rccl"
     errs = {k: v for k, v in line.items() if k.startswith("scale_check_rel_err")}
     assert len(errs) == 3 and line["scale_check_ok"] is True, line
+
+
+def test_bench_configs3_full_size(gpu):
+    """configs[3] at its full size -- the 32^4, n = 64 lattice contraction over the 2x2x2x1 grid
+    of 8 ranks (here sharing the test box's GPU through RCCL's socket transport) -- with the 4a,
+    4b-redistributed answers compared with the same global problem on one GPU (the chain at a
+    reduced lattice: its full size is test_gpu_chain.py's)"""
+    line = _bench_no_launcher(8, ["--steps", "1", "--warmup", "0", "--L", "32", "--ncols", "64",
+                                  "--chain-L", "4", "--chain-T", "8"], timeout=900)
+    assert line["n_gpus"] == 8 and line["world_size_seen_by_rccl"] == 8
+    assert line["config"]["parallelism"] == "xyzt grid 2x2x2x1"
+    errs = {k: v for k, v in line.items() if k.startswith("scale_check_rel_err")}
+    assert {"scale_check_rel_err_4a", "scale_check_rel_err_contraction_redistributed"} <= set(errs)
+    for k, v in errs.items():
+        assert v <= (1e-5 if k.endswith("_chain") else 1e-10), (k, v)
+    assert line["scale_check_ok"] is True

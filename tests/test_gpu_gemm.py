@@ -130,7 +130,7 @@ def test_gemm_same_operand(gpu, dtype, m, k):
 @pytest.mark.parametrize("dtype", [np.complex128, np.complex64, np.float64])
 @pytest.mark.parametrize("m,k,batch", [(48, 3072, 3), (40, 1000, 2), (48, 96, 5), (36, 24, 1)])
 @pytest.mark.parametrize("tb", ["T", "C"])
-@pytest.mark.parametrize("t48", [5, 13, 14, 16])
+@pytest.mark.parametrize("t48", [5, 13, 14, 16, 17])
 def test_gemm_same_operand_mmajor(gpu, dtype, m, k, batch, tb, t48):
     """A op(A) with one M-major buffer as both operands and one output tile per batch entry (the
     chain's y^H y shape): the wave-private slab-ring kernel (A-only slab images, no barrier in the
@@ -161,6 +161,42 @@ def test_gemm_same_operand_mmajor(gpu, dtype, m, k, batch, tb, t48):
                 a, m, k * m, 0.0, ref, m, m * m, batch)
     assert rel_err(outs[0], ref) < TOL[dtype]
     assert rel_err(outs[1], ref) < TOL[dtype]
+
+
+@pytest.mark.parametrize("dtype", [np.complex128, np.complex64, np.float64])
+@pytest.mark.parametrize("m,k,batch", [(48, 6144, 8), (40, 3000, 3), (48, 12288, 64)])
+def test_gemm_fused_splitk_sum(gpu, dtype, m, k, batch):
+    """gemm.t48 17: the wave-ring kernel with its split-K sum fused (write-through partials, the
+    last workgroup of a batch entry sums the splits in split order and resets its counter):
+    bit-identical to the two-kernel form (t48 5: the same partials, the same order), over
+    repeated calls (the per-stream counters return to zero) and with beta != 0 (C read back)"""
+    import torch
+    import superbblas_amd as sb
+    a = random_valued(k * m * batch, dtype, 11)
+    ta = torch.from_numpy(a).to(gpu)
+    c0 = random_valued(m * m * batch, dtype, 12)
+    cplx = np.dtype(dtype).kind == "c"
+    alpha, beta = (0.5 - 0.5j, 0.25 + 1j) if cplx else (0.5, 0.25)
+    old = sb.tune_get("gemm.t48")
+    outs = {}
+    try:
+        for t48 in (5, 17, 17, 17):
+            sb.tune_set("gemm.t48", t48)
+            c = torch.from_numpy(c0.copy()).to(gpu)
+            sb.xgemm_batch_strided("N", "C" if cplx else "T", m, m, k, alpha, ta, m, k * m, ta, m,
+                                   k * m, beta, c, m, m * m, batch)
+            torch.cuda.synchronize()
+            outs.setdefault(t48, []).append(c.cpu().numpy())
+    finally:
+        sb.tune_set("gemm.t48", old)
+    for o in outs[17]:
+        assert np.array_equal(o, outs[5][0])
+    if batch > 8:  # (the chain's own shape: bit identity with the two-kernel form is the check)
+        return
+    ref = c0 * beta
+    oracle_gemm("N", "C" if cplx else "T", m, m, k, alpha, a, m, k * m, a, m, k * m, 1.0, ref, m,
+                m * m, batch)
+    assert rel_err(outs[17][0], ref) < TOL[dtype]
 
 
 # the skinny forms (blas.h:686-800's dot / gemv shortcuts; tests/dist.cpp:160-195's inner-product
