@@ -1229,7 +1229,9 @@ def dense_bench(sb, dev, L=16, n=12, reps=5):
                     "dense_%s_12x12_kernel_GBps" % op: round(by / kern / 1e9, 1),
                     "dense_%s_12x12_call_us" % op: round(call * 1e6, 1)})
     if sb.tune_get("dense.wave"):
-        out["dense_kernel"] = "potrf_wave_kernel / gesv_wave_kernel (64 / n matrices per wave)"
+        out["dense_kernel"] = ("inversion: inv_wave_kernel (Gauss-Jordan in registers, a 16-lane row per "
+                               "matrix, DPP row broadcasts, in place); Cholesky: potrf_wave_kernel "
+                               "(64 / n matrices per wave)")
     out["dense_workload"] = "16^4 matrices of 12x12 complex<double> (one per site), tij, rows i"
     return out
 
