@@ -213,22 +213,6 @@ struct TiledArgs {
     Alpha alpha;
 };
 
-/// Offsets of item `idx` of a chain of dims (fastest first)
-__device__ __forceinline__ void chain_offsets(uint32_t idx, int n, const FastDiv *size,
-                                              const long *sst, const long *dst, long &so,
-                                              long &doff) {
-    so = 0;
-    doff = 0;
-    for (int i = 0; i < n; ++i) {
-        const uint32_t q = size[i].div(idx);
-        const uint32_t c = idx - q * size[i].d;
-        idx = q;
-        so += (long)c * sst[i];
-        doff += (long)c * dst[i];
-    }
-}
-
-
 /// Offsets of item `idx` of a chain of dims (fastest first), unrolled for short chains
 __device__ __forceinline__ void chain_offsets4(uint32_t idx, int n, const FastDiv *size,
                                                const long *sst, const long *dst, long &so,
