@@ -415,6 +415,7 @@ int sbx_tune_set(const char *key, long long value) {
         else if (k == "gemm.max_bytes") g_gemm_tune.max_bytes = (long)value;
         else if (k == "gemm.loaders") g_gemm_tune.loaders = (int)value;
         else if (k == "gemm.dma_spread") g_gemm_tune.dma_spread = (int)value;
+        else if (k == "gemm.dma_nt") g_gemm_tune.dma_nt = (int)value;
         else if (k == "gemm.skinny") g_gemm_tune.skinny = (int)value;
         else if (k == "bsr.variant") g_bsr_tune.variant = (int)value;
         else if (k == "bsr.row_max_cols") g_bsr_tune.row_max_cols = (long)value;
@@ -468,6 +469,7 @@ int sbx_tune_get(const char *key, long long *value) {
         else if (k == "gemm.max_bytes") *value = g_gemm_tune.max_bytes;
         else if (k == "gemm.loaders") *value = g_gemm_tune.loaders;
         else if (k == "gemm.dma_spread") *value = g_gemm_tune.dma_spread;
+        else if (k == "gemm.dma_nt") *value = g_gemm_tune.dma_nt;
         else if (k == "gemm.skinny") *value = g_gemm_tune.skinny;
         else if (k == "bsr.variant") *value = g_bsr_tune.variant;
         else if (k == "bsr.row_max_cols") *value = g_bsr_tune.row_max_cols;

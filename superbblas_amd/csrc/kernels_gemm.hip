@@ -112,6 +112,7 @@ struct GemmKArgs {
     // itself or its conjugate, e.g. the chain's correlator y^H y): a workgroup on a diagonal tile
     // (m0 == n0) stages one slab image and reads both operands' fragments from it
     int same_ab;
+    int dma_nt; // the loader waves' slab DMA with the non-temporal policy (gemm.dma_nt)
 };
 
 /// Offset of index i of a split group: (i / lo) * s_hi + (i % lo) * s (i < 2^31)
@@ -429,7 +430,7 @@ template <int R, int BKK, int LWT, int ES> struct DmaRowsK {
     // issue granules i in [ib, ie) of slab [k0, k0+BKK) into the image at `lds_base`
     __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, const char *lds_base,
                                           int wave, long k0, long k_end, long s_k, int ib,
-                                          int ie) const {
+                                          int ie, bool nt = false) const {
         const unsigned kpart = (unsigned)(k0 * s_k * ES);
         const bool kok = k0 + k < k_end;
 #pragma unroll
@@ -438,12 +439,20 @@ template <int R, int BKK, int LWT, int ES> struct DmaRowsK {
             const bool ok = kok && RSTEP * i < rleft;
             const unsigned off = ok ? off0 + (unsigned)i * step + kpart : 0x80000000u;
             const unsigned dst = lds_addr(lds_base) + (unsigned)(i * LWT + wave * 64) * 16;
-            asm volatile("s_mov_b32 m0, %1\n\t"
-                         "s_nop 0\n\t"
-                         "buffer_load_dwordx4 %0, %2, 0 offen lds"
-                         :
-                         : "v"(off), "s"(dst), "s"(rs)
-                         : "memory", "m0");
+            if (nt)
+                asm volatile("s_mov_b32 m0, %1\n\t"
+                             "s_nop 0\n\t"
+                             "buffer_load_dwordx4 %0, %2, 0 offen nt lds"
+                             :
+                             : "v"(off), "s"(dst), "s"(rs)
+                             : "memory", "m0");
+            else
+                asm volatile("s_mov_b32 m0, %1\n\t"
+                             "s_nop 0\n\t"
+                             "buffer_load_dwordx4 %0, %2, 0 offen lds"
+                             :
+                             : "v"(off), "s"(dst), "s"(rs)
+                             : "memory", "m0");
         }
     }
 };
@@ -451,7 +460,7 @@ template <int R, int BKK, int LWT, int ES> struct DmaRowsK {
 struct NoLoader { // (LW == 0: every wave issues its share through DmaOperand)
     static constexpr int NI = 0;
     __device__ void init(int, long, long, long, long) {}
-    __device__ void issue(__amdgpu_buffer_rsrc_t, const char *, int, long, long, long, int, int) const {}
+    __device__ void issue(__amdgpu_buffer_rsrc_t, const char *, int, long, long, long, int, int, bool = false) const {}
 };
 
 // M3: complex products in the 3-multiplication (Gauss) form, P1 = ar*br, P2 = ai*bi,
@@ -563,13 +572,25 @@ __global__ void __launch_bounds__(WM *WN *KG * 64) gemm_dma_kernel(const GemmKAr
             if (!share)
                 db.issue(rsB, base + BM * BKK * ES, wave, k_begin, k_end, p.sb_k, spl, p.k_lo, p.sb_k_hi);
         } else if (loader) {
-            la.issue(rsA, base, wave, k_begin, k_end, p.sa_k, 0, LdA::NI);
-            if (!share) lb.issue(rsB, base + BM * BKK * ES, wave, k_begin, k_end, p.sb_k, 0, LdB::NI);
+            la.issue(rsA, base, wave, k_begin, k_end, p.sa_k, 0, LdA::NI, p.dma_nt);
+            if (!share) lb.issue(rsB, base + BM * BKK * ES, wave, k_begin, k_end, p.sb_k, 0, LdB::NI, p.dma_nt);
         }
     }
     for (long s = 0; s < nslab; ++s) {
+#ifdef SBX_SLAB_PROBE
+        // (tools only: workgroup 0 stamps, per wave and slab, the clock before the DMA wait and
+        // after the barrier: probe[4096 + (wave * nslab + s) * 2 + 0 / 1])
+        const unsigned long long sp0 = __builtin_amdgcn_s_memtime();
+#endif
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // this wave's DMA of slab s landed
         __syncthreads(); // ... and every wave's; the other buffer is free again
+#ifdef SBX_SLAB_PROBE
+        if (p.probe && bid == 0 && lane == 0) {
+            const unsigned long long sp1 = __builtin_amdgcn_s_memtime();
+            p.probe[4096 + (wave * nslab + s) * 2] = sp0;
+            p.probe[4096 + (wave * nslab + s) * 2 + 1] = sp1;
+        }
+#endif
         const int cur = (int)(s & 1);
         const char *nb = base + (size_t)(cur ^ 1) * SLAB * ES;
         const long kn = k_begin + (s + 1) * BKK;
@@ -584,10 +605,10 @@ __global__ void __launch_bounds__(WM *WN *KG * 64) gemm_dma_kernel(const GemmKAr
             if constexpr (LW > 0) {
                 if (loader && s + 1 < nslab && q < SP) {
                     la.issue(rsA, nb, wave, kn, k_end, p.sa_k, q * LdA::NI / SP,
-                             (q + 1) * LdA::NI / SP);
+                             (q + 1) * LdA::NI / SP, p.dma_nt);
                     if (!share)
                         lb.issue(rsB, nb + BM * BKK * ES, wave, kn, k_end, p.sb_k,
-                                 q * LdB::NI / SP, (q + 1) * LdB::NI / SP);
+                                 q * LdB::NI / SP, (q + 1) * LdB::NI / SP, p.dma_nt);
                 }
             }
         };
@@ -1264,6 +1285,7 @@ void launch_dma_cfg(const GemmKArgs &p0, int device, hipStream_t stream, long sp
     GemmKArgs p = p0;
     Scratch work;
     if (g_gemm_tune.splits > 0) splits = g_gemm_tune.splits;
+    p.dma_nt = g_gemm_tune.dma_nt;
     p.same_ab = g_gemm_tune.share_ab && p.a == p.b && p.m == p.n && p.sa_m == p.sb_n &&
                 p.sa_k == p.sb_k && p.sa_b == p.sb_b && p.m_lo == p.n_lo &&
                 p.sa_m_hi == p.sb_n_hi && p.sa_k_hi == p.sb_k_hi;

@@ -247,6 +247,7 @@ struct GemmTune {
                      ///< (4, 8, 16) issue the slab DMA (0 = every wave its share); config 2: 1.491 ->
                      ///< 1.475 ms at 4 or 8 (tools/studies/gemm_loaders.py, profiles/r05_gemm_loaders.txt)
     int dma_spread = 1; ///< ... the loader waves spread their DMA over this many k-steps (1 or 4)
+    int dma_nt = 0;     ///< ... with the non-temporal policy (0 = the default policy)
     int skinny = 1; ///< outputs with a dimension of <= 4 (and <= 16 with a short k): the dot / rows
                     ///< kernels instead of MFMA tiles (0 = off)
 };

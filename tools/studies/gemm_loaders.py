@@ -12,7 +12,8 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import superbblas_amd as sb  # noqa: E402
 
-VARIANTS = [(0, 1), (4, 1), (4, 4), (8, 1), (8, 4), (16, 4)]
+VARIANTS = [tuple(int(x) for x in v.split(":")) for v in
+            os.environ.get("VARIANTS", "0:1,4:1,4:4,8:1,8:4,16:4").split(",")]  # loaders:spread[:nt]
 
 
 def main():
@@ -40,9 +41,11 @@ def main():
         step()
     torch.cuda.synchronize()
     for rnd in range(int(os.environ.get("ROUNDS", "4"))):
-        for lw, sp in VARIANTS:
+        for var in VARIANTS:
+            lw, sp = var[0], var[1]
             sb.tune_set("gemm.loaders", lw)
             sb.tune_set("gemm.dma_spread", sp)
+            sb.tune_set("gemm.dma_nt", var[2] if len(var) > 2 else 0)
             step()
             torch.cuda.synchronize()
             sb.timings_enable(True)
@@ -53,17 +56,19 @@ def main():
             torch.cuda.synchronize()
             ms, calls = sb.timings_get("gemm")
             sb.timings_enable(False)
-            times[(lw, sp)].append(ms / calls)
+            times[var].append(ms / calls)
             if ref is None:
                 ref = vr.clone()
             elif not torch.equal(ref, vr):
                 print(json.dumps({"error": "results differ", "lw": lw, "sp": sp,
                                   "maxdiff": float((ref - vr).abs().max())}), flush=True)
-    sb.tune_set("gemm.loaders", 0)
+    sb.tune_set("gemm.loaders", 8)
     sb.tune_set("gemm.dma_spread", 1)
-    for (lw, sp), t in times.items():
+    sb.tune_set("gemm.dma_nt", 0)
+    for var, t in times.items():
         t = sorted(t)
-        print(json.dumps({"loaders": lw, "spread": sp, "gemm_ms_min": round(t[0], 4),
+        print(json.dumps({"loaders": var[0], "spread": var[1], "nt": var[2] if len(var) > 2 else 0,
+                          "gemm_ms_min": round(t[0], 4),
                           "gemm_ms_median": round(t[len(t) // 2], 4),
                           "TFLOPs_median": round(flops / t[len(t) // 2] / 1e9, 2)}), flush=True)
 

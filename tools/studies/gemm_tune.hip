@@ -166,6 +166,49 @@ int main(int argc, char **argv) {
         }
         return 0;
     }
+#ifdef SBX_SLAB_PROBE
+    if (getenv("PROBE") && std::string(getenv("PROBE")) == "slab") {
+        // workgroup 0, per wave and slab: shader clocks spent waiting (own DMA + the barrier)
+        // and between barriers (fragment reads + MFMA issue), the default 8-loader form
+        const long nslab = 192;
+        unsigned long long *probe;
+        const size_t words = 4096 + 16 * nslab * 2;
+        (void)hipMalloc(&probe, 8 * words);
+        GemmKArgs q = p;
+        q.probe = probe;
+        g_gemm_tune.loaders = 8;
+        for (int r = 0; r < 12; ++r) {
+            launch_dma_cfg<double, true, true, true, 128, 128, 16, 4, 4, false, false, 1, false, 8, 1>(q, 0, get_stream(0), 0, 256);
+            (void)hipStreamSynchronize(get_stream(0));
+            if (r < 9) continue;
+            std::vector<unsigned long long> h(words);
+            (void)hipMemcpy(h.data(), probe, 8 * words, hipMemcpyDeviceToHost);
+            std::printf("rep %d: wg0 %.1f us at %.3f GHz\n", r, h[1] / 100.0, (double)h[0] / (h[1] / 100e6) / 1e9);
+            double tw = 0, tc = 0;
+            std::vector<double> waitv, compv;
+            for (int w = 0; w < 16; ++w) {
+                double sw = 0, sc = 0;
+                for (long sl = 0; sl < nslab; ++sl) {
+                    const unsigned long long *e = &h[4096 + (w * nslab + sl) * 2];
+                    sw += (double)(e[1] - e[0]);
+                    if (sl + 1 < nslab) sc += (double)(e[2] - e[1]);
+                    waitv.push_back((double)(e[1] - e[0]));
+                    if (sl + 1 < nslab) compv.push_back((double)(e[2] - e[1]));
+                }
+                tw += sw;
+                tc += sc;
+                std::printf("  wave %2d: wait+barrier %7.0f clk/slab, between barriers %7.0f clk/slab\n", w,
+                            sw / nslab, sc / (nslab - 1));
+            }
+            auto pct = [](std::vector<double> v, double f) { std::sort(v.begin(), v.end()); return v[(size_t)(f * (v.size() - 1))]; };
+            std::printf("  all waves: wait+barrier mean %.0f (p10 %.0f med %.0f p90 %.0f max %.0f), between %.0f (p10 %.0f med %.0f p90 %.0f) clk/slab;"
+                        " 256 MFMAs per SIMD per slab = %d clk\n",
+                        tw / (16 * nslab), pct(waitv, 0.1), pct(waitv, 0.5), pct(waitv, 0.9), pct(waitv, 1.0),
+                        tc / (16 * (nslab - 1)), pct(compv, 0.1), pct(compv, 0.5), pct(compv, 0.9), 256 * 64);
+        }
+        return 0;
+    }
+#endif
     if (getenv("PROBE")) {
         // shader clock of workgroup 0 during the default 4M GEMM (s_memtime / s_memrealtime)
         unsigned long long *probe;
