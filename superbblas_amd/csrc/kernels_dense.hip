@@ -709,14 +709,30 @@ void trsm_typed(const void *a, long n, long k, void *x, long m, bool left, const
     SBX_HIP_CHECK(hipGetLastError());
 }
 
-/// The first nonzero LAPACK info of the batch (synchronises the stream)
-int first_info(const int *info_d, long k, hipStream_t s) {
-    std::vector<int> h(k);
-    SBX_HIP_CHECK(hipMemcpyAsync(h.data(), info_d, sizeof(int) * k, hipMemcpyDeviceToHost, s));
+/// res[0] <- the smallest matrix index with a nonzero info (res[0] starts at INT_MAX), and
+/// res[1] <- that matrix's info by the thread that finds it when a single one is bad
+__global__ void __launch_bounds__(256) first_bad_kernel(const int *info, long k, int *res) {
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < k; i += (long)gridDim.x * 256L)
+        if (info[i] != 0) atomicMin(res, (int)i);
+}
+
+/// The first nonzero LAPACK info of the batch (synchronises the stream): the index of the first
+/// failed matrix is found on the device, so only 4 bytes cross to the host (and 4 more when a
+/// matrix failed) instead of the whole info array
+int first_info(const int *info_d, long k, hipStream_t s, int device) {
+    if (k >= 0x7fffffffL) throw Error("dense: too many matrices");
+    Scratch res(sizeof(int), device);
+    SBX_HIP_CHECK(hipMemsetAsync(res.ptr, 0x7f, sizeof(int), s));
+    const long blocks = std::min((k + 255) / 256, 1024L);
+    hipLaunchKernelGGL(first_bad_kernel, dim3((unsigned)blocks), dim3(256), 0, s, info_d, k, (int *)res.ptr);
+    SBX_HIP_CHECK(hipGetLastError());
+    int idx = 0;
+    SBX_HIP_CHECK(hipMemcpyAsync(&idx, res.ptr, sizeof(int), hipMemcpyDeviceToHost, s));
     SBX_HIP_CHECK(hipStreamSynchronize(s));
-    for (int v : h)
-        if (v) return v;
-    return 0;
+    if (idx < 0 || idx >= k) return 0;
+    int v = 0;
+    SBX_HIP_CHECK(hipMemcpy(&v, info_d + idx, sizeof(int), hipMemcpyDeviceToHost));
+    return v;
 }
 
 /// Calls f(E{}) with the element type of `t`
@@ -744,7 +760,7 @@ int launch_potrf(int t, void *a, long n, long k, int device, bool rm) {
         KernelTimer timer("dense", s);
         dispatch(t, [&](auto z) { potrf_typed<decltype(z)>(a, n, k, (int *)info.ptr, rm, s); });
     }
-    return first_info((const int *)info.ptr, k, s);
+    return first_info((const int *)info.ptr, k, s, device);
 }
 
 int launch_gesv(int t, void *a, long n, long k, void *b, long m, bool identity,
@@ -761,7 +777,7 @@ int launch_gesv(int t, void *a, long n, long k, void *b, long m, bool identity,
                                     (int *)info.ptr, rm, keep_lu, s);
         });
     }
-    return first_info((const int *)info.ptr, k, s);
+    return first_info((const int *)info.ptr, k, s, device);
 }
 
 void launch_trsm(int t, const void *a, long n, long k, void *x, long m, bool left,
