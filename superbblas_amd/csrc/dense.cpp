@@ -231,6 +231,56 @@ void dense_solve(bool gesm, const Scalar &alpha, const DistTensor &c, const std:
         if (!has(rows ? y.labels : x.labels, l))
             throw Error(std::string(what) + ": missing labels to contract");
 
+    // Straight from x into y (trsm with small factors): x and y hold whole blocks of n x m
+    // elements per batch entry in one of the two orientations (the batch labels first, in C's
+    // order, then the contracted labels and the right-hand-side labels either way round), with
+    // the same batch ranges as C on every rank -- no working copies of x and y, and C in the
+    // caller's row-major order when it is whole (every rank decides alike from the global ranges)
+    if (!gesm) {
+        std::string ot, on;
+        for (char l : c.labels)
+            if (!has(orows, l) && !has(ocols, l)) ot += l;
+        for (char l : x.labels)
+            if (!has(c.labels, l)) on += l;
+        const std::string &lx = rows ? orows : ocols, &ly = rows ? ocols : orows;
+        long n = 1, m = 1;
+        for (char l : orows) n *= c.dim[c.labels.find(l)];
+        for (char l : on) m *= x.dim[x.labels.find(l)];
+        // 1: (batch, contracted, rhs): component i of rhs t at i * m + t; 2: (batch, rhs,
+        // contracted): at t * n + i; 0: neither, or the ranges do not match C's batch ranges
+        auto orient = [&](const DistTensor &v, const std::string &l) {
+            int o = v.labels == ot + l + on ? 1 : v.labels == ot + on + l ? 2 : 0;
+            if (!o || !v.mask.empty()) return 0;
+            for (std::size_t r = 0; r < v.ranges.size(); ++r)
+                for (std::size_t j = 0; j < v.ranges[r].size(); ++j) {
+                    const Range &q = v.ranges[r][j], &qc = c.ranges[r][j];
+                    if (volume(q.size) == 0 && volume(qc.size) == 0) continue;
+                    for (std::size_t d = 0; d < v.labels.size(); ++d) {
+                        const char lab = v.labels[d];
+                        const auto ic = c.labels.find(lab);
+                        if (has(ot, lab)) {
+                            if (q.from[d] != qc.from[ic] || q.size[d] != qc.size[ic]) return 0;
+                        } else if (q.from[d] != 0 || q.size[d] != v.dim[d]) {
+                            return 0;
+                        }
+                    }
+                }
+            return o;
+        };
+        const int ox = orient(x, lx), oy = orient(y, ly);
+        if (ox && oy && x.dtype == c.dtype && y.dtype == c.dtype && dense_wave_rows(n) &&
+            trsm_io_fits(n, m)) {
+            Work wc = prepare(c, orows, ocols, comm, true, what, true);
+            for (std::size_t j = 0; j < wc.t.ptr.size(); ++j) {
+                const long k = n ? volume(wc.t.ranges[comm.rank][j].size) / (n * n) : 0;
+                if (k == 0) continue;
+                launch_trsm_io(c.dtype, wc.t.ptr[j], n, k, wc.rm, x.ptr[j], ox == 1 ? (int)m : 1,
+                               ox == 1 ? 1 : (int)n, y.ptr[j], oy == 1 ? (int)m : 1, oy == 1 ? 1 : (int)n,
+                               m, !rows, alpha, x.dev[j]);
+            }
+            return;
+        }
+    }
     Work wc = prepare(c, orows, ocols, comm, true, what);
     const long n = wc.n;
     std::string on;

@@ -626,6 +626,86 @@ __global__ void __launch_bounds__(256) trsm_wave_kernel(const E *a, int n, long 
     }
 }
 
+// Triangular solves straight between the caller's tensors (n <= 16, m <= 64 right-hand sides
+// per matrix): a wave's 64 / m matrices have their right-hand sides x and their solutions y as
+// contiguous blocks of n x m elements; the wave moves its x blocks into LDS with coalesced
+// 16-byte loads, each lane reads its vector there (component i, right-hand side t at
+// i * xsi + t * xst of its block: either orientation), solves it exactly as trsm_wave_kernel does,
+// writes the result back into the slice in y's orientation and the wave stores the blocks with
+// coalesced stores.  The factor is read row- or column-major (rm).
+template <typename E, int WNM>
+__global__ void __launch_bounds__(256) trsm_io_kernel(const E *a, int n, long k, int rm, const E *x, int xsi,
+                                                      int xst, E *y, int ysi, int yst, int m, int left,
+                                                      double alpha_re, double alpha_im) {
+    typedef DOps<E> O;
+    __shared__ E io_s[4][64 * WNM];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int per = 64 / m, s = lane / m, t = lane - s * m;
+    const long mi0 = ((long)blockIdx.x * 4 + w) * per; // the wave's first matrix
+    const int nm = n * m;
+    const int nblk = (int)min((long)per, k - mi0 > 0 ? k - mi0 : 0L); // the wave's matrices
+    E *sl = io_s[w];
+    // the wave's x blocks (one contiguous run of nblk * n * m elements)
+    for (int e = lane; e < nblk * nm; e += 64) sl[e] = x[mi0 * nm + e];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    const bool live = s < nblk;
+    const long mi = live ? mi0 + s : 0;
+    Col<E, WNM> v;
+    const E *xb = sl + s * nm;
+#pragma unroll
+    for (int r = 0; r < WNM; ++r) v.set(r, (r < n && live) ? xb[r * xsi + t * xst] : O::real(0));
+    // the factors of the wave's matrices into the slice too when they fit it (m >= n): every
+    // product then reads its factor element from LDS (a broadcast within the matrix's lanes)
+    const int nn = n * n;
+    const bool ulds = per * nn <= 64 * WNM;
+    if (ulds) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // every lane has read its x
+        __builtin_amdgcn_wave_barrier();
+        for (int e = lane; e < nblk * nn; e += 64) sl[e] = a[mi0 * nn + e];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+    }
+    const E *U = ulds ? sl + s * nn : a + mi * nn;
+    auto u = [&](int r, int q) { return rm ? U[r * n + q] : U[r + q * n]; };
+    // the diagonal's reciprocals from the matrix's own lanes (m >= n), else per lane
+    const bool shared = m >= n;
+    const int tl = t < n ? t : 0;
+    const E rinv = O::inv(u(tl, tl));
+    auto dinv = [&](int r) { return shared ? wshfl<E>(rinv, s * m + r) : O::inv(u(r, r)); };
+    if (left) {
+#pragma unroll
+        for (int r = WNM - 1; r >= 0; --r) {
+            if (r >= n) continue;
+            E wv = scale_by<E>(v.get(r), alpha_re, alpha_im);
+#pragma unroll
+            for (int q = r + 1; q < WNM; ++q)
+                if (q < n) wv = O::sub(wv, O::mul(u(r, q), v.get(q)));
+            v.set(r, O::mul(wv, dinv(r)));
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < WNM; ++c) {
+            if (c >= n) continue;
+            E wv = scale_by<E>(v.get(c), alpha_re, alpha_im);
+#pragma unroll
+            for (int q = 0; q < c; ++q) wv = O::sub(wv, O::mul(v.get(q), u(q, c)));
+            v.set(c, O::mul(wv, dinv(c)));
+        }
+    }
+    // every lane has read its x vector (and its factor) before any lane overwrites the slice
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    E *yb = sl + s * nm;
+    if (live)
+#pragma unroll
+        for (int r = 0; r < WNM; ++r)
+            if (r < n) yb[r * ysi + t * yst] = v.get(r);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    for (int e = lane; e < nblk * nm; e += 64) y[mi0 * nm + e] = sl[e];
+}
+
 template <typename E> bool fits_lds(long n) { return n * n * (long)sizeof(E) <= DENSE_LDS_BYTES; }
 
 template <typename E> void potrf_typed(void *a, long n, long k, int *info, bool rm, hipStream_t s) {
@@ -778,6 +858,32 @@ int launch_gesv(int t, void *a, long n, long k, void *b, long m, bool identity,
         });
     }
     return first_info((const int *)info.ptr, k, s, device);
+}
+
+bool trsm_io_fits(long n, long m) { return g_dense_wave >= 2 && n >= 1 && n <= WNMAX && m >= 1 && m <= 64; }
+
+void launch_trsm_io(int t, const void *a, long n, long k, bool rm, const void *x, int xsi, int xst,
+                    void *y, int ysi, int yst, long m, bool left, const Scalar &alpha, int device) {
+    if (n == 0 || k == 0 || m == 0) return;
+    if (!trsm_io_fits(n, m)) throw Error("dense: internal error (trsm_io shape)");
+    if (k >= (1L << 31)) throw Error("dense: too many matrices");
+    set_device(device);
+    hipStream_t s = get_stream(device);
+    KernelTimer timer("dense", s);
+    dispatch(t, [&](auto z) {
+        typedef decltype(z) E;
+        const long per = 4 * (64 / m);
+        auto go = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3((unsigned)((k + per - 1) / per)), dim3(256), 0, s, (const E *)a, (int)n, k,
+                               rm ? 1 : 0, (const E *)x, xsi, xst, (E *)y, ysi, yst, (int)m, left ? 1 : 0,
+                               alpha.re, alpha.im);
+        };
+        if (n <= 4) go(trsm_io_kernel<E, 4>);
+        else if (n <= 8) go(trsm_io_kernel<E, 8>);
+        else if (n <= 12) go(trsm_io_kernel<E, 12>);
+        else go(trsm_io_kernel<E, 16>);
+        SBX_HIP_CHECK(hipGetLastError());
+    });
 }
 
 void launch_trsm(int t, const void *a, long n, long k, void *x, long m, bool left,

@@ -368,6 +368,12 @@ int launch_gesv(int t, void *a, long n, long k, void *b, long m, bool identity,
 /// left: X (n x m) <- alpha U^-1 X;  right: X (m x n) <- alpha X U^-1  (U upper, non-unit)
 void launch_trsm(int t, const void *a, long n, long k, void *x, long m, bool left,
                  const Scalar &alpha, int device);
+/// The same from x into y (both k contiguous blocks of n x m elements; the lane vector's
+/// component i of right-hand side t at i * si + t * st of a block), U row-major when rm: the
+/// small-matrix form only, when trsm_io_fits(n, m)
+bool trsm_io_fits(long n, long m);
+void launch_trsm_io(int t, const void *a, long n, long k, bool rm, const void *x, int xsi, int xst,
+                    void *y, int ysi, int yst, long m, bool left, const Scalar &alpha, int device);
 /// dst block q = (conj if conj_values) src block perm[q], q < nblocks, blocks of block_elems
 void launch_gather_blocks(int t, const void *src, const int *perm, long nblocks, long block_elems,
                           bool conj_values, void *dst, int device);

@@ -1,0 +1,104 @@
+"""Triangular solves straight between the caller's tensors (kernels_dense.hip trsm_io_kernel,
+dense.cpp dense_solve): small factors (n <= 16) and up to 64 right-hand sides per matrix, x and y
+in either orientation of their (contracted, right-hand-side) labels after the batch labels, the
+factor row- or column-major, left and right solves (dense.h:1160-1220, local_trsm 136-200), against
+a numpy solve and bit-identical to the path through working copies."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+TOL = {np.complex128: 1e-12, np.float64: 1e-12, np.complex64: 2e-5}
+
+
+def _rand(rng, n, dtype):
+    v = rng.uniform(-1, 1, n)
+    if np.dtype(dtype).kind == "c":
+        v = v + 1j * rng.uniform(-1, 1, n)
+    return v.astype(dtype)
+
+
+def _solve(gpu, dtype, cl, xl, yl, n, m, nt, side, alpha, wave=2):
+    """side 'j': x carries C's column label (left solve), 'i': C's row label (right solve)"""
+    import torch
+    import superbblas_amd as sb
+    rng = np.random.default_rng(3)
+    # C: upper triangle well conditioned
+    cm = _rand(rng, nt * n * n, dtype).reshape(nt, n, n)
+    cm = cm + (n + 2) * np.eye(n, dtype=dtype)[None]
+    dims = {"t": nt, "i": n, "j": n, "r": m}
+    cmat = cm if cl == "tij" else np.ascontiguousarray(cm.transpose(0, 2, 1))
+    u = np.triu(cm)
+    xs = [dims[l] for l in xl]
+    x = _rand(rng, int(np.prod(xs)), dtype).reshape(xs)
+    # reference, in (t, contracted, r) form
+    if side == "j":
+        xv = x if xl == "tjr" else x.transpose(0, 2, 1)           # (t, j, r)
+        ref = alpha * np.linalg.solve(u, xv)                        # (t, i, r)
+        refo = ref if yl == "tir" else ref.transpose(0, 2, 1)
+    else:
+        xv = x if xl == "tri" else x.transpose(0, 2, 1)           # (t, r, i)
+        ref = alpha * np.linalg.solve(u.transpose(0, 2, 1), xv.transpose(0, 2, 1)).transpose(0, 2, 1)  # (t, r, j)
+        refo = ref if yl == "trj" else ref.transpose(0, 2, 1)
+    dc = [nt, n, n]
+    ys = [dims[l] for l in yl]
+    tc = torch.from_numpy(cmat.reshape(-1).copy()).to(gpu)
+    tx = torch.from_numpy(x.reshape(-1).copy()).to(gpu)
+    ty = torch.zeros(int(np.prod(ys)), dtype=tx.dtype, device=gpu)
+    old = sb.tune_get("dense.wave")
+    sb.tune_set("dense.wave", wave)
+    try:
+        sb.trsm(alpha, [([0, 0, 0], dc)], dc, cl, [tc], "i", "j", [([0, 0, 0], xs)], xs, xl, [tx],
+                [([0, 0, 0], ys)], ys, yl, [ty])
+        torch.cuda.synchronize()
+    finally:
+        sb.tune_set("dense.wave", old)
+    out = ty.cpu().numpy().reshape(ys)
+    err = np.abs(out - refo).max() / max(1.0, np.abs(refo).max())
+    assert err < TOL[dtype], err
+    assert np.array_equal(tx.cpu().numpy().reshape(xs), x)  # x untouched
+    return out
+
+
+@pytest.mark.parametrize("dtype", [np.complex128, np.complex64, np.float64])
+@pytest.mark.parametrize("cl", ["tij", "tji"])
+@pytest.mark.parametrize("xl,yl", [("tjr", "tir"), ("trj", "tri"), ("tjr", "tri"), ("trj", "tir")])
+@pytest.mark.parametrize("n,m,nt", [(12, 12, 23), (3, 5, 50), (16, 4, 9), (12, 64, 5), (5, 1, 70)])
+def test_trsm_left_io(gpu, dtype, cl, xl, yl, n, m, nt):
+    _solve(gpu, dtype, cl, xl, yl, n, m, nt, "j", 0.5 if dtype != np.complex128 else 0.5 - 1j)
+
+
+@pytest.mark.parametrize("dtype", [np.complex128, np.float64])
+@pytest.mark.parametrize("cl", ["tij", "tji"])
+@pytest.mark.parametrize("xl,yl", [("tri", "trj"), ("tir", "tjr"), ("tri", "tjr")])
+@pytest.mark.parametrize("n,m,nt", [(12, 12, 23), (3, 7, 40)])
+def test_trsm_right_io(gpu, dtype, cl, xl, yl, n, m, nt):
+    _solve(gpu, dtype, cl, xl, yl, n, m, nt, "i", 2.0)
+
+
+def test_trsm_io_matches_working_copies(gpu):
+    """the direct path (dense.wave 2, n <= 16, m <= 64) and the working-copy path (m > 64 rhs
+    per matrix is not direct; here the same problem through dense.wave 1's LU-free small-matrix
+    route is not comparable, so compare against the wave-2 copy path by a layout it declines:
+    y with the batch label last)"""
+    import torch
+    import superbblas_amd as sb
+    rng = np.random.default_rng(9)
+    n, m, nt = 12, 12, 31
+    dtype = np.complex128
+    cm = _rand(rng, nt * n * n, dtype).reshape(nt, n, n) + (n + 2) * np.eye(n)[None]
+    x = _rand(rng, nt * n * m, dtype)
+    dc, dx = [nt, n, n], [nt, n, m]
+    tc = torch.from_numpy(cm.reshape(-1).copy()).to(gpu)
+    tx = torch.from_numpy(x).to(gpu)
+    y1 = torch.zeros(nt * n * m, dtype=tx.dtype, device=gpu)
+    y2 = torch.zeros(nt * n * m, dtype=tx.dtype, device=gpu)
+    sb.trsm(1.5, [([0, 0, 0], dc)], dc, "tij", [tc], "i", "j", [([0, 0, 0], dx)], dx, "tjr", [tx],
+            [([0, 0, 0], dx)], dx, "tir", [y1])
+    dy2 = [n, m, nt]
+    sb.trsm(1.5, [([0, 0, 0], dc)], dc, "tij", [tc], "i", "j", [([0, 0, 0], dx)], dx, "tjr", [tx],
+            [([0, 0, 0], dy2)], dy2, "irt", [y2])
+    torch.cuda.synchronize()
+    a = y1.cpu().numpy().reshape(nt, n, m)
+    b = y2.cpu().numpy().reshape(n, m, nt).transpose(2, 0, 1)
+    assert np.array_equal(a, b)
