@@ -231,12 +231,13 @@ void dense_solve(bool gesm, const Scalar &alpha, const DistTensor &c, const std:
         if (!has(rows ? y.labels : x.labels, l))
             throw Error(std::string(what) + ": missing labels to contract");
 
-    // Straight from x into y (trsm with small factors): x and y hold whole blocks of n x m
+    // Straight from x into y (small factors): x and y hold whole blocks of n x m
     // elements per batch entry in one of the two orientations (the batch labels first, in C's
     // order, then the contracted labels and the right-hand-side labels either way round), with
     // the same batch ranges as C on every rank -- no working copies of x and y, and C in the
-    // caller's row-major order when it is whole (every rank decides alike from the global ranges)
-    if (!gesm) {
+    // caller's row-major order when it is whole (every rank decides alike from the global
+    // ranges); gesm factors C in registers without writing it back and scales by alpha there
+    {
         std::string ot, on;
         for (char l : c.labels)
             if (!has(orows, l) && !has(ocols, l)) ot += l;
@@ -269,15 +270,24 @@ void dense_solve(bool gesm, const Scalar &alpha, const DistTensor &c, const std:
         };
         const int ox = orient(x, lx), oy = orient(y, ly);
         if (ox && oy && x.dtype == c.dtype && y.dtype == c.dtype && dense_wave_rows(n) &&
-            trsm_io_fits(n, m)) {
+            (gesm ? n * m < (1L << 31) : trsm_io_fits(n, m))) {
             Work wc = prepare(c, orows, ocols, comm, true, what, true);
+            int bad = 0;
             for (std::size_t j = 0; j < wc.t.ptr.size(); ++j) {
                 const long k = n ? volume(wc.t.ranges[comm.rank][j].size) / (n * n) : 0;
                 if (k == 0) continue;
-                launch_trsm_io(c.dtype, wc.t.ptr[j], n, k, wc.rm, x.ptr[j], ox == 1 ? (int)m : 1,
-                               ox == 1 ? 1 : (int)n, y.ptr[j], oy == 1 ? (int)m : 1, oy == 1 ? 1 : (int)n,
-                               m, !rows, alpha, x.dev[j]);
+                const int xsi = ox == 1 ? (int)m : 1, xst = ox == 1 ? 1 : (int)n;
+                const int ysi = oy == 1 ? (int)m : 1, yst = oy == 1 ? 1 : (int)n;
+                if (gesm) {
+                    const int info = launch_gesv_io(c.dtype, wc.t.ptr[j], n, k, wc.rm, x.ptr[j], xsi,
+                                                    xst, y.ptr[j], ysi, yst, m, alpha, x.dev[j]);
+                    if (!bad) bad = info;
+                } else {
+                    launch_trsm_io(c.dtype, wc.t.ptr[j], n, k, wc.rm, x.ptr[j], xsi, xst, y.ptr[j], ysi,
+                                   yst, m, !rows, alpha, x.dev[j]);
+                }
             }
+            check_info(bad);
             return;
         }
     }

@@ -347,9 +347,10 @@ __global__ void __launch_bounds__(256) potrf_wave_kernel(E *a, int n, long k, in
 }
 
 template <typename E, int WNM>
-__global__ void __launch_bounds__(256) gesv_wave_kernel(E *a, int n, long k, E *b, long m, int identity,
+__global__ void __launch_bounds__(256) gesv_wave_kernel(E *a, int n, long k, const E *bx, E *b, long m, int identity,
                                                         double alpha_re, double alpha_im,
-                                                        int *info, int rm, int keep_lu) {
+                                                        int *info, int rm, int keep_lu, int xsi, int xst,
+                                                        int ysi, int yst) {
     typedef DOps<E> O;
     __shared__ E lu_s[4][64 * WNM];
     __shared__ E dinv_s[4][64];
@@ -422,15 +423,17 @@ __global__ void __launch_bounds__(256) gesv_wave_kernel(E *a, int n, long k, E *
         const E *M = lu_s[w] + s0 * n;
         const E *Dinv = dinv_s[w] + s0;
         const int *piv = piv_s[w] + s0;
+        // right-hand side column col: element r at r * xsi + col * xst of the matrix's n x m
+        // block of bx, the solution written at r * ysi + col * yst of b's (bx may be b)
+        const E *BX = bx + mi * n * m;
         E *B = b + mi * n * m;
         for (long col = c; col < m; col += n) {
-            // column col of the n x m right-hand side: column-major, or row-major (rm)
-            E *xg = rm ? B + col : B + col * n;
-            const long xs = rm ? m : 1;
+            const E *xg = BX + col * xst;
+            E *yg = B + col * yst;
             Col<E, WNM> x;
 #pragma unroll
             for (int r = 0; r < WNM; ++r)
-                x.set(r, r < n ? (identity ? (r == col ? O::one() : O::real(0)) : xg[r * xs]) : O::real(0));
+                x.set(r, r < n ? (identity ? (r == col ? O::one() : O::real(0)) : xg[r * xsi]) : O::real(0));
 #pragma unroll
             for (int j = 0; j < WNM; ++j) {
                 if (j >= n) continue;
@@ -468,7 +471,7 @@ __global__ void __launch_bounds__(256) gesv_wave_kernel(E *a, int n, long k, E *
                 for (int r = 0; r < WNM; ++r) x.set(r, scale_by<E>(x.get(r), alpha_re, alpha_im));
 #pragma unroll
             for (int r = 0; r < WNM; ++r)
-                if (r < n) xg[r * xs] = x.get(r);
+                if (r < n) yg[r * ysi] = x.get(r);
         }
     }
     if (valid && c == 0) info[mi] = bad;
@@ -728,9 +731,14 @@ template <typename E> void potrf_typed(void *a, long n, long k, int *info, bool 
                        lds ? (size_t)(n * n * sizeof(E)) : 0, s, (E *)a, n, lds ? 1 : 0, info);
     SBX_HIP_CHECK(hipGetLastError());
 }
+struct GesvIO {
+    const void *x = nullptr; // right-hand sides (nullptr: b itself)
+    int xsi = 0, xst = 0, ysi = 0, yst = 0; // 0: the orientation of rm (row-major or column-major)
+};
+
 template <typename E>
 void gesv_typed(void *a, long n, long k, void *b, long m, bool identity, const Scalar &alpha,
-                int *ipiv, int *info, bool rm, bool keep_lu, hipStream_t s) {
+                int *ipiv, int *info, bool rm, bool keep_lu, hipStream_t s, const GesvIO &io = GesvIO{}) {
     if (n <= WNMAX && g_dense_wave && identity && !keep_lu && alpha.re == 1 && alpha.im == 0) {
         // the inverse only (the factors not kept): Gauss-Jordan, a 16-lane row per matrix
         auto go = [&](auto kern) {
@@ -745,11 +753,13 @@ void gesv_typed(void *a, long n, long k, void *b, long m, bool identity, const S
         return;
     }
     if (n <= WNMAX && g_dense_wave) {
+        const int xsi = io.xsi ? io.xsi : (rm ? (int)m : 1), xst = io.xst ? io.xst : (rm ? 1 : (int)n);
+        const int ysi = io.ysi ? io.ysi : (rm ? (int)m : 1), yst = io.yst ? io.yst : (rm ? 1 : (int)n);
         auto go = [&](auto kern) {
             const long per = 4 * (64 / n);
             hipLaunchKernelGGL(kern, dim3((unsigned)((k + per - 1) / per)), dim3(256), 0, s, (E *)a, (int)n, k,
-                               (E *)b, m, identity ? 1 : 0, alpha.re, alpha.im, info, rm ? 1 : 0,
-                               keep_lu ? 1 : 0);
+                               (const E *)(io.x ? io.x : b), (E *)b, m, identity ? 1 : 0, alpha.re, alpha.im,
+                               info, rm ? 1 : 0, keep_lu ? 1 : 0, xsi, xst, ysi, yst);
         };
         if (n <= 4) go(gesv_wave_kernel<E, 4>);
         else if (n <= 8) go(gesv_wave_kernel<E, 8>);
@@ -760,6 +770,7 @@ void gesv_typed(void *a, long n, long k, void *b, long m, bool identity, const S
     }
     if (rm) throw Error("dense: internal error (row-major matrices need the wave kernels)");
     if (!keep_lu || a == b) throw Error("dense: internal error (in-place inversion needs the wave kernels)");
+    if (io.x) throw Error("dense: internal error (separate right-hand sides need the wave kernels)");
     const bool lds = fits_lds<E>(n);
     hipLaunchKernelGGL(gesv_kernel<E>, dim3((unsigned)k), dim3(DTH),
                        lds ? (size_t)(n * n * sizeof(E)) : 0, s, (E *)a, n, (E *)b, m,
@@ -884,6 +895,27 @@ void launch_trsm_io(int t, const void *a, long n, long k, bool rm, const void *x
         else go(trsm_io_kernel<E, 16>);
         SBX_HIP_CHECK(hipGetLastError());
     });
+}
+
+int launch_gesv_io(int t, const void *a, long n, long k, bool rm, const void *x, int xsi, int xst,
+                   void *y, int ysi, int yst, long m, const Scalar &alpha, int device) {
+    if (n == 0 || k == 0 || m == 0) return 0;
+    if (!dense_wave_rows(n)) throw Error("dense: internal error (gesv_io shape)");
+    if (k >= (1L << 31)) throw Error("dense: too many matrices");
+    set_device(device);
+    hipStream_t s = get_stream(device);
+    Scratch info(sizeof(int) * k, device);
+    GesvIO io;
+    io.x = x;
+    io.xsi = xsi, io.xst = xst, io.ysi = ysi, io.yst = yst;
+    {
+        KernelTimer timer("dense", s);
+        dispatch(t, [&](auto z) {
+            gesv_typed<decltype(z)>(const_cast<void *>(a), n, k, y, m, false, alpha, nullptr, (int *)info.ptr, rm,
+                                    false, s, io);
+        });
+    }
+    return first_info((const int *)info.ptr, k, s, device);
 }
 
 void launch_trsm(int t, const void *a, long n, long k, void *x, long m, bool left,

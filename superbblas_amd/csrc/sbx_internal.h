@@ -372,6 +372,10 @@ void launch_trsm(int t, const void *a, long n, long k, void *x, long m, bool lef
 /// component i of right-hand side t at i * si + t * st of a block), U row-major when rm: the
 /// small-matrix form only, when trsm_io_fits(n, m)
 bool trsm_io_fits(long n, long m);
+/// gesm from x into y (same block conventions as launch_trsm_io), the LU of A (row-major when rm)
+/// kept in the kernel: A is not written (dense_wave_rows(n) only); the first nonzero info
+int launch_gesv_io(int t, const void *a, long n, long k, bool rm, const void *x, int xsi, int xst,
+                   void *y, int ysi, int yst, long m, const Scalar &alpha, int device);
 void launch_trsm_io(int t, const void *a, long n, long k, bool rm, const void *x, int xsi, int xst,
                     void *y, int ysi, int yst, long m, bool left, const Scalar &alpha, int device);
 /// dst block q = (conj if conj_values) src block perm[q], q < nblocks, blocks of block_elems

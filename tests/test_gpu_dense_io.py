@@ -1,8 +1,10 @@
-"""Triangular solves straight between the caller's tensors (kernels_dense.hip trsm_io_kernel,
-dense.cpp dense_solve): small factors (n <= 16) and up to 64 right-hand sides per matrix, x and y
-in either orientation of their (contracted, right-hand-side) labels after the batch labels, the
-factor row- or column-major, left and right solves (dense.h:1160-1220, local_trsm 136-200), against
-a numpy solve and bit-identical to the path through working copies."""
+"""Solves straight between the caller's tensors (dense.cpp dense_solve).  trsm (kernels_dense.hip
+trsm_io_kernel): small factors (n <= 16) and up to 64 right-hand sides per matrix, x and y in either
+orientation of their (contracted, right-hand-side) labels after the batch labels, the factor row- or
+column-major, left and right solves (dense.h:1160-1220, local_trsm 136-200).  gesm (gesv_wave_kernel
+reading x and writing y in their own orientations, C factored in registers and left untouched; any
+number of right-hand sides; dense.h:1239-1266, local_gesm).  Against a numpy solve and bit-identical
+to the path through working copies."""
 import numpy as np
 import pytest
 
@@ -97,6 +99,82 @@ def test_trsm_io_matches_working_copies(gpu):
             [([0, 0, 0], dx)], dx, "tir", [y1])
     dy2 = [n, m, nt]
     sb.trsm(1.5, [([0, 0, 0], dc)], dc, "tij", [tc], "i", "j", [([0, 0, 0], dx)], dx, "tjr", [tx],
+            [([0, 0, 0], dy2)], dy2, "irt", [y2])
+    torch.cuda.synchronize()
+    a = y1.cpu().numpy().reshape(nt, n, m)
+    b = y2.cpu().numpy().reshape(n, m, nt).transpose(2, 0, 1)
+    assert np.array_equal(a, b)
+
+
+def _gesm(gpu, dtype, cl, xl, yl, n, m, nt, alpha, wave=2, singular=None):
+    import torch
+    import superbblas_amd as sb
+    rng = np.random.default_rng(4)
+    cm = _rand(rng, nt * n * n, dtype).reshape(nt, n, n) + 0.5 * np.eye(n, dtype=dtype)[None]
+    if singular is not None:
+        cm[singular] = 0
+    dims = {"t": nt, "i": n, "j": n, "r": m}
+    cmat = cm if cl == "tij" else np.ascontiguousarray(cm.transpose(0, 2, 1))
+    xs = [dims[l] for l in xl]
+    ys = [dims[l] for l in yl]
+    x = _rand(rng, int(np.prod(xs)), dtype).reshape(xs)
+    xv = x if xl == "tjr" else x.transpose(0, 2, 1)
+    dc = [nt, n, n]
+    tc = torch.from_numpy(cmat.reshape(-1).copy()).to(gpu)
+    tx = torch.from_numpy(x.reshape(-1).copy()).to(gpu)
+    ty = torch.zeros(int(np.prod(ys)), dtype=tx.dtype, device=gpu)
+    old = sb.tune_get("dense.wave")
+    sb.tune_set("dense.wave", wave)
+    try:
+        sb.gesm(alpha, [([0, 0, 0], dc)], dc, cl, [tc], "i", "j", [([0, 0, 0], xs)], xs, xl, [tx],
+                [([0, 0, 0], ys)], ys, yl, [ty])
+        torch.cuda.synchronize()
+    finally:
+        sb.tune_set("dense.wave", old)
+    ref = alpha * np.linalg.solve(cm, xv)
+    refo = ref if yl == "tir" else ref.transpose(0, 2, 1)
+    out = ty.cpu().numpy().reshape(ys)
+    cond = max(np.linalg.cond(cm[t]) for t in range(nt))
+    err = np.abs(out - refo).max() / max(1.0, np.abs(refo).max())
+    assert err < TOL[dtype] * max(1.0, cond / 10), (err, cond)
+    assert np.array_equal(tx.cpu().numpy().reshape(xs), x)  # x untouched
+    assert np.array_equal(tc.cpu().numpy(), cmat.reshape(-1))  # C untouched
+    return out
+
+
+@pytest.mark.parametrize("dtype", [np.complex128, np.complex64, np.float64])
+@pytest.mark.parametrize("cl", ["tij", "tji"])
+@pytest.mark.parametrize("xl,yl", [("tjr", "tir"), ("trj", "tri"), ("tjr", "tri"), ("trj", "tir")])
+@pytest.mark.parametrize("n,m,nt", [(12, 12, 23), (3, 5, 50), (16, 4, 9), (12, 100, 5), (5, 1, 70)])
+def test_gesm_io(gpu, dtype, cl, xl, yl, n, m, nt):
+    _gesm(gpu, dtype, cl, xl, yl, n, m, nt, 0.5 if dtype != np.complex128 else 0.5 - 1j)
+
+
+def test_gesm_io_singular(gpu):
+    """a singular matrix: the LAPACK-style error of the working-copy path, C left alone"""
+    with pytest.raises(Exception, match="lapack"):
+        _gesm(gpu, np.complex128, "tij", "tjr", "tir", 12, 12, 8, 1.0, singular=5)
+
+
+def test_gesm_io_matches_working_copies(gpu):
+    """alpha 1: the direct path and the working-copy path (y with the batch label last, a layout
+    the direct path declines) give the same bits"""
+    import torch
+    import superbblas_amd as sb
+    rng = np.random.default_rng(10)
+    n, m, nt = 12, 12, 31
+    dtype = np.complex128
+    cm = _rand(rng, nt * n * n, dtype).reshape(nt, n, n) + 0.5 * np.eye(n)[None]
+    x = _rand(rng, nt * n * m, dtype)
+    dc, dx = [nt, n, n], [nt, n, m]
+    tc = torch.from_numpy(cm.reshape(-1).copy()).to(gpu)
+    tx = torch.from_numpy(x).to(gpu)
+    y1 = torch.zeros(nt * n * m, dtype=tx.dtype, device=gpu)
+    y2 = torch.zeros(nt * n * m, dtype=tx.dtype, device=gpu)
+    sb.gesm(1.0, [([0, 0, 0], dc)], dc, "tij", [tc], "i", "j", [([0, 0, 0], dx)], dx, "tjr", [tx],
+            [([0, 0, 0], dx)], dx, "tir", [y1])
+    dy2 = [n, m, nt]
+    sb.gesm(1.0, [([0, 0, 0], dc)], dc, "tij", [tc], "i", "j", [([0, 0, 0], dx)], dx, "tjr", [tx],
             [([0, 0, 0], dy2)], dy2, "irt", [y2])
     torch.cuda.synchronize()
     a = y1.cpu().numpy().reshape(nt, n, m)
