@@ -1320,9 +1320,12 @@ def wilson_bench(sb, dev, L, ncols=12, reps=5):
                                     dimx, [x], 0.0, px, "pxyztcns", [0] * 8, dimx, dimx, "p", [y]))
     by = 16.0 * (81 * V + 2 * 12 * V * ncols) + 4.0 * 9 * V
     form = sb.tune_get("bsr.last_kernel")
-    out.update({"kron_n12_kernel": ("bsr_kron_mfma_packed_kernel (a wave's 16 column slots over "
-                                    "several rows; " if form == 6 else "bsr_kron_mfma_kernel (") +
-                                   "color on the VALU, spin on v_mfma_f64_4x4x4_4b)",
+    out.update({"kron_n12_kernel": ("bsr_kron_spin_kernel (spin first on the VALU, a lane per (row, "
+                                    "column) pair, zero spin entries skipped, rows in the XCD order)"
+                                    if form == 9 else
+                                    ("bsr_kron_mfma_packed_kernel (a wave's 16 column slots over "
+                                     "several rows; " if form == 6 else "bsr_kron_mfma_kernel (") +
+                                    "color on the VALU, spin on v_mfma_f64_4x4x4_4b)"),
                 "kron_n12_kernel_ms": round(t * 1e3, 4),
                 "kron_n12_kernel_GBps": round(by / t / 1e9, 1),
                 "kron_n12_kernel_frac_hbm": round(by / t / 1e9 / PEAK_HBM_GBPS, 4),

@@ -43,6 +43,7 @@ struct BsrComp {
     void *owned_v = nullptr;         // values owned by the operator (transposed operator, or
                                      // the device copy of a host component's values)
     void *owned_kron = nullptr;      // device copy of a host component's Kronecker matrices
+    int *kron_perm = nullptr;        // Kronecker operators: block rows in the XCD order
 };
 
 struct BsrOp {
@@ -68,6 +69,7 @@ struct BsrOp {
             if (c.owned_v) (void)hipFree(c.owned_v);
             if (c.owned_kron) (void)hipFree(c.owned_kron);
             if (c.tile_buf) (void)hipFree(c.tile_buf);
+            if (c.kron_perm) (void)hipFree(c.kron_perm);
         }
     }
 };
@@ -153,6 +155,70 @@ void build_tile_schedule(BsrComp &bc, const Coor &isize, const Coor &blocki) {
     bc.tile_loc = (const unsigned char *)(b + b_rows + b_uniq);
     bc.tile_umax = umax;
     bc.tile_chunks = nchunks;
+}
+
+/// The XCD order of a lattice operator's block rows (bsr_kron_spin_kernel): the rows are the
+/// component's image sites (SlowToFast over the image dims without the blocked and
+/// Kronecker-blocked ones); the lattice is cut into 8 boxes, halving the longest extent of every
+/// box three times (the slowest dim on ties: 16^4 -> 8x8x8x16), the boxes laid end to end, each
+/// in its natural order.  The kernel hands each XCD a contiguous eighth of the row slots, so an
+/// XCD sweeps one box: the x sites its rows' neighbours share are read within a short distance
+/// of each other (16^4: the slowest neighbour 1024 rows apart instead of 4096) and the box's
+/// faces are the only sites two XCDs both fetch.  No order (nullptr) for a component that is not
+/// a whole box of sites.
+void build_kron_order(BsrComp &bc, const Coor &isize, const Coor &blocki, const Coor &kroni) {
+    std::vector<long> dims;
+    for (std::size_t d = 0; d < isize.size(); ++d) {
+        const long r = isize[d] / std::max(1L, (long)blocki[d] * kroni[d]);
+        if (r > 1) dims.push_back(r);
+    }
+    long vol = 1;
+    for (long r : dims) vol *= r;
+    if (dims.empty() || vol != bc.block_rows || vol < 64) return;
+    const int nd = (int)dims.size();
+    struct Box {
+        std::vector<long> from, size;
+    };
+    std::vector<Box> boxes{Box{std::vector<long>(nd, 0), dims}};
+    for (int cut = 0; cut < 3; ++cut) {
+        std::vector<Box> next;
+        for (const Box &b : boxes) {
+            int at = 0;
+            for (int d = 1; d < nd; ++d)
+                if (b.size[d] > b.size[at]) at = d;
+            if (b.size[at] < 2) {
+                next.push_back(b);
+                continue;
+            }
+            Box lo = b, hi = b;
+            lo.size[at] = b.size[at] / 2;
+            hi.from[at] = b.from[at] + lo.size[at];
+            hi.size[at] = b.size[at] - lo.size[at];
+            next.push_back(lo);
+            next.push_back(hi);
+        }
+        boxes.swap(next);
+    }
+    std::vector<long> stride(nd, 1);
+    for (int d = nd - 2; d >= 0; --d) stride[d] = stride[d + 1] * dims[d + 1];
+    std::vector<int> perm;
+    perm.reserve(vol);
+    std::vector<long> c(nd);
+    for (const Box &b : boxes) {
+        long bv = 1;
+        for (long e : b.size) bv *= e;
+        for (long e = 0; e < bv; ++e) {
+            long r = e, row = 0;
+            for (int d = nd - 1; d >= 0; --d) {
+                c[d] = r % b.size[d];
+                r /= b.size[d];
+                row += (b.from[d] + c[d]) * stride[d];
+            }
+            perm.push_back((int)row);
+        }
+    }
+    SBX_HIP_CHECK(hipMalloc(&bc.kron_perm, sizeof(int) * vol));
+    SBX_HIP_CHECK(hipMemcpy(bc.kron_perm, perm.data(), sizeof(int) * vol, hipMemcpyHostToDevice));
 }
 
 } // namespace
@@ -290,6 +356,8 @@ BsrOp *bsr_create(int nd, int ni, int dtype, const std::vector<std::vector<Range
         SBX_HIP_CHECK(hipMemcpy(bc.ii, rowptr.data(), sizeof(int) * (nii + 1), hipMemcpyHostToDevice));
         if (nnz > 0)
             SBX_HIP_CHECK(hipMemcpy(bc.jj, hjj.data(), sizeof(int) * nnz, hipMemcpyHostToDevice));
+        if (op->is_kron && volume(op->kroni) == 4 && bi == 3 && bd == 3 && dtype == SBX_CDOUBLE)
+            build_kron_order(bc, ri.size, blocki, op->kroni);
         if (!op->is_kron) {
             bc.h_rowptr = std::move(rowptr);
             bc.h_jj = std::move(hjj);
@@ -751,6 +819,7 @@ void bsr_krylov(const BsrOp &op, const Scalar &alpha, const std::string &oi,
                     d.ki = (int)volume(op.kroni);
                     d.kd = (int)volume(op.krond);
                     d.kron = bc.kron;
+                    d.kron_perm = bc.kron_perm;
                     launch_bsr_kron(d, bc.dev);
                 } else {
                     launch_bsr(d, bc.dev);

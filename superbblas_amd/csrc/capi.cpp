@@ -428,6 +428,9 @@ int sbx_tune_set(const char *key, long long value) {
         else if (k == "bsr.kron_pack") g_bsr_tune.kron_pack = (int)value;
         else if (k == "bsr.kron_xlds") g_bsr_tune.kron_xlds = (int)value;
         else if (k == "bsr.kron_ylds") g_bsr_tune.kron_ylds = (int)value;
+        else if (k == "bsr.kron_spin") g_bsr_tune.kron_spin = (int)value;
+        else if (k == "bsr.kron_spin_min_cols") g_bsr_tune.kron_spin_min_cols = (long)value;
+        else if (k == "bsr.kron_order") g_bsr_tune.kron_order = (int)value;
         else if (k == "bsr.nt") g_bsr_tune.nt = (int)value;
         else if (k == "dense.wave") g_dense_wave = (int)value;
         else if (k == "bsr.blk_pd") g_bsr_tune.blk_pd = (int)value;
@@ -482,6 +485,9 @@ int sbx_tune_get(const char *key, long long *value) {
         else if (k == "bsr.kron_pack") *value = g_bsr_tune.kron_pack;
         else if (k == "bsr.kron_xlds") *value = g_bsr_tune.kron_xlds;
         else if (k == "bsr.kron_ylds") *value = g_bsr_tune.kron_ylds;
+        else if (k == "bsr.kron_spin") *value = g_bsr_tune.kron_spin;
+        else if (k == "bsr.kron_spin_min_cols") *value = g_bsr_tune.kron_spin_min_cols;
+        else if (k == "bsr.kron_order") *value = g_bsr_tune.kron_order;
         else if (k == "bsr.nt") *value = g_bsr_tune.nt;
         else if (k == "dense.wave") *value = g_dense_wave;
         else if (k == "bsr.blk_pd") *value = g_bsr_tune.blk_pd;

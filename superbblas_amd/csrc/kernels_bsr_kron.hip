@@ -35,6 +35,7 @@ struct KronArgs {
     int add;
     int ylds; ///< the XL kernels: y written through the wave's LDS ring in whole 64-B spin pieces
     long x_rows; ///< domain rows of x (sites * bd): the extent x's LDS-DMA buffer offsets address
+    const int *perm; ///< the spin-first kernel: block row of each row slot (nullptr: the identity)
 };
 
 template <typename E, int BI, int BD, int KI, int KD>
@@ -672,12 +673,239 @@ __global__ void __launch_bounds__(256) bsr_kron_mfma_packed_kernel(const KronArg
     }
 }
 
+
+// complex<double>, 3x3 color blocks, 4x4 spin matrices, from 8 rhs columns, spin first -- the
+// reference's order (contract_kron_cols applies K_mu to x, then bsrmm the color blocks,
+// bsr.h:933-998): a lane owns one (block row, rhs column) pair and its 12 outputs, so no lane idles
+// at any column count (pair p = row slot p / n, column p % n), and
+//   h(d, a) = sum_b K_mu(a, b) x(J_mu, d, col, b)    (VALU; the zero entries of K_mu skipped and
+//                                                    real / imaginary-only entries taken as such,
+//                                                    by scalar branches on its wave-uniform values)
+//   acc(i, a) += U_mu(i, d) h(d, a)
+// per step (mu, d).  The Wilson-type spin matrices (1 -+ gamma_mu: 8 of 16 entries, each +-1 or
+// +-i) cost 16 FMAs per step against the 4x4x4 MFMA form's 48 (and its 36 colour FMAs per spin
+// group of 16 columns become 48 per 64 columns); the K_mu values are read at run time as the
+// MFMA kernels do.  Per wave and step one LDS-DMA group, one step ahead: x of the 64 pairs (4
+// KB: 16 pairs' 4 spins a 1-KB piece, the pieces lane-linear over the pairs' 64-B spin runs; a
+// lane reads its spins back rotated by (b + p / 4) mod 4, conflict-free for ds_read_b128's lane
+// groups), U_mu(., d) of the wave's rows (<= 9 rows of 3 values, lanes < 32), and at d = 0 the
+// wave rows' block columns of the next neighbour (one dword per row).  Rows optionally visited in
+// the host's XCD order (perm: each XCD's share of slots a compact lattice box).
+constexpr int KS_WAVE_LDS = 2 * 4096 + 2 * 512 + 2 * 256;
+
+/// DMA of 16 (or 4: dword) bytes per lane into LDS at m0 = base (+ 16 or 4 per lane)
+__device__ __forceinline__ void dma16(unsigned off, unsigned base, __amdgpu_buffer_rsrc_t r) {
+    asm volatile("s_mov_b32 m0, %1\n\t"
+                 "s_nop 0\n\t"
+                 "buffer_load_dwordx4 %0, %2, 0 offen lds"
+                 :
+                 : "v"(off), "s"(__builtin_amdgcn_readfirstlane(base)), "s"(r)
+                 : "memory", "m0");
+}
+__device__ __forceinline__ void dma4(unsigned off, unsigned base, __amdgpu_buffer_rsrc_t r) {
+    asm volatile("s_mov_b32 m0, %1\n\t"
+                 "s_nop 0\n\t"
+                 "buffer_load_dword %0, %2, 0 offen lds"
+                 :
+                 : "v"(off), "s"(__builtin_amdgcn_readfirstlane(base)), "s"(r)
+                 : "memory", "m0");
+}
+
+/// nonzero test of a wave-uniform double on its bits (scalar ALU; -0 counts as zero)
+__device__ __forceinline__ unsigned nz_bits(double v) {
+    const long long b = __double_as_longlong(v);
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32)) & 0x7fffffffu;
+    return (lo | hi) != 0 ? 1u : 0u;
+}
+
+__global__ void __launch_bounds__(256) bsr_kron_spin_kernel(const KronArgs p) {
+    typedef double2 E;
+    extern __shared__ __attribute__((aligned(16))) char smem_s[];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // XCD-contiguous workgroup order: the hardware deals workgroups round robin over the 8 XCDs
+    const int bid = blockIdx.x, nwg = gridDim.x;
+    const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int wgi = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    // (launcher: pairs, x, values and block columns below 2^31 elements / bytes)
+    const int n = (int)p.ncols, nnz = p.nnz;
+    const int total = (int)(p.block_rows * n);
+    const int pw0 = (wgi * 4 + w) * 64; // the wave's first pair
+    if (pw0 >= total) return;
+    const int slot_lo = pw0 / n;
+    const int rows_w = min(pw0 + 63, total - 1) / n - slot_lo + 1; // <= 9 (n >= 8)
+    const int *perm = p.perm;
+    auto row_of = [&](int slot) -> int { return perm ? perm[slot] : slot; };
+    // the lane's pair
+    const int pp = min(pw0 + lane, total - 1);
+    const bool live = pw0 + lane < total;
+    const int slot = pp / n, col = pp - slot * n;
+    const int wr = slot - slot_lo;
+    // LDS per wave: x slots [2][4096], U slots [2][512], J slots [2][256]
+    char *wl = smem_s + w * KS_WAVE_LDS;
+    const unsigned wl_a = (unsigned)(size_t)(const __attribute__((address_space(3))) void *)wl;
+    const E *xs = (const E *)wl;
+    const E *us = (const E *)(wl + 8192);
+    const int *js = (const int *)(wl + 9216);
+    // x DMA: instruction k, lane l -> pair q = 16 k + l / 4, spin (l % 4 - q / 4) mod 4; its
+    // (column * 4 + spin) in elements (-1: past the last pair) and wave row
+    const int xd = 4 * n; // elements between the colors of a site
+    int xcolb[4], xwr[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int q = 16 * k + (lane >> 2);
+        const int pq = pw0 + q, pc = min(pq, total - 1);
+        const int b = ((lane & 3) - (q >> 2)) & 3;
+        const int sq = pc / n;
+        xwr[k] = sq - slot_lo;
+        xcolb[k] = pq < total ? (pc - sq * n) * 4 + b : -1;
+    }
+    // U DMA: lane l < 3 rows_w -> value i = l % 3 of wave row l / 3; J DMA: lane l < rows_w -> row l
+    const bool u_ok = lane < 3 * rows_w;
+    const int ui = lane % 3;
+    const int ubase = (u_ok ? row_of(slot_lo + lane / 3) : 0) * nnz * 9 + (p.block_im_fast ? ui : 3 * ui);
+    const int ustep = p.block_im_fast ? 3 : 1;
+    const bool j_ok = lane < rows_w;
+    const int jbase = (j_ok ? row_of(slot_lo + lane) : 0) * nnz;
+    const int orow = row_of(slot); // the output row
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)p.x, (short)0, (int)(p.x_rows * 4 * n * 16), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ru = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)p.v, (short)0, (int)(p.block_rows * nnz * 9 * 16), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rj = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)p.jj, (short)0, (int)(p.block_rows * nnz * 4), 0x00020000);
+    // block columns of the x pieces for the current neighbour: mu = 0 from global memory, then
+    // from the J slots
+    int jx[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) jx[k] = p.jj[row_of(slot_lo + xwr[k]) * nnz];
+    auto issue = [&](int mu, int d, int par) {
+        const unsigned xb = wl_a + (unsigned)par * 4096u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            dma16(xcolb[k] >= 0 ? (unsigned)((jx[k] * 3 + d) * xd + xcolb[k]) * 16u : 0x80000000u,
+                  xb + (unsigned)k * 1024u, rx);
+        if (lane < 32)
+            dma16(u_ok ? (unsigned)(ubase + mu * 9 + d * ustep) * 16u : 0x80000000u,
+                  wl_a + 8192u + (unsigned)par * 512u, ru);
+        if (d == 0 && mu + 1 < nnz)
+            dma4(j_ok ? (unsigned)(jbase + mu + 1) * 4u : 0x80000000u,
+                 wl_a + 9216u + (unsigned)((mu + 1) & 1) * 256u, rj);
+    };
+    double ar[3][4], ai[3][4];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int a = 0; a < 4; ++a) ar[i][a] = 0, ai[i][a] = 0;
+    const int rot = lane >> 2;
+    const E *kron = (const E *)p.kron;
+    issue(0, 0, 0);
+#pragma unroll 1
+    for (int mu = 0; mu < nnz; ++mu) {
+        // the spin matrix's nonzero real / imaginary parts, bit 4 a + b (scalar)
+        const E *K = kron + mu * 16;
+        unsigned mr = 0, mi = 0;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const E kv = Uniform<E>::load(K, p.block_im_fast ? (e >> 2) + 4 * (e & 3) : e);
+            mr |= nz_bits(kv.x) << e;
+            mi |= nz_bits(kv.y) << e;
+        }
+        mr = __builtin_amdgcn_readfirstlane(mr);
+        mi = __builtin_amdgcn_readfirstlane(mi);
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            const int t = mu * 3 + d, par = t & 1;
+            const bool more = t + 1 < 3 * nnz;
+            // the slot about to be refilled was read in step t - 1
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (more) {
+                if (d == 2) {
+                    // the next neighbour's block columns (landed with step t - 2's group)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) jx[k] = js[((mu + 1) & 1) * 64 + xwr[k]];
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    issue(mu + 1, 0, par ^ 1);
+                } else {
+                    issue(mu, d + 1, par ^ 1);
+                }
+            }
+            // step t's group landed; step t + 1's (5 instructions, 6 with a J piece) may stay in flight
+            if (!more) wait_vmcnt(0);
+            else if (d == 2 && mu + 2 < nnz) wait_vmcnt(6);
+            else wait_vmcnt(5);
+            const E *xp = xs + par * 256;
+            E xv[4];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) xv[b] = xp[4 * lane + ((b + rot) & 3)];
+            const E *up = us + par * 32 + wr * 3;
+            E uv[3];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) uv[i] = up[i];
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                if (((mr | mi) >> (4 * a) & 15) == 0) continue; // a zero row of K_mu
+                double hr = 0, hi = 0;
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const int e = 4 * a + b;
+                    const int me = p.block_im_fast ? a + 4 * b : e;
+                    // (the empty asm keeps the compiler from turning the branches into selects)
+                    if (mr >> e & 1) {
+                        const double k = Uniform<E>::load(K, me).x;
+                        hr = __builtin_fma(k, xv[b].x, hr);
+                        hi = __builtin_fma(k, xv[b].y, hi);
+                        asm volatile("" : "+v"(hr), "+v"(hi));
+                    }
+                    if (mi >> e & 1) {
+                        const double k = Uniform<E>::load(K, me).y;
+                        hr = __builtin_fma(-k, xv[b].y, hr);
+                        hi = __builtin_fma(k, xv[b].x, hi);
+                        asm volatile("" : "+v"(hr), "+v"(hi));
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    ar[i][a] = __builtin_fma(uv[i].x, hr, ar[i][a]);
+                    ar[i][a] = __builtin_fma(-uv[i].y, hi, ar[i][a]);
+                    ai[i][a] = __builtin_fma(uv[i].x, hi, ai[i][a]);
+                    ai[i][a] = __builtin_fma(uv[i].y, hr, ai[i][a]);
+                }
+            }
+        }
+    }
+    if (!live) return;
+    E *yp = (E *)p.y + ((long)orow * 3 * n + col) * 4;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            E o = Ops<E>::scale(E{ar[i][a], ai[i][a]}, p.alpha_re, p.alpha_im);
+            if (p.add) o = Ops<E>::add(o, yp[(long)i * n * 4 + a]);
+            yp[(long)i * n * 4 + a] = o;
+        }
+}
+
 constexpr long KRON_LDS_BYTES = 64 * 1024;
 
 template <typename E> void launch_kron_typed(const KronArgs &a, hipStream_t s) {
     KernelTimer timer("bsr", s);
     const long row_bytes = (long)a.nnz * (a.bi * a.bd * sizeof(E) + sizeof(int));
     if constexpr (std::is_same<E, double2>::value) {
+        if (g_bsr_tune.kron_spin && a.bi == 3 && a.bd == 3 && a.ki == 4 && a.kd == 4 && a.nnz >= 1 &&
+            a.nnz <= 64 && a.ncols >= std::max(8L, g_bsr_tune.kron_spin_min_cols) &&
+            a.block_rows * a.nnz * 9 * 16 < (1L << 31) && a.x_rows * 4 * a.ncols * 16 < (1L << 31) &&
+            a.block_rows * a.ncols + 1024 < (1L << 31)) {
+            const long waves = (a.block_rows * a.ncols + 63) / 64, blocks = (waves + 3) / 4;
+            if (blocks < (1L << 31)) {
+                g_bsr_tune.last = 9;
+                const size_t lds = 4 * (size_t)KS_WAVE_LDS;
+                hipLaunchKernelGGL(bsr_kron_spin_kernel, dim3((unsigned)blocks), dim3(256), lds, s, a);
+                SBX_HIP_CHECK(hipGetLastError());
+                return;
+            }
+        }
         if (g_bsr_tune.kron_mfma && a.bi == 3 && a.bd == 3 && a.ki == 4 && a.kd == 4 && a.nnz == 9 &&
             a.ncols >= g_bsr_tune.kron_mfma_min_cols && a.block_rows * 81L * 16 < (1L << 31)) {
             // packed slots: W waves of 16 (row, column) slots hold RW = 16 W / n whole rows
@@ -791,6 +1019,7 @@ void launch_bsr_kron(const BsrDesc &d, int device) {
     // domain sites can exceed block_rows (halo sites): the x staging's 32-bit buffer offsets are
     // bounded by x's extent, not y's
     a.x_rows = d.x_rows > 0 ? d.x_rows : d.block_rows * d.bd;
+    a.perm = g_bsr_tune.kron_order ? d.kron_perm : nullptr;
     switch (d.t) {
     case SBX_CDOUBLE: return launch_kron_typed<double2>(a, s);
     case SBX_CFLOAT: return launch_kron_typed<float2>(a, s);

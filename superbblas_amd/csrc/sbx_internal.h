@@ -269,6 +269,10 @@ struct BsrTune {
     int kron_xlds = 1;           ///< ... x staged by LDS-DMA, a column's 4 spins as one 64-B piece, this many
                                  ///< neighbours ahead (0 = off: per-lane loads one ahead; 1..3)
     int kron_ylds = 0;           ///< ... with x staged: y written through the same ring in whole pieces
+    int kron_spin = 1;           ///< ... spin first on the VALU, a lane per (row, column) (bsr_kron_spin_kernel;
+                                 ///< before the MFMA forms)
+    long kron_spin_min_cols = 8; ///< ... from this many rhs columns (at least 8)
+    int kron_order = 1;          ///< ... rows in the operator's XCD order (bsr.cpp build_kron_order)
     int blk_pd = 1; ///< 12x12 blocks by LDS-DMA: blocks in flight ahead of the one in use (1..3)
     int tile = 0;   ///< 9-point 3x3 complex<double> operators, row-major x and y: site tiles with
                     ///< their halo staged in LDS (bsr_ell9_tile_kernel) ... (opt-in: 16^4 n = 64
@@ -283,7 +287,8 @@ struct BsrTune {
     /// of the last launch -- 1 one thread per block (3x3), 2 split rows (3x3), 3 row chunks (3x3),
     /// 4 site tiles (3x3),
     /// 5 Kronecker on MFMA, 6 the same with packed column slots, 7 12x12 blocks by LDS-DMA, 8 the
-    /// same with packed slots, 10 12x12 fragment gathers (9 blocks per row), 11 12x12 generic rows,
+    /// same with packed slots, 9 Kronecker spin first (VALU), 10 12x12 fragment gathers (9 blocks
+    /// per row), 11 12x12 generic rows,
     /// 0 another kernel
     std::atomic<int> last{0};
 };
@@ -347,6 +352,7 @@ struct BsrDesc {
     // (block row, bi, ncols, ki), both row major; jj holds the domain site of each nonzero
     int ki = 1, kd = 1;
     const void *kron = nullptr; ///< num_nnz_per_row matrices of ki x kd
+    const int *kron_perm = nullptr; ///< block row per row slot in the XCD order (nullptr: none)
     // site tiles of 3x3 9-point operators (bsr.cpp build_tile_schedule; tile_rows == nullptr: none)
     const int *tile_rows = nullptr, *tile_uniq = nullptr;
     const unsigned char *tile_loc = nullptr;

@@ -196,6 +196,8 @@ def test_kron_mfma_kernel(gpu, ncols, L, bif, sparse):
     dimy = [power] + dimx[1:]
     outs = []
     old_xl, old_yl = sb.tune_get("bsr.kron_xlds"), sb.tune_get("bsr.kron_ylds")
+    old_spin = sb.tune_get("bsr.kron_spin")
+    sb.tune_set("bsr.kron_spin", 0)  # the MFMA forms (the spin-first kernel: test_kron_spin_kernel)
     try:
         # packed column slots (8 and 12 columns: several rows per wave), one row per wave, no MFMA
         # (MFMA kernels, packed slots, x staging depth, y staged)
@@ -216,6 +218,7 @@ def test_kron_mfma_kernel(gpu, ncols, L, bif, sparse):
         sb.tune_set("bsr.kron_pack", 1)
         sb.tune_set("bsr.kron_xlds", old_xl)
         sb.tune_set("bsr.kron_ylds", old_yl)
+        sb.tune_set("bsr.kron_spin", old_spin)
         op.destroy()
     packed = 6 if ncols in (8, 12) else 5
     assert [o[0] for o in outs[:7]] == [packed] * 4 + [5] * 3 and outs[7][0] not in (5, 6)
@@ -266,3 +269,105 @@ def test_kron_fuzz(gpu, seed):
     out = ty.cpu().numpy().astype(np.complex128)
     assert np.array_equal(out, ref if cplx else ref.real.astype(np.complex128)), \
         (dtype, L, spin, color, ncols, bif, kind)
+
+
+def wilson_spin():
+    """1, 1 -+ gamma_mu (chiral basis): the bench's spin matrices (bench.py wilson_bench)"""
+    i_ = 1j
+    g = [np.array([[0, 0, 0, i_], [0, 0, i_, 0], [0, -i_, 0, 0], [-i_, 0, 0, 0]]),
+         np.array([[0, 0, 0, -1], [0, 0, 1, 0], [0, 1, 0, 0], [-1, 0, 0, 0]]),
+         np.array([[0, 0, i_, 0], [0, 0, 0, -i_], [-i_, 0, 0, 0], [0, i_, 0, 0]]),
+         np.array([[0, 0, 1, 0], [0, 0, 0, 1], [1, 0, 0, 0], [0, 1, 0, 0]])]
+    ks = [np.eye(4)]
+    for gm in g:
+        ks += [np.eye(4) - gm, np.eye(4) + gm]
+    return np.array(ks, np.complex128).ravel()
+
+
+@pytest.mark.parametrize("ncols,L", [(8, 4), (12, 4), (12, 3), (13, 3), (16, 5), (40, 2), (64, 4)])
+@pytest.mark.parametrize("bif,kind", [(False, "dense"), (True, "sparse"), (False, "wilson")])
+def test_kron_spin_kernel(gpu, ncols, L, bif, kind):
+    """complex<double> 3x3 x 4x4 from 8 rhs columns, spin first on the VALU (bsr_kron_spin_kernel:
+    a lane per (row, column) pair, so pairs run across row boundaries and the last wave is
+    ragged at every column count; zero / real-only / imaginary-only spin entries taken by scalar
+    branches; rows in the XCD order or not), complex alpha, beta, powers; integer data: exact,
+    the same bits with the XCD order off and the same values as the MFMA kernels."""
+    import torch
+    import superbblas_amd as sb
+    spin, color, power = 4, 3, 2
+    ii, jj, vals, kron = kron_lattice(L, spin, color, sparse_kron=kind == "sparse")
+    if kind == "wilson":
+        kron = wilson_spin()
+        if bif:
+            kron = kron.reshape(9, 4, 4).transpose(0, 2, 1).ravel().copy()
+    V = L ** 4
+    n = V * color * ncols * spin
+    g = np.arange(n)
+    x = ((g % 5 - 2) + 1j * (g % 3 - 1)).astype(np.complex128)
+    y0 = ((np.arange(n * power) % 7 - 3) + 1j).astype(np.complex128)
+    alpha, beta = 1 - 1j, 2.0
+    ref = reference(L, spin, color, ncols, vals, kron, jj, x, alpha, beta, y0, power, bif)
+    dim = [L, L, L, L, spin, color]
+    full = [([0] * 6, dim)]
+    blk, kr = [1, 1, 1, 1, 1, color], [1, 1, 1, 1, spin, 1]
+    op = sb.create_kron_bsr(full, dim, full, dim, blk, blk, kr, kr, bif,
+                            [torch.from_numpy(ii).to(gpu)], [torch.from_numpy(jj).to(gpu)],
+                            [torch.from_numpy(vals).to(gpu)], [torch.from_numpy(kron).to(gpu)])
+    dimx = [1, L, L, L, L, color, ncols, spin]
+    dimy = [power] + dimx[1:]
+    outs = []
+    try:
+        for spin_on, order in ((1, 1), (1, 0), (0, 1)):
+            sb.tune_set("bsr.kron_spin", spin_on)
+            sb.tune_set("bsr.kron_order", order)
+            ty = torch.from_numpy(y0.copy()).to(gpu)
+            sb.bsr_krylov(alpha, op, "xyztsc", "XYZTSC", [([0] * 8, dimx)], "pXYZTCnS", [0] * 8,
+                          dimx, dimx, [torch.from_numpy(x).to(gpu)], beta, [([0] * 8, dimy)],
+                          "pxyztcns", [0] * 8, dimy, dimy, "p", [ty])
+            torch.cuda.synchronize()
+            outs.append((sb.tune_get("bsr.last_kernel"), ty.cpu().numpy()))
+    finally:
+        sb.tune_set("bsr.kron_spin", 1)
+        sb.tune_set("bsr.kron_order", 1)
+        op.destroy()
+    assert outs[0][0] == 9 and outs[1][0] == 9 and outs[2][0] != 9
+    for form, out in outs:
+        assert np.array_equal(out, ref), form
+
+
+def test_kron_spin_random_values(gpu):
+    """random values (16^4 would be the bench; 6^4 here): the spin-first kernel within rounding
+    of the oracle and of the color-first MFMA kernel (the sums are associated differently)"""
+    import torch
+    import superbblas_amd as sb
+    L, spin, color, ncols = 6, 4, 3, 12
+    rng = np.random.default_rng(11)
+    ii, jj, _, _ = kron_lattice(L, spin, color)
+    V = L ** 4
+    vals = rng.standard_normal(V * 81) + 1j * rng.standard_normal(V * 81)
+    kron = wilson_spin()
+    x = rng.standard_normal(V * 12 * ncols) + 1j * rng.standard_normal(V * 12 * ncols)
+    ref = reference(L, spin, color, ncols, vals, kron, jj, x, 1.0, 0.0, np.zeros_like(x), 1)
+    dim = [L, L, L, L, spin, color]
+    full = [([0] * 6, dim)]
+    blk, kr = [1, 1, 1, 1, 1, color], [1, 1, 1, 1, spin, 1]
+    op = sb.create_kron_bsr(full, dim, full, dim, blk, blk, kr, kr, False,
+                            [torch.from_numpy(ii).to(gpu)], [torch.from_numpy(jj).to(gpu)],
+                            [torch.from_numpy(vals).to(gpu)], [torch.from_numpy(kron).to(gpu)])
+    dimx = [1, L, L, L, L, color, ncols, spin]
+    outs = []
+    try:
+        for on in (1, 0):
+            sb.tune_set("bsr.kron_spin", on)
+            ty = torch.zeros(V * 12 * ncols, dtype=torch.complex128, device=gpu)
+            sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", [([0] * 8, dimx)], "pXYZTCnS", [0] * 8,
+                          dimx, dimx, [torch.from_numpy(x).to(gpu)], 0.0, [([0] * 8, dimx)],
+                          "pxyztcns", [0] * 8, dimx, dimx, "p", [ty])
+            torch.cuda.synchronize()
+            outs.append(ty.cpu().numpy())
+    finally:
+        sb.tune_set("bsr.kron_spin", 1)
+        op.destroy()
+    scale = np.abs(ref).max()
+    for out in outs:
+        assert np.abs(out - ref).max() / scale < 1e-14

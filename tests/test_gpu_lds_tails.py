@@ -87,10 +87,12 @@ def test_12x12_tails(gpu, dtype, ncols, form):
     assert np.array_equal(ty.cpu().numpy(), yref)
 
 
-@pytest.mark.parametrize("ncols,form", [(8, 6), (12, 6), (16, 5), (20, 5)])
-def test_kron_tails(gpu, ncols, form):
-    """bsr_kron_mfma_packed_kernel (rw = 16 W / n rows per workgroup) and bsr_kron_mfma_kernel (4
-    (row, column group) tasks per workgroup) on a 3^4 lattice: 81 block rows"""
+@pytest.mark.parametrize("ncols,form,spin_first", [(8, 6, 0), (12, 6, 0), (16, 5, 0), (20, 5, 0),
+                                                    (8, 9, 1), (12, 9, 1), (20, 9, 1)])
+def test_kron_tails(gpu, ncols, form, spin_first):
+    """bsr_kron_mfma_packed_kernel (rw = 16 W / n rows per workgroup), bsr_kron_mfma_kernel (4
+    (row, column group) tasks per workgroup) and bsr_kron_spin_kernel (64 (row, column) pairs per
+    wave, rows in the XCD order) on a 3^4 lattice: 81 block rows"""
     import torch
     import superbblas_amd as sb
     rng = np.random.default_rng(ncols)
@@ -113,12 +115,16 @@ def test_kron_tails(gpu, ncols, form):
                             [torch.from_numpy(vals).to(gpu)], [torch.from_numpy(kron).to(gpu)])
     dimx = [1, L, L, L, L, color, ncols, spin]
     ty = torch.zeros(len(x), dtype=torch.complex128, device=gpu)
-    sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", [([0] * 8, dimx)], "pXYZTCnS", [0] * 8, dimx, dimx,
-                  [torch.from_numpy(x).to(gpu)], 0.0, [([0] * 8, dimx)], "pxyztcns", [0] * 8,
-                  dimx, dimx, "p", [ty])
-    torch.cuda.synchronize()
-    used = sb.tune_get("bsr.last_kernel")
-    op.destroy()
+    sb.tune_set("bsr.kron_spin", spin_first)
+    try:
+        sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", [([0] * 8, dimx)], "pXYZTCnS", [0] * 8, dimx,
+                      dimx, [torch.from_numpy(x).to(gpu)], 0.0, [([0] * 8, dimx)], "pxyztcns",
+                      [0] * 8, dimx, dimx, "p", [ty])
+        torch.cuda.synchronize()
+        used = sb.tune_get("bsr.last_kernel")
+    finally:
+        sb.tune_set("bsr.kron_spin", 1)
+        op.destroy()
     assert used == form, used
     assert np.array_equal(ty.cpu().numpy(), yref)
 
