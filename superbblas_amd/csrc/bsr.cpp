@@ -44,6 +44,7 @@ struct BsrComp {
                                      // the device copy of a host component's values)
     void *owned_kron = nullptr;      // device copy of a host component's Kronecker matrices
     int *kron_perm = nullptr;        // Kronecker operators: block rows in the XCD order
+    void *kron_terms = nullptr;      // ... the spin rows as two terms (build_kron_terms)
 };
 
 struct BsrOp {
@@ -70,6 +71,7 @@ struct BsrOp {
             if (c.owned_kron) (void)hipFree(c.owned_kron);
             if (c.tile_buf) (void)hipFree(c.tile_buf);
             if (c.kron_perm) (void)hipFree(c.kron_perm);
+            if (c.kron_terms) (void)hipFree(c.kron_terms);
         }
     }
 };
@@ -221,6 +223,40 @@ void build_kron_order(BsrComp &bc, const Coor &isize, const Coor &blocki, const 
     SBX_HIP_CHECK(hipMemcpy(bc.kron_perm, perm.data(), sizeof(int) * vol, hipMemcpyHostToDevice));
 }
 
+/// The 4x4 complex<double> spin matrices of a Kronecker operator with at most two nonzeros in
+/// every row, as a table for bsr_kron_spin_kernel: per matrix mu and row a, two (spin index,
+/// coefficient) terms (a row with one nonzero: the second coefficient zero; with none: both).
+/// Taken from the matrices at creation, as the reference analyses them there (kron_cpu, the
+/// density and the repeated matrices, bsr.h:690-717).  No table (the MFMA kernels run) when a row
+/// has more nonzeros.
+void build_kron_terms(BsrComp &bc, bool block_im_fast) {
+    const int nnz = bc.nnz_per_row;
+    if (nnz <= 0 || !bc.kron) return;
+    std::vector<double> k((std::size_t)nnz * 32);
+    SBX_HIP_CHECK(hipMemcpy(k.data(), bc.kron, k.size() * sizeof(double), hipMemcpyDefault));
+    std::vector<double> coef((std::size_t)nnz * 16, 0.0);
+    std::vector<int> bidx((std::size_t)nnz * 8, 0);
+    for (int mu = 0; mu < nnz; ++mu)
+        for (int a = 0; a < 4; ++a) {
+            int t = 0;
+            for (int b = 0; b < 4; ++b) {
+                const std::size_t e = (std::size_t)mu * 16 + (block_im_fast ? a + 4 * b : 4 * a + b);
+                const double re = k[2 * e], im = k[2 * e + 1];
+                if (re == 0 && im == 0) continue;
+                if (t == 2) return; // a third nonzero in the row
+                coef[mu * 16 + 4 * a + 2 * t] = re;
+                coef[mu * 16 + 4 * a + 2 * t + 1] = im;
+                bidx[mu * 8 + 2 * a + t] = b;
+                if (t == 0) bidx[mu * 8 + 2 * a + 1] = b;
+                ++t;
+            }
+        }
+    const std::size_t cb = coef.size() * sizeof(double), bb = bidx.size() * sizeof(int);
+    SBX_HIP_CHECK(hipMalloc(&bc.kron_terms, cb + bb));
+    SBX_HIP_CHECK(hipMemcpy(bc.kron_terms, coef.data(), cb, hipMemcpyHostToDevice));
+    SBX_HIP_CHECK(hipMemcpy((char *)bc.kron_terms + cb, bidx.data(), bb, hipMemcpyHostToDevice));
+}
+
 } // namespace
 
 BsrOp *bsr_create(int nd, int ni, int dtype, const std::vector<std::vector<Range>> &pi,
@@ -356,8 +392,11 @@ BsrOp *bsr_create(int nd, int ni, int dtype, const std::vector<std::vector<Range
         SBX_HIP_CHECK(hipMemcpy(bc.ii, rowptr.data(), sizeof(int) * (nii + 1), hipMemcpyHostToDevice));
         if (nnz > 0)
             SBX_HIP_CHECK(hipMemcpy(bc.jj, hjj.data(), sizeof(int) * nnz, hipMemcpyHostToDevice));
-        if (op->is_kron && volume(op->kroni) == 4 && bi == 3 && bd == 3 && dtype == SBX_CDOUBLE)
+        if (op->is_kron && volume(op->kroni) == 4 && volume(op->krond) == 4 && bi == 3 && bd == 3 &&
+            dtype == SBX_CDOUBLE) {
             build_kron_order(bc, ri.size, blocki, op->kroni);
+            build_kron_terms(bc, block_im_fast);
+        }
         if (!op->is_kron) {
             bc.h_rowptr = std::move(rowptr);
             bc.h_jj = std::move(hjj);
@@ -820,6 +859,7 @@ void bsr_krylov(const BsrOp &op, const Scalar &alpha, const std::string &oi,
                     d.kd = (int)volume(op.krond);
                     d.kron = bc.kron;
                     d.kron_perm = bc.kron_perm;
+                    d.kron_terms = bc.kron_terms;
                     launch_bsr_kron(d, bc.dev);
                 } else {
                     launch_bsr(d, bc.dev);

@@ -36,6 +36,7 @@ struct KronArgs {
     int ylds; ///< the XL kernels: y written through the wave's LDS ring in whole 64-B spin pieces
     long x_rows; ///< domain rows of x (sites * bd): the extent x's LDS-DMA buffer offsets address
     const int *perm; ///< the spin-first kernel: block row of each row slot (nullptr: the identity)
+    const void *ktab; ///< ... the spin matrices' rows as two terms (bsr.cpp build_kron_terms)
 };
 
 template <typename E, int BI, int BD, int KI, int KD>
@@ -674,23 +675,23 @@ __global__ void __launch_bounds__(256) bsr_kron_mfma_packed_kernel(const KronArg
 }
 
 
-// complex<double>, 3x3 color blocks, 4x4 spin matrices, from 8 rhs columns, spin first -- the
-// reference's order (contract_kron_cols applies K_mu to x, then bsrmm the color blocks,
-// bsr.h:933-998): a lane owns one (block row, rhs column) pair and its 12 outputs, so no lane idles
-// at any column count (pair p = row slot p / n, column p % n), and
-//   h(d, a) = sum_b K_mu(a, b) x(J_mu, d, col, b)    (VALU; the zero entries of K_mu skipped and
-//                                                    real / imaginary-only entries taken as such,
-//                                                    by scalar branches on its wave-uniform values)
-//   acc(i, a) += U_mu(i, d) h(d, a)
-// per step (mu, d).  The Wilson-type spin matrices (1 -+ gamma_mu: 8 of 16 entries, each +-1 or
-// +-i) cost 16 FMAs per step against the 4x4x4 MFMA form's 48 (and its 36 colour FMAs per spin
-// group of 16 columns become 48 per 64 columns); the K_mu values are read at run time as the
-// MFMA kernels do.  Per wave and step one LDS-DMA group, one step ahead: x of the 64 pairs (4
-// KB: 16 pairs' 4 spins a 1-KB piece, the pieces lane-linear over the pairs' 64-B spin runs; a
-// lane reads its spins back rotated by (b + p / 4) mod 4, conflict-free for ds_read_b128's lane
-// groups), U_mu(., d) of the wave's rows (<= 9 rows of 3 values, lanes < 32), and at d = 0 the
-// wave rows' block columns of the next neighbour (one dword per row).  Rows optionally visited in
-// the host's XCD order (perm: each XCD's share of slots a compact lattice box).
+// complex<double>, 3x3 color blocks, 4x4 spin matrices with at most two nonzeros per row (the
+// Wilson projectors 1 -+ gamma_mu, the identity, gamma matrices), from 8 rhs columns, spin first
+// -- the reference's order (contract_kron_cols applies K_mu to x, then bsrmm the color blocks,
+// bsr.h:933-998).  A lane owns one (block row, rhs column) pair and its 12 outputs, so no lane
+// idles at any column count (pair p = row slot p / n, column p % n); per step (mu, d):
+//   h(a) = c0 x(J_mu, d, col, b0) + c1 x(J_mu, d, col, b1)   (row a of K_mu as two terms: the
+//                                                           host's table, build_kron_terms)
+//   acc(i, a) += U_mu(i, d) h(a)
+// i.e. 32 + 48 FMAs a step, no branches; the MFMA form spends 48 FMA-equivalents of 4x4x4 MFMA
+// on the spin product of a dense K_mu and leaves a quarter of its lanes idle at 12 columns.
+// Per wave and step one LDS-DMA group, one step ahead: x of the 64 pairs (4 KB: 16 pairs' 4
+// spins a 1-KB piece, lane-linear over the pairs' 64-B spin runs, spin b of pair q at position
+// b ^ (q / 4 % 4): a read of one spin by 16 lanes hits distinct banks in each of
+// ds_read_b128's lane groups), U_mu(., d) of the wave's rows (<= 9 rows of 3 values, lanes <
+// 32), and at d = 0 the wave rows' block columns of the next neighbour (one dword per row).
+// Rows optionally visited in the host's XCD order (perm: each XCD's share of the row slots one
+// compact lattice box).
 constexpr int KS_WAVE_LDS = 2 * 4096 + 2 * 512 + 2 * 256;
 
 /// DMA of 16 (or 4: dword) bytes per lane into LDS at m0 = base (+ 16 or 4 per lane)
@@ -709,14 +710,6 @@ __device__ __forceinline__ void dma4(unsigned off, unsigned base, __amdgpu_buffe
                  :
                  : "v"(off), "s"(__builtin_amdgcn_readfirstlane(base)), "s"(r)
                  : "memory", "m0");
-}
-
-/// nonzero test of a wave-uniform double on its bits (scalar ALU; -0 counts as zero)
-__device__ __forceinline__ unsigned nz_bits(double v) {
-    const long long b = __double_as_longlong(v);
-    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b);
-    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32)) & 0x7fffffffu;
-    return (lo | hi) != 0 ? 1u : 0u;
 }
 
 __global__ void __launch_bounds__(256) bsr_kron_spin_kernel(const KronArgs p) {
@@ -748,7 +741,7 @@ __global__ void __launch_bounds__(256) bsr_kron_spin_kernel(const KronArgs p) {
     const E *xs = (const E *)wl;
     const E *us = (const E *)(wl + 8192);
     const int *js = (const int *)(wl + 9216);
-    // x DMA: instruction k, lane l -> pair q = 16 k + l / 4, spin (l % 4 - q / 4) mod 4; its
+    // x DMA: instruction k, lane l -> pair q = 16 k + l / 4, spin (l % 4) ^ (q / 4 % 4); its
     // (column * 4 + spin) in elements (-1: past the last pair) and wave row
     const int xd = 4 * n; // elements between the colors of a site
     int xcolb[4], xwr[4];
@@ -756,7 +749,7 @@ __global__ void __launch_bounds__(256) bsr_kron_spin_kernel(const KronArgs p) {
     for (int k = 0; k < 4; ++k) {
         const int q = 16 * k + (lane >> 2);
         const int pq = pw0 + q, pc = min(pq, total - 1);
-        const int b = ((lane & 3) - (q >> 2)) & 3;
+        const int b = (lane & 3) ^ ((q >> 2) & 3);
         const int sq = pc / n;
         xwr[k] = sq - slot_lo;
         xcolb[k] = pq < total ? (pc - sq * n) * 4 + b : -1;
@@ -780,40 +773,36 @@ __global__ void __launch_bounds__(256) bsr_kron_spin_kernel(const KronArgs p) {
     int jx[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) jx[k] = p.jj[row_of(slot_lo + xwr[k]) * nnz];
+    // (offsets past the buffers for the pieces without data: the DMA writes zeros; selects, not
+    // branches)
+    unsigned xbad = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) xbad |= (xcolb[k] < 0 ? 1u : 0u) << k;
+    const unsigned ubad = u_ok ? 0u : 0x80000000u, jbad = j_ok ? 0u : 0x80000000u;
     auto issue = [&](int mu, int d, int par) {
         const unsigned xb = wl_a + (unsigned)par * 4096u;
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            dma16(xcolb[k] >= 0 ? (unsigned)((jx[k] * 3 + d) * xd + xcolb[k]) * 16u : 0x80000000u,
-                  xb + (unsigned)k * 1024u, rx);
-        if (lane < 32)
-            dma16(u_ok ? (unsigned)(ubase + mu * 9 + d * ustep) * 16u : 0x80000000u,
-                  wl_a + 8192u + (unsigned)par * 512u, ru);
+        for (int k = 0; k < 4; ++k) {
+            const unsigned off = (unsigned)((jx[k] * 3 + d) * xd + xcolb[k]) * 16u;
+            dma16((xbad >> k & 1) ? 0x80000000u : off, xb + (unsigned)k * 1024u, rx);
+        }
+        if (lane < 32) dma16((unsigned)(ubase + mu * 9 + d * ustep) * 16u | ubad, wl_a + 8192u + (unsigned)par * 512u, ru);
         if (d == 0 && mu + 1 < nnz)
-            dma4(j_ok ? (unsigned)(jbase + mu + 1) * 4u : 0x80000000u,
-                 wl_a + 9216u + (unsigned)((mu + 1) & 1) * 256u, rj);
+            dma4((unsigned)(jbase + mu + 1) * 4u | jbad, wl_a + 9216u + (unsigned)((mu + 1) & 1) * 256u, rj);
     };
     double ar[3][4], ai[3][4];
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
         for (int a = 0; a < 4; ++a) ar[i][a] = 0, ai[i][a] = 0;
-    const int rot = lane >> 2;
-    const E *kron = (const E *)p.kron;
+    // spin b of the lane's pair sits at piece 4 lane + (b ^ (lane / 4 % 4)) of an x slot: byte
+    // address xa0 ^ 16 b
+    const unsigned xa0 = (unsigned)(64 * lane + 16 * ((lane >> 2) & 3));
+    const double *ctab = (const double *)p.ktab;          // [nnz][4 rows][2 terms] complex
+    const int *btab = (const int *)(ctab + 16L * nnz);    // [nnz][4 rows][2 terms] spin index
     issue(0, 0, 0);
 #pragma unroll 1
     for (int mu = 0; mu < nnz; ++mu) {
-        // the spin matrix's nonzero real / imaginary parts, bit 4 a + b (scalar)
-        const E *K = kron + mu * 16;
-        unsigned mr = 0, mi = 0;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            const E kv = Uniform<E>::load(K, p.block_im_fast ? (e >> 2) + 4 * (e & 3) : e);
-            mr |= nz_bits(kv.x) << e;
-            mi |= nz_bits(kv.y) << e;
-        }
-        mr = __builtin_amdgcn_readfirstlane(mr);
-        mi = __builtin_amdgcn_readfirstlane(mi);
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
             const int t = mu * 3 + d, par = t & 1;
@@ -833,38 +822,34 @@ __global__ void __launch_bounds__(256) bsr_kron_spin_kernel(const KronArgs p) {
             }
             // step t's group landed; step t + 1's (5 instructions, 6 with a J piece) may stay in flight
             if (!more) wait_vmcnt(0);
-            else if (d == 2 && mu + 2 < nnz) wait_vmcnt(6);
+            else if (d == 2 && mu + 2 < nnz) wait_vmcnt(6); // (mu + 1, 0) carries the J piece
             else wait_vmcnt(5);
-            const E *xp = xs + par * 256;
-            E xv[4];
-#pragma unroll
-            for (int b = 0; b < 4; ++b) xv[b] = xp[4 * lane + ((b + rot) & 3)];
+            const char *xp = (const char *)(xs + par * 256);
             const E *up = us + par * 32 + wr * 3;
             E uv[3];
 #pragma unroll
             for (int i = 0; i < 3; ++i) uv[i] = up[i];
 #pragma unroll
             for (int a = 0; a < 4; ++a) {
-                if (((mr | mi) >> (4 * a) & 15) == 0) continue; // a zero row of K_mu
-                double hr = 0, hi = 0;
-#pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    const int e = 4 * a + b;
-                    const int me = p.block_im_fast ? a + 4 * b : e;
-                    // (the empty asm keeps the compiler from turning the branches into selects)
-                    if (mr >> e & 1) {
-                        const double k = Uniform<E>::load(K, me).x;
-                        hr = __builtin_fma(k, xv[b].x, hr);
-                        hi = __builtin_fma(k, xv[b].y, hi);
-                        asm volatile("" : "+v"(hr), "+v"(hi));
-                    }
-                    if (mi >> e & 1) {
-                        const double k = Uniform<E>::load(K, me).y;
-                        hr = __builtin_fma(-k, xv[b].y, hr);
-                        hi = __builtin_fma(k, xv[b].x, hi);
-                        asm volatile("" : "+v"(hr), "+v"(hi));
-                    }
-                }
+                // (the compiler barrier keeps the scalar loads of the 12 rows of a neighbour from
+                // being hoisted together: 96 SGPRs, spilled)
+                asm volatile("" ::: "memory");
+                // h(a) = c0 x(b0) + c1 x(b1): the row's (at most) two nonzero spin entries
+                const int b0 = Uniform<int>::load(btab, mu * 8 + 2 * a);
+                const int b1 = Uniform<int>::load(btab, mu * 8 + 2 * a + 1);
+                const E x0 = *(const E *)(xp + (xa0 ^ (unsigned)(16 * b0)));
+                const E x1 = *(const E *)(xp + (xa0 ^ (unsigned)(16 * b1)));
+                const double c0r = Uniform<double>::load(ctab, mu * 16 + 4 * a);
+                const double c0i = Uniform<double>::load(ctab, mu * 16 + 4 * a + 1);
+                const double c1r = Uniform<double>::load(ctab, mu * 16 + 4 * a + 2);
+                const double c1i = Uniform<double>::load(ctab, mu * 16 + 4 * a + 3);
+                double hr = c0r * x0.x, hi = c0r * x0.y;
+                hr = __builtin_fma(-c0i, x0.y, hr);
+                hi = __builtin_fma(c0i, x0.x, hi);
+                hr = __builtin_fma(c1r, x1.x, hr);
+                hi = __builtin_fma(c1r, x1.y, hi);
+                hr = __builtin_fma(-c1i, x1.y, hr);
+                hi = __builtin_fma(c1i, x1.x, hi);
 #pragma unroll
                 for (int i = 0; i < 3; ++i) {
                     ar[i][a] = __builtin_fma(uv[i].x, hr, ar[i][a]);
@@ -873,6 +858,12 @@ __global__ void __launch_bounds__(256) bsr_kron_spin_kernel(const KronArgs p) {
                     ai[i][a] = __builtin_fma(uv[i].y, hr, ai[i][a]);
                 }
             }
+            // the step's products finish before the next step's waits and DMAs (otherwise the
+            // compiler overlaps the steps and holds two steps' x values: 167 VGPRs)
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+                asm volatile("" : "+v"(ar[i][0]), "+v"(ar[i][1]), "+v"(ar[i][2]), "+v"(ar[i][3]),
+                             "+v"(ai[i][0]), "+v"(ai[i][1]), "+v"(ai[i][2]), "+v"(ai[i][3]));
         }
     }
     if (!live) return;
@@ -893,7 +884,7 @@ template <typename E> void launch_kron_typed(const KronArgs &a, hipStream_t s) {
     KernelTimer timer("bsr", s);
     const long row_bytes = (long)a.nnz * (a.bi * a.bd * sizeof(E) + sizeof(int));
     if constexpr (std::is_same<E, double2>::value) {
-        if (g_bsr_tune.kron_spin && a.bi == 3 && a.bd == 3 && a.ki == 4 && a.kd == 4 && a.nnz >= 1 &&
+        if (g_bsr_tune.kron_spin && a.ktab && a.bi == 3 && a.bd == 3 && a.ki == 4 && a.kd == 4 && a.nnz >= 1 &&
             a.nnz <= 64 && a.ncols >= std::max(8L, g_bsr_tune.kron_spin_min_cols) &&
             a.block_rows * a.nnz * 9 * 16 < (1L << 31) && a.x_rows * 4 * a.ncols * 16 < (1L << 31) &&
             a.block_rows * a.ncols + 1024 < (1L << 31)) {
@@ -1020,6 +1011,7 @@ void launch_bsr_kron(const BsrDesc &d, int device) {
     // bounded by x's extent, not y's
     a.x_rows = d.x_rows > 0 ? d.x_rows : d.block_rows * d.bd;
     a.perm = g_bsr_tune.kron_order ? d.kron_perm : nullptr;
+    a.ktab = d.kron_terms;
     switch (d.t) {
     case SBX_CDOUBLE: return launch_kron_typed<double2>(a, s);
     case SBX_CFLOAT: return launch_kron_typed<float2>(a, s);

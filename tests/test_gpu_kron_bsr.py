@@ -197,7 +197,7 @@ def test_kron_mfma_kernel(gpu, ncols, L, bif, sparse):
     outs = []
     old_xl, old_yl = sb.tune_get("bsr.kron_xlds"), sb.tune_get("bsr.kron_ylds")
     old_spin = sb.tune_get("bsr.kron_spin")
-    sb.tune_set("bsr.kron_spin", 0)  # the MFMA forms (the spin-first kernel: test_kron_spin_kernel)
+    sb.tune_set("bsr.kron_spin", 0)  # the MFMA forms (the opt-in spin-first kernel: test_kron_spin_kernel)
     try:
         # packed column slots (8 and 12 columns: several rows per wave), one row per wave, no MFMA
         # (MFMA kernels, packed slots, x staging depth, y staged)
@@ -285,21 +285,29 @@ def wilson_spin():
 
 
 @pytest.mark.parametrize("ncols,L", [(8, 4), (12, 4), (12, 3), (13, 3), (16, 5), (40, 2), (64, 4)])
-@pytest.mark.parametrize("bif,kind", [(False, "dense"), (True, "sparse"), (False, "wilson")])
+@pytest.mark.parametrize("bif,kind", [(False, "dense"), (True, "sparse"), (False, "wilson"),
+                                      (True, "wilson"), (False, "thin")])
 def test_kron_spin_kernel(gpu, ncols, L, bif, kind):
     """complex<double> 3x3 x 4x4 from 8 rhs columns, spin first on the VALU (bsr_kron_spin_kernel:
     a lane per (row, column) pair, so pairs run across row boundaries and the last wave is
-    ragged at every column count; zero / real-only / imaginary-only spin entries taken by scalar
-    branches; rows in the XCD order or not), complex alpha, beta, powers; integer data: exact,
-    the same bits with the XCD order off and the same values as the MFMA kernels."""
+    ragged at every column count; every spin row as two terms from the operator's table; rows
+    in the XCD order or not) when no spin row has more than two nonzeros (sparse: two per row;
+    Wilson projectors; thin: rows with one nonzero and zero rows), the MFMA kernels otherwise
+    (dense); complex alpha, beta, powers; integer data: exact, the same bits with the XCD order
+    off and the same values as the MFMA kernels."""
     import torch
     import superbblas_amd as sb
     spin, color, power = 4, 3, 2
     ii, jj, vals, kron = kron_lattice(L, spin, color, sparse_kron=kind == "sparse")
     if kind == "wilson":
         kron = wilson_spin()
-        if bif:
-            kron = kron.reshape(9, 4, 4).transpose(0, 2, 1).ravel().copy()
+    if kind == "thin":
+        kron = kron.reshape(9, 4, 4).copy()
+        kron[:, :, 1:] = 0           # one nonzero per row
+        kron[::2, 2, :] = 0          # and zero rows
+        kron = kron.ravel()
+    if bif and kind == "wilson":
+        kron = kron.reshape(9, 4, 4).transpose(0, 2, 1).ravel().copy()
     V = L ** 4
     n = V * color * ncols * spin
     g = np.arange(n)
@@ -327,10 +335,11 @@ def test_kron_spin_kernel(gpu, ncols, L, bif, kind):
             torch.cuda.synchronize()
             outs.append((sb.tune_get("bsr.last_kernel"), ty.cpu().numpy()))
     finally:
-        sb.tune_set("bsr.kron_spin", 1)
+        sb.tune_set("bsr.kron_spin", 0)
         sb.tune_set("bsr.kron_order", 1)
         op.destroy()
-    assert outs[0][0] == 9 and outs[1][0] == 9 and outs[2][0] != 9
+    spin_form = 9 if kind != "dense" else outs[2][0]
+    assert outs[0][0] == spin_form and outs[1][0] == spin_form and outs[2][0] != 9
     for form, out in outs:
         assert np.array_equal(out, ref), form
 
@@ -366,7 +375,7 @@ def test_kron_spin_random_values(gpu):
             torch.cuda.synchronize()
             outs.append(ty.cpu().numpy())
     finally:
-        sb.tune_set("bsr.kron_spin", 1)
+        sb.tune_set("bsr.kron_spin", 0)
         op.destroy()
     scale = np.abs(ref).max()
     for out in outs:

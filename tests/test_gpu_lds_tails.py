@@ -103,6 +103,10 @@ def test_kron_tails(gpu, ncols, form, spin_first):
     ii = np.full(V, 9, np.int32)
     vals = _ints(rng, V * 9 * color * color, np.complex128)
     kron = _ints(rng, 9 * spin * spin, np.complex128)
+    if spin_first:  # two nonzeros per spin row (the spin-first kernel's shape)
+        kron = kron.reshape(9, 4, 4)
+        kron[:, :, 1:3] = 0
+        kron = kron.ravel().copy()
     x = _ints(rng, V * color * ncols * spin, np.complex128)
     yref = np.zeros_like(x)
     oracle_kron_bsr(T_CDOUBLE, [L, L, L, L, 1, 1], 0, V, 9, color, color, spin, spin, jj, vals,
@@ -123,7 +127,7 @@ def test_kron_tails(gpu, ncols, form, spin_first):
         torch.cuda.synchronize()
         used = sb.tune_get("bsr.last_kernel")
     finally:
-        sb.tune_set("bsr.kron_spin", 1)
+        sb.tune_set("bsr.kron_spin", 0)
         op.destroy()
     assert used == form, used
     assert np.array_equal(ty.cpu().numpy(), yref)

@@ -45,7 +45,7 @@ def main():
     blk, kr = [1, 1, 1, 1, 1, 3], [1, 1, 1, 1, 4, 1]
     ks = spin_matrices()
     for kind in kinds:
-        jj, nnz = columns(kind, L)
+        jj, nnz = columns(kind, (L, L, L, L))
         kron = torch.from_numpy(ks[:nnz].reshape(-1)).to(dev)
         cvals = torch.randn(V * nnz * 9, dtype=torch.complex128, device=dev)
         op = sb.create_kron_bsr(full, dim, full, dim, blk, blk, kr, kr, False,

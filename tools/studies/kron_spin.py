@@ -37,7 +37,7 @@ def main():
     ks = spin_matrices()
     g = torch.Generator(device=dev).manual_seed(7)
     for kind in kinds:
-        jj, nnz = columns(kind, L)
+        jj, nnz = columns(kind, (L, L, L, L))
         kron = torch.from_numpy(ks[:nnz].reshape(-1)).to(dev)
         cvals = torch.randn(V * nnz * 9, dtype=torch.complex128, device=dev, generator=g)
         op = sb.create_kron_bsr(full, dim, full, dim, blk, blk, kr, kr, False,
@@ -72,7 +72,7 @@ def main():
                     times[v].append(ms / calls / 1e3)
                     forms[v] = sb.tune_get("bsr.last_kernel")
                     outs[v] = y.clone()
-            sb.tune_set("bsr.kron_spin", 1)
+            sb.tune_set("bsr.kron_spin", 0)
             sb.tune_set("bsr.kron_order", 1)
             algo = 16.0 * (81 * V + 2 * 12 * V * n) + 4.0 * 9 * V  # the stencil's
             base = outs[variants[0]]
