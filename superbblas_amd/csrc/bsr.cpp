@@ -45,6 +45,7 @@ struct BsrComp {
     void *owned_kron = nullptr;      // device copy of a host component's Kronecker matrices
     int *kron_perm = nullptr;        // Kronecker operators: block rows in the XCD order
     void *kron_terms = nullptr;      // ... the spin rows as two terms (build_kron_terms)
+    void *kron_xor = nullptr;        // ... as diagonal + XOR partner (build_kron_terms)
 };
 
 struct BsrOp {
@@ -72,6 +73,7 @@ struct BsrOp {
             if (c.tile_buf) (void)hipFree(c.tile_buf);
             if (c.kron_perm) (void)hipFree(c.kron_perm);
             if (c.kron_terms) (void)hipFree(c.kron_terms);
+            if (c.kron_xor) (void)hipFree(c.kron_xor);
         }
     }
 };
@@ -255,6 +257,44 @@ void build_kron_terms(BsrComp &bc, bool block_im_fast) {
     SBX_HIP_CHECK(hipMalloc(&bc.kron_terms, cb + bb));
     SBX_HIP_CHECK(hipMemcpy(bc.kron_terms, coef.data(), cb, hipMemcpyHostToDevice));
     SBX_HIP_CHECK(hipMemcpy((char *)bc.kron_terms + cb, bidx.data(), bb, hipMemcpyHostToDevice));
+    // the diagonal + XOR-partner form (bsr_kron_xor_kernel): row a nonzero at most at spins a and
+    // a ^ s_mu, one s_mu per matrix; c0 the diagonal entry, c1 the partner's
+    std::vector<double> xc((std::size_t)nnz * 16, 0.0);
+    std::vector<int> xs(nnz, 0);
+    for (int mu = 0; mu < nnz; ++mu) {
+        auto at = [&](int a, int b) {
+            const std::size_t e = (std::size_t)mu * 16 + (block_im_fast ? a + 4 * b : 4 * a + b);
+            return std::make_pair(k[2 * e], k[2 * e + 1]);
+        };
+        int sm = 0;
+        for (int a = 0; a < 4 && sm == 0; ++a)
+            for (int b = 0; b < 4; ++b) {
+                const auto v = at(a, b);
+                if (b != a && (v.first != 0 || v.second != 0)) {
+                    sm = a ^ b;
+                    break;
+                }
+            }
+        for (int a = 0; a < 4; ++a)
+            for (int b = 0; b < 4; ++b) {
+                const auto v = at(a, b);
+                if (v.first == 0 && v.second == 0) continue;
+                if (b == a) {
+                    xc[mu * 16 + 4 * a] = v.first;
+                    xc[mu * 16 + 4 * a + 1] = v.second;
+                } else if (b == (a ^ sm)) {
+                    xc[mu * 16 + 4 * a + 2] = v.first;
+                    xc[mu * 16 + 4 * a + 3] = v.second;
+                } else {
+                    return; // not of that form
+                }
+            }
+        xs[mu] = sm;
+    }
+    const std::size_t xcb = xc.size() * sizeof(double), xsb = xs.size() * sizeof(int);
+    SBX_HIP_CHECK(hipMalloc(&bc.kron_xor, xcb + xsb));
+    SBX_HIP_CHECK(hipMemcpy(bc.kron_xor, xc.data(), xcb, hipMemcpyHostToDevice));
+    SBX_HIP_CHECK(hipMemcpy((char *)bc.kron_xor + xcb, xs.data(), xsb, hipMemcpyHostToDevice));
 }
 
 } // namespace
@@ -860,6 +900,7 @@ void bsr_krylov(const BsrOp &op, const Scalar &alpha, const std::string &oi,
                     d.kron = bc.kron;
                     d.kron_perm = bc.kron_perm;
                     d.kron_terms = bc.kron_terms;
+                    d.kron_xor = bc.kron_xor;
                     launch_bsr_kron(d, bc.dev);
                 } else {
                     launch_bsr(d, bc.dev);

@@ -37,6 +37,7 @@ struct KronArgs {
     long x_rows; ///< domain rows of x (sites * bd): the extent x's LDS-DMA buffer offsets address
     const int *perm; ///< the spin-first kernel: block row of each row slot (nullptr: the identity)
     const void *ktab; ///< ... the spin matrices' rows as two terms (bsr.cpp build_kron_terms)
+    const void *xtab; ///< ... as diagonal + XOR partner (nullptr: not of that form)
 };
 
 template <typename E, int BI, int BD, int KI, int KD>
@@ -878,13 +879,150 @@ __global__ void __launch_bounds__(256) bsr_kron_spin_kernel(const KronArgs p) {
         }
 }
 
+
+// The same spin-first product with the spin rows in "diagonal + XOR partner" form (every row a of
+// K_mu nonzero at most at spins a and a ^ s_mu: the Wilson projectors 1 -+ gamma_mu and the gamma
+// matrices in the chiral, Dirac-Pauli and DeGrand-Rossi bases), so that a lane keeps its pair's
+// 4 spins in registers and the partner is a compile-time register (one instantiation of the
+// step per s, chosen per neighbour by a scalar switch):
+//   h(a) = c0(a) x(a) + c1(a) x(a ^ s)                  (the host's table, build_kron_terms)
+//   acc(i, a) += U_mu(i, d) h(a)
+// and everything comes by plain vector loads one step ahead (a pair's x: 64 contiguous bytes per
+// lane and color; U_mu(., d) of its row; J_mu one neighbour ahead) -- no LDS and no LDS-DMA,
+// whose issue cost (about 60 cycles a piece, MI355X_MICROARCH.md) set the first form's time.
+/// h(a) = c0(a) x(a) + c1(a) x(a ^ S), the coefficients from the table by scalar loads
+template <int S>
+__device__ __forceinline__ void kron_xor_h(const double2 (&x)[4], const double *c, double (&hr)[4], double (&hi)[4]) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+        const double c0r = Uniform<double>::load(c, 4 * a), c0i = Uniform<double>::load(c, 4 * a + 1);
+        const double2 x0 = x[a], x1 = x[a ^ S];
+        hr[a] = c0r * x0.x;
+        hi[a] = c0r * x0.y;
+        hr[a] = __builtin_fma(-c0i, x0.y, hr[a]);
+        hi[a] = __builtin_fma(c0i, x0.x, hi[a]);
+        if (S != 0) {
+            const double c1r = Uniform<double>::load(c, 4 * a + 2), c1i = Uniform<double>::load(c, 4 * a + 3);
+            hr[a] = __builtin_fma(c1r, x1.x, hr[a]);
+            hi[a] = __builtin_fma(c1r, x1.y, hi[a]);
+            hr[a] = __builtin_fma(-c1i, x1.y, hr[a]);
+            hi[a] = __builtin_fma(c1i, x1.x, hi[a]);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) bsr_kron_xor_kernel(const KronArgs p) {
+    typedef double2 E;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int bid = blockIdx.x, nwg = gridDim.x;
+    const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int wgi = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    // (launcher: pairs, x and values below 2^31 elements)
+    const int n = (int)p.ncols, nnz = p.nnz;
+    const int total = (int)(p.block_rows * n);
+    const int pw0 = (wgi * 4 + w) * 64;
+    if (pw0 >= total) return;
+    const int pp = min(pw0 + lane, total - 1);
+    const bool live = pw0 + lane < total;
+    const int slot = pp / n, col = pp - slot * n;
+    const int row = p.perm ? p.perm[slot] : slot;
+    const E *x = (const E *)p.x, *v = (const E *)p.v;
+    const int *jrow = p.jj + (long)row * nnz;
+    const E *urow = v + (long)row * nnz * 9;
+    const int xd = 4 * n; // elements between the colors of a site
+    const int ust = p.block_im_fast ? 3 : 1, uis = p.block_im_fast ? 1 : 3;
+    // the table: [nnz] { c[4 rows][c0 re, c0 im, c1 re, c1 im] } then [nnz] s
+    const double *ctab = (const double *)p.ktab;
+    const int *stab = (const int *)(ctab + 16L * nnz);
+    double ar[3][4], ai[3][4];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int a = 0; a < 4; ++a) ar[i][a] = 0, ai[i][a] = 0;
+    E xv[4], uv[3], xn[4], un[3];
+    auto load = [&](int J, int mu, int d, E (&xo)[4], E (&uo)[3]) {
+        const E *xp = x + (long)(J * 3 + d) * xd + col * 4;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) xo[b] = xp[b];
+        const E *up = urow + mu * 9 + d * ust;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) uo[i] = up[i * uis];
+    };
+    int J = jrow[0];
+    load(J, 0, 0, xv, uv);
+#pragma unroll 1
+    for (int mu = 0; mu < nnz; ++mu) {
+        const int Jn = mu + 1 < nnz ? jrow[mu + 1] : J;
+        const int sm = Uniform<int>::load(stab, mu);
+        const double *c = ctab + mu * 16;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            // the next step's operands (the last step reloads its own: harmless)
+            if (d < 2) load(J, mu, d + 1, xn, un);
+            else load(Jn, mu + 1 < nnz ? mu + 1 : mu, 0, xn, un);
+            // spin: one instantiation per partner (only h crosses the branches)
+            double hr[4], hi[4];
+            switch (sm) {
+            case 0: kron_xor_h<0>(xv, c, hr, hi); break;
+            case 1: kron_xor_h<1>(xv, c, hr, hi); break;
+            case 2: kron_xor_h<2>(xv, c, hr, hi); break;
+            default: kron_xor_h<3>(xv, c, hr, hi); break;
+            }
+            // color
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    ar[i][a] = __builtin_fma(uv[i].x, hr[a], ar[i][a]);
+                    ar[i][a] = __builtin_fma(-uv[i].y, hi[a], ar[i][a]);
+                    ai[i][a] = __builtin_fma(uv[i].x, hi[a], ai[i][a]);
+                    ai[i][a] = __builtin_fma(uv[i].y, hr[a], ai[i][a]);
+                }
+            // the step's products finish before the next step's loads are issued
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+                asm volatile("" : "+v"(ar[i][0]), "+v"(ar[i][1]), "+v"(ar[i][2]), "+v"(ar[i][3]),
+                             "+v"(ai[i][0]), "+v"(ai[i][1]), "+v"(ai[i][2]), "+v"(ai[i][3])::"memory");
+#pragma unroll
+            for (int b = 0; b < 4; ++b) xv[b] = xn[b];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) uv[i] = un[i];
+        }
+        J = Jn;
+    }
+    if (!live) return;
+    E *yp = (E *)p.y + ((long)row * 3 * n + col) * 4;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            E o = Ops<E>::scale(E{ar[i][a], ai[i][a]}, p.alpha_re, p.alpha_im);
+            if (p.add) o = Ops<E>::add(o, yp[(long)i * n * 4 + a]);
+            yp[(long)i * n * 4 + a] = o;
+        }
+}
+
 constexpr long KRON_LDS_BYTES = 64 * 1024;
 
 template <typename E> void launch_kron_typed(const KronArgs &a, hipStream_t s) {
     KernelTimer timer("bsr", s);
     const long row_bytes = (long)a.nnz * (a.bi * a.bd * sizeof(E) + sizeof(int));
     if constexpr (std::is_same<E, double2>::value) {
-        if (g_bsr_tune.kron_spin && a.ktab && a.bi == 3 && a.bd == 3 && a.ki == 4 && a.kd == 4 && a.nnz >= 1 &&
+        if (g_bsr_tune.kron_spin == 2 && a.xtab && a.bi == 3 && a.bd == 3 && a.ki == 4 && a.kd == 4 &&
+            a.nnz >= 1 && a.ncols >= g_bsr_tune.kron_spin_min_cols && a.x_rows * 4 * a.ncols < (1L << 31) &&
+            a.block_rows * a.ncols + 1024 < (1L << 31)) {
+            const long waves = (a.block_rows * a.ncols + 63) / 64, blocks = (waves + 3) / 4;
+            if (blocks < (1L << 31)) {
+                g_bsr_tune.last = 12;
+                KronArgs b = a;
+                b.ktab = a.xtab;
+                hipLaunchKernelGGL(bsr_kron_xor_kernel, dim3((unsigned)blocks), dim3(256), 0, s, b);
+                SBX_HIP_CHECK(hipGetLastError());
+                return;
+            }
+        }
+        if (g_bsr_tune.kron_spin == 1 && a.ktab && a.bi == 3 && a.bd == 3 && a.ki == 4 && a.kd == 4 && a.nnz >= 1 &&
             a.nnz <= 64 && a.ncols >= std::max(8L, g_bsr_tune.kron_spin_min_cols) &&
             a.block_rows * a.nnz * 9 * 16 < (1L << 31) && a.x_rows * 4 * a.ncols * 16 < (1L << 31) &&
             a.block_rows * a.ncols + 1024 < (1L << 31)) {
@@ -1012,6 +1150,7 @@ void launch_bsr_kron(const BsrDesc &d, int device) {
     a.x_rows = d.x_rows > 0 ? d.x_rows : d.block_rows * d.bd;
     a.perm = g_bsr_tune.kron_order ? d.kron_perm : nullptr;
     a.ktab = d.kron_terms;
+    a.xtab = d.kron_xor;
     switch (d.t) {
     case SBX_CDOUBLE: return launch_kron_typed<double2>(a, s);
     case SBX_CFLOAT: return launch_kron_typed<float2>(a, s);

@@ -269,9 +269,10 @@ struct BsrTune {
     int kron_xlds = 1;           ///< ... x staged by LDS-DMA, a column's 4 spins as one 64-B piece, this many
                                  ///< neighbours ahead (0 = off: per-lane loads one ahead; 1..3)
     int kron_ylds = 0;           ///< ... with x staged: y written through the same ring in whole pieces
-    int kron_spin = 0;           ///< ... spin first on the VALU, a lane per (row, column) (bsr_kron_spin_kernel,
-                                 ///< spin rows of at most two nonzeros; opt-in: n = 12 181 vs 146 us for the
-                                 ///< MFMA form -- FP64 VALU FMAs issue at 8 cycles)
+    int kron_spin = 0;           ///< ... spin first on the VALU, a lane per (row, column): 1 bsr_kron_spin_kernel
+                                 ///< (spin rows of at most two nonzeros, operands by LDS-DMA), 2 bsr_kron_xor_kernel
+                                 ///< (diagonal + XOR-partner spin rows, plain loads); 0 = the MFMA forms (the
+                                 ///< default: n = 12 142 us against 180 / 190)
     long kron_spin_min_cols = 8; ///< ... from this many rhs columns (at least 8)
     int kron_order = 1;          ///< ... rows in the operator's XCD order (bsr.cpp build_kron_order)
     int blk_pd = 1; ///< 12x12 blocks by LDS-DMA: blocks in flight ahead of the one in use (1..3)
@@ -289,7 +290,7 @@ struct BsrTune {
     /// 4 site tiles (3x3),
     /// 5 Kronecker on MFMA, 6 the same with packed column slots, 7 12x12 blocks by LDS-DMA, 8 the
     /// same with packed slots, 9 Kronecker spin first (VALU), 10 12x12 fragment gathers (9 blocks
-    /// per row), 11 12x12 generic rows,
+    /// per row), 11 12x12 generic rows, 12 Kronecker spin first with XOR-partner spin rows,
     /// 0 another kernel
     std::atomic<int> last{0};
 };
@@ -355,6 +356,7 @@ struct BsrDesc {
     const void *kron = nullptr; ///< num_nnz_per_row matrices of ki x kd
     const int *kron_perm = nullptr; ///< block row per row slot in the XCD order (nullptr: none)
     const void *kron_terms = nullptr; ///< spin rows as two terms (nullptr: a row has more nonzeros)
+    const void *kron_xor = nullptr;   ///< spin rows as diagonal + XOR partner (nullptr: not of that form)
     // site tiles of 3x3 9-point operators (bsr.cpp build_tile_schedule; tile_rows == nullptr: none)
     const int *tile_rows = nullptr, *tile_uniq = nullptr;
     const unsigned char *tile_loc = nullptr;

@@ -325,7 +325,7 @@ def test_kron_spin_kernel(gpu, ncols, L, bif, kind):
     dimy = [power] + dimx[1:]
     outs = []
     try:
-        for spin_on, order in ((1, 1), (1, 0), (0, 1)):
+        for spin_on, order in ((1, 1), (1, 0), (0, 1), (2, 1), (2, 0)):
             sb.tune_set("bsr.kron_spin", spin_on)
             sb.tune_set("bsr.kron_order", order)
             ty = torch.from_numpy(y0.copy()).to(gpu)
@@ -339,7 +339,9 @@ def test_kron_spin_kernel(gpu, ncols, L, bif, kind):
         sb.tune_set("bsr.kron_order", 1)
         op.destroy()
     spin_form = 9 if kind != "dense" else outs[2][0]
-    assert outs[0][0] == spin_form and outs[1][0] == spin_form and outs[2][0] != 9
+    xor_form = 12 if kind == "wilson" else outs[2][0]  # (diagonal + XOR partner: Wilson only)
+    assert outs[0][0] == spin_form and outs[1][0] == spin_form and outs[2][0] not in (9, 12)
+    assert outs[3][0] == xor_form and outs[4][0] == xor_form
     for form, out in outs:
         assert np.array_equal(out, ref), form
 
@@ -366,7 +368,7 @@ def test_kron_spin_random_values(gpu):
     dimx = [1, L, L, L, L, color, ncols, spin]
     outs = []
     try:
-        for on in (1, 0):
+        for on in (1, 0, 2):
             sb.tune_set("bsr.kron_spin", on)
             ty = torch.zeros(V * 12 * ncols, dtype=torch.complex128, device=gpu)
             sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", [([0] * 8, dimx)], "pXYZTCnS", [0] * 8,

@@ -28,7 +28,7 @@ def main():
     kinds = os.environ.get("KINDS", "stencil").split(",")
     ncols_list = [int(v) for v in os.environ.get("NCOLS", "12").split(",")]
     variants = [tuple(int(x) for x in v.split(":"))
-                for v in os.environ.get("VARIANTS", "1:1,1:0,0:1").split(",")]
+                for v in os.environ.get("VARIANTS", "2:1,2:0,1:1,0:1").split(",")]
     rounds = int(os.environ.get("ROUNDS", "3"))
     dims = [L, L, L, L]
     dim = dims + [4, 3]
