@@ -14,6 +14,8 @@
 #include "elem_ops.h"
 #include "sbx_internal.h"
 
+#include <type_traits>
+
 #include <algorithm>
 
 namespace sbx {
@@ -306,8 +308,10 @@ template <int N> struct Col<float2, N> : CCol<float2, float, N> {};
 
 // A wave holds G = 64 / n matrices: lane l = n s + c is column c of slot s (lanes past G n
 // idle); slots past the batch hold the identity and write nothing.
-template <typename E, int WNM>
-__global__ void __launch_bounds__(256) potrf_wave_kernel(E *a, int n, long k, int *info, int rm) {
+template <typename E, int WNM, bool FULL = false>
+__global__ void __launch_bounds__(256) potrf_wave_kernel(E *a, int n_, long k, int *info, int rm) {
+    const int n = FULL ? WNM : n_; // (FULL: a compile-time size, no conditional steps; the
+                                   // solve kernels spill in that form, so only potrf / inversion)
     typedef DOps<E> O;
     const int lane = threadIdx.x & 63, G = 64 / n;
     const int s = lane / n, c = lane - s * n, s0 = s * n;
@@ -499,6 +503,33 @@ template <int L> __device__ __forceinline__ float2 rbc(float2 v) { return float2
 // pivot column is replaced by the inverse's column as it is eliminated, and the row swaps are
 // undone on the columns at the end (one shuffle per element).  getrf + getri in one pass over
 // registers: n^3 complex multiply-adds per matrix, the matrix read and written once.
+/// One Gauss-Jordan elimination update of a complex<double> element on every lane:
+///   (re, im) = (x, y) s - (x, y)[lane L of the 16-lane row] * (ar, ai)
+/// the broadcast folded into the FP64 FMAs as their DPP row_newbcast operand (the separate 32-bit
+/// broadcast moves cost 4 VALU instructions per element, the selects of lane L's column 4 more);
+/// the two multiplies come first, so the DPP reads of x and y are 2 instructions after any write
+template <int L>
+__device__ __forceinline__ void gj_update(double x, double y, double s, double ar, double ai, double &re, double &im) {
+    const double nar = -ar, nai = -ai;
+    asm volatile("v_mul_f64 %0, %2, %4\n\t"
+                 "v_mul_f64 %1, %3, %4\n\t"
+                 "v_fmac_f64_dpp %0, %2, %5 row_newbcast:%8 row_mask:0xf bank_mask:0xf\n\t"
+                 "v_fmac_f64_dpp %0, %3, %6 row_newbcast:%8 row_mask:0xf bank_mask:0xf\n\t"
+                 "v_fmac_f64_dpp %1, %2, %7 row_newbcast:%8 row_mask:0xf bank_mask:0xf\n\t"
+                 "v_fmac_f64_dpp %1, %3, %5 row_newbcast:%8 row_mask:0xf bank_mask:0xf"
+                 : "=&v"(re), "=&v"(im)
+                 : "v"(x), "v"(y), "v"(s), "v"(nar), "v"(ai), "v"(nai), "i"(L));
+}
+/// the real form: re = x s - x[lane L] * ar
+template <int L> __device__ __forceinline__ void gj_update(double x, double s, double ar, double &re) {
+    const double nar = -ar;
+    asm volatile("v_mul_f64 %0, %1, %2\n\t"
+                 "s_nop 0\n\t"
+                 "v_fmac_f64_dpp %0, %1, %3 row_newbcast:%4 row_mask:0xf bank_mask:0xf"
+                 : "=&v"(re)
+                 : "v"(x), "v"(s), "v"(nar), "i"(L));
+}
+
 template <typename E, int WNM, int J>
 __device__ __forceinline__ void gj_step(Col<E, WNM> &v, int n, int c, int &bad, int (&pj)[WNM]) {
     typedef DOps<E> O;
@@ -535,11 +566,31 @@ __device__ __forceinline__ void gj_step(Col<E, WNM> &v, int n, int c, int &bad, 
             // singular matrix -- !ok -- goes on with infinities: its lanes are its own and its
             // result is not written.)
             const E aj = O::mul(c == J ? O::one() : v.get(J), dinv);
+            if constexpr (std::is_same<E, double2>::value || std::is_same<E, double>::value) {
+                // v(r) <- v(r) s - v(r)[lane J] aj with s = 0 on lane J (its column becomes the
+                // inverse's) and 1 elsewhere: a multiply and DPP-broadcast FMAs, no selects
+                const double sc = c == J ? 0.0 : 1.0;
 #pragma unroll
-            for (int r = 0; r < WNM; ++r) {
-                if (r >= n || r == J) continue;
-                const E mr = rbc<J>(v.get(r));
-                v.set(r, O::sub(c == J ? O::real(0) : v.get(r), O::mul(mr, aj)));
+                for (int r = 0; r < WNM; ++r) {
+                    if (r >= n || r == J) continue;
+                    const E vr = v.get(r);
+                    if constexpr (std::is_same<E, double2>::value) {
+                        double re, im;
+                        gj_update<J>(vr.x, vr.y, sc, aj.x, aj.y, re, im);
+                        v.set(r, double2{re, im});
+                    } else {
+                        double re;
+                        gj_update<J>(vr, sc, aj, re);
+                        v.set(r, re);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < WNM; ++r) {
+                    if (r >= n || r == J) continue;
+                    const E mr = rbc<J>(v.get(r));
+                    v.set(r, O::sub(c == J ? O::real(0) : v.get(r), O::mul(mr, aj)));
+                }
             }
             v.set(J, aj);
         }
@@ -547,9 +598,12 @@ __device__ __forceinline__ void gj_step(Col<E, WNM> &v, int n, int c, int &bad, 
     }
 }
 
-template <typename E, int WNM>
-__global__ void __launch_bounds__(256) inv_wave_kernel(const E *a, int n, long k, E *b, int *info, int rm) {
+// FULL: n == WNM (4, 8, 12, 16): the size a compile-time constant, so no step is conditional
+// (the conditional steps' register merges cost a 64-bit move per element and step)
+template <typename E, int WNM, bool FULL = false>
+__global__ void __launch_bounds__(256) inv_wave_kernel(const E *a, int n_, long k, E *b, int *info, int rm) {
     typedef DOps<E> O;
+    const int n = FULL ? WNM : n_;
     const int lane = threadIdx.x & 63, s = lane >> 4, c = lane & 15;
     const long mi = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * 4 + s;
     const bool live = mi < k, valid = live && c < n;
@@ -718,9 +772,13 @@ template <typename E> void potrf_typed(void *a, long n, long k, int *info, bool 
             hipLaunchKernelGGL(kern, dim3((unsigned)((k + per - 1) / per)), dim3(256), 0, s, (E *)a, (int)n, k, info,
                                rm ? 1 : 0);
         };
-        if (n <= 4) go(potrf_wave_kernel<E, 4>);
-        else if (n <= 8) go(potrf_wave_kernel<E, 8>);
-        else if (n <= 12) go(potrf_wave_kernel<E, 12>);
+        if (n == 4) go(potrf_wave_kernel<E, 4, true>);
+        else if (n < 4) go(potrf_wave_kernel<E, 4>);
+        else if (n == 8) go(potrf_wave_kernel<E, 8, true>);
+        else if (n < 8) go(potrf_wave_kernel<E, 8>);
+        else if (n == 12) go(potrf_wave_kernel<E, 12, true>);
+        else if (n < 12) go(potrf_wave_kernel<E, 12>);
+        else if (n == 16) go(potrf_wave_kernel<E, 16, true>);
         else go(potrf_wave_kernel<E, 16>);
         SBX_HIP_CHECK(hipGetLastError());
         return;
@@ -745,9 +803,13 @@ void gesv_typed(void *a, long n, long k, void *b, long m, bool identity, const S
             hipLaunchKernelGGL(kern, dim3((unsigned)((k + 15) / 16)), dim3(256), 0, s, (const E *)a, (int)n, k,
                                (E *)b, info, rm ? 1 : 0);
         };
-        if (n <= 4) go(inv_wave_kernel<E, 4>);
-        else if (n <= 8) go(inv_wave_kernel<E, 8>);
-        else if (n <= 12) go(inv_wave_kernel<E, 12>);
+        if (n == 4) go(inv_wave_kernel<E, 4, true>);
+        else if (n < 4) go(inv_wave_kernel<E, 4>);
+        else if (n == 8) go(inv_wave_kernel<E, 8, true>);
+        else if (n < 8) go(inv_wave_kernel<E, 8>);
+        else if (n == 12) go(inv_wave_kernel<E, 12, true>);
+        else if (n < 12) go(inv_wave_kernel<E, 12>);
+        else if (n == 16) go(inv_wave_kernel<E, 16, true>);
         else go(inv_wave_kernel<E, 16>);
         SBX_HIP_CHECK(hipGetLastError());
         return;
