@@ -382,3 +382,53 @@ def test_kron_spin_random_values(gpu):
     scale = np.abs(ref).max()
     for out in outs:
         assert np.abs(out - ref).max() / scale < 1e-14
+
+
+def dirac_pauli_spin():
+    """1, 1 -+ gamma_mu in the Dirac-Pauli basis: gamma_4 diagonal, gamma_k = [[0, s_k], [-s_k, 0]]
+    (rows nonzero at a and a ^ 3 or a ^ 2, or only at a)"""
+    s1 = np.array([[0, 1], [1, 0]])
+    s2 = np.array([[0, -1j], [1j, 0]])
+    s3 = np.array([[1, 0], [0, -1]])
+    z = np.zeros((2, 2))
+    g = [np.block([[z, sk], [-sk, z]]) for sk in (s1, s2, s3)]
+    g.append(np.diag([1, 1, -1, -1]))
+    ks = [np.eye(4)]
+    for gm in g:
+        ks += [np.eye(4) - gm, np.eye(4) + gm]
+    return np.array(ks, np.complex128).ravel()
+
+
+@pytest.mark.parametrize("ncols", [8, 12, 20])
+def test_kron_xor_kernel_dirac_pauli(gpu, ncols):
+    """the diagonal + XOR-partner kernel (bsr.kron_spin 2) takes the Dirac-Pauli projectors too
+    (a diagonal one among them: no partner); integer data, exact against the oracle"""
+    import torch
+    import superbblas_amd as sb
+    L, spin, color = 4, 4, 3
+    ii, jj, vals, _ = kron_lattice(L, spin, color)
+    kron = dirac_pauli_spin()
+    V = L ** 4
+    g = np.arange(V * color * ncols * spin)
+    x = ((g % 5 - 2) + 1j * (g % 3 - 1)).astype(np.complex128)
+    ref = reference(L, spin, color, ncols, vals, kron, jj, x, 1.0, 0.0, np.zeros_like(x), 1)
+    dim = [L, L, L, L, spin, color]
+    full = [([0] * 6, dim)]
+    blk, kr = [1, 1, 1, 1, 1, color], [1, 1, 1, 1, spin, 1]
+    op = sb.create_kron_bsr(full, dim, full, dim, blk, blk, kr, kr, False,
+                            [torch.from_numpy(ii).to(gpu)], [torch.from_numpy(jj).to(gpu)],
+                            [torch.from_numpy(vals).to(gpu)], [torch.from_numpy(kron).to(gpu)])
+    dimx = [1, L, L, L, L, color, ncols, spin]
+    ty = torch.zeros(V * 12 * ncols, dtype=torch.complex128, device=gpu)
+    try:
+        sb.tune_set("bsr.kron_spin", 2)
+        sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", [([0] * 8, dimx)], "pXYZTCnS", [0] * 8, dimx,
+                      dimx, [torch.from_numpy(x).to(gpu)], 0.0, [([0] * 8, dimx)], "pxyztcns",
+                      [0] * 8, dimx, dimx, "p", [ty])
+        torch.cuda.synchronize()
+        used = sb.tune_get("bsr.last_kernel")
+    finally:
+        sb.tune_set("bsr.kron_spin", 0)
+        op.destroy()
+    assert used == 12
+    assert np.array_equal(ty.cpu().numpy(), ref)
