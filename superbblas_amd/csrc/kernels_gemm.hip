@@ -576,7 +576,87 @@ __global__ void __launch_bounds__(WM *WN *KG * 64) gemm_dma_kernel(const GemmKAr
             if (!share) lb.issue(rsB, base + BM * BKK * ES, wave, k_begin, k_end, p.sb_k, 0, LdB::NI, p.dma_nt);
         }
     }
-    for (long s = 0; s < nslab; ++s) {
+    // EB (loader waves, SP == 0): the barrier of a slab moved before its last k-step, whose
+    // fragments are read first; after the barrier the loaders issue slab s + 2 and every wave
+    // reads the next slab's first fragments while the last k-step's MFMAs run -- the MFMA pipe
+    // has work the moment the barrier opens (the slab turnaround: 17.9k clocks per slab against
+    // the 16.4k its MFMAs take, profiles/r05_gemm_slab_probe.txt)
+    constexpr bool EB = LW > 0 && SP == 0;
+    static_assert(!EB || (KG == 1 && !PF && !M3 && BKK >= 8), "early barrier: plain 4M / real form");
+    if constexpr (EB) {
+        auto frag = [&](const E *As_, const E *Bs_, int kk, E (&af)[MT], E (&bf)[NT]) {
+#pragma unroll
+            for (int i = 0; i < MT; ++i) af[i] = As_[OpA::slot(frow + 16 * i, kk + kq)];
+#pragma unroll
+            for (int j = 0; j < NT; ++j) bf[j] = Bs_[OpB::slot(fcol + 16 * j, kk + kq)];
+        };
+        auto mma = [&](E (&af)[MT], E (&bf)[NT]) {
+            if constexpr (CPLX) {
+#pragma unroll
+                for (int i = 0; i < MT; ++i) af[i].y = flip(af[i].y, ma);
+#pragma unroll
+                for (int j = 0; j < NT; ++j) bf[j].y = flip(bf[j].y, mb);
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+#pragma unroll
+                    for (int j = 0; j < NT; ++j) {
+                        accR[i][j] = Mfma<R>::mma(af[i].x, bf[j].x, accR[i][j]);
+                        accI[i][j] = Mfma<R>::mma(af[i].x, bf[j].y, accI[i][j]);
+                    }
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+#pragma unroll
+                    for (int j = 0; j < NT; ++j) {
+                        accR[i][j] = Mfma<R>::mma(-af[i].y, bf[j].y, accR[i][j]);
+                        accI[i][j] = Mfma<R>::mma(af[i].y, bf[j].x, accI[i][j]);
+                    }
+            } else {
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+#pragma unroll
+                    for (int j = 0; j < NT; ++j) accR[i][j] = Mfma<R>::mma(af[i], bf[j], accR[i][j]);
+            }
+        };
+        auto issue_slab = [&](long sl, const char *dst) {
+            if (!loader || sl >= nslab) return;
+            const long kk0 = k_begin + sl * BKK;
+            la.issue(rsA, dst, wave, kk0, k_end, p.sa_k, 0, LdA::NI, p.dma_nt);
+            if (!share) lb.issue(rsB, dst + BM * BKK * ES, wave, kk0, k_end, p.sb_k, 0, LdB::NI, p.dma_nt);
+        };
+        E af0[MT], bf0[NT];
+        if (nslab > 0) {
+            // slab 0 (issued above) landed everywhere; slab 1 into the other buffer
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            issue_slab(1, base + (size_t)SLAB * ES);
+            frag(lds, share ? lds : lds + BM * BKK, 0, af0, bf0);
+        }
+        for (long s = 0; s < nslab; ++s) {
+            const int cur = (int)(s & 1);
+            const E *As = lds + cur * SLAB;
+            const E *Bs = share ? As : As + BM * BKK;
+            mma(af0, bf0);
+#pragma unroll
+            for (int kk = 4; kk < BKK - 4; kk += 4) {
+                E af[MT], bf[NT];
+                frag(As, Bs, kk, af, bf);
+                mma(af, bf);
+            }
+            E af3[MT], bf3[NT];
+            frag(As, Bs, BKK - 4, af3, bf3);
+            if (s + 1 < nslab) {
+                // every wave's reads of this slab done and slab s + 1 landed: this buffer is free
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                issue_slab(s + 2, base + (size_t)cur * SLAB * ES);
+                const E *An = lds + (cur ^ 1) * SLAB;
+                frag(An, share ? An : An + BM * BKK, 0, af0, bf0);
+            }
+            mma(af3, bf3);
+        }
+    }
+    for (long s = 0; s < (EB ? 0 : nslab); ++s) {
 #ifdef SBX_SLAB_PROBE
         // (tools only: workgroup 0 stamps, per wave and slab, the clock before the DMA wait and
         // after the barrier: probe[4096 + (wave * nslab + s) * 2 + 0 / 1])
@@ -602,7 +682,7 @@ __global__ void __launch_bounds__(WM *WN *KG * 64) gemm_dma_kernel(const GemmKAr
         // loader waves: the pieces of k-step q of SP (the next slab's DMA spread over this one's
         // first SP k-steps)
         auto load_part = [&](int q) {
-            if constexpr (LW > 0) {
+            if constexpr (LW > 0 && SP > 0) {
                 if (loader && s + 1 < nslab && q < SP) {
                     la.issue(rsA, nb, wave, kn, k_end, p.sa_k, q * LdA::NI / SP,
                              (q + 1) * LdA::NI / SP, p.dma_nt);
@@ -1411,6 +1491,8 @@ void launch_tiled(const GemmKArgs &p, int device, hipStream_t stream) {
                     launch_dma_cfg<R, CPLX, AK, BK, 128, 128, 16, 4, 4, false, false, 1, false, 4, 1>(p, device, stream, 0, 256);
                 else if (lw == 8 && sp == 4)
                     launch_dma_cfg<R, CPLX, AK, BK, 128, 128, 16, 4, 4, false, false, 1, false, 8, 4>(p, device, stream, 0, 256);
+                else if (lw == 8 && sp == 0)
+                    launch_dma_cfg<R, CPLX, AK, BK, 128, 128, 16, 4, 4, false, false, 1, false, 8, 0>(p, device, stream, 0, 256);
                 else if (lw == 8)
                     launch_dma_cfg<R, CPLX, AK, BK, 128, 128, 16, 4, 4, false, false, 1, false, 8, 1>(p, device, stream, 0, 256);
                 else if (lw == 16 && sp == 4)

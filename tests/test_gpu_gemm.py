@@ -221,3 +221,29 @@ def test_gemm_skinny(gpu, dtype, ta, tb, m, n, k, batch, skinny):
     finally:
         sb.tune_set("gemm.skinny", old)
     assert rel_err(out, ref) < TOL[dtype]
+
+
+@pytest.mark.parametrize("dtype", [np.complex128, np.float64, np.complex64])
+@pytest.mark.parametrize("m,n,k,batch", [(256, 256, 1000, 2), (129, 200, 16, 1), (300, 140, 40, 3),
+                                         (128, 128, 8, 1)])
+def test_gemm_loader_forms(gpu, dtype, m, n, k, batch):
+    """the slab DMA by 8 loader waves, spread over 1 / 4 k-steps or with the early barrier
+    (gemm.dma_spread 0: a slab's barrier before its last k-step), and by every wave (loaders
+    0): against the oracle and bit-identical to one another (the same MFMA order); partial
+    tiles and partial, single and half slabs"""
+    import torch
+    import superbblas_amd as sb
+    old_l, old_s = sb.tune_get("gemm.loaders"), sb.tune_get("gemm.dma_spread")
+    outs = []
+    try:
+        for lw, sp in ((8, 1), (8, 0), (8, 4), (0, 1)):
+            sb.tune_set("gemm.loaders", lw)
+            sb.tune_set("gemm.dma_spread", sp)
+            out, ref = _run(gpu, dtype, "T", "N", m, n, k, batch, 1.0, 0.0)
+            assert rel_err(out, ref) < TOL[dtype], (lw, sp)
+            outs.append(out)
+    finally:
+        sb.tune_set("gemm.loaders", old_l)
+        sb.tune_set("gemm.dma_spread", old_s)
+    for o in outs[1:3]:
+        assert np.array_equal(o, outs[0])
