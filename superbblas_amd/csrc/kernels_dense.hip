@@ -702,8 +702,20 @@ __global__ void __launch_bounds__(256) trsm_io_kernel(const E *a, int n, long k,
     const int nm = n * m;
     const int nblk = (int)min((long)per, k - mi0 > 0 ? k - mi0 : 0L); // the wave's matrices
     E *sl = io_s[w];
+    // a run of cnt elements from global memory into the slice: every load issued before the
+    // first LDS write (cnt <= 64 WNM: per m <= 64); a loop of load -> write pairs waits out one
+    // memory latency per pass
+    auto stage = [&](const E *src, int cnt) {
+        Col<E, WNM> t_; // (complex: separate real / imaginary arrays, kept in registers)
+#pragma unroll
+        for (int i = 0; i < WNM; ++i)
+            t_.set(i, lane + 64 * i < cnt ? src[lane + 64 * i] : O::real(0));
+#pragma unroll
+        for (int i = 0; i < WNM; ++i)
+            if (lane + 64 * i < cnt) sl[lane + 64 * i] = t_.get(i);
+    };
     // the wave's x blocks (one contiguous run of nblk * n * m elements)
-    for (int e = lane; e < nblk * nm; e += 64) sl[e] = x[mi0 * nm + e];
+    stage(x + mi0 * nm, nblk * nm);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
     const bool live = s < nblk;
@@ -719,7 +731,7 @@ __global__ void __launch_bounds__(256) trsm_io_kernel(const E *a, int n, long k,
     if (ulds) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // every lane has read its x
         __builtin_amdgcn_wave_barrier();
-        for (int e = lane; e < nblk * nn; e += 64) sl[e] = a[mi0 * nn + e];
+        stage(a + mi0 * nn, nblk * nn);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
     }
@@ -760,7 +772,15 @@ __global__ void __launch_bounds__(256) trsm_io_kernel(const E *a, int n, long k,
             if (r < n) yb[r * ysi + t * yst] = v.get(r);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
-    for (int e = lane; e < nblk * nm; e += 64) y[mi0 * nm + e] = sl[e];
+    {
+        Col<E, WNM> t_;
+        const int cnt = nblk * nm;
+#pragma unroll
+        for (int i = 0; i < WNM; ++i) t_.set(i, lane + 64 * i < cnt ? sl[lane + 64 * i] : O::real(0));
+#pragma unroll
+        for (int i = 0; i < WNM; ++i)
+            if (lane + 64 * i < cnt) y[mi0 * nm + lane + 64 * i] = t_.get(i);
+    }
 }
 
 template <typename E> bool fits_lds(long n) { return n * n * (long)sizeof(E) <= DENSE_LDS_BYTES; }
