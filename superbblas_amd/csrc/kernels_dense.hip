@@ -415,16 +415,20 @@ __global__ void __launch_bounds__(256) gesv_wave_kernel(E *a, int n, long k, con
             if (ok && c > j) v.set(r, O::sub(v.get(r), O::mul(l, vj)));
         }
     }
+    // the factors in LDS row-major (the lanes' writes consecutive), one element of padding per
+    // matrix where it fits: the matrices of a wave read their factors' element (r, q) together,
+    // and n^2 elements apart they would all fall on the same LDS banks
+    const int ldm = G * (n * n + 1) <= 64 * WNM ? n * n + 1 : n * n;
     if (s < G)
 #pragma unroll
         for (int r = 0; r < WNM; ++r)
             if (r < n) {
                 if (valid && keep_lu) g[rm ? c + (long)r * n : r + (long)c * n] = v.get(r);
-                lu_s[w][s0 * n + r + c * n] = v.get(r);
+                lu_s[w][s * ldm + r * n + c] = v.get(r);
             }
     if (valid && !bad && b) {
         // (the wave's LDS writes above are ordered before its reads below)
-        const E *M = lu_s[w] + s0 * n;
+        const E *M = lu_s[w] + s * ldm;
         const E *Dinv = dinv_s[w] + s0;
         const int *piv = piv_s[w] + s0;
         // right-hand side column col: element r at r * xsi + col * xst of the matrix's n x m
@@ -458,7 +462,7 @@ __global__ void __launch_bounds__(256) gesv_wave_kernel(E *a, int n, long k, con
                 if (r >= n) continue;
                 E t = x.get(r);
 #pragma unroll
-                for (int q = 0; q < r; ++q) t = O::sub(t, O::mul(M[r + q * n], x.get(q)));
+                for (int q = 0; q < r; ++q) t = O::sub(t, O::mul(M[r * n + q], x.get(q)));
                 x.set(r, t);
             }
 #pragma unroll
@@ -467,7 +471,7 @@ __global__ void __launch_bounds__(256) gesv_wave_kernel(E *a, int n, long k, con
                 E t = x.get(r);
 #pragma unroll
                 for (int q = r + 1; q < WNM; ++q)
-                    if (q < n) t = O::sub(t, O::mul(M[r + q * n], x.get(q)));
+                    if (q < n) t = O::sub(t, O::mul(M[r * n + q], x.get(q)));
                 x.set(r, O::mul(t, Dinv[r]));
             }
             if (alpha_re != 1 || alpha_im != 0)
@@ -728,14 +732,30 @@ __global__ void __launch_bounds__(256) trsm_io_kernel(const E *a, int n, long k,
     // product then reads its factor element from LDS (a broadcast within the matrix's lanes)
     const int nn = n * n;
     const bool ulds = per * nn <= 64 * WNM;
+    // (one element of padding per factor where it fits: the wave's matrices read their factors'
+    // element (r, q) together, and nn elements apart they would fall on the same LDS banks)
+    const int ldu = per * (nn + 1) <= 64 * WNM ? nn + 1 : nn;
     if (ulds) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // every lane has read its x
         __builtin_amdgcn_wave_barrier();
-        stage(a + mi0 * nn, nblk * nn);
+        if (ldu == nn) {
+            stage(a + mi0 * nn, nblk * nn);
+        } else {
+            const E *src = a + mi0 * nn;
+            const int cnt = nblk * nn;
+            Col<E, WNM> t_;
+#pragma unroll
+            for (int i = 0; i < WNM; ++i) t_.set(i, lane + 64 * i < cnt ? src[lane + 64 * i] : O::real(0));
+#pragma unroll
+            for (int i = 0; i < WNM; ++i) {
+                const int e = lane + 64 * i;
+                if (e < cnt) sl[e + e / nn] = t_.get(i);
+            }
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
     }
-    const E *U = ulds ? sl + s * nn : a + mi * nn;
+    const E *U = ulds ? sl + s * ldu : a + mi * nn;
     auto u = [&](int r, int q) { return rm ? U[r * n + q] : U[r + q * n]; };
     // the diagonal's reciprocals from the matrix's own lanes (m >= n), else per lane
     const bool shared = m >= n;
