@@ -43,8 +43,49 @@ def timed(f, reps=10):
     return statistics.median(w for w, _ in out), statistics.median(k for _, k in out)
 
 
+def wall_us(f, reps=20):
+    for _ in range(3):
+        f()
+    torch.cuda.synchronize()
+    out = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            f()
+        torch.cuda.synchronize()
+        out.append((time.perf_counter() - t0) / reps * 1e6)
+    return round(statistics.median(out), 1)
+
+
+def overhead(dev):
+    """OVERHEAD=1: where the inversion call's time beyond the kernel goes (site12, in place):
+    the refill copy alone, the call alone (timers off), the call on a tiny batch (host + launch +
+    the info check's round trip), and the kernel by the library timer"""
+    nb, n, dt = 16 ** 4, 12, torch.complex128
+    a0 = hpd(nb, n, dt, dev).reshape(-1)
+    v = a0.clone()
+    dim, full = [nb, n, n], [([0, 0, 0], [nb, n, n])]
+    s0 = hpd(64, n, dt, dev).reshape(-1)
+    small = s0.clone()
+    ds, fs = [64, n, n], [([0, 0, 0], [64, n, n])]
+    for op in ("inversion", "cholesky"):
+        r = {"op": op,
+             "refill_copy_us": wall_us(lambda: v.copy_(a0)),
+             # (in place again on its own output: an inverse of the inverse; a Cholesky factor is
+             # not a positive definite matrix, so Cholesky is timed with the refill only)
+             "call_only_us": (wall_us(lambda: sb.inversion(full, dim, "tij", [v], "i", "j"))
+                              if op == "inversion" else None),
+             "call_64_matrices_us": wall_us(lambda: (small.copy_(s0), getattr(sb, op)(fs, ds, "tij", [small], "i", "j"))),
+             "call_with_refill_us": wall_us(lambda: (v.copy_(a0), getattr(sb, op)(full, dim, "tij", [v], "i", "j")))}
+        _, kern = timed(lambda: (v.copy_(a0), getattr(sb, op)(full, dim, "tij", [v], "i", "j")))
+        r["kernel_us"] = round(kern * 1e6, 1)
+        print(json.dumps(r), flush=True)
+
+
 def main():
     dev = torch.device("cuda:0")
+    if os.environ.get("OVERHEAD"):
+        return overhead(dev)
     cases = os.environ.get("CASES", "site12,t48").split(",")
     shapes = {"site12": (16 ** 4, 12, torch.complex128), "t48": (64, 48, torch.complex64),
               "site3": (16 ** 4, 3, torch.complex128)}
