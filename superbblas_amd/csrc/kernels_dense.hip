@@ -110,9 +110,21 @@ template <typename E> __device__ __forceinline__ void stage_out(E *g, const E *m
     for (long e = threadIdx.x; e < nn; e += DTH) g[e] = m[e];
 }
 
+/// Where a factorization reports its LAPACK info: the per-matrix array in device memory and a
+/// host-mapped flag that any failed matrix sets, so that a batch without failures costs the host
+/// one stream synchronisation and a read of host memory (no memset, search kernel or copy back)
+struct InfoOut {
+    int *v;   // per matrix (device)
+    int *any; // host-mapped, coherent
+    __device__ __forceinline__ void put(long i, int bad) const {
+        v[i] = bad;
+        if (bad) *any = 1;
+    }
+};
+
 // Cholesky, upper: A = U^H U, U over the upper triangle, the strict lower part untouched
 template <typename E>
-__global__ void __launch_bounds__(DTH) potrf_kernel(E *a, long n, int lds, int *info) {
+__global__ void __launch_bounds__(DTH) potrf_kernel(E *a, long n, int lds, InfoOut info) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     typedef DOps<E> O;
     E *g = a + (long)blockIdx.x * n * n;
@@ -137,7 +149,7 @@ __global__ void __launch_bounds__(DTH) potrf_kernel(E *a, long n, int lds, int *
         }
     }
     stage_out(g, M, n * n, lds != 0);
-    if (threadIdx.x == 0) info[blockIdx.x] = bad;
+    if (threadIdx.x == 0) info.put(blockIdx.x, bad);
 }
 
 // LU with partial pivoting (getrf), then B <- alpha A^-1 B for the n x m column-major panel of
@@ -145,7 +157,7 @@ __global__ void __launch_bounds__(DTH) potrf_kernel(E *a, long n, int lds, int *
 template <typename E>
 __global__ void __launch_bounds__(DTH) gesv_kernel(E *a, long n, E *b, long m, int identity,
                                                    double alpha_re, double alpha_im, int lds,
-                                                   int *ipiv_g, int *info) {
+                                                   int *ipiv_g, InfoOut info) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     __shared__ double best_v[DTH];
     __shared__ int best_i[DTH];
@@ -234,7 +246,7 @@ __global__ void __launch_bounds__(DTH) gesv_kernel(E *a, long n, E *b, long m, i
         }
     }
     stage_out(g, M, n * n, lds != 0);
-    if (threadIdx.x == 0) info[blockIdx.x] = bad;
+    if (threadIdx.x == 0) info.put(blockIdx.x, bad);
 }
 
 // Upper triangular solve: left  X (n x m, ld n) <- alpha U^-1 X;  right X (m x n, ld m) <- alpha X U^-1
@@ -309,7 +321,7 @@ template <int N> struct Col<float2, N> : CCol<float2, float, N> {};
 // A wave holds G = 64 / n matrices: lane l = n s + c is column c of slot s (lanes past G n
 // idle); slots past the batch hold the identity and write nothing.
 template <typename E, int WNM, bool FULL = false>
-__global__ void __launch_bounds__(256) potrf_wave_kernel(E *a, int n_, long k, int *info, int rm) {
+__global__ void __launch_bounds__(256) potrf_wave_kernel(E *a, int n_, long k, InfoOut info, int rm) {
     const int n = FULL ? WNM : n_; // (FULL: a compile-time size, no conditional steps; the
                                    // solve kernels spill in that form, so only potrf / inversion)
     typedef DOps<E> O;
@@ -347,13 +359,13 @@ __global__ void __launch_bounds__(256) potrf_wave_kernel(E *a, int n_, long k, i
 #pragma unroll
         for (int r = 0; r < WNM; ++r)
             if (r < n) g[rm ? c + (long)r * n : r + (long)c * n] = v.get(r);
-    if (valid && c == 0) info[mi] = bad;
+    if (valid && c == 0) info.put(mi, bad);
 }
 
 template <typename E, int WNM>
 __global__ void __launch_bounds__(256) gesv_wave_kernel(E *a, int n, long k, const E *bx, E *b, long m, int identity,
                                                         double alpha_re, double alpha_im,
-                                                        int *info, int rm, int keep_lu, int xsi, int xst,
+                                                        InfoOut info, int rm, int keep_lu, int xsi, int xst,
                                                         int ysi, int yst) {
     typedef DOps<E> O;
     __shared__ E lu_s[4][64 * WNM];
@@ -482,7 +494,7 @@ __global__ void __launch_bounds__(256) gesv_wave_kernel(E *a, int n, long k, con
                 if (r < n) yg[r * ysi] = x.get(r);
         }
     }
-    if (valid && c == 0) info[mi] = bad;
+    if (valid && c == 0) info.put(mi, bad);
 }
 
 /// lane L's value of each 16-lane row (DPP row_newbcast: a VALU move, no LDS)
@@ -605,7 +617,7 @@ __device__ __forceinline__ void gj_step(Col<E, WNM> &v, int n, int c, int &bad, 
 // FULL: n == WNM (4, 8, 12, 16): the size a compile-time constant, so no step is conditional
 // (the conditional steps' register merges cost a 64-bit move per element and step)
 template <typename E, int WNM, bool FULL = false>
-__global__ void __launch_bounds__(256) inv_wave_kernel(const E *a, int n_, long k, E *b, int *info, int rm) {
+__global__ void __launch_bounds__(256) inv_wave_kernel(const E *a, int n_, long k, E *b, InfoOut info, int rm) {
     typedef DOps<E> O;
     const int n = FULL ? WNM : n_;
     const int lane = threadIdx.x & 63, s = lane >> 4, c = lane & 15;
@@ -632,7 +644,7 @@ __global__ void __launch_bounds__(256) inv_wave_kernel(const E *a, int n_, long 
         const E e = wshfl<E>(v.get(r), from);
         if (valid && !bad) o[rm ? c + (long)r * n : r + (long)c * n] = e;
     }
-    if (live && c == 0) info[mi] = bad;
+    if (live && c == 0) info.put(mi, bad);
 }
 
 // Triangular solves with small factors (n <= 16): a lane per right-hand side (left: a column of
@@ -805,7 +817,7 @@ __global__ void __launch_bounds__(256) trsm_io_kernel(const E *a, int n, long k,
 
 template <typename E> bool fits_lds(long n) { return n * n * (long)sizeof(E) <= DENSE_LDS_BYTES; }
 
-template <typename E> void potrf_typed(void *a, long n, long k, int *info, bool rm, hipStream_t s) {
+template <typename E> void potrf_typed(void *a, long n, long k, InfoOut info, bool rm, hipStream_t s) {
     if (n <= WNMAX && g_dense_wave) {
         auto go = [&](auto kern) {
             const long per = 4 * (64 / n);
@@ -836,7 +848,7 @@ struct GesvIO {
 
 template <typename E>
 void gesv_typed(void *a, long n, long k, void *b, long m, bool identity, const Scalar &alpha,
-                int *ipiv, int *info, bool rm, bool keep_lu, hipStream_t s, const GesvIO &io = GesvIO{}) {
+                int *ipiv, InfoOut info, bool rm, bool keep_lu, hipStream_t s, const GesvIO &io = GesvIO{}) {
     if (n <= WNMAX && g_dense_wave && identity && !keep_lu && alpha.re == 1 && alpha.im == 0) {
         // the inverse only (the factors not kept): Gauss-Jordan, a 16-lane row per matrix
         auto go = [&](auto kern) {
@@ -909,11 +921,31 @@ __global__ void __launch_bounds__(256) first_bad_kernel(const int *info, long k,
         if (info[i] != 0) atomicMin(res, (int)i);
 }
 
-/// The first nonzero LAPACK info of the batch (synchronises the stream): the index of the first
-/// failed matrix is found on the device, so only 4 bytes cross to the host (and 4 more when a
-/// matrix failed) instead of the whole info array
+/// The calling thread's host-mapped failure flag (one per thread: every dense call synchronises
+/// before it returns, so two calls never have it in flight together; kept for the thread's life)
+volatile int *host_flag() {
+    static thread_local int *flag = nullptr;
+    if (!flag)
+        SBX_HIP_CHECK(hipHostMalloc((void **)&flag, sizeof(int),
+                                    hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent));
+    return flag;
+}
+/// The info outputs of one launch over `v` (k ints), the flag cleared
+InfoOut info_out(const Scratch &v) {
+    volatile int *h = host_flag();
+    *h = 0;
+    int *dev = nullptr;
+    SBX_HIP_CHECK(hipHostGetDevicePointer((void **)&dev, (void *)h, 0));
+    return InfoOut{(int *)v.ptr, dev};
+}
+
+/// The first nonzero LAPACK info of the batch (synchronises the stream): with the host flag
+/// clear, 0 at once; otherwise the index of the first failed matrix is found on the device, so
+/// only 8 bytes cross to the host instead of the whole info array
 int first_info(const int *info_d, long k, hipStream_t s, int device) {
     if (k >= 0x7fffffffL) throw Error("dense: too many matrices");
+    SBX_HIP_CHECK(hipStreamSynchronize(s));
+    if (*host_flag() == 0) return 0;
     Scratch res(sizeof(int), device);
     SBX_HIP_CHECK(hipMemsetAsync(res.ptr, 0x7f, sizeof(int), s));
     const long blocks = std::min((k + 255) / 256, 1024L);
@@ -949,9 +981,10 @@ int launch_potrf(int t, void *a, long n, long k, int device, bool rm) {
     set_device(device);
     hipStream_t s = get_stream(device);
     Scratch info(sizeof(int) * k, device);
+    const InfoOut iout = info_out(info);
     {
         KernelTimer timer("dense", s);
-        dispatch(t, [&](auto z) { potrf_typed<decltype(z)>(a, n, k, (int *)info.ptr, rm, s); });
+        dispatch(t, [&](auto z) { potrf_typed<decltype(z)>(a, n, k, iout, rm, s); });
     }
     return first_info((const int *)info.ptr, k, s, device);
 }
@@ -963,11 +996,12 @@ int launch_gesv(int t, void *a, long n, long k, void *b, long m, bool identity,
     set_device(device);
     hipStream_t s = get_stream(device);
     Scratch info(sizeof(int) * k, device), ipiv(sizeof(int) * k * n, device);
+    const InfoOut iout = info_out(info);
     {
         KernelTimer timer("dense", s);
         dispatch(t, [&](auto z) {
             gesv_typed<decltype(z)>(a, n, k, b, m, identity, alpha, (int *)ipiv.ptr,
-                                    (int *)info.ptr, rm, keep_lu, s);
+                                    iout, rm, keep_lu, s);
         });
     }
     return first_info((const int *)info.ptr, k, s, device);
@@ -1007,13 +1041,14 @@ int launch_gesv_io(int t, const void *a, long n, long k, bool rm, const void *x,
     set_device(device);
     hipStream_t s = get_stream(device);
     Scratch info(sizeof(int) * k, device);
+    const InfoOut iout = info_out(info);
     GesvIO io;
     io.x = x;
     io.xsi = xsi, io.xst = xst, io.ysi = ysi, io.yst = yst;
     {
         KernelTimer timer("dense", s);
         dispatch(t, [&](auto z) {
-            gesv_typed<decltype(z)>(const_cast<void *>(a), n, k, y, m, false, alpha, nullptr, (int *)info.ptr, rm,
+            gesv_typed<decltype(z)>(const_cast<void *>(a), n, k, y, m, false, alpha, nullptr, iout, rm,
                                     false, s, io);
         });
     }

@@ -154,3 +154,36 @@ def test_dense_errors(gpu):
     with pytest.raises(sb.SuperbblasError, match="row labels"):
         sb.gesm(1.0, full, [nt, n, n], "tij", v, "i", "j", px, [nt, 2, n], "tni", x, px,
                 [nt, 2, n], "tnj", x)
+
+
+@pytest.mark.parametrize("wave", [1, 0])
+def test_dense_failure_flag(gpu, wave):
+    """a failure late in a large batch is reported with its LAPACK info (the host-mapped failure
+    flag, then the search for the first failed matrix), and the next call on the same thread sees a
+    clear flag: a good batch after a failed one succeeds"""
+    import torch
+    import superbblas_amd as sb
+    n, nt = 12, 300
+    dim = [nt, n, n]
+    full = [([0, 0, 0], dim)]
+    old = sb.tune_get("dense.wave")
+    sb.tune_set("dense.wave", wave)
+    try:
+        good = np.tile((np.eye(n) * 4 + 0.1).ravel(), nt)
+        bad = good.reshape(nt, n, n).copy()
+        bad[217, :, 5] = 0  # column 5 of matrix 217: LU stops at pivot 6
+        with pytest.raises(sb.SuperbblasError, match="lapack routine: 6"):
+            sb.inversion(full, dim, "tij", [torch.from_numpy(bad.ravel().copy()).to(gpu)], "i", "j")
+        v = torch.from_numpy(good.copy()).to(gpu)
+        sb.inversion(full, dim, "tij", [v], "i", "j")
+        ref = np.linalg.inv(good.reshape(nt, n, n))
+        assert np.abs(v.cpu().numpy().reshape(nt, n, n) - ref).max() < 1e-12
+        hp = np.tile(np.eye(n).ravel() * 2.0, nt).reshape(nt, n, n)
+        hp[299, 4, 4] = -1.0  # not positive definite at pivot 5
+        with pytest.raises(sb.SuperbblasError, match="lapack routine: 5"):
+            sb.cholesky(full, dim, "tij", [torch.from_numpy(hp.ravel().copy()).to(gpu)], "i", "j")
+        u = torch.from_numpy(np.tile(np.eye(n).ravel() * 4.0, nt)).to(gpu)
+        sb.cholesky(full, dim, "tij", [u], "i", "j")
+        assert np.allclose(u.cpu().numpy().reshape(nt, n, n)[:, range(n), range(n)], 2.0)
+    finally:
+        sb.tune_set("dense.wave", old)
