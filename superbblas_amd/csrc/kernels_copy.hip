@@ -1019,7 +1019,9 @@ bool prepare_trans(CopyLaunch &l, const Norm &n, int first, long R, long total) 
         ++nw;
     }
     a.nw = nw;
-    a.nt = g_copy_tune.nt > 0 || (g_copy_tune.nt == 0 && total * (long)sizeof(D) >= (8L << 20));
+    // streaming stores from 4 MB here (8 MB in the other copy kernels): the config-2p slice of
+    // complex<float> (6.3 MB written) measured 3.68 -> 3.98-4.10 TB/s with them
+    a.nt = g_copy_tune.nt > 0 || (g_copy_tune.nt == 0 && total * (long)sizeof(D) >= (4L << 20));
     // paired 16-byte accesses for 8-byte elements: even runs with even starts on that side
     bool ws_even = true, wd_even = true, ud_even = true;
     for (int i = 0; i < nw; ++i) {
