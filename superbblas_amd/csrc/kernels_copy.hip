@@ -376,6 +376,11 @@ __global__ void __launch_bounds__(256) copy_tiled3_kernel(const TiledArgs p) {
 // NU runs of QT*R destination elements.  Against the general tile kernel (a tile row spans only
 // part of U, offset tables per element, rows walked in several dependent rounds) the config-2p
 // slice loop goes 5.2 -> 3.5 us per slice (tools/permute_micro.hip).
+/// Destinations from this size are written with streaming (non-temporal) stores: written once,
+/// not re-read by the kernel.  4 MB: the config-2p slice of complex<float> (6.3 MB written)
+/// measured 3.68 -> 3.98-4.10 TB/s with them, and 4.7-6.3 MB block / tile copies 2-6 % faster
+/// (tools/studies/copy_shapes.py COPY_MID); it was 8 MB.
+constexpr long NT_MIN_BYTES = 4L << 20;
 constexpr int TRANS_EMAX = 1536; // elements per tile
 constexpr int TRANS_KMAX = TRANS_EMAX / 256;
 /// block transpose tile (elements): 24 KB of 16-byte elements, 3072 smaller ones (12 per thread)
@@ -1019,9 +1024,7 @@ bool prepare_trans(CopyLaunch &l, const Norm &n, int first, long R, long total) 
         ++nw;
     }
     a.nw = nw;
-    // streaming stores from 4 MB here (8 MB in the other copy kernels): the config-2p slice of
-    // complex<float> (6.3 MB written) measured 3.68 -> 3.98-4.10 TB/s with them
-    a.nt = g_copy_tune.nt > 0 || (g_copy_tune.nt == 0 && total * (long)sizeof(D) >= (4L << 20));
+    a.nt = g_copy_tune.nt > 0 || (g_copy_tune.nt == 0 && total * (long)sizeof(D) >= NT_MIN_BYTES);
     // paired 16-byte accesses for 8-byte elements: even runs with even starts on that side
     bool ws_even = true, wd_even = true, ud_even = true;
     for (int i = 0; i < nw; ++i) {
@@ -1262,7 +1265,7 @@ bool prepare_btrans(CopyLaunch &l, const Norm &n0, int first, long R, long total
         ++nw;
     }
     a.nw = nw;
-    a.nt = g_copy_tune.nt > 0 || (g_copy_tune.nt == 0 && total * (long)sizeof(D) >= (8L << 20));
+    a.nt = g_copy_tune.nt > 0 || (g_copy_tune.nt == 0 && total * (long)sizeof(D) >= NT_MIN_BYTES);
     // paired stores: even destination runs whose starts are even (V1, DO and outer strides)
     bool d_even = a.RD % 2 == 0 && a.dsv % 2 == 0;
     for (int k = 0; k < a.ndo; ++k) d_even = d_even && a.dost[k] % 2 == 0;
@@ -1307,7 +1310,7 @@ CopyLaunch prepare_pair(bool masked, Norm n, long total) {
     if (n.size.size() == 1 && n.ss[0] == 1 && n.ds[0] == 1) {
         l.kind = CopyLaunch::CONTIG;
         l.blocks = std::min((total + 255) / 256, 8192L);
-        l.nt = g_copy_tune.nt > 0 || (g_copy_tune.nt == 0 && total * (long)sizeof(D) >= (8L << 20));
+        l.nt = g_copy_tune.nt > 0 || (g_copy_tune.nt == 0 && total * (long)sizeof(D) >= NT_MIN_BYTES);
         return l;
     }
     if (total >= (1L << 32) - 1) throw Error("copy: boxes with 2^32 elements or more are not supported yet");
@@ -1458,7 +1461,7 @@ CopyLaunch prepare_pair(bool masked, Norm n, long total) {
     };
     // streaming stores for large destinations (written once, not re-read by this kernel):
     // the config-2p slice loop 6.8 -> 4.9 us per slice, the 1.6 GB permute 5.0 -> 5.2 TB/s
-    a.nt = g_copy_tune.nt > 0 || (g_copy_tune.nt == 0 && total * (long)sizeof(D) >= (8L << 20));
+    a.nt = g_copy_tune.nt > 0 || (g_copy_tune.nt == 0 && total * (long)sizeof(D) >= NT_MIN_BYTES);
     a.lr = lanes_log2(R * TU);
     a.lw = lanes_log2(R * TV);
     a.lr2 = lanes_log2((R * TU + 1) / 2);

@@ -93,6 +93,8 @@ def main():
         return sweep(os.environ["COPY_SWEEP"])
     if os.environ.get("COPY_KINDS"):
         return kinds()
+    if os.environ.get("COPY_MID"):
+        return mid()
     combos = ((0, 0, 0), (0, 0, -1), (0, 0, -2), (0, -1, 0))
     if os.environ.get("COPY_QUICK"):
         combos = combos[:3]
@@ -105,6 +107,21 @@ def main():
     sb.tune_set("copy.nt", 0)
     sb.tune_set("copy.pair", 0)
     sb.tune_set("copy.order", 0)
+
+
+def mid():
+    """COPY_MID=1: 4-8 MB outputs (under the 8 MB streaming-store threshold of the block and tile
+    kernels) with streaming stores off / on, twice"""
+    for nt in (0, 1, 0, 1):
+        sb.tune_set("copy.nt", nt if nt else 0)
+        print(json.dumps({"copy.nt": nt}))
+        case("redist_mid", "tnsxyzc", [4, 12, 4, 8, 8, 16, 3], "pxyztscn",
+             [1, 8, 8, 16, 4, 4, 3, 12], [0] * 8, torch.complex64, reps=50)
+        case("chain_mid", "pXYZTSCn", [1, 8, 8, 16, 4, 4, 3, 12], "TSnpXYZC",
+             [4, 4, 12, 1, 8, 8, 16, 3], [0] * 8, torch.complex64, reps=50)
+        case("big_mid", "xyztnsc", [8, 8, 8, 8, 16, 4, 3], "tnsxyzc", [8, 16, 4, 8, 8, 8, 3],
+             [0] * 7, torch.complex64, reps=50)
+    sb.tune_set("copy.nt", 0)
 
 
 def shapes():
