@@ -995,7 +995,8 @@ int launch_gesv(int t, void *a, long n, long k, void *b, long m, bool identity,
     if (k >= (1L << 31)) throw Error("dense: too many matrices");
     set_device(device);
     hipStream_t s = get_stream(device);
-    Scratch info(sizeof(int) * k, device), ipiv(sizeof(int) * k * n, device);
+    // (pivot indices only for the workgroup kernels: the wave kernels keep theirs in registers)
+    Scratch info(sizeof(int) * k, device), ipiv(dense_wave_rows(n) ? 0 : sizeof(int) * k * n, device);
     const InfoOut iout = info_out(info);
     {
         KernelTimer timer("dense", s);
