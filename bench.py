@@ -458,6 +458,10 @@ def main():
     sb.timings_enable(True)
     sb.timings_filter("gemm_total")
     sb.timings_reset()
+    # the shader clock the timed GEMMs ran at: workgroup 0 of every LDS-DMA GEMM launch sums its
+    # s_memtime (shader clock) and s_memrealtime (100 MHz) spans (three vector atomics by one
+    # thread per launch), so a slower box can be told apart from a slower kernel
+    sb.tune_set("gemm.clock", 1)
     progress("timed steps")
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -474,6 +478,10 @@ def main():
     gemm_ms, gemm_calls = sb.timings_get("gemm_total")
     sb.timings_enable(False)
     sb.timings_filter(None)
+    clk_cycles, clk_ticks = sb.tune_get("gemm.clock_cycles"), sb.tune_get("gemm.clock_ticks")
+    clk_launches = sb.tune_get("gemm.clock_launches")
+    sb.tune_set("gemm.clock", 0)
+    shader_ghz = round(clk_cycles / clk_ticks * 0.1, 4) if clk_ticks > 0 else None
     # one GEMM = the MFMA kernel launch + its split-K reduce (the reduce is part of the GEMM)
     kernel_s = gemm_ms / max(gemm_calls, 1) / 1e3
 
@@ -502,6 +510,11 @@ def main():
                 scaling_fields = {"value_1gpu_same_problem": round(flops_step / t1 / 1e9, 2),
                                   "ms_per_step_1gpu": round(t1 * 1e3, 4),
                                   "strong_scaling_vs_1gpu": round(t1 / (elapsed / args.steps), 3)}
+                if side.get("contraction_redistributed_ms"):
+                    # configs[3] 4b: the contraction whose second operand is redistributed by an
+                    # all-to-all, against the same global problem on one GPU
+                    scaling_fields["strong_scaling_vs_1gpu_4b"] = round(
+                        t1 * 1e3 / side["contraction_redistributed_ms"], 3)
                 for name, r in results.items():
                     scaling_fields["scale_check_rel_err_" + name] = rel_err(r, ref)
                 del ref
@@ -592,7 +605,10 @@ def main():
                          "complex_product": ("3-multiplication form (6 executed real flops per "
                                              "complex MAC; value and algorithmic_TFLOPs count 8)"
                                              if m3 else "4-multiplication form (BLAS rounding)"),
-                         "gemm_with_reduce_ms_avg": round(gemm_ms / max(gemm_calls, 1), 4)},
+                         "gemm_with_reduce_ms_avg": round(gemm_ms / max(gemm_calls, 1), 4),
+                         "shader_clock_GHz": shader_ghz,
+                         "shader_clock_source": ("s_memtime / s_memrealtime of workgroup 0 over "
+                                                 "%d timed GEMM launches" % clk_launches)},
             "cpu_baseline": base,
         }
         line.update(scaling_fields)

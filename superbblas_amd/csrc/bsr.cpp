@@ -33,13 +33,11 @@ struct BsrComp {
     const void *kron = nullptr; // Kronecker matrices (user memory, device)
     int nnz_per_row = -1;
     std::vector<int> h_rowptr, h_jj; // host copies of the pattern (for the transposed operator)
-    // site tiles of the 3x3 9-point kernel (bsr_ell9_tile_kernel): one device buffer holding
-    // rows [chunks][16], distinct block columns [chunks][umax], slots [chunks][16][9]
-    void *tile_buf = nullptr;
-    const int *tile_rows = nullptr, *tile_uniq = nullptr;
-    const unsigned char *tile_loc = nullptr;
-    int tile_umax = 0;
-    long tile_chunks = 0;
+    // site tiles of the 3x3 9-point kernels (bsr_ell9_tile_kernel): per schedule one device
+    // buffer holding rows [chunks][tt], distinct block columns [chunks][umax], slots [chunks][tt][9]
+    // ([0] 16-site tiles, [1] 8-site tiles)
+    void *tile_buf[2] = {nullptr, nullptr};
+    TileSched tiles[2];
     void *owned_v = nullptr;         // values owned by the operator (transposed operator, or
                                      // the device copy of a host component's values)
     void *owned_kron = nullptr;      // device copy of a host component's Kronecker matrices
@@ -70,7 +68,8 @@ struct BsrOp {
             if (c.jj) (void)hipFree(c.jj);
             if (c.owned_v) (void)hipFree(c.owned_v);
             if (c.owned_kron) (void)hipFree(c.owned_kron);
-            if (c.tile_buf) (void)hipFree(c.tile_buf);
+            for (void *b : c.tile_buf)
+                if (b) (void)hipFree(b);
             if (c.kron_perm) (void)hipFree(c.kron_perm);
             if (c.kron_terms) (void)hipFree(c.kron_terms);
             if (c.kron_xor) (void)hipFree(c.kron_xor);
@@ -82,13 +81,14 @@ namespace {
 
 /// The site-tile schedule of a 3x3-block operator with 9 nonzero blocks per row (the 9-point
 /// stencils): the block rows are the component's image sites (SlowToFast over the image dims
-/// without the block dims), grouped into tiles of up to 16 sites -- 2 along each of the fastest
-/// dims, 2x2x2x2 on a 4-d lattice -- visited with the fastest tile coordinate fastest; per tile
-/// its rows, its distinct block columns and the slot of each nonzero block among them.  Any
-/// pattern is valid (a tile whose columns are scattered only stages more rows); no schedule when
-/// a tile has more than 116 distinct columns (the kernel's LDS budget).
-void build_tile_schedule(BsrComp &bc, const Coor &isize, const Coor &blocki) {
-    constexpr int TT = 16, NNZ = 9, UMAX_LIMIT = 116;
+/// without the block dims), grouped into tiles of up to TT sites -- 2 along each of the fastest
+/// dims, 2x2x2x2 on a 4-d lattice for TT = 16, 2x2x2 for TT = 8 -- visited with the fastest tile
+/// coordinate fastest; per tile its rows, its distinct block columns and the slot of each nonzero
+/// block among them.  Any pattern is valid (a tile whose columns are scattered only stages more
+/// rows); no schedule when a tile has more distinct columns than the kernel's LDS budget (umax_limit).
+void build_tile_schedule(BsrComp &bc, const Coor &isize, const Coor &blocki, int which, int TT,
+                         int UMAX_LIMIT) {
+    constexpr int NNZ = 9;
     std::vector<long> dims;
     for (std::size_t d = 0; d < isize.size(); ++d) {
         const long r = blocki[d] > 0 ? isize[d] / blocki[d] : 1;
@@ -149,16 +149,18 @@ void build_tile_schedule(BsrComp &bc, const Coor &isize, const Coor &blocki) {
         std::copy(uniq[ch].begin(), uniq[ch].end(), flat.begin() + ch * umax);
     const std::size_t b_rows = rows.size() * sizeof(int), b_uniq = flat.size() * sizeof(int);
     const std::size_t total = b_rows + b_uniq + loc.size();
-    SBX_HIP_CHECK(hipMalloc(&bc.tile_buf, total));
-    char *b = (char *)bc.tile_buf;
+    SBX_HIP_CHECK(hipMalloc(&bc.tile_buf[which], total));
+    char *b = (char *)bc.tile_buf[which];
     SBX_HIP_CHECK(hipMemcpy(b, rows.data(), b_rows, hipMemcpyHostToDevice));
     SBX_HIP_CHECK(hipMemcpy(b + b_rows, flat.data(), b_uniq, hipMemcpyHostToDevice));
     SBX_HIP_CHECK(hipMemcpy(b + b_rows + b_uniq, loc.data(), loc.size(), hipMemcpyHostToDevice));
-    bc.tile_rows = (const int *)b;
-    bc.tile_uniq = (const int *)(b + b_rows);
-    bc.tile_loc = (const unsigned char *)(b + b_rows + b_uniq);
-    bc.tile_umax = umax;
-    bc.tile_chunks = nchunks;
+    TileSched &t = bc.tiles[which];
+    t.rows = (const int *)b;
+    t.uniq = (const int *)(b + b_rows);
+    t.loc = (const unsigned char *)(b + b_rows + b_uniq);
+    t.umax = umax;
+    t.tt = TT;
+    t.chunks = nchunks;
 }
 
 /// The XCD order of a lattice operator's block rows (bsr_kron_spin_kernel): the rows are the
@@ -440,8 +442,12 @@ BsrOp *bsr_create(int nd, int ni, int dtype, const std::vector<std::vector<Range
         if (!op->is_kron) {
             bc.h_rowptr = std::move(rowptr);
             bc.h_jj = std::move(hjj);
-            if (bi == 3 && bd == 3 && bc.nnz_per_row == 9 && dtype == SBX_CDOUBLE)
-                build_tile_schedule(bc, ri.size, blocki);
+            if (bi == 3 && bd == 3 && bc.nnz_per_row == 9 && dtype == SBX_CDOUBLE) {
+                // (the kernels' LDS budgets: 16 sites x 8 columns up to 116 staged rows, 8 sites
+                // x 16 columns up to 80)
+                build_tile_schedule(bc, ri.size, blocki, 0, 16, 116);
+                build_tile_schedule(bc, ri.size, blocki, 1, 8, 80);
+            }
         }
         op->comps.push_back(bc);
     }
@@ -889,11 +895,8 @@ void bsr_krylov(const BsrOp &op, const Scalar &alpha, const std::string &oi,
                 d.ncols = volC;
                 d.alpha = pw == 0 ? alpha : Scalar{1, 0};
                 d.add = plans[comm.rank][c].ydirect ? !beta.is_zero() : false;
-                d.tile_rows = bc.tile_rows;
-                d.tile_uniq = bc.tile_uniq;
-                d.tile_loc = bc.tile_loc;
-                d.tile_umax = bc.tile_umax;
-                d.tile_chunks = bc.tile_chunks;
+                d.tiles[0] = bc.tiles[0];
+                d.tiles[1] = bc.tiles[1];
                 if (op.is_kron) {
                     d.ki = (int)volume(op.kroni);
                     d.kd = (int)volume(op.krond);

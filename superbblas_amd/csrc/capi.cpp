@@ -55,6 +55,20 @@ using namespace sbx;
 
 namespace {
 
+/// Device of the last host-context detail call (tune key "detail.last_device", for the tests)
+int g_detail_last_device = -1;
+
+/// The calling thread's current device.  A detail call whose operands are all host memory runs
+/// there (the reference runs such calls on the CPU of the calling rank, platform.h:757-816; here
+/// they are mirrored through the GPU the caller selected, as pick_device does for the main path
+/// through the communicator's device, and never silently on device 0)
+int current_device() {
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess || d < 0) d = 0;
+    return d;
+}
+
+
 thread_local std::string g_last_error;
 
 template <typename F> int guard(F &&f) {
@@ -440,6 +454,11 @@ int sbx_tune_set(const char *key, long long value) {
         else if (k == "gemm.splits") g_gemm_tune.splits = (int)value;
         else if (k == "gemm.t48") g_gemm_tune.t48 = (int)value;
         else if (k == "gemm.share_ab") g_gemm_tune.share_ab = (int)value;
+        else if (k == "gemm.clock") {
+            g_gemm_tune.clock = (int)value;
+            unsigned long long v[3];
+            gemm_clock_read(current_device(), v, true); // a new measurement starts at zero
+        }
         else if (k == "dist.reduce") g_dist_reduce = (int)value;
         else if (k == "debug.level") g_debug_level = (int)value;
         else if (k == "debug.corrupt_copy") g_debug_corrupt = (int)value;
@@ -498,12 +517,19 @@ int sbx_tune_get(const char *key, long long *value) {
         else if (k == "gemm.splits") *value = g_gemm_tune.splits;
         else if (k == "gemm.t48") *value = g_gemm_tune.t48;
         else if (k == "gemm.share_ab") *value = g_gemm_tune.share_ab;
+        else if (k == "gemm.clock") *value = g_gemm_tune.clock;
+        else if (k == "gemm.clock_cycles" || k == "gemm.clock_ticks" || k == "gemm.clock_launches") {
+            unsigned long long v[3];
+            gemm_clock_read(current_device(), v, false);
+            *value = (long long)v[k == "gemm.clock_cycles" ? 0 : k == "gemm.clock_ticks" ? 1 : 2];
+        }
         else if (k == "dist.reduce") *value = g_dist_reduce;
         else if (k == "debug.level") *value = g_debug_level;
         else if (k == "debug.corrupt_copy") *value = g_debug_corrupt;
         else if (k == "dist.reduce_calls") *value = g_dist_reduce_calls;
         else if (k == "dist.force_peer") *value = g_dist_force_peer;
         else if (k == "dist.peer_copies") *value = g_dist_peer_copies;
+        else if (k == "detail.last_device") *value = g_detail_last_device;
         else if (k.compare(0, 6, "alloc.") == 0) alloc_tune(key, value, nullptr);
         else throw Error("tune_get: unknown key " + k);
     });
@@ -1208,7 +1234,7 @@ namespace {
 bool on_host(const sbx_context &c) { return c.plat != SBX_GPU; }
 
 /// The one device an entry point runs on: the device of its GPU operands (all must agree), or
-/// device 0 when every operand is host memory
+/// the calling thread's current device when every operand is host memory
 int single_device(std::initializer_list<sbx_context> ctxs, const char *what) {
     int dev = -1;
     for (const auto &c : ctxs) {
@@ -1218,7 +1244,8 @@ int single_device(std::initializer_list<sbx_context> ctxs, const char *what) {
             throw Error(std::string(what) + ": operands on different devices are not supported");
         dev = c.device;
     }
-    return dev < 0 ? 0 : dev;
+    if (dev < 0) g_detail_last_device = dev = current_device();
+    return dev;
 }
 
 /// Largest index of an index vector (read from the host or the device)
@@ -1369,7 +1396,7 @@ int sbx_xgemm_batch_strided_ctx(int t, char transa, char transb, int m, int n, i
     const void *da = nullptr, *db = nullptr;
     void *dc = nullptr;
     long span_c = 0;
-    const int dev = 0;
+    const int dev = g_detail_last_device = current_device();
     const int rc = guard([&] {
         const std::size_t es = dtype_size(t);
         const bool na = transa == 'n' || transa == 'N', nb = transb == 'n' || transb == 'N';

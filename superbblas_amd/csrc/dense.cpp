@@ -158,7 +158,10 @@ void dense_inversion(const DistTensor &v, const std::string &orows, const std::s
     DistTensor wi = w.t;
     if (dense_wave_rows(w.n)) {
         // the small-matrix wave kernels read a matrix whole before writing its inverse: inverted in
-        // place, no copy of the factors (a failed matrix is left as it was)
+        // place, no copy of the factors.  A singular matrix is left as it was, but unlike the
+        // reference (which inverts a copy, dense.h:1268-1290) the other matrices of the batch
+        // already hold their inverses when the error is thrown -- the same divergence as the
+        // Cholesky note above
         for (std::size_t c = 0; c < w.t.ptr.size(); ++c) {
             const long k = w.n ? volume(w.t.ranges[comm.rank][c].size) / (w.n * w.n) : 0;
             check_info(launch_gesv(v.dtype, w.t.ptr[c], w.n, k, w.t.ptr[c], w.n, true, Scalar{1, 0},
@@ -252,7 +255,10 @@ void dense_solve(bool gesm, const Scalar &alpha, const DistTensor &c, const std:
         auto orient = [&](const DistTensor &v, const std::string &l) {
             int o = v.labels == ot + l + on ? 1 : v.labels == ot + on + l ? 2 : 0;
             if (!o || !v.mask.empty()) return 0;
-            for (std::size_t r = 0; r < v.ranges.size(); ++r)
+            for (std::size_t r = 0; r < v.ranges.size(); ++r) {
+                // another rank's component count is checked only here (the generic path throws
+                // on it later): decline the direct path rather than index past C's ranges
+                if (r >= c.ranges.size() || v.ranges[r].size() != c.ranges[r].size()) return 0;
                 for (std::size_t j = 0; j < v.ranges[r].size(); ++j) {
                     const Range &q = v.ranges[r][j], &qc = c.ranges[r][j];
                     if (volume(q.size) == 0 && volume(qc.size) == 0) continue;
@@ -266,6 +272,7 @@ void dense_solve(bool gesm, const Scalar &alpha, const DistTensor &c, const std:
                         }
                     }
                 }
+            }
             return o;
         };
         const int ox = orient(x, lx), oy = orient(y, ly);

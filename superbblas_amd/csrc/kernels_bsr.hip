@@ -42,11 +42,8 @@ struct BsrArgs {
     int add;
     int ilv = 1; // bsr_ell9_kernel: an XCD's chunks visited as ilv interleaved parts
     int nt = 0;  // the value stream's LDS-DMA loads non-temporal: g_bsr_tune.nt's kernel bits
-    // site tiles (bsr_ell9_tile_kernel; t_rows == nullptr: none)
-    const int *t_rows = nullptr, *t_uniq = nullptr;
-    const unsigned char *t_loc = nullptr;
-    int t_umax = 0;
-    long t_chunks = 0;
+    // site tiles (bsr_ell9_tile_kernel; [0] 16-site, [1] 8-site tiles; rows == nullptr: none)
+    TileSched tiles[2];
 };
 
 template <typename E, int BI_, int BD_, bool YROW, bool XROW>
@@ -822,18 +819,26 @@ __global__ void __launch_bounds__(NT) bsr_ell9_kernel(const BsrArgs p, int rb) {
 
 // Site tiles with their halo in LDS (3x3 complex<double> blocks, 9 per row, many rhs columns;
 // row-major x and y).  The rows are grouped into tiles of up to TT lattice sites (the host's
-// schedule, bsr.cpp: 2x2x2x2 on a 4-d lattice) and a tile's distinct x rows -- its own sites and
-// their halo, UMAX at most -- are staged once per slice of NS rhs columns into LDS by LDS-DMA
-// (each x row 3 colours x NS columns, 128-byte runs), so the nine neighbours of every row are
-// read from LDS instead of nine gathers through the vector-memory path (5 staged rows per site
-// instead of 9 fetched ones on the 9-point stencil).  The tile's values (TT x 9 blocks) are
-// staged once and reused by every slice.  Thread (site s, colour i, column e) of 16 x 3 x 8.
-constexpr int TILE_T = 16;
-
+// schedule, bsr.cpp: 2x2x2x2 on a 4-d lattice for TT = 16, 2x2x2 for TT = 8) and a tile's distinct
+// x rows -- its own sites and their halo, umax at most -- are staged once per slice of NS rhs
+// columns into LDS by LDS-DMA (each x row 3 colours x NS columns, NS * 16-byte runs), so the nine
+// neighbours of every row are read from LDS instead of nine gathers through the vector-memory
+// path (5 staged rows per site instead of 9 fetched ones on the 9-point stencil at TT = 16, 6 at
+// TT = 8).  The tile's values (TT x 9 blocks) are staged once and reused by every slice.  Thread
+// (site s, colour i, column e) of TT x 3 x NS.
+//
+// LDS banks (ds_read_b128 serves a wave in four 16-lane groups, MI355X_MICROARCH.md LDS): the x
+// piece (slot u, colour d, column e) sits at 16-byte unit u * 3 NS + d NS + e, whose 16-byte bank
+// group is (u * 3 NS + d NS + e) mod 16.  NS = 8 (TT = 16): that is 8 ((u + d) mod 2) + e, so two
+// sites of one lane group whose neighbour slots have the same parity read the same 8 bank groups:
+// 2-way conflicts that depend on the schedule (round 5: 12.6 M conflict cycles per launch at 16^4,
+// n = 64).  NS = 16 (TT = 8): the bank group is e alone, and the lane map (s, i, e) puts two sites
+// in a lane group only with complementary column sets ({0-3, 12-15} against {4-11}), so no read
+// of x conflicts whatever the slots; the colours of a site read the same piece (a broadcast).
 struct TileArgs {
-    const int *rows;          // [chunk][TILE_T] block rows of the tile (-1: none)
+    const int *rows;          // [chunk][TT] block rows of the tile (-1: none)
     const int *uniq;          // [chunk][umax] first domain row of each distinct block column (-1: none)
-    const unsigned char *loc; // [chunk][TILE_T][9] slot of each nonzero block in uniq (255: skip)
+    const unsigned char *loc; // [chunk][TT][9] slot of each nonzero block in uniq (255: skip)
     int umax;
 };
 
@@ -854,13 +859,20 @@ __device__ __forceinline__ void dma16_lane(const void *src, unsigned m0, bool nt
                      : "memory", "m0");
 }
 
-// Thread (site s, colour i, rhs column e) of 16 x 3 x 8.  A slice's y stores are issued after
+// the x DMA passes of a slice: umax * 3 * NS pieces over TT * 3 * NS lanes (the launcher bounds umax)
+template <int TT, int NS> struct TileForm {
+    static constexpr int NT = TT * 3 * NS;
+    static constexpr int UMAX = TT == 16 ? 128 : 80;
+    static constexpr int MAXP = (UMAX * 3 * NS + NT - 1) / NT;
+};
+
+// Thread (site s, colour i, rhs column e) of TT x 3 x NS.  A slice's y stores are issued after
 // the next slice's DMA, so the wait for that DMA (vmcnt(1)) leaves them in flight.
-template <bool BIMF>
-__global__ void __launch_bounds__(TILE_T * 3 * 8) bsr_ell9_tile_kernel(const BsrArgs p, const TileArgs t, int nchunks) {
+template <bool BIMF, int TT, int NS>
+__global__ void __launch_bounds__(TT * 3 * NS) bsr_ell9_tile_kernel(const BsrArgs p, const TileArgs t, int nchunks) {
     typedef double2 E;
-    constexpr int NS = 8, NNZ = 9, VP = TILE_T * NNZ * 9, NT = TILE_T * 3 * NS; // value pieces (16 B)
-    constexpr int MAXP = 8; // x DMA passes: umax * 3 * NS <= MAXP * NT (launcher: umax <= 128)
+    constexpr int NNZ = 9, VP = TT * NNZ * 9, NT = TileForm<TT, NS>::NT; // value pieces (16 B)
+    constexpr int MAXP = TileForm<TT, NS>::MAXP;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     E *vals = (E *)smem;
     E *xs = vals + VP;
@@ -871,9 +883,9 @@ __global__ void __launch_bounds__(TILE_T * 3 * 8) bsr_ell9_tile_kernel(const Bsr
     const int chunk = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
     if (chunk >= nchunks) return;
     const int umax = t.umax, XP = umax * 3 * NS; // x pieces of a slice
-    const int *rows = t.rows + (long)chunk * TILE_T;
+    const int *rows = t.rows + (long)chunk * TT;
     const int *uq = t.uniq + (long)chunk * umax;
-    const unsigned char *lc = t.loc + (long)chunk * TILE_T * NNZ;
+    const unsigned char *lc = t.loc + (long)chunk * TT * NNZ;
     const unsigned vbase = lds_u32(vals), xbase = lds_u32(xs);
     // the values of the tile's rows (read once: nt)
     const E *v = (const E *)p.v;
@@ -940,24 +952,35 @@ __global__ void __launch_bounds__(TILE_T * 3 * 8) bsr_ell9_tile_kernel(const Bsr
     }
 }
 
-/// false: no tile schedule, not this shape, or bsr.tile off
-bool launch_ell9_tile(const BsrArgs &a, const TileArgs &t, long nchunks, bool yrow, bool xrow, hipStream_t s) {
-    constexpr int NS = 8;
-    if (!t.rows || !yrow || !xrow || g_bsr_tune.tile != 1 || a.ncols % NS != 0 || t.umax < 1 ||
-        t.umax > 128 || nchunks >= (1L << 31) || a.ldx < a.ncols || a.ldy < a.ncols ||
+/// false: no tile schedule, not this shape, or bsr.tile off.  bsr.tile 1: 16-site tiles, slices
+/// of 8 columns (schedule 0); 2: 8-site tiles, slices of 16 columns (schedule 1)
+bool launch_ell9_tile(const BsrArgs &a, bool yrow, bool xrow, hipStream_t s) {
+    const int form = g_bsr_tune.tile;
+    if (form != 1 && form != 2) return false;
+    const TileSched &ts = a.tiles[form - 1];
+    const int NS = form == 1 ? 8 : 16, TT = form == 1 ? 16 : 8;
+    const int umax_cap = form == 1 ? TileForm<16, 8>::UMAX : TileForm<8, 16>::UMAX;
+    if (!ts.rows || ts.tt != TT || !yrow || !xrow || a.ncols % NS != 0 || ts.umax < 1 ||
+        ts.umax > umax_cap || ts.chunks >= (1L << 31) || a.ldx < a.ncols || a.ldy < a.ncols ||
         a.x_rows <= 0 || a.x_rows * a.ldx >= (1L << 32))
         return false;
-    const long vp = TILE_T * 9L * 9, xp = t.umax * 3L * NS;
+    const TileArgs t{ts.rows, ts.uniq, ts.loc, ts.umax};
+    const long vp = TT * 9L * 9, xp = ts.umax * 3L * NS;
     const size_t lds = (size_t)(vp + xp) * 16;
     // the DMA passes write lanes L < vp (values) and L < xp (x) only
     check_dma_lds("bsr_ell9_tile_kernel", lds, 1, vp + xp);
-    g_bsr_tune.last = 4;
+    g_bsr_tune.last = form == 1 ? 4 : 13;
     KernelTimer timer("bsr", s);
     auto go = [&](auto kern) {
-        hipLaunchKernelGGL(kern, dim3((unsigned)nchunks), dim3(TILE_T * 3 * NS), lds, s, a, t, (int)nchunks);
+        hipLaunchKernelGGL(kern, dim3((unsigned)ts.chunks), dim3(TT * 3 * NS), lds, s, a, t, (int)ts.chunks);
     };
-    if (a.block_im_fast) go(bsr_ell9_tile_kernel<true>);
-    else go(bsr_ell9_tile_kernel<false>);
+    if (form == 1) {
+        if (a.block_im_fast) go(bsr_ell9_tile_kernel<true, 16, 8>);
+        else go(bsr_ell9_tile_kernel<false, 16, 8>);
+    } else {
+        if (a.block_im_fast) go(bsr_ell9_tile_kernel<true, 8, 16>);
+        else go(bsr_ell9_tile_kernel<false, 8, 16>);
+    }
     SBX_HIP_CHECK(hipGetLastError());
     return true;
 }
@@ -1342,7 +1365,7 @@ void launch_ell(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_t s) 
     }
     if constexpr (std::is_same<E, double2>::value && BI == 3 && BD == 3) {
         if (nnz == 9 && g_bsr_tune.variant != 1 && g_bsr_tune.tile && a.ncols >= g_bsr_tune.tile_min_cols &&
-            launch_ell9_tile(a, TileArgs{a.t_rows, a.t_uniq, a.t_loc, a.t_umax}, a.t_chunks, yrow, xrow, s))
+            launch_ell9_tile(a, yrow, xrow, s))
             return;
     }
     // (the row-chunk kernel takes at most 2 x 256 rhs columns per workgroup row)
@@ -1465,11 +1488,8 @@ void launch_bsr(const BsrDesc &d, int device) {
     a.add = d.add ? 1 : 0;
     a.ilv = 2; // an XCD's row chunks visited as two interleaved halves (bsr_ell9_kernel)
     a.nt = g_bsr_tune.nt;
-    a.t_rows = d.tile_rows;
-    a.t_uniq = d.tile_uniq;
-    a.t_loc = d.tile_loc;
-    a.t_umax = d.tile_umax;
-    a.t_chunks = d.tile_chunks;
+    a.tiles[0] = d.tiles[0];
+    a.tiles[1] = d.tiles[1];
     switch (d.t) {
     case SBX_CDOUBLE: return launch_typed<double2>(a, d.num_nnz_per_row, d.y_row_major, d.x_row_major, s);
     case SBX_CFLOAT: return launch_typed<float2>(a, d.num_nnz_per_row, d.y_row_major, d.x_row_major, s);

@@ -663,11 +663,18 @@ __global__ void __launch_bounds__(256) trsm_wave_kernel(const E *a, int n, long 
     const E *U = a + mi * n * n;
     E *X = x + mi * n * m;
     // the reciprocals of U's diagonal: when the matrix has at least n lanes, lane q of the matrix
-    // computes 1 / U(q, q) and the others read it (one reciprocal per lane instead of n divisions)
+    // computes 1 / U(q, q) and the others read it (one reciprocal per lane instead of n
+    // divisions).  The shuffles happen here, before the loop over right-hand sides, while every
+    // lane of the matrix is still active: with m > 64 the last pass leaves lanes l >= m % 64
+    // idle, and a cross-lane read from an idle lane is undefined.
     const int mp = m <= 64 ? (int)m : 64, base = m <= 64 ? s * (int)m : 0, tl = lane - base;
     const bool shared = mp >= n;
     const E rinv = O::inv(U[(tl < n ? tl : 0) * (n + 1)]);
-    auto dinv = [&](int r) { return shared ? wshfl<E>(rinv, base + r) : O::inv(U[r + r * n]); };
+    E dv[WNM];
+#pragma unroll
+    for (int r = 0; r < WNM; ++r)
+        dv[r] = r < n ? (shared ? wshfl<E>(rinv, base + r) : O::inv(U[r + r * n])) : O::real(0);
+    auto dinv = [&](int r) { return dv[r]; };
     for (long t = m <= 64 ? lane - (long)s * m : lane; t < m; t += (m <= 64 ? m : 64)) {
         Col<E, WNM> v;
         const long base = left ? t * n : t, st = left ? 1 : m;

@@ -524,7 +524,7 @@ __global__ void __launch_bounds__(WM *WN *KG * 64) gemm_dma_kernel(const GemmKAr
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     unsigned long long clk0 = 0, rt0 = 0;
-    if (p.probe && (bid == 0 || p.probe_all)) {
+    if (p.probe && (bid == 0 || p.probe_all > 0)) {
         clk0 = __builtin_amdgcn_s_memtime();
         rt0 = __builtin_amdgcn_s_memrealtime();
     }
@@ -830,10 +830,18 @@ __global__ void __launch_bounds__(WM *WN *KG * 64) gemm_dma_kernel(const GemmKAr
     if (p.probe && bid == 0 && tid == 0) {
         const unsigned long long clk1 = __builtin_amdgcn_s_memtime();
         const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
-        p.probe[0] = clk1 - clk0; // shader clock cycles
-        p.probe[1] = rt1 - rt0;   // 100 MHz reference ticks
+        if (p.probe_all < 0) {
+            // the library's clock meter (tune "gemm.clock"): summed over launches with vector
+            // atomics -- shader clock cycles, 100 MHz reference ticks, launches
+            atomicAdd(&p.probe[0], clk1 - clk0);
+            atomicAdd(&p.probe[1], rt1 - rt0);
+            atomicAdd(&p.probe[2], 1ull);
+        } else {
+            p.probe[0] = clk1 - clk0; // shader clock cycles
+            p.probe[1] = rt1 - rt0;   // 100 MHz reference ticks
+        }
     }
-    if (p.probe && p.probe_all && tid == 0) {
+    if (p.probe && p.probe_all > 0 && tid == 0) {
         p.probe[2 + 3 * bid] = rt0;
         p.probe[3 + 3 * bid] = __builtin_amdgcn_s_memrealtime();
     }
@@ -1353,6 +1361,33 @@ void launch_tiled_cfg(const GemmKArgs &p0, int device, hipStream_t stream, long 
     launch_reduce<R, CPLX>(p, stream);
 }
 
+/// The clock meter of the LDS-DMA kernel (tune key "gemm.clock" > 0): workgroup 0 of every
+/// launch adds its s_memtime (shader clock) and s_memrealtime (100 MHz) spans and a launch count
+/// into three counters per device, read back by "gemm.clock_cycles" / "gemm.clock_ticks" /
+/// "gemm.clock_launches" -- the clock the GEMMs ran at, so that a slower box can be told apart
+/// from a slower kernel (one thread's three atomics per launch)
+static unsigned long long *g_clock_meter[64];
+
+unsigned long long *gemm_clock_meter(int device) {
+    if (g_gemm_tune.clock <= 0 || device < 0 || device >= 64) return nullptr;
+    if (!g_clock_meter[device]) {
+        void *ptr = nullptr;
+        SBX_HIP_CHECK(hipMalloc(&ptr, 3 * sizeof(unsigned long long)));
+        SBX_HIP_CHECK(hipMemset(ptr, 0, 3 * sizeof(unsigned long long)));
+        g_clock_meter[device] = (unsigned long long *)ptr;
+    }
+    return g_clock_meter[device];
+}
+
+void clock_read_impl(int device, unsigned long long out[3], bool reset) {
+    out[0] = out[1] = out[2] = 0;
+    if (device < 0 || device >= 64 || !g_clock_meter[device]) return;
+    SBX_HIP_CHECK(hipDeviceSynchronize());
+    SBX_HIP_CHECK(hipMemcpy(out, g_clock_meter[device], 3 * sizeof(unsigned long long),
+                            hipMemcpyDeviceToHost));
+    if (reset) SBX_HIP_CHECK(hipMemset(g_clock_meter[device], 0, 3 * sizeof(unsigned long long)));
+}
+
 /// Launch one tile configuration of the LDS-DMA kernel
 template <typename R, bool CPLX, bool AK, bool BK, int BM, int BN, int BKK, int WM, int WN,
           bool ALLOW_M3 = true, bool PF = false, int KG = 1, bool SH = false, int LW = 0, int SP = 1>
@@ -1373,6 +1408,10 @@ void launch_dma_cfg(const GemmKArgs &p0, int device, hipStream_t stream, long sp
                                                                    target_wgs, work, device);
     if (SH && !(p.same_ab && p.tm == 1 && p.tn == 1))
         throw Error("gemm: internal error, shared slab image for a launch with off-diagonal tiles");
+    if (unsigned long long *meter = gemm_clock_meter(device)) {
+        p.probe = meter;
+        p.probe_all = -1;
+    }
     KernelTimer total("gemm_total", stream);
     {
         KernelTimer timer("gemm", stream);
@@ -1588,9 +1627,11 @@ template <typename R, bool CPLX> bool launch_skinny(const GemmKArgs &p0, int dev
         launch_reduce<R, CPLX>(p, s);
         return true;
     }
-    // one long output dimension, the other <= 16, and a short k (updates) or a vector
-    const bool rows = p.n <= 16 && p.m >= 2 * p.n && (p.k <= 64 || p.n == 1);
-    const bool cols = p.m <= 16 && p.n >= 2 * p.m && (p.k <= 64 || p.m == 1);
+    // one long output dimension, the other <= 16, and a short k (updates): a lane per output
+    // row walks k serially, so a long k (a gemv such as V^H w over a local volume) stays on the
+    // split-K MFMA tiles
+    const bool rows = p.n <= 16 && p.m >= 2 * p.n && p.k <= 64;
+    const bool cols = p.m <= 16 && p.n >= 2 * p.m && p.k <= 64;
     if (!rows && !cols) return false;
     if (!rows) { // C^T = op(B)^T op(A)^T: the long dimension becomes the rows
         std::swap(p.m, p.n);
@@ -1685,6 +1726,10 @@ GemmKArgs make_args(const GemmDesc &d) {
 }
 
 } // namespace
+
+void gemm_clock_read(int device, unsigned long long out[3], bool reset) {
+    clock_read_impl(device, out, reset);
+}
 
 void launch_gemm(const GemmDesc &d, int device) {
     if (d.m == 0 || d.n == 0 || d.batch == 0) return;

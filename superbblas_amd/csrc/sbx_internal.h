@@ -252,7 +252,11 @@ struct GemmTune {
     int dma_nt = 0;     ///< ... with the non-temporal policy (0 = the default policy)
     int skinny = 1; ///< outputs with a dimension of <= 4 (and <= 16 with a short k): the dot / rows
                     ///< kernels instead of MFMA tiles (0 = off)
+    int clock = 0; ///< LDS-DMA kernel clock meter (gemm_clock_meter, kernels_gemm.hip; 0 = off)
 };
+/// The LDS-DMA GEMM's clock meter of a device: {shader clock cycles, 100 MHz ticks, launches}
+/// summed since the last reset (zeros when the meter was never enabled)
+void gemm_clock_read(int device, unsigned long long out[3], bool reset);
 extern GemmTune g_gemm_tune;
 struct BsrTune {
     int variant = 0; ///< BSR kernels: 0 = the library's choice, 1 = the generic kernels only (no 9-point
@@ -279,9 +283,11 @@ struct BsrTune {
     int kron_order = 1;          ///< ... rows in the operator's XCD order (bsr.cpp build_kron_order)
     int blk_pd = 1; ///< 12x12 blocks by LDS-DMA: blocks in flight ahead of the one in use (1..3)
     int tile = 0;   ///< 9-point 3x3 complex<double> operators, row-major x and y: site tiles with
-                    ///< their halo staged in LDS (bsr_ell9_tile_kernel) ... (opt-in: 16^4 n = 64
-                    ///< 180 vs 169 us for the row-chunk kernel)
-    long tile_min_cols = 33; ///< ... from this many rhs columns (a multiple of 8)
+                    ///< their halo staged in LDS (bsr_ell9_tile_kernel) ... 1: 16-site tiles, slices
+                    ///< of 8 rhs columns (opt-in: 16^4 n = 64 180 vs 169 us for the row-chunk kernel,
+                    ///< DESIGN 5.3 round 5); 2: 8-site tiles, slices of 16 columns (no LDS bank
+                    ///< conflicts whatever the slots, round 6)
+    long tile_min_cols = 33; ///< ... from this many rhs columns (a multiple of 8, or 16 for tile 2)
     int nt = 11; ///< the value stream's LDS-DMA loads with the non-temporal (streaming) policy, per
                 ///< kernel: 1 12x12 blocks by LDS-DMA, 2 3x3 row chunks, 4 3x3 split rows, 8 3x3 one
                 ///< thread per block.  Default 1 | 2 | 8 (tools/bsr_bound.py NTS, warm, interleaved:
@@ -293,6 +299,7 @@ struct BsrTune {
     /// 5 Kronecker on MFMA, 6 the same with packed column slots, 7 12x12 blocks by LDS-DMA, 8 the
     /// same with packed slots, 9 Kronecker spin first (VALU), 10 12x12 fragment gathers (9 blocks
     /// per row), 11 12x12 generic rows, 12 Kronecker spin first with XOR-partner spin rows,
+    /// 13 site tiles of 8 sites and 16 columns (3x3),
     /// 0 another kernel
     std::atomic<int> last{0};
 };
@@ -333,6 +340,16 @@ void launch_index_copy(const IndexCopyDesc &d, int device);
 
 /// BSR SpMM on one component (reference bsr.h:535-650 builtin loop, bsr.h:855-928 GPU):
 ///   y[row-block i] = alpha * sum_{j in row i} V_j * x[jj_j],  for every rhs column
+/// A site-tile schedule of a 3x3 9-point operator (bsr.cpp build_tile_schedule): per tile of up
+/// to tt sites its block rows [chunks][tt] (-1: none), its distinct block columns [chunks][umax]
+/// (-1: none) and the slot of each nonzero block among them [chunks][tt][9] (255: skip)
+struct TileSched {
+    const int *rows = nullptr, *uniq = nullptr;
+    const unsigned char *loc = nullptr;
+    int umax = 0, tt = 0;
+    long chunks = 0;
+};
+
 struct BsrDesc {
     int t;
     long block_rows; ///< number of block rows
@@ -359,11 +376,9 @@ struct BsrDesc {
     const int *kron_perm = nullptr; ///< block row per row slot in the XCD order (nullptr: none)
     const void *kron_terms = nullptr; ///< spin rows as two terms (nullptr: a row has more nonzeros)
     const void *kron_xor = nullptr;   ///< spin rows as diagonal + XOR partner (nullptr: not of that form)
-    // site tiles of 3x3 9-point operators (bsr.cpp build_tile_schedule; tile_rows == nullptr: none)
-    const int *tile_rows = nullptr, *tile_uniq = nullptr;
-    const unsigned char *tile_loc = nullptr;
-    int tile_umax = 0;
-    long tile_chunks = 0;
+    // site tiles of 3x3 9-point operators (bsr.cpp build_tile_schedule): [0] 16-site tiles (the
+    // 8-column kernel), [1] 8-site tiles (the 16-column kernel); rows == nullptr: none
+    TileSched tiles[2];
 };
 void launch_bsr(const BsrDesc &d, int device);
 void launch_bsr_kron(const BsrDesc &d, int device);

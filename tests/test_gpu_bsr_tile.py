@@ -16,6 +16,10 @@ from _common import stencil_jj
 pytestmark = pytest.mark.gpu
 
 TILE, ROWS = 4, 3  # bsr.last_kernel: site tiles, row chunks
+# (bsr.tile form, bsr.last_kernel): 16-site tiles with slices of 8 columns, 8-site tiles with
+# slices of 16 columns (round 6: no LDS bank conflicts whatever the slots)
+FORMS = [(1, TILE), (2, 13)]
+FORM_IDS = ["tile16x8", "tile8x16"]
 
 
 def run_tile(gpu, dims, ncols, alpha=1.0, beta=0.0, y_layout="row", kind="stencil", cut=None,
@@ -70,26 +74,33 @@ def run_tile(gpu, dims, ncols, alpha=1.0, beta=0.0, y_layout="row", kind="stenci
         assert err < 1e-13
 
 
+@pytest.mark.parametrize("form", FORMS, ids=FORM_IDS)
 @pytest.mark.parametrize("ncols", [40, 64, 128])
-def test_tile_columns(gpu, ncols):
-    run_tile(gpu, (4, 4, 4, 4), ncols, integer=True)
+def test_tile_columns(gpu, ncols, form):
+    tile, kern = form
+    ns = 8 if tile == 1 else 16
+    run_tile(gpu, (4, 4, 4, 4), ncols, integer=True, tile=tile,
+             expect=kern if ncols % ns == 0 else ROWS)
 
 
 @pytest.mark.parametrize("dims", [(3, 5, 4, 6), (2, 2, 2, 2), (5, 3, 7, 2), (1, 1, 4, 9), (6, 6, 6, 6)])
-def test_tile_ragged_lattices(gpu, dims):
+@pytest.mark.parametrize("form", FORMS, ids=FORM_IDS)
+def test_tile_ragged_lattices(gpu, dims, form):
     """extents that leave partial tiles, and lattices with fewer than four extended dims"""
-    run_tile(gpu, dims, 64)
+    run_tile(gpu, dims, 64, tile=form[0], expect=form[1])
 
 
 @pytest.mark.parametrize("alpha,beta", [(0.5 - 2j, 0.0), (1.0, 1.0), (-1.5 + 0.5j, 2.0 - 1j)])
-def test_tile_alpha_beta(gpu, alpha, beta):
-    run_tile(gpu, (4, 4, 4, 8), 48, alpha=alpha, beta=beta)
+@pytest.mark.parametrize("form", FORMS, ids=FORM_IDS)
+def test_tile_alpha_beta(gpu, alpha, beta, form):
+    run_tile(gpu, (4, 4, 4, 8), 48, alpha=alpha, beta=beta, tile=form[0], expect=form[1])
 
 
-def test_tile_cut_and_random(gpu):
+@pytest.mark.parametrize("form", FORMS, ids=FORM_IDS)
+def test_tile_cut_and_random(gpu, form):
     """column -1 blocks (the interior operator of the core / halo pair) and 9 random columns"""
-    run_tile(gpu, (4, 4, 4, 4), 64, cut=4, integer=True)
-    run_tile(gpu, (4, 4, 4, 4), 64, kind="random", seed=5, expect=None)
+    run_tile(gpu, (4, 4, 4, 4), 64, cut=4, integer=True, tile=form[0], expect=form[1])
+    run_tile(gpu, (4, 4, 4, 4), 64, kind="random", seed=5, expect=None, tile=form[0])
 
 
 def test_tile_declined_shapes(gpu):
@@ -98,6 +109,7 @@ def test_tile_declined_shapes(gpu):
     run_tile(gpu, (4, 4, 4, 4), 64, y_layout="col", expect=ROWS)
     run_tile(gpu, (4, 4, 4, 4), 44, expect=ROWS)
     run_tile(gpu, (4, 4, 4, 4), 64, tile=0, expect=ROWS)
+    run_tile(gpu, (4, 4, 4, 4), 40, tile=2, expect=ROWS)  # 16-column slices: 40 declined
 
 
 def test_tile_default_choice(gpu):
@@ -107,3 +119,4 @@ def test_tile_default_choice(gpu):
     assert sb.tune_get("bsr.tile") == 0 and sb.tune_get("bsr.tile_min_cols") == 33
     run_tile(gpu, (8, 8, 8, 8), 64, integer=True, tile=0, expect=ROWS)
     run_tile(gpu, (8, 8, 8, 8), 64, integer=True)
+    run_tile(gpu, (8, 8, 8, 8), 64, integer=True, tile=2, expect=13)

@@ -78,6 +78,18 @@ def test_trsm_right_io(gpu, dtype, cl, xl, yl, n, m, nt):
     _solve(gpu, dtype, cl, xl, yl, n, m, nt, "i", 2.0)
 
 
+@pytest.mark.parametrize("dtype", [np.complex128, np.float64])
+@pytest.mark.parametrize("side", ["j", "i"])
+@pytest.mark.parametrize("n,m", [(12, 70), (12, 129), (16, 65), (3, 200)])
+def test_trsm_many_rhs(gpu, dtype, side, n, m):
+    """more than 64 right-hand sides per matrix: the direct path declines and trsm_wave_kernel
+    loops over the right-hand sides with a lane each, the last pass leaving lanes idle
+    (0 < m % 64 < 64): the diagonal reciprocals are shared before that loop"""
+    xl, yl = ("tjr", "tir") if side == "j" else ("tri", "trj")
+    for wave in (2, 1):
+        _solve(gpu, dtype, "tij", xl, yl, n, m, 7, side, 0.5, wave=wave)
+
+
 def test_trsm_io_matches_working_copies(gpu):
     """the direct path (dense.wave 2, n <= 16, m <= 64) and the working-copy path (m > 64 rhs
     per matrix is not direct; here the same problem through dense.wave 1's LU-free small-matrix

@@ -201,11 +201,11 @@ def test_gemm_fused_splitk_sum(gpu, dtype, m, k, batch):
 
 # the skinny forms (blas.h:686-800's dot / gemv shortcuts; tests/dist.cpp:160-195's inner-product
 # m = n <= 12, k = 6144 and update m = 6144, n = k <= 12 shapes): gemm_dot_kernel for m, n <= 4,
-# gemm_rows_kernel for one dimension <= 16 (and a short k, or a vector), the transposed problem
+# gemm_rows_kernel for one dimension <= 16 and a short k (vectors with a long k: the MFMA tiles), the transposed problem
 # for a short m; the same shapes through the MFMA tiles (gemm.skinny 0) agree with the oracle too
 SKINNY = [(1, 1, 6144, 8), (2, 2, 6144, 8), (3, 4, 6000, 2), (4, 1, 100, 5), (1, 3, 7, 3),
           (6144, 1, 1, 8), (6144, 3, 3, 2), (1000, 12, 12, 2), (999, 16, 5, 1), (1, 700, 9, 2),
-          (12, 500, 12, 2), (777, 1, 300, 2), (1, 500, 301, 1)]
+          (12, 500, 12, 2), (777, 1, 300, 2), (1, 500, 301, 1), (16, 1, 1 << 16, 1)]
 
 
 @pytest.mark.parametrize("dtype", [np.complex128, np.float64, np.complex64, np.float32])
@@ -247,3 +247,38 @@ def test_gemm_loader_forms(gpu, dtype, m, n, k, batch):
         sb.tune_set("gemm.dma_spread", old_s)
     for o in outs[1:3]:
         assert np.array_equal(o, outs[0])
+
+
+def test_host_context_calls_use_current_device(gpu):
+    """detail::xgemm_batch_strided and copy_n on host (CPU-context) operands run on the calling
+    thread's current device (the reference's CPU path runs on the calling rank, platform.h:757-816),
+    not on device 0: the device used is read back through the "detail.last_device" tune key"""
+    import ctypes
+    import torch
+    import superbblas_amd as sb
+    lib, ctx = sb._lib, sb._Ctx
+    dev = torch.cuda.current_device()
+    m, n, k = 5, 3, 7
+    a = random_valued(m * k, np.complex128, 1)
+    b = random_valued(k * n, np.complex128, 2)
+    c = np.zeros(m * n, np.complex128)
+    ref = c.copy()
+    oracle_gemm("N", "N", m, n, k, 1.0, a, m, 0, b, k, 0, 0.0, ref, m, 0, 1)
+    one, zero = (ctypes.c_double * 2)(1.0, 0.0), (ctypes.c_double * 2)(0.0, 0.0)
+    vp = ctypes.c_void_p
+    rc = lib.sbx_xgemm_batch_strided_ctx(
+        3, ctypes.c_char(b"N"), ctypes.c_char(b"N"), m, n, k, one, vp(a.ctypes.data), m,
+        ctypes.c_longlong(0), vp(b.ctypes.data), k, ctypes.c_longlong(0), zero, vp(c.ctypes.data), m,
+        ctypes.c_longlong(0), 1, ctx(sb.CPU, -1))
+    assert rc == 0, sb._lib.sbx_last_error()
+    assert rel_err(c, ref) < 1e-12
+    assert sb.tune_get("detail.last_device") == dev
+    # copy_n between host buffers (through device scratch): the same device
+    src = np.arange(16, dtype=np.float64)
+    dst = np.zeros(16, np.float64)
+    rc = lib.sbx_copy_n_blocking(one, 1, vp(src.ctypes.data), ctx(sb.CPU, -1), ctypes.c_longlong(1),
+                                 None, ctx(sb.CPU, -1), ctypes.c_longlong(16), 1, vp(dst.ctypes.data),
+                                 ctx(sb.CPU, -1), None, ctx(sb.CPU, -1), 0)
+    assert rc == 0, sb._lib.sbx_last_error()
+    assert np.array_equal(dst, src)
+    assert sb.tune_get("detail.last_device") == dev
