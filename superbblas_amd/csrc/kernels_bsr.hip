@@ -603,6 +603,389 @@ __global__ void __launch_bounds__(256) bsr_mfma_dma_kernel(const BsrArgs p, unsi
     }
 }
 
+// Values in registers, x by LDS-DMA (12x12 complex blocks, ELL with NNZ blocks per row, row-major
+// x with ldx == ncols <= 16; bsr.vreg).  The LDS-DMA kernel above moves both the value block and
+// the x block of every nonzero through the LDS, and its stream alone (MFMAs and fragment reads
+// removed) ran at 5.06 TB/s on the chain's operator (profiles/r05_bsr12_no_mfma.txt) against 7.1
+// TB/s for plain non-temporal 16-byte loads with several in flight per lane
+// (tools/studies/stream_ceiling.hip read_u8nt, profiles/r06_stream_ceiling.txt).  Here the value
+// block -- 82 % of the bytes, read once -- goes straight into the MFMA fragments: lane (row r,
+// quarter kq) takes the three contiguous k = 3 kq .. 3 kq + 2 of row r (the MFMA sums over k, so
+// any k-to-(step, quarter) assignment works when the x fragment follows it), one 16-byte and one
+// 8-byte load for complex<float> (16-byte aligned by the quarter's parity), three 16-byte loads
+// for complex<double>; column-major blocks (block_im_fast) take three loads along the block row.
+// The x block (reused by nine rows: an L2 hit) is staged by LDS-DMA into the wave's ring slot as
+// before, PD blocks ahead, and read as x[3 kq + s][c].
+template <typename E> struct VregOps;
+template <> struct VregOps<float2> {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    static constexpr int NV = 2; // load instructions per block (row-major blocks)
+    template <bool NT> static __device__ __forceinline__ float2 load1(const float2 *pa) {
+        const f2 t = NT ? __builtin_nontemporal_load((const f2 *)pa) : *(const f2 *)pa;
+        return float2{t.x, t.y};
+    }
+    template <bool NT> static __device__ __forceinline__ void load3(const float2 *pa, bool even, float2 (&a)[3]) {
+        const f4 *p16 = (const f4 *)(even ? pa : pa + 1);
+        const f2 *p8 = (const f2 *)(even ? pa + 2 : pa);
+        const f4 t = NT ? __builtin_nontemporal_load(p16) : *p16;
+        const f2 u = NT ? __builtin_nontemporal_load(p8) : *p8;
+        a[0] = even ? float2{t.x, t.y} : float2{u.x, u.y};
+        a[1] = even ? float2{t.z, t.w} : float2{t.x, t.y};
+        a[2] = even ? float2{u.x, u.y} : float2{t.z, t.w};
+    }
+};
+template <> struct VregOps<double2> {
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    static constexpr int NV = 3;
+    template <bool NT> static __device__ __forceinline__ double2 load1(const double2 *pa) {
+        const d2 t = NT ? __builtin_nontemporal_load((const d2 *)pa) : *(const d2 *)pa;
+        return double2{t.x, t.y};
+    }
+    template <bool NT> static __device__ __forceinline__ void load3(const double2 *pa, bool, double2 (&a)[3]) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const d2 t = NT ? __builtin_nontemporal_load((const d2 *)(pa + q)) : *(const d2 *)(pa + q);
+            a[q] = double2{t.x, t.y};
+        }
+    }
+};
+
+template <typename R, int BI, int BD, bool YROW, int NNZ, int PD, int NXI, bool NTV, bool BIMF>
+__global__ void __launch_bounds__(256) bsr_mfma_vreg_kernel(const BsrArgs p) {
+    typedef typename BsrMfmaElem<R, true>::type E;
+    typedef typename BsrMfma<R>::acc_t acc_t;
+    static_assert(BI == 12 && BD == 12, "12x12 blocks: three k per quarter");
+    constexpr int ES = (int)sizeof(E), ABLK = BI * BD;
+    constexpr int NVI = BIMF ? 3 : VregOps<E>::NV, NI = NVI + NXI; // load instructions per block
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    E *__restrict__ y = (E *)p.y;
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const long i = (long)blockIdx.x * 4 + w;
+    if (i >= p.block_rows) return; // whole waves only: MFMA needs all 64 lanes
+    const int nc = (int)p.ncols;
+    const unsigned XB = (unsigned)(BD * nc * ES), SLOT = (XB + 15u) & ~15u;
+    const long jb = i * NNZ;
+    int dj[NNZ];
+#pragma unroll
+    for (int k = 0; k < NNZ; ++k) dj[k] = p.jj[jb + k];
+    const int ar = lane & 15, kq = lane >> 4;
+    const bool arow_ok = ar < BI, bcol_ok = ar < nc;
+    const int arc = arow_ok ? ar : BI - 1;
+    const E *vrow = (const E *)p.v + jb * ABLK;
+    const unsigned slot0 = lds_u32(smem) + (unsigned)w * (SLOT * (PD + 1));
+    E va[PD + 1][3];
+    auto issue = [&](int k) {
+        // x block of nonzero k (a skipped block, column -1, reads x's first block row: unused)
+        const unsigned base = slot0 + (unsigned)(k % (PD + 1)) * SLOT;
+        const char *xrow = (const char *)((const E *)p.x + (long)(dj[k] < 0 ? 0 : dj[k]) * nc);
+#pragma unroll
+        for (int q = 0; q < NXI; ++q) {
+            const unsigned g = (unsigned)(lane + 64 * q) * 16u;
+            if (g < XB)
+                asm volatile("s_mov_b32 m0, %1\n\t"
+                             "s_nop 0\n\t"
+                             "global_load_lds_dwordx4 %0, off"
+                             :
+                             : "v"(xrow + g), "s"(__builtin_amdgcn_readfirstlane(base + (unsigned)q * 1024u))
+                             : "memory", "m0");
+        }
+        // value block of nonzero k straight into the fragments
+        const E *vb = vrow + (long)k * ABLK;
+        E (&a)[3] = va[k % (PD + 1)];
+        if constexpr (BIMF) {
+#pragma unroll
+            for (int s = 0; s < 3; ++s) a[s] = VregOps<E>::template load1<NTV>(vb + arc + (3 * kq + s) * BI);
+        } else {
+            VregOps<E>::template load3<NTV>(vb + arc * BD + 3 * kq, (kq & 1) == 0, a);
+        }
+    };
+    acc_t accR = acc_t{0, 0, 0, 0}, accI = acc_t{0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < PD && k < NNZ; ++k) issue(k);
+#pragma unroll
+    for (int k = 0; k < NNZ; ++k) {
+        // the x slot of block k + PD was last read in iteration k - 1: its reads have returned
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (k + PD < NNZ) issue(k + PD);
+        // block k landed (x in LDS, values in registers): the NI instructions of each later
+        // block issued so far may stay in flight
+        wait_vmcnt_n(NI * (NNZ - 1 - k < PD ? NNZ - 1 - k : PD));
+        if (dj[k] < 0) continue;
+        const E *sx = (const E *)(smem + (slot0 - lds_u32(smem)) + (k % (PD + 1)) * SLOT);
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+            const E a = arow_ok ? va[k % (PD + 1)][s] : E{};
+            const E b = bcol_ok ? sx[(3 * kq + s) * nc + ar] : E{};
+            accR = BsrMfma<R>::mma(a.x, b.x, accR);
+            accI = BsrMfma<R>::mma(a.x, b.y, accI);
+            accR = BsrMfma<R>::mma(-a.y, b.y, accR);
+            accI = BsrMfma<R>::mma(a.y, b.x, accI);
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int row = BsrMfma<R>::row(lane, q);
+        if (row >= BI || !bcol_ok) continue;
+        const long img = i * BI + row;
+        E *yp = YROW ? y + img * p.ldy + ar : y + img + ar * p.ldy;
+        const E out = Ops<E>::scale(E{accR[q], accI[q]}, p.alpha_re, p.alpha_im);
+        *yp = p.add ? Ops<E>::add(*yp, out) : out;
+    }
+}
+
+/// false: not this shape
+template <typename R, int NNZ, int PD>
+bool launch_bsr_mfma_vreg(const BsrArgs &a, bool yrow, hipStream_t s) {
+    typedef typename BsrMfmaElem<R, true>::type E;
+    constexpr int ES = (int)sizeof(E);
+    const long xb = 12L * a.ncols * ES;
+    if (a.x_rows <= 0 || a.ncols < 1 || a.ncols > 16 || xb % 16 || ((size_t)a.x & 15) ||
+        ((size_t)a.v & 15))
+        return false;
+    const long blocks = (a.block_rows + 3) / 4;
+    if (blocks >= (1L << 31)) return false;
+    const int nxi = (int)((xb + 1023) / 1024);
+    const size_t lds = (size_t)4 * (PD + 1) * xb;
+    check_dma_lds("bsr_mfma_vreg_kernel", lds, 0, 0, 4L * (PD + 1) * xb);
+    g_bsr_tune.last = 14;
+    KernelTimer timer("bsr", s);
+    auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), lds, s, a); };
+    const bool nt = (a.nt & 1) != 0, bimf = a.block_im_fast != 0;
+    // (template dispatch over y's layout, the x instruction count, the value policy and layout)
+    auto pick = [&](auto yr, auto nx) {
+        constexpr bool YR = decltype(yr)::value;
+        constexpr int NX = decltype(nx)::value;
+        if (nt && !bimf) go(bsr_mfma_vreg_kernel<R, 12, 12, YR, NNZ, PD, NX, true, false>);
+        else if (!bimf) go(bsr_mfma_vreg_kernel<R, 12, 12, YR, NNZ, PD, NX, false, false>);
+        else if (nt) go(bsr_mfma_vreg_kernel<R, 12, 12, YR, NNZ, PD, NX, true, true>);
+        else go(bsr_mfma_vreg_kernel<R, 12, 12, YR, NNZ, PD, NX, false, true>);
+    };
+    using T = std::true_type;
+    using F = std::false_type;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    if (nxi == 1) yrow ? pick(T{}, I1{}) : pick(F{}, I1{});
+    else if (nxi == 2) yrow ? pick(T{}, I2{}) : pick(F{}, I2{});
+    else yrow ? pick(T{}, I3{}) : pick(F{}, I3{});
+    SBX_HIP_CHECK(hipGetLastError());
+    return true;
+}
+
+/// s_waitcnt vmcnt(n) for a wave-uniform n known only at run time (0..63; one scalar branch)
+__device__ __forceinline__ void wait_vmcnt_rt(int n) {
+#define SBX_VM(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+    switch (n) {
+        SBX_VM(0) SBX_VM(1) SBX_VM(2) SBX_VM(3) SBX_VM(4) SBX_VM(5) SBX_VM(6) SBX_VM(7)
+        SBX_VM(8) SBX_VM(9) SBX_VM(10) SBX_VM(11) SBX_VM(12) SBX_VM(13) SBX_VM(14) SBX_VM(15)
+        SBX_VM(16) SBX_VM(17) SBX_VM(18) SBX_VM(19) SBX_VM(20) SBX_VM(21) SBX_VM(22) SBX_VM(23)
+        SBX_VM(24) SBX_VM(25) SBX_VM(26) SBX_VM(27) SBX_VM(28) SBX_VM(29) SBX_VM(30) SBX_VM(31)
+        SBX_VM(32) SBX_VM(33) SBX_VM(34) SBX_VM(35) SBX_VM(36) SBX_VM(37) SBX_VM(38) SBX_VM(39)
+        SBX_VM(40) SBX_VM(41) SBX_VM(42) SBX_VM(43) SBX_VM(44) SBX_VM(45) SBX_VM(46) SBX_VM(47)
+        SBX_VM(48) SBX_VM(49) SBX_VM(50) SBX_VM(51) SBX_VM(52) SBX_VM(53) SBX_VM(54) SBX_VM(55)
+        SBX_VM(56) SBX_VM(57) SBX_VM(58) SBX_VM(59) SBX_VM(60) SBX_VM(61) SBX_VM(62) SBX_VM(63)
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+#undef SBX_VM
+}
+
+// Streaming form of the packed 12x12 kernel (bsr.stream = workgroups per CU; ELL with NNZ blocks
+// per row, row-major x with ldx == ncols <= 16, packed value + x slots).  The LDS-DMA stream
+// itself runs at 7.1 TB/s with one workgroup of 4 waves per CU and 8 one-KB pieces in flight per
+// wave, but at 5.5-5.8 TB/s with 16-32 waves per CU (tools/studies/stream_ceiling.hip dma_r8nt_w4
+// against dma_r8nt_w8 / dma_r4nt_w16, profiles/r06_stream_ceiling.txt) -- and the one-row-per-wave
+// kernel above runs 32 waves per CU with one block in flight each.  Here a few waves per CU each
+// own every W-th block row and stream their rows' nonzero blocks through a RING-slot ring of their
+// own, RING - 1 blocks ahead across row boundaries, the fragments of the next block read while
+// the current one's MFMAs run; a row's y is written after its last block.  The block
+// columns come one block ahead through scalar loads; skipped blocks (column -1) are remembered
+// in a 32-bit mask (RING <= 32).  The y stores of a row are issued after the DMA of later blocks,
+// so the per-block wait vmcnt(PK * (blocks issued after this one)) over-waits at most (never
+// under-waits).
+template <typename R, bool CPLX, int BI, int BD, bool YROW, int NNZ, int RING, int PK>
+__global__ void __launch_bounds__(256) bsr_mfma_stream_kernel(const BsrArgs p) {
+    typedef typename BsrMfmaElem<R, CPLX>::type E;
+    typedef typename BsrMfma<R>::acc_t acc_t;
+    static_assert(BI <= 16 && BD % 4 == 0 && RING >= 2 && RING <= 32 && (RING & (RING - 1)) == 0,
+                  "block shape / ring");
+    constexpr int KS = BD / 4, ES = (int)sizeof(E), ABLK = BI * BD, PD = RING - 1;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    E *__restrict__ y = (E *)p.y;
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // rows round robin over the waves (wave gw: rows gw, gw + W, ...), the waves of one XCD
+    // adjacent: at any moment the chip streams one contiguous window of the value array.  (A
+    // contiguous range of rows per wave put the waves' streams 2.65 MB apart on the chain's
+    // operator -- a multiple of 8 x 4 KB, so a few HBM channels served them all: 1.2 TB/s.)
+    const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    const long W = (long)nwg * 4, gw = (long)wg * 4 + w;
+    const long nr = gw < p.block_rows ? (p.block_rows - gw + W - 1) / W : 0;
+    const long nb = nr * NNZ;
+    if (nb <= 0) return;
+    // global block index of the wave's block b (row gw + (b / NNZ) W, nonzero b % NNZ)
+    auto gblk = [&](long b) { return (gw + (b / NNZ) * W) * NNZ + b % NNZ; };
+    const int nc = (int)p.ncols;
+    const unsigned SLOT = (unsigned)(ABLK + BD * nc) * ES;
+    const unsigned slot0 = lds_u32(smem) + (unsigned)w * (SLOT * RING);
+    const E *vb0 = (const E *)p.v;
+    // the block columns through the constant address space: scalar loads (lgkmcnt), which the
+    // per-block lgkmcnt(0) retires -- a vector load here would cost a vmcnt(0) per block
+    typedef const __attribute__((address_space(4))) int *cint_p;
+    const cint_p jj0 = (cint_p)p.jj;
+    unsigned skip = 0; // bit b % 32: block b has column -1
+    auto issue = [&](long b, int d) {
+        const unsigned base = slot0 + (unsigned)(b & (RING - 1)) * SLOT;
+        const char *vrow = (const char *)(vb0 + gblk(b) * ABLK);
+        // a skipped block reads x's first block row (not used)
+        const char *xrow = (const char *)((const E *)p.x + (long)(d < 0 ? 0 : d) * nc);
+        if (d < 0) skip |= 1u << (b & 31);
+        else skip &= ~(1u << (b & 31));
+#pragma unroll
+        for (int q = 0; q < PK; ++q) {
+            const unsigned g = (unsigned)(lane + 64 * q) * 16u;
+            if (g < SLOT) {
+                const char *src = g < (unsigned)(ABLK * ES) ? vrow + g : xrow + (g - ABLK * ES);
+                if ((p.nt & 1) && (q + 1) * 1024 <= ABLK * ES)
+                    asm volatile("s_mov_b32 m0, %1\n\t"
+                                 "s_nop 0\n\t"
+                                 "global_load_lds_dwordx4 %0, off nt"
+                                 :
+                                 : "v"(src), "s"(__builtin_amdgcn_readfirstlane(base + (unsigned)q * 1024u))
+                                 : "memory", "m0");
+                else
+                    asm volatile("s_mov_b32 m0, %1\n\t"
+                                 "s_nop 0\n\t"
+                                 "global_load_lds_dwordx4 %0, off"
+                                 :
+                                 : "v"(src), "s"(__builtin_amdgcn_readfirstlane(base + (unsigned)q * 1024u))
+                                 : "memory", "m0");
+            }
+        }
+    };
+    const int ar = lane & 15, kq = lane >> 4;
+    const bool arow_ok = ar < BI, bcol_ok = ar < nc;
+    acc_t accR = acc_t{0, 0, 0, 0}, accI = acc_t{0, 0, 0, 0};
+    // the fragments of a block from its slot: all six reads issued before any is used (one LDS
+    // latency per block), one block ahead of its MFMAs
+    E fa[2][KS], fb[2][KS];
+    auto frag = [&](long bl, E (&a_)[KS], E (&b_)[KS]) {
+        const E *sa = (const E *)(smem + (slot0 - lds_u32(smem)) + (unsigned)(bl & (RING - 1)) * SLOT);
+        const E *sx = sa + ABLK;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const int e = ks * 4 + kq;
+            a_[ks] = arow_ok ? (p.block_im_fast ? sa[ar + e * BI] : sa[ar * BD + e]) : E{};
+            b_[ks] = bcol_ok ? sx[e * nc + ar] : E{};
+        }
+    };
+    // prologue: blocks 0 .. PD - 1, then block 0's fragments; dnext = the column of the next
+    // block to issue
+    for (long b = 0; b < PD && b < nb; ++b) issue(b, jj0[gblk(b)]);
+    int dnext = PD < nb ? jj0[gblk(PD)] : 0;
+    wait_vmcnt_rt(PK * (int)((nb < PD ? nb : PD) - 1));
+    frag(0, fa[0], fb[0]);
+    long row = gw;
+    int k = 0;
+    for (long b = 0; b < nb; ++b) {
+        const int cur = (int)(b & 1);
+        // block b's fragments are in registers and the slot of block b + PD (block b - 1's) was
+        // read one iteration ago: both retired by lgkmcnt(0)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (b + PD < nb) {
+            issue(b + PD, dnext);
+            dnext = b + PD + 1 < nb ? jj0[gblk(b + PD + 1)] : 0; // (used next iteration)
+        }
+        if (b + 1 < nb) {
+            // block b + 1 landed: the PK instructions of each block issued after it may stay in
+            // flight; its fragments are read while block b's MFMAs run
+            const long later = nb - 2 - b < PD - 1 ? nb - 2 - b : PD - 1;
+            wait_vmcnt_rt(PK * (int)later);
+            frag(b + 1, fa[cur ^ 1], fb[cur ^ 1]);
+        }
+        if (!((skip >> (b & 31)) & 1)) {
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const E a = fa[cur][ks], bb = fb[cur][ks];
+                if constexpr (CPLX) {
+                    accR = BsrMfma<R>::mma(a.x, bb.x, accR);
+                    accI = BsrMfma<R>::mma(a.x, bb.y, accI);
+                    accR = BsrMfma<R>::mma(-a.y, bb.y, accR);
+                    accI = BsrMfma<R>::mma(a.y, bb.x, accI);
+                } else {
+                    accR = BsrMfma<R>::mma(a, bb, accR);
+                }
+            }
+        }
+        if (++k == NNZ) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int rr = BsrMfma<R>::row(lane, q);
+                if (rr >= BI || !bcol_ok) continue;
+                const long img = row * BI + rr;
+                E *yp = YROW ? y + img * p.ldy + ar : y + img + ar * p.ldy;
+                E out;
+                if constexpr (CPLX)
+                    out = Ops<E>::scale(E{accR[q], accI[q]}, p.alpha_re, p.alpha_im);
+                else
+                    out = Ops<E>::scale(accR[q], p.alpha_re, p.alpha_im);
+                *yp = p.add ? Ops<E>::add(*yp, out) : out;
+            }
+            accR = acc_t{0, 0, 0, 0};
+            accI = acc_t{0, 0, 0, 0};
+            k = 0;
+            row += W;
+        }
+    }
+}
+
+/// false: not this shape (bsr.stream workgroups per CU; the ring depth from bsr.stream_ring)
+template <typename R, bool CPLX, int BI, int BD, int NNZ>
+bool launch_bsr_mfma_stream(const BsrArgs &a, bool yrow, hipStream_t s) {
+    typedef typename BsrMfmaElem<R, CPLX>::type E;
+    constexpr int ES = (int)sizeof(E);
+    const long slot = (long)(BI * BD + BD * a.ncols) * ES;
+    if (a.x_rows <= 0 || a.ncols < 1 || a.ncols > 16 || slot % 16 || ((size_t)a.x & 15) ||
+        ((size_t)a.v & 15) || a.block_rows <= 0)
+        return false;
+    // DMA instructions per slot: exactly ceil(slot / 1 KB), so none is wholly masked (the wait
+    // counts assume every one of them issues)
+    const int pk = (int)((slot + 1023) / 1024);
+    const int ring = g_bsr_tune.stream_ring;
+    if ((ring != 4 && ring != 8) || pk < 2 || pk > 6) return false;
+    int dev = 0, cus = 256;
+    SBX_HIP_CHECK(hipGetDevice(&dev));
+    SBX_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const long per_cu = std::max(1, g_bsr_tune.stream);
+    const long blocks = std::min((long)cus * per_cu, (a.block_rows + 3) / 4);
+    const size_t lds = (size_t)4 * ring * slot;
+    if (lds > 160 * 1024) return false;
+    // a slot's DMA writes the slot's bytes only (lanes past it are inactive)
+    check_dma_lds("bsr_mfma_stream_kernel", lds, 0, 0, 4L * ring * slot);
+    g_bsr_tune.last = 15;
+    KernelTimer timer("bsr", s);
+    auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), lds, s, a); };
+    auto with_pk = [&](auto yr, auto rg) {
+        constexpr bool YR = decltype(yr)::value;
+        constexpr int RG = decltype(rg)::value;
+        switch (pk) {
+        case 2: go(bsr_mfma_stream_kernel<R, CPLX, BI, BD, YR, NNZ, RG, 2>); break;
+        case 3: go(bsr_mfma_stream_kernel<R, CPLX, BI, BD, YR, NNZ, RG, 3>); break;
+        case 4: go(bsr_mfma_stream_kernel<R, CPLX, BI, BD, YR, NNZ, RG, 4>); break;
+        case 5: go(bsr_mfma_stream_kernel<R, CPLX, BI, BD, YR, NNZ, RG, 5>); break;
+        default: go(bsr_mfma_stream_kernel<R, CPLX, BI, BD, YR, NNZ, RG, 6>); break;
+        }
+    };
+    using T = std::true_type;
+    using F = std::false_type;
+    using G4 = std::integral_constant<int, 4>;
+    using G8 = std::integral_constant<int, 8>;
+    if (yrow) ring == 4 ? with_pk(T{}, G4{}) : with_pk(T{}, G8{});
+    else ring == 4 ? with_pk(F{}, G4{}) : with_pk(F{}, G8{});
+    SBX_HIP_CHECK(hipGetLastError());
+    return true;
+}
+
 /// false: not this shape (the register-staged kernel runs)
 template <typename R, bool CPLX, int BI, int BD, int NNZ, int PD>
 bool launch_bsr_mfma_dma(const BsrArgs &a, bool yrow, hipStream_t s) {
@@ -663,6 +1046,19 @@ void launch_bsr_mfma(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_
     // by LDS-DMA one ahead (16^4 complex<double> n = 12: 426 us for the round-1 fragment kernel,
     // 348-355 us staged; the chain's complex<float> operator 985 -> 693 us with packed slots;
     // two or three blocks of lookahead were slower, profiles/r02_bsr_blk_sweep.txt)
+    if constexpr (CPLX && BI == 12 && BD == 12) {
+        // values in registers (bsr.vreg = lookahead in blocks: 1, 2 or 3)
+        if (g_bsr_tune.variant == 0 && g_bsr_tune.vreg > 0 && nnz == 9 && xrow && a.ldx == a.ncols &&
+            !(g_gemm_tune.m3 > 0) &&
+            (g_bsr_tune.vreg == 3   ? launch_bsr_mfma_vreg<R, 9, 3>(a, yrow, s)
+             : g_bsr_tune.vreg == 2 ? launch_bsr_mfma_vreg<R, 9, 2>(a, yrow, s)
+                                    : launch_bsr_mfma_vreg<R, 9, 1>(a, yrow, s)))
+            return;
+    }
+    // the streaming form: a few waves per CU, each a contiguous range of rows (bsr.stream)
+    if (g_bsr_tune.variant == 0 && g_bsr_tune.stream > 0 && nnz == 9 && xrow && a.ldx == a.ncols &&
+        !(CPLX && g_gemm_tune.m3 > 0) && launch_bsr_mfma_stream<R, CPLX, BI, BD, 9>(a, yrow, s))
+        return;
     if (g_bsr_tune.variant == 0 && nnz == 9 && xrow && a.ldx == a.ncols && a.ncols <= 16 &&
         (g_bsr_tune.blk_pd == 2   ? launch_bsr_mfma_dma<R, CPLX, BI, BD, 9, 2>(a, yrow, s)
          : g_bsr_tune.blk_pd == 3 ? launch_bsr_mfma_dma<R, CPLX, BI, BD, 9, 3>(a, yrow, s)

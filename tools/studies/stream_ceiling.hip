@@ -174,5 +174,10 @@ int main(int argc, char **argv) {
     time("dma_r8nt", bytes, [&] { dma_kernel<1, 8><<<cus * 8, 256>>>(a, n, out); });
     time("dma_r16nt", bytes, [&] { dma_kernel<1, 16><<<cus * 4, 256>>>(a, n, out); });
     time("dma_r16", bytes, [&] { dma_kernel<0, 16><<<cus * 4, 256>>>(a, n, out); });
+    // fewer waves per CU, each with more pieces in flight
+    time("dma_r8nt_w4", bytes, [&] { dma_kernel<1, 8><<<cus * 1, 256>>>(a, n, out); });
+    time("dma_r8nt_w8", bytes, [&] { dma_kernel<1, 8><<<cus * 2, 256>>>(a, n, out); });
+    time("dma_r16nt_w8", bytes, [&] { dma_kernel<1, 16><<<cus * 2, 256>>>(a, n, out); });
+    time("dma_r4nt_w16", bytes, [&] { dma_kernel<1, 4><<<cus * 4, 256>>>(a, n, out); });
     return 0;
 }
