@@ -18,6 +18,7 @@
 #include "plan.h"
 
 #include <algorithm>
+#include <mutex>
 #include <functional>
 #include <memory>
 
@@ -44,6 +45,8 @@ struct BsrComp {
     int *kron_perm = nullptr;        // Kronecker operators: block rows in the XCD order
     void *kron_terms = nullptr;      // ... the spin rows as two terms (build_kron_terms)
     void *kron_xor = nullptr;        // ... as diagonal + XOR partner (build_kron_terms)
+    bool kron_terms_due = false;     // ... tables not built yet (built on the first launch that
+                                     // asks for a spin-first kernel, bsr.kron_spin)
 };
 
 struct BsrOp {
@@ -230,9 +233,12 @@ void build_kron_order(BsrComp &bc, const Coor &isize, const Coor &blocki, const 
 /// The 4x4 complex<double> spin matrices of a Kronecker operator with at most two nonzeros in
 /// every row, as a table for bsr_kron_spin_kernel: per matrix mu and row a, two (spin index,
 /// coefficient) terms (a row with one nonzero: the second coefficient zero; with none: both).
-/// Taken from the matrices at creation, as the reference analyses them there (kron_cpu, the
-/// density and the repeated matrices, bsr.h:690-717).  No table (the MFMA kernels run) when a row
-/// has more nonzeros.
+/// Built from the matrices on the first launch with bsr.kron_spin set (the default MFMA kernels
+/// read the caller's matrices on every call and need no table), as a snapshot of the matrices at
+/// that moment -- the reference analyses them at creation (kron_cpu, the density and the repeated
+/// matrices, bsr.h:690-717); a caller who changes them in place afterwards must recreate the
+/// operator for the spin-first kernels.  No table (the MFMA kernels run) when a row has more
+/// nonzeros.
 void build_kron_terms(BsrComp &bc, bool block_im_fast) {
     const int nnz = bc.nnz_per_row;
     if (nnz <= 0 || !bc.kron) return;
@@ -437,7 +443,7 @@ BsrOp *bsr_create(int nd, int ni, int dtype, const std::vector<std::vector<Range
         if (op->is_kron && volume(op->kroni) == 4 && volume(op->krond) == 4 && bi == 3 && bd == 3 &&
             dtype == SBX_CDOUBLE) {
             build_kron_order(bc, ri.size, blocki, op->kroni);
-            build_kron_terms(bc, block_im_fast);
+            bc.kron_terms_due = true;
         }
         if (!op->is_kron) {
             bc.h_rowptr = std::move(rowptr);
@@ -902,6 +908,17 @@ void bsr_krylov(const BsrOp &op, const Scalar &alpha, const std::string &oi,
                     d.kd = (int)volume(op.krond);
                     d.kron = bc.kron;
                     d.kron_perm = bc.kron_perm;
+                    if (bc.kron_terms_due && g_bsr_tune.kron_spin > 0) {
+                        // (first spin-first launch: the tables; one host thread at a time)
+                        static std::mutex mu;
+                        std::lock_guard<std::mutex> lock(mu);
+                        BsrComp &mc = const_cast<BsrComp &>(bc);
+                        if (mc.kron_terms_due) {
+                            SBX_HIP_CHECK(hipStreamSynchronize(get_stream(bc.dev)));
+                            build_kron_terms(mc, op.block_im_fast);
+                            mc.kron_terms_due = false;
+                        }
+                    }
                     d.kron_terms = bc.kron_terms;
                     d.kron_xor = bc.kron_xor;
                     launch_bsr_kron(d, bc.dev);

@@ -773,22 +773,12 @@ bool launch_bsr_mfma_vreg(const BsrArgs &a, bool yrow, hipStream_t s) {
     return true;
 }
 
-/// s_waitcnt vmcnt(n) for a wave-uniform n known only at run time (0..63; one scalar branch)
-__device__ __forceinline__ void wait_vmcnt_rt(int n) {
-#define SBX_VM(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
-    switch (n) {
-        SBX_VM(0) SBX_VM(1) SBX_VM(2) SBX_VM(3) SBX_VM(4) SBX_VM(5) SBX_VM(6) SBX_VM(7)
-        SBX_VM(8) SBX_VM(9) SBX_VM(10) SBX_VM(11) SBX_VM(12) SBX_VM(13) SBX_VM(14) SBX_VM(15)
-        SBX_VM(16) SBX_VM(17) SBX_VM(18) SBX_VM(19) SBX_VM(20) SBX_VM(21) SBX_VM(22) SBX_VM(23)
-        SBX_VM(24) SBX_VM(25) SBX_VM(26) SBX_VM(27) SBX_VM(28) SBX_VM(29) SBX_VM(30) SBX_VM(31)
-        SBX_VM(32) SBX_VM(33) SBX_VM(34) SBX_VM(35) SBX_VM(36) SBX_VM(37) SBX_VM(38) SBX_VM(39)
-        SBX_VM(40) SBX_VM(41) SBX_VM(42) SBX_VM(43) SBX_VM(44) SBX_VM(45) SBX_VM(46) SBX_VM(47)
-        SBX_VM(48) SBX_VM(49) SBX_VM(50) SBX_VM(51) SBX_VM(52) SBX_VM(53) SBX_VM(54) SBX_VM(55)
-        SBX_VM(56) SBX_VM(57) SBX_VM(58) SBX_VM(59) SBX_VM(60) SBX_VM(61) SBX_VM(62) SBX_VM(63)
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    }
-#undef SBX_VM
+/// s_waitcnt vmcnt(N) for a compile-time N (0..63)
+template <int N> __device__ __forceinline__ void wait_vmcnt_c() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
 }
+
 
 // Streaming form of the packed 12x12 kernel (bsr.stream = workgroups per CU; ELL with NNZ blocks
 // per row, row-major x with ldx == ncols <= 16, packed value + x slots).  The LDS-DMA stream
@@ -796,51 +786,44 @@ __device__ __forceinline__ void wait_vmcnt_rt(int n) {
 // wave, but at 5.5-5.8 TB/s with 16-32 waves per CU (tools/studies/stream_ceiling.hip dma_r8nt_w4
 // against dma_r8nt_w8 / dma_r4nt_w16, profiles/r06_stream_ceiling.txt) -- and the one-row-per-wave
 // kernel above runs 32 waves per CU with one block in flight each.  Here a few waves per CU each
-// own every W-th block row and stream their rows' nonzero blocks through a RING-slot ring of their
-// own, RING - 1 blocks ahead across row boundaries, the fragments of the next block read while
-// the current one's MFMAs run; a row's y is written after its last block.  The block
-// columns come one block ahead through scalar loads; skipped blocks (column -1) are remembered
-// in a 32-bit mask (RING <= 32).  The y stores of a row are issued after the DMA of later blocks,
-// so the per-block wait vmcnt(PK * (blocks issued after this one)) over-waits at most (never
-// under-waits).
+// own every W-th block row (rows round robin, the waves of one XCD adjacent, so the chip streams
+// one window of the value array at a time: a contiguous range of rows per wave put the waves'
+// streams 2.65 MB apart on the chain's operator, a multiple of 8 x 4 KB) and stream their rows'
+// nonzero blocks through a RING-slot ring of their own, RING - 1 blocks ahead across row
+// boundaries, the fragments of the next block read while the current one's MFMAs run; a row's y
+// is written after its last block.  The row loop is unrolled over its NNZ blocks, so a block's
+// column is a compile-time pick among the current and the next row's columns; the columns of the
+// row after next come by LDS-DMA a whole row ahead (a scalar load of each column one block ahead
+// waited out one L2 round trip per block: 2.9 ms per launch).  The y stores of
+// a row are issued after the DMA of later blocks, so the per-block wait vmcnt(PK * (blocks issued
+// after this one)) over-waits at most (never under-waits).
 template <typename R, bool CPLX, int BI, int BD, bool YROW, int NNZ, int RING, int PK>
 __global__ void __launch_bounds__(256) bsr_mfma_stream_kernel(const BsrArgs p) {
     typedef typename BsrMfmaElem<R, CPLX>::type E;
     typedef typename BsrMfma<R>::acc_t acc_t;
-    static_assert(BI <= 16 && BD % 4 == 0 && RING >= 2 && RING <= 32 && (RING & (RING - 1)) == 0,
+    static_assert(BI <= 16 && BD % 4 == 0 && RING >= 2 && RING - 1 <= NNZ && (RING & (RING - 1)) == 0,
                   "block shape / ring");
+    static_assert(NNZ <= 16, "a row's columns in one 64-byte LDS buffer");
     constexpr int KS = BD / 4, ES = (int)sizeof(E), ABLK = BI * BD, PD = RING - 1;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     E *__restrict__ y = (E *)p.y;
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // rows round robin over the waves (wave gw: rows gw, gw + W, ...), the waves of one XCD
-    // adjacent: at any moment the chip streams one contiguous window of the value array.  (A
-    // contiguous range of rows per wave put the waves' streams 2.65 MB apart on the chain's
-    // operator -- a multiple of 8 x 4 KB, so a few HBM channels served them all: 1.2 TB/s.)
     const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
     const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
     const long W = (long)nwg * 4, gw = (long)wg * 4 + w;
     const long nr = gw < p.block_rows ? (p.block_rows - gw + W - 1) / W : 0;
     const long nb = nr * NNZ;
     if (nb <= 0) return;
-    // global block index of the wave's block b (row gw + (b / NNZ) W, nonzero b % NNZ)
-    auto gblk = [&](long b) { return (gw + (b / NNZ) * W) * NNZ + b % NNZ; };
     const int nc = (int)p.ncols;
     const unsigned SLOT = (unsigned)(ABLK + BD * nc) * ES;
     const unsigned slot0 = lds_u32(smem) + (unsigned)w * (SLOT * RING);
     const E *vb0 = (const E *)p.v;
-    // the block columns through the constant address space: scalar loads (lgkmcnt), which the
-    // per-block lgkmcnt(0) retires -- a vector load here would cost a vmcnt(0) per block
-    typedef const __attribute__((address_space(4))) int *cint_p;
-    const cint_p jj0 = (cint_p)p.jj;
-    unsigned skip = 0; // bit b % 32: block b has column -1
-    auto issue = [&](long b, int d) {
+    // block b of the wave: row gw + (b / NNZ) W, nonzero b % NNZ
+    auto issue = [&](long b, long row, int k, int d) {
         const unsigned base = slot0 + (unsigned)(b & (RING - 1)) * SLOT;
-        const char *vrow = (const char *)(vb0 + gblk(b) * ABLK);
+        const char *vrow = (const char *)(vb0 + (row * NNZ + k) * ABLK);
         // a skipped block reads x's first block row (not used)
         const char *xrow = (const char *)((const E *)p.x + (long)(d < 0 ? 0 : d) * nc);
-        if (d < 0) skip |= 1u << (b & 31);
-        else skip &= ~(1u << (b & 31));
 #pragma unroll
         for (int q = 0; q < PK; ++q) {
             const unsigned g = (unsigned)(lane + 64 * q) * 16u;
@@ -865,10 +848,9 @@ __global__ void __launch_bounds__(256) bsr_mfma_stream_kernel(const BsrArgs p) {
     };
     const int ar = lane & 15, kq = lane >> 4;
     const bool arow_ok = ar < BI, bcol_ok = ar < nc;
-    acc_t accR = acc_t{0, 0, 0, 0}, accI = acc_t{0, 0, 0, 0};
-    // the fragments of a block from its slot: all six reads issued before any is used (one LDS
-    // latency per block), one block ahead of its MFMAs
-    E fa[2][KS], fb[2][KS];
+    // (current and next fragments as separate arrays copied at the end of a block: a run-time
+    // index into a two-deep array would put them in scratch)
+    E fa[KS], fb[KS], ga[KS], gb[KS];
     auto frag = [&](long bl, E (&a_)[KS], E (&b_)[KS]) {
         const E *sa = (const E *)(smem + (slot0 - lds_u32(smem)) + (unsigned)(bl & (RING - 1)) * SLOT);
         const E *sx = sa + ABLK;
@@ -879,62 +861,91 @@ __global__ void __launch_bounds__(256) bsr_mfma_stream_kernel(const BsrArgs p) {
             b_[ks] = bcol_ok ? sx[e * nc + ar] : E{};
         }
     };
-    // prologue: blocks 0 .. PD - 1, then block 0's fragments; dnext = the column of the next
-    // block to issue
-    for (long b = 0; b < PD && b < nb; ++b) issue(b, jj0[gblk(b)]);
-    int dnext = PD < nb ? jj0[gblk(PD)] : 0;
-    wait_vmcnt_rt(PK * (int)((nb < PD ? nb : PD) - 1));
-    frag(0, fa[0], fb[0]);
-    long row = gw;
-    int k = 0;
-    for (long b = 0; b < nb; ++b) {
-        const int cur = (int)(b & 1);
-        // block b's fragments are in registers and the slot of block b + PD (block b - 1's) was
-        // read one iteration ago: both retired by lgkmcnt(0)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (b + PD < nb) {
-            issue(b + PD, dnext);
-            dnext = b + PD + 1 < nb ? jj0[gblk(b + PD + 1)] : 0; // (used next iteration)
-        }
-        if (b + 1 < nb) {
-            // block b + 1 landed: the PK instructions of each block issued after it may stay in
-            // flight; its fragments are read while block b's MFMAs run
-            const long later = nb - 2 - b < PD - 1 ? nb - 2 - b : PD - 1;
-            wait_vmcnt_rt(PK * (int)later);
-            frag(b + 1, fa[cur ^ 1], fb[cur ^ 1]);
-        }
-        if (!((skip >> (b & 31)) & 1)) {
+    // the block columns of the current row and the next; those of the row after next travel by
+    // LDS-DMA into a two-deep per-wave buffer behind the slot rings (counted by vmcnt in order
+    // with the blocks: landed once any block issued after it has been waited for)
+    int jc[NNZ], jn[NNZ];
 #pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-                const E a = fa[cur][ks], bb = fb[cur][ks];
-                if constexpr (CPLX) {
-                    accR = BsrMfma<R>::mma(a.x, bb.x, accR);
-                    accI = BsrMfma<R>::mma(a.x, bb.y, accI);
-                    accR = BsrMfma<R>::mma(-a.y, bb.y, accR);
-                    accI = BsrMfma<R>::mma(a.y, bb.x, accI);
-                } else {
-                    accR = BsrMfma<R>::mma(a, bb, accR);
+    for (int k = 0; k < NNZ; ++k) {
+        jc[k] = p.jj[gw * NNZ + k];
+        jn[k] = nr > 1 ? p.jj[(gw + W) * NNZ + k] : 0;
+    }
+    const unsigned jbuf = lds_u32(smem) + 4u * RING * SLOT + (unsigned)w * 128u;
+    const int *jlds = (const int *)(smem + 4u * RING * SLOT + (unsigned)w * 128u);
+    // prologue: blocks 0 .. PD - 1 (all of row 0), then block 0's fragments
+#pragma unroll
+    for (int k = 0; k < PD; ++k) issue(k, gw, k, jc[k]);
+    wait_vmcnt_c<PK * (PD - 1)>();
+    frag(0, fa, fb);
+    acc_t accR = acc_t{0, 0, 0, 0}, accI = acc_t{0, 0, 0, 0};
+    for (long j = 0; j < nr; ++j) {
+        const long row = gw + j * W;
+        if (j + 2 < nr && lane < NNZ)
+            asm volatile("s_mov_b32 m0, %1\n\t"
+                         "s_nop 0\n\t"
+                         "global_load_lds_dword %0, off"
+                         :
+                         : "v"(p.jj + (row + 2 * W) * NNZ + lane),
+                           "s"(jbuf + (unsigned)(j & 1) * 64u)
+                         : "memory", "m0");
+#pragma unroll
+        for (int k = 0; k < NNZ; ++k) {
+            const long b = j * NNZ + k;
+            // block b + PD (row j or j + 1, nonzero (k + PD) % NNZ: a compile-time pick); its
+            // slot held block b - 1, whose fragments were read (and waited for) two blocks ago
+            if (b + PD < nb) {
+                if (k + PD < NNZ) issue(b + PD, row, k + PD, jc[(k + PD) % NNZ]);
+                else issue(b + PD, row + W, (k + PD) % NNZ, jn[(k + PD) % NNZ]);
+            }
+            if (b + 1 < nb) {
+                // block b + 1 landed: the PK instructions of each of the PD - 1 blocks issued
+                // after it may stay in flight (in the wave's last PD blocks: wait for all -- a
+                // compile-time count keeps the unrolled row small, for the instruction cache)
+                if (b + PD < nb) wait_vmcnt_c<PK * (PD - 1)>();
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                frag(b + 1, ga, gb);
+            }
+            if (jc[k] >= 0) {
+#pragma unroll
+                for (int ks = 0; ks < KS; ++ks) {
+                    const E a = fa[ks], bb = fb[ks];
+                    if constexpr (CPLX) {
+                        accR = BsrMfma<R>::mma(a.x, bb.x, accR);
+                        accI = BsrMfma<R>::mma(a.x, bb.y, accI);
+                        accR = BsrMfma<R>::mma(-a.y, bb.y, accR);
+                        accI = BsrMfma<R>::mma(a.y, bb.x, accI);
+                    } else {
+                        accR = BsrMfma<R>::mma(a, bb, accR);
+                    }
                 }
             }
-        }
-        if (++k == NNZ) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int rr = BsrMfma<R>::row(lane, q);
-                if (rr >= BI || !bcol_ok) continue;
-                const long img = row * BI + rr;
-                E *yp = YROW ? y + img * p.ldy + ar : y + img + ar * p.ldy;
-                E out;
-                if constexpr (CPLX)
-                    out = Ops<E>::scale(E{accR[q], accI[q]}, p.alpha_re, p.alpha_im);
-                else
-                    out = Ops<E>::scale(accR[q], p.alpha_re, p.alpha_im);
-                *yp = p.add ? Ops<E>::add(*yp, out) : out;
+            for (int ks = 0; ks < KS; ++ks) {
+                fa[ks] = ga[ks];
+                fb[ks] = gb[ks];
             }
-            accR = acc_t{0, 0, 0, 0};
-            accI = acc_t{0, 0, 0, 0};
-            k = 0;
-            row += W;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int rr = BsrMfma<R>::row(lane, q);
+            if (rr >= BI || !bcol_ok) continue;
+            const long img = row * BI + rr;
+            E *yp = YROW ? y + img * p.ldy + ar : y + img + ar * p.ldy;
+            E out;
+            if constexpr (CPLX)
+                out = Ops<E>::scale(E{accR[q], accI[q]}, p.alpha_re, p.alpha_im);
+            else
+                out = Ops<E>::scale(accR[q], p.alpha_re, p.alpha_im);
+            *yp = p.add ? Ops<E>::add(*yp, out) : out;
+        }
+        accR = acc_t{0, 0, 0, 0};
+        accI = acc_t{0, 0, 0, 0};
+        // the columns of row j + 2: their DMA (issued at this row's start) landed before block
+        // (j + 1) NNZ, which the last block of this row waited for
+#pragma unroll
+        for (int k = 0; k < NNZ; ++k) {
+            jc[k] = jn[k];
+            jn[k] = j + 2 < nr ? __builtin_amdgcn_readfirstlane(jlds[(j & 1) * 16 + k]) : 0;
         }
     }
 }
@@ -958,10 +969,11 @@ bool launch_bsr_mfma_stream(const BsrArgs &a, bool yrow, hipStream_t s) {
     SBX_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     const long per_cu = std::max(1, g_bsr_tune.stream);
     const long blocks = std::min((long)cus * per_cu, (a.block_rows + 3) / 4);
-    const size_t lds = (size_t)4 * ring * slot;
+    // 4 waves x ring slots, then 4 waves x two 64-byte column buffers
+    const size_t lds = (size_t)4 * ring * slot + 4 * 128;
     if (lds > 160 * 1024) return false;
     // a slot's DMA writes the slot's bytes only (lanes past it are inactive)
-    check_dma_lds("bsr_mfma_stream_kernel", lds, 0, 0, 4L * ring * slot);
+    check_dma_lds("bsr_mfma_stream_kernel", lds, 0, 0, 4L * ring * slot + 4 * 128);
     g_bsr_tune.last = 15;
     KernelTimer timer("bsr", s);
     auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), lds, s, a); };
