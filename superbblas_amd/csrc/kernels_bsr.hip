@@ -42,6 +42,7 @@ struct BsrArgs {
     int add;
     int ilv = 1; // bsr_ell9_kernel: an XCD's chunks visited as ilv interleaved parts
     int nt = 0;  // the value stream's LDS-DMA loads non-temporal: g_bsr_tune.nt's kernel bits
+    int smap = 0; // bsr_mfma_stream_kernel row map (g_bsr_tune.stream_map)
     // site tiles (bsr_ell9_tile_kernel; [0] 16-site, [1] 8-site tiles; rows == nullptr: none)
     TileSched tiles[2];
 };
@@ -810,8 +811,22 @@ __global__ void __launch_bounds__(256) bsr_mfma_stream_kernel(const BsrArgs p) {
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
     const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-    const long W = (long)nwg * 4, gw = (long)wg * 4 + w;
-    const long nr = gw < p.block_rows ? (p.block_rows - gw + W - 1) / W : 0;
+    // the wave's rows: base + j S.  smap 0: round robin over the chip's W waves (base = the wave's
+    // index, S = W); smap 1: each XCD a contiguous eighth of the rows, round robin over its own
+    // waves (x halo rows of the same XCD's rows stay in its L2)
+    long base, S, nr;
+    if (p.smap == 1) {
+        const long nx = q8 + (xcd < r8 ? 1 : 0), lo = p.block_rows * xcd / 8,
+                   hi = p.block_rows * (xcd + 1) / 8;
+        S = nx * 4;
+        base = lo + (long)(bid >> 3) * 4 + w;
+        nr = base < hi ? (hi - base + S - 1) / S : 0;
+    } else {
+        const long W = (long)nwg * 4, gw = (long)wg * 4 + w;
+        S = W;
+        base = gw;
+        nr = gw < p.block_rows ? (p.block_rows - gw + W - 1) / W : 0;
+    }
     const long nb = nr * NNZ;
     if (nb <= 0) return;
     const int nc = (int)p.ncols;
@@ -867,25 +882,25 @@ __global__ void __launch_bounds__(256) bsr_mfma_stream_kernel(const BsrArgs p) {
     int jc[NNZ], jn[NNZ];
 #pragma unroll
     for (int k = 0; k < NNZ; ++k) {
-        jc[k] = p.jj[gw * NNZ + k];
-        jn[k] = nr > 1 ? p.jj[(gw + W) * NNZ + k] : 0;
+        jc[k] = p.jj[base * NNZ + k];
+        jn[k] = nr > 1 ? p.jj[(base + S) * NNZ + k] : 0;
     }
     const unsigned jbuf = lds_u32(smem) + 4u * RING * SLOT + (unsigned)w * 128u;
     const int *jlds = (const int *)(smem + 4u * RING * SLOT + (unsigned)w * 128u);
     // prologue: blocks 0 .. PD - 1 (all of row 0), then block 0's fragments
 #pragma unroll
-    for (int k = 0; k < PD; ++k) issue(k, gw, k, jc[k]);
+    for (int k = 0; k < PD; ++k) issue(k, base, k, jc[k]);
     wait_vmcnt_c<PK * (PD - 1)>();
     frag(0, fa, fb);
     acc_t accR = acc_t{0, 0, 0, 0}, accI = acc_t{0, 0, 0, 0};
     for (long j = 0; j < nr; ++j) {
-        const long row = gw + j * W;
+        const long row = base + j * S;
         if (j + 2 < nr && lane < NNZ)
             asm volatile("s_mov_b32 m0, %1\n\t"
                          "s_nop 0\n\t"
                          "global_load_lds_dword %0, off"
                          :
-                         : "v"(p.jj + (row + 2 * W) * NNZ + lane),
+                         : "v"(p.jj + (row + 2 * S) * NNZ + lane),
                            "s"(jbuf + (unsigned)(j & 1) * 64u)
                          : "memory", "m0");
 #pragma unroll
@@ -895,7 +910,7 @@ __global__ void __launch_bounds__(256) bsr_mfma_stream_kernel(const BsrArgs p) {
             // slot held block b - 1, whose fragments were read (and waited for) two blocks ago
             if (b + PD < nb) {
                 if (k + PD < NNZ) issue(b + PD, row, k + PD, jc[(k + PD) % NNZ]);
-                else issue(b + PD, row + W, (k + PD) % NNZ, jn[(k + PD) % NNZ]);
+                else issue(b + PD, row + S, (k + PD) % NNZ, jn[(k + PD) % NNZ]);
             }
             if (b + 1 < nb) {
                 // block b + 1 landed: the PK instructions of each of the PD - 1 blocks issued
@@ -1896,6 +1911,7 @@ void launch_bsr(const BsrDesc &d, int device) {
     a.add = d.add ? 1 : 0;
     a.ilv = 2; // an XCD's row chunks visited as two interleaved halves (bsr_ell9_kernel)
     a.nt = g_bsr_tune.nt;
+    a.smap = g_bsr_tune.stream_map;
     a.tiles[0] = d.tiles[0];
     a.tiles[1] = d.tiles[1];
     switch (d.t) {

@@ -285,6 +285,7 @@ struct BsrTune {
     int stream = 0; ///< 12x12 blocks, 9 per row, row-major x (ldx == ncols <= 16): the streaming kernel
                     ///< (bsr_mfma_stream_kernel) with this many 4-wave workgroups per CU (0 = off)
     int stream_ring = 8; ///< ... ring slots per wave (4 or 8: blocks in flight + 1)
+    int stream_map = 0;  ///< ... rows: 0 round robin over the chip's waves, 1 an eighth per XCD
     int vreg = 0;   ///< 12x12 complex blocks, 9 per row, row-major x (ldx == ncols <= 16): the values
                     ///< straight into MFMA fragments, x by LDS-DMA (bsr_mfma_vreg_kernel), this many
                     ///< blocks ahead (1..3; 0 = off: bsr_mfma_dma_kernel)

@@ -346,10 +346,12 @@ def test_bsr_image_side_kernel_form(gpu, spin, color, ncols, form):
 
 
 FORMS_12 = [("bsr.vreg", 1, None, 14), ("bsr.vreg", 2, None, 14), ("bsr.vreg", 3, None, 14),
-            ("bsr.stream", 1, 4, 15), ("bsr.stream", 1, 8, 15), ("bsr.stream", 2, 8, 15)]
+            ("bsr.stream", 1, 4, 15), ("bsr.stream", 1, 8, 15), ("bsr.stream", 2, 8, 15),
+            ("bsr.stream", 3, 4, 15, 1), ("bsr.stream", 1, 8, 15, 1)]
 
 
-@pytest.mark.parametrize("form", FORMS_12, ids=lambda f: "%s%d_r%s" % (f[0][4:], f[1], f[2]))
+@pytest.mark.parametrize("form", FORMS_12, ids=lambda f: "%s%d_r%s_m%d" % (f[0][4:], f[1], f[2],
+                                                                          f[4] if len(f) > 4 else 0))
 @pytest.mark.parametrize("dtype,ncols", [(np.complex64, 12), (np.complex64, 16), (np.complex64, 5),
                                          (np.complex128, 12), (np.complex128, 13), (np.complex128, 1),
                                          (np.float32, 12), (np.float64, 3)])
@@ -365,7 +367,8 @@ def test_bsr_12x12_register_and_stream_forms(gpu, form, dtype, ncols, bimf, skip
     import torch
     import superbblas_amd as sb
     from _common import TYPE_OF
-    key, val, ring, kern = form
+    key, val, ring, kern = form[:4]
+    smap = form[4] if len(form) > 4 else 0
     cplx = np.dtype(dtype).kind == "c"
     if key == "bsr.vreg" and not cplx:
         pytest.skip("the values-in-registers form is complex only")
@@ -396,8 +399,9 @@ def test_bsr_12x12_register_and_stream_forms(gpu, form, dtype, ncols, bimf, skip
     oy, dimy = ("pnxyztsc", [1, ncols, L, L, L, L, spin, color]) if ycol else ("pxyztscn", dimx)
     ty = torch.full((n,), 3.0, dtype=getattr(torch, np.dtype(dtype).name), device=gpu)
     old = sb.tune_get(key)
-    old_ring = sb.tune_get("bsr.stream_ring")
+    old_ring, old_map = sb.tune_get("bsr.stream_ring"), sb.tune_get("bsr.stream_map")
     sb.tune_set(key, val)
+    sb.tune_set("bsr.stream_map", smap)
     if ring:
         sb.tune_set("bsr.stream_ring", ring)
     try:
@@ -408,6 +412,7 @@ def test_bsr_12x12_register_and_stream_forms(gpu, form, dtype, ncols, bimf, skip
     finally:
         sb.tune_set(key, old)
         sb.tune_set("bsr.stream_ring", old_ring)
+        sb.tune_set("bsr.stream_map", old_map)
     used = sb.tune_get("bsr.last_kernel")
     op.destroy()
     assert used == kern, used

@@ -64,7 +64,9 @@ def main():
     # VREGS: bsr.vreg values (12x12 complex: values straight into MFMA fragments, round 6)
     vregs = [int(v) for v in os.environ.get("VREGS", str(sb.tune_get("bsr.vreg"))).split(",")]
     # STREAMS: bsr.stream values as "workgroups per CU:ring" (12x12 streaming kernel, round 6)
-    streams = [tuple(int(u) for u in v.split(":")) if ":" in v else (int(v), sb.tune_get("bsr.stream_ring"))
+    # (":ring:map", map = bsr.stream_map)
+    streams = [tuple(int(u) for u in (v + ":%d:%d" % (sb.tune_get("bsr.stream_ring"),
+                                                      sb.tune_get("bsr.stream_map"))).split(":")[:3])
                for v in os.environ.get("STREAMS", str(sb.tune_get("bsr.stream"))).split(",")]
     tiles = [int(v) for v in os.environ.get("TILES", str(sb.tune_get("bsr.tile"))).split(",")]
     # BLK=12: spin 4 x color 3 blocks (config 3's secondary shape / the chain's operator);
@@ -90,6 +92,7 @@ def main():
             sb.tune_set("bsr.vreg", vreg)
             sb.tune_set("bsr.stream", st[0])
             sb.tune_set("bsr.stream_ring", st[1])
+            sb.tune_set("bsr.stream_map", st[2])
             sb.tune_set("bsr.variant", var)
             if reg >= 0:  # bsr.reg: the round-5 register-staged experiment (removed again)
                 sb.tune_set("bsr.reg", reg)
@@ -119,7 +122,7 @@ def main():
             t = statistics.median(ts)
             algo = es * (9 * b * b * V + 2 * b * V * n) + 4.0 * (9 * V + V + 1)  # the stencil's
             floor = es * (nnz * b * b * V + 2 * b * V * n) + 4.0 * (nnz * V + V + 1)
-            print(json.dumps({"blk": b, "dtype": str(dt), "kind": kind, "ncols": n, "nt": nt, "blk_pd": pd, "variant": var, "reg": reg, "tile": tile, "vreg": vreg, "stream": "%d:%d" % st,
+            print(json.dumps({"blk": b, "dtype": str(dt), "kind": kind, "ncols": n, "nt": nt, "blk_pd": pd, "variant": var, "reg": reg, "tile": tile, "vreg": vreg, "stream": "%d:%d:%d" % st,
                               "us": round(t * 1e6, 1),
                               "kernel": sb.tune_get("bsr.last_kernel"),
                               "stencil_bytes_frac_hbm": round(algo / t / 8e12, 4),
