@@ -448,10 +448,6 @@ int sbx_tune_set(const char *key, long long value) {
         else if (k == "bsr.nt") g_bsr_tune.nt = (int)value;
         else if (k == "dense.wave") g_dense_wave = (int)value;
         else if (k == "bsr.blk_pd") g_bsr_tune.blk_pd = (int)value;
-        else if (k == "bsr.vreg") g_bsr_tune.vreg = (int)value;
-        else if (k == "bsr.stream") g_bsr_tune.stream = (int)value;
-        else if (k == "bsr.stream_ring") g_bsr_tune.stream_ring = (int)value;
-        else if (k == "bsr.stream_map") g_bsr_tune.stream_map = (int)value;
         else if (k == "bsr.tile") g_bsr_tune.tile = (int)value;
         else if (k == "bsr.tile_min_cols") g_bsr_tune.tile_min_cols = value;
         else if (k == "gemm.m3") g_gemm_tune.m3 = (int)value;
@@ -514,10 +510,6 @@ int sbx_tune_get(const char *key, long long *value) {
         else if (k == "bsr.nt") *value = g_bsr_tune.nt;
         else if (k == "dense.wave") *value = g_dense_wave;
         else if (k == "bsr.blk_pd") *value = g_bsr_tune.blk_pd;
-        else if (k == "bsr.vreg") *value = g_bsr_tune.vreg;
-        else if (k == "bsr.stream") *value = g_bsr_tune.stream;
-        else if (k == "bsr.stream_ring") *value = g_bsr_tune.stream_ring;
-        else if (k == "bsr.stream_map") *value = g_bsr_tune.stream_map;
         else if (k == "bsr.tile") *value = g_bsr_tune.tile;
         else if (k == "bsr.tile_min_cols") *value = g_bsr_tune.tile_min_cols;
         else if (k == "bsr.last_kernel") *value = g_bsr_tune.last;

@@ -42,7 +42,6 @@ struct BsrArgs {
     int add;
     int ilv = 1; // bsr_ell9_kernel: an XCD's chunks visited as ilv interleaved parts
     int nt = 0;  // the value stream's LDS-DMA loads non-temporal: g_bsr_tune.nt's kernel bits
-    int smap = 0; // bsr_mfma_stream_kernel row map (g_bsr_tune.stream_map)
     // site tiles (bsr_ell9_tile_kernel; [0] 16-site, [1] 8-site tiles; rows == nullptr: none)
     TileSched tiles[2];
 };
@@ -604,415 +603,6 @@ __global__ void __launch_bounds__(256) bsr_mfma_dma_kernel(const BsrArgs p, unsi
     }
 }
 
-// Values in registers, x by LDS-DMA (12x12 complex blocks, ELL with NNZ blocks per row, row-major
-// x with ldx == ncols <= 16; bsr.vreg).  The LDS-DMA kernel above moves both the value block and
-// the x block of every nonzero through the LDS, and its stream alone (MFMAs and fragment reads
-// removed) ran at 5.06 TB/s on the chain's operator (profiles/r05_bsr12_no_mfma.txt) against 7.1
-// TB/s for plain non-temporal 16-byte loads with several in flight per lane
-// (tools/studies/stream_ceiling.hip read_u8nt, profiles/r06_stream_ceiling.txt).  Here the value
-// block -- 82 % of the bytes, read once -- goes straight into the MFMA fragments: lane (row r,
-// quarter kq) takes the three contiguous k = 3 kq .. 3 kq + 2 of row r (the MFMA sums over k, so
-// any k-to-(step, quarter) assignment works when the x fragment follows it), one 16-byte and one
-// 8-byte load for complex<float> (16-byte aligned by the quarter's parity), three 16-byte loads
-// for complex<double>; column-major blocks (block_im_fast) take three loads along the block row.
-// The x block (reused by nine rows: an L2 hit) is staged by LDS-DMA into the wave's ring slot as
-// before, PD blocks ahead, and read as x[3 kq + s][c].
-template <typename E> struct VregOps;
-template <> struct VregOps<float2> {
-    typedef float f4 __attribute__((ext_vector_type(4)));
-    typedef float f2 __attribute__((ext_vector_type(2)));
-    static constexpr int NV = 2; // load instructions per block (row-major blocks)
-    template <bool NT> static __device__ __forceinline__ float2 load1(const float2 *pa) {
-        const f2 t = NT ? __builtin_nontemporal_load((const f2 *)pa) : *(const f2 *)pa;
-        return float2{t.x, t.y};
-    }
-    template <bool NT> static __device__ __forceinline__ void load3(const float2 *pa, bool even, float2 (&a)[3]) {
-        const f4 *p16 = (const f4 *)(even ? pa : pa + 1);
-        const f2 *p8 = (const f2 *)(even ? pa + 2 : pa);
-        const f4 t = NT ? __builtin_nontemporal_load(p16) : *p16;
-        const f2 u = NT ? __builtin_nontemporal_load(p8) : *p8;
-        a[0] = even ? float2{t.x, t.y} : float2{u.x, u.y};
-        a[1] = even ? float2{t.z, t.w} : float2{t.x, t.y};
-        a[2] = even ? float2{u.x, u.y} : float2{t.z, t.w};
-    }
-};
-template <> struct VregOps<double2> {
-    typedef double d2 __attribute__((ext_vector_type(2)));
-    static constexpr int NV = 3;
-    template <bool NT> static __device__ __forceinline__ double2 load1(const double2 *pa) {
-        const d2 t = NT ? __builtin_nontemporal_load((const d2 *)pa) : *(const d2 *)pa;
-        return double2{t.x, t.y};
-    }
-    template <bool NT> static __device__ __forceinline__ void load3(const double2 *pa, bool, double2 (&a)[3]) {
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            const d2 t = NT ? __builtin_nontemporal_load((const d2 *)(pa + q)) : *(const d2 *)(pa + q);
-            a[q] = double2{t.x, t.y};
-        }
-    }
-};
-
-template <typename R, int BI, int BD, bool YROW, int NNZ, int PD, int NXI, bool NTV, bool BIMF>
-__global__ void __launch_bounds__(256) bsr_mfma_vreg_kernel(const BsrArgs p) {
-    typedef typename BsrMfmaElem<R, true>::type E;
-    typedef typename BsrMfma<R>::acc_t acc_t;
-    static_assert(BI == 12 && BD == 12, "12x12 blocks: three k per quarter");
-    constexpr int ES = (int)sizeof(E), ABLK = BI * BD;
-    constexpr int NVI = BIMF ? 3 : VregOps<E>::NV, NI = NVI + NXI; // load instructions per block
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    E *__restrict__ y = (E *)p.y;
-    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const long i = (long)blockIdx.x * 4 + w;
-    if (i >= p.block_rows) return; // whole waves only: MFMA needs all 64 lanes
-    const int nc = (int)p.ncols;
-    const unsigned XB = (unsigned)(BD * nc * ES), SLOT = (XB + 15u) & ~15u;
-    const long jb = i * NNZ;
-    int dj[NNZ];
-#pragma unroll
-    for (int k = 0; k < NNZ; ++k) dj[k] = p.jj[jb + k];
-    const int ar = lane & 15, kq = lane >> 4;
-    const bool arow_ok = ar < BI, bcol_ok = ar < nc;
-    const int arc = arow_ok ? ar : BI - 1;
-    const E *vrow = (const E *)p.v + jb * ABLK;
-    const unsigned slot0 = lds_u32(smem) + (unsigned)w * (SLOT * (PD + 1));
-    E va[PD + 1][3];
-    auto issue = [&](int k) {
-        // x block of nonzero k (a skipped block, column -1, reads x's first block row: unused)
-        const unsigned base = slot0 + (unsigned)(k % (PD + 1)) * SLOT;
-        const char *xrow = (const char *)((const E *)p.x + (long)(dj[k] < 0 ? 0 : dj[k]) * nc);
-#pragma unroll
-        for (int q = 0; q < NXI; ++q) {
-            const unsigned g = (unsigned)(lane + 64 * q) * 16u;
-            if (g < XB)
-                asm volatile("s_mov_b32 m0, %1\n\t"
-                             "s_nop 0\n\t"
-                             "global_load_lds_dwordx4 %0, off"
-                             :
-                             : "v"(xrow + g), "s"(__builtin_amdgcn_readfirstlane(base + (unsigned)q * 1024u))
-                             : "memory", "m0");
-        }
-        // value block of nonzero k straight into the fragments
-        const E *vb = vrow + (long)k * ABLK;
-        E (&a)[3] = va[k % (PD + 1)];
-        if constexpr (BIMF) {
-#pragma unroll
-            for (int s = 0; s < 3; ++s) a[s] = VregOps<E>::template load1<NTV>(vb + arc + (3 * kq + s) * BI);
-        } else {
-            VregOps<E>::template load3<NTV>(vb + arc * BD + 3 * kq, (kq & 1) == 0, a);
-        }
-    };
-    acc_t accR = acc_t{0, 0, 0, 0}, accI = acc_t{0, 0, 0, 0};
-#pragma unroll
-    for (int k = 0; k < PD && k < NNZ; ++k) issue(k);
-#pragma unroll
-    for (int k = 0; k < NNZ; ++k) {
-        // the x slot of block k + PD was last read in iteration k - 1: its reads have returned
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (k + PD < NNZ) issue(k + PD);
-        // block k landed (x in LDS, values in registers): the NI instructions of each later
-        // block issued so far may stay in flight
-        wait_vmcnt_n(NI * (NNZ - 1 - k < PD ? NNZ - 1 - k : PD));
-        if (dj[k] < 0) continue;
-        const E *sx = (const E *)(smem + (slot0 - lds_u32(smem)) + (k % (PD + 1)) * SLOT);
-#pragma unroll
-        for (int s = 0; s < 3; ++s) {
-            const E a = arow_ok ? va[k % (PD + 1)][s] : E{};
-            const E b = bcol_ok ? sx[(3 * kq + s) * nc + ar] : E{};
-            accR = BsrMfma<R>::mma(a.x, b.x, accR);
-            accI = BsrMfma<R>::mma(a.x, b.y, accI);
-            accR = BsrMfma<R>::mma(-a.y, b.y, accR);
-            accI = BsrMfma<R>::mma(a.y, b.x, accI);
-        }
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int row = BsrMfma<R>::row(lane, q);
-        if (row >= BI || !bcol_ok) continue;
-        const long img = i * BI + row;
-        E *yp = YROW ? y + img * p.ldy + ar : y + img + ar * p.ldy;
-        const E out = Ops<E>::scale(E{accR[q], accI[q]}, p.alpha_re, p.alpha_im);
-        *yp = p.add ? Ops<E>::add(*yp, out) : out;
-    }
-}
-
-/// false: not this shape
-template <typename R, int NNZ, int PD>
-bool launch_bsr_mfma_vreg(const BsrArgs &a, bool yrow, hipStream_t s) {
-    typedef typename BsrMfmaElem<R, true>::type E;
-    constexpr int ES = (int)sizeof(E);
-    const long xb = 12L * a.ncols * ES;
-    if (a.x_rows <= 0 || a.ncols < 1 || a.ncols > 16 || xb % 16 || ((size_t)a.x & 15) ||
-        ((size_t)a.v & 15))
-        return false;
-    const long blocks = (a.block_rows + 3) / 4;
-    if (blocks >= (1L << 31)) return false;
-    const int nxi = (int)((xb + 1023) / 1024);
-    const size_t lds = (size_t)4 * (PD + 1) * xb;
-    check_dma_lds("bsr_mfma_vreg_kernel", lds, 0, 0, 4L * (PD + 1) * xb);
-    g_bsr_tune.last = 14;
-    KernelTimer timer("bsr", s);
-    auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), lds, s, a); };
-    const bool nt = (a.nt & 1) != 0, bimf = a.block_im_fast != 0;
-    // (template dispatch over y's layout, the x instruction count, the value policy and layout)
-    auto pick = [&](auto yr, auto nx) {
-        constexpr bool YR = decltype(yr)::value;
-        constexpr int NX = decltype(nx)::value;
-        if (nt && !bimf) go(bsr_mfma_vreg_kernel<R, 12, 12, YR, NNZ, PD, NX, true, false>);
-        else if (!bimf) go(bsr_mfma_vreg_kernel<R, 12, 12, YR, NNZ, PD, NX, false, false>);
-        else if (nt) go(bsr_mfma_vreg_kernel<R, 12, 12, YR, NNZ, PD, NX, true, true>);
-        else go(bsr_mfma_vreg_kernel<R, 12, 12, YR, NNZ, PD, NX, false, true>);
-    };
-    using T = std::true_type;
-    using F = std::false_type;
-    using I1 = std::integral_constant<int, 1>;
-    using I2 = std::integral_constant<int, 2>;
-    using I3 = std::integral_constant<int, 3>;
-    if (nxi == 1) yrow ? pick(T{}, I1{}) : pick(F{}, I1{});
-    else if (nxi == 2) yrow ? pick(T{}, I2{}) : pick(F{}, I2{});
-    else yrow ? pick(T{}, I3{}) : pick(F{}, I3{});
-    SBX_HIP_CHECK(hipGetLastError());
-    return true;
-}
-
-/// s_waitcnt vmcnt(N) for a compile-time N (0..63)
-template <int N> __device__ __forceinline__ void wait_vmcnt_c() {
-    static_assert(N >= 0 && N < 64, "vmcnt range");
-    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
-}
-
-
-// Streaming form of the packed 12x12 kernel (bsr.stream = workgroups per CU; ELL with NNZ blocks
-// per row, row-major x with ldx == ncols <= 16, packed value + x slots).  The LDS-DMA stream
-// itself runs at 7.1 TB/s with one workgroup of 4 waves per CU and 8 one-KB pieces in flight per
-// wave, but at 5.5-5.8 TB/s with 16-32 waves per CU (tools/studies/stream_ceiling.hip dma_r8nt_w4
-// against dma_r8nt_w8 / dma_r4nt_w16, profiles/r06_stream_ceiling.txt) -- and the one-row-per-wave
-// kernel above runs 32 waves per CU with one block in flight each.  Here a few waves per CU each
-// own every W-th block row (rows round robin, the waves of one XCD adjacent, so the chip streams
-// one window of the value array at a time: a contiguous range of rows per wave put the waves'
-// streams 2.65 MB apart on the chain's operator, a multiple of 8 x 4 KB) and stream their rows'
-// nonzero blocks through a RING-slot ring of their own, RING - 1 blocks ahead across row
-// boundaries, the fragments of the next block read while the current one's MFMAs run; a row's y
-// is written after its last block.  The row loop is unrolled over its NNZ blocks, so a block's
-// column is a compile-time pick among the current and the next row's columns; the columns of the
-// row after next come by LDS-DMA a whole row ahead (a scalar load of each column one block ahead
-// waited out one L2 round trip per block: 2.9 ms per launch).  The y stores of
-// a row are issued after the DMA of later blocks, so the per-block wait vmcnt(PK * (blocks issued
-// after this one)) over-waits at most (never under-waits).
-template <typename R, bool CPLX, int BI, int BD, bool YROW, int NNZ, int RING, int PK>
-__global__ void __launch_bounds__(256) bsr_mfma_stream_kernel(const BsrArgs p) {
-    typedef typename BsrMfmaElem<R, CPLX>::type E;
-    typedef typename BsrMfma<R>::acc_t acc_t;
-    static_assert(BI <= 16 && BD % 4 == 0 && RING >= 2 && RING - 1 <= NNZ && (RING & (RING - 1)) == 0,
-                  "block shape / ring");
-    static_assert(NNZ <= 16, "a row's columns in one 64-byte LDS buffer");
-    constexpr int KS = BD / 4, ES = (int)sizeof(E), ABLK = BI * BD, PD = RING - 1;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    E *__restrict__ y = (E *)p.y;
-    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-    // the wave's rows: base + j S.  smap 0: round robin over the chip's W waves (base = the wave's
-    // index, S = W); smap 1: each XCD a contiguous eighth of the rows, round robin over its own
-    // waves (x halo rows of the same XCD's rows stay in its L2)
-    long base, S, nr;
-    if (p.smap == 1) {
-        const long nx = q8 + (xcd < r8 ? 1 : 0), lo = p.block_rows * xcd / 8,
-                   hi = p.block_rows * (xcd + 1) / 8;
-        S = nx * 4;
-        base = lo + (long)(bid >> 3) * 4 + w;
-        nr = base < hi ? (hi - base + S - 1) / S : 0;
-    } else {
-        const long W = (long)nwg * 4, gw = (long)wg * 4 + w;
-        S = W;
-        base = gw;
-        nr = gw < p.block_rows ? (p.block_rows - gw + W - 1) / W : 0;
-    }
-    const long nb = nr * NNZ;
-    if (nb <= 0) return;
-    const int nc = (int)p.ncols;
-    const unsigned SLOT = (unsigned)(ABLK + BD * nc) * ES;
-    const unsigned slot0 = lds_u32(smem) + (unsigned)w * (SLOT * RING);
-    const E *vb0 = (const E *)p.v;
-    // block b of the wave: row gw + (b / NNZ) W, nonzero b % NNZ
-    auto issue = [&](long b, long row, int k, int d) {
-        const unsigned base = slot0 + (unsigned)(b & (RING - 1)) * SLOT;
-        const char *vrow = (const char *)(vb0 + (row * NNZ + k) * ABLK);
-        // a skipped block reads x's first block row (not used)
-        const char *xrow = (const char *)((const E *)p.x + (long)(d < 0 ? 0 : d) * nc);
-#pragma unroll
-        for (int q = 0; q < PK; ++q) {
-            const unsigned g = (unsigned)(lane + 64 * q) * 16u;
-            if (g < SLOT) {
-                const char *src = g < (unsigned)(ABLK * ES) ? vrow + g : xrow + (g - ABLK * ES);
-                if ((p.nt & 1) && (q + 1) * 1024 <= ABLK * ES)
-                    asm volatile("s_mov_b32 m0, %1\n\t"
-                                 "s_nop 0\n\t"
-                                 "global_load_lds_dwordx4 %0, off nt"
-                                 :
-                                 : "v"(src), "s"(__builtin_amdgcn_readfirstlane(base + (unsigned)q * 1024u))
-                                 : "memory", "m0");
-                else
-                    asm volatile("s_mov_b32 m0, %1\n\t"
-                                 "s_nop 0\n\t"
-                                 "global_load_lds_dwordx4 %0, off"
-                                 :
-                                 : "v"(src), "s"(__builtin_amdgcn_readfirstlane(base + (unsigned)q * 1024u))
-                                 : "memory", "m0");
-            }
-        }
-    };
-    const int ar = lane & 15, kq = lane >> 4;
-    const bool arow_ok = ar < BI, bcol_ok = ar < nc;
-    // (current and next fragments as separate arrays copied at the end of a block: a run-time
-    // index into a two-deep array would put them in scratch)
-    E fa[KS], fb[KS], ga[KS], gb[KS];
-    auto frag = [&](long bl, E (&a_)[KS], E (&b_)[KS]) {
-        const E *sa = (const E *)(smem + (slot0 - lds_u32(smem)) + (unsigned)(bl & (RING - 1)) * SLOT);
-        const E *sx = sa + ABLK;
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-            const int e = ks * 4 + kq;
-            a_[ks] = arow_ok ? (p.block_im_fast ? sa[ar + e * BI] : sa[ar * BD + e]) : E{};
-            b_[ks] = bcol_ok ? sx[e * nc + ar] : E{};
-        }
-    };
-    // the block columns of the current row and the next; those of the row after next travel by
-    // LDS-DMA into a two-deep per-wave buffer behind the slot rings (counted by vmcnt in order
-    // with the blocks: landed once any block issued after it has been waited for)
-    int jc[NNZ], jn[NNZ];
-#pragma unroll
-    for (int k = 0; k < NNZ; ++k) {
-        jc[k] = p.jj[base * NNZ + k];
-        jn[k] = nr > 1 ? p.jj[(base + S) * NNZ + k] : 0;
-    }
-    const unsigned jbuf = lds_u32(smem) + 4u * RING * SLOT + (unsigned)w * 128u;
-    const int *jlds = (const int *)(smem + 4u * RING * SLOT + (unsigned)w * 128u);
-    // prologue: blocks 0 .. PD - 1 (all of row 0), then block 0's fragments
-#pragma unroll
-    for (int k = 0; k < PD; ++k) issue(k, base, k, jc[k]);
-    wait_vmcnt_c<PK * (PD - 1)>();
-    frag(0, fa, fb);
-    acc_t accR = acc_t{0, 0, 0, 0}, accI = acc_t{0, 0, 0, 0};
-    for (long j = 0; j < nr; ++j) {
-        const long row = base + j * S;
-        if (j + 2 < nr && lane < NNZ)
-            asm volatile("s_mov_b32 m0, %1\n\t"
-                         "s_nop 0\n\t"
-                         "global_load_lds_dword %0, off"
-                         :
-                         : "v"(p.jj + (row + 2 * S) * NNZ + lane),
-                           "s"(jbuf + (unsigned)(j & 1) * 64u)
-                         : "memory", "m0");
-#pragma unroll
-        for (int k = 0; k < NNZ; ++k) {
-            const long b = j * NNZ + k;
-            // block b + PD (row j or j + 1, nonzero (k + PD) % NNZ: a compile-time pick); its
-            // slot held block b - 1, whose fragments were read (and waited for) two blocks ago
-            if (b + PD < nb) {
-                if (k + PD < NNZ) issue(b + PD, row, k + PD, jc[(k + PD) % NNZ]);
-                else issue(b + PD, row + S, (k + PD) % NNZ, jn[(k + PD) % NNZ]);
-            }
-            if (b + 1 < nb) {
-                // block b + 1 landed: the PK instructions of each of the PD - 1 blocks issued
-                // after it may stay in flight (in the wave's last PD blocks: wait for all -- a
-                // compile-time count keeps the unrolled row small, for the instruction cache)
-                if (b + PD < nb) wait_vmcnt_c<PK * (PD - 1)>();
-                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                frag(b + 1, ga, gb);
-            }
-            if (jc[k] >= 0) {
-#pragma unroll
-                for (int ks = 0; ks < KS; ++ks) {
-                    const E a = fa[ks], bb = fb[ks];
-                    if constexpr (CPLX) {
-                        accR = BsrMfma<R>::mma(a.x, bb.x, accR);
-                        accI = BsrMfma<R>::mma(a.x, bb.y, accI);
-                        accR = BsrMfma<R>::mma(-a.y, bb.y, accR);
-                        accI = BsrMfma<R>::mma(a.y, bb.x, accI);
-                    } else {
-                        accR = BsrMfma<R>::mma(a, bb, accR);
-                    }
-                }
-            }
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-                fa[ks] = ga[ks];
-                fb[ks] = gb[ks];
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int rr = BsrMfma<R>::row(lane, q);
-            if (rr >= BI || !bcol_ok) continue;
-            const long img = row * BI + rr;
-            E *yp = YROW ? y + img * p.ldy + ar : y + img + ar * p.ldy;
-            E out;
-            if constexpr (CPLX)
-                out = Ops<E>::scale(E{accR[q], accI[q]}, p.alpha_re, p.alpha_im);
-            else
-                out = Ops<E>::scale(accR[q], p.alpha_re, p.alpha_im);
-            *yp = p.add ? Ops<E>::add(*yp, out) : out;
-        }
-        accR = acc_t{0, 0, 0, 0};
-        accI = acc_t{0, 0, 0, 0};
-        // the columns of row j + 2: their DMA (issued at this row's start) landed before block
-        // (j + 1) NNZ, which the last block of this row waited for
-#pragma unroll
-        for (int k = 0; k < NNZ; ++k) {
-            jc[k] = jn[k];
-            jn[k] = j + 2 < nr ? __builtin_amdgcn_readfirstlane(jlds[(j & 1) * 16 + k]) : 0;
-        }
-    }
-}
-
-/// false: not this shape (bsr.stream workgroups per CU; the ring depth from bsr.stream_ring)
-template <typename R, bool CPLX, int BI, int BD, int NNZ>
-bool launch_bsr_mfma_stream(const BsrArgs &a, bool yrow, hipStream_t s) {
-    typedef typename BsrMfmaElem<R, CPLX>::type E;
-    constexpr int ES = (int)sizeof(E);
-    const long slot = (long)(BI * BD + BD * a.ncols) * ES;
-    if (a.x_rows <= 0 || a.ncols < 1 || a.ncols > 16 || slot % 16 || ((size_t)a.x & 15) ||
-        ((size_t)a.v & 15) || a.block_rows <= 0)
-        return false;
-    // DMA instructions per slot: exactly ceil(slot / 1 KB), so none is wholly masked (the wait
-    // counts assume every one of them issues)
-    const int pk = (int)((slot + 1023) / 1024);
-    const int ring = g_bsr_tune.stream_ring;
-    if ((ring != 4 && ring != 8) || pk < 2 || pk > 6) return false;
-    int dev = 0, cus = 256;
-    SBX_HIP_CHECK(hipGetDevice(&dev));
-    SBX_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    const long per_cu = std::max(1, g_bsr_tune.stream);
-    const long blocks = std::min((long)cus * per_cu, (a.block_rows + 3) / 4);
-    // 4 waves x ring slots, then 4 waves x two 64-byte column buffers
-    const size_t lds = (size_t)4 * ring * slot + 4 * 128;
-    if (lds > 160 * 1024) return false;
-    // a slot's DMA writes the slot's bytes only (lanes past it are inactive)
-    check_dma_lds("bsr_mfma_stream_kernel", lds, 0, 0, 4L * ring * slot + 4 * 128);
-    g_bsr_tune.last = 15;
-    KernelTimer timer("bsr", s);
-    auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), lds, s, a); };
-    auto with_pk = [&](auto yr, auto rg) {
-        constexpr bool YR = decltype(yr)::value;
-        constexpr int RG = decltype(rg)::value;
-        switch (pk) {
-        case 2: go(bsr_mfma_stream_kernel<R, CPLX, BI, BD, YR, NNZ, RG, 2>); break;
-        case 3: go(bsr_mfma_stream_kernel<R, CPLX, BI, BD, YR, NNZ, RG, 3>); break;
-        case 4: go(bsr_mfma_stream_kernel<R, CPLX, BI, BD, YR, NNZ, RG, 4>); break;
-        case 5: go(bsr_mfma_stream_kernel<R, CPLX, BI, BD, YR, NNZ, RG, 5>); break;
-        default: go(bsr_mfma_stream_kernel<R, CPLX, BI, BD, YR, NNZ, RG, 6>); break;
-        }
-    };
-    using T = std::true_type;
-    using F = std::false_type;
-    using G4 = std::integral_constant<int, 4>;
-    using G8 = std::integral_constant<int, 8>;
-    if (yrow) ring == 4 ? with_pk(T{}, G4{}) : with_pk(T{}, G8{});
-    else ring == 4 ? with_pk(F{}, G4{}) : with_pk(F{}, G8{});
-    SBX_HIP_CHECK(hipGetLastError());
-    return true;
-}
-
 /// false: not this shape (the register-staged kernel runs)
 template <typename R, bool CPLX, int BI, int BD, int NNZ, int PD>
 bool launch_bsr_mfma_dma(const BsrArgs &a, bool yrow, hipStream_t s) {
@@ -1072,20 +662,11 @@ void launch_bsr_mfma(const BsrArgs &a, int nnz, bool yrow, bool xrow, hipStream_
     // contiguous x blocks (row-major x, ldx == ncols <= 16), 9 blocks per row: the blocks staged
     // by LDS-DMA one ahead (16^4 complex<double> n = 12: 426 us for the round-1 fragment kernel,
     // 348-355 us staged; the chain's complex<float> operator 985 -> 693 us with packed slots;
-    // two or three blocks of lookahead were slower, profiles/r02_bsr_blk_sweep.txt)
-    if constexpr (CPLX && BI == 12 && BD == 12) {
-        // values in registers (bsr.vreg = lookahead in blocks: 1, 2 or 3)
-        if (g_bsr_tune.variant == 0 && g_bsr_tune.vreg > 0 && nnz == 9 && xrow && a.ldx == a.ncols &&
-            !(g_gemm_tune.m3 > 0) &&
-            (g_bsr_tune.vreg == 3   ? launch_bsr_mfma_vreg<R, 9, 3>(a, yrow, s)
-             : g_bsr_tune.vreg == 2 ? launch_bsr_mfma_vreg<R, 9, 2>(a, yrow, s)
-                                    : launch_bsr_mfma_vreg<R, 9, 1>(a, yrow, s)))
-            return;
-    }
-    // the streaming form: a few waves per CU, each a contiguous range of rows (bsr.stream)
-    if (g_bsr_tune.variant == 0 && g_bsr_tune.stream > 0 && nnz == 9 && xrow && a.ldx == a.ncols &&
-        !(CPLX && g_gemm_tune.m3 > 0) && launch_bsr_mfma_stream<R, CPLX, BI, BD, 9>(a, yrow, s))
-        return;
+    // two or three blocks of lookahead were slower, profiles/r02_bsr_blk_sweep.txt; round 6:
+    // the value blocks straight into the MFMA fragments with x by LDS-DMA, 757 against 689 us on
+    // the chain's operator, and a streaming form with 1-4 workgroups per CU whose waves stream
+    // every W-th row through an 8-slot ring, 787-1221 against 695 us -- both removed again,
+    // profiles/r06_bsr12_vreg_chain.txt, r06_bsr12_stream_chain.txt, commit ad3532b)
     if (g_bsr_tune.variant == 0 && nnz == 9 && xrow && a.ldx == a.ncols && a.ncols <= 16 &&
         (g_bsr_tune.blk_pd == 2   ? launch_bsr_mfma_dma<R, CPLX, BI, BD, 9, 2>(a, yrow, s)
          : g_bsr_tune.blk_pd == 3 ? launch_bsr_mfma_dma<R, CPLX, BI, BD, 9, 3>(a, yrow, s)
@@ -1911,7 +1492,6 @@ void launch_bsr(const BsrDesc &d, int device) {
     a.add = d.add ? 1 : 0;
     a.ilv = 2; // an XCD's row chunks visited as two interleaved halves (bsr_ell9_kernel)
     a.nt = g_bsr_tune.nt;
-    a.smap = g_bsr_tune.stream_map;
     a.tiles[0] = d.tiles[0];
     a.tiles[1] = d.tiles[1];
     switch (d.t) {

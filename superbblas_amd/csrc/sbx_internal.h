@@ -282,13 +282,6 @@ struct BsrTune {
     long kron_spin_min_cols = 8; ///< ... from this many rhs columns (at least 8)
     int kron_order = 1;          ///< ... rows in the operator's XCD order (bsr.cpp build_kron_order)
     int blk_pd = 1; ///< 12x12 blocks by LDS-DMA: blocks in flight ahead of the one in use (1..3)
-    int stream = 0; ///< 12x12 blocks, 9 per row, row-major x (ldx == ncols <= 16): the streaming kernel
-                    ///< (bsr_mfma_stream_kernel) with this many 4-wave workgroups per CU (0 = off)
-    int stream_ring = 8; ///< ... ring slots per wave (4 or 8: blocks in flight + 1)
-    int stream_map = 0;  ///< ... rows: 0 round robin over the chip's waves, 1 an eighth per XCD
-    int vreg = 0;   ///< 12x12 complex blocks, 9 per row, row-major x (ldx == ncols <= 16): the values
-                    ///< straight into MFMA fragments, x by LDS-DMA (bsr_mfma_vreg_kernel), this many
-                    ///< blocks ahead (1..3; 0 = off: bsr_mfma_dma_kernel)
     int tile = 0;   ///< 9-point 3x3 complex<double> operators, row-major x and y: site tiles with
                     ///< their halo staged in LDS (bsr_ell9_tile_kernel) ... 1: 16-site tiles, slices
                     ///< of 8 rhs columns (opt-in: 16^4 n = 64 180 vs 169 us for the row-chunk kernel,
@@ -306,7 +299,7 @@ struct BsrTune {
     /// 5 Kronecker on MFMA, 6 the same with packed column slots, 7 12x12 blocks by LDS-DMA, 8 the
     /// same with packed slots, 9 Kronecker spin first (VALU), 10 12x12 fragment gathers (9 blocks
     /// per row), 11 12x12 generic rows, 12 Kronecker spin first with XOR-partner spin rows,
-    /// 13 site tiles of 8 sites and 16 columns (3x3), 14 12x12 values in registers, 15 12x12 streaming,
+    /// 13 site tiles of 8 sites and 16 columns (3x3),
     /// 0 another kernel
     std::atomic<int> last{0};
 };

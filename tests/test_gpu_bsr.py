@@ -343,77 +343,3 @@ def test_bsr_image_side_kernel_form(gpu, spin, color, ncols, form):
     op.destroy()
     assert used == form, used
     assert np.array_equal(ty.cpu().numpy(), yref)
-
-
-FORMS_12 = [("bsr.vreg", 1, None, 14), ("bsr.vreg", 2, None, 14), ("bsr.vreg", 3, None, 14),
-            ("bsr.stream", 1, 4, 15), ("bsr.stream", 1, 8, 15), ("bsr.stream", 2, 8, 15),
-            ("bsr.stream", 3, 4, 15, 1), ("bsr.stream", 1, 8, 15, 1)]
-
-
-@pytest.mark.parametrize("form", FORMS_12, ids=lambda f: "%s%d_r%s_m%d" % (f[0][4:], f[1], f[2],
-                                                                          f[4] if len(f) > 4 else 0))
-@pytest.mark.parametrize("dtype,ncols", [(np.complex64, 12), (np.complex64, 16), (np.complex64, 5),
-                                         (np.complex128, 12), (np.complex128, 13), (np.complex128, 1),
-                                         (np.float32, 12), (np.float64, 3)])
-@pytest.mark.parametrize("bimf,skip,ycol", [(False, False, False), (True, False, False),
-                                            (False, True, False), (True, True, True)])
-def test_bsr_12x12_register_and_stream_forms(gpu, form, dtype, ncols, bimf, skip, ycol):
-    """bsr.vreg (bsr_mfma_vreg_kernel: the value blocks straight into the MFMA fragments, three
-    contiguous k per lane quarter, x by LDS-DMA 1-3 blocks ahead; complex only) and bsr.stream
-    (bsr_mfma_stream_kernel: 1-2 workgroups per CU, each wave a contiguous range of rows streamed
-    through a 4- or 8-slot ring across row boundaries): column-major blocks (bimf), skipped
-    blocks (column -1, a row with none, the last block of the value array), column-major y;
-    exact vs the oracle on integer-valued operators."""
-    import torch
-    import superbblas_amd as sb
-    from _common import TYPE_OF
-    key, val, ring, kern = form[:4]
-    smap = form[4] if len(form) > 4 else 0
-    cplx = np.dtype(dtype).kind == "c"
-    if key == "bsr.vreg" and not cplx:
-        pytest.skip("the values-in-registers form is complex only")
-    # (the streaming form at 6^4: 1296 rows over 1024 or 2048 waves -- ranges of one and two rows,
-    # and idle waves)
-    L, spin, color = (6 if key == "bsr.stream" else 4), 4, 3
-    dim, ii, jj, vals, nb = lattice_operator(L, spin, color, dtype)
-    b = spin * color
-    vol = L ** 4
-    if skip:
-        jj = jj.reshape(vol, nb, 6).copy()
-        jj[::3, 1, :] = -1
-        jj[-1, nb - 1, :] = -1
-        jj[-2, :, :] = -1
-        jj = jj.reshape(-1)
-    g = np.arange(vol * b * ncols)
-    x = ((g % 9 - 4) + (1j * (g % 5 - 2) if cplx else 0)).astype(dtype)
-    n = vol * b * ncols
-    yref = np.zeros(n, dtype)
-    oracle_bsr(TYPE_OF[np.dtype(dtype)], dim, 0, vol, b, b, ii, jj, vals, bimf, x, ncols, True,
-               yref, vol * b if ycol else ncols, not ycol, ncols, 1.0)
-    full = [([0] * 6, dim)]
-    blk = [1, 1, 1, 1, spin, color]
-    tv = torch.from_numpy(vals).to(gpu)
-    op = sb.create_bsr(full, dim, full, dim, blk, blk, bimf, [torch.from_numpy(ii).to(gpu)],
-                       [torch.from_numpy(jj).to(gpu)], [tv])
-    dimx = [1, L, L, L, L, spin, color, ncols]
-    oy, dimy = ("pnxyztsc", [1, ncols, L, L, L, L, spin, color]) if ycol else ("pxyztscn", dimx)
-    ty = torch.full((n,), 3.0, dtype=getattr(torch, np.dtype(dtype).name), device=gpu)
-    old = sb.tune_get(key)
-    old_ring, old_map = sb.tune_get("bsr.stream_ring"), sb.tune_get("bsr.stream_map")
-    sb.tune_set(key, val)
-    sb.tune_set("bsr.stream_map", smap)
-    if ring:
-        sb.tune_set("bsr.stream_ring", ring)
-    try:
-        sb.bsr_krylov(1.0, op, "xyztsc", "XYZTSC", [([0] * 8, dimx)], "pXYZTSCn", [0] * 8, dimx,
-                      dimx, [torch.from_numpy(x).to(gpu)], 0.0, [([0] * 8, dimy)], oy, [0] * 8,
-                      dimy, dimy, "p", [ty])
-        torch.cuda.synchronize()
-    finally:
-        sb.tune_set(key, old)
-        sb.tune_set("bsr.stream_ring", old_ring)
-        sb.tune_set("bsr.stream_map", old_map)
-    used = sb.tune_get("bsr.last_kernel")
-    op.destroy()
-    assert used == kern, used
-    assert np.array_equal(ty.cpu().numpy(), yref)

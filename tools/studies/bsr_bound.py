@@ -61,13 +61,7 @@ def main():
     pds = [int(v) for v in os.environ.get("PDS", str(sb.tune_get("bsr.blk_pd"))).split(",")]
     variants = [int(v) for v in os.environ.get("VARIANTS", str(sb.tune_get("bsr.variant"))).split(",")]
     regs = [int(v) for v in os.environ.get("REGS", "-1").split(",")]
-    # VREGS: bsr.vreg values (12x12 complex: values straight into MFMA fragments, round 6)
-    vregs = [int(v) for v in os.environ.get("VREGS", str(sb.tune_get("bsr.vreg"))).split(",")]
-    # STREAMS: bsr.stream values as "workgroups per CU:ring" (12x12 streaming kernel, round 6)
-    # (":ring:map", map = bsr.stream_map)
-    streams = [tuple(int(u) for u in (v + ":%d:%d" % (sb.tune_get("bsr.stream_ring"),
-                                                      sb.tune_get("bsr.stream_map"))).split(":")[:3])
-               for v in os.environ.get("STREAMS", str(sb.tune_get("bsr.stream"))).split(",")]
+    # (VREGS / STREAMS: the round-6 bsr.vreg / bsr.stream experiments, removed again: commit ad3532b)
     tiles = [int(v) for v in os.environ.get("TILES", str(sb.tune_get("bsr.tile"))).split(",")]
     # BLK=12: spin 4 x color 3 blocks (config 3's secondary shape / the chain's operator);
     # DT=cf: complex<float>
@@ -84,15 +78,10 @@ def main():
         op = sb.create_bsr(full, dim, full, dim, blk, blk, False,
                            [torch.full((V,), nnz, dtype=torch.int32, device=dev)],
                            [torch.from_numpy(jj.reshape(-1)).to(dev)], [vals])
-        for n, nt, pd, var, reg, tile, vreg, st in [
-                (n, nt, pd, var, reg, tile, vreg, st) for n in ncols_list for nt in nts for pd in pds
-                for var in variants for reg in regs for tile in tiles for vreg in vregs
-                for st in streams]:
+        for n, nt, pd, var, reg, tile in [(n, nt, pd, var, reg, tile) for n in ncols_list for nt in nts
+                                          for pd in pds for var in variants for reg in regs
+                                          for tile in tiles]:
             sb.tune_set("bsr.tile", tile)
-            sb.tune_set("bsr.vreg", vreg)
-            sb.tune_set("bsr.stream", st[0])
-            sb.tune_set("bsr.stream_ring", st[1])
-            sb.tune_set("bsr.stream_map", st[2])
             sb.tune_set("bsr.variant", var)
             if reg >= 0:  # bsr.reg: the round-5 register-staged experiment (removed again)
                 sb.tune_set("bsr.reg", reg)
@@ -122,7 +111,7 @@ def main():
             t = statistics.median(ts)
             algo = es * (9 * b * b * V + 2 * b * V * n) + 4.0 * (9 * V + V + 1)  # the stencil's
             floor = es * (nnz * b * b * V + 2 * b * V * n) + 4.0 * (nnz * V + V + 1)
-            print(json.dumps({"blk": b, "dtype": str(dt), "kind": kind, "ncols": n, "nt": nt, "blk_pd": pd, "variant": var, "reg": reg, "tile": tile, "vreg": vreg, "stream": "%d:%d:%d" % st,
+            print(json.dumps({"blk": b, "dtype": str(dt), "kind": kind, "ncols": n, "nt": nt, "blk_pd": pd, "variant": var, "reg": reg, "tile": tile,
                               "us": round(t * 1e6, 1),
                               "kernel": sb.tune_get("bsr.last_kernel"),
                               "stencil_bytes_frac_hbm": round(algo / t / 8e12, 4),
