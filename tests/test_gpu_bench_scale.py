@@ -100,17 +100,24 @@ def test_bench_real_startup_nccl_pg(gpu, n):
     assert len(errs) == 3 and line["scale_check_ok"] is True, line
 
 
-def test_bench_configs3_full_size(gpu):
-    """configs[3] at its full size -- the 32^4, n = 64 lattice contraction over the 2x2x2x1 grid
-    of 8 ranks (here sharing the test box's GPU through RCCL's socket transport) -- with the 4a,
-    4b-redistributed answers compared with the same global problem on one GPU (the chain at a
-    reduced lattice: its full size is test_gpu_chain.py's)"""
-    line = _bench_no_launcher(8, ["--steps", "1", "--warmup", "0", "--L", "32", "--ncols", "64",
-                                  "--chain-L", "4", "--chain-T", "8"], timeout=900)
+def test_bench_scale_command_defaults(gpu):
+    """the driver's SCALE command at its defaults -- `bench.py --gpus 8`, nothing else, here with
+    the 8 ranks sharing the test box's GPU (--share-gpu nccl: the real init_process_group("nccl")
+    start-up, one RCCL host id per rank): 20 timed steps of configs[3] (32^4, n = 64, the 2x2x2x1
+    grid), the 4b redistribution and redistributing contraction, and configs[4]'s full 32^3 x 64
+    chain, each checked against the same global problem on one GPU (45 s on the GPU box, peak
+    146 GB of device memory: profiles/r06_scale8_share_nccl*)"""
+    line = _bench_no_launcher(8, [], timeout=900, share="nccl")
     assert line["n_gpus"] == 8 and line["world_size_seen_by_rccl"] == 8
-    assert line["config"]["parallelism"] == "xyzt grid 2x2x2x1"
+    assert line["steps"] == 20 and line["warmup"] == 10
+    assert line["config"]["parallelism"] == "xyzt grid 2x2x2x1" and line["config"]["L"] == 32
+    assert line["config"]["n"] == 64
+    assert "32x32x32x64" in line["chain_dist_workload"]
     errs = {k: v for k, v in line.items() if k.startswith("scale_check_rel_err")}
-    assert {"scale_check_rel_err_4a", "scale_check_rel_err_contraction_redistributed"} <= set(errs)
+    assert set(errs) == {"scale_check_rel_err_4a", "scale_check_rel_err_contraction_redistributed",
+                         "scale_check_rel_err_chain"}, line
     for k, v in errs.items():
         assert v <= (1e-5 if k.endswith("_chain") else 1e-10), (k, v)
     assert line["scale_check_ok"] is True
+    assert line["strong_scaling_vs_1gpu"] > 0 and line["strong_scaling_vs_1gpu_4b"] > 0
+    assert line["redistribute_exact"] is True
