@@ -1237,6 +1237,93 @@ __global__ void __launch_bounds__(256) gemm_rows_kernel(const GemmKArgs p) {
     }
 }
 
+// Small outputs and tall-skinny products straight from global memory into MFMA fragments: one
+// wave per (16 x 16 output tile, batch entry, k-split), no LDS.  The reference's dist.cpp
+// xgemm_batch_strided sweep (tests/dist.cpp:160-195, the Krylov inner products m = n <= 64 with
+// k = the local volume, and the updates m = volume, n = k <= 64) ran through the 64x64 LDS-DMA
+// tiles (99 % MFMA padding at m = n = 8: 0.22 TFLOP/s) or one lane per output row walking k
+// serially (the updates: 1.2 TFLOP/s at n = k = 8), 10-50x under the HBM roofline of those
+// shapes.  Lane (r, q) of a k-step reads A(m0 + r, k + q) and B(k + q, n0 + r) through buffer
+// descriptors (an offset past the range reads zero: rows, columns and k past the ends), UK
+// k-steps per group, the next group's loads issued before the current group's MFMAs; the
+// split-K partials go to the work array and the split-K reduce sums them in split order.
+template <typename R, bool CPLX, int UK>
+__global__ void __launch_bounds__(256) gemm_frag_kernel(const GemmKArgs p) {
+    typedef typename Elem<R, CPLX>::type E;
+    typedef typename Mfma<R>::acc_t acc_t;
+    constexpr int ES = (int)sizeof(E);
+    const int lane = threadIdx.x & 63;
+    const long item = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const long items = (long)p.tm * p.tn * p.batch * p.splits;
+    if (item >= items) return; // whole waves only: MFMA needs all 64 lanes
+    const int split = (int)(item % p.splits);
+    long rest = item / p.splits;
+    const long ti = rest % p.tm;
+    rest /= p.tm;
+    const long tj = rest % p.tn;
+    const long bb = rest / p.tn;
+    const long m0 = ti * 16, n0 = tj * 16;
+    const long k_begin = (long)split * p.kchunk, k_end = min(p.k, k_begin + p.kchunk);
+    const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)((const E *)p.a + bb * p.sa_b), (short)0, (int)p.a_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)((const E *)p.b + bb * p.sb_b), (short)0, (int)p.b_bytes, 0x00020000);
+    const int r = lane & 15, q = lane >> 4;
+    const bool okA = m0 + r < p.m, okB = n0 + r < p.n;
+    const long baseA = (m0 + r) * p.sa_m, baseB = (n0 + r) * p.sb_n;
+    typedef typename std::conditional<sizeof(R) == 8, unsigned long long, unsigned>::type U;
+    const U sign = (U)1 << (sizeof(R) * 8 - 1);
+    const U ma = p.conja ? sign : 0, mb = p.conjb ? sign : 0;
+    auto flip = [](R v, U m) { return __builtin_bit_cast(R, __builtin_bit_cast(U, v) ^ m); };
+    auto load = [&](long k0, E (&a)[UK], E (&b)[UK]) {
+#pragma unroll
+        for (int u = 0; u < UK; ++u) {
+            const long kk = k0 + 4 * u + q;
+            const bool kin = kk < k_end;
+            a[u] = buf_load<E>(rsA, okA && kin ? (unsigned)((baseA + kk * p.sa_k) * ES) : 0x80000000u);
+            b[u] = buf_load<E>(rsB, okB && kin ? (unsigned)((baseB + kk * p.sb_k) * ES) : 0x80000000u);
+        }
+    };
+    acc_t accR = acc_t{0, 0, 0, 0}, accI = acc_t{0, 0, 0, 0};
+    E a[UK], b[UK], an[UK], bn[UK];
+    if (k_begin < k_end) load(k_begin, a, b);
+    for (long k = k_begin; k < k_end; k += 4 * UK) {
+        if (k + 4 * UK < k_end) load(k + 4 * UK, an, bn);
+#pragma unroll
+        for (int u = 0; u < UK; ++u) {
+            if constexpr (CPLX) {
+                const R ar = a[u].x, ai = flip(a[u].y, ma), br = b[u].x, bi = flip(b[u].y, mb);
+                accR = Mfma<R>::mma(ar, br, accR);
+                accI = Mfma<R>::mma(ar, bi, accI);
+                accR = Mfma<R>::mma(-ai, bi, accR);
+                accI = Mfma<R>::mma(ai, br, accI);
+            } else {
+                accR = Mfma<R>::mma(a[u], b[u], accR);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < UK; ++u) {
+            a[u] = an[u];
+            b[u] = bn[u];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const long gi = m0 + Mfma<R>::row(lane, i), gj = n0 + r;
+        if (gi >= p.m || gj >= p.n) continue;
+        const R vr = accR[i], vi = CPLX ? accI[i] : R(0);
+        if (p.splits == 1) {
+            epilogue_store<R>((R *)((E *)p.c + bb * p.sc_b + gi * p.sc_m + gj * p.sc_n), vr, vi, p, CPLX);
+        } else {
+            E *w = (E *)p.work + (((long)split * p.batch + bb) * p.n + gj) * p.m + gi;
+            if constexpr (CPLX)
+                *w = E{vr, vi};
+            else
+                *w = vr;
+        }
+    }
+}
+
 // C = alpha * sum_s W[s] + beta * C, summed in split order (deterministic)
 template <typename R, bool CPLX>
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(const GemmKArgs p) {
@@ -1660,7 +1747,41 @@ template <typename R, bool CPLX> bool launch_skinny(const GemmKArgs &p0, int dev
     return true;
 }
 
+/// The fragment kernel (gemm_frag_kernel) for small outputs with a long k (m, n <= 32) and
+/// tall-skinny products (one output dimension <= 16 with k <= 64, or <= 16 against a long k);
+/// false when the shape is for the tiled kernels
+template <typename R, bool CPLX> bool launch_frag(const GemmKArgs &p0, int device, hipStream_t s) {
+    // (the opt-in 3-multiplication form runs on the tiled kernels only)
+    if (!g_gemm_tune.frag || p0.split || (CPLX && g_gemm_tune.m3 > 0)) return false;
+    // (measured, tools/studies/gemm_skinny_bench.py, profiles/r06_gemm_skinny.txt: inner products
+    // m = n = 8 / 12 / 16 / 32, k = 49152, batch 32: 794 / 792 / 794 / 802 -> 143 / 173 / 228 /
+    // 490 us; updates m = 49152, n = k = 12 / 16: 291 / 453 -> 173 / 208 us; n = k <= 4 stay on
+    // the rows kernel, 21-49 us against 122)
+    const bool small = p0.m <= 32 && p0.n <= 32;
+    const bool tall = (p0.n <= 16 && p0.n > 4 && ((p0.k <= 64 && p0.k > 4) || p0.m <= 16)) ||
+                      (p0.m <= 16 && p0.m > 4 && p0.k <= 64 && p0.k > 4);
+    if (!small && !tall) return false;
+    if (g_gemm_tune.skinny && p0.m <= 4 && p0.n <= 4 && g_gemm_tune.frag < 2) return false;
+    typedef typename Elem<R, CPLX>::type E;
+    constexpr int UK = 4;
+    GemmKArgs p = p0;
+    Scratch work;
+    // ~4096 waves: split-K when the tiles alone are fewer
+    const long items = prepare_launch<E>(p, 16, 16, 4 * UK, 0, 4096, work, device);
+    const long blocks = (items + 3) / 4;
+    if (blocks > 0x7fffffffL) return false;
+    KernelTimer total("gemm_total", s);
+    {
+        KernelTimer timer("gemm", s);
+        hipLaunchKernelGGL((gemm_frag_kernel<R, CPLX, UK>), dim3((unsigned)blocks), dim3(256), 0, s, p);
+        SBX_HIP_CHECK(hipGetLastError());
+    }
+    launch_reduce<R, CPLX>(p, s);
+    return true;
+}
+
 template <typename R, bool CPLX> void launch_typed(const GemmKArgs &p, int device, hipStream_t s) {
+    if (launch_frag<R, CPLX>(p, device, s)) return;
     if (launch_skinny<R, CPLX>(p, device, s)) return;
     // Pick the stage-load thread map from the unit stride of each operand
     const bool ak = (p.sa_k == 1) || (p.sa_m != 1 && std::labs(p.sa_k) <= std::labs(p.sa_m));

@@ -253,6 +253,8 @@ struct GemmTune {
     int skinny = 1; ///< outputs with a dimension of <= 4 (and <= 16 with a short k): the dot / rows
                     ///< kernels instead of MFMA tiles (0 = off)
     int clock = 0; ///< LDS-DMA kernel clock meter (gemm_clock_meter, kernels_gemm.hip; 0 = off)
+    int frag = 1;  ///< small outputs (m, n <= 32) and tall-skinny products on gemm_frag_kernel (MFMA
+                   ///< fragments straight from global memory); 2 also for m, n <= 4; 0 = off
 };
 /// The LDS-DMA GEMM's clock meter of a device: {shader clock cycles, 100 MHz ticks, launches}
 /// summed since the last reset (zeros when the meter was never enabled)

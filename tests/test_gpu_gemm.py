@@ -282,3 +282,27 @@ def test_host_context_calls_use_current_device(gpu):
     assert rc == 0, sb._lib.sbx_last_error()
     assert np.array_equal(dst, src)
     assert sb.tune_get("detail.last_device") == dev
+
+
+# tests/dist.cpp's xgemm_batch_strided sweep at a reduced k (inner products m = n, k = volume;
+# updates m = volume, n = k) and neighbouring shapes: gemm_frag_kernel (MFMA fragments straight
+# from global memory; gemm.frag 1, the default) against the oracle, with partial tiles, split-K
+# and every trans pair; gemm.frag 0 runs the same shapes through the other kernels
+FRAG = [(5, 5, 6144, 4), (8, 8, 6144, 4), (12, 12, 3000, 3), (16, 16, 6144, 2), (32, 32, 4096, 2),
+        (17, 30, 777, 3), (6144, 8, 8, 2), (6144, 12, 12, 2), (3000, 16, 16, 1), (999, 13, 64, 2),
+        (16, 1, 1 << 15, 1), (1, 16, 1 << 15, 1), (16, 5000, 7, 1), (1000, 3, 50, 2)]
+
+
+@pytest.mark.parametrize("dtype", [np.complex128, np.float64, np.complex64, np.float32])
+@pytest.mark.parametrize("ta,tb", [("N", "N"), ("T", "N"), ("C", "N"), ("N", "C"), ("C", "T")])
+@pytest.mark.parametrize("m,n,k,batch", FRAG)
+@pytest.mark.parametrize("frag", [1, 0])
+def test_gemm_frag(gpu, dtype, ta, tb, m, n, k, batch, frag):
+    import superbblas_amd as sb
+    old = sb.tune_get("gemm.frag")
+    sb.tune_set("gemm.frag", frag)
+    try:
+        out, ref = _run(gpu, dtype, ta, tb, m, n, k, batch, 0.5 - 0.25j, 0.75 + 0.5j, pad=1)
+    finally:
+        sb.tune_set("gemm.frag", old)
+    assert rel_err(out, ref) < TOL[dtype]

@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""tests/dist.cpp's xgemm_batch_strided shapes (test_gemm, tests/dist.cpp:160-195) at its default
+lattice (local volume 16*16*16*32*... k = 49152 sites x colors, batch 32): inner products
+(m = n = s, k = 49152) and updates (m = 49152, n = k = s), complex<double>, with gemm.frag on and
+off (and gemm.skinny), timed by the library's kernel timers (GEMM + split-K reduce).  Reports
+TFLOP/s (8 real flops per complex MAC) and the HBM rate of the operand and output bytes.  Not
+part of the product.  FRAGS=1,0: the gemm.frag values; SIZES=1,2,4,8,12,16,32,64."""
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import superbblas_amd as sb  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda:0")
+    K, batch = 49152, 32
+    sizes = [int(v) for v in os.environ.get("SIZES", "1,2,4,8,12,16,32,64").split(",")]
+    frags = [int(v) for v in os.environ.get("FRAGS", "1,0").split(",")]
+    for kind in ("inner", "update"):
+        for s in sizes:
+            m, n, k = (s, s, K) if kind == "inner" else (K, s, s)
+            ta, tb = ("C", "N") if kind == "inner" else ("N", "N")
+            lda = k if ta != "N" else m
+            a = torch.randn(batch * m * k, dtype=torch.complex128, device=dev)
+            b = torch.randn(batch * k * n, dtype=torch.complex128, device=dev)
+            c = torch.zeros(batch * m * n, dtype=torch.complex128, device=dev)
+            for frag in frags:
+                sb.tune_set("gemm.frag", frag)
+
+                def f():
+                    sb.xgemm_batch_strided(ta, tb, m, n, k, 1.0, a, lda, m * k, b, k, k * n, 0.0,
+                                           c, m, m * n, batch)
+                for _ in range(5):
+                    f()
+                torch.cuda.synchronize()
+                ts = []
+                for _ in range(3):
+                    sb.timings_enable(True)
+                    sb.timings_reset()
+                    for _ in range(10):
+                        f()
+                    torch.cuda.synchronize()
+                    ms, calls = sb.timings_get("gemm_total")
+                    sb.timings_enable(False)
+                    ts.append(ms / calls / 1e3)
+                t = statistics.median(ts)
+                flops = 8.0 * m * n * k * batch
+                byts = 16.0 * batch * (m * k + k * n + m * n)
+                print(json.dumps({"kind": kind, "m": m, "n": n, "k": k, "batch": batch, "frag": frag,
+                                  "us": round(t * 1e6, 1), "TFLOPs": round(flops / t / 1e12, 3),
+                                  "TBps": round(byts / t / 1e12, 3)}), flush=True)
+            del a, b, c
+    sb.tune_set("gemm.frag", 1)
+
+
+if __name__ == "__main__":
+    main()
