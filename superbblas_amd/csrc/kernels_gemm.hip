@@ -349,22 +349,14 @@ struct DmaOperand {
     static constexpr int NI = (GTOT + NTH - 1) / NTH; // DMA lanes per thread per slab
     // a partial last pass is skipped by whole waves (a DMA instruction writes 64 lanes of LDS,
     // out-of-range lanes included): the image must be a whole number of wave passes
-    static_assert(GTOT * EPG == R * BKK && GTOT % 64 == 0 && GR >= 1 && (!XK || GR <= 16 || GR == 20),
+    static_assert(GTOT * EPG == R * BKK && GTOT % 64 == 0 && GR >= 1 && (!XK || GR <= 16),
                   "tile/threads mismatch");
     unsigned roff[NI]; // byte offset of this lane's granule at k0 = 0
     int kl[NI];        // first k of the granule within the slab
     bool rok[NI];
     // K-major image: granule swizzle so that 16 consecutive rows read at one k hit distinct
-    // 16-B bank groups (a 256-B bank row holds 16/GR image rows).  GR = 20 (20-deep slabs of
-    // 16-B elements): a row starts 4 bank groups after the previous one, so rows r and r + 4
-    // collide unless the low two bits of the granule index are flipped by (r / 4) mod 4 (the
-    // flip stays inside an aligned group of four granules, so inside the row)
-    static constexpr bool PW2 = (GR & (GR - 1)) == 0;
-    static_assert(PW2 || GR == 20, "granules per row: a power of two or 20");
-    static __device__ __forceinline__ int swz(int row) {
-        if constexpr (PW2) return (row / (16 / GR)) & (GR - 1);
-        else return (row >> 2) & 3;
-    }
+    // 16-B bank groups (a 256-B bank row holds 16/GR image rows)
+    static __device__ __forceinline__ int swz(int row) { return (row / (16 / GR)) & (GR - 1); }
     __device__ __forceinline__ void init(int tid, long r0, long nrows, long s_r, long s_k,
                                          bool split = false, long r_lo = 1, long s_r_hi = 0) {
 #pragma unroll
@@ -424,20 +416,13 @@ struct DmaOperand {
 template <int R, int BKK, int LWT, int ES> struct DmaRowsK {
     static constexpr int EPG = 16 / ES, GR = BKK / EPG, GTOT = R * BKK / EPG, NI = GTOT / LWT;
     static constexpr int RSTEP = LWT / GR; // rows between a lane's consecutive granules
-    static constexpr bool PW2 = (GR & (GR - 1)) == 0;
-    // (the swizzle of DmaOperand<true>: the same for a lane's every granule)
-    static_assert(GTOT % LWT == 0 && LWT % GR == 0 &&
-                      (PW2 ? GR <= 16 && (RSTEP / (16 / GR)) % GR == 0 : GR == 20 && RSTEP % 16 == 0),
+    static_assert(GTOT % LWT == 0 && LWT % GR == 0 && GR <= 16 && (RSTEP / (16 / GR)) % GR == 0,
                   "loader lane map");
-    static __device__ __forceinline__ int swz(int row) {
-        if constexpr (PW2) return (row / (16 / GR)) & (GR - 1);
-        else return (row >> 2) & 3;
-    }
     unsigned off0, step;
     int k, rleft;
     __device__ __forceinline__ void init(int tid, long r0, long nrows, long s_r, long s_k) {
         const int r = tid / GR;
-        k = ((tid % GR) ^ swz(r)) * EPG;
+        k = ((tid % GR) ^ ((r / (16 / GR)) & (GR - 1))) * EPG;
         rleft = (int)min(nrows - r0 - r, (long)0x7fffffff);
         off0 = (unsigned)(((r0 + r) * s_r + (long)k * s_k) * ES); // (used only while in range)
         step = (unsigned)((long)RSTEP * s_r * ES);
@@ -1626,12 +1611,6 @@ void launch_tiled(const GemmKArgs &p, int device, hipStream_t stream) {
                 // loader waves (gemm.loaders / gemm.dma_spread, K-major operands without split
                 // groups): only waves 0..LW-1 issue the slab DMA
                 const int lw = p.split ? 0 : g_gemm_tune.loaders, sp = g_gemm_tune.dma_spread;
-                // 20-deep slabs (gemm.slab 20): the two slab buffers fill the 160 KB of LDS, one
-                // barrier per 20 k instead of 16 (10 loader waves: 2560 granules per operand)
-                if (g_gemm_tune.slab == 20 && lw > 0)
-                    return launch_dma_cfg<R, CPLX, AK, BK, 128, 128, 20, 4, 4, false, false, 1, false, 10, 1>(p, device, stream, 0, 256);
-                if (g_gemm_tune.slab == 20)
-                    return launch_dma_cfg<R, CPLX, AK, BK, 128, 128, 20, 4, 4, false>(p, device, stream, 0, 256);
                 if (lw == 4 && sp == 4)
                     launch_dma_cfg<R, CPLX, AK, BK, 128, 128, 16, 4, 4, false, false, 1, false, 4, 4>(p, device, stream, 0, 256);
                 else if (lw == 4)

@@ -253,8 +253,6 @@ struct GemmTune {
     int skinny = 1; ///< outputs with a dimension of <= 4 (and <= 16 with a short k): the dot / rows
                     ///< kernels instead of MFMA tiles (0 = off)
     int clock = 0; ///< LDS-DMA kernel clock meter (gemm_clock_meter, kernels_gemm.hip; 0 = off)
-    int slab = 16; ///< complex<double> 128x128 LDS-DMA kernel, K-major operands: slab depth (16, or 20: the
-                   ///< two buffers fill the 160 KB of LDS)
     int frag = 1;  ///< small outputs (m, n <= 32) and tall-skinny products on gemm_frag_kernel (MFMA
                    ///< fragments straight from global memory); 2 also for m, n <= 4; 0 = off
 };

@@ -306,23 +306,3 @@ def test_gemm_frag(gpu, dtype, ta, tb, m, n, k, batch, frag):
     finally:
         sb.tune_set("gemm.frag", old)
     assert rel_err(out, ref) < TOL[dtype]
-
-
-@pytest.mark.parametrize("dtype", [np.complex128])
-@pytest.mark.parametrize("m,n,k,batch", [(256, 256, 1000, 2), (129, 200, 20, 1), (300, 140, 41, 3),
-                                         (128, 128, 8, 1), (256, 128, 3080, 1)])
-def test_gemm_slab20(gpu, dtype, m, n, k, batch):
-    """20-deep slabs (gemm.slab 20: the two slab buffers fill the 160 KB of LDS; the K-major slab
-    image swizzled by flipping the low two granule bits per four rows), with the 10 loader waves
-    and with every wave loading: against the oracle, partial tiles and partial slabs"""
-    import superbblas_amd as sb
-    old_s, old_l = sb.tune_get("gemm.slab"), sb.tune_get("gemm.loaders")
-    try:
-        for lw in (8, 0):
-            sb.tune_set("gemm.slab", 20)
-            sb.tune_set("gemm.loaders", lw)
-            out, ref = _run(gpu, dtype, "T", "N", m, n, k, batch, 1.0 - 0.5j, 0.5)
-            assert rel_err(out, ref) < TOL[dtype], lw
-    finally:
-        sb.tune_set("gemm.slab", old_s)
-        sb.tune_set("gemm.loaders", old_l)

@@ -13,7 +13,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspa
 import superbblas_amd as sb  # noqa: E402
 
 VARIANTS = [tuple(int(x) for x in v.split(":")) for v in
-            os.environ.get("VARIANTS", "0:1,4:1,4:4,8:1,8:4,16:4").split(",")]  # loaders:spread[:nt[:slab]]
+            os.environ.get("VARIANTS", "0:1,4:1,4:4,8:1,8:4,16:4").split(",")]  # loaders:spread[:nt]
 
 
 def main():
@@ -35,7 +35,7 @@ def main():
         sb.contraction(1.0, [(z7, d0)], z7, d0, d0, "tnsxyzc", False, [v0], [(z7, d0)], z7, d0,
                        d0, "tNSxyzc", False, [v1], 0.0, [(z5, dr)], z5, dr, dr, "tNSns", [vr])
 
-    ref = {}
+    ref = None
     times = {v: [] for v in VARIANTS}
     for _ in range(30):  # clocks up
         step()
@@ -46,8 +46,6 @@ def main():
             sb.tune_set("gemm.loaders", lw)
             sb.tune_set("gemm.dma_spread", sp)
             sb.tune_set("gemm.dma_nt", var[2] if len(var) > 2 else 0)
-            slab = var[3] if len(var) > 3 else 16
-            sb.tune_set("gemm.slab", slab)
             step()
             torch.cuda.synchronize()
             sb.timings_enable(True)
@@ -59,20 +57,17 @@ def main():
             ms, calls = sb.timings_get("gemm")
             sb.timings_enable(False)
             times[var].append(ms / calls)
-            # (the slab depth changes the split-K chunks, hence the summation order)
-            if slab not in ref:
-                ref[slab] = vr.clone()
-            elif not torch.equal(ref[slab], vr):
+            if ref is None:
+                ref = vr.clone()
+            elif not torch.equal(ref, vr):
                 print(json.dumps({"error": "results differ", "lw": lw, "sp": sp,
                                   "maxdiff": float((ref - vr).abs().max())}), flush=True)
     sb.tune_set("gemm.loaders", 8)
     sb.tune_set("gemm.dma_spread", 1)
     sb.tune_set("gemm.dma_nt", 0)
-    sb.tune_set("gemm.slab", 16)
     for var, t in times.items():
         t = sorted(t)
         print(json.dumps({"loaders": var[0], "spread": var[1], "nt": var[2] if len(var) > 2 else 0,
-                          "slab": var[3] if len(var) > 3 else 16,
                           "gemm_ms_min": round(t[0], 4),
                           "gemm_ms_median": round(t[len(t) // 2], 4),
                           "TFLOPs_median": round(flops / t[len(t) // 2] / 1e9, 2)}), flush=True)
