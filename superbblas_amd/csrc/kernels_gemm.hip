@@ -1168,18 +1168,27 @@ __global__ void __launch_bounds__(256) gemm_dot_kernel(const GemmKArgs p) {
     for (int i = 0; i < MM; ++i)
 #pragma unroll
         for (int j = 0; j < NN; ++j) acc[i][j] = zero_elem<E>();
-    for (long k = k0 + threadIdx.x; k < k1; k += 256) {
-        E a[MM], b[NN];
+    // four k per thread per pass, all their loads issued before the first product
+    constexpr int U = 4;
+    for (long k = k0 + threadIdx.x; k < k1; k += 256 * U) {
+        E a[U][MM], b[U][NN];
 #pragma unroll
-        for (int i = 0; i < MM; ++i)
-            a[i] = i < m ? conj_if(A[i * p.sa_m + k * p.sa_k], p.conja) : zero_elem<E>();
+        for (int u = 0; u < U; ++u) {
+            const long kk = k + 256L * u;
+            const bool in = kk < k1;
 #pragma unroll
-        for (int j = 0; j < NN; ++j)
-            b[j] = j < n ? conj_if(B[k * p.sb_k + j * p.sb_n], p.conjb) : zero_elem<E>();
+            for (int i = 0; i < MM; ++i)
+                a[u][i] = in && i < m ? conj_if(A[i * p.sa_m + kk * p.sa_k], p.conja) : zero_elem<E>();
 #pragma unroll
-        for (int i = 0; i < MM; ++i)
+            for (int j = 0; j < NN; ++j)
+                b[u][j] = in && j < n ? conj_if(B[kk * p.sb_k + j * p.sb_n], p.conjb) : zero_elem<E>();
+        }
 #pragma unroll
-            for (int j = 0; j < NN; ++j) acc[i][j] = madd(acc[i][j], a[i], b[j]);
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int i = 0; i < MM; ++i)
+#pragma unroll
+                for (int j = 0; j < NN; ++j) acc[i][j] = madd(acc[i][j], a[u][i], b[u][j]);
     }
     __shared__ E red[4][MM * NN];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1687,8 +1696,9 @@ template <typename R, bool CPLX> bool launch_skinny(const GemmKArgs &p0, int dev
     typedef typename Elem<R, CPLX>::type E;
     GemmKArgs p = p0;
     if (p.m <= 4 && p.n <= 4) {
-        // split-K to ~256 workgroups, chunks of >= 1024 k
-        long splits = std::max(1L, std::min((256 + p.batch - 1) / p.batch, (p.k + 1023) / 1024));
+        // split-K to ~gemm.dot_wgs workgroups (256: one per CU), chunks of >= 1024 k
+        const long wgs = std::max(1, g_gemm_tune.dot_wgs);
+        long splits = std::max(1L, std::min((wgs + p.batch - 1) / p.batch, (p.k + 1023) / 1024));
         p.kchunk = (p.k + splits - 1) / splits;
         splits = std::max(1L, (p.k + p.kchunk - 1) / p.kchunk);
         p.splits = (int)splits;

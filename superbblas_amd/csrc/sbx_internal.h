@@ -253,6 +253,8 @@ struct GemmTune {
     int skinny = 1; ///< outputs with a dimension of <= 4 (and <= 16 with a short k): the dot / rows
                     ///< kernels instead of MFMA tiles (0 = off)
     int clock = 0; ///< LDS-DMA kernel clock meter (gemm_clock_meter, kernels_gemm.hip; 0 = off)
+    int dot_wgs = 256; ///< gemm_dot_kernel (m, n <= 4): split-K to about this many workgroups (1024 / 2048:
+                       ///< no faster, m = n = 4 slower; profiles/r06_gemm_dot_wgs.txt)
     int frag = 1;  ///< small outputs (m, n <= 32) and tall-skinny products on gemm_frag_kernel (MFMA
                    ///< fragments straight from global memory); 2 also for m, n <= 4; 0 = off
 };

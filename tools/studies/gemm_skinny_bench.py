@@ -21,7 +21,10 @@ def main():
     K, batch = 49152, 32
     sizes = [int(v) for v in os.environ.get("SIZES", "1,2,4,8,12,16,32,64").split(",")]
     frags = [int(v) for v in os.environ.get("FRAGS", "1,0").split(",")]
-    for kind in ("inner", "update"):
+    # DOTS: gemm.dot_wgs values (m, n <= 4); KINDS: inner,update
+    dots = [int(v) for v in os.environ.get("DOTS", str(sb.tune_get("gemm.dot_wgs"))).split(",")]
+    kinds = os.environ.get("KINDS", "inner,update").split(",")
+    for kind in kinds:
         for s in sizes:
             m, n, k = (s, s, K) if kind == "inner" else (K, s, s)
             ta, tb = ("C", "N") if kind == "inner" else ("N", "N")
@@ -29,8 +32,9 @@ def main():
             a = torch.randn(batch * m * k, dtype=torch.complex128, device=dev)
             b = torch.randn(batch * k * n, dtype=torch.complex128, device=dev)
             c = torch.zeros(batch * m * n, dtype=torch.complex128, device=dev)
-            for frag in frags:
+            for frag, dot in [(f, d) for f in frags for d in dots]:
                 sb.tune_set("gemm.frag", frag)
+                sb.tune_set("gemm.dot_wgs", dot)
 
                 def f():
                     sb.xgemm_batch_strided(ta, tb, m, n, k, 1.0, a, lda, m * k, b, k, k * n, 0.0,
@@ -51,7 +55,7 @@ def main():
                 t = statistics.median(ts)
                 flops = 8.0 * m * n * k * batch
                 byts = 16.0 * batch * (m * k + k * n + m * n)
-                print(json.dumps({"kind": kind, "m": m, "n": n, "k": k, "batch": batch, "frag": frag,
+                print(json.dumps({"kind": kind, "m": m, "n": n, "k": k, "batch": batch, "frag": frag, "dot_wgs": dot,
                                   "us": round(t * 1e6, 1), "TFLOPs": round(flops / t / 1e12, 3),
                                   "TBps": round(byts / t / 1e12, 3)}), flush=True)
             del a, b, c
