@@ -4,6 +4,7 @@
 // mirrors host (CPU-context) components through device scratch so that every data movement
 // and every flop runs on the GPU, and turns C++ exceptions into status codes.
 #include "plan.h"
+#include <atomic>
 #include <algorithm>
 #include <functional>
 #include <memory>
@@ -56,7 +57,7 @@ using namespace sbx;
 namespace {
 
 /// Device of the last host-context detail call (tune key "detail.last_device", for the tests)
-int g_detail_last_device = -1;
+std::atomic<int> g_detail_last_device{-1};
 
 /// The calling thread's current device.  A detail call whose operands are all host memory runs
 /// there (the reference runs such calls on the CPU of the calling rank, platform.h:757-816; here
@@ -67,7 +68,6 @@ int current_device() {
     if (hipGetDevice(&d) != hipSuccess || d < 0) d = 0;
     return d;
 }
-
 
 thread_local std::string g_last_error;
 
@@ -1248,7 +1248,10 @@ int single_device(std::initializer_list<sbx_context> ctxs, const char *what) {
             throw Error(std::string(what) + ": operands on different devices are not supported");
         dev = c.device;
     }
-    if (dev < 0) g_detail_last_device = dev = current_device();
+    if (dev < 0) {
+        dev = current_device();
+        g_detail_last_device = dev;
+    }
     return dev;
 }
 
@@ -1400,7 +1403,8 @@ int sbx_xgemm_batch_strided_ctx(int t, char transa, char transb, int m, int n, i
     const void *da = nullptr, *db = nullptr;
     void *dc = nullptr;
     long span_c = 0;
-    const int dev = g_detail_last_device = current_device();
+    const int dev = current_device();
+    g_detail_last_device = dev;
     const int rc = guard([&] {
         const std::size_t es = dtype_size(t);
         const bool na = transa == 'n' || transa == 'N', nb = transb == 'n' || transb == 'N';

@@ -1463,9 +1463,11 @@ void launch_tiled_cfg(const GemmKArgs &p0, int device, hipStream_t stream, long 
 /// "gemm.clock_launches" -- the clock the GEMMs ran at, so that a slower box can be told apart
 /// from a slower kernel (one thread's three atomics per launch)
 static unsigned long long *g_clock_meter[64];
+static std::mutex g_clock_mu;
 
 unsigned long long *gemm_clock_meter(int device) {
     if (g_gemm_tune.clock <= 0 || device < 0 || device >= 64) return nullptr;
+    std::lock_guard<std::mutex> lock(g_clock_mu);
     if (!g_clock_meter[device]) {
         void *ptr = nullptr;
         SBX_HIP_CHECK(hipMalloc(&ptr, 3 * sizeof(unsigned long long)));
@@ -1477,6 +1479,7 @@ unsigned long long *gemm_clock_meter(int device) {
 
 void clock_read_impl(int device, unsigned long long out[3], bool reset) {
     out[0] = out[1] = out[2] = 0;
+    std::lock_guard<std::mutex> lock(g_clock_mu);
     if (device < 0 || device >= 64 || !g_clock_meter[device]) return;
     SBX_HIP_CHECK(hipDeviceSynchronize());
     SBX_HIP_CHECK(hipMemcpy(out, g_clock_meter[device], 3 * sizeof(unsigned long long),
