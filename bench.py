@@ -301,7 +301,7 @@ def main():
     ap.add_argument("--no-side", action="store_true", help="skip the side measurements")
     ap.add_argument("--skip", default="",
                     help="comma-separated side measurements to skip (permute, bsr, chain, 3m, "
-                         "chain_dist, redistribution)")
+                         "chain_dist, redistribution, dense, skinny)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--no-1gpu", action="store_true",
                     help="N > 1: skip the same global problem on rank 0's GPU alone")
@@ -400,7 +400,8 @@ def main():
     side = {}
     skip = set(x for x in args.skip.split(",") if x)
     if args.no_side:
-        skip |= {"permute", "bsr", "wilson", "chain", "3m", "chain_dist", "redistribution", "dense"}
+        skip |= {"permute", "bsr", "wilson", "chain", "3m", "chain_dist", "redistribution", "dense",
+                 "skinny"}
     if world == 1 and "permute" not in skip:
         side.update(permute_bench(sb, dev, 16, 64))
     if world == 1 and "bsr" not in skip:
@@ -415,6 +416,11 @@ def main():
             side.update(dense_bench(sb, dev))
         except Exception as e:  # a side measurement never takes the bench down
             side["dense_error"] = str(e)[:200]
+    if world == 1 and "skinny" not in skip:
+        try:
+            side.update(skinny_gemm_bench(sb, dev))
+        except Exception as e:  # a side measurement never takes the bench down
+            side["skinny_error"] = str(e)[:200]
     if world == 1 and "chain" not in skip:
         try:
             side.update(chain_bench(sb, dev))
@@ -1249,6 +1255,48 @@ def dense_bench(sb, dev, L=16, n=12, reps=5):
                                "matrix, DPP row broadcasts, in place); Cholesky: potrf_wave_kernel "
                                "(64 / n matrices per wave)")
     out["dense_workload"] = "16^4 matrices of 12x12 complex<double> (one per site), tij, rows i"
+    return out
+
+
+def skinny_gemm_bench(sb, dev, reps=10):
+    """The reference's own xgemm_batch_strided sweep shapes (tests/dist.cpp test_gemm, at its
+    default lattice: k = 49152 local sites x colors, batch 32, complex<double>): the Krylov inner
+    product m = n = 12 ('C', 'N') and the update m = 49152, n = k = 12 ('N', 'N'), on
+    gemm_frag_kernel; kernel time (GEMM + split-K reduce) from the library's timers, bytes = the
+    operands and the output once."""
+    out = {}
+    K, batch, s = 49152, 32, 12
+    for kind, (m, n, k, ta) in (("inner", (s, s, K, "C")), ("update", (K, s, s, "N"))):
+        g = torch.Generator(device=dev).manual_seed(11)
+        a = torch.randn(batch * m * k, dtype=torch.complex128, device=dev, generator=g)
+        b = torch.randn(batch * k * n, dtype=torch.complex128, device=dev, generator=g)
+        c = torch.zeros(batch * m * n, dtype=torch.complex128, device=dev)
+        lda = k if ta != "N" else m
+
+        def f():
+            sb.xgemm_batch_strided(ta, "N", m, n, k, 1.0, a, lda, m * k, b, k, k * n, 0.0, c, m,
+                                   m * n, batch)
+        for _ in range(3):
+            f()
+        torch.cuda.synchronize()
+        sb.timings_enable(True)
+        sb.timings_filter("gemm_total")
+        sb.timings_reset()
+        for _ in range(reps):
+            f()
+        torch.cuda.synchronize()
+        ms, calls = sb.timings_get("gemm_total")
+        sb.timings_enable(False)
+        sb.timings_filter(None)
+        t = ms / max(calls, 1) / 1e3
+        by = 16.0 * batch * (m * k + k * n + m * n)
+        out.update({"gemm_%s12_us" % kind: round(t * 1e6, 1),
+                    "gemm_%s12_TFLOPs" % kind: round(8.0 * m * n * k * batch / t / 1e12, 2),
+                    "gemm_%s12_frac_hbm" % kind: round(by / t / 8e12, 3)})
+        del a, b, c
+    out["gemm_skinny_workload"] = ("tests/dist.cpp xgemm_batch_strided shapes, complex<double>, "
+                                   "batch 32: inner product m = n = 12, k = 49152 (C,N); update "
+                                   "m = 49152, n = k = 12 (N,N); gemm_frag_kernel")
     return out
 
 

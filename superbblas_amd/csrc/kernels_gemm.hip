@@ -1776,17 +1776,28 @@ template <typename R, bool CPLX> bool launch_frag(const GemmKArgs &p0, int devic
     if (!small && !tall) return false;
     if (g_gemm_tune.skinny && p0.m <= 4 && p0.n <= 4 && g_gemm_tune.frag < 2) return false;
     typedef typename Elem<R, CPLX>::type E;
-    constexpr int UK = 4;
+    // k-steps per load group: 2 for a k of 8 or less and for small outputs, else 4 (0 = this
+    // rule; profiles/r06_gemm_frag_cfg.txt: inner products m = n = 16 229 -> 204 us, the update
+    // n = k = 8 150 -> 113 us with 2; n = k = 16 208 -> 226 us, so 4 there)
+    const int auto_uk = p0.k <= 8 || (p0.m <= 32 && p0.n <= 32) ? 2 : 4;
+    const int uk = g_gemm_tune.frag_uk == 0 ? auto_uk : g_gemm_tune.frag_uk == 8 ? 8
+                 : g_gemm_tune.frag_uk == 2 ? 2 : 4;
     GemmKArgs p = p0;
     Scratch work;
-    // ~4096 waves: split-K when the tiles alone are fewer
-    const long items = prepare_launch<E>(p, 16, 16, 4 * UK, 0, 4096, work, device);
+    // ~gemm.frag_waves waves: split-K when the tiles alone are fewer
+    const long items = prepare_launch<E>(p, 16, 16, 4 * uk, 0, std::max(64, g_gemm_tune.frag_waves),
+                                         work, device);
     const long blocks = (items + 3) / 4;
     if (blocks > 0x7fffffffL) return false;
     KernelTimer total("gemm_total", s);
     {
         KernelTimer timer("gemm", s);
-        hipLaunchKernelGGL((gemm_frag_kernel<R, CPLX, UK>), dim3((unsigned)blocks), dim3(256), 0, s, p);
+        if (uk == 8)
+            hipLaunchKernelGGL((gemm_frag_kernel<R, CPLX, 8>), dim3((unsigned)blocks), dim3(256), 0, s, p);
+        else if (uk == 2)
+            hipLaunchKernelGGL((gemm_frag_kernel<R, CPLX, 2>), dim3((unsigned)blocks), dim3(256), 0, s, p);
+        else
+            hipLaunchKernelGGL((gemm_frag_kernel<R, CPLX, 4>), dim3((unsigned)blocks), dim3(256), 0, s, p);
         SBX_HIP_CHECK(hipGetLastError());
     }
     launch_reduce<R, CPLX>(p, s);

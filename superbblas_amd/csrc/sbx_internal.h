@@ -255,6 +255,8 @@ struct GemmTune {
     int clock = 0; ///< LDS-DMA kernel clock meter (gemm_clock_meter, kernels_gemm.hip; 0 = off)
     int dot_wgs = 256; ///< gemm_dot_kernel (m, n <= 4): split-K to about this many workgroups (1024 / 2048:
                        ///< no faster, m = n = 4 slower; profiles/r06_gemm_dot_wgs.txt)
+    int frag_uk = 0;      ///< ... gemm_frag_kernel: k-steps of 4 per load group (2, 4 or 8; 0 = by shape)
+    int frag_waves = 4096; ///< ... split-K to about this many waves
     int frag = 1;  ///< small outputs (m, n <= 32) and tall-skinny products on gemm_frag_kernel (MFMA
                    ///< fragments straight from global memory); 2 also for m, n <= 4; 0 = off
 };

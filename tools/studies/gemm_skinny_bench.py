@@ -24,6 +24,9 @@ def main():
     # DOTS: gemm.dot_wgs values (m, n <= 4); KINDS: inner,update
     dots = [int(v) for v in os.environ.get("DOTS", str(sb.tune_get("gemm.dot_wgs"))).split(",")]
     kinds = os.environ.get("KINDS", "inner,update").split(",")
+    # FRAGCFG: "uk:waves" pairs for gemm_frag_kernel
+    cfgs = [tuple(int(u) for u in v.split(":")) for v in os.environ.get(
+        "FRAGCFG", "%d:%d" % (sb.tune_get("gemm.frag_uk"), sb.tune_get("gemm.frag_waves"))).split(",")]
     for kind in kinds:
         for s in sizes:
             m, n, k = (s, s, K) if kind == "inner" else (K, s, s)
@@ -32,9 +35,11 @@ def main():
             a = torch.randn(batch * m * k, dtype=torch.complex128, device=dev)
             b = torch.randn(batch * k * n, dtype=torch.complex128, device=dev)
             c = torch.zeros(batch * m * n, dtype=torch.complex128, device=dev)
-            for frag, dot in [(f, d) for f in frags for d in dots]:
+            for frag, dot, cfg in [(f, d, c) for f in frags for d in dots for c in cfgs]:
                 sb.tune_set("gemm.frag", frag)
                 sb.tune_set("gemm.dot_wgs", dot)
+                sb.tune_set("gemm.frag_uk", cfg[0])
+                sb.tune_set("gemm.frag_waves", cfg[1])
 
                 def f():
                     sb.xgemm_batch_strided(ta, tb, m, n, k, 1.0, a, lda, m * k, b, k, k * n, 0.0,
@@ -55,11 +60,13 @@ def main():
                 t = statistics.median(ts)
                 flops = 8.0 * m * n * k * batch
                 byts = 16.0 * batch * (m * k + k * n + m * n)
-                print(json.dumps({"kind": kind, "m": m, "n": n, "k": k, "batch": batch, "frag": frag, "dot_wgs": dot,
+                print(json.dumps({"kind": kind, "m": m, "n": n, "k": k, "batch": batch, "frag": frag, "dot_wgs": dot, "uk_waves": "%d:%d" % cfg,
                                   "us": round(t * 1e6, 1), "TFLOPs": round(flops / t / 1e12, 3),
                                   "TBps": round(byts / t / 1e12, 3)}), flush=True)
             del a, b, c
     sb.tune_set("gemm.frag", 1)
+    sb.tune_set("gemm.frag_uk", 0)
+    sb.tune_set("gemm.frag_waves", 4096)
 
 
 if __name__ == "__main__":
