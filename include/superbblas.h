@@ -28,6 +28,7 @@
 #include <cmath>
 #include <complex>
 #include <cstddef>
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -819,6 +820,32 @@ enum checksum_type { NoChecksum = 0, GlobalChecksum = 1, BlockChecksum = 2 };
 
 /// Handle to a tensor storage (storage.h:2127)
 using Storage_handle = sbx_storage;
+
+namespace detail {
+/// The values type of a scalar type (storage.h:80-90)
+template <typename T> values_datatype get_values_datatype();
+template <> inline values_datatype get_values_datatype<float>() { return FLOAT; }
+template <> inline values_datatype get_values_datatype<double>() { return DOUBLE; }
+template <> inline values_datatype get_values_datatype<std::complex<float>>() { return CFLOAT; }
+template <> inline values_datatype get_values_datatype<std::complex<double>>() { return CDOUBLE; }
+template <> inline values_datatype get_values_datatype<int>() { return INT; }
+template <> inline values_datatype get_values_datatype<char>() { return CHAR; }
+
+/// Checksum value type and default block size (storage.h:689-693)
+using checksum_t = std::uint32_t;
+const std::size_t default_checksum_blocksize = 64 * 1024 * 1024; // 64 MiB
+
+/// do_checksum (storage.h:701-731): CRC-32 of size elements of str continuing from
+/// prev_checksum, or with checksum_blocksize > 0 the CRC of the CRCs of blocks of that many bytes
+template <typename T>
+checksum_t do_checksum(const T *str, std::size_t size = 1, std::size_t checksum_blocksize = 0,
+                       checksum_t prev_checksum = 0) {
+    unsigned out = 0;
+    sbx_detail::check(sbx_checksum((const void *)str, (unsigned long long)(size * sizeof(T)),
+                                   (unsigned long long)checksum_blocksize, prev_checksum, &out));
+    return out;
+}
+} // namespace detail
 
 namespace sbx_detail {
 /// get_storage_context (storage.h:1630-1645): the template parameters must match the file

@@ -386,6 +386,11 @@ int sbx_memset_zero(void *ptr, sbx_context ctx, unsigned long long bytes);
 int sbx_copy_n_blocking(const double *alpha, int tv, const void *v, sbx_context vctx,
                         long long blocking, const int *iv, sbx_context ivctx, long long n, int tw,
                         void *w, sbx_context wctx, const int *iw, sbx_context iwctx, int copyadd);
+/* do_checksum (storage.h:701-731): the S3T format's CRC-32 (zlib polynomial) of `bytes` host
+   bytes continuing from `prev`, or with blocksize > 0 the CRC of the CRCs of blocksize-byte
+   chunks (prev must then be 0); host memory, computed on the host like the reference's */
+int sbx_checksum(const void *p, unsigned long long bytes, unsigned long long blocksize,
+                 unsigned prev, unsigned *out);
 /* intersection(from0, size0, from1, size1, dim) of two periodic ranges (dist.h:461-486): up to
    maxout pieces of 2*nd ints {from, size}, first dimension fastest; *nout is the count */
 int sbx_intersection(int nd, const int *from0, const int *size0, const int *from1,

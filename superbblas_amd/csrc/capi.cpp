@@ -1380,6 +1380,14 @@ int sbx_copy_n_blocking(const double *alpha, int tv, const void *v, sbx_context 
     });
 }
 
+int sbx_checksum(const void *p, unsigned long long bytes, unsigned long long blocksize,
+                 unsigned prev, unsigned *out) {
+    return guard([&] {
+        if (!out || (!p && bytes > 0)) throw Error("do_checksum: null argument");
+        *out = storage_checksum(p, bytes, blocksize, prev);
+    });
+}
+
 int sbx_intersection(int nd, const int *from0, const int *size0, const int *from1,
                      const int *size1, const int *dim, int maxout, int *out, int *nout) {
     return guard([&] {

@@ -260,6 +260,9 @@ struct GemmTune {
     int frag = 1;  ///< small outputs (m, n <= 32) and tall-skinny products on gemm_frag_kernel (MFMA
                    ///< fragments straight from global memory); 2 also for m, n <= 4; 0 = off
 };
+/// The S3T checksum (storage.cpp; storage.h:701-731): CRC-32 (zlib polynomial) of the bytes, or
+/// with blocksize > 0 the CRC of the CRCs of blocksize chunks (prev must then be 0)
+uint32_t storage_checksum(const void *p, std::size_t bytes, std::size_t blocksize, uint32_t prev);
 /// The LDS-DMA GEMM's clock meter of a device: {shader clock cycles, 100 MHz ticks, launches}
 /// summed since the last reset (zeros when the meter was never enabled)
 void gemm_clock_read(int device, unsigned long long out[3], bool reset);

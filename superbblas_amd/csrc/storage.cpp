@@ -137,6 +137,11 @@ std::size_t scalar_width(int dtype) {
 
 } // namespace
 
+/// the checksum of the S3T format (storage.h:701-731) for detail::do_checksum (sbx_checksum)
+uint32_t storage_checksum(const void *p, std::size_t bytes, std::size_t blocksize, uint32_t prev) {
+    return do_checksum(p, bytes, blocksize, prev);
+}
+
 struct StorageCtx {
     int fd = -1;
     int dtype = SBX_CDOUBLE; // element type of the values

@@ -1,12 +1,13 @@
 """The reference's own test programs as callers of the drop-in build (shared by the golden
 generator and the tests).
 
-tests/refcallers/Makefile compiles superbblas's tests/bsr.cpp, contract.cpp, dist.cpp, blas.cpp
-and dense.cpp, unchanged and from where they lie under /root/reference, against
+tests/refcallers/Makefile compiles superbblas's tests/bsr.cpp, contract.cpp, dist.cpp, blas.cpp,
+dense.cpp and storage.cpp, unchanged and from where they lie under /root/reference, against
 include/superbblas.h and libsuperbblas_amd.so.  oracle/Makefile (`refcallers`) builds the same
 sources against the reference's own headers (CPU, OpenBLAS).  The checks the programs carry
 (bsr.cpp:287-352 exact product values at SB_DEBUG=1, contract.cpp:238-271 against a brute-force
-contraction, blas.cpp:47-63 copy_n against host loops) print "Caught error: ..." or abort; so
+contraction, blas.cpp:47-63 copy_n against host loops, storage.cpp:280-351 every value read back
+from the file and its metadata, dimensions and type) print "Caught error: ..." or abort; so
 what a run prints, with the timings blanked, is compared against what the reference prints for
 the same invocation (tests/golden/refcallers.json, tests/golden/make_refcallers_golden.py).
 """
@@ -23,6 +24,7 @@ INVOCATIONS = [
     ("dense", ["--dim=2 2 2 2 2 3"], {"SB_DEBUG": "1"}),
     ("dist", ["--dim=8 8 8 8 8", "--reps=2"], {}),
     ("blas", ["--size=1000", "--rep=2"], {}),
+    ("storage", [], {}),
 ] + [("contract", ["--test=%d" % t], {}) for t in
      # spread over both scalar types: 0..663551 real double, 663552.. complex<double>
      (0, 1, 2, 3, 17, 255, 4567, 12345, 55295, 89012, 200001, 345678, 500000, 663551,

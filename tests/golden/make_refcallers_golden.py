@@ -10,6 +10,7 @@ import json
 import os
 import subprocess
 import sys
+import tempfile
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
@@ -23,7 +24,10 @@ def main():
     for name, args, env in INVOCATIONS:
         exe = os.path.join(ROOT, "oracle", "_ref", "contract" if name == "contract" else "test_" + name)
         e = dict(os.environ, OMP_NUM_THREADS="4", **env)
-        r = subprocess.run([exe] + args, capture_output=True, text=True, env=e, timeout=600)
+        # (storage.cpp writes tensor.s3t into its working directory)
+        with tempfile.TemporaryDirectory() as wd:
+            r = subprocess.run([exe] + args, capture_output=True, text=True, env=e, timeout=600,
+                               cwd=wd)
         if r.returncode != 0:
             raise SystemExit("reference %s %s failed: rc %d\n%s" % (name, args, r.returncode, r.stderr))
         out[key(name, args, env)] = events(name, r.stdout)

@@ -51,3 +51,36 @@ def test_copy_plan_single_process():
     send, recv, local = sb.copy_plan(p, "xyz", [1, 2, 3], [3, 4, 5], dim, 1, q, "zxy", [0, 0, 0],
                                      [5, 4, 6], 1, 1, 0)
     assert send == [0] and recv == [0] and local == 3 * 4 * 5
+
+
+def test_checksum_matches_zlib_crc32():
+    """sbx_checksum (detail::do_checksum, storage.h:701-731) is the zlib CRC-32, continued from a
+    previous value, and with a block size the CRC of the blocks' CRCs (host-only: no GPU call)"""
+    import struct
+    import zlib
+    import superbblas_amd as sb
+    lib = ctypes.CDLL(sb.LIB_PATH)
+    data = b"Quixote was a great guy" * 37
+    out = ctypes.c_uint(0)
+
+    def cs(buf, bs=0, prev=0):
+        rc = lib.sbx_checksum(buf, ctypes.c_ulonglong(len(buf)), ctypes.c_ulonglong(bs),
+                              ctypes.c_uint(prev), ctypes.byref(out))
+        assert rc == 0
+        return out.value
+    assert cs(data) == zlib.crc32(data)
+    assert cs(data[10:], prev=zlib.crc32(data[:10])) == zlib.crc32(data)
+    blocks = [data[i:i + 64] for i in range(0, len(data), 64)]
+    want = zlib.crc32(b"".join(struct.pack("<I", zlib.crc32(b)) for b in blocks))
+    assert cs(data, bs=64) == want
+
+
+def test_library_has_no_undefined_internal_symbols():
+    """every sbx:: function the library calls is defined in it (a shared library links with
+    undefined symbols; a missing definition would only fail at load time on the GPU box)"""
+    import subprocess
+    import superbblas_amd as sb
+    r = subprocess.run(["nm", "-C", "-u", sb.LIB_PATH], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    bad = [l for l in r.stdout.splitlines() if "sbx::" in l or " sbx_" in l]
+    assert not bad, bad

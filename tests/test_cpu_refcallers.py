@@ -1,6 +1,6 @@
 """The reference's own test programs compile unchanged against the drop-in header
 (include/superbblas.h with its superbblas::detail surface): superbblas's tests/bsr.cpp,
-contract.cpp, dist.cpp, blas.cpp and dense.cpp, syntax-checked with plain g++ from where they
+contract.cpp, dist.cpp, blas.cpp, dense.cpp and storage.cpp, syntax-checked with plain g++ from where they
 lie under /root/reference (skipped where the reference is absent, e.g. on the GPU box)."""
 import os
 import subprocess
@@ -12,7 +12,7 @@ REF = "/root/reference/tests"
 
 
 @pytest.mark.skipif(not os.path.isdir(REF), reason="the reference is not present here")
-@pytest.mark.parametrize("name", ["bsr", "contract", "dist", "blas", "dense"])
+@pytest.mark.parametrize("name", ["bsr", "contract", "dist", "blas", "dense", "storage"])
 @pytest.mark.parametrize("std", ["-std=c++14", "-std=c++17"])
 def test_reference_caller_compiles(name, std):
     r = subprocess.run(["g++", std, "-fsyntax-only", "-fopenmp", "-I", os.path.join(ROOT, "include"),

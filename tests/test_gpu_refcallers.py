@@ -25,13 +25,13 @@ BIN = os.path.join(HERE, "refcallers", "bin")
 GOLDEN = json.load(open(os.path.join(HERE, "golden", "refcallers.json")))
 
 
-def _run(name, args, env):
+def _run(name, args, env, cwd=None):
     exe = os.path.join(BIN, name)
     if not os.path.exists(exe):
         pytest.fail("%s missing: build it where /root/reference exists (make -C tests/refcallers)" % exe)
     e = dict(os.environ, OMP_NUM_THREADS="8", **env)
     e.pop("SB_TRACK_TIME", None)
-    r = subprocess.run([exe] + args, capture_output=True, text=True, env=e, timeout=240)
+    r = subprocess.run([exe] + args, capture_output=True, text=True, env=e, timeout=240, cwd=cwd)
     assert r.returncode == 0, (name, args, r.returncode, r.stdout[-3000:], r.stderr[-3000:])
     assert "libsuperbblas_amd" not in r.stderr, r.stderr[-2000:]
     return r.stdout
@@ -123,3 +123,21 @@ def test_contract_strided_sample(gpu):
         bad = [(t, msg) for t, ok, msg in pool.map(one, cases) if not ok]
     assert not bad, bad[:3]
     assert len(cases) == 629
+
+
+def test_storage_program(gpu, tmp_path):
+    """storage.cpp (the S3T tensor storage): create / append / read / check with no,
+    per-block and global checksums, float and complex<double>, CPU contexts (mirrored through the
+    GPU), then its GPU section (complex<double>, block checksums); every value read back is checked
+    by the program (storage.cpp:280-351), as are the metadata, dimensions and type it recovers,
+    and its checksum associativity test (do_checksum, storage.h:701-731).  The CPU sections print
+    the reference's events, the GPU section those of the reference's block-checksum run."""
+    inv = [i for i in INVOCATIONS if i[0] == "storage"][0]
+    ref = _sections([tuple(x) for x in GOLDEN[key(*inv)]])
+    got = _sections(events(inv[0], _run(*inv, cwd=str(tmp_path))))
+    kinds = [k for k, _ in got]
+    assert kinds == [k for k, _ in ref] + [">>> test for complex double"], kinds
+    for (_, g), (_, r) in zip(got, ref):
+        assert g == r
+    # the GPU section: one block-checksum test (the reference's six events of that mode)
+    assert got[-1][1] == ref[-1][1][6:12]
