@@ -242,6 +242,11 @@ template <> struct dtype<std::complex<float>> { static constexpr int value = SBX
 template <> struct dtype<std::complex<double>> { static constexpr int value = SBX_CDOUBLE; };
 template <> struct dtype<int> { static constexpr int value = SBX_INT; };
 template <> struct dtype<std::size_t> { static constexpr int value = SBX_SIZE_T; };
+/// char has no values type in the C ABI (the reference's own char save / load do not compile,
+/// tensor.h:1091, no multiplication_cost<char>): -1 fails every library call on char tensors
+/// loudly, while programs that only name the type (tests/storage_details.cpp's type switch over a
+/// file's values_datatype) compile
+template <> struct dtype<char> { static constexpr int value = -1; };
 
 template <typename T> inline std::array<double, 2> scalar(const T &v) { return {{(double)v, 0.0}}; }
 template <typename T> inline std::array<double, 2> scalar(const std::complex<T> &v) {

@@ -58,3 +58,14 @@ def events(name, out):
             s = s.split("(")[0].strip()  # type and operation; the throughputs follow
         ev.append((section, NUM.sub("#", s)))
     return ev
+
+
+# storage_details.cpp (the S3T inspection tool) on the golden storage files (tests/golden/*.s3t,
+# written by the reference): name, arguments after the file
+STORAGE_DETAILS = [("show", "--list-blocks"), ("show", "--only-metadata")]
+STORAGE_FILES = ["sto_block.s3t", "sto_block_cf.s3t", "sto_f2s.s3t", "sto_general.s3t",
+                 "sto_global.s3t", "sto_plain.s3t"]
+
+
+def details_key(fname, args):
+    return " ".join(["storage_details", fname] + list(args))

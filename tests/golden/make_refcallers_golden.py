@@ -15,7 +15,8 @@ import tempfile
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, os.path.dirname(HERE))
-from _refcallers import INVOCATIONS, events, key  # noqa: E402
+from _refcallers import (INVOCATIONS, STORAGE_DETAILS, STORAGE_FILES, details_key,  # noqa: E402
+                         events, key)
 
 
 def main():
@@ -32,6 +33,17 @@ def main():
             raise SystemExit("reference %s %s failed: rc %d\n%s" % (name, args, r.returncode, r.stderr))
         out[key(name, args, env)] = events(name, r.stdout)
         print(key(name, args, env), len(out[key(name, args, env)]), "events")
+    # storage_details.cpp on the golden storage files: its whole output
+    exe = os.path.join(ROOT, "oracle", "_ref", "test_storage_details")
+    for fname in STORAGE_FILES:
+        for args in STORAGE_DETAILS:
+            r = subprocess.run([exe, os.path.join(HERE, fname)] + list(args), capture_output=True,
+                               text=True, timeout=120)
+            if r.returncode != 0:
+                raise SystemExit("reference storage_details %s %s failed: rc %d\n%s"
+                                 % (fname, args, r.returncode, r.stderr))
+            out[details_key(fname, args)] = r.stdout
+            print(details_key(fname, args), len(r.stdout.splitlines()), "lines")
     with open(os.path.join(HERE, "refcallers.json"), "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
 

@@ -16,7 +16,7 @@ import subprocess
 
 import pytest
 
-from _refcallers import INVOCATIONS, events, key
+from _refcallers import INVOCATIONS, STORAGE_DETAILS, STORAGE_FILES, details_key, events, key
 
 pytestmark = pytest.mark.gpu
 
@@ -141,3 +141,26 @@ def test_storage_program(gpu, tmp_path):
         assert g == r
     # the GPU section: one block-checksum test (the reference's six events of that mode)
     assert got[-1][1] == ref[-1][1][6:12]
+
+
+@pytest.mark.parametrize("fname", STORAGE_FILES)
+@pytest.mark.parametrize("args", STORAGE_DETAILS, ids=lambda a: a[1])
+def test_storage_details_program(gpu, fname, args):
+    """storage_details.cpp (the reference's S3T inspection tool: read_storage_header, open_storage,
+    check_storage, get_blocks) on the golden storage files the reference wrote: the same output as
+    the reference's own build -- except the order of the listed blocks, which the reference takes
+    from its block hash and this library from the append order (DESIGN, storage notes)"""
+    exe = os.path.join(BIN, "storage_details")
+    if not os.path.exists(exe):
+        pytest.fail("%s missing: build it where /root/reference exists (make -C tests/refcallers)" % exe)
+    r = subprocess.run([exe, os.path.join(HERE, "golden", fname)] + list(args), capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
+    ref = GOLDEN[details_key(fname, args)]
+    if "--list-blocks" in args:
+        head_got, _, blocks_got = r.stdout.partition("blocks:\n")
+        head_ref, _, blocks_ref = ref.partition("blocks:\n")
+        assert head_got == head_ref
+        assert sorted(blocks_got.splitlines()) == sorted(blocks_ref.splitlines())
+    else:
+        assert r.stdout == ref
