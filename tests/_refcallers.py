@@ -2,7 +2,7 @@
 generator and the tests).
 
 tests/refcallers/Makefile compiles superbblas's tests/bsr.cpp, contract.cpp, dist.cpp, blas.cpp,
-dense.cpp and storage.cpp, unchanged and from where they lie under /root/reference, against
+dense.cpp, storage.cpp and storage_details.cpp, unchanged and from where they lie under /root/reference, against
 include/superbblas.h and libsuperbblas_amd.so.  oracle/Makefile (`refcallers`) builds the same
 sources against the reference's own headers (CPU, OpenBLAS).  The checks the programs carry
 (bsr.cpp:287-352 exact product values at SB_DEBUG=1, contract.cpp:238-271 against a brute-force
