@@ -428,7 +428,6 @@ int sbx_tune_set(const char *key, long long value) {
         else if (k == "copy.btrans") g_copy_tune.btrans = (int)value;
         else if (k == "gemm.max_bytes") g_gemm_tune.max_bytes = (long)value;
         else if (k == "gemm.loaders") g_gemm_tune.loaders = (int)value;
-        else if (k == "gemm.pf") g_gemm_tune.pf = (int)value;
         else if (k == "gemm.dma_spread") g_gemm_tune.dma_spread = (int)value;
         else if (k == "gemm.dma_nt") g_gemm_tune.dma_nt = (int)value;
         else if (k == "gemm.skinny") g_gemm_tune.skinny = (int)value;
@@ -495,7 +494,6 @@ int sbx_tune_get(const char *key, long long *value) {
         else if (k == "copy.last_pair") *value = g_copy_tune.last_pair;
         else if (k == "gemm.max_bytes") *value = g_gemm_tune.max_bytes;
         else if (k == "gemm.loaders") *value = g_gemm_tune.loaders;
-        else if (k == "gemm.pf") *value = g_gemm_tune.pf;
         else if (k == "gemm.dma_spread") *value = g_gemm_tune.dma_spread;
         else if (k == "gemm.dma_nt") *value = g_gemm_tune.dma_nt;
         else if (k == "gemm.skinny") *value = g_gemm_tune.skinny;

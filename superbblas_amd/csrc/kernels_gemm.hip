@@ -493,7 +493,7 @@ __global__ void __launch_bounds__(WM *WN *KG * 64) gemm_dma_kernel(const GemmKAr
     static_assert(MT * 16 == WTM && NT * 16 == WTN, "bad wave tile");
     typedef DmaOperand<AK, BM, BKK, NTH, ES> OpA;
     typedef DmaOperand<BK, BN, BKK, NTH, ES> OpB;
-    static_assert(LW == 0 || (AK && BK && !SH && KG == 1 && (!PF || SP == 1)), "loader waves: K-major operands");
+    static_assert(LW == 0 || (AK && BK && !SH && KG == 1 && !PF), "loader waves: K-major operands");
     typedef typename std::conditional<(LW > 0), DmaRowsK<BM, BKK, LW * 64, ES>, NoLoader>::type LdA;
     typedef typename std::conditional<(LW > 0), DmaRowsK<BN, BKK, LW * 64, ES>, NoLoader>::type LdB;
     static_assert(LW == 0 || BKK / 4 >= SP, "loader spread: SP k-steps per slab at most");
@@ -705,12 +705,8 @@ __global__ void __launch_bounds__(WM *WN *KG * 64) gemm_dma_kernel(const GemmKAr
             frag(0, af[0], bf[0]);
 #pragma unroll
             for (int kk = 0; kk < BKK; kk += 4) {
-                load_part(kk / 4);
                 const int c = (kk / 4) & 1;
                 if (kk + 4 < BKK) frag(kk + 4, af[c ^ 1], bf[c ^ 1]);
-                // (LW > 0: pin the next k-step's reads above this k-step's MFMAs; the scheduler
-                // otherwise sinks them below, ISA of round 6)
-                if constexpr (LW > 0) __builtin_amdgcn_sched_barrier(0);
                 E *a = af[c], *b = bf[c];
 #pragma unroll
                 for (int i = 0; i < MT; ++i) a[i].y = flip(a[i].y, ma);
@@ -1635,8 +1631,6 @@ void launch_tiled(const GemmKArgs &p, int device, hipStream_t stream) {
                     launch_dma_cfg<R, CPLX, AK, BK, 128, 128, 16, 4, 4, false, false, 1, false, 8, 4>(p, device, stream, 0, 256);
                 else if (lw == 8 && sp == 0)
                     launch_dma_cfg<R, CPLX, AK, BK, 128, 128, 16, 4, 4, false, false, 1, false, 8, 0>(p, device, stream, 0, 256);
-                else if (lw == 8 && g_gemm_tune.pf)
-                    launch_dma_cfg<R, CPLX, AK, BK, 128, 128, 16, 4, 4, false, true, 1, false, 8, 1>(p, device, stream, 0, 256);
                 else if (lw == 8)
                     launch_dma_cfg<R, CPLX, AK, BK, 128, 128, 16, 4, 4, false, false, 1, false, 8, 1>(p, device, stream, 0, 256);
                 else if (lw == 16 && sp == 4)

@@ -246,8 +246,6 @@ struct GemmTune {
     int loaders = 8; ///< complex<double> 128x128 LDS-DMA kernel, K-major operands: only this many waves
                      ///< (4, 8, 16) issue the slab DMA (0 = every wave its share); config 2: 1.491 ->
                      ///< 1.475 ms at 4 or 8 (tools/studies/gemm_loaders.py, profiles/r05_gemm_loaders.txt)
-    int pf = 0; ///< 8 loader waves: each wave reads the next k-step's fragments before the current
-                ///< k-step's MFMAs (a register double buffer)
     int dma_spread = 1; ///< ... the loader waves spread their DMA over this many k-steps (1 or 4); 0 (8
                         ///< loaders): the early barrier -- a slab's barrier before its last k-step,
                         ///< whose fragments are already read, the next slab's first ones read after it

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Config-2 GEMM (16^4, n = 64, complex<double>): who issues the slab DMA (not part of the product;
-sbx_tune_set("gemm.loaders" / "gemm.dma_spread" / "gemm.pf")).  Every wave its share (0), or only waves 0..LW-1
+sbx_tune_set("gemm.loaders" / "gemm.dma_spread")).  Every wave its share (0), or only waves 0..LW-1
 (LW = 4 / 8 / 16) spreading it over SP k-steps.  Variants interleaved over several rounds, warm;
 GEMM kernel time from the library's HIP-event timers; results must be bit-identical."""
 import json
@@ -46,7 +46,6 @@ def main():
             sb.tune_set("gemm.loaders", lw)
             sb.tune_set("gemm.dma_spread", sp)
             sb.tune_set("gemm.dma_nt", var[2] if len(var) > 2 else 0)
-            sb.tune_set("gemm.pf", var[3] if len(var) > 3 else 0)
             step()
             torch.cuda.synchronize()
             sb.timings_enable(True)
@@ -66,11 +65,9 @@ def main():
     sb.tune_set("gemm.loaders", 8)
     sb.tune_set("gemm.dma_spread", 1)
     sb.tune_set("gemm.dma_nt", 0)
-    sb.tune_set("gemm.pf", 0)
     for var, t in times.items():
         t = sorted(t)
         print(json.dumps({"loaders": var[0], "spread": var[1], "nt": var[2] if len(var) > 2 else 0,
-                          "pf": var[3] if len(var) > 3 else 0,
                           "gemm_ms_min": round(t[0], 4),
                           "gemm_ms_median": round(t[len(t) // 2], 4),
                           "TFLOPs_median": round(flops / t[len(t) // 2] / 1e9, 2)}), flush=True)
