@@ -226,6 +226,22 @@ int main(int argc, char **argv) {
         return 0;
     }
     const char *only = getenv("ONLY");
+    if (only && std::string(only) == "w8") {
+        // round 6: 8 waves of 64x32 (2 per SIMD, 0.19 fragment reads per MFMA instead of 0.25)
+        // against the default 16 waves of 32x32, 8 loader waves
+#define DMAL(NAME, WM, WN, LW)                                                                    \
+    run(NAME, [&](const GemmKArgs &q, hipStream_t s) {                                            \
+        launch_dma_cfg<double, true, true, true, 128, 128, 16, WM, WN, false, false, 1, false, LW, 1>(q, 0, s, 0, 256); \
+    }, p, reps, flops, &ref, C, nc)
+        for (int rep = 0; rep < 4; ++rep) {
+            DMAL("w16 4x4 loaders 8 (default)", 4, 4, 8);
+            DMAL("w8 2x4 loaders 4", 2, 4, 4);
+            DMAL("w8 4x2 loaders 4", 4, 2, 4);
+            DMAL("w8 2x4 loaders 8", 2, 4, 8);
+            DMAL("w8 4x2 loaders 8", 4, 2, 8);
+        }
+        return 0;
+    }
     for (int rep = 0; rep < 3; ++rep) {
         if (!only || std::string(only) == "a") DMA(128, 128, 8, 4, 2, 0, 256);
         if (!only || std::string(only) == "b") DMA(128, 128, 16, 4, 2, 0, 256);
