@@ -456,14 +456,31 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    # kernel timer: one HIP event pair around every GEMM launch together with its split-K reduce,
-    # on the library's (= torch's current) stream ("gemm_total"; each event record costs a few us
-    # of stream time, so the timed region carries no other events)
+    # GEMM launches per step (one untimed step with the library's per-launch timers)
     sb.timings_enable(True)
     sb.timings_filter("gemm_total")
     sb.timings_reset()
+    step()
+    torch.cuda.synchronize()
+    calls_per_step = sb.timings_get("gemm_total")[1]
+    sb.timings_enable(False)
+    barrier()
+    torch.cuda.synchronize()
+    # kernel time on the library's (= torch's current) stream by HIP events.  N = 1, where a step
+    # is one GEMM launch and its split-K reduce: one event pair around the K timed steps, so the
+    # average launch duration is the stream time per step (GEMM + reduce + the launch gaps
+    # between them).  Otherwise one event pair around every GEMM launch with its reduce
+    # ("gemm_total"); those two event records per launch cost ~9 us of stream time per step
+    # (marker packets between the kernels), which is why N = 1 does not use them.
+    per_launch = world > 1 or calls_per_step != 1
+    if per_launch:
+        sb.timings_enable(True)
+        sb.timings_filter("gemm_total")
+        sb.timings_reset()
+    else:
+        ev_start = torch.cuda.Event(enable_timing=True)
+        ev_end = torch.cuda.Event(enable_timing=True)
+        ev_start.record()
     # the shader clock the timed GEMMs ran at: workgroup 0 of every LDS-DMA GEMM launch sums its
     # s_memtime (shader clock) and s_memrealtime (100 MHz) spans (three vector atomics by one
     # thread per launch), so a slower box can be told apart from a slower kernel
@@ -472,6 +489,8 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         step()
+    if not per_launch:
+        ev_end.record()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -481,8 +500,11 @@ def main():
                          device="cpu" if args.share_gpu in ("host", "rccl") else dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
-    gemm_ms, gemm_calls = sb.timings_get("gemm_total")
-    sb.timings_enable(False)
+    if per_launch:
+        gemm_ms, gemm_calls = sb.timings_get("gemm_total")
+        sb.timings_enable(False)
+    else:
+        gemm_ms, gemm_calls = ev_start.elapsed_time(ev_end), args.steps
     sb.timings_filter(None)
     clk_cycles, clk_ticks = sb.tune_get("gemm.clock_cycles"), sb.tune_get("gemm.clock_ticks")
     clk_launches = sb.tune_get("gemm.clock_launches")
@@ -602,9 +624,12 @@ def main():
                                  "one GEMM launch"),
                          "kernel": "gemm_dma_kernel<complex<double>, 128x128x%d, %d waves> (FP64 "
                                    "MFMA 16x16x4, complex %s) + split-K reduce, %d launches, %.4f "
-                                   "ms avg (HIP events on its launch stream)" % (
+                                   "ms avg (HIP events on its launch stream, %s)" % (
                                        8 if m3 else 16, 8 if m3 else 16, "3M" if m3 else "4M",
-                                       gemm_calls, kernel_s * 1e3),
+                                       gemm_calls, kernel_s * 1e3,
+                                       "a pair around every launch" if per_launch else
+                                       "one pair around the timed steps: GEMM + reduce + launch "
+                                       "gaps per step"),
                          "flops_per_launch": flops_launch,
                          "executed_flops_per_launch": flops_launch * exec_per_alg,
                          "algorithmic_TFLOPs": round(algorithmic, 3),

@@ -357,7 +357,10 @@ int sbx_clear_caches(void) {
 }
 
 int sbx_clear_handles(void) {
-    return guard([&] { destroy_streams(); });
+    return guard([&] {
+        trim_pools(); // cached scratch may name a library stream as its last user
+        destroy_streams();
+    });
 }
 
 int sbx_allocate(unsigned long long bytes, sbx_context ctx, void **ptr) {

@@ -60,6 +60,15 @@ hipStream_t get_side_stream(int device) {
     return st.side;
 }
 
+/// A stream that lives as long as the library's handles: the null stream and the library's own
+/// streams (sbx_clear_handles releases the scratch cache before destroying them)
+bool durable_stream(int device, hipStream_t s) {
+    if (s == nullptr) return true;
+    std::lock_guard<std::mutex> g(g_mutex);
+    const DeviceState &st = state(device);
+    return s == st.own || s == st.side;
+}
+
 void stream_after(hipStream_t to, hipStream_t from) {
     if (to == from) return;
     hipEvent_t ev;
@@ -112,9 +121,13 @@ void destroy_streams() {
 
 //
 // Scratch memory: a caching allocator over hipMalloc (the reference's allocateBufferResouce
-// cache, alloc.h:323-391).  A freed block goes back to a per-device free list together with an
-// event recorded on the stream that last used it; a later allocation reuses it at once on the
-// same stream (stream order) or after waiting on that event from another stream.  Blocks stay
+// cache, alloc.h:323-391).  A freed block goes back to a per-device free list together with the
+// stream that last used it; a later allocation reuses it at once on the same stream (stream
+// order) or, from another stream, after waiting on that stream.  A block freed on a caller's
+// stream also carries an event recorded at the free (the caller may destroy its stream); one
+// freed on the null stream or a library stream does not: an event record is a marker packet the
+// GPU processes between two kernels (~4 us of stream time per GEMM call that used split-K
+// scratch), and those streams outlive the cache (sbx_clear_handles trims it first).  Blocks stay
 // mapped for the life of the cache: hipMallocAsync's pool was measured to hand back reused
 // memory with stale contents after many queued launches on this platform, so it is not used.
 //
@@ -226,6 +239,8 @@ void release_blocks(const std::vector<Block> &blocks, int device) {
         if (b.ev) {
             (void)hipEventSynchronize(b.ev); // its last use is done
             (void)hipEventDestroy(b.ev);
+        } else {
+            (void)hipStreamSynchronize(b.stream);
         }
         device_free(b.p, device);
     }
@@ -266,6 +281,8 @@ void *scratch_alloc(std::size_t bytes, int device) {
         if (b.ev) {
             if (b.stream != s) SBX_HIP_CHECK(hipStreamWaitEvent(s, b.ev, 0));
             SBX_HIP_CHECK(hipEventDestroy(b.ev));
+        } else if (b.stream != s) {
+            stream_after(s, b.stream); // (a durable stream: the null or a library stream)
         }
         c.live[b.p] = Live{b.bytes, s};
         return b.p;
@@ -364,6 +381,7 @@ void scratch_free(void *p, int device) {
     if (!p) return;
     set_device(device);
     const hipStream_t s = get_stream(device);
+    const bool durable = durable_stream(device, s);
     std::vector<Block> evict;
     {
     std::lock_guard<std::mutex> g(g_cache_mutex);
@@ -378,8 +396,10 @@ void scratch_free(void *p, int device) {
         ++g_cross_stream_frees;
     }
     c.live.erase(it);
-    SBX_HIP_CHECK(hipEventCreateWithFlags(&b.ev, hipEventDisableTiming));
-    SBX_HIP_CHECK(hipEventRecord(b.ev, s));
+    if (!durable) {
+        SBX_HIP_CHECK(hipEventCreateWithFlags(&b.ev, hipEventDisableTiming));
+        SBX_HIP_CHECK(hipEventRecord(b.ev, s));
+    }
     c.free_blocks.emplace(b.bytes, b);
     c.cached_bytes += b.bytes;
     evict = take_over_cap(device);
