@@ -115,3 +115,40 @@ torch.cuda.synchronize()
 assert torch.allclose(c, a @ b.T, rtol=1e-12, atol=1e-12)
 print('OK')
 """, {"SB_DEBUG": "1"})
+
+
+def test_scratch_reuse_across_streams(gpu):
+    """Split-K scratch freed on the null stream (no event recorded: a durable stream) and reused at
+    once from a caller's stream, and the other way round: the second GEMM waits for the first's
+    reduce (results bit-identical to the same GEMMs run one at a time)."""
+    import torch
+    import superbblas_amd as sb
+    m, k, batch = 256, 8192, 16  # split-K over 4 pieces: a 67 MB scratch block per call
+    g = torch.Generator(device=gpu).manual_seed(3)
+    a = [torch.randn(batch * m * k, dtype=torch.complex128, device=gpu, generator=g) for _ in range(2)]
+    b = [torch.randn(batch * k * m, dtype=torch.complex128, device=gpu, generator=g) for _ in range(2)]
+
+    def gemm(i, c):
+        sb.xgemm_batch_strided("T", "N", m, m, k, 1.0, a[i], k, m * k, b[i], k, k * m, 0.0, c, m,
+                               m * m, batch)
+
+    ref = [torch.zeros(batch * m * m, dtype=torch.complex128, device=gpu) for _ in range(2)]
+    for i in range(2):
+        gemm(i, ref[i])
+        torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    for first_on_user_stream in (False, True):
+        out = [torch.zeros_like(ref[0]) for _ in range(2)]
+        torch.cuda.synchronize()
+        if first_on_user_stream:
+            with torch.cuda.stream(s):
+                gemm(0, out[0])
+            gemm(1, out[1])
+        else:
+            gemm(0, out[0])
+            with torch.cuda.stream(s):
+                out[1].zero_()
+                gemm(1, out[1])
+        torch.cuda.synchronize()
+        for i in range(2):
+            assert torch.equal(out[i], ref[i]), (first_on_user_stream, i)
