@@ -469,18 +469,14 @@ def main():
     # kernel time on the library's (= torch's current) stream by HIP events.  N = 1, where a step
     # is one GEMM launch and its split-K reduce: one event pair around the K timed steps, so the
     # average launch duration is the stream time per step (GEMM + reduce + the launch gaps
-    # between them).  Otherwise one event pair around every GEMM launch with its reduce
-    # ("gemm_total"); those two event records per launch cost ~9 us of stream time per step
-    # (marker packets between the kernels), which is why N = 1 does not use them.
+    # between them).  Otherwise (N > 1: a step's GEMM is cut in T chunks beside the exchanges)
+    # one event pair around every GEMM launch with its reduce ("gemm_total") over K more steps
+    # right after the timed ones: those two event records per launch cost ~9 us of stream time
+    # each (marker packets between the kernels), so no timed step carries them.
     per_launch = world > 1 or calls_per_step != 1
-    if per_launch:
-        sb.timings_enable(True)
-        sb.timings_filter("gemm_total")
-        sb.timings_reset()
-    else:
-        ev_start = torch.cuda.Event(enable_timing=True)
-        ev_end = torch.cuda.Event(enable_timing=True)
-        ev_start.record()
+    ev_start = torch.cuda.Event(enable_timing=True)
+    ev_end = torch.cuda.Event(enable_timing=True)
+    ev_start.record()
     # the shader clock the timed GEMMs ran at: workgroup 0 of every LDS-DMA GEMM launch sums its
     # s_memtime (shader clock) and s_memrealtime (100 MHz) spans (three vector atomics by one
     # thread per launch), so a slower box can be told apart from a slower kernel
@@ -489,8 +485,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         step()
-    if not per_launch:
-        ev_end.record()
+    ev_end.record()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -500,15 +495,23 @@ def main():
                          device="cpu" if args.share_gpu in ("host", "rccl") else dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
+    clk_cycles, clk_ticks = sb.tune_get("gemm.clock_cycles"), sb.tune_get("gemm.clock_ticks")
+    clk_launches = sb.tune_get("gemm.clock_launches")
+    sb.tune_set("gemm.clock", 0)
     if per_launch:
+        progress("per-launch GEMM timing")
+        sb.timings_enable(True)
+        sb.timings_filter("gemm_total")
+        sb.timings_reset()
+        for i in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        barrier()
         gemm_ms, gemm_calls = sb.timings_get("gemm_total")
         sb.timings_enable(False)
     else:
         gemm_ms, gemm_calls = ev_start.elapsed_time(ev_end), args.steps
     sb.timings_filter(None)
-    clk_cycles, clk_ticks = sb.tune_get("gemm.clock_cycles"), sb.tune_get("gemm.clock_ticks")
-    clk_launches = sb.tune_get("gemm.clock_launches")
-    sb.tune_set("gemm.clock", 0)
     shader_ghz = round(clk_cycles / clk_ticks * 0.1, 4) if clk_ticks > 0 else None
     # one GEMM = the MFMA kernel launch + its split-K reduce (the reduce is part of the GEMM)
     kernel_s = gemm_ms / max(gemm_calls, 1) / 1e3
@@ -627,7 +630,8 @@ def main():
                                    "ms avg (HIP events on its launch stream, %s)" % (
                                        8 if m3 else 16, 8 if m3 else 16, "3M" if m3 else "4M",
                                        gemm_calls, kernel_s * 1e3,
-                                       "a pair around every launch" if per_launch else
+                                       "a pair around every launch, K steps right after the "
+                                       "timed ones" if per_launch else
                                        "one pair around the timed steps: GEMM + reduce + launch "
                                        "gaps per step"),
                          "flops_per_launch": flops_launch,
