@@ -119,16 +119,19 @@ print('OK')
 
 def test_scratch_reuse_across_streams(gpu):
     """Split-K scratch freed on the null stream (no event recorded: a durable stream) and reused at
-    once from a caller's stream, and the other way round: the second GEMM waits for the first's
-    reduce (results bit-identical to the same GEMMs run one at a time)."""
+    once from a caller's stream, and the other way round: the second call's GEMM (short, the same
+    scratch size) must not write its partials before the first call's reduce has read them --
+    results bit-identical to the same GEMMs run one at a time."""
     import torch
     import superbblas_amd as sb
-    m, k, batch = 256, 8192, 16  # split-K over 4 pieces: a 67 MB scratch block per call
+    m, batch = 256, 16
+    ks = (8192, 1024)  # both split over 4 pieces: one 67 MB scratch block each
     g = torch.Generator(device=gpu).manual_seed(3)
-    a = [torch.randn(batch * m * k, dtype=torch.complex128, device=gpu, generator=g) for _ in range(2)]
-    b = [torch.randn(batch * k * m, dtype=torch.complex128, device=gpu, generator=g) for _ in range(2)]
+    a = [torch.randn(batch * m * k, dtype=torch.complex128, device=gpu, generator=g) for k in ks]
+    b = [torch.randn(batch * k * m, dtype=torch.complex128, device=gpu, generator=g) for k in ks]
 
     def gemm(i, c):
+        k = ks[i]
         sb.xgemm_batch_strided("T", "N", m, m, k, 1.0, a[i], k, m * k, b[i], k, k * m, 0.0, c, m,
                                m * m, batch)
 
@@ -137,18 +140,18 @@ def test_scratch_reuse_across_streams(gpu):
         gemm(i, ref[i])
         torch.cuda.synchronize()
     s = torch.cuda.Stream()
-    for first_on_user_stream in (False, True):
-        out = [torch.zeros_like(ref[0]) for _ in range(2)]
-        torch.cuda.synchronize()
-        if first_on_user_stream:
-            with torch.cuda.stream(s):
-                gemm(0, out[0])
-            gemm(1, out[1])
-        else:
-            gemm(0, out[0])
-            with torch.cuda.stream(s):
-                out[1].zero_()
+    for rep in range(3):
+        for first_on_user_stream in (False, True):
+            out = [torch.zeros_like(ref[0]) for _ in range(2)]
+            torch.cuda.synchronize()
+            if first_on_user_stream:
+                with torch.cuda.stream(s):
+                    gemm(0, out[0])
                 gemm(1, out[1])
-        torch.cuda.synchronize()
-        for i in range(2):
-            assert torch.equal(out[i], ref[i]), (first_on_user_stream, i)
+            else:
+                gemm(0, out[0])
+                with torch.cuda.stream(s):
+                    gemm(1, out[1])
+            torch.cuda.synchronize()
+            for i in range(2):
+                assert torch.equal(out[i], ref[i]), (rep, first_on_user_stream, i)
