@@ -459,6 +459,8 @@ int sbx_tune_set(const char *key, long long value) {
         else if (k == "gemm.share_ab") g_gemm_tune.share_ab = (int)value;
         else if (k == "gemm.frag") g_gemm_tune.frag = (int)value;
         else if (k == "gemm.dot_wgs") g_gemm_tune.dot_wgs = (int)value;
+        else if (k == "gemm.frag_tall") g_gemm_tune.frag_tall = (int)value;
+        else if (k == "gemm.frag_pair") g_gemm_tune.frag_pair = (int)value;
         else if (k == "gemm.frag_uk") g_gemm_tune.frag_uk = (int)value;
         else if (k == "gemm.frag_waves") g_gemm_tune.frag_waves = (int)value;
         else if (k == "gemm.clock") {
@@ -526,6 +528,8 @@ int sbx_tune_get(const char *key, long long *value) {
         else if (k == "gemm.share_ab") *value = g_gemm_tune.share_ab;
         else if (k == "gemm.frag") *value = g_gemm_tune.frag;
         else if (k == "gemm.dot_wgs") *value = g_gemm_tune.dot_wgs;
+        else if (k == "gemm.frag_tall") *value = g_gemm_tune.frag_tall;
+        else if (k == "gemm.frag_pair") *value = g_gemm_tune.frag_pair;
         else if (k == "gemm.frag_uk") *value = g_gemm_tune.frag_uk;
         else if (k == "gemm.frag_waves") *value = g_gemm_tune.frag_waves;
         else if (k == "gemm.clock") *value = g_gemm_tune.clock;

@@ -113,6 +113,9 @@ struct GemmKArgs {
     // (m0 == n0) stages one slab image and reads both operands' fragments from it
     int same_ab;
     int dma_nt; // the loader waves' slab DMA with the non-temporal policy (gemm.dma_nt)
+    // gemm_frag_kernel<., KP = true>: the operand's k pairs are one 16-byte load (8-byte
+    // elements, unit k stride, 16-byte aligned rows)
+    int pair_a, pair_b;
 };
 
 /// Offset of index i of a split group: (i / lo) * s_hi + (i % lo) * s (i < 2^31)
@@ -1256,7 +1259,11 @@ __global__ void __launch_bounds__(256) gemm_rows_kernel(const GemmKArgs p) {
 // descriptors (an offset past the range reads zero: rows, columns and k past the ends), UK
 // k-steps per group, the next group's loads issued before the current group's MFMAs; the
 // split-K partials go to the work array and the split-K reduce sums them in split order.
-template <typename R, bool CPLX, int UK>
+// KP (8-byte elements, k even): lane q of the k-steps u, u + 1 of a group takes the pair k0 + 4u +
+// 2q, + 1 (the same permutation of a group's k for A and B), so an operand with unit k stride
+// reads each pair with one 16-byte load: 64 contiguous bytes per row and instruction instead of
+// 32 (pair_a / pair_b; the other operand reads the pair's two elements)
+template <typename R, bool CPLX, int UK, bool KP = false>
 __global__ void __launch_bounds__(256) gemm_frag_kernel(const GemmKArgs p) {
     typedef typename Elem<R, CPLX>::type E;
     typedef typename Mfma<R>::acc_t acc_t;
@@ -1284,13 +1291,39 @@ __global__ void __launch_bounds__(256) gemm_frag_kernel(const GemmKArgs p) {
     const U sign = (U)1 << (sizeof(R) * 8 - 1);
     const U ma = p.conja ? sign : 0, mb = p.conjb ? sign : 0;
     auto flip = [](R v, U m) { return __builtin_bit_cast(R, __builtin_bit_cast(U, v) ^ m); };
+    static_assert(!KP || (ES == 8 && UK % 2 == 0), "k pairs: 8-byte elements, even UK");
     auto load = [&](long k0, E (&a)[UK], E (&b)[UK]) {
+        if constexpr (KP) {
 #pragma unroll
-        for (int u = 0; u < UK; ++u) {
-            const long kk = k0 + 4 * u + q;
-            const bool kin = kk < k_end;
-            a[u] = buf_load<E>(rsA, okA && kin ? (unsigned)((baseA + kk * p.sa_k) * ES) : 0x80000000u);
-            b[u] = buf_load<E>(rsB, okB && kin ? (unsigned)((baseB + kk * p.sb_k) * ES) : 0x80000000u);
+            for (int u = 0; u < UK; u += 2) {
+                const long kk = k0 + 4 * u + 2 * q; // (k_end even: kk + 1 is in range with kk)
+                const bool kin = kk < k_end;
+                auto pair = [&](__amdgpu_buffer_rsrc_t rs, bool ok, bool paired, long base, long sk,
+                                E &lo, E &hi) {
+                    if (paired) {
+                        const auto v = __builtin_amdgcn_raw_buffer_load_b128(
+                            rs, ok && kin ? (unsigned)((base + kk) * ES) : 0x80000000u, 0, 0);
+                        typedef typename std::conditional<sizeof(R) == 8, double, float2>::type H;
+                        struct Two { H lo, hi; };
+                        const Two t = __builtin_bit_cast(Two, v);
+                        lo = __builtin_bit_cast(E, t.lo);
+                        hi = __builtin_bit_cast(E, t.hi);
+                    } else {
+                        lo = buf_load<E>(rs, ok && kin ? (unsigned)((base + kk * sk) * ES) : 0x80000000u);
+                        hi = buf_load<E>(rs, ok && kin ? (unsigned)((base + (kk + 1) * sk) * ES) : 0x80000000u);
+                    }
+                };
+                pair(rsA, okA, p.pair_a != 0, baseA, p.sa_k, a[u], a[u + 1]);
+                pair(rsB, okB, p.pair_b != 0, baseB, p.sb_k, b[u], b[u + 1]);
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < UK; ++u) {
+                const long kk = k0 + 4 * u + q;
+                const bool kin = kk < k_end;
+                a[u] = buf_load<E>(rsA, okA && kin ? (unsigned)((baseA + kk * p.sa_k) * ES) : 0x80000000u);
+                b[u] = buf_load<E>(rsB, okB && kin ? (unsigned)((baseB + kk * p.sb_k) * ES) : 0x80000000u);
+            }
         }
     };
     acc_t accR = acc_t{0, 0, 0, 0}, accI = acc_t{0, 0, 0, 0};
@@ -1761,7 +1794,8 @@ template <typename R, bool CPLX> bool launch_skinny(const GemmKArgs &p0, int dev
 }
 
 /// The fragment kernel (gemm_frag_kernel) for small outputs with a long k (m, n <= 32) and
-/// tall-skinny products (one output dimension <= 16 with k <= 64, or <= 16 against a long k);
+/// tall-skinny products (one output dimension <= 16 -- 32 for complex<float> -- with k <= 64, or
+/// <= 16 against a long k);
 /// false when the shape is for the tiled kernels
 template <typename R, bool CPLX> bool launch_frag(const GemmKArgs &p0, int device, hipStream_t s) {
     // (the opt-in 3-multiplication form runs on the tiled kernels only)
@@ -1771,11 +1805,18 @@ template <typename R, bool CPLX> bool launch_frag(const GemmKArgs &p0, int devic
     // 490 us; updates m = 49152, n = k = 12 / 16: 291 / 453 -> 173 / 208 us; n = k <= 4 stay on
     // the rows kernel, 21-49 us against 122)
     const bool small = p0.m <= 32 && p0.n <= 32;
-    const bool tall = (p0.n <= 16 && p0.n > 4 && ((p0.k <= 64 && p0.k > 4) || p0.m <= 16)) ||
-                      (p0.m <= 16 && p0.m > 4 && p0.k <= 64 && p0.k > 4);
+    // the short output dimension against a short k: up to 32 for complex<float> (updates m =
+    // 49152, n = k = 24 / 32, batch 32: 416 / 463 -> 327 / 427 us against the tiled kernels; 48
+    // and 64 no better), 16 otherwise (complex<double> n = k = 32 / 48 / 64: no gain);
+    // profiles/r06_gemm_frag_tall.txt; gemm.frag_tall > 0 overrides
+    typedef typename Elem<R, CPLX>::type E;
+    const long tn = g_gemm_tune.frag_tall > 0 ? g_gemm_tune.frag_tall
+                    : (CPLX && sizeof(R) == 4) ? 32 : 16;
+    const bool tall = (p0.n <= 16 && p0.n > 4 && p0.m <= 16) ||
+                      (p0.n <= tn && p0.n > 4 && p0.k <= 64 && p0.k > 4) ||
+                      (p0.m <= tn && p0.m > 4 && p0.k <= 64 && p0.k > 4);
     if (!small && !tall) return false;
     if (g_gemm_tune.skinny && p0.m <= 4 && p0.n <= 4 && g_gemm_tune.frag < 2) return false;
-    typedef typename Elem<R, CPLX>::type E;
     // k-steps per load group: 2 for a k of 8 or less and for small outputs, else 4 (0 = this
     // rule; profiles/r06_gemm_frag_cfg.txt: inner products m = n = 16 229 -> 204 us, the update
     // n = k = 8 150 -> 113 us with 2; n = k = 16 208 -> 226 us, so 4 there)
@@ -1789,15 +1830,40 @@ template <typename R, bool CPLX> bool launch_frag(const GemmKArgs &p0, int devic
                                          work, device);
     const long blocks = (items + 3) / 4;
     if (blocks > 0x7fffffffL) return false;
+    // 16-byte k pairs for an operand with 8-byte elements, unit k stride and 16-byte aligned rows
+    // (gemm.frag_pair 0 = off)
+    auto aligned = [](const void *ptr, long s1, long s2) {
+        return ((std::uintptr_t)ptr % 16) == 0 && s1 % 2 == 0 && s2 % 2 == 0;
+    };
+    constexpr bool E8 = sizeof(E) == 8;
+    p.pair_a = E8 && p.sa_k == 1 && aligned(p.a, p.sa_m, p.sa_b);
+    p.pair_b = E8 && p.sb_k == 1 && aligned(p.b, p.sb_n, p.sb_b);
+    // (measured, complex<float>, tools/studies/gemm_skinny_bench.py GEMM_PAIR, profiles/
+    // r06_gemm_frag_pairs.txt: inner products, both operands paired, m = n = 8 / 12 / 16 / 32
+    // 121 / 139 / 172 / 428 -> 100 / 122 / 160 / 288 us; updates, B alone paired, n = k = 8 / 12
+    // 80 / 136 -> 82 / 142 us, 16 the same, 32 427 -> 385 us: so B alone from n > 16)
+    const bool kp = E8 && g_gemm_tune.frag_pair && p.k % 2 == 0 &&
+                    (p.pair_a || (p.pair_b && p.n > 16));
     KernelTimer total("gemm_total", s);
     {
         KernelTimer timer("gemm", s);
-        if (uk == 8)
-            hipLaunchKernelGGL((gemm_frag_kernel<R, CPLX, 8>), dim3((unsigned)blocks), dim3(256), 0, s, p);
-        else if (uk == 2)
-            hipLaunchKernelGGL((gemm_frag_kernel<R, CPLX, 2>), dim3((unsigned)blocks), dim3(256), 0, s, p);
-        else
-            hipLaunchKernelGGL((gemm_frag_kernel<R, CPLX, 4>), dim3((unsigned)blocks), dim3(256), 0, s, p);
+        const dim3 grid((unsigned)blocks), wg(256);
+        if constexpr (E8) {
+            if (kp && uk == 8)
+                hipLaunchKernelGGL((gemm_frag_kernel<R, CPLX, 8, true>), grid, wg, 0, s, p);
+            else if (kp && uk == 2)
+                hipLaunchKernelGGL((gemm_frag_kernel<R, CPLX, 2, true>), grid, wg, 0, s, p);
+            else if (kp)
+                hipLaunchKernelGGL((gemm_frag_kernel<R, CPLX, 4, true>), grid, wg, 0, s, p);
+        }
+        if (!kp) {
+            if (uk == 8)
+                hipLaunchKernelGGL((gemm_frag_kernel<R, CPLX, 8>), grid, wg, 0, s, p);
+            else if (uk == 2)
+                hipLaunchKernelGGL((gemm_frag_kernel<R, CPLX, 2>), grid, wg, 0, s, p);
+            else
+                hipLaunchKernelGGL((gemm_frag_kernel<R, CPLX, 4>), grid, wg, 0, s, p);
+        }
         SBX_HIP_CHECK(hipGetLastError());
     }
     launch_reduce<R, CPLX>(p, s);

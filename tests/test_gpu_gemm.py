@@ -290,7 +290,9 @@ def test_host_context_calls_use_current_device(gpu):
 # and every trans pair; gemm.frag 0 runs the same shapes through the other kernels
 FRAG = [(5, 5, 6144, 4), (8, 8, 6144, 4), (12, 12, 3000, 3), (16, 16, 6144, 2), (32, 32, 4096, 2),
         (17, 30, 777, 3), (6144, 8, 8, 2), (6144, 12, 12, 2), (3000, 16, 16, 1), (999, 13, 64, 2),
-        (16, 1, 1 << 15, 1), (1, 16, 1 << 15, 1), (16, 5000, 7, 1), (1000, 3, 50, 2)]
+        (16, 1, 1 << 15, 1), (1, 16, 1 << 15, 1), (16, 5000, 7, 1), (1000, 3, 50, 2),
+        # tall-skinny with a short dimension of 17-32 (the fragment kernel for complex<float>)
+        (4100, 32, 32, 2), (24, 3001, 20, 2), (2050, 17, 64, 1)]
 
 
 @pytest.mark.parametrize("dtype", [np.complex128, np.float64, np.complex64, np.float32])
@@ -305,4 +307,27 @@ def test_gemm_frag(gpu, dtype, ta, tb, m, n, k, batch, frag):
         out, ref = _run(gpu, dtype, ta, tb, m, n, k, batch, 0.5 - 0.25j, 0.75 + 0.5j, pad=1)
     finally:
         sb.tune_set("gemm.frag", old)
+    assert rel_err(out, ref) < TOL[dtype]
+
+
+FRAG_PAIRS = [(12, 12, 4096, 3), (32, 32, 2048, 2), (5, 9, 1000, 2), (4100, 32, 32, 2),
+              (2050, 24, 64, 1), (8, 8, 1001, 2)]
+
+
+@pytest.mark.parametrize("dtype", [np.complex64, np.float64])
+@pytest.mark.parametrize("ta,tb", [("T", "N"), ("C", "N"), ("N", "N"), ("C", "T")])
+@pytest.mark.parametrize("m,n,k,batch", FRAG_PAIRS)
+@pytest.mark.parametrize("pad", [0, 2])
+@pytest.mark.parametrize("pair", [1, 0])
+def test_gemm_frag_pairs(gpu, dtype, ta, tb, m, n, k, batch, pad, pair):
+    """gemm_frag_kernel with 8-byte elements: an operand with unit k stride and even strides reads
+    its k pairs as one 16-byte load (gemm.frag_pair; the pair permutes a load group's k the same
+    way for A and B), odd k or odd strides keep the element loads"""
+    import superbblas_amd as sb
+    old = sb.tune_get("gemm.frag_pair")
+    sb.tune_set("gemm.frag_pair", pair)
+    try:
+        out, ref = _run(gpu, dtype, ta, tb, m, n, k, batch, 0.5 - 0.25j, 0.75 + 0.5j, pad=pad)
+    finally:
+        sb.tune_set("gemm.frag_pair", old)
     assert rel_err(out, ref) < TOL[dtype]

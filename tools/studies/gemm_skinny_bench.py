@@ -4,7 +4,8 @@ lattice (local volume 16*16*16*32*... k = 49152 sites x colors, batch 32): inner
 (m = n = s, k = 49152) and updates (m = 49152, n = k = s), complex<double>, with gemm.frag on and
 off (and gemm.skinny), timed by the library's kernel timers (GEMM + split-K reduce).  Reports
 TFLOP/s (8 real flops per complex MAC) and the HBM rate of the operand and output bytes.  Not
-part of the product.  FRAGS=1,0: the gemm.frag values; SIZES=1,2,4,8,12,16,32,64."""
+part of the product.  FRAGS=1,0: the gemm.frag values; SIZES=1,2,4,8,12,16,32,64; DTYPE=cdouble or
+cfloat; TALLS: gemm.frag_tall values."""
 import json
 import os
 import statistics
@@ -24,6 +25,11 @@ def main():
     # DOTS: gemm.dot_wgs values (m, n <= 4); KINDS: inner,update
     dots = [int(v) for v in os.environ.get("DOTS", str(sb.tune_get("gemm.dot_wgs"))).split(",")]
     kinds = os.environ.get("KINDS", "inner,update").split(",")
+    dt = {"cdouble": torch.complex128, "cfloat": torch.complex64}[os.environ.get("DTYPE", "cdouble")]
+    es = 16 if dt == torch.complex128 else 8
+    talls = [int(v) for v in os.environ.get("TALLS", str(sb.tune_get("gemm.frag_tall"))).split(",")]
+    # GEMM_PAIR: gemm.frag_pair (16-byte k pairs for 8-byte elements)
+    sb.tune_set("gemm.frag_pair", int(os.environ.get("GEMM_PAIR", "1")))
     # FRAGCFG: "uk:waves" pairs for gemm_frag_kernel
     cfgs = [tuple(int(u) for u in v.split(":")) for v in os.environ.get(
         "FRAGCFG", "%d:%d" % (sb.tune_get("gemm.frag_uk"), sb.tune_get("gemm.frag_waves"))).split(",")]
@@ -32,11 +38,13 @@ def main():
             m, n, k = (s, s, K) if kind == "inner" else (K, s, s)
             ta, tb = ("C", "N") if kind == "inner" else ("N", "N")
             lda = k if ta != "N" else m
-            a = torch.randn(batch * m * k, dtype=torch.complex128, device=dev)
-            b = torch.randn(batch * k * n, dtype=torch.complex128, device=dev)
-            c = torch.zeros(batch * m * n, dtype=torch.complex128, device=dev)
-            for frag, dot, cfg in [(f, d, c) for f in frags for d in dots for c in cfgs]:
+            a = torch.randn(batch * m * k, dtype=dt, device=dev)
+            b = torch.randn(batch * k * n, dtype=dt, device=dev)
+            c = torch.zeros(batch * m * n, dtype=dt, device=dev)
+            for frag, dot, cfg, tall in [(f, d, c, t) for f in frags for d in dots for c in cfgs
+                                         for t in talls]:
                 sb.tune_set("gemm.frag", frag)
+                sb.tune_set("gemm.frag_tall", tall)
                 sb.tune_set("gemm.dot_wgs", dot)
                 sb.tune_set("gemm.frag_uk", cfg[0])
                 sb.tune_set("gemm.frag_waves", cfg[1])
@@ -59,14 +67,18 @@ def main():
                     ts.append(ms / calls / 1e3)
                 t = statistics.median(ts)
                 flops = 8.0 * m * n * k * batch
-                byts = 16.0 * batch * (m * k + k * n + m * n)
-                print(json.dumps({"kind": kind, "m": m, "n": n, "k": k, "batch": batch, "frag": frag, "dot_wgs": dot, "uk_waves": "%d:%d" % cfg,
+                byts = float(es) * batch * (m * k + k * n + m * n)
+                print(json.dumps({"kind": kind, "dtype": str(dt), "m": m, "n": n, "k": k,
+                                  "batch": batch, "frag": frag, "frag_tall": tall, "dot_wgs": dot,
+                                  "uk_waves": "%d:%d" % cfg,
                                   "us": round(t * 1e6, 1), "TFLOPs": round(flops / t / 1e12, 3),
                                   "TBps": round(byts / t / 1e12, 3)}), flush=True)
             del a, b, c
     sb.tune_set("gemm.frag", 1)
     sb.tune_set("gemm.frag_uk", 0)
     sb.tune_set("gemm.frag_waves", 4096)
+    sb.tune_set("gemm.frag_tall", 0)
+    sb.tune_set("gemm.frag_pair", 1)
 
 
 if __name__ == "__main__":
