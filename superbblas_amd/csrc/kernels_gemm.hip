@@ -1672,8 +1672,6 @@ void launch_tiled(const GemmKArgs &p, int device, hipStream_t stream) {
                     launch_dma_cfg<R, CPLX, AK, BK, 128, 128, 16, 4, 4, false>(p, device, stream, 0, 256);
             } else
                 launch_dma_cfg<R, CPLX, AK, BK, 128, 128, 16, 4, 4, false>(p, device, stream, 0, 256);
-        } else if (g_gemm_tune.tall64 && p.m >= 128 && p.n > 32 && p.n <= 64) {
-            launch_dma_cfg<R, CPLX, AK, BK, 128, 64, 8, 4, 2>(p, device, stream, 0, 512);
         } else {
             launch_dma_cfg<R, CPLX, AK, BK, 64, 64, 8, 2, 2>(p, device, stream, 0, 1024);
         }
@@ -1720,8 +1718,6 @@ void launch_tiled(const GemmKArgs &p, int device, hipStream_t stream) {
         }
         // 8-byte and 4-byte elements: 32-deep slabs (fewer barriers per MFMA; measured against
         // 16 and 64 on the lattice shape: double 50.5, complex<float> 116, float 107 TFLOP/s)
-        if (g_gemm_tune.tall64 && p.m >= 128 && p.n > 32 && p.n <= 64)
-            return launch_dma_cfg<R, CPLX, AK, BK, 128, 64, 32, 4, 2>(p, device, stream, 0, 512);
         if (p.m >= 128 && p.n >= 128)
             launch_dma_cfg<R, CPLX, AK, BK, 128, 128, 32, 4, 2>(p, device, stream, 0, 256);
         else

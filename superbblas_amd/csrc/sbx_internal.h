@@ -259,7 +259,6 @@ struct GemmTune {
     int frag_waves = 4096; ///< ... split-K to about this many waves
     int frag = 1;  ///< small outputs (m, n <= 32) and tall-skinny products on gemm_frag_kernel (MFMA
                    ///< fragments straight from global memory); 2 also for m, n <= 4; 0 = off
-    int tall64 = 0; ///< LDS-DMA tiles of 128 x 64 for outputs of 33-64 columns and >= 128 rows
     int frag_pair = 1; ///< ... 8-byte elements: k pairs of a unit-k-stride operand as one 16-byte load
     int frag_tall = 0; ///< ... tall-skinny products: the short output dimension up to this (k <= 64;
                        ///< 0 = 32 for complex<float>, else 16)
