@@ -1263,7 +1263,10 @@ __global__ void __launch_bounds__(256) gemm_rows_kernel(const GemmKArgs p) {
 // 2q, + 1 (the same permutation of a group's k for A and B), so an operand with unit k stride
 // reads each pair with one 16-byte load: 64 contiguous bytes per row and instruction instead of
 // 32 (pair_a / pair_b; the other operand reads the pair's two elements)
-template <typename R, bool CPLX, int UK, bool KP = false>
+// NT > 1: the wave computes NT adjacent 16 x 16 tiles of a row of tiles (columns n0 .. n0 + 16 NT),
+// so its A fragments are loaded once for NT tiles (the tall-skinny updates n = 32 / 64: A was
+// re-read n / 16 times)
+template <typename R, bool CPLX, int UK, bool KP = false, int NT = 1>
 __global__ void __launch_bounds__(256) gemm_frag_kernel(const GemmKArgs p) {
     typedef typename Elem<R, CPLX>::type E;
     typedef typename Mfma<R>::acc_t acc_t;
@@ -1278,21 +1281,28 @@ __global__ void __launch_bounds__(256) gemm_frag_kernel(const GemmKArgs p) {
     rest /= p.tm;
     const long tj = rest % p.tn;
     const long bb = rest / p.tn;
-    const long m0 = ti * 16, n0 = tj * 16;
+    const long m0 = ti * 16, n0 = tj * 16 * NT;
     const long k_begin = (long)split * p.kchunk, k_end = min(p.k, k_begin + p.kchunk);
     const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
         (void *)((const E *)p.a + bb * p.sa_b), (short)0, (int)p.a_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
         (void *)((const E *)p.b + bb * p.sb_b), (short)0, (int)p.b_bytes, 0x00020000);
     const int r = lane & 15, q = lane >> 4;
-    const bool okA = m0 + r < p.m, okB = n0 + r < p.n;
-    const long baseA = (m0 + r) * p.sa_m, baseB = (n0 + r) * p.sb_n;
+    const bool okA = m0 + r < p.m;
+    const long baseA = (m0 + r) * p.sa_m;
+    bool okB[NT];
+    long baseB[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        okB[j] = n0 + 16 * j + r < p.n;
+        baseB[j] = (n0 + 16 * j + r) * p.sb_n;
+    }
     typedef typename std::conditional<sizeof(R) == 8, unsigned long long, unsigned>::type U;
     const U sign = (U)1 << (sizeof(R) * 8 - 1);
     const U ma = p.conja ? sign : 0, mb = p.conjb ? sign : 0;
     auto flip = [](R v, U m) { return __builtin_bit_cast(R, __builtin_bit_cast(U, v) ^ m); };
     static_assert(!KP || (ES == 8 && UK % 2 == 0), "k pairs: 8-byte elements, even UK");
-    auto load = [&](long k0, E (&a)[UK], E (&b)[UK]) {
+    auto load = [&](long k0, E (&a)[UK], E (&b)[NT][UK]) {
         if constexpr (KP) {
 #pragma unroll
             for (int u = 0; u < UK; u += 2) {
@@ -1314,7 +1324,9 @@ __global__ void __launch_bounds__(256) gemm_frag_kernel(const GemmKArgs p) {
                     }
                 };
                 pair(rsA, okA, p.pair_a != 0, baseA, p.sa_k, a[u], a[u + 1]);
-                pair(rsB, okB, p.pair_b != 0, baseB, p.sb_k, b[u], b[u + 1]);
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+                    pair(rsB, okB[j], p.pair_b != 0, baseB[j], p.sb_k, b[j][u], b[j][u + 1]);
             }
         } else {
 #pragma unroll
@@ -1322,46 +1334,62 @@ __global__ void __launch_bounds__(256) gemm_frag_kernel(const GemmKArgs p) {
                 const long kk = k0 + 4 * u + q;
                 const bool kin = kk < k_end;
                 a[u] = buf_load<E>(rsA, okA && kin ? (unsigned)((baseA + kk * p.sa_k) * ES) : 0x80000000u);
-                b[u] = buf_load<E>(rsB, okB && kin ? (unsigned)((baseB + kk * p.sb_k) * ES) : 0x80000000u);
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+                    b[j][u] = buf_load<E>(rsB, okB[j] && kin ? (unsigned)((baseB[j] + kk * p.sb_k) * ES) : 0x80000000u);
             }
         }
     };
-    acc_t accR = acc_t{0, 0, 0, 0}, accI = acc_t{0, 0, 0, 0};
-    E a[UK], b[UK], an[UK], bn[UK];
+    acc_t accR[NT], accI[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        accR[j] = acc_t{0, 0, 0, 0};
+        accI[j] = acc_t{0, 0, 0, 0};
+    }
+    E a[UK], b[NT][UK], an[UK], bn[NT][UK];
     if (k_begin < k_end) load(k_begin, a, b);
     for (long k = k_begin; k < k_end; k += 4 * UK) {
         if (k + 4 * UK < k_end) load(k + 4 * UK, an, bn);
 #pragma unroll
         for (int u = 0; u < UK; ++u) {
             if constexpr (CPLX) {
-                const R ar = a[u].x, ai = flip(a[u].y, ma), br = b[u].x, bi = flip(b[u].y, mb);
-                accR = Mfma<R>::mma(ar, br, accR);
-                accI = Mfma<R>::mma(ar, bi, accI);
-                accR = Mfma<R>::mma(-ai, bi, accR);
-                accI = Mfma<R>::mma(ai, br, accI);
+                const R ar = a[u].x, ai = flip(a[u].y, ma);
+#pragma unroll
+                for (int j = 0; j < NT; ++j) {
+                    const R br = b[j][u].x, bi = flip(b[j][u].y, mb);
+                    accR[j] = Mfma<R>::mma(ar, br, accR[j]);
+                    accI[j] = Mfma<R>::mma(ar, bi, accI[j]);
+                    accR[j] = Mfma<R>::mma(-ai, bi, accR[j]);
+                    accI[j] = Mfma<R>::mma(ai, br, accI[j]);
+                }
             } else {
-                accR = Mfma<R>::mma(a[u], b[u], accR);
+#pragma unroll
+                for (int j = 0; j < NT; ++j) accR[j] = Mfma<R>::mma(a[u], b[j][u], accR[j]);
             }
         }
 #pragma unroll
         for (int u = 0; u < UK; ++u) {
             a[u] = an[u];
-            b[u] = bn[u];
+#pragma unroll
+            for (int j = 0; j < NT; ++j) b[j][u] = bn[j][u];
         }
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const long gi = m0 + Mfma<R>::row(lane, i), gj = n0 + r;
-        if (gi >= p.m || gj >= p.n) continue;
-        const R vr = accR[i], vi = CPLX ? accI[i] : R(0);
-        if (p.splits == 1) {
-            epilogue_store<R>((R *)((E *)p.c + bb * p.sc_b + gi * p.sc_m + gj * p.sc_n), vr, vi, p, CPLX);
-        } else {
-            E *w = (E *)p.work + (((long)split * p.batch + bb) * p.n + gj) * p.m + gi;
-            if constexpr (CPLX)
-                *w = E{vr, vi};
-            else
-                *w = vr;
+    for (int j = 0; j < NT; ++j) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const long gi = m0 + Mfma<R>::row(lane, i), gj = n0 + 16 * j + r;
+            if (gi >= p.m || gj >= p.n) continue;
+            const R vr = accR[j][i], vi = CPLX ? accI[j][i] : R(0);
+            if (p.splits == 1) {
+                epilogue_store<R>((R *)((E *)p.c + bb * p.sc_b + gi * p.sc_m + gj * p.sc_n), vr, vi, p, CPLX);
+            } else {
+                E *w = (E *)p.work + (((long)split * p.batch + bb) * p.n + gj) * p.m + gi;
+                if constexpr (CPLX)
+                    *w = E{vr, vi};
+                else
+                    *w = vr;
+            }
         }
     }
 }
@@ -1794,7 +1822,7 @@ template <typename R, bool CPLX> bool launch_skinny(const GemmKArgs &p0, int dev
 }
 
 /// The fragment kernel (gemm_frag_kernel) for small outputs with a long k (m, n <= 32) and
-/// tall-skinny products (one output dimension <= 16 -- 32 for complex<float> -- with k <= 64, or
+/// tall-skinny products (one output dimension <= 16 -- 48 for complex<float> -- with k <= 64, or
 /// <= 16 against a long k);
 /// false when the shape is for the tiled kernels
 template <typename R, bool CPLX> bool launch_frag(const GemmKArgs &p0, int device, hipStream_t s) {
@@ -1810,8 +1838,10 @@ template <typename R, bool CPLX> bool launch_frag(const GemmKArgs &p0, int devic
     // and 64 no better), 16 otherwise (complex<double> n = k = 32 / 48 / 64: no gain);
     // profiles/r06_gemm_frag_tall.txt; gemm.frag_tall > 0 overrides
     typedef typename Elem<R, CPLX>::type E;
+    // (with the k pairs: complex<float> n = k = 48 805 -> 652 us; 64 855 -> 974, so up to 48;
+    // profiles/r06_gemm_frag_nt.txt)
     const long tn = g_gemm_tune.frag_tall > 0 ? g_gemm_tune.frag_tall
-                    : (CPLX && sizeof(R) == 4) ? 32 : 16;
+                    : (CPLX && sizeof(R) == 4) ? 48 : 16;
     const bool tall = (p0.n <= 16 && p0.n > 4 && p0.m <= 16) ||
                       (p0.n <= tn && p0.n > 4 && p0.k <= 64 && p0.k > 4) ||
                       (p0.m <= tn && p0.m > 4 && p0.k <= 64 && p0.k > 4);
@@ -1823,11 +1853,17 @@ template <typename R, bool CPLX> bool launch_frag(const GemmKArgs &p0, int devic
     const int auto_uk = p0.k <= 8 || (p0.m <= 32 && p0.n <= 32) ? 2 : 4;
     const int uk = g_gemm_tune.frag_uk == 0 ? auto_uk : g_gemm_tune.frag_uk == 8 ? 8
                  : g_gemm_tune.frag_uk == 2 ? 2 : 4;
+    // 16 x 16 tiles per wave along n (gemm.frag_nt 1, 2 or 4; 0 = 2 for small outputs of 17-32
+    // columns, else 1: inner products m = n = 32 300 / 488 -> 250 / 451 us for complex<float> /
+    // <double>; the updates n = k = 24-64 gain nothing from 2 and lose with 4,
+    // profiles/r06_gemm_frag_nt.txt)
+    const int nt = g_gemm_tune.frag_nt == 4 ? 4 : g_gemm_tune.frag_nt == 2 ? 2
+                 : g_gemm_tune.frag_nt == 0 && small && p0.n > 16 ? 2 : 1;
     GemmKArgs p = p0;
     Scratch work;
     // ~gemm.frag_waves waves: split-K when the tiles alone are fewer
-    const long items = prepare_launch<E>(p, 16, 16, 4 * uk, 0, std::max(64, g_gemm_tune.frag_waves),
-                                         work, device);
+    const long items = prepare_launch<E>(p, 16, 16 * nt, 4 * uk, 0,
+                                         std::max(64, g_gemm_tune.frag_waves), work, device);
     const long blocks = (items + 3) / 4;
     if (blocks > 0x7fffffffL) return false;
     // 16-byte k pairs for an operand with 8-byte elements, unit k stride and 16-byte aligned rows
@@ -1848,22 +1884,31 @@ template <typename R, bool CPLX> bool launch_frag(const GemmKArgs &p0, int devic
     {
         KernelTimer timer("gemm", s);
         const dim3 grid((unsigned)blocks), wg(256);
-        if constexpr (E8) {
-            if (kp && uk == 8)
-                hipLaunchKernelGGL((gemm_frag_kernel<R, CPLX, 8, true>), grid, wg, 0, s, p);
-            else if (kp && uk == 2)
-                hipLaunchKernelGGL((gemm_frag_kernel<R, CPLX, 2, true>), grid, wg, 0, s, p);
-            else if (kp)
-                hipLaunchKernelGGL((gemm_frag_kernel<R, CPLX, 4, true>), grid, wg, 0, s, p);
-        }
-        if (!kp) {
-            if (uk == 8)
-                hipLaunchKernelGGL((gemm_frag_kernel<R, CPLX, 8>), grid, wg, 0, s, p);
-            else if (uk == 2)
-                hipLaunchKernelGGL((gemm_frag_kernel<R, CPLX, 2>), grid, wg, 0, s, p);
+        auto go = [&](auto ukc, auto kpc, auto ntc) {
+            constexpr int UKv = decltype(ukc)::value, NTv = decltype(ntc)::value;
+            constexpr bool KPv = decltype(kpc)::value;
+            hipLaunchKernelGGL((gemm_frag_kernel<R, CPLX, UKv, KPv, NTv>), grid, wg, 0, s, p);
+        };
+        auto by_nt = [&](auto ukc, auto kpc) {
+            if (nt == 4)
+                go(ukc, kpc, std::integral_constant<int, 4>());
+            else if (nt == 2)
+                go(ukc, kpc, std::integral_constant<int, 2>());
             else
-                hipLaunchKernelGGL((gemm_frag_kernel<R, CPLX, 4>), grid, wg, 0, s, p);
+                go(ukc, kpc, std::integral_constant<int, 1>());
+        };
+        auto by_uk = [&](auto kpc) {
+            if (uk == 8)
+                by_nt(std::integral_constant<int, 8>(), kpc);
+            else if (uk == 2)
+                by_nt(std::integral_constant<int, 2>(), kpc);
+            else
+                by_nt(std::integral_constant<int, 4>(), kpc);
+        };
+        if constexpr (E8) {
+            if (kp) by_uk(std::true_type());
         }
+        if (!kp) by_uk(std::false_type());
         SBX_HIP_CHECK(hipGetLastError());
     }
     launch_reduce<R, CPLX>(p, s);

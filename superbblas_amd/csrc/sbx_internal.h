@@ -259,9 +259,10 @@ struct GemmTune {
     int frag_waves = 4096; ///< ... split-K to about this many waves
     int frag = 1;  ///< small outputs (m, n <= 32) and tall-skinny products on gemm_frag_kernel (MFMA
                    ///< fragments straight from global memory); 2 also for m, n <= 4; 0 = off
+    int frag_nt = 0; ///< ... 16 x 16 tiles per wave along n (1, 2 or 4; 0 = 2 for 17-32-column small outputs)
     int frag_pair = 1; ///< ... 8-byte elements: k pairs of a unit-k-stride operand as one 16-byte load
     int frag_tall = 0; ///< ... tall-skinny products: the short output dimension up to this (k <= 64;
-                       ///< 0 = 32 for complex<float>, else 16)
+                       ///< 0 = 48 for complex<float>, else 16)
 };
 /// The S3T checksum (storage.cpp; storage.h:701-731): CRC-32 (zlib polynomial) of the bytes, or
 /// with blocksize > 0 the CRC of the CRCs of blocksize chunks (prev must then be 0)

@@ -291,8 +291,8 @@ def test_host_context_calls_use_current_device(gpu):
 FRAG = [(5, 5, 6144, 4), (8, 8, 6144, 4), (12, 12, 3000, 3), (16, 16, 6144, 2), (32, 32, 4096, 2),
         (17, 30, 777, 3), (6144, 8, 8, 2), (6144, 12, 12, 2), (3000, 16, 16, 1), (999, 13, 64, 2),
         (16, 1, 1 << 15, 1), (1, 16, 1 << 15, 1), (16, 5000, 7, 1), (1000, 3, 50, 2),
-        # tall-skinny with a short dimension of 17-32 (the fragment kernel for complex<float>)
-        (4100, 32, 32, 2), (24, 3001, 20, 2), (2050, 17, 64, 1)]
+        # tall-skinny with a short dimension of 17-48 (the fragment kernel for complex<float>)
+        (4100, 32, 32, 2), (24, 3001, 20, 2), (2050, 17, 64, 1), (3000, 48, 48, 1)]
 
 
 @pytest.mark.parametrize("dtype", [np.complex128, np.float64, np.complex64, np.float32])
@@ -330,4 +330,27 @@ def test_gemm_frag_pairs(gpu, dtype, ta, tb, m, n, k, batch, pad, pair):
         out, ref = _run(gpu, dtype, ta, tb, m, n, k, batch, 0.5 - 0.25j, 0.75 + 0.5j, pad=pad)
     finally:
         sb.tune_set("gemm.frag_pair", old)
+    assert rel_err(out, ref) < TOL[dtype]
+
+
+FRAG_NT = [(4100, 64, 64, 2), (2050, 48, 32, 1), (999, 40, 17, 2), (32, 32, 4096, 2),
+           (12, 12, 3000, 3), (6144, 8, 8, 2)]
+
+
+@pytest.mark.parametrize("dtype", [np.complex128, np.float64, np.complex64, np.float32])
+@pytest.mark.parametrize("ta,tb", [("N", "N"), ("C", "N"), ("N", "T")])
+@pytest.mark.parametrize("m,n,k,batch", FRAG_NT)
+@pytest.mark.parametrize("nt", [2, 4])
+def test_gemm_frag_nt(gpu, dtype, ta, tb, m, n, k, batch, nt):
+    """gemm_frag_kernel with NT 16 x 16 tiles per wave along n (gemm.frag_nt; the A fragments
+    loaded once for the NT tiles), the tall form widened to 64 columns (gemm.frag_tall)"""
+    import superbblas_amd as sb
+    old_nt, old_tall = sb.tune_get("gemm.frag_nt"), sb.tune_get("gemm.frag_tall")
+    sb.tune_set("gemm.frag_nt", nt)
+    sb.tune_set("gemm.frag_tall", 64)
+    try:
+        out, ref = _run(gpu, dtype, ta, tb, m, n, k, batch, 0.5 - 0.25j, 0.75 + 0.5j, pad=1)
+    finally:
+        sb.tune_set("gemm.frag_nt", old_nt)
+        sb.tune_set("gemm.frag_tall", old_tall)
     assert rel_err(out, ref) < TOL[dtype]

@@ -30,6 +30,8 @@ def main():
     talls = [int(v) for v in os.environ.get("TALLS", str(sb.tune_get("gemm.frag_tall"))).split(",")]
     # GEMM_PAIR: gemm.frag_pair (16-byte k pairs for 8-byte elements)
     sb.tune_set("gemm.frag_pair", int(os.environ.get("GEMM_PAIR", "1")))
+    # NTS: gemm.frag_nt values (16 x 16 tiles per wave along n)
+    nts = [int(v) for v in os.environ.get("NTS", str(sb.tune_get("gemm.frag_nt"))).split(",")]
     # FRAGCFG: "uk:waves" pairs for gemm_frag_kernel
     cfgs = [tuple(int(u) for u in v.split(":")) for v in os.environ.get(
         "FRAGCFG", "%d:%d" % (sb.tune_get("gemm.frag_uk"), sb.tune_get("gemm.frag_waves"))).split(",")]
@@ -41,8 +43,9 @@ def main():
             a = torch.randn(batch * m * k, dtype=dt, device=dev)
             b = torch.randn(batch * k * n, dtype=dt, device=dev)
             c = torch.zeros(batch * m * n, dtype=dt, device=dev)
-            for frag, dot, cfg, tall in [(f, d, c, t) for f in frags for d in dots for c in cfgs
-                                         for t in talls]:
+            for frag, dot, cfg, tall, nt in [(f, d, c, t, u) for f in frags for d in dots
+                                             for c in cfgs for t in talls for u in nts]:
+                sb.tune_set("gemm.frag_nt", nt)
                 sb.tune_set("gemm.frag", frag)
                 sb.tune_set("gemm.frag_tall", tall)
                 sb.tune_set("gemm.dot_wgs", dot)
@@ -69,7 +72,7 @@ def main():
                 flops = 8.0 * m * n * k * batch
                 byts = float(es) * batch * (m * k + k * n + m * n)
                 print(json.dumps({"kind": kind, "dtype": str(dt), "m": m, "n": n, "k": k,
-                                  "batch": batch, "frag": frag, "frag_tall": tall, "dot_wgs": dot,
+                                  "batch": batch, "frag": frag, "frag_tall": tall, "frag_nt": nt, "dot_wgs": dot,
                                   "uk_waves": "%d:%d" % cfg,
                                   "us": round(t * 1e6, 1), "TFLOPs": round(flops / t / 1e12, 3),
                                   "TBps": round(byts / t / 1e12, 3)}), flush=True)
@@ -79,6 +82,7 @@ def main():
     sb.tune_set("gemm.frag_waves", 4096)
     sb.tune_set("gemm.frag_tall", 0)
     sb.tune_set("gemm.frag_pair", 1)
+    sb.tune_set("gemm.frag_nt", 0)
 
 
 if __name__ == "__main__":
