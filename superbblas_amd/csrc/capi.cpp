@@ -462,6 +462,7 @@ int sbx_tune_set(const char *key, long long value) {
         else if (k == "gemm.frag_tall") g_gemm_tune.frag_tall = (int)value;
         else if (k == "gemm.frag_pair") g_gemm_tune.frag_pair = (int)value;
         else if (k == "gemm.frag_nt") g_gemm_tune.frag_nt = (int)value;
+        else if (k == "gemm.frag_small") g_gemm_tune.frag_small = (int)value;
         else if (k == "gemm.frag_uk") g_gemm_tune.frag_uk = (int)value;
         else if (k == "gemm.frag_waves") g_gemm_tune.frag_waves = (int)value;
         else if (k == "gemm.clock") {
@@ -532,6 +533,7 @@ int sbx_tune_get(const char *key, long long *value) {
         else if (k == "gemm.frag_tall") *value = g_gemm_tune.frag_tall;
         else if (k == "gemm.frag_pair") *value = g_gemm_tune.frag_pair;
         else if (k == "gemm.frag_nt") *value = g_gemm_tune.frag_nt;
+        else if (k == "gemm.frag_small") *value = g_gemm_tune.frag_small;
         else if (k == "gemm.frag_uk") *value = g_gemm_tune.frag_uk;
         else if (k == "gemm.frag_waves") *value = g_gemm_tune.frag_waves;
         else if (k == "gemm.clock") *value = g_gemm_tune.clock;

@@ -1832,7 +1832,8 @@ template <typename R, bool CPLX> bool launch_frag(const GemmKArgs &p0, int devic
     // m = n = 8 / 12 / 16 / 32, k = 49152, batch 32: 794 / 792 / 794 / 802 -> 143 / 173 / 228 /
     // 490 us; updates m = 49152, n = k = 12 / 16: 291 / 453 -> 173 / 208 us; n = k <= 4 stay on
     // the rows kernel, 21-49 us against 122)
-    const bool small = p0.m <= 32 && p0.n <= 32;
+    const long sm = g_gemm_tune.frag_small;
+    const bool small = p0.m <= sm && p0.n <= sm;
     // the short output dimension against a short k: up to 32 for complex<float> (updates m =
     // 49152, n = k = 24 / 32, batch 32: 416 / 463 -> 327 / 427 us against the tiled kernels; 48
     // and 64 no better), 16 otherwise (complex<double> n = k = 32 / 48 / 64: no gain);

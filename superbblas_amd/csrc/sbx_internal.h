@@ -259,6 +259,7 @@ struct GemmTune {
     int frag_waves = 4096; ///< ... split-K to about this many waves
     int frag = 1;  ///< small outputs (m, n <= 32) and tall-skinny products on gemm_frag_kernel (MFMA
                    ///< fragments straight from global memory); 2 also for m, n <= 4; 0 = off
+    int frag_small = 32; ///< ... small outputs: m, n up to this
     int frag_nt = 0; ///< ... 16 x 16 tiles per wave along n (1, 2 or 4; 0 = 2 for 17-32-column small outputs)
     int frag_pair = 1; ///< ... 8-byte elements: k pairs of a unit-k-stride operand as one 16-byte load
     int frag_tall = 0; ///< ... tall-skinny products: the short output dimension up to this (k <= 64;

@@ -32,6 +32,8 @@ def main():
     sb.tune_set("gemm.frag_pair", int(os.environ.get("GEMM_PAIR", "1")))
     # NTS: gemm.frag_nt values (16 x 16 tiles per wave along n)
     nts = [int(v) for v in os.environ.get("NTS", str(sb.tune_get("gemm.frag_nt"))).split(",")]
+    # SMALL: gemm.frag_small (the small-output limit of the fragment kernel)
+    sb.tune_set("gemm.frag_small", int(os.environ.get("SMALL", str(sb.tune_get("gemm.frag_small")))))
     # FRAGCFG: "uk:waves" pairs for gemm_frag_kernel
     cfgs = [tuple(int(u) for u in v.split(":")) for v in os.environ.get(
         "FRAGCFG", "%d:%d" % (sb.tune_get("gemm.frag_uk"), sb.tune_get("gemm.frag_waves"))).split(",")]
@@ -83,6 +85,7 @@ def main():
     sb.tune_set("gemm.frag_tall", 0)
     sb.tune_set("gemm.frag_pair", 1)
     sb.tune_set("gemm.frag_nt", 0)
+    sb.tune_set("gemm.frag_small", 32)
 
 
 if __name__ == "__main__":
