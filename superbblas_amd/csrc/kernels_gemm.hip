@@ -1878,7 +1878,8 @@ template <typename R, bool CPLX> bool launch_frag(const GemmKArgs &p0, int devic
     // (measured, complex<float>, tools/studies/gemm_skinny_bench.py GEMM_PAIR, profiles/
     // r06_gemm_frag_pairs.txt: inner products, both operands paired, m = n = 8 / 12 / 16 / 32
     // 121 / 139 / 172 / 428 -> 100 / 122 / 160 / 288 us; updates, B alone paired, n = k = 8 / 12
-    // 80 / 136 -> 82 / 142 us, 16 the same, 32 427 -> 385 us: so B alone from n > 16)
+    // 80 / 136 -> 82 / 142 us, 16 the same, 32 427 -> 385 us: so B alone from n > 16; inner
+    // products with an m-contiguous A, B alone paired: within 3 %, profiles/r06_gemm_frag_pairs_nn.txt)
     const bool kp = E8 && g_gemm_tune.frag_pair && p.k % 2 == 0 &&
                     (p.pair_a || (p.pair_b && p.n > 16));
     KernelTimer total("gemm_total", s);

@@ -40,7 +40,8 @@ def main():
     for kind in kinds:
         for s in sizes:
             m, n, k = (s, s, K) if kind == "inner" else (K, s, s)
-            ta, tb = ("C", "N") if kind == "inner" else ("N", "N")
+            # TA_INNER: the inner products' A form (C: k contiguous, the default; N: m contiguous)
+            ta, tb = (os.environ.get("TA_INNER", "C"), "N") if kind == "inner" else ("N", "N")
             lda = k if ta != "N" else m
             a = torch.randn(batch * m * k, dtype=dt, device=dev)
             b = torch.randn(batch * k * n, dtype=dt, device=dev)
